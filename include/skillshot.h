@@ -1,0 +1,197 @@
+/*
+ * skillshot.h — C ABI of libskillshot, the MI355X-native batched Skillshot
+ * environment engine (drop-in for the per-tick step path of
+ * adrientremblay/Skillshot_Learning).
+ *
+ * The reference has no FFI: its step path is the Python class API of
+ * SkillshotGame / Player / Projectile driven by SkillshotLearner's per-tick
+ * protocol.  Every entry point below is the batched (N envs per call)
+ * replacement of one reference method; the file:line it replaces is cited on
+ * each declaration.  The Python layer (skillshot_learning_amd/) binds these
+ * with ctypes and re-exposes the reference class API on top.
+ *
+ * Conventions
+ *  - return 0 on success, a negative SK_E* code on error; sk_last_error()
+ *    returns a thread-local message for the last failure.  No exceptions
+ *    cross the ABI.
+ *  - Every pointer argument other than the handle is a DEVICE pointer on the
+ *    handle's device unless documented otherwise; all calls are ordered on
+ *    the given hipStream_t (passed as void*, NULL = legacy default stream).
+ *  - A handle must not be used from two host threads concurrently.
+ *  - Player ids follow the reference: 1 and 2 (SkillshotGame.py:20-21).
+ *    Player-indexed arrays use index p = id - 1.
+ *
+ * Device state layout (struct-of-arrays of 16-byte vectors, 88 B per env;
+ * SURVEY.md §8(d) canonical state).  For env e:
+ *    pos   [e] : int4    (p1.x, p1.y, p2.x, p2.y)          Player.pos
+ *    rot   [e] : double2 (p1.rotation, p2.rotation)       Player.rotation
+ *    qpos  [e] : int4    (q1.x, q1.y, q2.x, q2.y)          Projectile.pos
+ *    qrot  [e] : double2 (q1.rotation, q2.rotation)       Projectile.rotation
+ *    qcdage[e] : int4    (q1.cooldown, q1.age, q2.cooldown, q2.age)
+ *    misc  [e] : int2    (ticks, flags)
+ *        flags byte0 = q1.valid, byte1 = q2.valid, byte2 = game_live,
+ *              byte3 = winner_id (id of the player who was HIT,
+ *              SkillshotGame.py:76-78; 0 while no hit)
+ * Actions  : float [2][N][2]  (player, env, {move speed, look angle})
+ * Obs      : float [2][N][12] (player, env, prepare_states feature order,
+ *                              SkillshotLearner.py:512-543)
+ * Reward   : float [2][N]
+ * Features : double [N][2][18] (get_state per-player dict values in
+ *                               SkillshotGame.py:145-163 key order)
+ */
+#ifndef SKILLSHOT_H
+#define SKILLSHOT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SK_ABI_VERSION 1
+
+enum {
+  SK_OK = 0,
+  SK_EINVAL = -1,   /* bad argument (null handle, n_envs <= 0, bad player id) */
+  SK_EHIP = -2,     /* HIP runtime error (message in sk_last_error) */
+  SK_ENOMEM = -3,   /* device allocation failed */
+  SK_ENODEV = -4    /* no usable gfx950 device */
+};
+
+/* Game constants; sk_config_default() fills the reference values
+ * (SkillshotGame.py:11, Player.py:9-15, Projectile.py:5-10). */
+typedef struct sk_config {
+  int32_t board_w, board_h;          /* 250, 250 */
+  int32_t player_size;               /* 5 (5x5 box) */
+  int32_t projectile_size;           /* 3 (3x3 box) */
+  int32_t player_speed;              /* 3 */
+  int32_t projectile_speed;          /* 5 */
+  int32_t cooldown_max;              /* 15 */
+  double look_speed;                 /* 0.25 */
+  int32_t fixed_p1_x, fixed_p1_y;    /* 50, 50   (SkillshotGame.py:17) */
+  int32_t fixed_p2_x, fixed_p2_y;    /* 200, 200 (SkillshotGame.py:18) */
+  int32_t rand_lo, rand_hi;          /* 25, 225 (np.random.randint, hi exclusive) */
+} sk_config;
+
+/* Raw device pointers of one env batch's state (layout above). */
+typedef struct sk_state_view {
+  int32_t n_envs;
+  int32_t* pos;
+  double* rot;
+  int32_t* qpos;
+  double* qrot;
+  int32_t* qcdage;
+  int32_t* misc;
+} sk_state_view;
+
+typedef struct sk_env sk_env;
+
+/* Episode counters accumulated on device by the step kernels (wavefront
+ * ballot + popcount, one atomic per wave). */
+typedef struct sk_counters {
+  uint64_t dones;          /* episodes finished (hit or tick limit) */
+  uint64_t hits_p1;        /* episodes ending with winner_id == 1 */
+  uint64_t hits_p2;        /* episodes ending with winner_id == 2 */
+  uint64_t ticks_sum;      /* sum of final ticks over finished episodes */
+} sk_counters;
+
+const char* sk_last_error(void);
+int sk_abi_version(void);
+void sk_config_default(sk_config* cfg);
+
+/* Create a batch of n_envs games on `device` with engine-owned state, reset to
+ * the fixed start (SkillshotGame.__init__(random_positions=False),
+ * SkillshotGame.py:10-25).  env_offset = global id of env 0 (multi-GPU
+ * sharding: the counter-based RNG is keyed by global env id).  cfg may be NULL
+ * (reference defaults). */
+int sk_env_create(sk_env** out, int32_t n_envs, int64_t env_offset, uint64_t seed,
+                  int32_t device, const sk_config* cfg);
+/* Same, over caller-owned device buffers (e.g. torch tensors).  The view's
+ * pointers must stay valid until sk_env_destroy. */
+int sk_env_attach(sk_env** out, const sk_state_view* view, int64_t env_offset, uint64_t seed,
+                  int32_t device, const sk_config* cfg);
+int sk_env_destroy(sk_env* env);
+int sk_env_get_view(const sk_env* env, sk_state_view* out);
+/* Device counters (sk_counters, device memory) the step kernels accumulate into. */
+int sk_env_counters_ptr(const sk_env* env, sk_counters** out);
+/* Host-side RNG step counter: every step / reset call consumes one value
+ * (random starts and random actions are Philox4x32-10 keyed by
+ * (seed, global env id, step counter)). */
+int sk_env_get_step_counter(const sk_env* env, uint64_t* out);
+int sk_env_set_step_counter(sk_env* env, uint64_t value);
+
+/* SkillshotGame.game_reset(random_positions) (SkillshotGame.py:168-169 ->
+ * __init__ :10-25) for the envs whose mask byte is non-zero (mask NULL = all).
+ * random_positions: positions uniform in [rand_lo, rand_hi) per coordinate
+ * (np.random.randint(25, 225, (2, 2)), SkillshotGame.py:15) drawn from
+ * Philox4x32-10 instead of MT19937. */
+int sk_env_reset(sk_env* env, const uint8_t* mask, int32_t random_positions, void* stream);
+
+/* --- per-method batched ops (the reference's per-call protocol) ---------- */
+
+/* Player.move_direction_float(speed) (Player.py:57-68): clamp to [-1,1],
+ * new = int(round(pos - (sin|cos)(rot)*3*speed)), commit iff in bounds.
+ * speeds: device double[N] or NULL to use speed_scalar for every env. */
+int sk_player_move_direction(sk_env* env, int32_t player_id, const double* speeds,
+                             double speed_scalar, void* stream);
+/* Player.move_look_float(angle) (Player.py:33-39): rot += clamp(angle)*0.25 */
+int sk_player_move_look(sk_env* env, int32_t player_id, const double* angles,
+                        double angle_scalar, void* stream);
+/* Keyboard moves (Player.py:27-31, 41-55):
+ * kind 0 = move_forwards, 1 = move_backwards, 2 = move_look_left,
+ * 3 = move_look_right. */
+int sk_player_move_discrete(sk_env* env, int32_t player_id, int32_t kind, const uint8_t* mask,
+                            void* stream);
+/* Player.move_shoot_projectile() (Player.py:78-89) for envs with mask != 0
+ * (mask NULL = all). */
+int sk_player_shoot(sk_env* env, int32_t player_id, const uint8_t* mask, void* stream);
+/* SkillshotGame.game_tick() (SkillshotGame.py:115-122): live envs only;
+ * ticks += 1, both Projectile.tick() (Projectile.py:49-53), check_collision
+ * (SkillshotGame.py:58-94). */
+int sk_game_tick(sk_env* env, void* stream);
+
+/* --- observation / reward ----------------------------------------------- */
+
+/* get_state() numerics (SkillshotGame.py:136-166): feat = double[N][2][18]. */
+int sk_env_features(sk_env* env, double* feat, void* stream);
+
+enum { SK_REWARD_LOOKING = 0, SK_REWARD_SIMPLE = 1 };
+
+/* prepare_states (SkillshotLearner.py:512-543) -> obs float[2][N][12] and
+ * calculate_rewards_looking (:575-588) / _simple (:590-603) -> reward
+ * float[2][N], both of the CURRENT state.  obs / reward may be NULL. */
+int sk_env_observe(sk_env* env, float* obs, float* reward, int32_t reward_kind, void* stream);
+
+/* --- fused hot path ------------------------------------------------------ */
+
+/* One learner tick for every env (SkillshotLearner.py:302-318):
+ *   do_actions(1, actions[0][e]); do_actions(2, actions[1][e])  (:206-213)
+ *   game_tick()                                                (SkillshotGame.py:115)
+ *   obs/reward of the post-tick state                          (:314, :324)
+ *   done = !game_live || ticks >= tick_limit                   (:302)
+ * actions: float[2][N][2].  obs (float[2][N][12]), reward (float[2][N]),
+ * done (uint8[N]), winner (uint8[N]) may each be NULL.  The outputs describe
+ * the post-tick (terminal) state.  If auto_reset != 0, envs that are done are
+ * then reset (random_positions as in sk_env_reset) and, if obs_reset is not
+ * NULL, obs_reset receives the obs of the state the next tick acts on (equal
+ * to obs for envs that were not reset).  Episode counters are accumulated. */
+int sk_env_step(sk_env* env, const float* actions, float* obs, float* reward, int32_t reward_kind,
+                uint8_t* done, uint8_t* winner, int32_t tick_limit, int32_t auto_reset,
+                int32_t random_positions, float* obs_reset, void* stream);
+
+/* Random-policy actions (config 2 synthetic input): float[n_ticks][2][N][2]
+ * uniform in [-1,1) from Philox4x32-10 keyed (seed, global env id, step
+ * counter + t).  Does not advance the step counter. */
+int sk_gen_random_actions(sk_env* env, float* actions, int32_t n_ticks, void* stream);
+
+/* n_ticks random-policy ticks in ONE launch with per-env state held in
+ * registers (actions generated in-kernel exactly as sk_gen_random_actions,
+ * auto-reset with random starts at done).  Bit-identical to n_ticks calls of
+ * sk_env_step on sk_gen_random_actions output.  Advances the step counter by
+ * n_ticks. */
+int sk_env_rollout_random(sk_env* env, int32_t n_ticks, int32_t tick_limit, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SKILLSHOT_H */
