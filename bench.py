@@ -1,0 +1,263 @@
+#!/usr/bin/env python3
+"""Benchmark: env-steps/s of the fused Skillshot step kernel on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs 65536]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json metric "env-steps/sec (whole node) at 65536 self-play
+envs"): every GPU steps 65,536 games (weak scaling:
+envs shard by global id, no data-path collective) with the random policy.
+One bench step = one k_step launch over all of a GPU's games: both players'
+do_actions (SkillshotLearner.py:206-213) + game_tick (SkillshotGame.py:115-122)
++ done + random auto-reset.  Actions are Philox uniform(-1,1) float32
+pre-generated into HBM (K4, not timed), a distinct 1 MiB slab per tick, read
+from a ring larger than the 256 MiB Infinity Cache.  The K timed steps are
+replayed from hipGraphs of `--graph-len` captured launches (the engine's RNG
+step counter lives on device, so replays stay correctly keyed).
+
+Roofline: algorithmic bytes per env-step = 193 B (state 88 B read + 88 B
+written, actions 16 B, done 1 B: SURVEY.md §8(d)); per-launch duration from
+HIP events around individual launches queued back-to-back behind a spin
+kernel on the launch stream.  cpu_baseline: the C oracle (a port of the
+reference step) on one host core over a bounded sample of the same workload.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "env-steps/sec (whole node) at 65536 self-play envs; 1/2/4/8 GPU scaling"
+BYTES_PER_ENV_STEP = 193  # SURVEY.md §8(d) step-only contract
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=4000)
+    p.add_argument("--warmup", type=int, default=400)
+    p.add_argument("--envs", type=int, default=65536, help="games per GPU")
+    p.add_argument("--tick-limit", type=int, default=2000)
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--graph-len", type=int, default=400, help="launches per captured hipGraph")
+    p.add_argument("--action-ring", type=int, default=400, help="distinct per-tick action slabs in HBM")
+    p.add_argument("--roofline-launches", type=int, default=300)
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-rollout", action="store_true")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_k_step.json"))
+    return p.parse_args()
+
+
+def cpu_baseline(n_envs, seconds, tick_limit, seed):
+    """C oracle (port of the reference step, oracle/skillshot_oracle.c) on one
+    core: the same workload (random policy, fused step, auto-reset), bounded
+    to about `seconds` of CPU work."""
+    from oracle import oracle
+    s = oracle.OracleState(n_envs, seed=seed)
+    s.reset(random_positions=True)
+    chunk = 8
+    acts = s.gen_random_actions(chunk)  # pre-generated, untimed (as on the GPU)
+    steps = 0
+    t0 = time.perf_counter()
+    while True:
+        for t in range(chunk):
+            s.step(acts[t], tick_limit=tick_limit, auto_reset=True, random_positions=True, want_obs=False)
+        steps += chunk
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    rate = n_envs * steps / el
+    return dict(value=rate, unit="env-steps/s", cores=1, kind="port",
+                sample=f"C oracle (oracle/skillshot_oracle.c, restatement of the reference step) "
+                       f"{n_envs} envs x {steps} ticks ({el:.1f} s, 1 thread); reference Python on the "
+                       f"survey host: 59.2k env-steps/s per core (BASELINE.md)")
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from skillshot_learning_amd import VecSkillshotGame
+
+    n = args.envs
+    env = VecSkillshotGame(n, device=dev, seed=args.seed, env_offset=rank * n, tick_limit=args.tick_limit,
+                           random_positions=True)
+    stream = torch.cuda.Stream(device=dev)
+    G = max(2, args.graph_len - (args.graph_len % 2))  # even: keeps the step-slot parity invariant
+    ring = max(G, args.action_ring)
+    with torch.cuda.stream(stream):
+        env.reset(random_positions=True)
+        actions = env.gen_random_actions(ring)  # [ring, 2, N, 2] f32, 16 B/env/tick
+        done = torch.empty(n, dtype=torch.uint8, device=dev)
+    stream.synchronize()
+
+    a_ptr0 = actions.data_ptr()
+    slab = 2 * n * 2 * 4
+    d_ptr = done.data_ptr()
+    import ctypes
+    sp = ctypes.c_void_p(stream.cuda_stream)
+
+    def launch(t):
+        env.step_raw(ctypes.c_void_p(a_ptr0 + (t % ring) * slab), ctypes.c_void_p(d_ptr), stream=sp)
+
+    # capture one graph of G launches (eager warm-up first so code objects load)
+    with torch.cuda.stream(stream):
+        for t in range(4):
+            launch(t)
+    stream.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=stream):
+        for t in range(G):
+            launch(t)
+    stream.synchronize()
+
+    def run(k):
+        """k launches: whole graph replays, remainder eager (parity-safe)."""
+        with torch.cuda.stream(stream):
+            for _ in range(k // G):
+                graph.replay()
+            for t in range(k % G):
+                launch(t)
+
+    env.clear_counters()
+    run(args.warmup)
+    stream.synchronize()
+
+    K = args.steps
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with torch.cuda.stream(stream):
+        ev0.record()
+    run(K)
+    with torch.cuda.stream(stream):
+        ev1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ev_ms = ev0.elapsed_time(ev1)
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    total_env_steps = n * world * K
+    value = total_env_steps / elapsed
+
+    # ---- roofline: per-launch durations, launches queued behind a spin kernel
+    M = args.roofline_launches
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(M)]
+    with torch.cuda.stream(stream):
+        torch.cuda._sleep(int(2.4e9 * 0.05))  # ~50 ms so the host queues all M launches first
+        for m in range(M):
+            evs[m][0].record()
+            launch(m)
+            evs[m][1].record()
+    stream.synchronize()
+    durs = sorted(a.elapsed_time(b) for a, b in evs)
+    kern_ms = sum(durs) / len(durs)
+    achieved = BYTES_PER_ENV_STEP * n / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            if tj.get("envs") == n:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    counters = env.counters()
+
+    # ---- secondary: register-resident multi-tick random-policy kernel
+    rollout = None
+    if not args.no_rollout:
+        ticks = 200
+        with torch.cuda.stream(stream):
+            env.rollout_random(ticks)
+        stream.synchronize()
+        r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 10
+        with torch.cuda.stream(stream):
+            r0.record()
+            for _ in range(reps):
+                env.rollout_random(ticks)
+            r1.record()
+        stream.synchronize()
+        rms = r0.elapsed_time(r1)
+        rollout = dict(kernel="k_rollout_random", ticks_per_launch=ticks,
+                       env_steps_per_s_per_gpu=n * ticks * reps / (rms * 1e-3),
+                       note="state held in registers across ticks; reported beside, not as, the headline")
+
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(n, args.cpu_seconds, args.tick_limit, args.seed)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / K,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {
+                "workload": f"config-2 step kernel: {n} games/GPU, random policy (Philox f32 actions pre-generated "
+                            f"in HBM), fused k_step per tick (do_actions x2 + game_tick + done + random "
+                            f"auto-reset), tick_limit {args.tick_limit}",
+                "envs_per_gpu": n,
+                "total_envs": n * world,
+                "global_batch": n * world,
+                "parallelism": f"env-shard dp{world}",
+                "graph_len": G,
+                "event_ms_per_step": ev_ms / K,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel": "k_step",
+                "bytes_per_env_step": BYTES_PER_ENV_STEP,
+                "kernel_us": kern_ms * 1e3,
+                "kernel_us_p10_p90": [durs[len(durs) // 10] * 1e3, durs[(9 * len(durs)) // 10] * 1e3],
+            },
+            "cpu_baseline": cpu,
+            "episodes": counters,
+            "rollout_random": rollout,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    env.close()
+
+
+if __name__ == "__main__":
+    main()

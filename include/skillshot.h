@@ -114,6 +114,10 @@ int sk_env_destroy(sk_env* env);
 int sk_env_get_view(const sk_env* env, sk_state_view* out);
 /* Device counters (sk_counters, device memory) the step kernels accumulate into. */
 int sk_env_counters_ptr(const sk_env* env, sk_counters** out);
+/* Copy the episode counters to host memory (synchronises `stream`), and
+ * zero them (stream-ordered). */
+int sk_env_read_counters(sk_env* env, sk_counters* host_out, void* stream);
+int sk_env_clear_counters(sk_env* env, void* stream);
 /* Host-side RNG step counter: every step / reset call consumes one value
  * (random starts and random actions are Philox4x32-10 keyed by
  * (seed, global env id, step counter)). */

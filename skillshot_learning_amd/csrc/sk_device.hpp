@@ -1,0 +1,316 @@
+// sk_device.hpp — per-env Skillshot game logic for gfx950 (device side).
+//
+// One lane owns one env (both players: they interact only through the
+// collision test, SkillshotGame.py:58-94).  State lives in registers as an
+// `Env` between one coalesced 16-byte-per-lane load of each SoA plane and one
+// store (layout: include/skillshot.h).
+//
+// Numerics: positions are integers produced by int(round(fp64)) (Player.py:63-64,
+// Projectile.py:40-41), so the move/projectile arithmetic is fp64 in the
+// reference's operation order with FMA contraction OFF (a fused x - s*5 rounds
+// differently); Python's round() is round-half-even = v_rndne_f64.
+#pragma once
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/skillshot.h"
+
+namespace sk {
+
+constexpr double kPi = 3.141592653589793;     // math.pi
+constexpr double kPi2 = 1.5707963267948966;   // math.pi / 2
+
+struct Cfg {  // device copy of sk_config (kernel argument)
+  int W, H, psize, qsize, pspeed, qspeed, cdmax;
+  double look;
+  int f1x, f1y, f2x, f2y, rlo, rhi;
+  double max_dist;  // (2*250**2)**0.5, SkillshotLearner.py:43
+};
+
+struct View {  // device pointers, layout of include/skillshot.h
+  int4* pos;
+  double2* rot;
+  int4* qpos;
+  double2* qrot;
+  int4* qcdage;
+  int2* misc;
+};
+
+struct Env {
+  int px[2], py[2];
+  double rot[2];
+  int qx[2], qy[2];
+  double qrot[2];
+  int qcd[2], qage[2];
+  int ticks;
+  int qvalid[2], live, winner;
+};
+
+__device__ __forceinline__ void load_env(const View& v, int64_t i, Env& e) {
+  int4 p = v.pos[i];
+  double2 r = v.rot[i];
+  int4 q = v.qpos[i];
+  double2 qr = v.qrot[i];
+  int4 ca = v.qcdage[i];
+  int2 m = v.misc[i];
+  e.px[0] = p.x; e.py[0] = p.y; e.px[1] = p.z; e.py[1] = p.w;
+  e.rot[0] = r.x; e.rot[1] = r.y;
+  e.qx[0] = q.x; e.qy[0] = q.y; e.qx[1] = q.z; e.qy[1] = q.w;
+  e.qrot[0] = qr.x; e.qrot[1] = qr.y;
+  e.qcd[0] = ca.x; e.qage[0] = ca.y; e.qcd[1] = ca.z; e.qage[1] = ca.w;
+  e.ticks = m.x;
+  unsigned f = (unsigned)m.y;
+  e.qvalid[0] = f & 0xff; e.qvalid[1] = (f >> 8) & 0xff;
+  e.live = (f >> 16) & 0xff; e.winner = (f >> 24) & 0xff;
+}
+
+__device__ __forceinline__ void store_env(const View& v, int64_t i, const Env& e) {
+  v.pos[i] = make_int4(e.px[0], e.py[0], e.px[1], e.py[1]);
+  v.rot[i] = make_double2(e.rot[0], e.rot[1]);
+  v.qpos[i] = make_int4(e.qx[0], e.qy[0], e.qx[1], e.qy[1]);
+  v.qrot[i] = make_double2(e.qrot[0], e.qrot[1]);
+  v.qcdage[i] = make_int4(e.qcd[0], e.qage[0], e.qcd[1], e.qage[1]);
+  unsigned f = (unsigned)(e.qvalid[0] & 0xff) | ((unsigned)(e.qvalid[1] & 0xff) << 8) |
+               ((unsigned)(e.live & 0xff) << 16) | ((unsigned)(e.winner & 0xff) << 24);
+  v.misc[i] = make_int2(e.ticks, (int)f);
+}
+
+// ---------------------------------------------------------------- Philox4x32-10
+struct U4 { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+    uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    U4 n = {hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    c = n;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// counter = (global env lo, hi, step lo, step hi ^ stream<<28); stream 0 =
+// random actions, 1 = random starts.  Keyed by the GLOBAL env id so an N-GPU
+// run equals the concatenation of single-GPU runs over the same id ranges.
+__device__ __forceinline__ U4 draw4(uint64_t seed, uint64_t genv, uint64_t step, uint32_t stream) {
+  U4 c = {(uint32_t)genv, (uint32_t)(genv >> 32), (uint32_t)step,
+          (uint32_t)(step >> 32) ^ (stream << 28)};
+  return philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+
+__device__ __forceinline__ float u32_to_action(uint32_t u) {  // uniform [-1,1), exact
+  return (float)((int32_t)(u >> 8) - 8388608) * 0x1p-23f;
+}
+
+__device__ __forceinline__ int u32_to_pos(uint32_t u, int lo, int hi) {
+  return lo + (int)(((uint64_t)u * (uint64_t)(hi - lo)) >> 32);
+}
+
+// ---------------------------------------------------------------- reset
+__device__ __forceinline__ void reset_fixed(const Cfg& c, Env& e) {  // SkillshotGame.py:10-25
+  e.px[0] = c.f1x; e.py[0] = c.f1y; e.px[1] = c.f2x; e.py[1] = c.f2y;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    e.rot[p] = 0.0; e.qx[p] = 0; e.qy[p] = 0; e.qrot[p] = 0.0;
+    e.qcd[p] = 0; e.qage[p] = 0; e.qvalid[p] = 0;
+  }
+  e.ticks = 0; e.live = 1; e.winner = 0;
+}
+
+__device__ __forceinline__ void reset_random(const Cfg& c, Env& e, uint64_t seed, uint64_t genv,
+                                             uint64_t step) {
+  U4 u = draw4(seed, genv, step, 1u);
+  reset_fixed(c, e);
+  e.px[0] = u32_to_pos(u.x, c.rlo, c.rhi);
+  e.py[0] = u32_to_pos(u.y, c.rlo, c.rhi);
+  e.px[1] = u32_to_pos(u.z, c.rlo, c.rhi);
+  e.py[1] = u32_to_pos(u.w, c.rlo, c.rhi);
+}
+
+// ---------------------------------------------------------------- Player
+__device__ __forceinline__ double clamp_action(double a) {  // Player.py:36-37, :60-61
+  a = (a >= 1.0) ? 1.0 : a;
+  a = (a <= -1.0) ? -1.0 : a;
+  return a;
+}
+
+__device__ __forceinline__ bool player_pos_valid(const Cfg& c, int x, int y) {  // Player.py:70-76
+  return (x + c.psize <= c.W) & (x >= 0) & (y + c.psize <= c.H) & (y >= 0);
+}
+
+// Player.move_direction_float (Player.py:57-68)
+__device__ __forceinline__ void move_direction(const Cfg& c, Env& e, int p, double speed) {
+  speed = clamp_action(speed);
+  double s, co;
+  sincos(e.rot[p], &s, &co);
+  const double sp = (double)c.pspeed;
+  double nxf = __builtin_rint((double)e.px[p] - (s * sp) * speed);
+  double nyf = __builtin_rint((double)e.py[p] - (co * sp) * speed);
+  // compare in fp64 first: a NaN speed (the reference raises ValueError in
+  // int(round(nan))) never commits a move here
+  bool ok = (nxf >= 0.0) & (nxf + (double)c.psize <= (double)c.W) & (nyf >= 0.0) &
+            (nyf + (double)c.psize <= (double)c.H);
+  if (ok) { e.px[p] = (int)nxf; e.py[p] = (int)nyf; }
+}
+
+// Player.move_forwards / move_backwards (Player.py:41-55)
+__device__ __forceinline__ void move_fwd_back(const Cfg& c, Env& e, int p, bool backwards) {
+  double s, co;
+  sincos(e.rot[p], &s, &co);
+  double dx = s * (double)c.pspeed, dy = co * (double)c.pspeed;
+  double nxf = backwards ? __builtin_rint((double)e.px[p] + dx) : __builtin_rint((double)e.px[p] - dx);
+  double nyf = backwards ? __builtin_rint((double)e.py[p] + dy) : __builtin_rint((double)e.py[p] - dy);
+  int nx = (int)nxf, ny = (int)nyf;
+  if (player_pos_valid(c, nx, ny)) { e.px[p] = nx; e.py[p] = ny; }
+}
+
+// Player.move_look_float (Player.py:33-39)
+__device__ __forceinline__ void move_look(const Cfg& c, Env& e, int p, double angle) {
+  angle = clamp_action(angle);
+  e.rot[p] = e.rot[p] + angle * c.look;
+}
+
+// Player.move_shoot_projectile (Player.py:78-89)
+__device__ __forceinline__ void shoot(const Cfg& c, Env& e, int p) {
+  if (e.qcd[p] <= 0) {
+    e.qx[p] = e.px[p]; e.qy[p] = e.py[p]; e.qrot[p] = e.rot[p];
+    e.qvalid[p] = 1; e.qcd[p] = c.cdmax; e.qage[p] = 0;
+  }
+}
+
+// ---------------------------------------------------------------- Projectile
+// Projectile.tick (Projectile.py:49-53) -> move_forwards (:38-47).  An invalid
+// projectile's candidate position is never committed (valid stays False), so
+// its trig is skipped: no observable difference.
+__device__ __forceinline__ void projectile_tick(const Cfg& c, Env& e, int p) {
+  if (e.qvalid[p]) {
+    double s, co;
+    sincos(e.qrot[p], &s, &co);
+    const double sp = (double)c.qspeed;
+    int nx = (int)__builtin_rint((double)e.qx[p] - s * sp);
+    int ny = (int)__builtin_rint((double)e.qy[p] - co * sp);
+    bool ok = (nx + c.qsize <= c.W) & (nx >= 0) & (ny + c.qsize <= c.H) & (ny >= 0);
+    if (ok) { e.qx[p] = nx; e.qy[p] = ny; } else { e.qvalid[p] = 0; }
+  }
+  e.qcd[p] -= 1;
+  e.qage[p] += 1;
+}
+
+// SkillshotGame.check_collision (SkillshotGame.py:58-94): integer corner test
+// of player p's box against the OTHER player's projectile corners
+// x in {qx+3, qx}, y in {qy, qy-3}; player 1 is tested first and wins ties.
+__device__ __forceinline__ bool hit_test(const Cfg& c, const Env& e, int p) {
+  int q = 1 - p;
+  int L = e.px[p], R = e.px[p] + c.psize, T = e.py[p], B = e.py[p] + c.psize;
+  int ql = e.qx[q], qr = e.qx[q] + c.qsize, qt = e.qy[q], qb = e.qy[q] - c.qsize;
+  bool xr = (L <= qr) & (qr <= R), xl = (L <= ql) & (ql <= R);
+  bool yt = (T <= qt) & (qt <= B), yb = (T <= qb) & (qb <= B);
+  return e.qvalid[q] && ((xr | xl) & (yt | yb));
+}
+
+// SkillshotGame.game_tick (SkillshotGame.py:115-122)
+__device__ __forceinline__ void game_tick(const Cfg& c, Env& e) {
+  if (e.live) {
+    e.ticks += 1;
+    projectile_tick(c, e, 0);
+    projectile_tick(c, e, 1);
+    if (hit_test(c, e, 0)) { e.winner = 1; e.live = 0; }
+    else if (hit_test(c, e, 1)) { e.winner = 2; e.live = 0; }
+  }
+}
+
+// ---------------------------------------------------------------- features
+__device__ __forceinline__ double grad_of(double rot) {  // Player.py:94, Projectile.py:58
+  return tan(-rot + kPi2);
+}
+
+// SkillshotGame.get_dist_line_point (SkillshotGame.py:124-130); g**2 as g*g
+__device__ __forceinline__ double dist_line_point(double g, int lx, int ly, int cx, int cy) {
+  double cc = (double)ly - g * (double)lx;
+  return fabs(g * (double)cx - (double)cy + cc) / sqrt(g * g + 1.0);
+}
+
+// SkillshotGame.get_dist_point_point (SkillshotGame.py:132-134): exact integer
+// sum of squares, then sqrt (correctly rounded)
+__device__ __forceinline__ double dist_point_point(int ax, int ay, int bx, int by) {
+  int dx = ax - bx, dy = ay - by;
+  return sqrt((double)(dx * dx + dy * dy));
+}
+
+// SkillshotGame.check_future_collision (SkillshotGame.py:96-113) for the
+// projectile of player p against opponent o: the x_dir gate (:109) is always
+// true for the first projectile x bound, so the test reduces to
+// valid && exists X in {Ox, Ox+5}: Oy <= g*X + (qy - g*qx) <= Oy+5.
+__device__ __forceinline__ bool future_collision(const Cfg& c, const Env& e, int p, double g) {
+  if (!e.qvalid[p]) return false;
+  int o = 1 - p;
+  double yi = (double)e.qy[p] - g * (double)e.qx[p];
+  double lo = (double)e.py[o], hi = (double)(e.py[o] + c.psize);
+  double v0 = g * (double)e.px[o] + yi;
+  double v1 = g * (double)(e.px[o] + c.psize) + yi;
+  return ((lo <= v0) & (v0 <= hi)) | ((lo <= v1) & (v1 <= hi));
+}
+
+__device__ __forceinline__ double py_mod2(double r) {  // Python float % 2 (floored)
+  double m = fmod(r, 2.0);
+  if (m != 0.0) {
+    if (m < 0.0) m += 2.0;
+  } else {
+    m = 0.0;
+  }
+  return m;
+}
+
+// prepare_states (SkillshotLearner.py:512-543) for player p; also returns the
+// calculate_rewards_looking reward (:584) through *reward_looking.
+__device__ __forceinline__ void obs12(const Cfg& c, const Env& e, int p, float out[12],
+                                      double* path_dist) {
+  int o = 1 - p;
+  double gp = grad_of(e.rot[p]);
+  double gq = grad_of(e.qrot[p]);
+  double D = c.max_dist;
+  double pd = dist_line_point(gp, e.px[p], e.py[p], e.px[o], e.py[o]);
+  *path_dist = pd;
+  out[0] = (float)(pd / D);
+  out[1] = (float)(dist_point_point(e.px[p], e.py[p], e.px[o], e.py[o]) / D);
+  out[2] = (float)((double)e.px[p] / (double)c.W);
+  out[3] = (float)((double)e.py[p] / (double)c.H);
+  out[4] = (float)(((py_mod2(e.rot[p]) * kPi) / 2.0) * kPi);  // `% 2 * np.pi) / 2 * np.pi`
+  out[5] = (float)((double)e.qcd[p] / (double)c.cdmax);
+  out[6] = (float)(dist_point_point(e.qx[p], e.qy[p], e.px[o], e.py[o]) / D);
+  out[7] = (float)((double)e.qx[p] / (double)c.W);
+  out[8] = (float)((double)e.qy[p] / (double)c.H);
+  out[9] = (float)(((py_mod2(e.qrot[p]) * kPi) / 2.0) * kPi);
+  out[10] = (float)(dist_line_point(gq, e.qx[p], e.qy[p], e.px[o], e.py[o]) / D);
+  out[11] = future_collision(c, e, p, gq) ? 1.0f : 0.0f;
+}
+
+// get_state per-player dict values (SkillshotGame.py:145-163 key order)
+__device__ __forceinline__ void features18(const Cfg& c, const Env& e, int p, double f[18]) {
+  int o = 1 - p;
+  double gp = grad_of(e.rot[p]);
+  double gq = grad_of(e.qrot[p]);
+  f[0] = gp;
+  f[1] = (-sin(e.rot[p]) >= 0.0) ? 1.0 : -1.0;
+  f[2] = dist_line_point(gp, e.px[p], e.py[p], e.px[o], e.py[o]);
+  f[3] = dist_point_point(e.px[p], e.py[p], e.px[o], e.py[o]);
+  f[4] = e.px[p];
+  f[5] = e.py[p];
+  f[6] = e.rot[p];
+  f[7] = e.qcd[p];
+  f[8] = gq;
+  f[9] = (-sin(e.qrot[p]) >= 0.0) ? 1.0 : -1.0;
+  f[10] = dist_line_point(gq, e.qx[p], e.qy[p], e.px[o], e.py[o]);
+  f[11] = e.qx[p];
+  f[12] = e.qy[p];
+  f[13] = e.qrot[p];
+  f[14] = e.qage[p];
+  f[15] = e.qvalid[p];
+  f[16] = dist_point_point(e.qx[p], e.qy[p], e.px[o], e.py[o]);
+  f[17] = future_collision(c, e, p, gq) ? 1.0 : 0.0;
+}
+
+}  // namespace sk

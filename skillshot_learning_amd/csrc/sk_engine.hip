@@ -1,0 +1,675 @@
+// sk_engine.hip — libskillshot: batched Skillshot env kernels for gfx950 and
+// the C ABI declared in include/skillshot.h.
+//
+// Kernels (one lane = one env; 256-lane workgroups; every SoA plane moved
+// with one 16-byte-per-lane load/store):
+//   k_step            fused learner tick: do_actions x2 + game_tick + obs/reward
+//                     + done/winner + masked auto-reset  (the hot path, K1+K2+K3)
+//   k_rollout_random  n ticks of the random policy in one launch, state held in
+//                     registers, in-kernel Philox actions (K4 fused)
+//   k_gen_actions     random-policy actions into HBM (K4)
+//   k_reset / k_move_* / k_shoot / k_game_tick / k_observe / k_features:
+//                     the reference's per-method API, batched
+// Episode counters use a wavefront ballot + popcount and one atomic per wave.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "sk_device.hpp"
+
+using namespace sk;
+
+struct sk_env {
+  int32_t n;
+  int64_t env_offset;
+  uint64_t seed;
+  int32_t device;
+  sk_config cfg;
+  Cfg dcfg;
+  View view;
+  sk_state_view hview;
+  bool owned;
+  sk_counters* d_counters;
+  // RNG step counter, device-resident so every call is hipGraph-capturable:
+  // two slots ping-pong; a kernel reads slots[parity] and block 0 writes
+  // slots[1-parity] = value + advance, then the host flips parity.
+  uint64_t* d_step;
+  int parity;
+};
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                 \
+  do {                                                                                \
+    hipError_t _e = (expr);                                                           \
+    if (_e != hipSuccess)                                                             \
+      return fail(SK_EHIP, std::string(#expr) + ": " + hipGetErrorString(_e));       \
+  } while (0)
+
+static constexpr int kBlock = 256;
+
+static inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+// ------------------------------------------------------------------ counters
+// wavefront ballot: count done / hit-by-id lanes, sum final ticks; lane 0 of
+// each wave issues the atomics.
+__device__ __forceinline__ void wave_count(sk_counters* ctr, bool done, int winner, int ticks) {
+  uint64_t m_done = __ballot(done);
+  if (m_done == 0) return;  // wave-uniform
+  uint64_t m_w1 = __ballot(done && winner == 1);
+  uint64_t m_w2 = __ballot(done && winner == 2);
+  uint64_t t = done ? (uint64_t)ticks : 0;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd((unsigned long long*)&ctr->dones, (unsigned long long)__popcll(m_done));
+    if (m_w1) atomicAdd((unsigned long long*)&ctr->hits_p1, (unsigned long long)__popcll(m_w1));
+    if (m_w2) atomicAdd((unsigned long long*)&ctr->hits_p2, (unsigned long long)__popcll(m_w2));
+    atomicAdd((unsigned long long*)&ctr->ticks_sum, (unsigned long long)t);
+  }
+}
+
+__device__ __forceinline__ void store_obs(float* obs, int64_t n, int p, int64_t i, const float o[12]) {
+  float4* d = reinterpret_cast<float4*>(obs + ((int64_t)p * n + i) * 12);
+  d[0] = make_float4(o[0], o[1], o[2], o[3]);
+  d[1] = make_float4(o[4], o[5], o[6], o[7]);
+  d[2] = make_float4(o[8], o[9], o[10], o[11]);
+}
+
+__device__ __forceinline__ float reward_of(const Cfg& c, const Env& e, int p, int kind, double path_dist) {
+  if (kind == SK_REWARD_SIMPLE) {  // SkillshotLearner.py:600
+    int o = 1 - p;
+    double mine = dist_point_point(e.qx[p], e.qy[p], e.px[o], e.py[o]);
+    double theirs = dist_point_point(e.qx[o], e.qy[o], e.px[p], e.py[p]);
+    return (float)(mine - theirs);
+  }
+  return (float)(-path_dist / (double)c.W);  // SkillshotLearner.py:584
+}
+
+// ------------------------------------------------------------------ step slots
+struct StepRef {
+  uint64_t* slots;
+  int parity;
+};
+
+__device__ __forceinline__ uint64_t step_read(const StepRef& s) {
+  return __hip_atomic_load(s.slots + s.parity, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void step_advance(const StepRef& s, uint64_t base, uint64_t inc) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) s.slots[1 - s.parity] = base + inc;
+}
+
+// ------------------------------------------------------------------ kernels
+struct StepArgs {
+  View v;
+  int64_t n;
+  const float2* actions;  // [2][N] float2
+  float* obs;
+  float* reward;
+  int reward_kind;
+  uint8_t* done;
+  uint8_t* winner;
+  int tick_limit;
+  int auto_reset;
+  int random_positions;
+  float* obs_reset;
+  uint64_t seed;
+  int64_t env_offset;
+  StepRef step;
+  sk_counters* ctr;
+};
+
+__global__ void __launch_bounds__(kBlock) k_step(StepArgs a, Cfg c) {
+  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint64_t step = step_read(a.step);
+  step_advance(a.step, step, 1);
+  bool in = i < a.n;
+  bool d = false;
+  Env e;
+  if (in) {
+    load_env(a.v, i, e);
+    float2 a0 = a.actions[i];
+    float2 a1 = a.actions[a.n + i];
+    // do_actions(1, ...), do_actions(2, ...)  SkillshotLearner.py:206-213
+    move_direction(c, e, 0, (double)a0.x);
+    move_look(c, e, 0, (double)a0.y);
+    shoot(c, e, 0);
+    move_direction(c, e, 1, (double)a1.x);
+    move_look(c, e, 1, (double)a1.y);
+    shoot(c, e, 1);
+    game_tick(c, e);
+    if (a.obs || a.reward) {
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        float o[12];
+        double pd;
+        obs12(c, e, p, o, &pd);
+        if (a.obs) store_obs(a.obs, a.n, p, i, o);
+        if (a.reward) a.reward[(int64_t)p * a.n + i] = reward_of(c, e, p, a.reward_kind, pd);
+      }
+    }
+    d = (!e.live) || (e.ticks >= a.tick_limit);  // SkillshotLearner.py:302
+    if (a.done) a.done[i] = (uint8_t)d;
+    if (a.winner) a.winner[i] = (uint8_t)e.winner;
+  }
+  if (a.ctr) wave_count(a.ctr, d, in ? e.winner : 0, in ? e.ticks : 0);
+  if (!in) return;
+  if (d && a.auto_reset) {
+    if (a.random_positions) reset_random(c, e, a.seed, (uint64_t)(a.env_offset + i), step);
+    else reset_fixed(c, e);
+  }
+  if (a.obs_reset) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      float o[12];
+      double pd;
+      obs12(c, e, p, o, &pd);
+      store_obs(a.obs_reset, a.n, p, i, o);
+    }
+  }
+  store_env(a.v, i, e);
+}
+
+struct RolloutArgs {
+  View v;
+  int64_t n;
+  int n_ticks;
+  int tick_limit;
+  uint64_t seed;
+  int64_t env_offset;
+  StepRef step;
+  sk_counters* ctr;
+};
+
+__global__ void __launch_bounds__(kBlock) k_rollout_random(RolloutArgs a, Cfg c) {
+  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  bool in = i < a.n;
+  const uint64_t step0 = step_read(a.step);
+  step_advance(a.step, step0, (uint64_t)a.n_ticks);
+  Env e;
+  if (in) load_env(a.v, i, e);
+  uint64_t genv = (uint64_t)(a.env_offset + i);
+  unsigned dones = 0, w1 = 0, w2 = 0;
+  uint64_t tsum = 0;
+  if (in) {
+    for (int t = 0; t < a.n_ticks; ++t) {
+      uint64_t step = step0 + (uint64_t)t;
+      U4 u = draw4(a.seed, genv, step, 0u);
+      move_direction(c, e, 0, (double)u32_to_action(u.x));
+      move_look(c, e, 0, (double)u32_to_action(u.y));
+      shoot(c, e, 0);
+      move_direction(c, e, 1, (double)u32_to_action(u.z));
+      move_look(c, e, 1, (double)u32_to_action(u.w));
+      shoot(c, e, 1);
+      game_tick(c, e);
+      if ((!e.live) || (e.ticks >= a.tick_limit)) {
+        dones += 1;
+        w1 += (e.winner == 1);
+        w2 += (e.winner == 2);
+        tsum += (uint64_t)e.ticks;
+        reset_random(c, e, a.seed, genv, step);
+      }
+    }
+    store_env(a.v, i, e);
+  }
+  if (a.ctr) {
+    uint64_t vals[4] = {dones, w1, w2, tsum};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      uint64_t x = vals[k];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+      vals[k] = x;
+    }
+    if ((threadIdx.x & 63) == 0 && vals[0]) {
+      unsigned long long* base = (unsigned long long*)a.ctr;
+      for (int k = 0; k < 4; ++k)
+        if (vals[k]) atomicAdd(base + k, (unsigned long long)vals[k]);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_gen_actions(float4* out, int64_t n, int n_ticks, uint64_t seed,
+                                                        int64_t env_offset, StepRef sref) {
+  const uint64_t step0 = step_read(sref);
+  // out: [T][2][N] float2 viewed as pairs; each lane writes both players' float2
+  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  float2* o = reinterpret_cast<float2*>(out);
+  for (int t = 0; t < n_ticks; ++t) {
+    U4 u = draw4(seed, (uint64_t)(env_offset + i), step0 + (uint64_t)t, 0u);
+    o[(int64_t)t * 2 * n + i] = make_float2(u32_to_action(u.x), u32_to_action(u.y));
+    o[(int64_t)t * 2 * n + n + i] = make_float2(u32_to_action(u.z), u32_to_action(u.w));
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_reset(View v, int64_t n, const uint8_t* mask, int random,
+                                                  uint64_t seed, int64_t env_offset, StepRef sref, Cfg c) {
+  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint64_t step = step_read(sref);
+  step_advance(sref, step, 1);
+  if (i >= n || (mask && !mask[i])) return;
+  Env e;
+  if (random) reset_random(c, e, seed, (uint64_t)(env_offset + i), step);
+  else reset_fixed(c, e);
+  store_env(v, i, e);
+}
+
+__global__ void __launch_bounds__(kBlock) k_move_direction(View v, int64_t n, int p, const double* vals,
+                                                           double scalar, Cfg c) {
+  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  Env e;
+  load_env(v, i, e);
+  double x = vals ? vals[i] : scalar;
+  if (p == 0) move_direction(c, e, 0, x); else move_direction(c, e, 1, x);
+  store_env(v, i, e);
+}
+
+__global__ void __launch_bounds__(kBlock) k_move_look(View v, int64_t n, int p, const double* vals,
+                                                      double scalar, Cfg c) {
+  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  Env e;
+  load_env(v, i, e);
+  double x = vals ? vals[i] : scalar;
+  if (p == 0) move_look(c, e, 0, x); else move_look(c, e, 1, x);
+  store_env(v, i, e);
+}
+
+__global__ void __launch_bounds__(kBlock) k_move_discrete(View v, int64_t n, int p, int kind,
+                                                          const uint8_t* mask, Cfg c) {
+  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n || (mask && !mask[i])) return;
+  Env e;
+  load_env(v, i, e);
+  if (kind == 0) { if (p == 0) move_fwd_back(c, e, 0, false); else move_fwd_back(c, e, 1, false); }
+  else if (kind == 1) { if (p == 0) move_fwd_back(c, e, 0, true); else move_fwd_back(c, e, 1, true); }
+  else if (kind == 2) { if (p == 0) e.rot[0] += c.look; else e.rot[1] += c.look; }  // Player.py:27-28
+  else { if (p == 0) e.rot[0] -= c.look; else e.rot[1] -= c.look; }                  // Player.py:30-31
+  store_env(v, i, e);
+}
+
+__global__ void __launch_bounds__(kBlock) k_shoot(View v, int64_t n, int p, const uint8_t* mask, Cfg c) {
+  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n || (mask && !mask[i])) return;
+  Env e;
+  load_env(v, i, e);
+  if (p == 0) shoot(c, e, 0); else shoot(c, e, 1);
+  store_env(v, i, e);
+}
+
+__global__ void __launch_bounds__(kBlock) k_game_tick(View v, int64_t n, Cfg c) {
+  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  Env e;
+  load_env(v, i, e);
+  game_tick(c, e);
+  store_env(v, i, e);
+}
+
+__global__ void __launch_bounds__(kBlock) k_observe(View v, int64_t n, float* obs, float* reward, int kind,
+                                                    Cfg c) {
+  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  Env e;
+  load_env(v, i, e);
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    float o[12];
+    double pd;
+    obs12(c, e, p, o, &pd);
+    if (obs) store_obs(obs, n, p, i, o);
+    if (reward) reward[(int64_t)p * n + i] = reward_of(c, e, p, kind, pd);
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_features(View v, int64_t n, double* feat, Cfg c) {
+  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  Env e;
+  load_env(v, i, e);
+  for (int p = 0; p < 2; ++p) {
+    double f[18];
+    features18(c, e, p, f);
+    double* d = feat + (i * 2 + p) * 18;
+    for (int k = 0; k < 18; ++k) d[k] = f[k];
+  }
+}
+
+// ------------------------------------------------------------------ host ABI
+extern "C" {
+
+const char* sk_last_error(void) { return g_err.c_str(); }
+
+int sk_abi_version(void) { return SK_ABI_VERSION; }
+
+void sk_config_default(sk_config* c) {
+  if (!c) return;
+  c->board_w = 250; c->board_h = 250;
+  c->player_size = 5; c->projectile_size = 3;
+  c->player_speed = 3; c->projectile_speed = 5;
+  c->cooldown_max = 15; c->look_speed = 0.25;
+  c->fixed_p1_x = 50; c->fixed_p1_y = 50;
+  c->fixed_p2_x = 200; c->fixed_p2_y = 200;
+  c->rand_lo = 25; c->rand_hi = 225;
+}
+
+static Cfg to_dcfg(const sk_config& s) {
+  Cfg c;
+  c.W = s.board_w; c.H = s.board_h; c.psize = s.player_size; c.qsize = s.projectile_size;
+  c.pspeed = s.player_speed; c.qspeed = s.projectile_speed; c.cdmax = s.cooldown_max;
+  c.look = s.look_speed;
+  c.f1x = s.fixed_p1_x; c.f1y = s.fixed_p1_y; c.f2x = s.fixed_p2_x; c.f2y = s.fixed_p2_y;
+  c.rlo = s.rand_lo; c.rhi = s.rand_hi;
+  // (2 * (250 ** 2)) ** 0.5 : CPython float_pow -> libm pow(125000.0, 0.5)
+  c.max_dist = std::pow(2.0 * (double)s.board_w * (double)s.board_w, 0.5);
+  return c;
+}
+
+static int check_device(int32_t device) {
+  int count = 0;
+  hipError_t e = hipGetDeviceCount(&count);
+  if (e != hipSuccess || count == 0) return fail(SK_ENODEV, "no HIP device available");
+  if (device < 0 || device >= count) return fail(SK_EINVAL, "device index out of range");
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(SK_ENODEV, std::string("libskillshot is built for gfx950, device is ") + prop.gcnArchName);
+  return SK_OK;
+}
+
+static int validate_cfg(const sk_config& c) {
+  if (c.board_w <= 0 || c.board_h <= 0 || c.player_size <= 0 || c.projectile_size <= 0 ||
+      c.cooldown_max <= 0 || c.rand_hi <= c.rand_lo)
+    return fail(SK_EINVAL, "invalid sk_config");
+  return SK_OK;
+}
+
+static int make_env(sk_env** out, const sk_state_view* view, int32_t n, int64_t env_offset, uint64_t seed,
+                    int32_t device, const sk_config* cfg) {
+  if (!out) return fail(SK_EINVAL, "out is NULL");
+  *out = nullptr;
+  if (n <= 0) return fail(SK_EINVAL, "n_envs must be > 0");
+  int rc = check_device(device);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(device));
+  sk_env* e = new sk_env();
+  e->n = n;
+  e->env_offset = env_offset;
+  e->seed = seed;
+  e->device = device;
+  if (cfg) e->cfg = *cfg; else sk_config_default(&e->cfg);
+  if ((rc = validate_cfg(e->cfg))) { delete e; return rc; }
+  e->dcfg = to_dcfg(e->cfg);
+  e->parity = 0;
+  if (view) {
+    if (view->n_envs != n || !view->pos || !view->rot || !view->qpos || !view->qrot || !view->qcdage ||
+        !view->misc) {
+      delete e;
+      return fail(SK_EINVAL, "incomplete sk_state_view");
+    }
+    e->hview = *view;
+    e->owned = false;
+  } else {
+    e->owned = true;
+    e->hview.n_envs = n;
+    void* p = nullptr;
+    size_t bytes = (size_t)n * 88;
+    if (hipMalloc(&p, bytes) != hipSuccess) { delete e; return fail(SK_ENOMEM, "hipMalloc state"); }
+    char* b = (char*)p;  // 16-B planes first, int2 last: every plane stays 16-B aligned
+    e->hview.pos = (int32_t*)b; b += (size_t)n * 16;
+    e->hview.rot = (double*)b; b += (size_t)n * 16;
+    e->hview.qpos = (int32_t*)b; b += (size_t)n * 16;
+    e->hview.qrot = (double*)b; b += (size_t)n * 16;
+    e->hview.qcdage = (int32_t*)b; b += (size_t)n * 16;
+    e->hview.misc = (int32_t*)b;
+  }
+  e->view.pos = (int4*)e->hview.pos;
+  e->view.rot = (double2*)e->hview.rot;
+  e->view.qpos = (int4*)e->hview.qpos;
+  e->view.qrot = (double2*)e->hview.qrot;
+  e->view.qcdage = (int4*)e->hview.qcdage;
+  e->view.misc = (int2*)e->hview.misc;
+  for (void* p : {(void*)e->view.pos, (void*)e->view.rot, (void*)e->view.qpos, (void*)e->view.qrot,
+                  (void*)e->view.qcdage}) {
+    if (((uintptr_t)p) & 15) {
+      if (e->owned) (void)hipFree(e->hview.pos);
+      delete e;
+      return fail(SK_EINVAL, "state planes must be 16-byte aligned");
+    }
+  }
+  if (((uintptr_t)e->view.misc) & 7) {
+    if (e->owned) (void)hipFree(e->hview.pos);
+    delete e;
+    return fail(SK_EINVAL, "misc plane must be 8-byte aligned");
+  }
+  if (hipMalloc(&e->d_counters, sizeof(sk_counters) + 2 * sizeof(uint64_t)) != hipSuccess) {
+    if (e->owned) (void)hipFree(e->hview.pos);
+    delete e;
+    return fail(SK_ENOMEM, "hipMalloc counters");
+  }
+  HIP_TRY(hipMemset(e->d_counters, 0, sizeof(sk_counters) + 2 * sizeof(uint64_t)));
+  e->d_step = reinterpret_cast<uint64_t*>(e->d_counters + 1);
+  if (e->owned) {
+    k_reset<<<grid_for(n), kBlock, 0, 0>>>(e->view, n, nullptr, 0, seed, env_offset, StepRef{e->d_step, 0},
+                                           e->dcfg);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipDeviceSynchronize());
+    // creation does not consume a step value
+    HIP_TRY(hipMemset(e->d_step, 0, 2 * sizeof(uint64_t)));
+    HIP_TRY(hipDeviceSynchronize());
+  }
+  *out = e;
+  return SK_OK;
+}
+
+int sk_env_create(sk_env** out, int32_t n_envs, int64_t env_offset, uint64_t seed, int32_t device,
+                  const sk_config* cfg) {
+  return make_env(out, nullptr, n_envs, env_offset, seed, device, cfg);
+}
+
+int sk_env_attach(sk_env** out, const sk_state_view* view, int64_t env_offset, uint64_t seed, int32_t device,
+                  const sk_config* cfg) {
+  if (!view) return fail(SK_EINVAL, "view is NULL");
+  return make_env(out, view, view->n_envs, env_offset, seed, device, cfg);
+}
+
+int sk_env_destroy(sk_env* e) {
+  if (!e) return fail(SK_EINVAL, "NULL handle");
+  (void)hipSetDevice(e->device);
+  if (e->owned) (void)hipFree(e->hview.pos);
+  (void)hipFree(e->d_counters);
+  delete e;
+  return SK_OK;
+}
+
+int sk_env_get_view(const sk_env* e, sk_state_view* out) {
+  if (!e || !out) return fail(SK_EINVAL, "NULL argument");
+  *out = e->hview;
+  return SK_OK;
+}
+
+int sk_env_counters_ptr(const sk_env* e, sk_counters** out) {
+  if (!e || !out) return fail(SK_EINVAL, "NULL argument");
+  *out = e->d_counters;
+  return SK_OK;
+}
+
+int sk_env_read_counters(sk_env* e, sk_counters* out, void* stream) {
+  if (!e || !out) return fail(SK_EINVAL, "NULL argument");
+  HIP_TRY(hipMemcpyAsync(out, e->d_counters, sizeof(sk_counters), hipMemcpyDeviceToHost, (hipStream_t)stream));
+  HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  return SK_OK;
+}
+
+int sk_env_clear_counters(sk_env* e, void* stream) {
+  if (!e) return fail(SK_EINVAL, "NULL handle");
+  HIP_TRY(hipMemsetAsync(e->d_counters, 0, sizeof(sk_counters), (hipStream_t)stream));
+  return SK_OK;
+}
+
+int sk_env_get_step_counter(const sk_env* e, uint64_t* out) {
+  if (!e || !out) return fail(SK_EINVAL, "NULL argument");
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(out, e->d_step + e->parity, sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return SK_OK;
+}
+
+int sk_env_set_step_counter(sk_env* e, uint64_t v) {
+  if (!e) return fail(SK_EINVAL, "NULL handle");
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(e->d_step + e->parity, &v, sizeof(uint64_t), hipMemcpyHostToDevice));
+  return SK_OK;
+}
+
+#define SK_CHECK_ENV(e) \
+  if (!(e)) return fail(SK_EINVAL, "NULL handle")
+#define SK_CHECK_PID(pid) \
+  if ((pid) != 1 && (pid) != 2) return fail(SK_EINVAL, "player_id must be 1 or 2")
+#define SK_LAUNCH_CHECK() HIP_TRY(hipGetLastError())
+
+int sk_env_reset(sk_env* e, const uint8_t* mask, int32_t random_positions, void* stream) {
+  SK_CHECK_ENV(e);
+  k_reset<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(e->view, e->n, mask, random_positions, e->seed,
+                                                               e->env_offset, StepRef{e->d_step, e->parity}, e->dcfg);
+  SK_LAUNCH_CHECK();
+  e->parity ^= 1;
+  return SK_OK;
+}
+
+int sk_player_move_direction(sk_env* e, int32_t pid, const double* speeds, double scalar, void* stream) {
+  SK_CHECK_ENV(e);
+  SK_CHECK_PID(pid);
+  k_move_direction<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(e->view, e->n, pid - 1, speeds, scalar,
+                                                                        e->dcfg);
+  SK_LAUNCH_CHECK();
+  return SK_OK;
+}
+
+int sk_player_move_look(sk_env* e, int32_t pid, const double* angles, double scalar, void* stream) {
+  SK_CHECK_ENV(e);
+  SK_CHECK_PID(pid);
+  k_move_look<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(e->view, e->n, pid - 1, angles, scalar,
+                                                                   e->dcfg);
+  SK_LAUNCH_CHECK();
+  return SK_OK;
+}
+
+int sk_player_move_discrete(sk_env* e, int32_t pid, int32_t kind, const uint8_t* mask, void* stream) {
+  SK_CHECK_ENV(e);
+  SK_CHECK_PID(pid);
+  if (kind < 0 || kind > 3) return fail(SK_EINVAL, "kind must be 0..3");
+  k_move_discrete<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(e->view, e->n, pid - 1, kind, mask,
+                                                                       e->dcfg);
+  SK_LAUNCH_CHECK();
+  return SK_OK;
+}
+
+int sk_player_shoot(sk_env* e, int32_t pid, const uint8_t* mask, void* stream) {
+  SK_CHECK_ENV(e);
+  SK_CHECK_PID(pid);
+  k_shoot<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(e->view, e->n, pid - 1, mask, e->dcfg);
+  SK_LAUNCH_CHECK();
+  return SK_OK;
+}
+
+int sk_game_tick(sk_env* e, void* stream) {
+  SK_CHECK_ENV(e);
+  k_game_tick<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(e->view, e->n, e->dcfg);
+  SK_LAUNCH_CHECK();
+  return SK_OK;
+}
+
+int sk_env_features(sk_env* e, double* feat, void* stream) {
+  SK_CHECK_ENV(e);
+  if (!feat) return fail(SK_EINVAL, "feat is NULL");
+  k_features<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(e->view, e->n, feat, e->dcfg);
+  SK_LAUNCH_CHECK();
+  return SK_OK;
+}
+
+int sk_env_observe(sk_env* e, float* obs, float* reward, int32_t kind, void* stream) {
+  SK_CHECK_ENV(e);
+  if (kind != SK_REWARD_LOOKING && kind != SK_REWARD_SIMPLE) return fail(SK_EINVAL, "bad reward_kind");
+  if (((uintptr_t)obs) & 15) return fail(SK_EINVAL, "obs must be 16-byte aligned");
+  if (!obs && !reward) return SK_OK;
+  k_observe<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(e->view, e->n, obs, reward, kind, e->dcfg);
+  SK_LAUNCH_CHECK();
+  return SK_OK;
+}
+
+int sk_env_step(sk_env* e, const float* actions, float* obs, float* reward, int32_t reward_kind, uint8_t* done,
+                uint8_t* winner, int32_t tick_limit, int32_t auto_reset, int32_t random_positions,
+                float* obs_reset, void* stream) {
+  SK_CHECK_ENV(e);
+  if (!actions) return fail(SK_EINVAL, "actions is NULL");
+  if (((uintptr_t)actions) & 7) return fail(SK_EINVAL, "actions must be 8-byte aligned");
+  if ((((uintptr_t)obs) & 15) || (((uintptr_t)obs_reset) & 15))
+    return fail(SK_EINVAL, "obs buffers must be 16-byte aligned");
+  if (reward_kind != SK_REWARD_LOOKING && reward_kind != SK_REWARD_SIMPLE)
+    return fail(SK_EINVAL, "bad reward_kind");
+  StepArgs a;
+  a.v = e->view;
+  a.n = e->n;
+  a.actions = reinterpret_cast<const float2*>(actions);
+  a.obs = obs;
+  a.reward = reward;
+  a.reward_kind = reward_kind;
+  a.done = done;
+  a.winner = winner;
+  a.tick_limit = tick_limit;
+  a.auto_reset = auto_reset;
+  a.random_positions = random_positions;
+  a.obs_reset = obs_reset;
+  a.seed = e->seed;
+  a.env_offset = e->env_offset;
+  a.step = StepRef{e->d_step, e->parity};
+  a.ctr = e->d_counters;
+  k_step<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(a, e->dcfg);
+  SK_LAUNCH_CHECK();
+  e->parity ^= 1;
+  return SK_OK;
+}
+
+int sk_gen_random_actions(sk_env* e, float* actions, int32_t n_ticks, void* stream) {
+  SK_CHECK_ENV(e);
+  if (!actions || n_ticks <= 0) return fail(SK_EINVAL, "bad actions / n_ticks");
+  if (((uintptr_t)actions) & 7) return fail(SK_EINVAL, "actions must be 8-byte aligned");
+  k_gen_actions<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(
+      reinterpret_cast<float4*>(actions), e->n, n_ticks, e->seed, e->env_offset, StepRef{e->d_step, e->parity});
+  SK_LAUNCH_CHECK();
+  return SK_OK;
+}
+
+int sk_env_rollout_random(sk_env* e, int32_t n_ticks, int32_t tick_limit, void* stream) {
+  SK_CHECK_ENV(e);
+  if (n_ticks <= 0) return fail(SK_EINVAL, "n_ticks must be > 0");
+  RolloutArgs a;
+  a.v = e->view;
+  a.n = e->n;
+  a.n_ticks = n_ticks;
+  a.tick_limit = tick_limit;
+  a.seed = e->seed;
+  a.env_offset = e->env_offset;
+  a.step = StepRef{e->d_step, e->parity};
+  a.ctr = e->d_counters;
+  k_rollout_random<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(a, e->dcfg);
+  SK_LAUNCH_CHECK();
+  e->parity ^= 1;
+  return SK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,274 @@
+"""VecSkillshotGame — N Skillshot games stepped on one MI355X by libskillshot.
+
+State lives in HBM as torch tensors (the struct-of-arrays layout of
+include/skillshot.h) that the C engine is attached to, so observations,
+rewards and the state itself are torch tensors with no copies.  Every method
+is the batched form of a reference method (cited per method); the fused
+`step` is the learner's whole per-tick protocol (SkillshotLearner.py:302-324)
+in one kernel launch.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _capi
+from ._capi import SkillshotError, check
+
+PLANES = (("pos", torch.int32, 4), ("rot", torch.float64, 2), ("qpos", torch.int32, 4),
+          ("qrot", torch.float64, 2), ("qcdage", torch.int32, 4), ("misc", torch.int32, 2))
+
+REWARD_KINDS = {"looking": _capi.SK_REWARD_LOOKING, "simple": _capi.SK_REWARD_SIMPLE}
+
+# get_state per-player key order (SkillshotGame.py:145-163); sk_env_features columns
+FEATURE_KEYS = ("player_grad", "player_x_dir", "player_path_dist_opponent", "player_dist_opponent",
+                "player_pos_x", "player_pos_y", "player_rotation", "projectile_cooldown",
+                "projectile_grad", "projectile_x_dir", "projectile_path_dist_opponent",
+                "projectile_pos_x", "projectile_pos_y", "projectile_rotation", "projectile_age",
+                "projectile_valid", "projectile_dist_opponent", "projectile_future_collision_opponent")
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _require_gpu(device):
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        raise SkillshotError("VecSkillshotGame runs on a gfx950 GPU only (no CPU fallback)")
+    if not torch.cuda.is_available():
+        raise SkillshotError("no GPU visible: libskillshot has no CPU fallback")
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    return torch.device("cuda", idx)
+
+
+class VecSkillshotGame:
+    """N independent games (the reference SkillshotGame, batched).
+
+    n_envs      games on this device
+    env_offset  global id of game 0 (multi-GPU sharding; RNG is keyed by global id)
+    seed        Philox key for random starts / random-policy actions
+    tick_limit  episode length cap (SkillshotLearner.model_param_game_tick_limit, :62)
+    random_positions  use random starts on reset (SkillshotLearner.use_random_start, :44)
+    """
+
+    def __init__(self, n_envs, device="cuda", seed=0, env_offset=0, tick_limit=2000,
+                 random_positions=True, config=None):
+        self.device = _require_gpu(device)
+        self.n = int(n_envs)
+        if self.n <= 0:
+            raise ValueError("n_envs must be > 0")
+        self.seed = int(seed)
+        self.env_offset = int(env_offset)
+        self.tick_limit = int(tick_limit)
+        self.random_positions = bool(random_positions)
+        self._L = _capi.load()
+        with torch.cuda.device(self.device):
+            for name, dt, w in PLANES:
+                setattr(self, name, torch.zeros((self.n, w), dtype=dt, device=self.device))
+        view = _capi.SkStateView(self.n, *[getattr(self, name).data_ptr() for name, _, _ in PLANES])
+        cfg = config if config is not None else _capi.default_config()
+        self.config = cfg
+        h = ctypes.c_void_p()
+        torch.cuda.synchronize(self.device)
+        check(self._L.sk_env_attach(ctypes.byref(h), ctypes.byref(view), self.env_offset, self.seed,
+                                    self.device.index, ctypes.byref(cfg)))
+        self._h = h
+        cp = ctypes.c_void_p()
+        check(self._L.sk_env_counters_ptr(self._h, ctypes.byref(cp)))
+        self._counters_ptr = cp.value
+        self.reset(random_positions=False)
+
+    # ------------------------------------------------------------------ utils
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            torch.cuda.synchronize(self.device)
+            self._L.sk_env_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def step_counter(self):
+        v = ctypes.c_uint64()
+        check(self._L.sk_env_get_step_counter(self._h, ctypes.byref(v)))
+        return v.value
+
+    @step_counter.setter
+    def step_counter(self, value):
+        check(self._L.sk_env_set_step_counter(self._h, int(value)))
+
+    def state_dict(self):
+        """Host copy of the state planes (engine layout) + RNG counter."""
+        d = {name: getattr(self, name).cpu().numpy().copy() for name, _, _ in PLANES}
+        d["step_counter"] = self.step_counter
+        return d
+
+    def load_state_dict(self, d):
+        torch.cuda.synchronize(self.device)
+        for name, dt, w in PLANES:
+            src = torch.as_tensor(np.asarray(d[name]).reshape(self.n, w)).to(dt)
+            getattr(self, name).copy_(src)
+        if "step_counter" in d:
+            self.step_counter = int(d["step_counter"])
+        torch.cuda.synchronize(self.device)
+
+    # convenience decoded views -------------------------------------------
+    @property
+    def ticks(self):
+        return self.misc[:, 0]
+
+    @property
+    def flags(self):
+        return self.misc[:, 1]
+
+    @property
+    def game_live(self):
+        return ((self.misc[:, 1] >> 16) & 0xFF).to(torch.bool)
+
+    @property
+    def winner_id(self):
+        return ((self.misc[:, 1] >> 24) & 0xFF).to(torch.uint8)
+
+    @property
+    def projectile_valid(self):
+        f = self.misc[:, 1]
+        return torch.stack([(f & 0xFF), (f >> 8) & 0xFF], -1).to(torch.bool)
+
+    def counters(self):
+        """Episode counters (dones, hits by id, tick sum) accumulated on device
+        by the step kernels' wavefront ballots."""
+        c = _capi.SkCounters()
+        check(self._L.sk_env_read_counters(self._h, ctypes.byref(c), self._stream()))
+        return dict(dones=c.dones, hits_p1=c.hits_p1, hits_p2=c.hits_p2, ticks_sum=c.ticks_sum)
+
+    def clear_counters(self):
+        check(self._L.sk_env_clear_counters(self._h, self._stream()))
+
+    # ------------------------------------------------------------ reference API
+    def reset(self, mask=None, random_positions=None):
+        """SkillshotGame.game_reset (SkillshotGame.py:168-169) for masked envs."""
+        rp = self.random_positions if random_positions is None else bool(random_positions)
+        m = None if mask is None else self._u8(mask)
+        check(self._L.sk_env_reset(self._h, _ptr(m), int(rp), self._stream()))
+
+    def move_direction(self, player_id, speeds):
+        """Player.move_direction_float (Player.py:57-68) for one player of every env."""
+        v, s = self._f64_or_scalar(speeds)
+        check(self._L.sk_player_move_direction(self._h, int(player_id), _ptr(v), s, self._stream()))
+
+    def move_look(self, player_id, angles):
+        """Player.move_look_float (Player.py:33-39)."""
+        v, s = self._f64_or_scalar(angles)
+        check(self._L.sk_player_move_look(self._h, int(player_id), _ptr(v), s, self._stream()))
+
+    def move_discrete(self, player_id, kind, mask=None):
+        """Keyboard moves (Player.py:27-55): kind 0 forwards, 1 backwards, 2 look left, 3 look right."""
+        m = None if mask is None else self._u8(mask)
+        check(self._L.sk_player_move_discrete(self._h, int(player_id), int(kind), _ptr(m), self._stream()))
+
+    def shoot(self, player_id, mask=None):
+        """Player.move_shoot_projectile (Player.py:78-89) for masked envs."""
+        m = None if mask is None else self._u8(mask)
+        check(self._L.sk_player_shoot(self._h, int(player_id), _ptr(m), self._stream()))
+
+    def game_tick(self):
+        """SkillshotGame.game_tick (SkillshotGame.py:115-122)."""
+        check(self._L.sk_game_tick(self._h, self._stream()))
+
+    def features(self, out=None):
+        """get_state() numerics (SkillshotGame.py:136-166): float64 [N, 2, 18] in FEATURE_KEYS order."""
+        f = out if out is not None else torch.empty((self.n, 2, 18), dtype=torch.float64, device=self.device)
+        check(self._L.sk_env_features(self._h, _ptr(f), self._stream()))
+        return f
+
+    def observe(self, reward="looking", obs_out=None, reward_out=None):
+        """prepare_states (SkillshotLearner.py:512-543) -> obs [2,N,12] f32 and
+        calculate_rewards_<reward> (:575-603) -> reward [2,N] f32 of the current state."""
+        obs = obs_out if obs_out is not None else self.new_obs()
+        rew = reward_out if reward_out is not None else torch.empty((2, self.n), dtype=torch.float32,
+                                                                      device=self.device)
+        check(self._L.sk_env_observe(self._h, _ptr(obs), _ptr(rew), REWARD_KINDS[reward], self._stream()))
+        return obs, rew
+
+    # ---------------------------------------------------------------- hot path
+    def new_obs(self):
+        return torch.empty((2, self.n, 12), dtype=torch.float32, device=self.device)
+
+    def step(self, actions, obs=True, reward="looking", auto_reset=True, reset_obs=False, out=None):
+        """One learner tick for every env (SkillshotLearner.py:302-324), one launch.
+
+        actions: float32 [2, N, 2] (player, env, {speed, look}).
+        Returns dict(obs [2,N,12] | None, reward [2,N] | None, done u8[N], winner u8[N],
+        obs_reset [2,N,12] | None): obs/reward/done/winner describe the post-tick
+        (terminal) state; with auto_reset the done envs are then reset and
+        obs_reset holds the obs the next tick acts on.
+        """
+        a = self._actions(actions)
+        o = out or {}
+        obs_t = (o.get("obs") if o.get("obs") is not None else self.new_obs()) if obs else None
+        rew_t = (o.get("reward") if o.get("reward") is not None else
+                 torch.empty((2, self.n), dtype=torch.float32, device=self.device)) if obs else None
+        done = o.get("done") if o.get("done") is not None else torch.empty(self.n, dtype=torch.uint8,
+                                                                            device=self.device)
+        win = o.get("winner") if o.get("winner") is not None else torch.empty(self.n, dtype=torch.uint8,
+                                                                               device=self.device)
+        obs_r = (o.get("obs_reset") if o.get("obs_reset") is not None else self.new_obs()) if reset_obs else None
+        check(self._L.sk_env_step(self._h, _ptr(a), _ptr(obs_t), _ptr(rew_t), REWARD_KINDS[reward], _ptr(done),
+                                  _ptr(win), self.tick_limit, int(bool(auto_reset)), int(self.random_positions),
+                                  _ptr(obs_r), self._stream()))
+        return dict(obs=obs_t, reward=rew_t, done=done, winner=win, obs_reset=obs_r)
+
+    def step_raw(self, actions_ptr, done_ptr=None, obs_ptr=None, reward_ptr=None, winner_ptr=None,
+                 auto_reset=True, stream=None):
+        """Pointer-level fused step (bench / graph capture; no allocation)."""
+        check(self._L.sk_env_step(self._h, actions_ptr, obs_ptr, reward_ptr, 0, done_ptr, winner_ptr,
+                                  self.tick_limit, int(bool(auto_reset)), int(self.random_positions), None,
+                                  stream if stream is not None else self._stream()))
+
+    def gen_random_actions(self, n_ticks, out=None):
+        """Random-policy actions float32 [n_ticks, 2, N, 2] (config 2 synthetic input)."""
+        a = out if out is not None else torch.empty((n_ticks, 2, self.n, 2), dtype=torch.float32,
+                                                    device=self.device)
+        check(self._L.sk_gen_random_actions(self._h, _ptr(a), int(n_ticks), self._stream()))
+        return a
+
+    def rollout_random(self, n_ticks):
+        """n_ticks random-policy ticks with auto-reset, one launch, state in registers."""
+        check(self._L.sk_env_rollout_random(self._h, int(n_ticks), self.tick_limit, self._stream()))
+
+    # ---------------------------------------------------------------- helpers
+    def _u8(self, mask):
+        m = torch.as_tensor(mask, device=self.device)
+        if m.dtype != torch.uint8:
+            m = m.to(torch.uint8)
+        m = m.contiguous()
+        if m.numel() != self.n:
+            raise ValueError("mask must have n_envs elements")
+        return m
+
+    def _f64_or_scalar(self, x):
+        if isinstance(x, (int, float)):
+            return None, float(x)
+        t = torch.as_tensor(x, device=self.device).to(torch.float64).contiguous()
+        if t.numel() == 1:
+            return None, float(t.item())
+        if t.numel() != self.n:
+            raise ValueError("need one value per env")
+        return t, 0.0
+
+    def _actions(self, actions):
+        a = torch.as_tensor(actions, device=self.device)
+        if a.dtype != torch.float32:
+            a = a.to(torch.float32)
+        a = a.contiguous()
+        if tuple(a.shape) != (2, self.n, 2):
+            raise ValueError(f"actions must be float32 [2, {self.n}, 2], got {tuple(a.shape)}")
+        return a

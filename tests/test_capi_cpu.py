@@ -1,0 +1,76 @@
+"""CPU-side checks of the drop-in boundary: libskillshot builds, loads, exports
+every symbol include/skillshot.h declares, and fails loudly without a GPU
+(no CPU fallback)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+import torch
+
+import skillshot_learning_amd as ssa
+from skillshot_learning_amd import _capi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "skillshot.h")
+
+
+def header_symbols():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(sk_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_header_and_binding_agree():
+    assert header_symbols() == sorted(_capi.EXPORTS)
+
+
+def test_library_exports_every_header_symbol():
+    path = _capi.lib_path()
+    ssa.load_library()
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (sk_[a-z_0-9]+)$", out, flags=re.M))
+    missing = set(header_symbols()) - exported
+    assert not missing, missing
+    L = ssa.load_library()
+    for name in header_symbols():
+        assert getattr(L, name) is not None
+
+
+def test_library_is_gfx950_code_object():
+    data = open(_capi.lib_path(), "rb").read()
+    assert b"hipv4-amdgcn-amd-amdhsa--gfx950" in data  # the offload bundle targets gfx950 only
+    assert b"--gfx94" not in data and b"--gfx90" not in data
+
+
+def test_default_config_is_reference():
+    c = _capi.default_config()
+    # SkillshotGame.py:11,17-18,15 ; Player.py:9-15 ; Projectile.py:5-10
+    assert (c.board_w, c.board_h) == (250, 250)
+    assert (c.player_size, c.projectile_size) == (5, 3)
+    assert (c.player_speed, c.projectile_speed, c.cooldown_max) == (3, 5, 15)
+    assert c.look_speed == 0.25
+    assert (c.fixed_p1_x, c.fixed_p1_y, c.fixed_p2_x, c.fixed_p2_y) == (50, 50, 200, 200)
+    assert (c.rand_lo, c.rand_hi) == (25, 225)
+
+
+def test_abi_errors_without_device():
+    L = ssa.load_library()
+    h = ctypes.c_void_p()
+    assert L.sk_env_create(ctypes.byref(h), 0, 0, 0, 0, None) == _capi.SK_EINVAL
+    assert b"n_envs" in L.sk_last_error()
+    assert L.sk_env_destroy(None) == _capi.SK_EINVAL
+    assert L.sk_env_step(None, None, None, None, 0, None, None, 0, 0, 0, None, None) == _capi.SK_EINVAL
+    if not torch.cuda.is_available():
+        rc = L.sk_env_create(ctypes.byref(h), 16, 0, 0, 0, None)
+        assert rc == _capi.SK_ENODEV
+        assert h.value is None
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU failure path")
+def test_no_cpu_fallback():
+    with pytest.raises(ssa.SkillshotError):
+        ssa.VecSkillshotGame(8, device="cuda")
+    with pytest.raises(ssa.SkillshotError):
+        ssa.VecSkillshotGame(8, device="cpu")

@@ -1,0 +1,283 @@
+"""GPU parity: the HIP engine (libskillshot, through the C ABI) against the
+reference golden vectors and the CPU oracle.
+
+Bar: bit-exact on every state field (positions, fp64
+rotations, projectile state, ticks, live, winner) and on done/winner;
+obs/reward within 1e-5 relative to max(1,|ref|); the future-collision flag
+(obs[11]) exact.
+"""
+import numpy as np
+import pytest
+import torch
+
+import golden_replay as gr
+
+pytestmark = pytest.mark.gpu
+
+OBS_TOL = 1e-5
+
+
+@pytest.fixture(scope="module")
+def ssa():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import skillshot_learning_amd as m
+    m.load_library()
+    return m
+
+
+def to_np(arrs):
+    return {k: (v.cpu().numpy() if torch.is_tensor(v) else v) for k, v in arrs.items()}
+
+
+class GpuEngine:
+    """Adapter: golden_replay's engine protocol over VecSkillshotGame."""
+
+    def __init__(self, ssa, n, **kw):
+        self.g = ssa.VecSkillshotGame(n, **kw)
+
+    def load(self, arrays):
+        self.g.load_state_dict(arrays)
+
+    def arrays(self):
+        torch.cuda.synchronize()
+        d = self.g.state_dict()
+        d.pop("step_counter")
+        return d
+
+    def step(self, actions, tick_limit):
+        self.g.tick_limit = tick_limit
+        out = self.g.step(torch.as_tensor(actions).cuda(), obs=True, auto_reset=False)
+        return to_np(out)
+
+    def move_direction(self, pid, v):
+        self.g.move_direction(pid, torch.as_tensor(v).cuda())
+
+    def move_look(self, pid, v):
+        self.g.move_look(pid, torch.as_tensor(v).cuda())
+
+    def shoot(self, pid, mask):
+        self.g.shoot(pid, torch.as_tensor(mask).cuda())
+
+    def game_tick(self):
+        self.g.game_tick()
+
+    def observe(self):
+        o, r = self.g.observe()
+        return o.cpu().numpy(), r.cpu().numpy()
+
+
+@pytest.mark.parametrize("name", gr.fixture_names())
+def test_golden_fixture(ssa, name):
+    d = gr.load(name)
+    n = gr.replay(GpuEngine(ssa, d["pos"].shape[0]), d, obs_tol=OBS_TOL)
+    assert n == int(d["n_steps"].sum())
+
+
+def _random_state(oracle_mod, n, seed):
+    s = oracle_mod.OracleState(n, seed=seed)
+    s.reset(random_positions=True)
+    return s
+
+
+def _assert_state_equal(got, want, where):
+    for k in want:
+        g, w = np.asarray(got[k]), np.asarray(want[k])
+        if k in ("rot", "qrot"):
+            same = (g.view(np.int64) == w.view(np.int64)) | ((g == 0) & (w == 0))
+        else:
+            same = g == w
+        if not same.all():
+            bad = np.argwhere(~same)
+            raise AssertionError(f"{where}: {k} differs in {len(bad)} entries, first {bad[0]}: "
+                                 f"{g[tuple(bad[0])]} vs {w[tuple(bad[0])]}")
+
+
+def test_fused_step_matches_oracle_random_policy(ssa, oracle_mod):
+    """8192 envs x 2500 ticks, random policy, random auto-reset (the learner
+    protocol of configs 2/3): state bit-exact every 100 ticks, obs/reward/done/
+    winner compared on sampled ticks, counters equal."""
+    n, T = 8192, 2500
+    ref = _random_state(oracle_mod, n, seed=42)
+    g = ssa.VecSkillshotGame(n, seed=42, tick_limit=2000)
+    g.load_state_dict(ref.arrays())
+    g.step_counter = ref.step_counter
+    g.clear_counters()
+    checked = 0
+    for t in range(T):
+        acts = g.gen_random_actions(1)[0]
+        ra = ref.gen_random_actions(1)[0]
+        want_obs = (t % 97 == 0) or t == T - 1
+        out = g.step(acts, obs=want_obs, auto_reset=True, reset_obs=want_obs)
+        wo = ref.step(ra, tick_limit=2000, auto_reset=True, random_positions=True, want_obs=want_obs,
+                      want_reset_obs=want_obs)
+        if want_obs or t % 100 == 0:
+            torch.cuda.synchronize()
+            assert np.array_equal(acts.cpu().numpy(), ra), f"actions t={t}"
+            assert np.array_equal(out["done"].cpu().numpy(), wo["done"]), f"done t={t}"
+            assert np.array_equal(out["winner"].cpu().numpy(), wo["winner"]), f"winner t={t}"
+            st = g.state_dict()
+            st.pop("step_counter")
+            _assert_state_equal(st, ref.arrays(), f"t={t}")
+        if want_obs:
+            o = out["obs"].cpu().numpy().astype(np.float64)
+            err = np.abs(o - wo["obs"]) / np.maximum(1.0, np.abs(wo["obs"]))
+            assert err.max() <= OBS_TOL, (t, err.max())
+            assert np.array_equal(o[..., 11], wo["obs"][..., 11])
+            r = out["reward"].cpu().numpy().astype(np.float64)
+            assert (np.abs(r - wo["reward"]) / np.maximum(1.0, np.abs(wo["reward"]))).max() <= OBS_TOL
+            orr = out["obs_reset"].cpu().numpy().astype(np.float64)
+            assert (np.abs(orr - wo["obs_reset"]) / np.maximum(1.0, np.abs(wo["obs_reset"]))).max() <= OBS_TOL
+            checked += 1
+    c = g.counters()
+    assert [c["dones"], c["hits_p1"], c["hits_p2"], c["ticks_sum"]] == [int(x) for x in ref.counters]
+    assert c["dones"] > 1000 and c["hits_p1"] > 0 and c["hits_p2"] > 0
+    assert checked > 10
+
+
+@pytest.mark.parametrize("n,T", [(65536, 600), (1000, 4100)])
+def test_rollout_random_matches_oracle(ssa, oracle_mod, n, T):
+    """The multi-tick register-resident random-policy kernel (bench path) is
+    bit-identical to the oracle's rollout, including ragged N (not a multiple
+    of the 256-lane workgroup) and episodes crossing the 2000-tick limit."""
+    ref = _random_state(oracle_mod, n, seed=7)
+    g = ssa.VecSkillshotGame(n, seed=7, tick_limit=2000)
+    g.load_state_dict(ref.arrays())
+    g.step_counter = ref.step_counter
+    g.clear_counters()
+    done_ticks = 0
+    for chunk in (1, T // 3, T - 1 - T // 3):
+        g.rollout_random(chunk)
+        ref.rollout_random(chunk, tick_limit=2000)
+        done_ticks += chunk
+        torch.cuda.synchronize()
+        st = g.state_dict()
+        assert st.pop("step_counter") == ref.step_counter
+        _assert_state_equal(st, ref.arrays(), f"after {done_ticks} ticks")
+    c = g.counters()
+    assert [c["dones"], c["hits_p1"], c["hits_p2"], c["ticks_sum"]] == [int(x) for x in ref.counters]
+
+
+def test_rollout_equals_stepwise_on_gpu(ssa):
+    """rollout_random(T) == T x (gen_random_actions + fused step) on device."""
+    n, T = 3000, 300
+    a = ssa.VecSkillshotGame(n, seed=3, tick_limit=120)
+    a.reset(random_positions=True)
+    b = ssa.VecSkillshotGame(n, seed=3, tick_limit=120)
+    b.load_state_dict(a.state_dict())
+    a.rollout_random(T)
+    for _ in range(T):
+        b.step(b.gen_random_actions(1)[0], obs=False, auto_reset=True)
+    sa, sb = a.state_dict(), b.state_dict()
+    for k in sa:
+        assert np.array_equal(np.asarray(sa[k]), np.asarray(sb[k])), k
+    assert a.counters() == b.counters()
+
+
+def test_sharding_invariance(ssa):
+    """Envs are keyed by GLOBAL id: two half-size shards (env_offset) equal one
+    full run, the multi-GPU decomposition of SURVEY.md §8(e)."""
+    n, T = 4096, 500
+    full = ssa.VecSkillshotGame(n, seed=11, tick_limit=300)
+    full.reset(random_positions=True)
+    lo = ssa.VecSkillshotGame(n // 2, seed=11, env_offset=0, tick_limit=300)
+    hi = ssa.VecSkillshotGame(n // 2, seed=11, env_offset=n // 2, tick_limit=300)
+    lo.reset(random_positions=True)
+    hi.reset(random_positions=True)
+    full.rollout_random(T)
+    lo.rollout_random(T)
+    hi.rollout_random(T)
+    f, a, b = full.state_dict(), lo.state_dict(), hi.state_dict()
+    for k in f:
+        if k == "step_counter":
+            continue
+        assert np.array_equal(f[k], np.concatenate([a[k], b[k]])), k
+
+
+def test_features_match_oracle(ssa, oracle_mod):
+    n = 20000
+    ref = _random_state(oracle_mod, n, seed=5)
+    # advance to get valid projectiles / varied rotations
+    ref.rollout_random(37, tick_limit=2000)
+    g = ssa.VecSkillshotGame(n)
+    g.load_state_dict(ref.arrays())
+    f = g.features().cpu().numpy()
+    w = ref.features()
+    # exact columns: x_dir, positions, rotation, cooldown, age, valid, future collision
+    exact = [1, 4, 5, 6, 7, 9, 11, 12, 13, 14, 15, 17]
+    assert np.array_equal(f[..., exact], w[..., exact])
+    err = np.abs(f - w) / np.maximum(1.0, np.abs(w))
+    assert err.max() <= 1e-12, err.max()
+
+
+def test_per_method_ops_match_oracle(ssa, oracle_mod):
+    """Discrete keyboard moves, masked shoot/reset, look and direction with
+    per-env and scalar arguments, reward 'simple'."""
+    n = 5000
+    rng = np.random.default_rng(0)
+    ref = _random_state(oracle_mod, n, seed=8)
+    g = ssa.VecSkillshotGame(n, seed=8)
+    g.load_state_dict(ref.arrays())
+    g.step_counter = ref.step_counter
+    for t in range(200):
+        pid = 1 + (t % 2)
+        sp = rng.uniform(-1.5, 1.5, n)
+        ang = rng.uniform(-1.5, 1.5, n)
+        mask = (rng.random(n) < 0.3).astype(np.uint8)
+        kind = int(rng.integers(0, 4))
+        g.move_direction(pid, torch.as_tensor(sp).cuda())
+        ref.move_direction(pid, sp)
+        g.move_look(pid, 0.125 if t % 5 == 0 else torch.as_tensor(ang).cuda())
+        ref.move_look(pid, 0.125 if t % 5 == 0 else ang)
+        g.move_discrete(pid, kind, torch.as_tensor(mask).cuda())
+        ref.move_discrete(pid, kind, mask)
+        if t % 3 == 0:
+            g.shoot(pid, torch.as_tensor(1 - mask).cuda())
+            ref.shoot(pid, 1 - mask)
+        g.game_tick()
+        ref.game_tick()
+        if t % 50 == 49:
+            rmask = (rng.random(n) < 0.1).astype(np.uint8)
+            g.reset(torch.as_tensor(rmask).cuda(), random_positions=True)
+            ref.reset(rmask, random_positions=True)
+    torch.cuda.synchronize()
+    st = g.state_dict()
+    assert st.pop("step_counter") == ref.step_counter
+    _assert_state_equal(st, ref.arrays(), "per-method")
+    o, r = g.observe(reward="simple")
+    wo, wr = ref.observe(reward_kind=1)
+    assert (np.abs(o.cpu().numpy() - wo) / np.maximum(1, np.abs(wo))).max() <= OBS_TOL
+    assert (np.abs(r.cpu().numpy() - wr) / np.maximum(1, np.abs(wr))).max() <= OBS_TOL
+
+
+def test_large_batch_invariants(ssa):
+    """Size-independent properties at the bench size (65,536 envs, config 2):
+    bounds, tick limit, cooldown range under the always-shoot protocol, and
+    counter consistency."""
+    n = 65536
+    g = ssa.VecSkillshotGame(n, seed=1, tick_limit=2000)
+    g.reset(random_positions=True)
+    g.clear_counters()
+    g.rollout_random(3000)
+    torch.cuda.synchronize()
+    pos = g.pos.cpu().numpy()
+    assert pos.min() >= 0 and pos.max() <= 245
+    assert int(g.ticks.max()) <= 2000 and int(g.ticks.min()) >= 0
+    cd = g.qcdage[:, [0, 2]].cpu().numpy()
+    assert cd.min() >= 0 and cd.max() <= 15
+    c = g.counters()
+    assert c["dones"] >= c["hits_p1"] + c["hits_p2"]
+    assert c["dones"] > n // 2
+    # random policy: hits split about evenly between ids
+    frac = c["hits_p1"] / max(1, c["hits_p1"] + c["hits_p2"])
+    assert 0.4 < frac < 0.6
+    mean_len = c["ticks_sum"] / c["dones"]
+    assert 500 < mean_len < 1800
+
+
+def test_errors_are_loud(ssa):
+    g = ssa.VecSkillshotGame(64)
+    with pytest.raises(ValueError):
+        g.step(torch.zeros(2, 63, 2, device="cuda"))
+    with pytest.raises(ssa.SkillshotError):
+        g.move_direction(3, 0.5)
