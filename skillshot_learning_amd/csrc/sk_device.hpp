@@ -131,6 +131,8 @@ __device__ __forceinline__ void reset_random(const Cfg& c, Env& e, uint64_t seed
 }
 
 // ---------------------------------------------------------------- Player
+// Scalar per-player helpers: a kernel may hold one player per lane (the split
+// kernel) or both players of an env per lane (the Env wrappers below).
 __device__ __forceinline__ double clamp_action(double a) {  // Player.py:36-37, :60-61
   a = (a >= 1.0) ? 1.0 : a;
   a = (a <= -1.0) ? -1.0 : a;
@@ -142,42 +144,43 @@ __device__ __forceinline__ bool player_pos_valid(const Cfg& c, int x, int y) {  
 }
 
 // Player.move_direction_float (Player.py:57-68)
-__device__ __forceinline__ void move_direction(const Cfg& c, Env& e, int p, double speed) {
+__device__ __forceinline__ void move_direction_s(const Cfg& c, int& x, int& y, double rot, double speed) {
   speed = clamp_action(speed);
   double s, co;
-  sincos(e.rot[p], &s, &co);
+  sincos(rot, &s, &co);
   const double sp = (double)c.pspeed;
-  double nxf = __builtin_rint((double)e.px[p] - (s * sp) * speed);
-  double nyf = __builtin_rint((double)e.py[p] - (co * sp) * speed);
+  double nxf = __builtin_rint((double)x - (s * sp) * speed);
+  double nyf = __builtin_rint((double)y - (co * sp) * speed);
   // compare in fp64 first: a NaN speed (the reference raises ValueError in
   // int(round(nan))) never commits a move here
   bool ok = (nxf >= 0.0) & (nxf + (double)c.psize <= (double)c.W) & (nyf >= 0.0) &
             (nyf + (double)c.psize <= (double)c.H);
-  if (ok) { e.px[p] = (int)nxf; e.py[p] = (int)nyf; }
+  if (ok) { x = (int)nxf; y = (int)nyf; }
 }
 
 // Player.move_forwards / move_backwards (Player.py:41-55)
-__device__ __forceinline__ void move_fwd_back(const Cfg& c, Env& e, int p, bool backwards) {
+__device__ __forceinline__ void move_fwd_back_s(const Cfg& c, int& x, int& y, double rot, bool backwards) {
   double s, co;
-  sincos(e.rot[p], &s, &co);
+  sincos(rot, &s, &co);
   double dx = s * (double)c.pspeed, dy = co * (double)c.pspeed;
-  double nxf = backwards ? __builtin_rint((double)e.px[p] + dx) : __builtin_rint((double)e.px[p] - dx);
-  double nyf = backwards ? __builtin_rint((double)e.py[p] + dy) : __builtin_rint((double)e.py[p] - dy);
+  double nxf = backwards ? __builtin_rint((double)x + dx) : __builtin_rint((double)x - dx);
+  double nyf = backwards ? __builtin_rint((double)y + dy) : __builtin_rint((double)y - dy);
   int nx = (int)nxf, ny = (int)nyf;
-  if (player_pos_valid(c, nx, ny)) { e.px[p] = nx; e.py[p] = ny; }
+  if (player_pos_valid(c, nx, ny)) { x = nx; y = ny; }
 }
 
 // Player.move_look_float (Player.py:33-39)
-__device__ __forceinline__ void move_look(const Cfg& c, Env& e, int p, double angle) {
+__device__ __forceinline__ void move_look_s(const Cfg& c, double& rot, double angle) {
   angle = clamp_action(angle);
-  e.rot[p] = e.rot[p] + angle * c.look;
+  rot = rot + angle * c.look;
 }
 
 // Player.move_shoot_projectile (Player.py:78-89)
-__device__ __forceinline__ void shoot(const Cfg& c, Env& e, int p) {
-  if (e.qcd[p] <= 0) {
-    e.qx[p] = e.px[p]; e.qy[p] = e.py[p]; e.qrot[p] = e.rot[p];
-    e.qvalid[p] = 1; e.qcd[p] = c.cdmax; e.qage[p] = 0;
+__device__ __forceinline__ void shoot_s(const Cfg& c, int px, int py, double rot, int& qx, int& qy, double& qrot,
+                                        int& qcd, int& qage, int& qvalid) {
+  if (qcd <= 0) {
+    qx = px; qy = py; qrot = rot;
+    qvalid = 1; qcd = c.cdmax; qage = 0;
   }
 }
 
@@ -185,30 +188,54 @@ __device__ __forceinline__ void shoot(const Cfg& c, Env& e, int p) {
 // Projectile.tick (Projectile.py:49-53) -> move_forwards (:38-47).  An invalid
 // projectile's candidate position is never committed (valid stays False), so
 // its trig is skipped: no observable difference.
-__device__ __forceinline__ void projectile_tick(const Cfg& c, Env& e, int p) {
-  if (e.qvalid[p]) {
+__device__ __forceinline__ void projectile_tick_s(const Cfg& c, int& qx, int& qy, double qrot, int& qcd,
+                                                  int& qage, int& qvalid) {
+  if (qvalid) {
     double s, co;
-    sincos(e.qrot[p], &s, &co);
+    sincos(qrot, &s, &co);
     const double sp = (double)c.qspeed;
-    int nx = (int)__builtin_rint((double)e.qx[p] - s * sp);
-    int ny = (int)__builtin_rint((double)e.qy[p] - co * sp);
+    int nx = (int)__builtin_rint((double)qx - s * sp);
+    int ny = (int)__builtin_rint((double)qy - co * sp);
     bool ok = (nx + c.qsize <= c.W) & (nx >= 0) & (ny + c.qsize <= c.H) & (ny >= 0);
-    if (ok) { e.qx[p] = nx; e.qy[p] = ny; } else { e.qvalid[p] = 0; }
+    if (ok) { qx = nx; qy = ny; } else { qvalid = 0; }
   }
-  e.qcd[p] -= 1;
-  e.qage[p] += 1;
+  qcd -= 1;
+  qage += 1;
 }
 
 // SkillshotGame.check_collision (SkillshotGame.py:58-94): integer corner test
-// of player p's box against the OTHER player's projectile corners
-// x in {qx+3, qx}, y in {qy, qy-3}; player 1 is tested first and wins ties.
-__device__ __forceinline__ bool hit_test(const Cfg& c, const Env& e, int p) {
-  int q = 1 - p;
-  int L = e.px[p], R = e.px[p] + c.psize, T = e.py[p], B = e.py[p] + c.psize;
-  int ql = e.qx[q], qr = e.qx[q] + c.qsize, qt = e.qy[q], qb = e.qy[q] - c.qsize;
+// of a player's box (px,py) against the OTHER player's projectile corners
+// x in {qx+3, qx}, y in {qy, qy-3}.
+__device__ __forceinline__ bool hit_test_s(const Cfg& c, int px, int py, int oqx, int oqy, int oqvalid) {
+  int L = px, R = px + c.psize, T = py, B = py + c.psize;
+  int ql = oqx, qr = oqx + c.qsize, qt = oqy, qb = oqy - c.qsize;
   bool xr = (L <= qr) & (qr <= R), xl = (L <= ql) & (ql <= R);
   bool yt = (T <= qt) & (qt <= B), yb = (T <= qb) & (qb <= B);
-  return e.qvalid[q] && ((xr | xl) & (yt | yb));
+  return oqvalid && ((xr | xl) & (yt | yb));
+}
+
+// collision outcome for the env: player 1 is tested first and wins ties
+__device__ __forceinline__ void collide_s(const Cfg& c, int p1x, int p1y, int q1x, int q1y, int q1v, int p2x,
+                                          int p2y, int q2x, int q2y, int q2v, int& live, int& winner) {
+  if (hit_test_s(c, p1x, p1y, q2x, q2y, q2v)) { winner = 1; live = 0; }
+  else if (hit_test_s(c, p2x, p2y, q1x, q1y, q1v)) { winner = 2; live = 0; }
+}
+
+// ---- Env (both players in one lane) wrappers
+__device__ __forceinline__ void move_direction(const Cfg& c, Env& e, int p, double speed) {
+  move_direction_s(c, e.px[p], e.py[p], e.rot[p], speed);
+}
+__device__ __forceinline__ void move_fwd_back(const Cfg& c, Env& e, int p, bool backwards) {
+  move_fwd_back_s(c, e.px[p], e.py[p], e.rot[p], backwards);
+}
+__device__ __forceinline__ void move_look(const Cfg& c, Env& e, int p, double angle) {
+  move_look_s(c, e.rot[p], angle);
+}
+__device__ __forceinline__ void shoot(const Cfg& c, Env& e, int p) {
+  shoot_s(c, e.px[p], e.py[p], e.rot[p], e.qx[p], e.qy[p], e.qrot[p], e.qcd[p], e.qage[p], e.qvalid[p]);
+}
+__device__ __forceinline__ void projectile_tick(const Cfg& c, Env& e, int p) {
+  projectile_tick_s(c, e.qx[p], e.qy[p], e.qrot[p], e.qcd[p], e.qage[p], e.qvalid[p]);
 }
 
 // SkillshotGame.game_tick (SkillshotGame.py:115-122)
@@ -217,8 +244,8 @@ __device__ __forceinline__ void game_tick(const Cfg& c, Env& e) {
     e.ticks += 1;
     projectile_tick(c, e, 0);
     projectile_tick(c, e, 1);
-    if (hit_test(c, e, 0)) { e.winner = 1; e.live = 0; }
-    else if (hit_test(c, e, 1)) { e.winner = 2; e.live = 0; }
+    collide_s(c, e.px[0], e.py[0], e.qx[0], e.qy[0], e.qvalid[0], e.px[1], e.py[1], e.qx[1], e.qy[1],
+              e.qvalid[1], e.live, e.winner);
   }
 }
 
@@ -240,18 +267,23 @@ __device__ __forceinline__ double dist_point_point(int ax, int ay, int bx, int b
   return sqrt((double)(dx * dx + dy * dy));
 }
 
-// SkillshotGame.check_future_collision (SkillshotGame.py:96-113) for the
-// projectile of player p against opponent o: the x_dir gate (:109) is always
+// SkillshotGame.check_future_collision (SkillshotGame.py:96-113) for a
+// projectile against an opponent at (ox, oy): the x_dir gate (:109) is always
 // true for the first projectile x bound, so the test reduces to
 // valid && exists X in {Ox, Ox+5}: Oy <= g*X + (qy - g*qx) <= Oy+5.
-__device__ __forceinline__ bool future_collision(const Cfg& c, const Env& e, int p, double g) {
-  if (!e.qvalid[p]) return false;
-  int o = 1 - p;
-  double yi = (double)e.qy[p] - g * (double)e.qx[p];
-  double lo = (double)e.py[o], hi = (double)(e.py[o] + c.psize);
-  double v0 = g * (double)e.px[o] + yi;
-  double v1 = g * (double)(e.px[o] + c.psize) + yi;
+__device__ __forceinline__ bool future_collision_s(const Cfg& c, int qx, int qy, int qvalid, int ox, int oy,
+                                                   double g) {
+  if (!qvalid) return false;
+  double yi = (double)qy - g * (double)qx;
+  double lo = (double)oy, hi = (double)(oy + c.psize);
+  double v0 = g * (double)ox + yi;
+  double v1 = g * (double)(ox + c.psize) + yi;
   return ((lo <= v0) & (v0 <= hi)) | ((lo <= v1) & (v1 <= hi));
+}
+
+__device__ __forceinline__ bool future_collision(const Cfg& c, const Env& e, int p, double g) {
+  int o = 1 - p;
+  return future_collision_s(c, e.qx[p], e.qy[p], e.qvalid[p], e.px[o], e.py[o], g);
 }
 
 __device__ __forceinline__ double py_mod2(double r) {  // Python float % 2 (floored)
@@ -264,28 +296,34 @@ __device__ __forceinline__ double py_mod2(double r) {  // Python float % 2 (floo
   return m;
 }
 
-// prepare_states (SkillshotLearner.py:512-543) for player p; also returns the
-// calculate_rewards_looking reward (:584) through *reward_looking.
-__device__ __forceinline__ void obs12(const Cfg& c, const Env& e, int p, float out[12],
-                                      double* path_dist) {
-  int o = 1 - p;
-  double gp = grad_of(e.rot[p]);
-  double gq = grad_of(e.qrot[p]);
+// prepare_states (SkillshotLearner.py:512-543) for one player (own player
+// and projectile state, opponent position); *path_dist receives the player's
+// line distance, the calculate_rewards_looking input (:584).
+__device__ __forceinline__ void obs12_s(const Cfg& c, int px, int py, double rot, int qx, int qy, double qrot,
+                                        int qcd, int qvalid, int ox, int oy, float out[12], double* path_dist) {
+  double gp = grad_of(rot);
+  double gq = grad_of(qrot);
   double D = c.max_dist;
-  double pd = dist_line_point(gp, e.px[p], e.py[p], e.px[o], e.py[o]);
+  double pd = dist_line_point(gp, px, py, ox, oy);
   *path_dist = pd;
   out[0] = (float)(pd / D);
-  out[1] = (float)(dist_point_point(e.px[p], e.py[p], e.px[o], e.py[o]) / D);
-  out[2] = (float)((double)e.px[p] / (double)c.W);
-  out[3] = (float)((double)e.py[p] / (double)c.H);
-  out[4] = (float)(((py_mod2(e.rot[p]) * kPi) / 2.0) * kPi);  // `% 2 * np.pi) / 2 * np.pi`
-  out[5] = (float)((double)e.qcd[p] / (double)c.cdmax);
-  out[6] = (float)(dist_point_point(e.qx[p], e.qy[p], e.px[o], e.py[o]) / D);
-  out[7] = (float)((double)e.qx[p] / (double)c.W);
-  out[8] = (float)((double)e.qy[p] / (double)c.H);
-  out[9] = (float)(((py_mod2(e.qrot[p]) * kPi) / 2.0) * kPi);
-  out[10] = (float)(dist_line_point(gq, e.qx[p], e.qy[p], e.px[o], e.py[o]) / D);
-  out[11] = future_collision(c, e, p, gq) ? 1.0f : 0.0f;
+  out[1] = (float)(dist_point_point(px, py, ox, oy) / D);
+  out[2] = (float)((double)px / (double)c.W);
+  out[3] = (float)((double)py / (double)c.H);
+  out[4] = (float)(((py_mod2(rot) * kPi) / 2.0) * kPi);  // `% 2 * np.pi) / 2 * np.pi`
+  out[5] = (float)((double)qcd / (double)c.cdmax);
+  out[6] = (float)(dist_point_point(qx, qy, ox, oy) / D);
+  out[7] = (float)((double)qx / (double)c.W);
+  out[8] = (float)((double)qy / (double)c.H);
+  out[9] = (float)(((py_mod2(qrot) * kPi) / 2.0) * kPi);
+  out[10] = (float)(dist_line_point(gq, qx, qy, ox, oy) / D);
+  out[11] = future_collision_s(c, qx, qy, qvalid, ox, oy, gq) ? 1.0f : 0.0f;
+}
+
+__device__ __forceinline__ void obs12(const Cfg& c, const Env& e, int p, float out[12], double* path_dist) {
+  int o = 1 - p;
+  obs12_s(c, e.px[p], e.py[p], e.rot[p], e.qx[p], e.qy[p], e.qrot[p], e.qcd[p], e.qvalid[p], e.px[o], e.py[o],
+          out, path_dist);
 }
 
 // get_state per-player dict values (SkillshotGame.py:145-163 key order)

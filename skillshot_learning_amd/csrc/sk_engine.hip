@@ -39,6 +39,7 @@ struct sk_env {
   // slots[1-parity] = value + advance, then the host flips parity.
   uint64_t* d_step;
   int parity;
+  int step_variant;  // 0 = one lane per env, 1 = player-split (SK_STEP_VARIANT)
 };
 
 static thread_local std::string g_err;
@@ -178,6 +179,109 @@ __global__ void __launch_bounds__(kBlock) k_step(StepArgs a, Cfg c) {
     }
   }
   store_env(a.v, i, e);
+}
+
+// Player-split fused step: lanes (2i, 2i+1) own players 1 and 2 of env i.
+// Each lane loads only its player's half of every plane (8-byte lanes, the
+// pair covering the env's 16 bytes: still fully coalesced), runs that
+// player's do_actions and projectile tick (a player's actions never read the
+// other player), then the pair swaps positions/projectiles with one
+// __shfl_xor(.,1) each for the collision test, which both lanes evaluate
+// identically.  Twice the waves of k_step, half the dependent chain per lane.
+__global__ void __launch_bounds__(kBlock) k_step_split(StepArgs a, Cfg c) {
+  const int64_t gt = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t i = gt >> 1;
+  const int p = (int)(gt & 1);
+  const uint64_t step = step_read(a.step);
+  step_advance(a.step, step, 1);
+  const bool in = i < a.n;
+  const int64_t h = 2 * i + p;  // this lane's half-plane index
+  int px = 0, py = 0, qx = 0, qy = 0, qcd = 0, qage = 0, ticks = 0, flags = 0;
+  double rot = 0.0, qrot = 0.0;
+  float2 act = make_float2(0.f, 0.f);
+  if (in) {
+    int2 pp = reinterpret_cast<const int2*>(a.v.pos)[h];
+    int2 qq = reinterpret_cast<const int2*>(a.v.qpos)[h];
+    int2 ca = reinterpret_cast<const int2*>(a.v.qcdage)[h];
+    int2 m = a.v.misc[i];
+    rot = reinterpret_cast<const double*>(a.v.rot)[h];
+    qrot = reinterpret_cast<const double*>(a.v.qrot)[h];
+    act = a.actions[(int64_t)p * a.n + i];
+    px = pp.x; py = pp.y; qx = qq.x; qy = qq.y; qcd = ca.x; qage = ca.y;
+    ticks = m.x; flags = m.y;
+  }
+  int qvalid = ((unsigned)flags >> (8 * p)) & 0xff;
+  int live = ((unsigned)flags >> 16) & 0xff;
+  int winner = ((unsigned)flags >> 24) & 0xff;
+  // do_actions(p+1, ...)  SkillshotLearner.py:206-213
+  move_direction_s(c, px, py, rot, (double)act.x);
+  move_look_s(c, rot, (double)act.y);
+  shoot_s(c, px, py, rot, qx, qy, qrot, qcd, qage, qvalid);
+  // game_tick  SkillshotGame.py:115-122 (live is identical in both lanes)
+  if (live) {
+    ticks += 1;
+    projectile_tick_s(c, qx, qy, qrot, qcd, qage, qvalid);
+  }
+  const int opx = __shfl_xor(px, 1, 64), opy = __shfl_xor(py, 1, 64);
+  const int oqx = __shfl_xor(qx, 1, 64), oqy = __shfl_xor(qy, 1, 64), oqv = __shfl_xor(qvalid, 1, 64);
+  if (live) {
+    if (p == 0) collide_s(c, px, py, qx, qy, qvalid, opx, opy, oqx, oqy, oqv, live, winner);
+    else collide_s(c, opx, opy, oqx, oqy, oqv, px, py, qx, qy, qvalid, live, winner);
+  }
+  const bool d = in && ((!live) || (ticks >= a.tick_limit));  // SkillshotLearner.py:302
+  if (in && (a.obs || a.reward)) {
+    float o[12];
+    double pd;
+    obs12_s(c, px, py, rot, qx, qy, qrot, qcd, qvalid, opx, opy, o, &pd);
+    if (a.obs) store_obs(a.obs, a.n, p, i, o);
+    if (a.reward) {
+      float r;
+      if (a.reward_kind == SK_REWARD_SIMPLE) {
+        double mine = dist_point_point(qx, qy, opx, opy);
+        double theirs = dist_point_point(oqx, oqy, px, py);
+        r = (float)(mine - theirs);
+      } else {
+        r = (float)(-pd / (double)c.W);
+      }
+      a.reward[(int64_t)p * a.n + i] = r;
+    }
+  }
+  if (in && p == 0) {
+    if (a.done) a.done[i] = (uint8_t)d;
+    if (a.winner) a.winner[i] = (uint8_t)winner;
+  }
+  if (a.ctr) wave_count(a.ctr, d && p == 0, winner, ticks);
+  if (!in) return;
+  if (d && a.auto_reset) {  // SkillshotGame.__init__ :10-25 for this lane's player
+    if (a.random_positions) {
+      U4 u = draw4(a.seed, (uint64_t)(a.env_offset + i), step, 1u);
+      px = u32_to_pos(p ? u.z : u.x, c.rlo, c.rhi);
+      py = u32_to_pos(p ? u.w : u.y, c.rlo, c.rhi);
+    } else {
+      px = p ? c.f2x : c.f1x;
+      py = p ? c.f2y : c.f1y;
+    }
+    rot = 0.0; qx = 0; qy = 0; qrot = 0.0; qcd = 0; qage = 0; qvalid = 0;
+    ticks = 0; live = 1; winner = 0;
+  }
+  if (a.obs_reset) {
+    const int rpx = __shfl_xor(px, 1, 64), rpy = __shfl_xor(py, 1, 64);
+    float o[12];
+    double pd;
+    obs12_s(c, px, py, rot, qx, qy, qrot, qcd, qvalid, rpx, rpy, o, &pd);
+    store_obs(a.obs_reset, a.n, p, i, o);
+  }
+  reinterpret_cast<int2*>(a.v.pos)[h] = make_int2(px, py);
+  reinterpret_cast<double*>(a.v.rot)[h] = rot;
+  reinterpret_cast<int2*>(a.v.qpos)[h] = make_int2(qx, qy);
+  reinterpret_cast<double*>(a.v.qrot)[h] = qrot;
+  reinterpret_cast<int2*>(a.v.qcdage)[h] = make_int2(qcd, qage);
+  const int ov = __shfl_xor(qvalid, 1, 64);
+  if (p == 0) {
+    unsigned f = (unsigned)(qvalid & 0xff) | ((unsigned)(ov & 0xff) << 8) | ((unsigned)(live & 0xff) << 16) |
+                 ((unsigned)(winner & 0xff) << 24);
+    a.v.misc[i] = make_int2(ticks, (int)f);
+  }
 }
 
 struct RolloutArgs {
@@ -413,6 +517,8 @@ static int make_env(sk_env** out, const sk_state_view* view, int32_t n, int64_t 
   if ((rc = validate_cfg(e->cfg))) { delete e; return rc; }
   e->dcfg = to_dcfg(e->cfg);
   e->parity = 0;
+  e->step_variant = 1;
+  if (const char* sv = std::getenv("SK_STEP_VARIANT")) e->step_variant = std::atoi(sv);
   if (view) {
     if (view->n_envs != n || !view->pos || !view->rot || !view->qpos || !view->qrot || !view->qcdage ||
         !view->misc) {
@@ -638,7 +744,10 @@ int sk_env_step(sk_env* e, const float* actions, float* obs, float* reward, int3
   a.env_offset = e->env_offset;
   a.step = StepRef{e->d_step, e->parity};
   a.ctr = e->d_counters;
-  k_step<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(a, e->dcfg);
+  if (e->step_variant == 1)
+    k_step_split<<<grid_for(2 * (int64_t)e->n), kBlock, 0, (hipStream_t)stream>>>(a, e->dcfg);
+  else
+    k_step<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(a, e->dcfg);
   SK_LAUNCH_CHECK();
   e->parity ^= 1;
   return SK_OK;

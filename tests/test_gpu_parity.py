@@ -67,8 +67,15 @@ class GpuEngine:
         return o.cpu().numpy(), r.cpu().numpy()
 
 
+@pytest.fixture(params=[0, 1], ids=["lane_per_env", "player_split"])
+def step_variant(request, monkeypatch):
+    """Both fused-step kernels (k_step, k_step_split) must meet the same bar."""
+    monkeypatch.setenv("SK_STEP_VARIANT", str(request.param))
+    return request.param
+
+
 @pytest.mark.parametrize("name", gr.fixture_names())
-def test_golden_fixture(ssa, name):
+def test_golden_fixture(ssa, name, step_variant):
     d = gr.load(name)
     n = gr.replay(GpuEngine(ssa, d["pos"].shape[0]), d, obs_tol=OBS_TOL)
     assert n == int(d["n_steps"].sum())
@@ -93,7 +100,7 @@ def _assert_state_equal(got, want, where):
                                  f"{g[tuple(bad[0])]} vs {w[tuple(bad[0])]}")
 
 
-def test_fused_step_matches_oracle_random_policy(ssa, oracle_mod):
+def test_fused_step_matches_oracle_random_policy(ssa, oracle_mod, step_variant):
     """8192 envs x 2500 ticks, random policy, random auto-reset (the learner
     protocol of configs 2/3): state bit-exact every 100 ticks, obs/reward/done/
     winner compared on sampled ticks, counters equal."""
@@ -158,7 +165,7 @@ def test_rollout_random_matches_oracle(ssa, oracle_mod, n, T):
     assert [c["dones"], c["hits_p1"], c["hits_p2"], c["ticks_sum"]] == [int(x) for x in ref.counters]
 
 
-def test_rollout_equals_stepwise_on_gpu(ssa):
+def test_rollout_equals_stepwise_on_gpu(ssa, step_variant):
     """rollout_random(T) == T x (gen_random_actions + fused step) on device."""
     n, T = 3000, 300
     a = ssa.VecSkillshotGame(n, seed=3, tick_limit=120)

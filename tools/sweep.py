@@ -1,0 +1,83 @@
+"""A/B sweep of step-kernel variants x batch sizes (graph-replayed fused step).
+
+    python tools/sweep.py [--variants 0,1] [--envs 65536,262144,1048576] [--steps 2000]
+Prints one JSON line per (variant, N): us/step, env-steps/s, GB/s at 193 B/env-step.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def run(variant, n, steps, graph_len, ring, obs=False):
+    os.environ["SK_STEP_VARIANT"] = str(variant)
+    from skillshot_learning_amd import VecSkillshotGame
+    env = VecSkillshotGame(n, seed=0, tick_limit=2000)
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):
+        env.reset(random_positions=True)
+        ring = max(ring, graph_len)
+        acts = env.gen_random_actions(ring)
+        done = torch.empty(n, dtype=torch.uint8, device="cuda")
+        o = torch.empty((2, n, 12), dtype=torch.float32, device="cuda") if obs else None
+        r = torch.empty((2, n), dtype=torch.float32, device="cuda") if obs else None
+    st.synchronize()
+    slab = 16 * n
+    sp = ctypes.c_void_p(st.cuda_stream)
+    a0 = acts.data_ptr()
+
+    def launch(t):
+        env.step_raw(ctypes.c_void_p(a0 + (t % ring) * slab), ctypes.c_void_p(done.data_ptr()),
+                     obs_ptr=None if o is None else ctypes.c_void_p(o.data_ptr()),
+                     reward_ptr=None if r is None else ctypes.c_void_p(r.data_ptr()), stream=sp)
+
+    with torch.cuda.stream(st):
+        for t in range(4):
+            launch(t)
+    st.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=st):
+        for t in range(graph_len):
+            launch(t)
+    reps = max(1, steps // graph_len)
+    with torch.cuda.stream(st):
+        g.replay()
+    st.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(st):
+        e0.record()
+        for _ in range(reps):
+            g.replay()
+        e1.record()
+    st.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / (reps * graph_len)
+    nb = 297 if obs else 193
+    res = dict(variant=variant, envs=n, obs=obs, us_per_step=us, env_steps_per_s=n / (us * 1e-6),
+               gbs=nb * n / (us * 1e-6) / 1e9, frac=nb * n / (us * 1e-6) / 8e12)
+    env.close()
+    del g
+    return res
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--variants", default="0,1")
+    p.add_argument("--envs", default="65536,262144,1048576")
+    p.add_argument("--steps", type=int, default=2000)
+    p.add_argument("--graph-len", type=int, default=200)
+    p.add_argument("--ring", type=int, default=300)
+    p.add_argument("--obs", action="store_true")
+    a = p.parse_args()
+    for v in [int(x) for x in a.variants.split(",")]:
+        for n in [int(x) for x in a.envs.split(",")]:
+            ring = a.ring if n <= 262144 else max(a.graph_len, 64)
+            print(json.dumps(run(v, n, a.steps, a.graph_len, ring, obs=a.obs)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
