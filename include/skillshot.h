@@ -87,7 +87,10 @@ typedef struct sk_state_view {
 typedef struct sk_env sk_env;
 
 /* Episode counters accumulated on device by the step kernels (wavefront
- * ballot + popcount, one atomic per wave). */
+ * ballot + popcount, one atomic per wave and counter).  On device they are
+ * spread over SK_COUNTER_SLOTS slots (no hot line); the totals are the sums
+ * (sk_env_read_counters returns the sums). */
+#define SK_COUNTER_SLOTS 256
 typedef struct sk_counters {
   uint64_t dones;          /* episodes finished (hit or tick limit) */
   uint64_t hits_p1;        /* episodes ending with winner_id == 1 */
@@ -112,7 +115,8 @@ int sk_env_attach(sk_env** out, const sk_state_view* view, int64_t env_offset, u
                   int32_t device, const sk_config* cfg);
 int sk_env_destroy(sk_env* env);
 int sk_env_get_view(const sk_env* env, sk_state_view* out);
-/* Device counters (sk_counters, device memory) the step kernels accumulate into. */
+/* Device counter slots (SK_COUNTER_SLOTS x sk_counters, device memory) the
+ * step kernels accumulate into. */
 int sk_env_counters_ptr(const sk_env* env, sk_counters** out);
 /* Copy the episode counters to host memory (synchronises `stream`), and
  * zero them (stream-ordered). */

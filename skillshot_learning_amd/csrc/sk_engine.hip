@@ -33,7 +33,8 @@ struct sk_env {
   View view;
   sk_state_view hview;
   bool owned;
-  sk_counters* d_counters;
+  char* d_aux;               // [step slots: 256 B][counter slots]
+  sk_counters* d_counters;   // SK_COUNTER_SLOTS slots
   // RNG step counter, device-resident so every call is hipGraph-capturable:
   // two slots ping-pong; a kernel reads slots[parity] and block 0 writes
   // slots[1-parity] = value + advance, then the host flips parity.
@@ -57,12 +58,21 @@ static int fail(int code, const std::string& msg) {
   } while (0)
 
 static constexpr int kBlock = 256;
+static constexpr size_t kAuxBytes = 256 + SK_COUNTER_SLOTS * sizeof(sk_counters);
 
 static inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
 // ------------------------------------------------------------------ counters
-// wavefront ballot: count done / hit-by-id lanes, sum final ticks; lane 0 of
-// each wave issues the atomics.
+// Episode counters live in SK_COUNTER_SLOTS slots of 32 B; the host sums
+// them.  Each wave ballots its done / hit-by-id lanes and sums final ticks
+// across lanes, then lane 0 adds into the slot picked by its global wave
+// index: no single hot line (a one-line counter serialises every wave's
+// atomics at the memory side and stalled 1M-env launches).
+__device__ __forceinline__ sk_counters* ctr_slot(sk_counters* base) {
+  unsigned wave = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  return base + (wave & (SK_COUNTER_SLOTS - 1));
+}
+
 __device__ __forceinline__ void wave_count(sk_counters* ctr, bool done, int winner, int ticks) {
   uint64_t m_done = __ballot(done);
   if (m_done == 0) return;  // wave-uniform
@@ -72,10 +82,11 @@ __device__ __forceinline__ void wave_count(sk_counters* ctr, bool done, int winn
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
   if ((threadIdx.x & 63) == 0) {
-    atomicAdd((unsigned long long*)&ctr->dones, (unsigned long long)__popcll(m_done));
-    if (m_w1) atomicAdd((unsigned long long*)&ctr->hits_p1, (unsigned long long)__popcll(m_w1));
-    if (m_w2) atomicAdd((unsigned long long*)&ctr->hits_p2, (unsigned long long)__popcll(m_w2));
-    atomicAdd((unsigned long long*)&ctr->ticks_sum, (unsigned long long)t);
+    sk_counters* c = ctr_slot(ctr);
+    atomicAdd((unsigned long long*)&c->dones, (unsigned long long)__popcll(m_done));
+    if (m_w1) atomicAdd((unsigned long long*)&c->hits_p1, (unsigned long long)__popcll(m_w1));
+    if (m_w2) atomicAdd((unsigned long long*)&c->hits_p2, (unsigned long long)__popcll(m_w2));
+    atomicAdd((unsigned long long*)&c->ticks_sum, (unsigned long long)t);
   }
 }
 
@@ -102,8 +113,11 @@ struct StepRef {
   int parity;
 };
 
+// Wave-uniform plain load (one s_load per wave through the scalar cache; the
+// dispatch boundary's cache invalidation makes the previous launch's write
+// visible).  Per-lane agent-scope loads of this one line throttled big grids.
 __device__ __forceinline__ uint64_t step_read(const StepRef& s) {
-  return __hip_atomic_load(s.slots + s.parity, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return s.slots[s.parity];
 }
 
 __device__ __forceinline__ void step_advance(const StepRef& s, uint64_t base, uint64_t inc) {
@@ -336,7 +350,7 @@ __global__ void __launch_bounds__(kBlock) k_rollout_random(RolloutArgs a, Cfg c)
       vals[k] = x;
     }
     if ((threadIdx.x & 63) == 0 && vals[0]) {
-      unsigned long long* base = (unsigned long long*)a.ctr;
+      unsigned long long* base = (unsigned long long*)ctr_slot(a.ctr);
       for (int k = 0; k < 4; ++k)
         if (vals[k]) atomicAdd(base + k, (unsigned long long)vals[k]);
     }
@@ -560,13 +574,14 @@ static int make_env(sk_env** out, const sk_state_view* view, int32_t n, int64_t 
     delete e;
     return fail(SK_EINVAL, "misc plane must be 8-byte aligned");
   }
-  if (hipMalloc(&e->d_counters, sizeof(sk_counters) + 2 * sizeof(uint64_t)) != hipSuccess) {
+  if (hipMalloc(&e->d_aux, kAuxBytes) != hipSuccess) {
     if (e->owned) (void)hipFree(e->hview.pos);
     delete e;
     return fail(SK_ENOMEM, "hipMalloc counters");
   }
-  HIP_TRY(hipMemset(e->d_counters, 0, sizeof(sk_counters) + 2 * sizeof(uint64_t)));
-  e->d_step = reinterpret_cast<uint64_t*>(e->d_counters + 1);
+  HIP_TRY(hipMemset(e->d_aux, 0, kAuxBytes));
+  e->d_step = reinterpret_cast<uint64_t*>(e->d_aux);
+  e->d_counters = reinterpret_cast<sk_counters*>(e->d_aux + 256);
   if (e->owned) {
     k_reset<<<grid_for(n), kBlock, 0, 0>>>(e->view, n, nullptr, 0, seed, env_offset, StepRef{e->d_step, 0},
                                            e->dcfg);
@@ -595,7 +610,7 @@ int sk_env_destroy(sk_env* e) {
   if (!e) return fail(SK_EINVAL, "NULL handle");
   (void)hipSetDevice(e->device);
   if (e->owned) (void)hipFree(e->hview.pos);
-  (void)hipFree(e->d_counters);
+  (void)hipFree(e->d_aux);
   delete e;
   return SK_OK;
 }
@@ -614,14 +629,23 @@ int sk_env_counters_ptr(const sk_env* e, sk_counters** out) {
 
 int sk_env_read_counters(sk_env* e, sk_counters* out, void* stream) {
   if (!e || !out) return fail(SK_EINVAL, "NULL argument");
-  HIP_TRY(hipMemcpyAsync(out, e->d_counters, sizeof(sk_counters), hipMemcpyDeviceToHost, (hipStream_t)stream));
+  sk_counters slots[SK_COUNTER_SLOTS];
+  HIP_TRY(hipMemcpyAsync(slots, e->d_counters, sizeof(slots), hipMemcpyDeviceToHost, (hipStream_t)stream));
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  sk_counters sum = {0, 0, 0, 0};
+  for (int k = 0; k < SK_COUNTER_SLOTS; ++k) {
+    sum.dones += slots[k].dones;
+    sum.hits_p1 += slots[k].hits_p1;
+    sum.hits_p2 += slots[k].hits_p2;
+    sum.ticks_sum += slots[k].ticks_sum;
+  }
+  *out = sum;
   return SK_OK;
 }
 
 int sk_env_clear_counters(sk_env* e, void* stream) {
   if (!e) return fail(SK_EINVAL, "NULL handle");
-  HIP_TRY(hipMemsetAsync(e->d_counters, 0, sizeof(sk_counters), (hipStream_t)stream));
+  HIP_TRY(hipMemsetAsync(e->d_counters, 0, SK_COUNTER_SLOTS * sizeof(sk_counters), (hipStream_t)stream));
   return SK_OK;
 }
 
