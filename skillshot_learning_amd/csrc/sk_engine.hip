@@ -531,7 +531,7 @@ static int make_env(sk_env** out, const sk_state_view* view, int32_t n, int64_t 
   if ((rc = validate_cfg(e->cfg))) { delete e; return rc; }
   e->dcfg = to_dcfg(e->cfg);
   e->parity = 0;
-  e->step_variant = 1;
+  e->step_variant = 0;
   if (const char* sv = std::getenv("SK_STEP_VARIANT")) e->step_variant = std::atoi(sv);
   if (view) {
     if (view->n_envs != n || !view->pos || !view->rot || !view->qpos || !view->qrot || !view->qcdage ||

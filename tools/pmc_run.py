@@ -1,0 +1,43 @@
+"""Eager k_step launches for rocprofv3 --pmc passes (graph replay is avoided so
+every dispatch is attributed).  Same workload as bench.py (random policy,
+pre-generated actions ring, done output, random auto-reset).
+
+    rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d OUT -o pmc \
+        -- python3 tools/pmc_run.py --envs 65536 --launches 300
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--envs", type=int, default=65536)
+    p.add_argument("--launches", type=int, default=300)
+    p.add_argument("--ring", type=int, default=300)
+    p.add_argument("--obs", action="store_true")
+    a = p.parse_args()
+    from skillshot_learning_amd import VecSkillshotGame
+    n = a.envs
+    env = VecSkillshotGame(n, seed=0, tick_limit=2000)
+    env.reset(random_positions=True)
+    acts = env.gen_random_actions(a.ring)
+    done = torch.empty(n, dtype=torch.uint8, device="cuda")
+    o = torch.empty((2, n, 12), dtype=torch.float32, device="cuda") if a.obs else None
+    r = torch.empty((2, n), dtype=torch.float32, device="cuda") if a.obs else None
+    torch.cuda.synchronize()
+    for t in range(a.launches):
+        env.step_raw(ctypes.c_void_p(acts.data_ptr() + (t % a.ring) * 16 * n), ctypes.c_void_p(done.data_ptr()),
+                     obs_ptr=None if o is None else ctypes.c_void_p(o.data_ptr()),
+                     reward_ptr=None if r is None else ctypes.c_void_p(r.data_ptr()))
+    torch.cuda.synchronize()
+    print("launches", a.launches, "envs", n)
+
+
+if __name__ == "__main__":
+    main()

@@ -15,7 +15,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def run(variant, n, steps, graph_len, ring, obs=False):
-    os.environ["SK_STEP_VARIANT"] = str(variant)
+    """variant 0/1 = k_step / k_step_split; 'empty' / 'copy' = sk_diag floors."""
+    os.environ["SK_STEP_VARIANT"] = str(variant if isinstance(variant, int) else 0)
     from skillshot_learning_amd import VecSkillshotGame
     env = VecSkillshotGame(n, seed=0, tick_limit=2000)
     st = torch.cuda.Stream()
@@ -31,7 +32,19 @@ def run(variant, n, steps, graph_len, ring, obs=False):
     sp = ctypes.c_void_p(st.cuda_stream)
     a0 = acts.data_ptr()
 
-    def launch(t):
+    planes = (ctypes.c_void_p * 6)(*[getattr(env, k).data_ptr() for k in ("pos", "rot", "qpos", "qrot", "qcdage", "misc")])
+    diag = {"empty": 0, "copy": 1}.get(variant)
+    if diag is not None:
+        L = env._L
+        L.skdiag_launch.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                    ctypes.c_void_p]
+
+        def launch(t):
+            rc = L.skdiag_launch(diag, planes, ctypes.c_void_p(a0 + (t % ring) * slab), ctypes.c_void_p(done.data_ptr()),
+                                 n, sp)
+            assert rc == 0
+    else:
+      def launch(t):
         env.step_raw(ctypes.c_void_p(a0 + (t % ring) * slab), ctypes.c_void_p(done.data_ptr()),
                      obs_ptr=None if o is None else ctypes.c_void_p(o.data_ptr()),
                      reward_ptr=None if r is None else ctypes.c_void_p(r.data_ptr()), stream=sp)
@@ -73,7 +86,7 @@ def main():
     p.add_argument("--ring", type=int, default=300)
     p.add_argument("--obs", action="store_true")
     a = p.parse_args()
-    for v in [int(x) for x in a.variants.split(",")]:
+    for v in [int(x) if x.isdigit() else x for x in a.variants.split(",")]:
         for n in [int(x) for x in a.envs.split(",")]:
             ring = a.ring if n <= 262144 else max(a.graph_len, 64)
             print(json.dumps(run(v, n, a.steps, a.graph_len, ring, obs=a.obs)), flush=True)
