@@ -92,5 +92,68 @@ def main():
             print(json.dumps(run(v, n, a.steps, a.graph_len, ring, obs=a.obs)), flush=True)
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and not os.environ.get("SWEEP_SHARDS"):
     main()
+
+
+def run_sharded(n_total, shards, steps, graph_len, ring, variant=0):
+    """n_total games as `shards` independent env shards on separate streams,
+    each replaying its own captured chain; time for every shard to advance
+    `steps` ticks."""
+    os.environ["SK_STEP_VARIANT"] = str(variant)
+    from skillshot_learning_amd import VecSkillshotGame
+    n = n_total // shards
+    envs, streams, graphs, keep = [], [], [], []
+    for s in range(shards):
+        env = VecSkillshotGame(n, seed=0, env_offset=s * n, tick_limit=2000)
+        st = torch.cuda.Stream()
+        with torch.cuda.stream(st):
+            env.reset(random_positions=True)
+            acts = env.gen_random_actions(ring)
+            done = torch.empty(n, dtype=torch.uint8, device="cuda")
+        st.synchronize()
+        sp = ctypes.c_void_p(st.cuda_stream)
+
+        def launch(t, env=env, acts=acts, done=done, sp=sp):
+            env.step_raw(ctypes.c_void_p(acts.data_ptr() + (t % ring) * 16 * n), ctypes.c_void_p(done.data_ptr()),
+                         stream=sp)
+
+        with torch.cuda.stream(st):
+            for t in range(4):
+                launch(t)
+        st.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=st):
+            for t in range(graph_len):
+                launch(t)
+        envs.append(env); streams.append(st); graphs.append(g); keep.append((acts, done))
+    torch.cuda.synchronize()
+    reps = max(1, steps // graph_len)
+    main = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(2):  # second pass is the timed one
+        e0.record(main)
+        for st, g in zip(streams, graphs):
+            st.wait_event(e0)
+            with torch.cuda.stream(st):
+                for _ in range(reps):
+                    g.replay()
+        ends = []
+        for st in streams:
+            ev = torch.cuda.Event()
+            ev.record(st)
+            main.wait_event(ev)
+        e1.record(main)
+        torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / (reps * graph_len)
+    res = dict(variant=variant, envs=n_total, shards=shards, us_per_step=us, env_steps_per_s=n_total / (us * 1e-6),
+               frac=193 * n_total / (us * 1e-6) / 8e12)
+    for e in envs:
+        e.close()
+    return res
+
+
+if __name__ == "__main__" and os.environ.get("SWEEP_SHARDS"):
+    for S in [int(x) for x in os.environ["SWEEP_SHARDS"].split(",")]:
+        for v in (0, 1):
+            print(json.dumps(run_sharded(65536, S, 2000, 200, 300, variant=v)), flush=True)
