@@ -158,6 +158,15 @@ int sk_player_shoot(sk_env* env, int32_t player_id, const uint8_t* mask, void* s
  * (SkillshotGame.py:58-94). */
 int sk_game_tick(sk_env* env, void* stream);
 
+/* Projectile.move_forwards() (Projectile.py:38-47) when tick == 0, or
+ * Projectile.tick() (:49-53: move, cooldown -= 1, age += 1) when tick != 0,
+ * for player_id's projectile in envs with mask != 0 (mask NULL = all). */
+int sk_projectile_move(sk_env* env, int32_t player_id, int32_t tick, const uint8_t* mask, void* stream);
+/* SkillshotGame.check_collision() (SkillshotGame.py:58-94), live or not, as
+ * the reference.  hit_out (uint8[N], nullable) receives the id of the player
+ * hit by this call (0 = none) so a caller can reproduce the reference's print. */
+int sk_game_check_collision(sk_env* env, uint8_t* hit_out, void* stream);
+
 /* --- observation / reward ----------------------------------------------- */
 
 /* get_state() numerics (SkillshotGame.py:136-166): feat = double[N][2][18]. */

@@ -46,6 +46,8 @@ def lib():
         L.orc_move_discrete.argtypes = view + [i64, i32, i32, P]
         L.orc_shoot.argtypes = view + [i64, i32, P]
         L.orc_game_tick.argtypes = view + [i64]
+        L.orc_projectile_move.argtypes = view + [i64, i32, i32, P]
+        L.orc_check_collision.argtypes = view + [i64, P]
         L.orc_features.argtypes = view + [i64, P]
         L.orc_observe.argtypes = view + [i64, P, P, i32]
         L.orc_step.argtypes = view + [i64, P, P, P, i32, P, P, i32, i32, i32, P, u64, i64, u64, P]
@@ -133,6 +135,15 @@ class OracleState:
 
     def game_tick(self):
         lib().orc_game_tick(*self._view(), self.n)
+
+    def projectile_move(self, pid, tick=True, mask=None):
+        m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        lib().orc_projectile_move(*self._view(), self.n, pid, int(bool(tick)), _p(m))
+
+    def check_collision(self):
+        h = np.zeros(self.n, np.uint8)
+        lib().orc_check_collision(*self._view(), self.n, _p(h))
+        return h
 
     def features(self):
         f = np.zeros((self.n, 2, 18), dtype=np.float64)

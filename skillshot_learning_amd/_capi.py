@@ -24,7 +24,7 @@ EXPORTS = (
     "sk_env_destroy", "sk_env_get_view", "sk_env_counters_ptr", "sk_env_read_counters",
     "sk_env_clear_counters", "sk_env_get_step_counter",
     "sk_env_set_step_counter", "sk_env_reset", "sk_player_move_direction", "sk_player_move_look",
-    "sk_player_move_discrete", "sk_player_shoot", "sk_game_tick", "sk_env_features", "sk_env_observe",
+    "sk_player_move_discrete", "sk_player_shoot", "sk_projectile_move", "sk_game_check_collision", "sk_game_tick", "sk_env_features", "sk_env_observe",
     "sk_env_step", "sk_gen_random_actions", "sk_env_rollout_random",
 )
 
@@ -93,6 +93,8 @@ def load(build_if_missing=True):
         "sk_player_move_look": ([P, i32, P, f64, P], ctypes.c_int),
         "sk_player_move_discrete": ([P, i32, i32, P, P], ctypes.c_int),
         "sk_player_shoot": ([P, i32, P, P], ctypes.c_int),
+        "sk_projectile_move": ([P, i32, i32, P, P], ctypes.c_int),
+        "sk_game_check_collision": ([P, P, P], ctypes.c_int),
         "sk_game_tick": ([P, P], ctypes.c_int),
         "sk_env_features": ([P, P, P], ctypes.c_int),
         "sk_env_observe": ([P, P, P, i32, P], ctypes.c_int),

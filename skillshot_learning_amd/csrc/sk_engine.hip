@@ -427,6 +427,36 @@ __global__ void __launch_bounds__(kBlock) k_shoot(View v, int64_t n, int p, cons
   store_env(v, i, e);
 }
 
+__global__ void __launch_bounds__(kBlock) k_projectile_move(View v, int64_t n, int p, int tick,
+                                                            const uint8_t* mask, Cfg c) {
+  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n || (mask && !mask[i])) return;
+  Env e;
+  load_env(v, i, e);
+  if (p == 0) projectile_tick_s(c, e.qx[0], e.qy[0], e.qrot[0], e.qcd[0], e.qage[0], e.qvalid[0]);
+  else projectile_tick_s(c, e.qx[1], e.qy[1], e.qrot[1], e.qcd[1], e.qage[1], e.qvalid[1]);
+  if (!tick) {  // move_forwards alone: undo the tick's cooldown/age update
+    if (p == 0) { e.qcd[0] += 1; e.qage[0] -= 1; } else { e.qcd[1] += 1; e.qage[1] -= 1; }
+  }
+  store_env(v, i, e);
+}
+
+__global__ void __launch_bounds__(kBlock) k_check_collision(View v, int64_t n, uint8_t* hit_out, Cfg c) {
+  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  Env e;
+  load_env(v, i, e);
+  int live = e.live, winner = e.winner;
+  int hit_live = 1, hit = 0;
+  collide_s(c, e.px[0], e.py[0], e.qx[0], e.qy[0], e.qvalid[0], e.px[1], e.py[1], e.qx[1], e.qy[1], e.qvalid[1],
+            hit_live, hit);
+  if (hit) { winner = hit; live = 0; }
+  e.live = live;
+  e.winner = winner;
+  if (hit_out) hit_out[i] = (uint8_t)hit;
+  store_env(v, i, e);
+}
+
 __global__ void __launch_bounds__(kBlock) k_game_tick(View v, int64_t n, Cfg c) {
   int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
@@ -712,6 +742,22 @@ int sk_player_shoot(sk_env* e, int32_t pid, const uint8_t* mask, void* stream) {
   SK_CHECK_ENV(e);
   SK_CHECK_PID(pid);
   k_shoot<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(e->view, e->n, pid - 1, mask, e->dcfg);
+  SK_LAUNCH_CHECK();
+  return SK_OK;
+}
+
+int sk_projectile_move(sk_env* e, int32_t pid, int32_t tick, const uint8_t* mask, void* stream) {
+  SK_CHECK_ENV(e);
+  SK_CHECK_PID(pid);
+  k_projectile_move<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(e->view, e->n, pid - 1, tick, mask,
+                                                                         e->dcfg);
+  SK_LAUNCH_CHECK();
+  return SK_OK;
+}
+
+int sk_game_check_collision(sk_env* e, uint8_t* hit_out, void* stream) {
+  SK_CHECK_ENV(e);
+  k_check_collision<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(e->view, e->n, hit_out, e->dcfg);
   SK_LAUNCH_CHECK();
   return SK_OK;
 }

@@ -179,6 +179,17 @@ class VecSkillshotGame:
         m = None if mask is None else self._u8(mask)
         check(self._L.sk_player_shoot(self._h, int(player_id), _ptr(m), self._stream()))
 
+    def projectile_move(self, player_id, tick=True, mask=None):
+        """Projectile.tick (Projectile.py:49-53) or, with tick=False, move_forwards (:38-47)."""
+        m = None if mask is None else self._u8(mask)
+        check(self._L.sk_projectile_move(self._h, int(player_id), int(bool(tick)), _ptr(m), self._stream()))
+
+    def check_collision(self, hit_out=None):
+        """SkillshotGame.check_collision (SkillshotGame.py:58-94); returns u8[N] id of the player hit (0 = none)."""
+        h = hit_out if hit_out is not None else torch.empty(self.n, dtype=torch.uint8, device=self.device)
+        check(self._L.sk_game_check_collision(self._h, _ptr(h), self._stream()))
+        return h
+
     def game_tick(self):
         """SkillshotGame.game_tick (SkillshotGame.py:115-122)."""
         check(self._L.sk_game_tick(self._h, self._stream()))

@@ -408,7 +408,7 @@ def scenario_raw(seed=19):
          note="per-method calls, sparse shooting, stepping continues 40 ticks after game end")
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and "--boards" not in sys.argv:
     scenario_random_policy("fixed_random", 8, 2000, 2000, "fixed", 1)
     scenario_random_policy("numpy_start", 8, 2000, 2000, "numpy", 2)
     scenario_random_policy("int_start_limit200", 12, 200, 200, "int", 3)
@@ -418,3 +418,49 @@ if __name__ == "__main__":
     scenario_clamp()
     scenario_both_hit()
     scenario_raw()
+
+
+def scenario_boards():
+    """get_board (SkillshotGame.py:36-56) and raw get_state dicts (:136-166) on
+    states sampled from reference trajectories (F4 row / class-API parity)."""
+    rng = random.Random(23)
+    states, boards, feats, general = [], [], [], []
+    keys = ["player_grad", "player_x_dir", "player_path_dist_opponent", "player_dist_opponent",
+            "player_pos_x", "player_pos_y", "player_rotation", "projectile_cooldown", "projectile_grad",
+            "projectile_x_dir", "projectile_path_dist_opponent", "projectile_pos_x", "projectile_pos_y",
+            "projectile_rotation", "projectile_age", "projectile_valid", "projectile_dist_opponent",
+            "projectile_future_collision_opponent"]
+    with contextlib.redirect_stdout(io.StringIO()):
+        for e in range(6):
+            g = SkillshotGame()
+            init = fixed_init()
+            init["pos"] = [[rng.randrange(0, 246), rng.randrange(0, 246)] for _ in range(2)]
+            set_state(g, init)
+            learner = LearnerStub(g)
+            for t in range(120):
+                for pid in (1, 2):
+                    learner.do_actions(pid, [rng.uniform(-1, 1), rng.uniform(-1, 1)])
+                g.game_tick()
+                if t % 20 == 7:
+                    snap = snapshot(g)
+                    st = g.get_state()
+                    states.append(snap)
+                    boards.append(g.get_board().astype(np.int8))
+                    feats.append([[float(st[pid][k]) for k in keys] for pid in (1, 2)])
+                    general.append([int(bool(st["game_live"])), int(st["ticks"]), int(st["game_winner"])])
+    out = dict(
+        pos=np.array([s["pos"] for s in states], np.int32), rot=np.array([s["rot"] for s in states]),
+        qpos=np.array([s["qpos"] for s in states], np.int32), qrot=np.array([s["qrot"] for s in states]),
+        qcd=np.array([s["qcd"] for s in states], np.int32), qage=np.array([s["qage"] for s in states], np.int32),
+        qvalid=np.array([s["qvalid"] for s in states], np.uint8),
+        ticks=np.array([s["ticks"] for s in states], np.int32), live=np.array([s["live"] for s in states], np.uint8),
+        winner=np.array([s["winner"] for s in states], np.uint8),
+        board=np.stack(boards), features=np.array(feats, np.float64), general=np.array(general, np.int64),
+        numpy_version=np.array(np.__version__))
+    path = os.path.join(OUT, "boards.npz")
+    np.savez_compressed(path, **out)
+    print(f"boards: {len(states)} states -> {os.path.getsize(path)} bytes")
+
+
+if __name__ == "__main__":
+    scenario_boards()

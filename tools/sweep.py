@@ -33,7 +33,7 @@ def run(variant, n, steps, graph_len, ring, obs=False):
     a0 = acts.data_ptr()
 
     planes = (ctypes.c_void_p * 6)(*[getattr(env, k).data_ptr() for k in ("pos", "rot", "qpos", "qrot", "qcdage", "misc")])
-    diag = {"empty": 0, "copy": 1}.get(variant)
+    diag = {"empty": 0, "copy": 1, "copy_xcc": 2, "copy_b8": 3}.get(variant)
     if diag is not None:
         L = env._L
         L.skdiag_launch.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
