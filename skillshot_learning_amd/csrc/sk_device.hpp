@@ -16,6 +16,7 @@
 #include <stdint.h>
 
 #include "../../include/skillshot.h"
+#include "sk_trig.hpp"
 
 namespace sk {
 
@@ -244,6 +245,79 @@ __device__ __forceinline__ void game_tick(const Cfg& c, Env& e) {
     e.ticks += 1;
     projectile_tick(c, e, 0);
     projectile_tick(c, e, 1);
+    collide_s(c, e.px[0], e.py[0], e.qx[0], e.qy[0], e.qvalid[0], e.px[1], e.py[1], e.qx[1], e.qy[1],
+              e.qvalid[1], e.live, e.winner);
+  }
+}
+
+// ---------------------------------------------------------------- fused tick
+// One learner tick of one env (do_actions(1), do_actions(2), game_tick) with
+// the four sin/cos the tick needs evaluated up front: the players' move
+// directions use the pre-look rotations, and each projectile flies with the
+// rotation it has after shoot — player p's post-look rotation if its cooldown
+// allows firing (Player.py:80-84), else its stored one — all known from the
+// loaded state and actions.  The four branch-free sincos_bf chains are
+// independent, so they interleave (4-way ILP at one wave per SIMD).  Every
+// arithmetic step that feeds the state is the same expression as in the
+// per-method helpers above.
+__device__ __forceinline__ void move_direction_sc(const Cfg& c, int& x, int& y, sktrig::SinCos t, double speed) {
+  speed = clamp_action(speed);  // Player.py:57-68
+  const double sp = (double)c.pspeed;
+  double nxf = __builtin_rint((double)x - (t.s * sp) * speed);
+  double nyf = __builtin_rint((double)y - (t.c * sp) * speed);
+  bool ok = (nxf >= 0.0) & (nxf + (double)c.psize <= (double)c.W) & (nyf >= 0.0) &
+            (nyf + (double)c.psize <= (double)c.H);
+  if (ok) { x = (int)nxf; y = (int)nyf; }
+}
+
+__device__ __forceinline__ void projectile_tick_sc(const Cfg& c, int& qx, int& qy, sktrig::SinCos t, int& qcd,
+                                                   int& qage, int& qvalid) {
+  if (qvalid) {  // Projectile.py:38-53
+    const double sp = (double)c.qspeed;
+    int nx = (int)__builtin_rint((double)qx - t.s * sp);
+    int ny = (int)__builtin_rint((double)qy - t.c * sp);
+    bool ok = (nx + c.qsize <= c.W) & (nx >= 0) & (ny + c.qsize <= c.H) & (ny >= 0);
+    if (ok) { qx = nx; qy = ny; } else { qvalid = 0; }
+  }
+  qcd -= 1;
+  qage += 1;
+}
+
+__device__ __attribute__((noinline)) sktrig::SinCos sincos_lib(double x) {  // |x| >= 1.6e6 or non-finite
+  sktrig::SinCos o;
+  sincos(x, &o.s, &o.c);
+  return o;
+}
+
+__device__ __forceinline__ void tick_env(const Cfg& c, Env& e, double a0_move, double a0_look, double a1_move,
+                                         double a1_look) {
+  const double rn0 = e.rot[0] + clamp_action(a0_look) * c.look;  // == move_look_s
+  const double rn1 = e.rot[1] + clamp_action(a1_look) * c.look;
+  const double q0 = (e.qcd[0] <= 0) ? rn0 : e.qrot[0];
+  const double q1 = (e.qcd[1] <= 0) ? rn1 : e.qrot[1];
+  bool k0, k1, k2, k3;
+  sktrig::SinCos m0 = sktrig::sincos_bf(e.rot[0], &k0);
+  sktrig::SinCos m1 = sktrig::sincos_bf(e.rot[1], &k1);
+  sktrig::SinCos t0 = sktrig::sincos_bf(q0, &k2);
+  sktrig::SinCos t1 = sktrig::sincos_bf(q1, &k3);
+  if (!(k0 & k1 & k2 & k3)) {
+    if (!k0) m0 = sincos_lib(e.rot[0]);
+    if (!k1) m1 = sincos_lib(e.rot[1]);
+    if (!k2) t0 = sincos_lib(q0);
+    if (!k3) t1 = sincos_lib(q1);
+  }
+  // do_actions(1, ...), do_actions(2, ...)  SkillshotLearner.py:206-213
+  move_direction_sc(c, e.px[0], e.py[0], m0, a0_move);
+  e.rot[0] = rn0;
+  shoot(c, e, 0);
+  move_direction_sc(c, e.px[1], e.py[1], m1, a1_move);
+  e.rot[1] = rn1;
+  shoot(c, e, 1);
+  // game_tick  SkillshotGame.py:115-122
+  if (e.live) {
+    e.ticks += 1;
+    projectile_tick_sc(c, e.qx[0], e.qy[0], t0, e.qcd[0], e.qage[0], e.qvalid[0]);
+    projectile_tick_sc(c, e.qx[1], e.qy[1], t1, e.qcd[1], e.qage[1], e.qvalid[1]);
     collide_s(c, e.px[0], e.py[0], e.qx[0], e.qy[0], e.qvalid[0], e.px[1], e.py[1], e.qx[1], e.qy[1],
               e.qvalid[1], e.live, e.winner);
   }

@@ -155,14 +155,7 @@ __global__ void __launch_bounds__(kBlock) k_step(StepArgs a, Cfg c) {
     load_env(a.v, i, e);
     float2 a0 = a.actions[i];
     float2 a1 = a.actions[a.n + i];
-    // do_actions(1, ...), do_actions(2, ...)  SkillshotLearner.py:206-213
-    move_direction(c, e, 0, (double)a0.x);
-    move_look(c, e, 0, (double)a0.y);
-    shoot(c, e, 0);
-    move_direction(c, e, 1, (double)a1.x);
-    move_look(c, e, 1, (double)a1.y);
-    shoot(c, e, 1);
-    game_tick(c, e);
+    tick_env(c, e, (double)a0.x, (double)a0.y, (double)a1.x, (double)a1.y);
     if (a.obs || a.reward) {
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
@@ -227,14 +220,23 @@ __global__ void __launch_bounds__(kBlock) k_step_split(StepArgs a, Cfg c) {
   int qvalid = ((unsigned)flags >> (8 * p)) & 0xff;
   int live = ((unsigned)flags >> 16) & 0xff;
   int winner = ((unsigned)flags >> 24) & 0xff;
-  // do_actions(p+1, ...)  SkillshotLearner.py:206-213
-  move_direction_s(c, px, py, rot, (double)act.x);
-  move_look_s(c, rot, (double)act.y);
+  // do_actions(p+1, ...)  SkillshotLearner.py:206-213, both sincos up front (tick_env)
+  const double rn = rot + clamp_action((double)act.y) * c.look;
+  const double qn = (qcd <= 0) ? rn : qrot;
+  bool k0, k1;
+  sktrig::SinCos m = sktrig::sincos_bf(rot, &k0);
+  sktrig::SinCos t = sktrig::sincos_bf(qn, &k1);
+  if (!(k0 & k1)) {
+    if (!k0) m = sincos_lib(rot);
+    if (!k1) t = sincos_lib(qn);
+  }
+  move_direction_sc(c, px, py, m, (double)act.x);
+  rot = rn;
   shoot_s(c, px, py, rot, qx, qy, qrot, qcd, qage, qvalid);
   // game_tick  SkillshotGame.py:115-122 (live is identical in both lanes)
   if (live) {
     ticks += 1;
-    projectile_tick_s(c, qx, qy, qrot, qcd, qage, qvalid);
+    projectile_tick_sc(c, qx, qy, t, qcd, qage, qvalid);
   }
   const int opx = __shfl_xor(px, 1, 64), opy = __shfl_xor(py, 1, 64);
   const int oqx = __shfl_xor(qx, 1, 64), oqy = __shfl_xor(qy, 1, 64), oqv = __shfl_xor(qvalid, 1, 64);
@@ -323,13 +325,8 @@ __global__ void __launch_bounds__(kBlock) k_rollout_random(RolloutArgs a, Cfg c)
     for (int t = 0; t < a.n_ticks; ++t) {
       uint64_t step = step0 + (uint64_t)t;
       U4 u = draw4(a.seed, genv, step, 0u);
-      move_direction(c, e, 0, (double)u32_to_action(u.x));
-      move_look(c, e, 0, (double)u32_to_action(u.y));
-      shoot(c, e, 0);
-      move_direction(c, e, 1, (double)u32_to_action(u.z));
-      move_look(c, e, 1, (double)u32_to_action(u.w));
-      shoot(c, e, 1);
-      game_tick(c, e);
+      tick_env(c, e, (double)u32_to_action(u.x), (double)u32_to_action(u.y), (double)u32_to_action(u.z),
+               (double)u32_to_action(u.w));
       if ((!e.live) || (e.ticks >= a.tick_limit)) {
         dones += 1;
         w1 += (e.winner == 1);

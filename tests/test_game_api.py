@@ -135,7 +135,8 @@ def test_reset_and_errors(game_mod):
     assert g.player1.rotation == 0.25
     g.player1.move_forwards()
     assert g.player1.pos == [int(round(60 - math.sin(0.25) * 3)), int(round(50 - math.cos(0.25) * 3))]
-    g.player2.projectile.pos = [52, 56]
+    x, y = g.player1.pos
+    g.player2.projectile.pos = [x + 1, y + 3]  # corners (x+4|x+1, y+3|y) inside P1's 5x5 box
     g.player2.projectile.valid = True
     out = io.StringIO()
     with contextlib.redirect_stdout(out):
