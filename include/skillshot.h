@@ -42,6 +42,7 @@
 #ifndef SKILLSHOT_H
 #define SKILLSHOT_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -207,6 +208,24 @@ int sk_gen_random_actions(sk_env* env, float* actions, int32_t n_ticks, void* st
  * sk_env_step on sk_gen_random_actions output.  Advances the step counter by
  * n_ticks. */
 int sk_env_rollout_random(sk_env* env, int32_t n_ticks, int32_t tick_limit, void* stream);
+
+/* --- actor forward (A13) ------------------------------------------------ */
+
+/* Fused MFMA forward of the actor of model_define_actor
+ * (SkillshotLearner.py:70-96): a = tanh(W3 relu(W2 relu(W1 s + b1) + b2) + b3),
+ * 12 -> 256 -> 128 -> 2, bf16 operands with fp32 accumulation, for `rows`
+ * observations (obs float[rows][12] -> actions float[rows][2]).
+ * noise_sd != 0 samples model_act_param_noise (:245-281) for every row
+ * independently (w -> w(1 + noise_sd*N(0,1)), exact in distribution by local
+ * reparameterisation), keyed by (seed, row, call).
+ * Weights are the torch Linear fp32 tensors ([out][in] row-major, device
+ * memory), packed once per update by sk_actor_pack into a device buffer of
+ * sk_actor_packed_bytes() bytes (16-byte aligned). */
+size_t sk_actor_packed_bytes(void);
+int sk_actor_pack(const float* W1, const float* b1, const float* W2, const float* b2, const float* W3,
+                  const float* b3, void* packed, void* stream);
+int sk_actor_forward(const void* packed, const float* obs, float* actions, int64_t rows, float noise_sd,
+                     uint64_t seed, uint64_t call, void* stream);
 
 #ifdef __cplusplus
 }

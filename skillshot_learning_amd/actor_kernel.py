@@ -1,0 +1,57 @@
+"""Fused MFMA actor forward (csrc/sk_actor.hip) bound to a torch Actor.
+
+The torch module stays the master copy (fp32, trained by autograd); after each
+optimiser step `refresh()` repacks its weights into the kernel's bf16 MFMA
+fragment layout on device (one small kernel, no host copy).
+"""
+import ctypes
+
+import torch
+
+from . import _capi
+from ._capi import SkillshotError
+
+
+class ActorKernel:
+    def __init__(self, actor, seed=0):
+        self.actor = actor
+        self.L = _capi.load()
+        p = next(actor.parameters())
+        if p.device.type != "cuda":
+            raise SkillshotError("ActorKernel needs the actor on a gfx950 GPU")
+        self.device = p.device
+        self.buf = torch.empty(int(self.L.sk_actor_packed_bytes()), dtype=torch.uint8, device=self.device)
+        self.seed = int(seed) & ((1 << 64) - 1)
+        self.calls = 0
+        self.refresh()
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    @torch.no_grad()
+    def refresh(self):
+        a = self.actor
+        ws = [t.detach().contiguous() for t in (a.l1.weight, a.l1.bias, a.l2.weight, a.l2.bias, a.l3.weight,
+                                                a.l3.bias)]
+        self._keep = ws
+        rc = self.L.sk_actor_pack(*[ctypes.c_void_p(t.data_ptr()) for t in ws], ctypes.c_void_p(self.buf.data_ptr()),
+                                  self._stream())
+        if rc != 0:
+            raise SkillshotError(f"sk_actor_pack failed ({rc})")
+
+    @torch.no_grad()
+    def __call__(self, obs, noise_sd=0.0, generator=None, out=None):
+        """obs float32 [M, 12] -> actions float32 [M, 2]."""
+        x = obs if obs.dtype == torch.float32 else obs.float()
+        x = x.contiguous()
+        if x.dim() != 2 or x.shape[1] != 12:
+            raise ValueError("obs must be [M, 12]")
+        m = x.shape[0]
+        y = out if out is not None else torch.empty((m, 2), dtype=torch.float32, device=self.device)
+        self.calls += 1
+        rc = self.L.sk_actor_forward(ctypes.c_void_p(self.buf.data_ptr()), ctypes.c_void_p(x.data_ptr()),
+                                     ctypes.c_void_p(y.data_ptr()), m, float(noise_sd), self.seed, self.calls,
+                                     self._stream())
+        if rc != 0:
+            raise SkillshotError(f"sk_actor_forward failed ({rc})")
+        return y

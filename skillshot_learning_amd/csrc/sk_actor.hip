@@ -1,0 +1,336 @@
+// sk_actor.hip — fused actor MLP forward on MFMA (gfx950), with per-row
+// parameter noise by local reparameterisation.
+//
+// Replaces the batched form of model_actor.predict (SkillshotLearner.py:222,
+// 235, 271) on the actor of model_define_actor (:70-96):
+//     a = tanh(W3 relu(W2 relu(W1 s + b1) + b2) + b3),  s: 12 -> 256 -> 128 -> 2
+// and model_act_param_noise (:245-281), where every weight and bias becomes
+// w(1 + sd*eps) afresh per call: with one independent noisy actor per row,
+// each noisy weight is used once per row, so every pre-activation is exactly
+//     y = W x + b + sd * sqrt(W^2 x^2 + b^2) * xi,  xi ~ N(0,1) per unit and row.
+//
+// Layout (cdna_hip_programming.md §3 "accumulator tile as the next MFMA's
+// operand"): activations are kept TRANSPOSED, H^T = W X^T, with the batch row
+// on the lane and hidden units in the 16 accumulator registers of a
+// v_mfma_f32_32x32x16_bf16 tile, so each layer's accumulator converts in
+// registers to the next layer's B operand; the weights are pre-packed
+// (k_actor_pack) into A fragments in the matching permuted k order.
+// Per 32-row tile: layer 1 8 MFMAs, layer 2 64, layer 3 8 (x2 with noise).
+// W2 (and W2^2) fragments are staged once per workgroup in LDS (64/128 KiB);
+// W1/W3 fragments (8 KiB each) are read through L1.  bf16 operands, fp32
+// accumulate, fp32 bias/noise/activation epilogues.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/skillshot.h"
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+constexpr int kIn = 12, kH1 = 256, kH2 = 128, kOut = 2;
+constexpr int kThreads = 512;  // 8 waves: two per SIMD
+
+// packed buffer layout (bytes)
+constexpr int kW1Frag = 8 * 64 * 16;        // 8 hidden chunks x 64 lanes x 8 bf16
+constexpr int kW2Frag = 4 * 16 * 64 * 16;   // 4 out chunks x 16 k-steps x 64 lanes x 8 bf16
+constexpr int kW3Frag = 8 * 64 * 16;        // 8 k-steps x 64 lanes x 8 bf16
+constexpr size_t kOffW1 = 0, kOffW1s = kOffW1 + kW1Frag;
+constexpr size_t kOffW2 = kOffW1s + kW1Frag, kOffW2s = kOffW2 + kW2Frag;
+constexpr size_t kOffW3 = kOffW2s + kW2Frag, kOffW3s = kOffW3 + kW3Frag;
+constexpr size_t kOffB = kOffW3s + kW3Frag;  // fp32: b1[256] b2[128] b3[2] (pad 512)
+constexpr size_t kPackedBytes = kOffB + 512 * 4;
+
+__device__ __forceinline__ short f2bf(float f) {  // round-to-nearest-even (v_cvt_pk_bf16_f32)
+  return __builtin_bit_cast(short, (__bf16)f);
+}
+
+// elementwise square of a bf16 fragment (the variance chain's operand x^2 is
+// derived at use instead of stored: keeps the noise kernel inside 256 VGPRs)
+__device__ __forceinline__ bf16x8 sq_bf16(bf16x8 a) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float v = (float)__builtin_bit_cast(__bf16, a[j]);
+    r[j] = f2bf(v * v);
+  }
+  return r;
+}
+
+// ---------------------------------------------------------------- packing
+// W1: [256][12] row-major (torch Linear weight [out][in]); A fragment of
+// hidden chunk c, lane (r, h), element j = W1[32c + r][8h + j] (k >= 12 -> 0).
+// W2: [128][256]; chunk t, k-step kk, lane (r, h), element j =
+//     W2[32t + r][32(kk>>1) + 16(kk&1) + 8(j>>2) + 4h + (j&3)]  (the row order
+//     of the previous accumulator's registers 8s..8s+7, s = kk&1).
+// W3: [2][128] padded to 32 rows; k-step kk as W2.
+__global__ void k_actor_pack(const float* W1, const float* b1, const float* W2, const float* b2, const float* W3,
+                             const float* b3, char* out) {
+  int t = blockIdx.x * blockDim.x + threadIdx.x;
+  short* w1 = (short*)(out + kOffW1);
+  short* w1s = (short*)(out + kOffW1s);
+  short* w2 = (short*)(out + kOffW2);
+  short* w2s = (short*)(out + kOffW2s);
+  short* w3 = (short*)(out + kOffW3);
+  short* w3s = (short*)(out + kOffW3s);
+  float* bias = (float*)(out + kOffB);
+  // one thread per (fragment, lane): layer 1 (8*64), layer 2 (64*64), layer 3 (8*64)
+  if (t < 8 * 64) {
+    int c = t >> 6, lane = t & 63, r = lane & 31, h = lane >> 5;
+    for (int j = 0; j < 8; ++j) {
+      int k = 8 * h + j;
+      float v = k < kIn ? W1[(32 * c + r) * kIn + k] : 0.f;
+      w1[t * 8 + j] = f2bf(v);
+      w1s[t * 8 + j] = f2bf(v * v);
+    }
+  } else if (t < 8 * 64 + 64 * 64) {
+    int u = t - 8 * 64;
+    int frag = u >> 6, lane = u & 63, r = lane & 31, h = lane >> 5;
+    int tt = frag >> 4, kk = frag & 15;
+    for (int j = 0; j < 8; ++j) {
+      int k = 32 * (kk >> 1) + 16 * (kk & 1) + 8 * (j >> 2) + 4 * h + (j & 3);
+      float v = W2[(32 * tt + r) * kH1 + k];
+      w2[u * 8 + j] = f2bf(v);
+      w2s[u * 8 + j] = f2bf(v * v);
+    }
+  } else if (t < 8 * 64 + 64 * 64 + 8 * 64) {
+    int u = t - 8 * 64 - 64 * 64;
+    int kk = u >> 6, lane = u & 63, r = lane & 31, h = lane >> 5;
+    for (int j = 0; j < 8; ++j) {
+      int k = 32 * (kk >> 1) + 16 * (kk & 1) + 8 * (j >> 2) + 4 * h + (j & 3);
+      float v = r < kOut ? W3[r * kH2 + k] : 0.f;
+      w3[u * 8 + j] = f2bf(v);
+      w3s[u * 8 + j] = f2bf(v * v);
+    }
+  } else if (t < 8 * 64 + 64 * 64 + 8 * 64 + 512) {
+    int u = t - 8 * 64 - 64 * 64 - 8 * 64;
+    float v = 0.f;
+    if (u < kH1) v = b1[u];
+    else if (u < kH1 + kH2) v = b2[u - kH1];
+    else if (u < kH1 + kH2 + kOut) v = b3[u - kH1 - kH2];
+    bias[u] = v;
+  }
+}
+
+// ---------------------------------------------------------------- noise
+__device__ __forceinline__ uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+    uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// 16 standard normals for (row, stream): Box-Muller on 4 Philox draws.
+// v_sin/v_cos take revolutions, v_log is log2.
+__device__ __forceinline__ void normals16(uint64_t seed, uint64_t call, uint32_t row, uint32_t stream,
+                                          float z[16]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint4 u = philox(make_uint4(row, stream * 4 + q, (uint32_t)call, (uint32_t)(call >> 32)), (uint32_t)seed,
+                     (uint32_t)(seed >> 32));
+    uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      float u1 = ((float)(w[2 * p] >> 8) + 0.5f) * 0x1p-24f;  // (0, 1)
+      float u2 = (float)(w[2 * p + 1] >> 8) * 0x1p-24f;       // [0, 1)
+      float rad = __builtin_sqrtf(-2.0f * 0.69314718056f * __builtin_amdgcn_logf(u1));
+      z[4 * q + 2 * p] = rad * __builtin_amdgcn_cosf(u2);
+      z[4 * q + 2 * p + 1] = rad * __builtin_amdgcn_sinf(u2);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- forward
+template <bool NOISE>
+__global__ void __launch_bounds__(kThreads) k_actor_fwd(const float* __restrict__ X, float* __restrict__ out,
+                                                        int64_t M, const char* __restrict__ packed, float sd,
+                                                        uint64_t seed, uint64_t call) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16x8* sW2 = (bf16x8*)smem;                               // [4][16][64]
+  bf16x8* sW2s = (bf16x8*)(smem + kW2Frag);                  // NOISE only
+  float* sB = (float*)(smem + (NOISE ? 2 : 1) * kW2Frag);    // b1 b2 b3
+
+  {  // stage W2 fragments (+ squares) and biases once per workgroup
+    const uint4* g = (const uint4*)(packed + kOffW2);
+    uint4* s = (uint4*)smem;
+    const int n16 = (NOISE ? 2 : 1) * kW2Frag / 16;
+    for (int k = threadIdx.x; k < n16; k += kThreads) s[k] = g[k];  // W2s follows W2 in the buffer
+    const float* gb = (const float*)(packed + kOffB);
+    for (int k = threadIdx.x; k < 512; k += kThreads) sB[k] = gb[k];
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int64_t ntiles = (M + 31) / 32;
+  const int64_t wave = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * (kThreads / 64);
+
+  for (int64_t tile = wave; tile < ntiles; tile += nwaves) {
+    // launder the weight base each tile: otherwise LICM hoists all 32 W1/W3
+    // fragment loads out of the tile loop and spills them
+    const char* pk = packed;
+    asm volatile("" : "+s"(pk));
+    const bf16x8* gW1 = (const bf16x8*)(pk + kOffW1);
+    const bf16x8* gW1s = (const bf16x8*)(pk + kOffW1s);
+    const bf16x8* gW3 = (const bf16x8*)(pk + kOffW3);
+    const bf16x8* gW3s = (const bf16x8*)(pk + kOffW3s);
+    const int64_t row = tile * 32 + r;
+    const bool valid = row < M;
+    // ---- X^T fragment: B[k = 8h + j][col r] = X[row][8h + j]
+    float x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = 0.f;
+    if (valid) {
+      const float* xr = X + row * kIn + 8 * h;
+      if (h == 0) {
+        float4 a = *(const float4*)xr, b = *(const float4*)(xr + 4);
+        x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+      } else {
+        float4 a = *(const float4*)xr;
+        x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
+      }
+    }
+    bf16x8 xb, xs;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      xb[j] = f2bf(x[j]);
+      xs[j] = f2bf(x[j] * x[j]);
+    }
+
+    // ---- layer 1: H1^T = relu(W1 X^T + b1 [+ noise]) -> 16 B fragments (k-steps of layer 2)
+    bf16x8 h1[16];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      f32x16 acc = {0}, var = {0};
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gW1[c * 64 + lane], xb, acc, 0, 0, 0);
+      if (NOISE) var = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gW1s[c * 64 + lane], xs, var, 0, 0, 0);
+      float z[16];
+      if (NOISE) normals16(seed, call, (uint32_t)row, (uint32_t)c, z);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int hid = 32 * c + (i & 3) + 8 * (i >> 2) + 4 * h;
+        const float b = sB[hid];
+        float y = acc[i] + b;
+        if (NOISE) y += sd * __builtin_sqrtf(fmaxf(var[i] + b * b, 0.f)) * z[i];
+        y = fmaxf(y, 0.f);
+        acc[i] = y;
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = f2bf(acc[8 * s + j]);
+        h1[2 * c + s] = f;
+      }
+      __builtin_amdgcn_sched_barrier(0);  // one chunk's accumulators live at a time
+    }
+
+    // ---- layer 2: H2^T = relu(W2 H1^T + b2 [+ noise])
+    bf16x8 h2[8];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      f32x16 acc = {0}, var = {0};
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) {
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sW2[(t * 16 + kk) * 64 + lane], h1[kk], acc, 0, 0, 0);
+        if (NOISE)
+          var = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sW2s[(t * 16 + kk) * 64 + lane], sq_bf16(h1[kk]), var, 0, 0,
+                                                        0);
+        if (NOISE && (kk & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // cap hoisted LDS fragments
+      }
+      float z[16];
+      if (NOISE) normals16(seed, call, (uint32_t)row, (uint32_t)(8 + t), z);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int hid = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
+        const float b = sB[kH1 + hid];
+        float y = acc[i] + b;
+        if (NOISE) y += sd * __builtin_sqrtf(fmaxf(var[i] + b * b, 0.f)) * z[i];
+        acc[i] = fmaxf(y, 0.f);
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = f2bf(acc[8 * s + j]);
+        h2[2 * t + s] = f;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+
+    // ---- layer 3: a = tanh(W3 H2^T + b3 [+ noise]); rows 0,1 = registers 0,1 of lanes 0..31
+    f32x16 acc = {0}, var = {0};
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gW3[kk * 64 + lane], h2[kk], acc, 0, 0, 0);
+      if (NOISE) var = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gW3s[kk * 64 + lane], sq_bf16(h2[kk]), var, 0, 0, 0);
+    }
+    if (h == 0 && valid) {
+      float z[16];
+      if (NOISE) normals16(seed, call, (uint32_t)row, 12u, z);
+      float o[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const float b = sB[kH1 + kH2 + i];
+        float y = acc[i] + b;
+        if (NOISE) y += sd * __builtin_sqrtf(fmaxf(var[i] + b * b, 0.f)) * z[i];
+        o[i] = tanhf(y);
+      }
+      *(float2*)(out + row * kOut) = make_float2(o[0], o[1]);
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t sk_actor_packed_bytes(void) { return kPackedBytes; }
+
+int sk_actor_pack(const float* W1, const float* b1, const float* W2, const float* b2, const float* W3,
+                  const float* b3, void* packed, void* stream) {
+  if (!W1 || !b1 || !W2 || !b2 || !W3 || !b3 || !packed) return SK_EINVAL;
+  if (((uintptr_t)packed) & 15) return SK_EINVAL;
+  const int total = 8 * 64 + 64 * 64 + 8 * 64 + 512;
+  k_actor_pack<<<(total + 255) / 256, 256, 0, (hipStream_t)stream>>>(W1, b1, W2, b2, W3, b3, (char*)packed);
+  return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
+}
+
+int sk_actor_forward(const void* packed, const float* obs, float* actions, int64_t rows, float noise_sd,
+                     uint64_t seed, uint64_t call, void* stream) {
+  if (!packed || !obs || !actions || rows < 0) return SK_EINVAL;
+  if ((((uintptr_t)obs) & 15) || (((uintptr_t)actions) & 7) || (((uintptr_t)packed) & 15)) return SK_EINVAL;
+  if (rows == 0) return SK_OK;
+  int dev = 0, cus = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int64_t tiles = (rows + 31) / 32;
+  int64_t grid = (tiles + kThreads / 64 - 1) / (kThreads / 64);
+  if (grid > cus) grid = cus;  // one 512-thread workgroup per CU (LDS-limited), tiles grid-strided
+  const bool noise = noise_sd != 0.f;
+  const size_t lds = (noise ? 2 : 1) * kW2Frag + 512 * 4;
+  static bool attr_set = false;  // dynamic LDS above 64 KiB must be opted into once
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)k_actor_fwd<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              2 * kW2Frag + 512 * 4);
+    (void)hipFuncSetAttribute((const void*)k_actor_fwd<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              kW2Frag + 512 * 4);
+    attr_set = true;
+  }
+  if (noise) {
+    k_actor_fwd<true><<<(unsigned)grid, kThreads, lds, (hipStream_t)stream>>>(obs, actions, rows, (const char*)packed,
+                                                                             noise_sd, seed, call);
+  } else {
+    k_actor_fwd<false><<<(unsigned)grid, kThreads, lds, (hipStream_t)stream>>>(obs, actions, rows,
+                                                                              (const char*)packed, 0.f, seed, call);
+  }
+  return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
+}
+
+}  // extern "C"

@@ -1,0 +1,414 @@
+"""SkillshotLearner on PyTorch-ROCm over the batched GPU engine.
+
+Mirrors SkillshotLearner.py (adrientremblay/Skillshot_Learning):
+  * actor  12 -> 256 relu -> 128 relu -> 2 tanh, kernels N(0, 0.05), zero
+    biases (model_define_actor, :70-96)
+  * critic state -> 256 relu -> Dropout(0.2) -> concat(action) -> 128 relu
+    -> 1 linear, glorot-uniform hidden kernels, N(0, 0.05) output kernel
+    (model_define_critic, :98-121)
+  * the reference update rule (models_fit :419-443, model_actor_fit_step
+    :386-417): shuffle, critic MSE to the IMMEDIATE reward at batch 16 for one
+    pass with dropout active, then per batch of 16 an actor step on
+    -sum_batch Q(s, mu(s)) (critic in inference mode); Adam lr 1e-3, eps 1e-7
+    (Keras defaults)
+  * exploration (:215-281): deterministic, action noise N(0, 0.15), or
+    parameter noise w <- w + w * N(0, 0.5) drawn afresh per player per tick.
+    Batched, every (game, player) gets its own noisy actor; that is sampled
+    EXACTLY in distribution by local reparameterisation (each noisy weight is
+    used once per forward): per layer y = xW + b + 0.5 * sqrt(x^2 W^2 + b^2) * xi.
+
+Build-side extensions (BASELINE.json north_star; no reference row): an HBM
+replay ring (112 B per transition), target networks with soft update tau,
+a discount gamma (0 keeps the reference's immediate-reward critic), and the
+multi-GPU path: one process per GPU, games sharded by global id, gradients
+all-reduced (RCCL over xGMI; gloo on CPU) as one flat bucket per update, and
+each rank's sampled minibatch all-gathered into a shared batch.
+"""
+import math
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.nn.functional as F
+
+STATE_DIM = 12   # SkillshotLearner.py:54
+ACTION_DIM = 2   # :55
+
+
+def _keras_normal_(t, std=0.05):
+    with torch.no_grad():
+        t.normal_(0.0, std)
+
+
+def _glorot_uniform_(w):
+    fan_out, fan_in = w.shape
+    limit = math.sqrt(6.0 / (fan_in + fan_out))
+    with torch.no_grad():
+        w.uniform_(-limit, limit)
+
+
+class Actor(nn.Module):
+    """model_define_actor (SkillshotLearner.py:70-96)."""
+
+    def __init__(self):
+        super().__init__()
+        self.l1 = nn.Linear(STATE_DIM, 256)
+        self.l2 = nn.Linear(256, 128)
+        self.l3 = nn.Linear(128, ACTION_DIM)
+        for l in (self.l1, self.l2, self.l3):
+            _keras_normal_(l.weight, 0.05)  # RandomNormal(0, 0.05), :74
+            nn.init.zeros_(l.bias)          # Keras Dense default
+
+    def forward(self, s):
+        h = F.relu(self.l1(s))
+        h = F.relu(self.l2(h))
+        return torch.tanh(self.l3(h))
+
+    def forward_param_noise(self, s, sd, generator=None):
+        """Per-row independent parameter noise w' = w(1 + sd*eps), sampled by
+        local reparameterisation (exact in distribution, see module doc)."""
+        x = s
+        for k, l in enumerate((self.l1, self.l2, self.l3)):
+            mean = F.linear(x, l.weight, l.bias)
+            var = F.linear(x * x, l.weight * l.weight, l.bias * l.bias)
+            xi = torch.randn(mean.shape, device=mean.device, dtype=mean.dtype, generator=generator)
+            y = mean + sd * torch.sqrt(var) * xi
+            x = torch.tanh(y) if k == 2 else F.relu(y)
+        return x
+
+
+class Critic(nn.Module):
+    """model_define_critic (SkillshotLearner.py:98-121)."""
+
+    def __init__(self):
+        super().__init__()
+        self.l1 = nn.Linear(STATE_DIM, 256)
+        self.drop = nn.Dropout(0.2)
+        self.l2 = nn.Linear(256 + ACTION_DIM, 128)
+        self.l3 = nn.Linear(128, 1)
+        _glorot_uniform_(self.l1.weight)
+        _glorot_uniform_(self.l2.weight)
+        _keras_normal_(self.l3.weight, 0.05)  # kernel_initializer="RandomNormal"
+        for l in (self.l1, self.l2, self.l3):
+            nn.init.zeros_(l.bias)
+
+    def forward(self, s, a):
+        h = self.drop(F.relu(self.l1(s)))
+        h = F.relu(self.l2(torch.cat([h, a], dim=-1)))
+        return self.l3(h)
+
+
+def keras_adam(params):
+    return torch.optim.Adam(params, lr=1e-3, betas=(0.9, 0.999), eps=1e-7)
+
+
+class ReplayRing:
+    """Transitions (s 12f, a 2f, r 1f, s' 12f, done 1f = 112 B) in HBM."""
+
+    def __init__(self, capacity, device):
+        self.cap = int(capacity)
+        self.s = torch.zeros(self.cap, STATE_DIM, device=device)
+        self.a = torch.zeros(self.cap, ACTION_DIM, device=device)
+        self.r = torch.zeros(self.cap, device=device)
+        self.s2 = torch.zeros(self.cap, STATE_DIM, device=device)
+        self.d = torch.zeros(self.cap, device=device)
+        self.head = 0
+        self.size = 0
+
+    def add(self, s, a, r, s2, d):
+        n = s.shape[0]
+        if n > self.cap:
+            s, a, r, s2, d = s[-self.cap:], a[-self.cap:], r[-self.cap:], s2[-self.cap:], d[-self.cap:]
+            n = self.cap
+        idx = (torch.arange(n, device=s.device) + self.head) % self.cap
+        self.s[idx] = s
+        self.a[idx] = a
+        self.r[idx] = r
+        self.s2[idx] = s2
+        self.d[idx] = d
+        self.head = (self.head + n) % self.cap
+        self.size = min(self.cap, self.size + n)
+
+    def sample(self, b, generator=None):
+        idx = torch.randint(0, self.size, (b,), device=self.s.device, generator=generator)
+        return self.s[idx], self.a[idx], self.r[idx], self.s2[idx], self.d[idx]
+
+
+class DDPG:
+    """Actor/critic, optimisers and update rules (device-agnostic: CPU tests
+    and gloo multi-process tests drive it without a GPU)."""
+
+    def __init__(self, device="cpu", seed=0, batch_size=16, gamma=0.0, tau=None, replay_capacity=0,
+                 process_group=None, rank_seed_offset=0):
+        self.device = torch.device(device)
+        torch.manual_seed(seed)
+        self.model_actor = Actor().to(self.device)
+        self.model_critic = Critic().to(self.device)
+        self.group = process_group
+        self._sync_params()
+        self.optimiser = keras_adam(self.model_actor.parameters())         # SkillshotLearner.py:68
+        self.critic_optimiser = keras_adam(self.model_critic.parameters())  # critic.compile("adam"), :118
+        self.model_param_batch_size = batch_size
+        self.gamma = float(gamma)
+        self.tau = tau
+        if tau is not None:
+            self.target_actor = Actor().to(self.device)
+            self.target_critic = Critic().to(self.device)
+            self.target_actor.load_state_dict(self.model_actor.state_dict())
+            self.target_critic.load_state_dict(self.model_critic.state_dict())
+        self.replay = ReplayRing(replay_capacity, self.device) if replay_capacity else None
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(seed * 7919 + rank_seed_offset + 17)
+
+    # ------------------------------------------------------------ distributed
+    def world(self):
+        return dist.get_world_size(self.group) if dist.is_available() and dist.is_initialized() else 1
+
+    def _sync_params(self):
+        """Start every rank from rank 0's weights (broadcast)."""
+        if self.world() > 1:
+            for m in (self.model_actor, self.model_critic):
+                for p in m.parameters():
+                    dist.broadcast(p.data, src=0, group=self.group)
+
+    def _allreduce_grads(self, module):
+        """Gradient all-reduce (mean) as ONE flat bucket per update:
+        36,482 actor / 36,609 critic fp32 parameters (RCCL over xGMI)."""
+        if self.world() <= 1:
+            return
+        grads = [p.grad for p in module.parameters()]
+        flat = torch.cat([g.reshape(-1) for g in grads])
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+        flat /= self.world()
+        off = 0
+        for g in grads:
+            n = g.numel()
+            g.copy_(flat[off:off + n].view_as(g))
+            off += n
+
+    def _allgather_batch(self, *tensors):
+        """Shared replay sample: every rank contributes its local minibatch and
+        all ranks train on the concatenation (one all-gather of a packed buffer)."""
+        w = self.world()
+        if w <= 1:
+            return tensors
+        flat = torch.cat([t.reshape(t.shape[0], -1) for t in tensors], dim=1).contiguous()
+        out = torch.empty((w * flat.shape[0], flat.shape[1]), device=flat.device, dtype=flat.dtype)
+        dist.all_gather_into_tensor(out, flat, group=self.group)
+        res, off = [], 0
+        for t in tensors:
+            k = t[0].numel()
+            res.append(out[:, off:off + k].reshape((out.shape[0],) + tuple(t.shape[1:])))
+            off += k
+        return tuple(res)
+
+    # ------------------------------------------------------------ updates
+    def critic_step(self, s, a, target):
+        self.model_critic.train()  # Dropout active, as in critic.fit (:434)
+        q = self.model_critic(s, a).squeeze(-1)
+        loss = F.mse_loss(q, target)
+        self.critic_optimiser.zero_grad(set_to_none=False)
+        loss.backward()
+        self._allreduce_grads(self.model_critic)
+        self.critic_optimiser.step()
+        return loss.detach()
+
+    def model_actor_fit_step(self, s):
+        """model_actor_fit_step (:386-417): actor grads with output_gradients =
+        -dQ/da, i.e. descent on -sum_batch Q(s, mu(s)); critic in inference mode."""
+        self.model_critic.eval()
+        for p in self.model_critic.parameters():
+            p.requires_grad_(False)
+        q = self.model_critic(s, self.model_actor(s))
+        loss = -q.sum()
+        self.optimiser.zero_grad(set_to_none=False)
+        loss.backward()
+        for p in self.model_critic.parameters():
+            p.requires_grad_(True)
+        self._allreduce_grads(self.model_actor)
+        self.optimiser.step()
+        return loss.detach()
+
+    def models_fit(self, states, actions, rewards):
+        """models_fit (:419-443): shuffle, critic one pass at batch 16, then the
+        actor per batch of 16 on the same shuffled states."""
+        assert states.shape[0] == actions.shape[0] == rewards.shape[0]
+        idx = torch.randperm(states.shape[0], device=states.device, generator=self.gen)
+        states, actions, rewards = states[idx], actions[idx], rewards[idx]
+        b = self.model_param_batch_size
+        for k in range(0, states.shape[0], b):
+            self.critic_step(states[k:k + b], actions[k:k + b], rewards[k:k + b])
+        for k in range(0, states.shape[0], b):
+            self.model_actor_fit_step(states[k:k + b])
+
+    def replay_update(self, batch):
+        """Build-side extension: one critic + one actor step on a replay
+        minibatch (shared across ranks by all-gather), optional bootstrapped
+        target with target nets and soft update tau."""
+        s, a, r, s2, d = self.replay.sample(batch, generator=self.gen)
+        s, a, r, s2, d = self._allgather_batch(s, a, r, s2, d)
+        target = r
+        if self.gamma > 0.0:
+            with torch.no_grad():
+                actor_t = self.target_actor if self.tau is not None else self.model_actor
+                critic_t = self.target_critic if self.tau is not None else self.model_critic
+                critic_t.eval()
+                target = r + self.gamma * (1.0 - d) * critic_t(s2, actor_t(s2)).squeeze(-1)
+        lc = self.critic_step(s, a, target)
+        la = self.model_actor_fit_step(s)
+        if self.tau is not None:
+            self.soft_update()
+        return lc, la
+
+    @torch.no_grad()
+    def soft_update(self):
+        for tgt, src in ((self.target_actor, self.model_actor), (self.target_critic, self.model_critic)):
+            for pt, ps in zip(tgt.parameters(), src.parameters()):
+                pt.mul_(1.0 - self.tau).add_(ps, alpha=self.tau)
+
+
+class SkillshotLearner:
+    """Batched self-play DDPG learner (SkillshotLearner.py:13-682 API shape).
+
+    n_envs games on `device` (global ids env_offset.. when sharded over
+    ranks); both players of every game are driven by the same actor (self-play,
+    :304-308).
+    """
+    player_ids = (1, 2)
+
+    def __init__(self, n_envs=1, device="cuda", seed=0, env_offset=0, exploration="param_noise",
+                 tick_limit=2000, use_random_start=True, replay_capacity=1 << 20, batch_size=16,
+                 gamma=0.0, tau=None, actor_kernel=True, process_group=None):
+        from .vec_env import VecSkillshotGame
+        self.device = torch.device(device)
+        self.game_environment = VecSkillshotGame(n_envs, device=self.device, seed=seed, env_offset=env_offset,
+                                                 tick_limit=tick_limit, random_positions=use_random_start)
+        self.n_envs = n_envs
+        self.max_dist_normaliser = (2 * (250 ** 2)) ** 0.5    # :43
+        self.use_random_start = use_random_start               # :44
+        self.dim_state_space, self.dim_action_space, self.dim_reward_space = STATE_DIM, ACTION_DIM, 1
+        self.model_param_game_tick_limit = tick_limit          # :62
+        self.action_noise_sd = 0.15                            # :63
+        self.param_noise_sd = 0.5                              # :64
+        self.exploration = exploration
+        self.ddpg = DDPG(self.device, seed=seed, batch_size=batch_size, gamma=gamma, tau=tau,
+                         replay_capacity=replay_capacity, process_group=process_group, rank_seed_offset=env_offset)
+        self.gen = self.ddpg.gen
+        self.actor_kernel = None
+        if actor_kernel and self.device.type == "cuda":
+            from .actor_kernel import ActorKernel
+            self.actor_kernel = ActorKernel(self.model_actor, seed=seed * 1000003 + env_offset)
+        self.progress = dict(epoch_ticks=[], epoch_winner=[])
+
+    # reference attribute names
+    model_actor = property(lambda self: self.ddpg.model_actor)
+    model_critic = property(lambda self: self.ddpg.model_critic)
+    optimiser = property(lambda self: self.ddpg.optimiser)
+    replay = property(lambda self: self.ddpg.replay)
+    model_param_batch_size = property(lambda self: self.ddpg.model_param_batch_size)
+
+    def models_fit(self, states, actions, rewards):
+        self.ddpg.models_fit(states, actions, rewards)
+        if self.actor_kernel is not None:
+            self.actor_kernel.refresh()
+
+    def replay_update(self, batch):
+        return self.ddpg.replay_update(batch)
+
+    # ------------------------------------------------------------ acting
+    def prepare_states(self):
+        """prepare_states (:512-543) of the current state: obs [2, N, 12]."""
+        obs, _ = self.game_environment.observe()
+        return obs
+
+    @torch.no_grad()
+    def model_act(self, obs, mode=None):
+        """Actions [2, N, 2] for obs [2, N, 12] (model_act* :215-281)."""
+        mode = mode or self.exploration
+        x = obs.reshape(-1, STATE_DIM)
+        if mode == "param_noise":
+            if self.actor_kernel is not None:
+                a = self.actor_kernel(x, noise_sd=self.param_noise_sd, generator=self.gen)
+            else:
+                a = self.model_actor.forward_param_noise(x, self.param_noise_sd, generator=self.gen)
+        else:
+            a = self.actor_kernel(x) if self.actor_kernel is not None else self.model_actor(x)
+            if mode == "action_noise":
+                a = a + self.action_noise_sd * torch.randn(a.shape, device=a.device, generator=self.gen)
+        return a.reshape(2, -1, ACTION_DIM).contiguous()
+
+    def do_actions(self, actions, reset_obs=True):
+        """do_actions for both players + game_tick + obs/reward (:206-213, :312-324)."""
+        return self.game_environment.step(actions, obs=True, reward="looking", auto_reset=True,
+                                          reset_obs=reset_obs)
+
+    # ------------------------------------------------------------ training loops
+    def model_train(self, epochs, save_progress=False, save_boards=False):
+        """model_train (:283-384) with the reference update rule: each epoch
+        resets every game (random start), plays until every game has ended
+        (hit or tick limit), then fits on all of the epoch's transitions of both
+        players.  save_* flags are accepted for signature parity (on-disk
+        formats are out of scope)."""
+        g = self.game_environment
+        for _ in range(epochs):
+            g.reset(random_positions=self.use_random_start)
+            obs = self.prepare_states()
+            alive = torch.ones(self.n_envs, dtype=torch.bool, device=self.device)
+            S, A, R = [], [], []
+            ticks = torch.zeros(self.n_envs, dtype=torch.int32, device=self.device)
+            winner = torch.zeros(self.n_envs, dtype=torch.uint8, device=self.device)
+            while bool(alive.any()):
+                act = self.model_act(obs)
+                out = g.step(act, obs=True, reward="looking", auto_reset=False)
+                keep = alive.repeat(2)
+                S.append(obs.reshape(-1, STATE_DIM)[keep])
+                A.append(act.reshape(-1, ACTION_DIM)[keep])
+                R.append(out["reward"].reshape(-1)[keep])
+                done = out["done"].bool()
+                newly = alive & done
+                ticks = torch.where(newly, g.ticks, ticks)
+                winner = torch.where(newly, out["winner"], winner)
+                alive = alive & ~done
+                obs = out["obs"]
+            self.models_fit(torch.cat(S), torch.cat(A), torch.cat(R))
+            self.progress["epoch_ticks"].append(ticks.cpu())
+            self.progress["epoch_winner"].append(winner.cpu())
+        return self.progress
+
+    def train_ticks(self, n_ticks, batch=256, updates_per_tick=1, warmup=None):
+        """Build-side replay training: each tick acts
+        with the exploration policy for every game, steps (auto-reset), pushes
+        2N transitions into the HBM ring and runs `updates_per_tick` critic +
+        actor updates on `batch`-sized samples."""
+        g = self.game_environment
+        obs = self.prepare_states()
+        warmup = batch if warmup is None else warmup
+        stats = []
+        for _ in range(n_ticks):
+            act = self.model_act(obs)
+            out = self.do_actions(act, reset_obs=True)
+            d = out["done"].float().repeat(2)
+            self.replay.add(obs.reshape(-1, STATE_DIM), act.reshape(-1, ACTION_DIM), out["reward"].reshape(-1),
+                            out["obs"].reshape(-1, STATE_DIM), d)
+            obs = out["obs_reset"]
+            if self.replay.size >= warmup:
+                for _ in range(updates_per_tick):
+                    stats.append(self.replay_update(batch))
+            if self.actor_kernel is not None:
+                self.actor_kernel.refresh()
+        return stats
+
+    # ------------------------------------------------------------ persistence
+    def state_dict(self):
+        return dict(actor=self.model_actor.state_dict(), critic=self.model_critic.state_dict(),
+                    actor_opt=self.ddpg.optimiser.state_dict(), critic_opt=self.ddpg.critic_optimiser.state_dict(),
+                    env=self.game_environment.state_dict())
+
+    def load_state_dict(self, d):
+        self.model_actor.load_state_dict(d["actor"])
+        self.model_critic.load_state_dict(d["critic"])
+        self.ddpg.optimiser.load_state_dict(d["actor_opt"])
+        self.ddpg.critic_optimiser.load_state_dict(d["critic_opt"])
+        self.game_environment.load_state_dict(d["env"])
+        if self.actor_kernel is not None:
+            self.actor_kernel.refresh()
