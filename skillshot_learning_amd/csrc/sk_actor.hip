@@ -126,22 +126,25 @@ __device__ __forceinline__ uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
   return c;
 }
 
-// 16 standard normals for (row, stream): Box-Muller on 4 Philox draws.
-// v_sin/v_cos take revolutions, v_log is log2.
-__device__ __forceinline__ void normals16(uint64_t seed, uint64_t call, uint32_t row, uint32_t stream,
+// 16 standard normals for (row, stream, lane half h): Box-Muller on 4 Philox
+// draws.  The two lane halves hold different hidden units of the same row,
+// so h is part of the counter (independent noise per unit).
+__device__ __forceinline__ void normals16(uint64_t seed, uint64_t call, uint32_t row, uint32_t stream, int h,
                                           float z[16]) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    uint4 u = philox(make_uint4(row, stream * 4 + q, (uint32_t)call, (uint32_t)(call >> 32)), (uint32_t)seed,
-                     (uint32_t)(seed >> 32));
+    uint4 u = philox(make_uint4(row, (stream * 2 + (uint32_t)h) * 4 + q, (uint32_t)call, (uint32_t)(call >> 32)),
+                     (uint32_t)seed, (uint32_t)(seed >> 32));
     uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       float u1 = ((float)(w[2 * p] >> 8) + 0.5f) * 0x1p-24f;  // (0, 1)
       float u2 = (float)(w[2 * p + 1] >> 8) * 0x1p-24f;       // [0, 1)
-      float rad = __builtin_sqrtf(-2.0f * 0.69314718056f * __builtin_amdgcn_logf(u1));
-      z[4 * q + 2 * p] = rad * __builtin_amdgcn_cosf(u2);
-      z[4 * q + 2 * p + 1] = rad * __builtin_amdgcn_sinf(u2);
+      float rad = __builtin_sqrtf(-2.0f * __logf(u1));
+      float sn, cs;
+      __sincosf(6.283185307179586f * u2, &sn, &cs);
+      z[4 * q + 2 * p] = rad * cs;
+      z[4 * q + 2 * p + 1] = rad * sn;
     }
   }
 }
@@ -211,7 +214,7 @@ __global__ void __launch_bounds__(kThreads) k_actor_fwd(const float* __restrict_
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gW1[c * 64 + lane], xb, acc, 0, 0, 0);
       if (NOISE) var = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gW1s[c * 64 + lane], xs, var, 0, 0, 0);
       float z[16];
-      if (NOISE) normals16(seed, call, (uint32_t)row, (uint32_t)c, z);
+      if (NOISE) normals16(seed, call, (uint32_t)row, (uint32_t)c, h, z);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int hid = 32 * c + (i & 3) + 8 * (i >> 2) + 4 * h;
@@ -245,7 +248,7 @@ __global__ void __launch_bounds__(kThreads) k_actor_fwd(const float* __restrict_
         if (NOISE && (kk & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // cap hoisted LDS fragments
       }
       float z[16];
-      if (NOISE) normals16(seed, call, (uint32_t)row, (uint32_t)(8 + t), z);
+      if (NOISE) normals16(seed, call, (uint32_t)row, (uint32_t)(8 + t), h, z);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int hid = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
@@ -273,7 +276,7 @@ __global__ void __launch_bounds__(kThreads) k_actor_fwd(const float* __restrict_
     }
     if (h == 0 && valid) {
       float z[16];
-      if (NOISE) normals16(seed, call, (uint32_t)row, 12u, z);
+      if (NOISE) normals16(seed, call, (uint32_t)row, 12u, h, z);
       float o[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {

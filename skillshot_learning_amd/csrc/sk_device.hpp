@@ -28,6 +28,7 @@ struct Cfg {  // device copy of sk_config (kernel argument)
   double look;
   int f1x, f1y, f2x, f2y, rlo, rhi;
   double max_dist;  // (2*250**2)**0.5, SkillshotLearner.py:43
+  double inv_max_dist, inv_W, inv_H, inv_cdmax;  // obs scalings as products (rounded to f32 anyway)
 };
 
 struct View {  // device pointers, layout of include/skillshot.h
@@ -392,6 +393,56 @@ __device__ __forceinline__ void obs12_s(const Cfg& c, int px, int py, double rot
   out[9] = (float)(((py_mod2(qrot) * kPi) / 2.0) * kPi);
   out[10] = (float)(dist_line_point(gq, qx, qy, ox, oy) / D);
   out[11] = future_collision_s(c, qx, qy, qvalid, ox, oy, gq) ? 1.0f : 0.0f;
+}
+
+// Python's float r % 2 (floored, +0.0 for exact multiples): r - 2*floor(r/2)
+// is exact for every finite r (the product by 0.5 and by 2 are exact, and the
+// subtraction is exact or rounds the same single result fmod(r,2) + 2 does).
+__device__ __forceinline__ double py_mod2_fast(double r) { return r - 2.0 * floor(r * 0.5); }
+
+__device__ __attribute__((noinline)) double tan_lib(double y) { return tan(y); }
+
+// tan(-rot + pi/2) (Player.py:94) from the branch-free sincos of the ROUNDED
+// argument, as the reference rounds it before calling tan.
+__device__ __forceinline__ double grad_fast(double rot) {
+  const double y = -rot + kPi2;
+  bool ok;
+  sktrig::SinCos t = sktrig::sincos_bf(y, &ok);
+  double g = t.s / t.c;
+  if (!ok) g = tan_lib(y);
+  return g;
+}
+
+// prepare_states (SkillshotLearner.py:512-543) for one player given its two
+// gradients (fused step kernels: four grad_fast per game issued together).
+__device__ __forceinline__ void obs12_g(const Cfg& c, int px, int py, double rot, int qx, int qy, double qrot,
+                                        int qcd, int qvalid, int ox, int oy, double gp, double gq, float out[12],
+                                        double* path_dist) {
+  double pd = dist_line_point(gp, px, py, ox, oy);
+  *path_dist = pd;
+  out[0] = (float)(pd * c.inv_max_dist);
+  out[1] = (float)(dist_point_point(px, py, ox, oy) * c.inv_max_dist);
+  out[2] = (float)((double)px * c.inv_W);
+  out[3] = (float)((double)py * c.inv_H);
+  out[4] = (float)(((py_mod2_fast(rot) * kPi) / 2.0) * kPi);  // `% 2 * np.pi) / 2 * np.pi`
+  out[5] = (float)((double)qcd * c.inv_cdmax);
+  out[6] = (float)(dist_point_point(qx, qy, ox, oy) * c.inv_max_dist);
+  out[7] = (float)((double)qx * c.inv_W);
+  out[8] = (float)((double)qy * c.inv_H);
+  out[9] = (float)(((py_mod2_fast(qrot) * kPi) / 2.0) * kPi);
+  out[10] = (float)(dist_line_point(gq, qx, qy, ox, oy) * c.inv_max_dist);
+  out[11] = future_collision_s(c, qx, qy, qvalid, ox, oy, gq) ? 1.0f : 0.0f;
+}
+
+// both players' obs of one env (the fused step's obs/reward epilogue)
+__device__ __forceinline__ void obs_env(const Cfg& c, const Env& e, float o0[12], float o1[12], double* pd0,
+                                        double* pd1) {
+  const double gp0 = grad_fast(e.rot[0]), gq0 = grad_fast(e.qrot[0]);
+  const double gp1 = grad_fast(e.rot[1]), gq1 = grad_fast(e.qrot[1]);
+  obs12_g(c, e.px[0], e.py[0], e.rot[0], e.qx[0], e.qy[0], e.qrot[0], e.qcd[0], e.qvalid[0], e.px[1], e.py[1],
+          gp0, gq0, o0, pd0);
+  obs12_g(c, e.px[1], e.py[1], e.rot[1], e.qx[1], e.qy[1], e.qrot[1], e.qcd[1], e.qvalid[1], e.px[0], e.py[0],
+          gp1, gq1, o1, pd1);
 }
 
 __device__ __forceinline__ void obs12(const Cfg& c, const Env& e, int p, float out[12], double* path_dist) {

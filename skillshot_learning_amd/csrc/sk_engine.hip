@@ -157,13 +157,16 @@ __global__ void __launch_bounds__(kBlock) k_step(StepArgs a, Cfg c) {
     float2 a1 = a.actions[a.n + i];
     tick_env(c, e, (double)a0.x, (double)a0.y, (double)a1.x, (double)a1.y);
     if (a.obs || a.reward) {
-#pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        float o[12];
-        double pd;
-        obs12(c, e, p, o, &pd);
-        if (a.obs) store_obs(a.obs, a.n, p, i, o);
-        if (a.reward) a.reward[(int64_t)p * a.n + i] = reward_of(c, e, p, a.reward_kind, pd);
+      float o0[12], o1[12];
+      double pd0, pd1;
+      obs_env(c, e, o0, o1, &pd0, &pd1);
+      if (a.obs) {
+        store_obs(a.obs, a.n, 0, i, o0);
+        store_obs(a.obs, a.n, 1, i, o1);
+      }
+      if (a.reward) {
+        a.reward[i] = reward_of(c, e, 0, a.reward_kind, pd0);
+        a.reward[a.n + i] = reward_of(c, e, 1, a.reward_kind, pd1);
       }
     }
     d = (!e.live) || (e.ticks >= a.tick_limit);  // SkillshotLearner.py:302
@@ -177,13 +180,11 @@ __global__ void __launch_bounds__(kBlock) k_step(StepArgs a, Cfg c) {
     else reset_fixed(c, e);
   }
   if (a.obs_reset) {
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      float o[12];
-      double pd;
-      obs12(c, e, p, o, &pd);
-      store_obs(a.obs_reset, a.n, p, i, o);
-    }
+    float o0[12], o1[12];
+    double pd0, pd1;
+    obs_env(c, e, o0, o1, &pd0, &pd1);
+    store_obs(a.obs_reset, a.n, 0, i, o0);
+    store_obs(a.obs_reset, a.n, 1, i, o1);
   }
   store_env(a.v, i, e);
 }
@@ -248,7 +249,8 @@ __global__ void __launch_bounds__(kBlock) k_step_split(StepArgs a, Cfg c) {
   if (in && (a.obs || a.reward)) {
     float o[12];
     double pd;
-    obs12_s(c, px, py, rot, qx, qy, qrot, qcd, qvalid, opx, opy, o, &pd);
+    const double gp = grad_fast(rot), gq = grad_fast(qrot);
+    obs12_g(c, px, py, rot, qx, qy, qrot, qcd, qvalid, opx, opy, gp, gq, o, &pd);
     if (a.obs) store_obs(a.obs, a.n, p, i, o);
     if (a.reward) {
       float r;
@@ -284,7 +286,8 @@ __global__ void __launch_bounds__(kBlock) k_step_split(StepArgs a, Cfg c) {
     const int rpx = __shfl_xor(px, 1, 64), rpy = __shfl_xor(py, 1, 64);
     float o[12];
     double pd;
-    obs12_s(c, px, py, rot, qx, qy, qrot, qcd, qvalid, rpx, rpy, o, &pd);
+    const double gp = grad_fast(rot), gq = grad_fast(qrot);
+    obs12_g(c, px, py, rot, qx, qy, qrot, qcd, qvalid, rpx, rpy, gp, gq, o, &pd);
     store_obs(a.obs_reset, a.n, p, i, o);
   }
   reinterpret_cast<int2*>(a.v.pos)[h] = make_int2(px, py);
@@ -469,13 +472,16 @@ __global__ void __launch_bounds__(kBlock) k_observe(View v, int64_t n, float* ob
   if (i >= n) return;
   Env e;
   load_env(v, i, e);
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    float o[12];
-    double pd;
-    obs12(c, e, p, o, &pd);
-    if (obs) store_obs(obs, n, p, i, o);
-    if (reward) reward[(int64_t)p * n + i] = reward_of(c, e, p, kind, pd);
+  float o0[12], o1[12];
+  double pd0, pd1;
+  obs_env(c, e, o0, o1, &pd0, &pd1);
+  if (obs) {
+    store_obs(obs, n, 0, i, o0);
+    store_obs(obs, n, 1, i, o1);
+  }
+  if (reward) {
+    reward[i] = reward_of(c, e, 0, kind, pd0);
+    reward[n + i] = reward_of(c, e, 1, kind, pd1);
   }
 }
 
@@ -519,6 +525,10 @@ static Cfg to_dcfg(const sk_config& s) {
   c.rlo = s.rand_lo; c.rhi = s.rand_hi;
   // (2 * (250 ** 2)) ** 0.5 : CPython float_pow -> libm pow(125000.0, 0.5)
   c.max_dist = std::pow(2.0 * (double)s.board_w * (double)s.board_w, 0.5);
+  c.inv_max_dist = 1.0 / c.max_dist;
+  c.inv_W = 1.0 / (double)s.board_w;
+  c.inv_H = 1.0 / (double)s.board_h;
+  c.inv_cdmax = 1.0 / (double)s.cooldown_max;
   return c;
 }
 

@@ -7,9 +7,28 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-# bf16 operands (8-bit mantissa) through three layers, fp32 accumulation:
-# tolerance on tanh outputs for the deterministic path
-ACTOR_ATOL = 2.5e-2
+# The kernel's op: bf16 operands (inputs, weights, hidden activations), fp32
+# accumulation and epilogues.  Against a torch reference of exactly that op
+# (bf16-rounded operands, fp64 accumulation) only accumulation order differs,
+# but that can move a hidden activation across a bf16 rounding boundary (one
+# bf16 ulp, 2^-8 relative), so the bar is a mean and a max: EMU_*.  Against the
+# pure fp32 actor the operand rounding itself shows: FP32_* at 4x the
+# reference init scale (pre-activations ~O(10)).
+EMU_MEAN, EMU_MAX = 5e-4, 3e-2
+FP32_MEAN, FP32_MAX = 5e-3, 8e-2
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).to(torch.float64)
+
+
+def _emulated(a, x):
+    """The kernel's arithmetic in torch: bf16 operands, fp64 accumulation."""
+    h = x.double()
+    for k, l in enumerate((a.l1, a.l2, a.l3)):
+        h = _bf(h) @ _bf(l.weight.detach()).t() + l.bias.detach().double()
+        h = torch.tanh(h) if k == 2 else torch.relu(h).float().double()
+    return h.float()
 
 
 @pytest.fixture(scope="module")
@@ -39,9 +58,10 @@ def test_actor_kernel_matches_torch_fp32(mods, rows):
     x = torch.rand(rows, 12, device="cuda") * torch.tensor([1, 1, 1, 1, 9.8, 1, 1, 1, 1, 9.8, 1, 1.0],
                                                           device="cuda")
     got = k(x)
-    want = a(x)
-    err = (got - want).abs().max().item()
-    assert err < ACTOR_ATOL, err
+    emu = (got - _emulated(a, x)).abs()
+    assert emu.mean().item() < EMU_MEAN and emu.max().item() < EMU_MAX, (emu.mean().item(), emu.max().item())
+    err = (got - a(x)).abs()
+    assert err.mean().item() < FP32_MEAN and err.max().item() < FP32_MAX, (err.mean().item(), err.max().item())
     assert got.abs().max().item() > 0.2  # non-trivial outputs
 
 
@@ -53,7 +73,8 @@ def test_actor_kernel_refresh_tracks_weights(mods):
     with torch.no_grad():
         a.l3.bias.add_(0.5)
     k.refresh()
-    assert (k(x) - a(x)).abs().max().item() < ACTOR_ATOL
+    emu = (k(x) - _emulated(a, x)).abs()
+    assert emu.mean().item() < EMU_MEAN and emu.max().item() < EMU_MAX
 
 
 def test_param_noise_kernel_distribution(mods):
@@ -70,8 +91,10 @@ def test_param_noise_kernel_distribution(mods):
     for j in range(2):
         m1, m2 = got[:, j].mean().item(), want[:, j].mean().item()
         s1, s2 = got[:, j].std().item(), want[:, j].std().item()
-        assert abs(m1 - m2) < 0.02 + 5 * max(s1, s2) / math.sqrt(n), (j, m1, m2)
-        assert abs(s1 - s2) / max(s1, s2) < 0.05, (j, s1, s2)
+        # MC error ~ s/sqrt(n) = 0.002; bf16 operands of the mean and variance
+        # chains add a small deterministic bias
+        assert abs(m1 - m2) < 0.01 + 5 * max(s1, s2) / math.sqrt(n), (j, m1, m2)
+        assert abs(s1 - s2) / max(s1, s2) < 0.02, (j, s1, s2)
     # fresh noise per call and per row
     again = k(x, noise_sd=0.5)
     assert (again - got).abs().mean().item() > 1e-3
