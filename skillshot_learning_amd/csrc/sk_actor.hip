@@ -15,9 +15,10 @@
 // v_mfma_f32_32x32x16_bf16 tile, so each layer's accumulator converts in
 // registers to the next layer's B operand; the weights are pre-packed
 // (k_actor_pack) into A fragments in the matching permuted k order.
-// Per 32-row tile: layer 1 8 MFMAs, layer 2 64, layer 3 8 (x2 with noise).
+// Per 32-row tile: layer 1 8 MFMAs, layer 2 64 (x2 with noise); layer 3 (2 x 128) in
+// fp32 on the VALU from layer 2's accumulators.
 // W2 (and W2^2) fragments are staged once per workgroup in LDS (64/128 KiB);
-// W1/W3 fragments (8 KiB each) are read through L1.  bf16 operands, fp32
+// W1 fragments (8 KiB, + squares) are read through L1.  bf16 operands, fp32
 // accumulate, fp32 bias/noise/activation epilogues.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -30,17 +31,20 @@ typedef __attribute__((ext_vector_type(8))) short bf16x8;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 
 constexpr int kIn = 12, kH1 = 256, kH2 = 128, kOut = 2;
-constexpr int kThreads = 512;  // 8 waves: two per SIMD
+// deterministic: 8 waves (two per SIMD, 141 VGPRs); noise: 4 waves (one per
+// SIMD) so the mean and variance chains' operands (h1, h1^2: 128 VGPRs) plus
+// both accumulators fit the 512-register budget without spilling
+template <bool NOISE>
+constexpr int threads_for() { return NOISE ? 256 : 512; }
 
 // packed buffer layout (bytes)
 constexpr int kW1Frag = 8 * 64 * 16;        // 8 hidden chunks x 64 lanes x 8 bf16
 constexpr int kW2Frag = 4 * 16 * 64 * 16;   // 4 out chunks x 16 k-steps x 64 lanes x 8 bf16
-constexpr int kW3Frag = 8 * 64 * 16;        // 8 k-steps x 64 lanes x 8 bf16
 constexpr size_t kOffW1 = 0, kOffW1s = kOffW1 + kW1Frag;
 constexpr size_t kOffW2 = kOffW1s + kW1Frag, kOffW2s = kOffW2 + kW2Frag;
-constexpr size_t kOffW3 = kOffW2s + kW2Frag, kOffW3s = kOffW3 + kW3Frag;
-constexpr size_t kOffB = kOffW3s + kW3Frag;  // fp32: b1[256] b2[128] b3[2] (pad 512)
-constexpr size_t kPackedBytes = kOffB + 512 * 4;
+constexpr size_t kOffB = kOffW2s + kW2Frag;  // fp32: b1[256] b2[128] b3[2] (pad 512)
+constexpr size_t kOffW3f = kOffB + 512 * 4;  // fp32 W3[2][128] then W3^2[2][128] (layer 3 on the VALU)
+constexpr size_t kPackedBytes = kOffW3f + 512 * 4;
 
 __device__ __forceinline__ short f2bf(float f) {  // round-to-nearest-even (v_cvt_pk_bf16_f32)
   return __builtin_bit_cast(short, (__bf16)f);
@@ -64,7 +68,7 @@ __device__ __forceinline__ bf16x8 sq_bf16(bf16x8 a) {
 // W2: [128][256]; chunk t, k-step kk, lane (r, h), element j =
 //     W2[32t + r][32(kk>>1) + 16(kk&1) + 8(j>>2) + 4h + (j&3)]  (the row order
 //     of the previous accumulator's registers 8s..8s+7, s = kk&1).
-// W3: [2][128] padded to 32 rows; k-step kk as W2.
+// W3: [2][128] copied as fp32 (with its squares) for the VALU layer 3.
 __global__ void k_actor_pack(const float* W1, const float* b1, const float* W2, const float* b2, const float* W3,
                              const float* b3, char* out) {
   int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -72,10 +76,8 @@ __global__ void k_actor_pack(const float* W1, const float* b1, const float* W2, 
   short* w1s = (short*)(out + kOffW1s);
   short* w2 = (short*)(out + kOffW2);
   short* w2s = (short*)(out + kOffW2s);
-  short* w3 = (short*)(out + kOffW3);
-  short* w3s = (short*)(out + kOffW3s);
   float* bias = (float*)(out + kOffB);
-  // one thread per (fragment, lane): layer 1 (8*64), layer 2 (64*64), layer 3 (8*64)
+  // one thread per (fragment, lane): layer 1 (8*64), layer 2 (64*64); then biases, W3
   if (t < 8 * 64) {
     int c = t >> 6, lane = t & 63, r = lane & 31, h = lane >> 5;
     for (int j = 0; j < 8; ++j) {
@@ -94,22 +96,19 @@ __global__ void k_actor_pack(const float* W1, const float* b1, const float* W2, 
       w2[u * 8 + j] = f2bf(v);
       w2s[u * 8 + j] = f2bf(v * v);
     }
-  } else if (t < 8 * 64 + 64 * 64 + 8 * 64) {
+  } else if (t < 8 * 64 + 64 * 64 + 512) {
     int u = t - 8 * 64 - 64 * 64;
-    int kk = u >> 6, lane = u & 63, r = lane & 31, h = lane >> 5;
-    for (int j = 0; j < 8; ++j) {
-      int k = 32 * (kk >> 1) + 16 * (kk & 1) + 8 * (j >> 2) + 4 * h + (j & 3);
-      float v = r < kOut ? W3[r * kH2 + k] : 0.f;
-      w3[u * 8 + j] = f2bf(v);
-      w3s[u * 8 + j] = f2bf(v * v);
-    }
-  } else if (t < 8 * 64 + 64 * 64 + 8 * 64 + 512) {
-    int u = t - 8 * 64 - 64 * 64 - 8 * 64;
     float v = 0.f;
     if (u < kH1) v = b1[u];
     else if (u < kH1 + kH2) v = b2[u - kH1];
     else if (u < kH1 + kH2 + kOut) v = b3[u - kH1 - kH2];
     bias[u] = v;
+  } else if (t < 8 * 64 + 64 * 64 + 512 + 256) {
+    int u = t - 8 * 64 - 64 * 64 - 512;  // o * 128 + k
+    float v = W3[u];
+    float* w3f = (float*)(out + kOffW3f);
+    w3f[u] = v;
+    w3f[256 + u] = v * v;
   }
 }
 
@@ -150,22 +149,26 @@ __device__ __forceinline__ void normals16(uint64_t seed, uint64_t call, uint32_t
 }
 
 // ---------------------------------------------------------------- forward
-template <bool NOISE>
-__global__ void __launch_bounds__(kThreads) k_actor_fwd(const float* __restrict__ X, float* __restrict__ out,
+// DBG (diagnostics build only): dbg[row][386] receives every unit's
+// post-activation value (256 layer-1, 128 layer-2, 2 layer-3 pre-tanh).
+template <bool NOISE, bool DBG = false>
+__global__ void __launch_bounds__(threads_for<NOISE>()) k_actor_fwd(const float* __restrict__ X, float* __restrict__ out,
                                                         int64_t M, const char* __restrict__ packed, float sd,
-                                                        uint64_t seed, uint64_t call) {
+                                                        uint64_t seed, uint64_t call, float* dbg = nullptr) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16x8* sW2 = (bf16x8*)smem;                               // [4][16][64]
   bf16x8* sW2s = (bf16x8*)(smem + kW2Frag);                  // NOISE only
-  float* sB = (float*)(smem + (NOISE ? 2 : 1) * kW2Frag);    // b1 b2 b3
+  float* sB = (float*)(smem + (NOISE ? 2 : 1) * kW2Frag);    // b1 b2 b3 (512), W3 (256), W3^2 (256)
+  float* sW3 = sB + 512;
 
+  constexpr int kThreads = threads_for<NOISE>();
   {  // stage W2 fragments (+ squares) and biases once per workgroup
     const uint4* g = (const uint4*)(packed + kOffW2);
     uint4* s = (uint4*)smem;
     const int n16 = (NOISE ? 2 : 1) * kW2Frag / 16;
     for (int k = threadIdx.x; k < n16; k += kThreads) s[k] = g[k];  // W2s follows W2 in the buffer
     const float* gb = (const float*)(packed + kOffB);
-    for (int k = threadIdx.x; k < 512; k += kThreads) sB[k] = gb[k];
+    for (int k = threadIdx.x; k < 1024; k += kThreads) sB[k] = gb[k];  // biases then W3, W3^2 (contiguous)
   }
   __syncthreads();
 
@@ -181,8 +184,6 @@ __global__ void __launch_bounds__(kThreads) k_actor_fwd(const float* __restrict_
     asm volatile("" : "+s"(pk));
     const bf16x8* gW1 = (const bf16x8*)(pk + kOffW1);
     const bf16x8* gW1s = (const bf16x8*)(pk + kOffW1s);
-    const bf16x8* gW3 = (const bf16x8*)(pk + kOffW3);
-    const bf16x8* gW3s = (const bf16x8*)(pk + kOffW3s);
     const int64_t row = tile * 32 + r;
     const bool valid = row < M;
     // ---- X^T fragment: B[k = 8h + j][col r] = X[row][8h + j]
@@ -223,6 +224,7 @@ __global__ void __launch_bounds__(kThreads) k_actor_fwd(const float* __restrict_
         if (NOISE) y += sd * __builtin_sqrtf(fmaxf(var[i] + b * b, 0.f)) * z[i];
         y = fmaxf(y, 0.f);
         acc[i] = y;
+        if (DBG && valid) dbg[row * 386 + hid] = y;
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -234,8 +236,11 @@ __global__ void __launch_bounds__(kThreads) k_actor_fwd(const float* __restrict_
       __builtin_amdgcn_sched_barrier(0);  // one chunk's accumulators live at a time
     }
 
-    // ---- layer 2: H2^T = relu(W2 H1^T + b2 [+ noise])
-    bf16x8 h2[8];
+    // ---- layer 2: H2^T = relu(W2 H1^T + b2 [+ noise]), and layer 3 on the VALU:
+    // each lane accumulates fp32 partial dot products of W3 (and W3^2 for the
+    // noise variance) over the 64 layer-2 units it holds; the two lane halves
+    // are combined with one cross-half shuffle.
+    float m0 = 0.f, m1 = 0.f, q0 = 0.f, q1 = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       f32x16 acc = {0}, var = {0};
@@ -255,34 +260,36 @@ __global__ void __launch_bounds__(kThreads) k_actor_fwd(const float* __restrict_
         const float b = sB[kH1 + hid];
         float y = acc[i] + b;
         if (NOISE) y += sd * __builtin_sqrtf(fmaxf(var[i] + b * b, 0.f)) * z[i];
-        acc[i] = fmaxf(y, 0.f);
-      }
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        bf16x8 f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = f2bf(acc[8 * s + j]);
-        h2[2 * t + s] = f;
+        y = fmaxf(y, 0.f);
+        if (DBG && valid) dbg[row * 386 + kH1 + hid] = y;
+        m0 += sW3[hid] * y;
+        m1 += sW3[kH2 + hid] * y;
+        if (NOISE) {
+          q0 += sW3[2 * kH2 + hid] * (y * y);
+          q1 += sW3[3 * kH2 + hid] * (y * y);
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-
-    // ---- layer 3: a = tanh(W3 H2^T + b3 [+ noise]); rows 0,1 = registers 0,1 of lanes 0..31
-    f32x16 acc = {0}, var = {0};
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) {
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gW3[kk * 64 + lane], h2[kk], acc, 0, 0, 0);
-      if (NOISE) var = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gW3s[kk * 64 + lane], sq_bf16(h2[kk]), var, 0, 0, 0);
+    m0 += __shfl_xor(m0, 32, 64);
+    m1 += __shfl_xor(m1, 32, 64);
+    if (NOISE) {
+      q0 += __shfl_xor(q0, 32, 64);
+      q1 += __shfl_xor(q1, 32, 64);
     }
+
+    // ---- layer 3 epilogue: a = tanh(W3 h2 + b3 [+ noise]) for this lane's row
     if (h == 0 && valid) {
       float z[16];
       if (NOISE) normals16(seed, call, (uint32_t)row, 12u, h, z);
+      const float mm[2] = {m0, m1}, qq[2] = {q0, q1};
       float o[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const float b = sB[kH1 + kH2 + i];
-        float y = acc[i] + b;
-        if (NOISE) y += sd * __builtin_sqrtf(fmaxf(var[i] + b * b, 0.f)) * z[i];
+        float y = mm[i] + b;
+        if (NOISE) y += sd * __builtin_sqrtf(fmaxf(qq[i] + b * b, 0.f)) * z[i];
+        if (DBG) dbg[row * 386 + kH1 + kH2 + i] = y;
         o[i] = tanhf(y);
       }
       *(float2*)(out + row * kOut) = make_float2(o[0], o[1]);
@@ -300,7 +307,7 @@ int sk_actor_pack(const float* W1, const float* b1, const float* W2, const float
                   const float* b3, void* packed, void* stream) {
   if (!W1 || !b1 || !W2 || !b2 || !W3 || !b3 || !packed) return SK_EINVAL;
   if (((uintptr_t)packed) & 15) return SK_EINVAL;
-  const int total = 8 * 64 + 64 * 64 + 8 * 64 + 512;
+  const int total = 8 * 64 + 64 * 64 + 512 + 256;
   k_actor_pack<<<(total + 255) / 256, 256, 0, (hipStream_t)stream>>>(W1, b1, W2, b2, W3, b3, (char*)packed);
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
 }
@@ -313,26 +320,42 @@ int sk_actor_forward(const void* packed, const float* obs, float* actions, int64
   int dev = 0, cus = 256;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const int64_t tiles = (rows + 31) / 32;
-  int64_t grid = (tiles + kThreads / 64 - 1) / (kThreads / 64);
-  if (grid > cus) grid = cus;  // one 512-thread workgroup per CU (LDS-limited), tiles grid-strided
   const bool noise = noise_sd != 0.f;
-  const size_t lds = (noise ? 2 : 1) * kW2Frag + 512 * 4;
+  const int threads = noise ? threads_for<true>() : threads_for<false>();
+  const int64_t tiles = (rows + 31) / 32;
+  int64_t grid = (tiles + threads / 64 - 1) / (threads / 64);
+  if (grid > cus) grid = cus;  // one workgroup per CU (LDS-limited), 32-row tiles grid-strided
+  const size_t lds = (noise ? 2 : 1) * kW2Frag + 1024 * 4;
   static bool attr_set = false;  // dynamic LDS above 64 KiB must be opted into once
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)k_actor_fwd<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              2 * kW2Frag + 512 * 4);
+                              2 * kW2Frag + 1024 * 4);
     (void)hipFuncSetAttribute((const void*)k_actor_fwd<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              kW2Frag + 512 * 4);
+                              kW2Frag + 1024 * 4);
     attr_set = true;
   }
   if (noise) {
-    k_actor_fwd<true><<<(unsigned)grid, kThreads, lds, (hipStream_t)stream>>>(obs, actions, rows, (const char*)packed,
-                                                                             noise_sd, seed, call);
+    k_actor_fwd<true><<<(unsigned)grid, threads, lds, (hipStream_t)stream>>>(obs, actions, rows, (const char*)packed,
+                                                                            noise_sd, seed, call);
   } else {
-    k_actor_fwd<false><<<(unsigned)grid, kThreads, lds, (hipStream_t)stream>>>(obs, actions, rows,
-                                                                              (const char*)packed, 0.f, seed, call);
+    k_actor_fwd<false><<<(unsigned)grid, threads, lds, (hipStream_t)stream>>>(obs, actions, rows,
+                                                                             (const char*)packed, 0.f, seed, call);
   }
+  return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
+}
+
+// diagnostics only (not in include/skillshot.h): the noisy forward with every
+// unit's activation dumped to dbg[rows][386]
+int skdiag_actor_forward_dbg(const void* packed, const float* obs, float* actions, float* dbg, int64_t rows,
+                             float noise_sd, uint64_t seed, uint64_t call, void* stream) {
+  const int threads = threads_for<true>();
+  const int64_t tiles = (rows + 31) / 32;
+  int64_t grid = (tiles + threads / 64 - 1) / (threads / 64);
+  if (grid > 256) grid = 256;
+  const size_t lds = 2 * kW2Frag + 1024 * 4;
+  (void)hipFuncSetAttribute((const void*)k_actor_fwd<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  k_actor_fwd<true, true><<<(unsigned)grid, threads, lds, (hipStream_t)stream>>>(
+      obs, actions, rows, (const char*)packed, noise_sd, seed, call, dbg);
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
 }
 

@@ -99,7 +99,10 @@ class Critic(nn.Module):
 
 
 def keras_adam(params):
-    return torch.optim.Adam(params, lr=1e-3, betas=(0.9, 0.999), eps=1e-7)
+    """Keras Adam defaults (lr 1e-3, eps 1e-7); one fused multi-tensor kernel on GPU."""
+    params = list(params)
+    fused = bool(params) and params[0].is_cuda
+    return torch.optim.Adam(params, lr=1e-3, betas=(0.9, 0.999), eps=1e-7, fused=fused)
 
 
 class ReplayRing:
@@ -120,12 +123,11 @@ class ReplayRing:
         if n > self.cap:
             s, a, r, s2, d = s[-self.cap:], a[-self.cap:], r[-self.cap:], s2[-self.cap:], d[-self.cap:]
             n = self.cap
-        idx = (torch.arange(n, device=s.device) + self.head) % self.cap
-        self.s[idx] = s
-        self.a[idx] = a
-        self.r[idx] = r
-        self.s2[idx] = s2
-        self.d[idx] = d
+        first = min(n, self.cap - self.head)  # contiguous copies, at most two per buffer
+        for dst, src in ((self.s, s), (self.a, a), (self.r, r), (self.s2, s2), (self.d, d)):
+            dst[self.head:self.head + first].copy_(src[:first])
+            if first < n:
+                dst[:n - first].copy_(src[first:])
         self.head = (self.head + n) % self.cap
         self.size = min(self.cap, self.size + n)
 
