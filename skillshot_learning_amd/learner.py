@@ -33,6 +33,67 @@ import torch.nn.functional as F
 
 STATE_DIM = 12   # SkillshotLearner.py:54
 ACTION_DIM = 2   # :55
+MAX_DIST = (2 * (250 ** 2)) ** 0.5  # max_dist_normaliser, :43
+
+# get_state() feature indices used by calculate_rewards (vec_env.FEATURE_KEYS)
+_F_AGE, _F_DIST, _F_FC = 14, 16, 17
+
+
+def calculate_rewards_full(dist, future_collision, age, winner, lengths=None, max_dist=MAX_DIST,
+                           on_target_multiplier_reduction=0.25, loss_reward_multiplier=2,
+                           base_reward_multiplier=0.75):
+    """calculate_rewards (SkillshotLearner.py:605-661) batched over games.
+
+    Inputs describe game_states[1:] of each game's episode, tick-major:
+      dist [T, N, 2] float64   projectile_dist_opponent of players 1, 2
+      future_collision [T, N, 2] bool   projectile_future_collision_opponent
+      age [T, N, 2] int        projectile_age
+      winner [T, N] int        game_winner (0, or the id the reference stores
+                               in winner_id, SkillshotGame.py check_collision)
+      lengths [N]              episode length per game (<= T; default T)
+    Returns (rewards [T, N, 2] float64, raised [N] bool).
+
+    Follows the reference statement by statement, quirks included:
+      * per-player multiplier 0.75, 0.5 while the own projectile is on target
+        (:632-635), 2.75 for the loser of a won tick (:637-639, overrides);
+      * reward = (dist[opp] - dist[own] * multi + min_dist * 2) / max_dist
+        with min_dist always 0: :643 reads game_state["projectile_cooldown"],
+        a key the top-level state never has (SkillshotGame.py:139);
+      * a won tick t sets rewards[t - age(winner)][winner] = 1 (:624-627),
+        with Python list indexing over the t rewards built so far: a negative
+        index wraps once, anything outside [-t, t) raises IndexError, which
+        aborts the reference call; such games are flagged in `raised` and
+        their rewards are NaN.
+    """
+    T, N = winner.shape
+    dev = dist.device
+    if lengths is None:
+        lengths = torch.full((N,), T, dtype=torch.long, device=dev)
+    lengths = lengths.to(dev).long()
+    dist = dist.to(torch.float64)
+    w = winner.long()
+    base = torch.tensor(float(base_reward_multiplier), dtype=torch.float64, device=dev)
+    multi = torch.where(future_collision.bool(), base - on_target_multiplier_reduction, base)
+    loser = torch.where(w != 0, 3 - w, torch.zeros_like(w))  # the id in (1, 2) that is not winner_id
+    pid = torch.arange(1, 3, device=dev).view(1, 1, 2)
+    multi = torch.where(loser.unsqueeze(-1) == pid, base + loss_reward_multiplier, multi)
+    r = (dist.flip(-1) - dist * multi) / max_dist
+    tick = torch.arange(T, device=dev).view(T, 1)
+    valid = tick < lengths.view(1, N)
+    won = (w != 0) & valid
+    raised = torch.zeros(N, dtype=torch.bool, device=dev)
+    if bool(won.any()):
+        t_idx, n_idx = torch.nonzero(won, as_tuple=True)
+        wi = w[t_idx, n_idx] - 1
+        f = t_idx - age.long()[t_idx, n_idx, wi]
+        f = torch.where(f < 0, f + t_idx, f)             # list[-k] == list[len - k]
+        bad = (f < 0) | (f >= t_idx)
+        raised[n_idx[bad]] = True
+        ok = ~bad
+        r[f[ok], n_idx[ok], wi[ok]] = 1.0
+    r = torch.where(valid.unsqueeze(-1), r, torch.full_like(r, float("nan")))
+    r[:, raised] = float("nan")
+    return r, raised
 
 
 def _keras_normal_(t, std=0.05):
@@ -286,7 +347,7 @@ class SkillshotLearner:
         self.game_environment = VecSkillshotGame(n_envs, device=self.device, seed=seed, env_offset=env_offset,
                                                  tick_limit=tick_limit, random_positions=use_random_start)
         self.n_envs = n_envs
-        self.max_dist_normaliser = (2 * (250 ** 2)) ** 0.5    # :43
+        self.max_dist_normaliser = MAX_DIST                    # :43
         self.use_random_start = use_random_start               # :44
         self.dim_state_space, self.dim_action_space, self.dim_reward_space = STATE_DIM, ACTION_DIM, 1
         self.model_param_game_tick_limit = tick_limit          # :62
@@ -345,34 +406,54 @@ class SkillshotLearner:
                                           reset_obs=reset_obs)
 
     # ------------------------------------------------------------ training loops
-    def model_train(self, epochs, save_progress=False, save_boards=False):
+    def model_train(self, epochs, save_progress=False, save_boards=False, reward="looking"):
         """model_train (:283-384) with the reference update rule: each epoch
         resets every game (random start), plays until every game has ended
         (hit or tick limit), then fits on all of the epoch's transitions of both
-        players.  save_* flags are accepted for signature parity (on-disk
+        players.  reward picks the reference's reward function for the epoch
+        (:324-326): "looking" (the one it uses), "simple", or "full"
+        (calculate_rewards, computed once the episode is complete; a game on
+        which the reference would raise IndexError contributes no
+        transitions).  save_* flags are accepted for signature parity (on-disk
         formats are out of scope)."""
         g = self.game_environment
+        full = reward == "full"
         for _ in range(epochs):
             g.reset(random_positions=self.use_random_start)
             obs = self.prepare_states()
             alive = torch.ones(self.n_envs, dtype=torch.bool, device=self.device)
-            S, A, R = [], [], []
+            S, A, R, K, FT, W = [], [], [], [], [], []
             ticks = torch.zeros(self.n_envs, dtype=torch.int32, device=self.device)
+            lengths = torch.zeros(self.n_envs, dtype=torch.long, device=self.device)
             winner = torch.zeros(self.n_envs, dtype=torch.uint8, device=self.device)
             while bool(alive.any()):
                 act = self.model_act(obs)
-                out = g.step(act, obs=True, reward="looking", auto_reset=False)
+                out = g.step(act, obs=True, reward="looking" if full else reward, auto_reset=False)
                 keep = alive.repeat(2)
-                S.append(obs.reshape(-1, STATE_DIM)[keep])
-                A.append(act.reshape(-1, ACTION_DIM)[keep])
-                R.append(out["reward"].reshape(-1)[keep])
+                S.append(obs.reshape(-1, STATE_DIM))
+                A.append(act.reshape(-1, ACTION_DIM))
+                K.append(keep)
+                if full:
+                    f = g.features()
+                    FT.append(f[..., [_F_DIST, _F_FC, _F_AGE]])
+                    W.append(out["winner"].long())
+                else:
+                    R.append(out["reward"].reshape(-1))
                 done = out["done"].bool()
                 newly = alive & done
                 ticks = torch.where(newly, g.ticks, ticks)
                 winner = torch.where(newly, out["winner"], winner)
+                lengths = lengths + alive.long()
                 alive = alive & ~done
                 obs = out["obs"]
-            self.models_fit(torch.cat(S), torch.cat(A), torch.cat(R))
+            if full:
+                ft = torch.stack(FT)                              # [T, N, 2, 3]
+                rf, raised = calculate_rewards_full(ft[..., 0], ft[..., 1] != 0, ft[..., 2].long(),
+                                                    torch.stack(W), lengths, self.max_dist_normaliser)
+                R = [rt.t().reshape(-1).float() for rt in rf]    # [2N] player-major per tick
+                K = [k & ~raised.repeat(2) for k in K]
+            K = torch.cat(K)
+            self.models_fit(torch.cat(S)[K], torch.cat(A)[K], torch.cat(R)[K])
             self.progress["epoch_ticks"].append(ticks.cpu())
             self.progress["epoch_winner"].append(winner.cpu())
         return self.progress

@@ -43,7 +43,8 @@ SkillshotGame = _sg.SkillshotGame
 def _load_learner_methods():
     src = open(os.path.join(REF, "SkillshotLearner.py")).read()
     tree = ast.parse(src)
-    wanted = {"prepare_states", "calculate_rewards_looking", "calculate_rewards_simple", "do_actions"}
+    wanted = {"prepare_states", "calculate_rewards_looking", "calculate_rewards_simple", "calculate_rewards",
+              "do_actions"}
     fns = []
     for node in tree.body:
         if isinstance(node, ast.ClassDef) and node.name == "SkillshotLearner":
@@ -78,6 +79,17 @@ class LearnerStub:
 
     def rewards_simple(self, states):
         return _M["calculate_rewards_simple"](self, states)
+
+    def rewards_full(self, states):
+        """calculate_rewards (:605-661) over an episode's post-tick states."""
+        try:
+            r = _M["calculate_rewards"](self, states)
+        except IndexError:
+            return None, np.array([[st[1]["projectile_dist_opponent"], st[2]["projectile_dist_opponent"]]
+                                   for st in states], dtype=np.float64)  # the reference raised
+        return (np.array([[x[1], x[2]] for x in r], dtype=np.float64),
+                np.array([[st[1]["projectile_dist_opponent"], st[2]["projectile_dist_opponent"]]
+                          for st in states], dtype=np.float64))
 
     def do_actions(self, pid, pred):
         return _M["do_actions"](self, pid, pred)
@@ -131,6 +143,7 @@ def run_env(game, actions, tick_limit, protocol="learner", shoot=None, run_after
     """
     learner = LearnerStub(game)
     snaps = [snapshot(game)]
+    states = []
     o, rl, rs = features(learner, game)
     obs, rew, rsim = [o], [rl], [rs]
     done_at = None
@@ -156,6 +169,7 @@ def run_env(game, actions, tick_limit, protocol="learner", shoot=None, run_after
                         pl.move_shoot_projectile()
             game.game_tick()
             t += 1
+            states.append(game.get_state())
             snaps.append(snapshot(game))
             o, rl, rs = features(learner, game)
             obs.append(o)
@@ -163,12 +177,26 @@ def run_env(game, actions, tick_limit, protocol="learner", shoot=None, run_after
             rsim.append(rs)
             if done_at is None and not (game.game_live and game.ticks < tick_limit):
                 done_at = t
-    return snaps, obs, rew, rsim, t
+    full = learner.rewards_full(states) if protocol == "learner" and states else (None, None)
+    return snaps, obs, rew, rsim, t, full
 
 
 def pack(name, inits, acts, results, tick_limit, protocol, shoot=None, note=""):
     E = len(results)
     Tm = max(r[4] for r in results)
+    if protocol == "learner":
+        # calculate_rewards (:605-661) over states[1:] of each episode; NaN rows
+        # pad, and an episode on which the reference raises is all-NaN
+        rf = np.full((E, max(Tm, 1), 2), np.nan)
+        rd = np.full((E, max(Tm, 1), 2), np.nan)
+        for e, r in enumerate(results):
+            if r[5][0] is not None:
+                rf[e, :r[5][0].shape[0]] = r[5][0]
+            if r[5][1] is not None:
+                rd[e, :r[5][1].shape[0]] = r[5][1]
+        out_full = (rf, rd)
+    else:
+        out_full = None
     out = dict(
         scenario=np.array(name), protocol=np.array(protocol), note=np.array(note),
         tick_limit=np.int32(tick_limit), numpy_version=np.array(np.__version__),
@@ -205,6 +233,11 @@ def pack(name, inits, acts, results, tick_limit, protocol, shoot=None, note=""):
             arr.append(np.stack(seq))
         return np.stack(arr)
 
+    if out_full is not None:
+        # the reference's projectile_dist_opponent per post-tick state: its
+        # value depends on the coordinates' Python types (int ** 0.5 is libm
+        # pow, np.int64 ** 0.5 is numpy's sqrt), so the reward is pinned on it
+        out["reward_full"], out["reward_full_dist"] = out_full
     out["obs"] = series(1)
     out["reward"] = series(2)
     out["reward_simple"] = series(3)

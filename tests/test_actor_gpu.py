@@ -127,3 +127,15 @@ def test_learner_reference_epochs(mods):
         L.exploration = mode or "deterministic"
         act = L.model_act(L.prepare_states())
         assert act.shape == (2, 4, 2) and torch.isfinite(act).all()
+
+
+def test_learner_reference_epochs_full_reward(mods):
+    """model_train with the alternative reward functions (:324-326)."""
+    learner, _ = mods
+    for reward in ("full", "simple"):
+        L = learner.SkillshotLearner(n_envs=8, seed=4, tick_limit=80, exploration="param_noise")
+        before = [p.detach().clone() for p in L.model_critic.parameters()]
+        prog = L.model_train(epochs=1, reward=reward)
+        assert len(prog["epoch_ticks"]) == 1
+        moved = sum(float((p.detach() - b).abs().sum()) for p, b in zip(L.model_critic.parameters(), before))
+        assert moved > 0

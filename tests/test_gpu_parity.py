@@ -288,3 +288,34 @@ def test_errors_are_loud(ssa):
         g.step(torch.zeros(2, 63, 2, device="cuda"))
     with pytest.raises(ssa.SkillshotError):
         g.move_direction(3, 0.5)
+
+
+@pytest.mark.parametrize("name", [n for n in gr.fixture_names() if "reward_full" in gr.load(n)])
+def test_full_reward_on_engine_features(ssa, name):
+    """F3: calculate_rewards (SkillshotLearner.py:605-661) on the GPU, its
+    inputs gathered from the HIP engine's get_state() features while the
+    fixture's actions are replayed, against the reference's own output.  The
+    engine's distances are correctly rounded sqrt, the reference's are libm
+    pow or numpy sqrt by coordinate type (see test_rewards_full_cpu), so the
+    bar is 1e-12 absolute; raised games must match exactly."""
+    from skillshot_learning_amd.learner import calculate_rewards_full
+    d = gr.load(name)
+    E, T = d["pos"].shape[0], int(d["n_steps"].max())
+    g = ssa.VecSkillshotGame(E, tick_limit=int(d["tick_limit"]))
+    g.load_state_dict(gr.state_at(d, 0))
+    feats, wins = [], []
+    for t in range(T):
+        a = torch.as_tensor(np.ascontiguousarray(np.transpose(d["actions"][:, t], (1, 0, 2)))).cuda()
+        out = g.step(a, obs=False, auto_reset=False)
+        feats.append(g.features().clone())
+        wins.append(out["winner"].long())
+    f = torch.stack(feats)
+    lengths = torch.as_tensor(d["n_steps"].astype(np.int64)).cuda()
+    r, raised = calculate_rewards_full(f[..., 16], f[..., 17] != 0, f[..., 14].long(), torch.stack(wins), lengths)
+    want = d["reward_full"]
+    want_raised = np.isnan(want[:, 0, 0])
+    assert np.array_equal(raised.cpu().numpy(), want_raised)
+    got = r.permute(1, 0, 2).cpu().numpy()
+    m = ~np.isnan(want)
+    assert np.array_equal(np.isnan(got), ~m)
+    assert np.abs(got[m] - want[m]).max() <= 1e-12
