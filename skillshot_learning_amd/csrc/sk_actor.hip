@@ -51,15 +51,22 @@ __device__ __forceinline__ short f2bf(float f) {  // round-to-nearest-even (v_cv
 }
 
 // elementwise square of a bf16 fragment (the variance chain's operand x^2 is
-// derived at use instead of stored: keeps the noise kernel inside 256 VGPRs)
+// derived at use instead of stored: keeps the noise kernel inside 256 VGPRs).
+// Written on the packed dwords: the per-element __bf16 form of this loop was
+// compiled (ROCm 7.2 clang, gfx950) into element 0's square broadcast to all
+// eight elements.
+__device__ __forceinline__ uint32_t sq_bf16x2(uint32_t w) {
+  const float lo = __uint_as_float(w << 16), hi = __uint_as_float(w & 0xFFFF0000u);
+  const uint32_t a = (uint32_t)(uint16_t)f2bf(lo * lo), b = (uint32_t)(uint16_t)f2bf(hi * hi);
+  return a | (b << 16);
+}
 __device__ __forceinline__ bf16x8 sq_bf16(bf16x8 a) {
-  bf16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    float v = (float)__builtin_bit_cast(__bf16, a[j]);
-    r[j] = f2bf(v * v);
-  }
-  return r;
+  uint4 u = __builtin_bit_cast(uint4, a);
+  u.x = sq_bf16x2(u.x);
+  u.y = sq_bf16x2(u.y);
+  u.z = sq_bf16x2(u.z);
+  u.w = sq_bf16x2(u.w);
+  return __builtin_bit_cast(bf16x8, u);
 }
 
 // ---------------------------------------------------------------- packing
@@ -149,8 +156,11 @@ __device__ __forceinline__ void normals16(uint64_t seed, uint64_t call, uint32_t
 }
 
 // ---------------------------------------------------------------- forward
-// DBG (diagnostics build only): dbg[row][386] receives every unit's
-// post-activation value (256 layer-1, 128 layer-2, 2 layer-3 pre-tanh).
+// DBG (diagnostics build only): dbg[row][kDbgCols] receives every unit's
+// post-activation value (256 layer-1, 128 layer-2, 2 layer-3 pre-tanh), then
+// layer 2's pre-bias mean accumulator, variance accumulator and normal draw
+// (3 x 128).
+constexpr int kDbgCols = 386 + 3 * 128;
 template <bool NOISE, bool DBG = false>
 __global__ void __launch_bounds__(threads_for<NOISE>()) k_actor_fwd(const float* __restrict__ X, float* __restrict__ out,
                                                         int64_t M, const char* __restrict__ packed, float sd,
@@ -224,7 +234,7 @@ __global__ void __launch_bounds__(threads_for<NOISE>()) k_actor_fwd(const float*
         if (NOISE) y += sd * __builtin_sqrtf(fmaxf(var[i] + b * b, 0.f)) * z[i];
         y = fmaxf(y, 0.f);
         acc[i] = y;
-        if (DBG && valid) dbg[row * 386 + hid] = y;
+        if (DBG && valid) dbg[row * kDbgCols + hid] = y;
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -261,7 +271,12 @@ __global__ void __launch_bounds__(threads_for<NOISE>()) k_actor_fwd(const float*
         float y = acc[i] + b;
         if (NOISE) y += sd * __builtin_sqrtf(fmaxf(var[i] + b * b, 0.f)) * z[i];
         y = fmaxf(y, 0.f);
-        if (DBG && valid) dbg[row * 386 + kH1 + hid] = y;
+        if (DBG && valid) {
+          dbg[row * kDbgCols + kH1 + hid] = y;
+          dbg[row * kDbgCols + 386 + hid] = acc[i];
+          dbg[row * kDbgCols + 386 + kH2 + hid] = NOISE ? var[i] : 0.f;
+          dbg[row * kDbgCols + 386 + 2 * kH2 + hid] = NOISE ? z[i] : 0.f;
+        }
         m0 += sW3[hid] * y;
         m1 += sW3[kH2 + hid] * y;
         if (NOISE) {
@@ -289,7 +304,7 @@ __global__ void __launch_bounds__(threads_for<NOISE>()) k_actor_fwd(const float*
         const float b = sB[kH1 + kH2 + i];
         float y = mm[i] + b;
         if (NOISE) y += sd * __builtin_sqrtf(fmaxf(qq[i] + b * b, 0.f)) * z[i];
-        if (DBG) dbg[row * 386 + kH1 + kH2 + i] = y;
+        if (DBG) dbg[row * kDbgCols + kH1 + kH2 + i] = y;
         o[i] = tanhf(y);
       }
       *(float2*)(out + row * kOut) = make_float2(o[0], o[1]);
@@ -345,7 +360,7 @@ int sk_actor_forward(const void* packed, const float* obs, float* actions, int64
 }
 
 // diagnostics only (not in include/skillshot.h): the noisy forward with every
-// unit's activation dumped to dbg[rows][386]
+// unit's activation dumped to dbg[rows][kDbgCols]
 int skdiag_actor_forward_dbg(const void* packed, const float* obs, float* actions, float* dbg, int64_t rows,
                              float noise_sd, uint64_t seed, uint64_t call, void* stream) {
   const int threads = threads_for<true>();

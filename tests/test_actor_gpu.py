@@ -7,9 +7,10 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-# The kernel's op: bf16 operands (inputs, weights, hidden activations), fp32
-# accumulation and epilogues.  Against a torch reference of exactly that op
-# (bf16-rounded operands, fp64 accumulation) only accumulation order differs,
+# The kernel's op: layers 1-2 on MFMA with bf16 operands (inputs, weights,
+# layer-1 activations), fp32 accumulation and epilogues; layer 3 on the fp32
+# VALU (fp32 layer-2 activations and W3).  Against a torch reference of exactly
+# that op (same roundings, fp64 accumulation) only accumulation order differs,
 # but that can move a hidden activation across a bf16 rounding boundary (one
 # bf16 ulp, 2^-8 relative), so the bar is a mean and a max: EMU_*.  Against the
 # pure fp32 actor the operand rounding itself shows: FP32_* at 4x the
@@ -23,10 +24,12 @@ def _bf(t):
 
 
 def _emulated(a, x):
-    """The kernel's arithmetic in torch: bf16 operands, fp64 accumulation."""
+    """The kernel's arithmetic in torch: bf16 operands for layers 1-2, fp32
+    for layer 3, fp64 accumulation."""
     h = x.double()
     for k, l in enumerate((a.l1, a.l2, a.l3)):
-        h = _bf(h) @ _bf(l.weight.detach()).t() + l.bias.detach().double()
+        rnd = _bf if k < 2 else (lambda t: t.float().double())
+        h = rnd(h) @ rnd(l.weight.detach()).t() + l.bias.detach().double()
         h = torch.tanh(h) if k == 2 else torch.relu(h).float().double()
     return h.float()
 

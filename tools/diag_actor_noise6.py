@@ -15,7 +15,7 @@ L = k.L
 L.skdiag_actor_forward_dbg.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int64, ctypes.c_float, ctypes.c_uint64,
                                        ctypes.c_uint64, ctypes.c_void_p]
 sd = 0.1
-out = torch.empty(n, 2, device="cuda"); dbg = torch.zeros(n, 386, device="cuda")
+out = torch.empty(n, 2, device="cuda"); dbg = torch.zeros(n, 770, device="cuda")
 L.skdiag_actor_forward_dbg(ctypes.c_void_p(k.buf.data_ptr()), ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(out.data_ptr()),
                            ctypes.c_void_p(dbg.data_ptr()), n, sd, 7, 1, None)
 torch.cuda.synchronize()
