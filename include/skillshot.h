@@ -213,7 +213,8 @@ int sk_env_rollout_random(sk_env* env, int32_t n_ticks, int32_t tick_limit, void
 
 /* Fused MFMA forward of the actor of model_define_actor
  * (SkillshotLearner.py:70-96): a = tanh(W3 relu(W2 relu(W1 s + b1) + b2) + b3),
- * 12 -> 256 -> 128 -> 2, bf16 operands with fp32 accumulation, for `rows`
+ * 12 -> 256 -> 128 -> 2 (layers 1-2 on MFMA with bf16 operands and fp32
+ * accumulation, layer 3 in fp32), for `rows`
  * observations (obs float[rows][12] -> actions float[rows][2]).
  * noise_sd != 0 samples model_act_param_noise (:245-281) for every row
  * independently (w -> w(1 + noise_sd*N(0,1)), exact in distribution by local
@@ -226,6 +227,12 @@ int sk_actor_pack(const float* W1, const float* b1, const float* W2, const float
                   const float* b3, void* packed, void* stream);
 int sk_actor_forward(const void* packed, const float* obs, float* actions, int64_t rows, float noise_sd,
                      uint64_t seed, uint64_t call, void* stream);
+/* As sk_actor_forward, with the noise call number read on device from
+ * *call_counter (8-byte aligned device memory) when the kernel runs, so a
+ * captured hipGraph draws fresh noise on every replay; the caller advances
+ * the counter between calls (stream-ordered). */
+int sk_actor_forward_dev(const void* packed, const float* obs, float* actions, int64_t rows, float noise_sd,
+                         uint64_t seed, const uint64_t* call_counter, void* stream);
 
 #ifdef __cplusplus
 }

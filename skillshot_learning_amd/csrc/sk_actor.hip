@@ -164,7 +164,12 @@ constexpr int kDbgCols = 386 + 3 * 128;
 template <bool NOISE, bool DBG = false>
 __global__ void __launch_bounds__(threads_for<NOISE>()) k_actor_fwd(const float* __restrict__ X, float* __restrict__ out,
                                                         int64_t M, const char* __restrict__ packed, float sd,
-                                                        uint64_t seed, uint64_t call, float* dbg = nullptr) {
+                                                        uint64_t seed, uint64_t call,
+                                                        const uint64_t* __restrict__ call_dev = nullptr,
+                                                        float* dbg = nullptr) {
+  // the noise call number comes from device memory when given (graph replays
+  // then draw fresh noise per replay; the caller advances the counter)
+  if (NOISE && call_dev) call = *call_dev;  // wave-uniform scalar load
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16x8* sW2 = (bf16x8*)smem;                               // [4][16][64]
   bf16x8* sW2s = (bf16x8*)(smem + kW2Frag);                  // NOISE only
@@ -327,14 +332,22 @@ int sk_actor_pack(const float* W1, const float* b1, const float* W2, const float
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
 }
 
-int sk_actor_forward(const void* packed, const float* obs, float* actions, int64_t rows, float noise_sd,
-                     uint64_t seed, uint64_t call, void* stream) {
+static int actor_forward(const void* packed, const float* obs, float* actions, int64_t rows, float noise_sd,
+                         uint64_t seed, uint64_t call, const uint64_t* call_dev, void* stream) {
   if (!packed || !obs || !actions || rows < 0) return SK_EINVAL;
   if ((((uintptr_t)obs) & 15) || (((uintptr_t)actions) & 7) || (((uintptr_t)packed) & 15)) return SK_EINVAL;
+  if (call_dev && (((uintptr_t)call_dev) & 7)) return SK_EINVAL;
   if (rows == 0) return SK_OK;
-  int dev = 0, cus = 256;
+  int dev = 0;
   (void)hipGetDevice(&dev);
-  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  static int cus_of[64] = {0};  // CU count per device, queried once
+  if (dev < 0 || dev >= 64) return SK_EINVAL;
+  if (!cus_of[dev]) {
+    int c = 256;
+    (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+    cus_of[dev] = c;
+  }
+  const int cus = cus_of[dev];
   const bool noise = noise_sd != 0.f;
   const int threads = noise ? threads_for<true>() : threads_for<false>();
   const int64_t tiles = (rows + 31) / 32;
@@ -351,12 +364,23 @@ int sk_actor_forward(const void* packed, const float* obs, float* actions, int64
   }
   if (noise) {
     k_actor_fwd<true><<<(unsigned)grid, threads, lds, (hipStream_t)stream>>>(obs, actions, rows, (const char*)packed,
-                                                                            noise_sd, seed, call);
+                                                                            noise_sd, seed, call, call_dev);
   } else {
     k_actor_fwd<false><<<(unsigned)grid, threads, lds, (hipStream_t)stream>>>(obs, actions, rows,
                                                                              (const char*)packed, 0.f, seed, call);
   }
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
+}
+
+int sk_actor_forward(const void* packed, const float* obs, float* actions, int64_t rows, float noise_sd,
+                     uint64_t seed, uint64_t call, void* stream) {
+  return actor_forward(packed, obs, actions, rows, noise_sd, seed, call, nullptr, stream);
+}
+
+int sk_actor_forward_dev(const void* packed, const float* obs, float* actions, int64_t rows, float noise_sd,
+                         uint64_t seed, const uint64_t* call_counter, void* stream) {
+  if (!call_counter) return SK_EINVAL;
+  return actor_forward(packed, obs, actions, rows, noise_sd, seed, 0, call_counter, stream);
 }
 
 // diagnostics only (not in include/skillshot.h): the noisy forward with every
@@ -370,7 +394,7 @@ int skdiag_actor_forward_dbg(const void* packed, const float* obs, float* action
   const size_t lds = 2 * kW2Frag + 1024 * 4;
   (void)hipFuncSetAttribute((const void*)k_actor_fwd<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   k_actor_fwd<true, true><<<(unsigned)grid, threads, lds, (hipStream_t)stream>>>(
-      obs, actions, rows, (const char*)packed, noise_sd, seed, call, dbg);
+      obs, actions, rows, (const char*)packed, noise_sd, seed, call, nullptr, dbg);
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
 }
 

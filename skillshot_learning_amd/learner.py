@@ -160,14 +160,22 @@ class Critic(nn.Module):
 
 
 def keras_adam(params):
-    """Keras Adam defaults (lr 1e-3, eps 1e-7); one fused multi-tensor kernel on GPU."""
+    """Keras Adam defaults (lr 1e-3, eps 1e-7); on GPU one fused multi-tensor
+    kernel with the step count on device (capturable into a hipGraph)."""
     params = list(params)
-    fused = bool(params) and params[0].is_cuda
-    return torch.optim.Adam(params, lr=1e-3, betas=(0.9, 0.999), eps=1e-7, fused=fused)
+    gpu = bool(params) and params[0].is_cuda
+    return torch.optim.Adam(params, lr=1e-3, betas=(0.9, 0.999), eps=1e-7, fused=gpu, capturable=gpu)
 
 
 class ReplayRing:
-    """Transitions (s 12f, a 2f, r 1f, s' 12f, done 1f = 112 B) in HBM."""
+    """Transitions (s 12f, a 2f, r 1f, s' 12f, done 1f = 112 B) in HBM.
+
+    Two insert/sample paths: `add`/`sample` keep head and size on the host
+    (slice copies, Python-int range); `add_dev`/`sample_dev` keep them in
+    device scalars (`head_t`, `size_t`) so a captured hipGraph inserts at the
+    right slot and samples the right range on every replay.  Both paths keep
+    both copies in step (`sync_host` reads the device copy back after
+    replays)."""
 
     def __init__(self, capacity, device):
         self.cap = int(capacity)
@@ -178,6 +186,12 @@ class ReplayRing:
         self.d = torch.zeros(self.cap, device=device)
         self.head = 0
         self.size = 0
+        self.head_t = torch.zeros((), dtype=torch.int64, device=device)
+        self.size_t = torch.zeros((), dtype=torch.int64, device=device)
+        self._ar = {}
+
+    def _buffers(self):
+        return (self.s, self.a, self.r, self.s2, self.d)
 
     def add(self, s, a, r, s2, d):
         n = s.shape[0]
@@ -185,16 +199,43 @@ class ReplayRing:
             s, a, r, s2, d = s[-self.cap:], a[-self.cap:], r[-self.cap:], s2[-self.cap:], d[-self.cap:]
             n = self.cap
         first = min(n, self.cap - self.head)  # contiguous copies, at most two per buffer
-        for dst, src in ((self.s, s), (self.a, a), (self.r, r), (self.s2, s2), (self.d, d)):
+        for dst, src in zip(self._buffers(), (s, a, r, s2, d)):
             dst[self.head:self.head + first].copy_(src[:first])
             if first < n:
                 dst[:n - first].copy_(src[first:])
         self.head = (self.head + n) % self.cap
         self.size = min(self.cap, self.size + n)
+        self.head_t.fill_(self.head)
+        self.size_t.fill_(self.size)
 
     def sample(self, b, generator=None):
         idx = torch.randint(0, self.size, (b,), device=self.s.device, generator=generator)
         return self.s[idx], self.a[idx], self.r[idx], self.s2[idx], self.d[idx]
+
+    def add_dev(self, s, a, r, s2, d):
+        """Capturable insert of n <= capacity rows at the device-side head."""
+        n = s.shape[0]
+        if n > self.cap:
+            raise ValueError("add_dev: more rows than capacity")
+        ar = self._ar.get(n)
+        if ar is None:
+            ar = self._ar[n] = torch.arange(n, dtype=torch.int64, device=self.s.device)
+        idx = torch.remainder(ar + self.head_t, self.cap)
+        for dst, src in zip(self._buffers(), (s, a, r, s2, d)):
+            dst.index_copy_(0, idx, src.reshape(dst[:n].shape))
+        self.head_t.copy_(torch.remainder(self.head_t + n, self.cap))
+        self.size_t.copy_(torch.clamp(self.size_t + n, max=self.cap))
+        self.head = (self.head + n) % self.cap  # host mirror (exact while n is fixed)
+        self.size = min(self.cap, self.size + n)
+
+    def sample_dev(self, b, generator=None):
+        """Capturable uniform sample over the device-side size."""
+        u = torch.rand(b, dtype=torch.float64, device=self.s.device, generator=generator)
+        idx = torch.minimum((u * self.size_t).long(), self.size_t - 1)
+        return self.s[idx], self.a[idx], self.r[idx], self.s2[idx], self.d[idx]
+
+    def sync_host(self):
+        self.head, self.size = int(self.head_t), int(self.size_t)
 
 
 class DDPG:
@@ -304,11 +345,15 @@ class DDPG:
         for k in range(0, states.shape[0], b):
             self.model_actor_fit_step(states[k:k + b])
 
-    def replay_update(self, batch):
+    def replay_update(self, batch, device_sampling=False):
         """Build-side extension: one critic + one actor step on a replay
         minibatch (shared across ranks by all-gather), optional bootstrapped
-        target with target nets and soft update tau."""
-        s, a, r, s2, d = self.replay.sample(batch, generator=self.gen)
+        target with target nets and soft update tau.  device_sampling draws
+        the minibatch over the ring's device-side size (hipGraph capture)."""
+        if device_sampling:
+            s, a, r, s2, d = self.replay.sample_dev(batch, generator=self.gen)
+        else:
+            s, a, r, s2, d = self.replay.sample(batch, generator=self.gen)
         s, a, r, s2, d = self._allgather_batch(s, a, r, s2, d)
         target = r
         if self.gamma > 0.0:
@@ -325,9 +370,9 @@ class DDPG:
 
     @torch.no_grad()
     def soft_update(self):
+        """target <- target + tau (online - target), one multi-tensor op per net."""
         for tgt, src in ((self.target_actor, self.model_actor), (self.target_critic, self.model_critic)):
-            for pt, ps in zip(tgt.parameters(), src.parameters()):
-                pt.mul_(1.0 - self.tau).add_(ps, alpha=self.tau)
+            torch._foreach_lerp_(list(tgt.parameters()), list(src.parameters()), self.tau)
 
 
 class SkillshotLearner:
@@ -481,6 +526,28 @@ class SkillshotLearner:
                 self.actor_kernel.refresh()
         return stats
 
+    def tick_graph(self, batch=256, updates_per_tick=1, ticks_per_graph=2, warmup=3):
+        """The replay-rule tick of `train_ticks` captured as ONE hipGraph.
+
+        One replay runs `ticks_per_graph` ticks (even: the engine's device step
+        counter advances through two ping-pong slots): per tick the fused actor
+        kernel (noise call number on device), the fused env step with
+        obs/reward/auto-reset into static buffers, a device-side-head insert of
+        the 2N transitions, `updates_per_tick` critic + actor updates on
+        device-side samples (capturable fused Adam), the soft target update and
+        the actor repack.  Every per-tick quantity (ring head and size, step
+        and noise counters, RNG offsets) lives on device, so replays continue
+        the eager trajectory's semantics.  Single-GPU only: collectives stay
+        on the eager path.  Returns a TickGraph; `.run(n)` replays n times.
+        """
+        if self.device.type != "cuda":
+            raise RuntimeError("tick_graph needs the GPU engine")
+        if self.ddpg.world() > 1:
+            raise RuntimeError("tick_graph is single-GPU (the multi-rank update stays eager)")
+        if ticks_per_graph % 2:
+            raise ValueError("ticks_per_graph must be even (step-counter ping-pong slots)")
+        return TickGraph(self, batch, updates_per_tick, ticks_per_graph, warmup)
+
     # ------------------------------------------------------------ persistence
     def state_dict(self):
         return dict(actor=self.model_actor.state_dict(), critic=self.model_critic.state_dict(),
@@ -495,3 +562,71 @@ class SkillshotLearner:
         self.game_environment.load_state_dict(d["env"])
         if self.actor_kernel is not None:
             self.actor_kernel.refresh()
+
+
+class TickGraph:
+    """Captured replay-rule ticks (see SkillshotLearner.tick_graph)."""
+
+    def __init__(self, L, batch, updates_per_tick, ticks_per_graph, warmup):
+        self.L, self.batch, self.updates, self.ticks = L, batch, updates_per_tick, ticks_per_graph
+        g = L.game_environment
+        n = L.n_envs
+        dev = L.device
+        self.obs = L.prepare_states().clone()
+        self.act = torch.empty((2, n, ACTION_DIM), dtype=torch.float32, device=dev)
+        self.out = dict(obs=g.new_obs(), reward=torch.empty((2, n), dtype=torch.float32, device=dev),
+                        done=torch.empty(n, dtype=torch.uint8, device=dev),
+                        winner=torch.empty(n, dtype=torch.uint8, device=dev), obs_reset=g.new_obs())
+        self.stream = torch.cuda.Stream(device=dev)
+        self.stream.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(self.stream):
+            # fill the ring past one batch without updates, then warm the
+            # update path eagerly (allocator pools, autograd, Adam state)
+            while L.replay.size < batch:
+                self._tick(update=False)
+            for _ in range(max(warmup, 1)):
+                self._tick(update=True)
+        self.stream.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        self.graph.register_generator_state(L.gen)
+        mirror = (L.replay.head, L.replay.size)  # capture records the inserts without running them
+        with torch.cuda.graph(self.graph, stream=self.stream):
+            for _ in range(self.ticks):
+                self._tick(update=True)
+        self.stream.synchronize()
+        L.replay.head, L.replay.size = mirror
+        self.replays = 0
+
+    def _tick(self, update):
+        L = self.L
+        x = self.obs.view(-1, STATE_DIM)
+        a = self.act.view(-1, ACTION_DIM)
+        mode = L.exploration
+        if L.actor_kernel is not None:
+            L.actor_kernel(x, noise_sd=L.param_noise_sd if mode == "param_noise" else 0.0, out=a)
+            if mode == "action_noise":
+                a.add_(L.action_noise_sd * torch.randn(a.shape, device=a.device, generator=L.gen))
+        else:
+            a.copy_(L.model_act(self.obs).view(-1, ACTION_DIM))
+        o = L.game_environment.step(self.act, obs=True, reward="looking", auto_reset=True, reset_obs=True,
+                                    out=self.out)
+        L.replay.add_dev(x, a, o["reward"].view(-1), o["obs"].view(-1, STATE_DIM), o["done"].float().repeat(2))
+        self.obs.copy_(o["obs_reset"])
+        if update:
+            for _ in range(self.updates):
+                L.ddpg.replay_update(self.batch, device_sampling=True)
+            if L.actor_kernel is not None:
+                L.actor_kernel.refresh()
+
+    def run(self, n=1):
+        """n graph replays (n * ticks_per_graph ticks) on the graph's stream."""
+        cur = torch.cuda.current_stream(self.L.device)
+        self.stream.wait_stream(cur)
+        for _ in range(n):
+            self.graph.replay()
+        cur.wait_stream(self.stream)
+        self.replays += n
+        # host mirrors of the ring (2N rows per tick)
+        r, rows = self.L.replay, n * self.ticks * 2 * self.obs.shape[1]
+        r.head = (r.head + rows) % r.cap
+        r.size = min(r.cap, r.size + rows)

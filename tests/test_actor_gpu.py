@@ -142,3 +142,34 @@ def test_learner_reference_epochs_full_reward(mods):
         assert len(prog["epoch_ticks"]) == 1
         moved = sum(float((p.detach() - b).abs().sum()) for p, b in zip(L.model_critic.parameters(), before))
         assert moved > 0
+
+
+def test_tick_graph_replays_train(mods):
+    """The replay-rule tick captured as one hipGraph: replays keep inserting
+    at the device-side head, draw fresh parameter noise and keep training."""
+    learner, _ = mods
+    L = learner.SkillshotLearner(n_envs=1024, seed=6, tick_limit=300, replay_capacity=1 << 14, gamma=0.9, tau=0.01)
+    tg = L.tick_graph(batch=256, updates_per_tick=1, ticks_per_graph=2)
+    size0 = int(L.replay.size_t)
+    head0 = int(L.replay.head_t)
+    a0 = tg.act.clone()
+    w0 = [p.detach().clone() for p in L.model_actor.parameters()]
+    t0 = [p.detach().clone() for p in L.ddpg.target_actor.parameters()]
+    ctr0 = int(L.actor_kernel.counter)
+    step0 = L.game_environment.step_counter
+    tg.run(5)
+    torch.cuda.synchronize()
+    rows = 5 * 2 * 2 * 1024
+    assert int(L.replay.size_t) == min(1 << 14, size0 + rows)
+    assert int(L.replay.head_t) == (head0 + rows) % (1 << 14)
+    assert (L.replay.size, L.replay.head) == (int(L.replay.size_t), int(L.replay.head_t))
+    assert int(L.actor_kernel.counter) == ctr0 + 10            # one noisy call per tick
+    assert L.game_environment.step_counter == step0 + 10       # device step counter advanced per tick
+    assert (tg.act - a0).abs().mean().item() > 1e-3             # fresh actions
+    assert sum(float((p.detach() - w).abs().sum()) for p, w in zip(L.model_actor.parameters(), w0)) > 0
+    assert sum(float((p.detach() - w).abs().sum()) for p, w in zip(L.ddpg.target_actor.parameters(), t0)) > 0
+    for p in list(L.model_actor.parameters()) + list(L.model_critic.parameters()):
+        assert torch.isfinite(p).all()
+    # the ring holds the graph's transitions: finite obs, actions in [-1, 1]
+    assert torch.isfinite(L.replay.s[:L.replay.size]).all()
+    assert L.replay.a[:L.replay.size].abs().max().item() <= 1.0

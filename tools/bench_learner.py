@@ -30,6 +30,7 @@ def main():
     p.add_argument("--batch", type=int, default=4096)
     p.add_argument("--updates", type=int, default=1)
     p.add_argument("--exploration", default="param_noise")
+    p.add_argument("--graph", action="store_true", help="replay the tick as one captured hipGraph (1 GPU)")
     a = p.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -70,6 +71,25 @@ def main():
             for k, name in enumerate(phases):
                 ev[name].append((e[k], e[k + 1]))
 
+    if a.graph:
+        tg = L.tick_graph(batch=a.batch, updates_per_tick=a.updates, ticks_per_graph=2)
+        tg.run(max(a.warmup // 2, 1))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(tg.stream)
+        tg.run(a.ticks // 2)
+        e1.record(tg.stream)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        ticks = (a.ticks // 2) * 2
+        print(json.dumps(dict(
+            metric="env-steps/s with DDPG learner in the loop", value=a.envs * ticks / el, unit="env-steps/s",
+            n_gpus=1, envs_per_gpu=a.envs, ticks=ticks, batch_per_rank=a.batch, updates_per_tick=a.updates,
+            exploration=a.exploration, mode="hipgraph (2 ticks per replay)", ms_per_tick=el * 1e3 / ticks,
+            gpu_ms_per_tick=e0.elapsed_time(e1) / ticks, replay_size=L.replay.size,
+            episodes=g.counters())), flush=True)
+        return
     for _ in range(max(a.warmup, 2)):
         tick(False)
     torch.cuda.synchronize()
