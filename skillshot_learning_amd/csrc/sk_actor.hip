@@ -317,6 +317,155 @@ __global__ void __launch_bounds__(threads_for<NOISE>()) k_actor_fwd(const float*
   }
 }
 
+// One 32-row tile per WORKGROUP: for batches too small to give every SIMD its
+// own tile (the 4,096-game learner has 8,192 rows = 256 tiles for 1,024
+// SIMDs).  Wave w computes layer-1 chunks 2w, 2w+1 and layer-2 chunk w.  The
+// layer-1 output fragments meet in LDS in the B-operand lane layout, so every
+// wave reads fragment kk at [kk][lane]; layer 3's per-wave partial dot
+// products are summed across the four waves in LDS.  Same noise counters as
+// k_actor_fwd (row, unit chunk, lane half): the two modes draw identical
+// noise and differ only in layer 3's fp32 summation order.
+constexpr int kWgThreads = 256;
+constexpr size_t kWgExtra = 16 * 64 * 16 + 4 * 32 * 16;  // h1 fragments + layer-3 partials
+
+template <bool NOISE>
+__global__ void __launch_bounds__(kWgThreads) k_actor_fwd_wg(const float* __restrict__ X, float* __restrict__ out,
+                                                            int64_t M, const char* __restrict__ packed, float sd,
+                                                            uint64_t seed, uint64_t call,
+                                                            const uint64_t* __restrict__ call_dev) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16x8* sW2 = (bf16x8*)smem;
+  bf16x8* sW2s = (bf16x8*)(smem + kW2Frag);
+  float* sB = (float*)(smem + (NOISE ? 2 : 1) * kW2Frag);
+  float* sW3 = sB + 512;
+  bf16x8* sH1 = (bf16x8*)(sB + 1024);            // [16 k-steps][64 lanes]
+  float4* sPart = (float4*)(sH1 + 16 * 64);      // [4 waves][32 rows]: m0 m1 q0 q1
+  if (NOISE && call_dev) call = *call_dev;
+  {
+    const uint4* g = (const uint4*)(packed + kOffW2);
+    uint4* sm = (uint4*)smem;
+    const int n16 = (NOISE ? 2 : 1) * kW2Frag / 16;
+    for (int k = threadIdx.x; k < n16; k += kWgThreads) sm[k] = g[k];
+    const float* gb = (const float*)(packed + kOffB);
+    for (int k = threadIdx.x; k < 1024; k += kWgThreads) sB[k] = gb[k];
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5, w = threadIdx.x >> 6;
+  const int64_t ntiles = (M + 31) / 32;
+  const bf16x8* gW1 = (const bf16x8*)(packed + kOffW1);
+  const bf16x8* gW1s = (const bf16x8*)(packed + kOffW1s);
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t row = tile * 32 + r;
+    const bool valid = row < M;
+    float x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = 0.f;
+    if (valid) {
+      const float* xr = X + row * kIn + 8 * h;
+      float4 a = *(const float4*)xr;
+      x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
+      if (h == 0) {
+        float4 b = *(const float4*)(xr + 4);
+        x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+      }
+    }
+    bf16x8 xb, xs;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      xb[j] = f2bf(x[j]);
+      xs[j] = f2bf(x[j] * x[j]);
+    }
+    // ---- layer 1, chunks 2w and 2w+1 -> LDS
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      const int c = 2 * w + cc;
+      f32x16 acc = {0}, var = {0};
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gW1[c * 64 + lane], xb, acc, 0, 0, 0);
+      if (NOISE) var = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gW1s[c * 64 + lane], xs, var, 0, 0, 0);
+      float z[16];
+      if (NOISE) normals16(seed, call, (uint32_t)row, (uint32_t)c, h, z);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int hid = 32 * c + (i & 3) + 8 * (i >> 2) + 4 * h;
+        const float b = sB[hid];
+        float y = acc[i] + b;
+        if (NOISE) y += sd * __builtin_sqrtf(fmaxf(var[i] + b * b, 0.f)) * z[i];
+        acc[i] = fmaxf(y, 0.f);
+      }
+#pragma unroll
+      for (int sidx = 0; sidx < 2; ++sidx) {
+        bf16x8 f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = f2bf(acc[8 * sidx + j]);
+        sH1[(2 * c + sidx) * 64 + lane] = f;
+      }
+    }
+    __syncthreads();
+    // ---- layer 2, chunk t = w, and this wave's share of layer 3
+    float m0 = 0.f, m1 = 0.f, q0 = 0.f, q1 = 0.f;
+    {
+      const int t = w;
+      f32x16 acc = {0}, var = {0};
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) {
+        const bf16x8 hb = sH1[kk * 64 + lane];
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sW2[(t * 16 + kk) * 64 + lane], hb, acc, 0, 0, 0);
+        if (NOISE)
+          var = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sW2s[(t * 16 + kk) * 64 + lane], sq_bf16(hb), var, 0, 0, 0);
+      }
+      float z[16];
+      if (NOISE) normals16(seed, call, (uint32_t)row, (uint32_t)(8 + t), h, z);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int hid = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
+        const float b = sB[kH1 + hid];
+        float y = acc[i] + b;
+        if (NOISE) y += sd * __builtin_sqrtf(fmaxf(var[i] + b * b, 0.f)) * z[i];
+        y = fmaxf(y, 0.f);
+        m0 += sW3[hid] * y;
+        m1 += sW3[kH2 + hid] * y;
+        if (NOISE) {
+          q0 += sW3[2 * kH2 + hid] * (y * y);
+          q1 += sW3[3 * kH2 + hid] * (y * y);
+        }
+      }
+    }
+    m0 += __shfl_xor(m0, 32, 64);
+    m1 += __shfl_xor(m1, 32, 64);
+    if (NOISE) {
+      q0 += __shfl_xor(q0, 32, 64);
+      q1 += __shfl_xor(q1, 32, 64);
+    }
+    if (h == 0) sPart[w * 32 + r] = make_float4(m0, m1, q0, q1);
+    __syncthreads();
+    // ---- layer 3 epilogue on wave 0
+    if (w == 0 && h == 0 && valid) {
+      float4 p = sPart[r];
+#pragma unroll
+      for (int k = 1; k < 4; ++k) {
+        const float4 o = sPart[k * 32 + r];
+        p.x += o.x; p.y += o.y; p.z += o.z; p.w += o.w;
+      }
+      float z[16];
+      if (NOISE) normals16(seed, call, (uint32_t)row, 12u, 0, z);
+      const float mm[2] = {p.x, p.y}, qq[2] = {p.z, p.w};
+      float o2[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const float b = sB[kH1 + kH2 + i];
+        float y = mm[i] + b;
+        if (NOISE) y += sd * __builtin_sqrtf(fmaxf(qq[i] + b * b, 0.f)) * z[i];
+        o2[i] = tanhf(y);
+      }
+      *(float2*)(out + row * kOut) = make_float2(o2[0], o2[1]);
+    }
+  }
+}
+
+// launch-mode override for tests and sweeps: 0 auto, 1 tile per wave, 2 tile per workgroup
+int g_actor_mode = 0;
+
 }  // namespace
 
 extern "C" {
@@ -362,6 +511,26 @@ static int actor_forward(const void* packed, const float* obs, float* actions, i
                               kW2Frag + 1024 * 4);
     attr_set = true;
   }
+  // tile per workgroup when tile-per-wave would leave SIMDs idle
+  const bool wg_mode = g_actor_mode == 2 || (g_actor_mode == 0 && tiles < (int64_t)cus * (threads / 64));
+  if (wg_mode) {
+    static bool wg_attr_set = false;
+    if (!wg_attr_set) {
+      (void)hipFuncSetAttribute((const void*)k_actor_fwd_wg<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                2 * kW2Frag + 1024 * 4 + kWgExtra);
+      (void)hipFuncSetAttribute((const void*)k_actor_fwd_wg<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                kW2Frag + 1024 * 4 + kWgExtra);
+      wg_attr_set = true;
+    }
+    const int64_t wgrid = tiles < cus ? tiles : cus;
+    if (noise)
+      k_actor_fwd_wg<true><<<(unsigned)wgrid, kWgThreads, lds + kWgExtra, (hipStream_t)stream>>>(
+          obs, actions, rows, (const char*)packed, noise_sd, seed, call, call_dev);
+    else
+      k_actor_fwd_wg<false><<<(unsigned)wgrid, kWgThreads, lds + kWgExtra, (hipStream_t)stream>>>(
+          obs, actions, rows, (const char*)packed, 0.f, seed, call, nullptr);
+    return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
+  }
   if (noise) {
     k_actor_fwd<true><<<(unsigned)grid, threads, lds, (hipStream_t)stream>>>(obs, actions, rows, (const char*)packed,
                                                                             noise_sd, seed, call, call_dev);
@@ -381,6 +550,14 @@ int sk_actor_forward_dev(const void* packed, const float* obs, float* actions, i
                          uint64_t seed, const uint64_t* call_counter, void* stream) {
   if (!call_counter) return SK_EINVAL;
   return actor_forward(packed, obs, actions, rows, noise_sd, seed, 0, call_counter, stream);
+}
+
+// diagnostics only (not in include/skillshot.h): force the launch mode
+// (0 auto, 1 one tile per wave, 2 one tile per workgroup)
+int skdiag_actor_set_mode(int mode) {
+  if (mode < 0 || mode > 2) return SK_EINVAL;
+  g_actor_mode = mode;
+  return SK_OK;
 }
 
 // diagnostics only (not in include/skillshot.h): the noisy forward with every

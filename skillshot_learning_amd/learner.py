@@ -168,49 +168,59 @@ def keras_adam(params):
 
 
 class ReplayRing:
-    """Transitions (s 12f, a 2f, r 1f, s' 12f, done 1f = 112 B) in HBM.
+    """Transitions (s 12f, a 2f, r 1f, s' 12f, done 1f = 112 B) in HBM, packed
+    as one [capacity, 28] float32 row per transition so an insert is one
+    scatter and a minibatch one gather (`s`, `a`, `r`, `s2`, `d` are column
+    views).
 
     Two insert/sample paths: `add`/`sample` keep head and size on the host
     (slice copies, Python-int range); `add_dev`/`sample_dev` keep them in
     device scalars (`head_t`, `size_t`) so a captured hipGraph inserts at the
     right slot and samples the right range on every replay.  Both paths keep
-    both copies in step (`sync_host` reads the device copy back after
-    replays)."""
+    both copies in step (`sync_host` reads the device copy back)."""
+
+    WIDTH = 2 * STATE_DIM + ACTION_DIM + 2
 
     def __init__(self, capacity, device):
         self.cap = int(capacity)
-        self.s = torch.zeros(self.cap, STATE_DIM, device=device)
-        self.a = torch.zeros(self.cap, ACTION_DIM, device=device)
-        self.r = torch.zeros(self.cap, device=device)
-        self.s2 = torch.zeros(self.cap, STATE_DIM, device=device)
-        self.d = torch.zeros(self.cap, device=device)
+        self.buf = torch.zeros(self.cap, self.WIDTH, device=device)
+        self.s, self.a, self.r, self.s2, self.d = self._split(self.buf)
         self.head = 0
         self.size = 0
         self.head_t = torch.zeros((), dtype=torch.int64, device=device)
         self.size_t = torch.zeros((), dtype=torch.int64, device=device)
         self._ar = {}
 
-    def _buffers(self):
-        return (self.s, self.a, self.r, self.s2, self.d)
+    @staticmethod
+    def _split(rows):
+        S, A = STATE_DIM, ACTION_DIM
+        return (rows[:, :S], rows[:, S:S + A], rows[:, S + A], rows[:, S + A + 1:2 * S + A + 1],
+                rows[:, 2 * S + A + 1])
+
+    @staticmethod
+    def _pack(s, a, r, s2, d):
+        n = s.shape[0]
+        # one kernel: cat promotes (e.g. a uint8 done column) to float32
+        return torch.cat([s.reshape(n, STATE_DIM), a.reshape(n, ACTION_DIM), r.reshape(n, 1),
+                          s2.reshape(n, STATE_DIM), d.reshape(n, 1)], 1).float()
 
     def add(self, s, a, r, s2, d):
         n = s.shape[0]
+        rows = self._pack(s, a, r, s2, d)
         if n > self.cap:
-            s, a, r, s2, d = s[-self.cap:], a[-self.cap:], r[-self.cap:], s2[-self.cap:], d[-self.cap:]
-            n = self.cap
-        first = min(n, self.cap - self.head)  # contiguous copies, at most two per buffer
-        for dst, src in zip(self._buffers(), (s, a, r, s2, d)):
-            dst[self.head:self.head + first].copy_(src[:first])
-            if first < n:
-                dst[:n - first].copy_(src[first:])
+            rows, n = rows[-self.cap:], self.cap
+        first = min(n, self.cap - self.head)  # contiguous copies, at most two
+        self.buf[self.head:self.head + first].copy_(rows[:first])
+        if first < n:
+            self.buf[:n - first].copy_(rows[first:])
         self.head = (self.head + n) % self.cap
         self.size = min(self.cap, self.size + n)
         self.head_t.fill_(self.head)
         self.size_t.fill_(self.size)
 
     def sample(self, b, generator=None):
-        idx = torch.randint(0, self.size, (b,), device=self.s.device, generator=generator)
-        return self.s[idx], self.a[idx], self.r[idx], self.s2[idx], self.d[idx]
+        idx = torch.randint(0, self.size, (b,), device=self.buf.device, generator=generator)
+        return self._split(self.buf[idx])
 
     def add_dev(self, s, a, r, s2, d):
         """Capturable insert of n <= capacity rows at the device-side head."""
@@ -219,10 +229,8 @@ class ReplayRing:
             raise ValueError("add_dev: more rows than capacity")
         ar = self._ar.get(n)
         if ar is None:
-            ar = self._ar[n] = torch.arange(n, dtype=torch.int64, device=self.s.device)
-        idx = torch.remainder(ar + self.head_t, self.cap)
-        for dst, src in zip(self._buffers(), (s, a, r, s2, d)):
-            dst.index_copy_(0, idx, src.reshape(dst[:n].shape))
+            ar = self._ar[n] = torch.arange(n, dtype=torch.int64, device=self.buf.device)
+        self.buf.index_copy_(0, torch.remainder(ar + self.head_t, self.cap), self._pack(s, a, r, s2, d))
         self.head_t.copy_(torch.remainder(self.head_t + n, self.cap))
         self.size_t.copy_(torch.clamp(self.size_t + n, max=self.cap))
         self.head = (self.head + n) % self.cap  # host mirror (exact while n is fixed)
@@ -230,9 +238,9 @@ class ReplayRing:
 
     def sample_dev(self, b, generator=None):
         """Capturable uniform sample over the device-side size."""
-        u = torch.rand(b, dtype=torch.float64, device=self.s.device, generator=generator)
+        u = torch.rand(b, dtype=torch.float64, device=self.buf.device, generator=generator)
         idx = torch.minimum((u * self.size_t).long(), self.size_t - 1)
-        return self.s[idx], self.a[idx], self.r[idx], self.s2[idx], self.d[idx]
+        return self._split(self.buf[idx])
 
     def sync_host(self):
         self.head, self.size = int(self.head_t), int(self.size_t)
@@ -311,7 +319,7 @@ class DDPG:
         self.model_critic.train()  # Dropout active, as in critic.fit (:434)
         q = self.model_critic(s, a).squeeze(-1)
         loss = F.mse_loss(q, target)
-        self.critic_optimiser.zero_grad(set_to_none=False)
+        self.critic_optimiser.zero_grad(set_to_none=True)  # backward writes the grads (no accumulate)
         loss.backward()
         self._allreduce_grads(self.model_critic)
         self.critic_optimiser.step()
@@ -325,7 +333,7 @@ class DDPG:
             p.requires_grad_(False)
         q = self.model_critic(s, self.model_actor(s))
         loss = -q.sum()
-        self.optimiser.zero_grad(set_to_none=False)
+        self.optimiser.zero_grad(set_to_none=True)
         loss.backward()
         for p in self.model_critic.parameters():
             p.requires_grad_(True)
@@ -392,6 +400,10 @@ class SkillshotLearner:
         self.game_environment = VecSkillshotGame(n_envs, device=self.device, seed=seed, env_offset=env_offset,
                                                  tick_limit=tick_limit, random_positions=use_random_start)
         self.n_envs = n_envs
+        # every game starts its first episode the way model_train starts each
+        # epoch, game_reset(random_positions=use_random_start) (:291); auto-
+        # reset then keeps that start mode for later episodes
+        self.game_environment.reset(random_positions=use_random_start)
         self.max_dist_normaliser = MAX_DIST                    # :43
         self.use_random_start = use_random_start               # :44
         self.dim_state_space, self.dim_action_space, self.dim_reward_space = STATE_DIM, ACTION_DIM, 1
@@ -610,7 +622,8 @@ class TickGraph:
             a.copy_(L.model_act(self.obs).view(-1, ACTION_DIM))
         o = L.game_environment.step(self.act, obs=True, reward="looking", auto_reset=True, reset_obs=True,
                                     out=self.out)
-        L.replay.add_dev(x, a, o["reward"].view(-1), o["obs"].view(-1, STATE_DIM), o["done"].float().repeat(2))
+        L.replay.add_dev(x, a, o["reward"].view(-1), o["obs"].view(-1, STATE_DIM),
+                         o["done"].view(1, -1).expand(2, -1))  # done per (player, game) row
         self.obs.copy_(o["obs_reset"])
         if update:
             for _ in range(self.updates):
@@ -622,8 +635,9 @@ class TickGraph:
         """n graph replays (n * ticks_per_graph ticks) on the graph's stream."""
         cur = torch.cuda.current_stream(self.L.device)
         self.stream.wait_stream(cur)
-        for _ in range(n):
-            self.graph.replay()
+        with torch.cuda.stream(self.stream):  # replay() launches on the current stream
+            for _ in range(n):
+                self.graph.replay()
         cur.wait_stream(self.stream)
         self.replays += n
         # host mirrors of the ring (2N rows per tick)
