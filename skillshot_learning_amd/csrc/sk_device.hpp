@@ -290,18 +290,22 @@ __device__ __attribute__((noinline)) sktrig::SinCos sincos_lib(double x) {  // |
   return o;
 }
 
-__device__ __forceinline__ void tick_env(const Cfg& c, Env& e, double a0_move, double a0_look, double a1_move,
-                                         double a1_look) {
+// The tick with the players' sincos (of the OLD rotations, Player.py:63-64,
+// action-independent) supplied by the caller, who can evaluate them while
+// the actions are still in flight from memory.  ok01: both were in range.
+__device__ __forceinline__ void tick_env_m(const Cfg& c, Env& e, sktrig::SinCos m0, sktrig::SinCos m1, bool ok01,
+                                           double a0_move, double a0_look, double a1_move, double a1_look) {
   const double rn0 = e.rot[0] + clamp_action(a0_look) * c.look;  // == move_look_s
   const double rn1 = e.rot[1] + clamp_action(a1_look) * c.look;
   const double q0 = (e.qcd[0] <= 0) ? rn0 : e.qrot[0];
   const double q1 = (e.qcd[1] <= 0) ? rn1 : e.qrot[1];
-  bool k0, k1, k2, k3;
-  sktrig::SinCos m0 = sktrig::sincos_bf(e.rot[0], &k0);
-  sktrig::SinCos m1 = sktrig::sincos_bf(e.rot[1], &k1);
+  bool k2, k3;
   sktrig::SinCos t0 = sktrig::sincos_bf(q0, &k2);
   sktrig::SinCos t1 = sktrig::sincos_bf(q1, &k3);
-  if (!(k0 & k1 & k2 & k3)) {
+  if (!(ok01 & k2 & k3)) {
+    bool k0, k1;
+    (void)sktrig::sincos_bf(e.rot[0], &k0);
+    (void)sktrig::sincos_bf(e.rot[1], &k1);
     if (!k0) m0 = sincos_lib(e.rot[0]);
     if (!k1) m1 = sincos_lib(e.rot[1]);
     if (!k2) t0 = sincos_lib(q0);
@@ -322,6 +326,14 @@ __device__ __forceinline__ void tick_env(const Cfg& c, Env& e, double a0_move, d
     collide_s(c, e.px[0], e.py[0], e.qx[0], e.qy[0], e.qvalid[0], e.px[1], e.py[1], e.qx[1], e.qy[1],
               e.qvalid[1], e.live, e.winner);
   }
+}
+
+__device__ __forceinline__ void tick_env(const Cfg& c, Env& e, double a0_move, double a0_look, double a1_move,
+                                         double a1_look) {
+  bool k0, k1;
+  const sktrig::SinCos m0 = sktrig::sincos_bf(e.rot[0], &k0);
+  const sktrig::SinCos m1 = sktrig::sincos_bf(e.rot[1], &k1);
+  tick_env_m(c, e, m0, m1, k0 & k1, a0_move, a0_look, a1_move, a1_look);
 }
 
 // ---------------------------------------------------------------- features

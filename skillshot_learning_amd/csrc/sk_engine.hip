@@ -152,10 +152,18 @@ __global__ void __launch_bounds__(kBlock) k_step(StepArgs a, Cfg c) {
   bool d = false;
   Env e;
   if (in) {
+    // state first, actions last (in issue order, so the waits for the state
+    // do not wait for the actions): the players' sincos of the old rotations
+    // then run while the actions arrive
     load_env(a.v, i, e);
-    float2 a0 = a.actions[i];
-    float2 a1 = a.actions[a.n + i];
-    tick_env(c, e, (double)a0.x, (double)a0.y, (double)a1.x, (double)a1.y);
+    __builtin_amdgcn_sched_barrier(0);
+    const float2 a0 = a.actions[i];
+    const float2 a1 = a.actions[a.n + i];
+    __builtin_amdgcn_sched_barrier(0);
+    bool k0, k1;
+    const sktrig::SinCos m0 = sktrig::sincos_bf(e.rot[0], &k0);
+    const sktrig::SinCos m1 = sktrig::sincos_bf(e.rot[1], &k1);
+    tick_env_m(c, e, m0, m1, k0 & k1, (double)a0.x, (double)a0.y, (double)a1.x, (double)a1.y);
     if (a.obs || a.reward) {
       float o0[12], o1[12];
       double pd0, pd1;
