@@ -234,6 +234,28 @@ int sk_actor_forward(const void* packed, const float* obs, float* actions, int64
 int sk_actor_forward_dev(const void* packed, const float* obs, float* actions, int64_t rows, float noise_sd,
                          uint64_t seed, const uint64_t* call_counter, void* stream);
 
+/* --- critic forward and the DDPG bootstrap target (A16) ------------------- */
+
+/* Fused MFMA forward of the critic of model_define_critic
+ * (SkillshotLearner.py:98-121) at inference (Dropout = identity):
+ * q = W3 relu(W2 [relu(W1 s + b1); a] + b2) + b3, 12 -> 256 -> (256+2) -> 128
+ * -> 1; layers 1-2 on MFMA with bf16 operands and fp32 accumulation for the
+ * 256 hidden inputs, the two action inputs and layer 3 in fp32.  Weights are
+ * the torch Linear fp32 tensors (W2 is [128][258]), packed by sk_critic_pack
+ * into a device buffer of sk_critic_packed_bytes() bytes (16-byte aligned).
+ * obs float[rows][12], actions float[rows][2] -> q float[rows]. */
+size_t sk_critic_packed_bytes(void);
+int sk_critic_pack(const float* W1, const float* b1, const float* W2, const float* b2, const float* W3,
+                   const float* b3, void* packed, void* stream);
+int sk_critic_forward(const void* packed, const float* obs, const float* actions, float* q, int64_t rows,
+                      void* stream);
+/* The DDPG bootstrap term Q'(s, mu'(s)) in one launch: the (target) actor
+ * packed by sk_actor_pack, deterministic, then the (target) critic packed by
+ * sk_critic_pack, on the same rows.  actions (nullable) receives mu'(s),
+ * bit-identical to sk_actor_forward with noise_sd = 0. */
+int sk_target_q(const void* actor_packed, const void* critic_packed, const float* obs, float* q, float* actions,
+                int64_t rows, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

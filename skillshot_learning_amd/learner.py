@@ -269,6 +269,7 @@ class DDPG:
             self.target_actor.load_state_dict(self.model_actor.state_dict())
             self.target_critic.load_state_dict(self.model_critic.state_dict())
         self.replay = ReplayRing(replay_capacity, self.device) if replay_capacity else None
+        self._tq = None  # fused target-Q kernel (GPU), created at first use
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(seed * 7919 + rank_seed_offset + 17)
 
@@ -366,10 +367,7 @@ class DDPG:
         target = r
         if self.gamma > 0.0:
             with torch.no_grad():
-                actor_t = self.target_actor if self.tau is not None else self.model_actor
-                critic_t = self.target_critic if self.tau is not None else self.model_critic
-                critic_t.eval()
-                target = r + self.gamma * (1.0 - d) * critic_t(s2, actor_t(s2)).squeeze(-1)
+                target = r + self.gamma * (1.0 - d) * self.target_q(s2)
         lc = self.critic_step(s, a, target)
         la = self.model_actor_fit_step(s)
         if self.tau is not None:
@@ -377,10 +375,29 @@ class DDPG:
         return lc, la
 
     @torch.no_grad()
+    def target_q(self, s2):
+        """Q'(s', mu'(s')) with the target nets (the online nets when tau is
+        None).  On the GPU one fused MFMA launch (sk_target_q) on weights
+        packed after every change of the nets; on CPU the torch modules."""
+        actor_t = self.target_actor if self.tau is not None else self.model_actor
+        critic_t = self.target_critic if self.tau is not None else self.model_critic
+        if self.device.type != "cuda":
+            critic_t.eval()
+            return critic_t(s2, actor_t(s2)).squeeze(-1)
+        if self._tq is None:
+            from .critic_kernel import TargetQKernel
+            self._tq = TargetQKernel(actor_t, critic_t)
+        elif self.tau is None:
+            self._tq.refresh()  # online nets moved since the last call
+        return self._tq(s2)
+
+    @torch.no_grad()
     def soft_update(self):
         """target <- target + tau (online - target), one multi-tensor op per net."""
         for tgt, src in ((self.target_actor, self.model_actor), (self.target_critic, self.model_critic)):
             torch._foreach_lerp_(list(tgt.parameters()), list(src.parameters()), self.tau)
+        if self._tq is not None:
+            self._tq.refresh()
 
 
 class SkillshotLearner:
@@ -562,9 +579,13 @@ class SkillshotLearner:
 
     # ------------------------------------------------------------ persistence
     def state_dict(self):
-        return dict(actor=self.model_actor.state_dict(), critic=self.model_critic.state_dict(),
-                    actor_opt=self.ddpg.optimiser.state_dict(), critic_opt=self.ddpg.critic_optimiser.state_dict(),
-                    env=self.game_environment.state_dict())
+        d = dict(actor=self.model_actor.state_dict(), critic=self.model_critic.state_dict(),
+                 actor_opt=self.ddpg.optimiser.state_dict(), critic_opt=self.ddpg.critic_optimiser.state_dict(),
+                 env=self.game_environment.state_dict())
+        if self.ddpg.tau is not None:
+            d["target_actor"] = self.ddpg.target_actor.state_dict()
+            d["target_critic"] = self.ddpg.target_critic.state_dict()
+        return d
 
     def load_state_dict(self, d):
         self.model_actor.load_state_dict(d["actor"])
@@ -572,8 +593,13 @@ class SkillshotLearner:
         self.ddpg.optimiser.load_state_dict(d["actor_opt"])
         self.ddpg.critic_optimiser.load_state_dict(d["critic_opt"])
         self.game_environment.load_state_dict(d["env"])
+        if self.ddpg.tau is not None and "target_actor" in d:
+            self.ddpg.target_actor.load_state_dict(d["target_actor"])
+            self.ddpg.target_critic.load_state_dict(d["target_critic"])
         if self.actor_kernel is not None:
             self.actor_kernel.refresh()
+        if self.ddpg._tq is not None:
+            self.ddpg._tq.refresh()
 
 
 class TickGraph:
