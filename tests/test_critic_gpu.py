@@ -68,7 +68,8 @@ def test_critic_kernel_matches_torch(mods, rows):
         ref = c(s, act).squeeze(-1)
     err = (got - ref).abs()
     assert err.mean().item() < FP32_MEAN and err.max().item() < FP32_MAX, (err.mean().item(), err.max().item())
-    assert ref.std().item() > 0.05  # non-trivial Q values
+    if rows > 1:
+        assert ref.std().item() > 0.05  # non-trivial Q values
 
 
 @pytest.mark.parametrize("rows", [1, 257, 8192, 40000])
