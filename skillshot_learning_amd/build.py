@@ -12,7 +12,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB_DIR = os.path.join(HERE, "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libskillshot.so")
+# SK_LIB_PATH: load a prebuilt variant instead (A/B experiments, tools/gpu_lib_ab.sh)
+LIB_PATH = os.environ.get("SK_LIB_PATH") or os.path.join(LIB_DIR, "libskillshot.so")
 SOURCES = [os.path.join(HERE, "csrc", "sk_engine.hip"), os.path.join(HERE, "csrc", "sk_diag.hip"),
            os.path.join(HERE, "csrc", "sk_actor.hip"),
            os.path.join(HERE, "csrc", "sk_critic.hip")]
@@ -28,6 +29,8 @@ FLAGS = ["-O3", "--offload-arch=gfx950", "-fPIC", "-shared", "-std=c++17", "-ffp
 
 
 def needs_build():
+    if os.environ.get("SK_LIB_PATH"):
+        return False
     if not os.path.exists(LIB_PATH):
         return True
     t = os.path.getmtime(LIB_PATH)

@@ -50,13 +50,26 @@ struct Env {
   int qvalid[2], live, winner;
 };
 
-__device__ __forceinline__ void load_env(const View& v, int64_t i, Env& e) {
-  int4 p = v.pos[i];
-  double2 r = v.rot[i];
-  int4 q = v.qpos[i];
-  double2 qr = v.qrot[i];
-  int4 ca = v.qcdage[i];
-  int2 m = v.misc[i];
+struct EnvRaw {  // one env's six planes as loaded (decode with decode_env)
+  int4 p;
+  double2 r;
+  int4 q;
+  double2 qr;
+  int4 ca;
+  int2 m;
+};
+
+__device__ __forceinline__ EnvRaw load_env_raw(const View& v, int64_t i) {
+  return EnvRaw{v.pos[i], v.rot[i], v.qpos[i], v.qrot[i], v.qcdage[i], v.misc[i]};
+}
+
+__device__ __forceinline__ void decode_env(const EnvRaw& w, Env& e) {
+  const int4 p = w.p;
+  const double2 r = w.r;
+  const int4 q = w.q;
+  const double2 qr = w.qr;
+  const int4 ca = w.ca;
+  const int2 m = w.m;
   e.px[0] = p.x; e.py[0] = p.y; e.px[1] = p.z; e.py[1] = p.w;
   e.rot[0] = r.x; e.rot[1] = r.y;
   e.qx[0] = q.x; e.qy[0] = q.y; e.qx[1] = q.z; e.qy[1] = q.w;
@@ -66,6 +79,83 @@ __device__ __forceinline__ void load_env(const View& v, int64_t i, Env& e) {
   unsigned f = (unsigned)m.y;
   e.qvalid[0] = f & 0xff; e.qvalid[1] = (f >> 8) & 0xff;
   e.live = (f >> 16) & 0xff; e.winner = (f >> 24) & 0xff;
+}
+
+__device__ __forceinline__ void load_env(const View& v, int64_t i, Env& e) { decode_env(load_env_raw(v, i), e); }
+
+// The fused step's load phase with the issue order and the waits pinned.
+// Issue order: rot, qrot, qcdage, misc, pos, qpos, both action words — back
+// to back.  The caller then works through the data in
+// arrival order: the players' fp32 sincos once the rotations are in
+// (wait_rot), the projectiles' once theirs are (wait_qrot), the decode with
+// the rest of the state (wait_state), the tick with the actions (streamed
+// from HBM; the state sits in the Infinity Cache) (wait_actions).  Vector
+// loads return in
+// issue order on gfx9, so vmcnt(k) = "all but the last k issued".  The
+// loads are inline asm because the compiler hoisted decode arithmetic (and
+// its vmcnt waits) in front of the action loads.  Each wait takes the
+// registers it releases as "+v" operands (no use can be scheduled before
+// it) together with the results computed since the previous wait (so that
+// work cannot sink below it).
+typedef int skv4i __attribute__((ext_vector_type(4)));
+typedef int skv2i __attribute__((ext_vector_type(2)));
+typedef double skv2d __attribute__((ext_vector_type(2)));
+typedef float skv2f __attribute__((ext_vector_type(2)));
+
+struct StepLoads {  // native vector types: inline asm cannot bind HIP's struct vectors
+  skv2d r, qr;
+  skv4i p, q, ca;
+  skv2i m;
+  skv2f a0, a1;
+};
+
+__device__ __forceinline__ void issue_step_loads(const View& v, const float2* act, int64_t n, int64_t i,
+                                                 StepLoads& L) {
+  skv2d r, qr;
+  skv4i p, q, ca;
+  skv2i m;
+  skv2f a0, a1;
+  asm volatile(
+      "global_load_dwordx4 %0, %8, off\n\t"
+      "global_load_dwordx4 %1, %9, off\n\t"
+      "global_load_dwordx4 %2, %10, off\n\t"
+      "global_load_dwordx2 %3, %11, off\n\t"
+      "global_load_dwordx4 %4, %12, off\n\t"
+      "global_load_dwordx4 %5, %13, off\n\t"
+      "global_load_dwordx2 %6, %14, off\n\t"
+      "global_load_dwordx2 %7, %15, off"
+      : "=&v"(r), "=&v"(qr), "=&v"(ca), "=&v"(m), "=&v"(p), "=&v"(q), "=&v"(a0), "=&v"(a1)
+      : "v"(v.rot + i), "v"(v.qrot + i), "v"(v.qcdage + i), "v"(v.misc + i), "v"(v.pos + i), "v"(v.qpos + i),
+        "v"(act + i), "v"(act + n + i)
+      : "memory");
+  L.r = r; L.qr = qr; L.ca = ca; L.m = m; L.p = p; L.q = q; L.a0 = a0; L.a1 = a1;
+}
+__device__ __forceinline__ void wait_rot(StepLoads& L) {
+  skv2d r = L.r;
+  asm volatile("s_waitcnt vmcnt(7)" : "+v"(r));
+  L.r = r;
+}
+__device__ __forceinline__ void wait_qrot(StepLoads& L, sktrig::SinCosF& m0, sktrig::SinCosF& m1) {
+  skv2d qr = L.qr;
+  asm volatile("s_waitcnt vmcnt(6)" : "+v"(qr), "+v"(m0.s), "+v"(m0.c), "+v"(m1.s), "+v"(m1.c));
+  L.qr = qr;
+}
+__device__ __forceinline__ void wait_state(StepLoads& L, sktrig::SinCosF& t0, sktrig::SinCosF& t1) {
+  skv4i p = L.p, q = L.q, ca = L.ca;
+  skv2i m = L.m;
+  asm volatile("s_waitcnt vmcnt(2)" : "+v"(p), "+v"(q), "+v"(ca), "+v"(m), "+v"(t0.s), "+v"(t0.c), "+v"(t1.s),
+               "+v"(t1.c));
+  L.p = p; L.q = q; L.ca = ca; L.m = m;
+}
+__device__ __forceinline__ void wait_actions(StepLoads& L) {
+  skv2f a0 = L.a0, a1 = L.a1;
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(a0), "+v"(a1));
+  L.a0 = a0; L.a1 = a1;
+}
+__device__ __forceinline__ EnvRaw step_loads_env(const StepLoads& L) {
+  return EnvRaw{make_int4(L.p.x, L.p.y, L.p.z, L.p.w), make_double2(L.r.x, L.r.y),
+                make_int4(L.q.x, L.q.y, L.q.z, L.q.w), make_double2(L.qr.x, L.qr.y),
+                make_int4(L.ca.x, L.ca.y, L.ca.z, L.ca.w), make_int2(L.m.x, L.m.y)};
 }
 
 __device__ __forceinline__ void store_env(const View& v, int64_t i, const Env& e) {
@@ -334,6 +424,106 @@ __device__ __forceinline__ void tick_env(const Cfg& c, Env& e, double a0_move, d
   const sktrig::SinCos m0 = sktrig::sincos_bf(e.rot[0], &k0);
   const sktrig::SinCos m1 = sktrig::sincos_bf(e.rot[1], &k1);
   tick_env_m(c, e, m0, m1, k0 & k1, a0_move, a0_look, a1_move, a1_look);
+}
+
+// ---------------------------------------------------------------- fast tick
+// The same tick with fp32 trig (sktrig::sincos_fast / sincos_add).  Every
+// position the tick writes is int(round(p - d)) with d = sin/cos * speed
+// (Player.py:63-64, Projectile.py:40-41); the fp32 d decides that rounding
+// exactly whenever it is farther than its error bound from a half-integer
+// (sktrig::round_safe).  A lane where any of its (up to) eight deltas is
+// within the bound, or whose rotation is out of the fast range / non-finite,
+// or whose action is NaN, redoes the whole tick with tick_env (the fp64
+// path above) from the untouched state: same result bit for bit, at a rate
+// of ~1e-5 per delta (one wave in a few hundred takes the fp64 branch).
+//
+// Inputs: m_p = sincos of player p's rotation (its move direction,
+// Player.py:63-64), tq_p = sincos of its projectile's STORED rotation, okm /
+// okq = those four were in the fast range.  A projectile fired this tick
+// flies with the player's post-look rotation rot + a*look (Player.py:33-39,
+// :80-84), whose sincos is the angle addition of m_p and the look step; so
+// all four reductions depend on state alone and the caller can run them
+// while the actions are still in flight.
+//
+// Error budget of a delta fl(fl(s_f * k) * a), |a| <= 1, k = speed:
+//   move: k*SKT_FAST_ERR + 2*k*2^-24 <= 4.2e-7*k, threshold 1e-6*k;
+//   projectile: k*SKT_ADD_ERR + k*2^-24 <= 6.6e-7*k, threshold 2e-6*k
+// (the fp64 reference value itself is within ~1e-13 of the real one).
+__device__ __forceinline__ float clamp_action_f(float a) {  // Player.py:36-37, :60-61
+  a = (a >= 1.0f) ? 1.0f : a;
+  a = (a <= -1.0f) ? -1.0f : a;
+  return a;
+}
+
+__device__ __forceinline__ void tick_env_fast(const Cfg& c, Env& e, sktrig::SinCosF m0, sktrig::SinCosF m1,
+                                              sktrig::SinCosF tq0, sktrig::SinCosF tq1, bool okm, bool okq0,
+                                              bool okq1, float a0_move, float a0_look, float a1_move,
+                                              float a1_look) {
+  using sktrig::round_safe;
+  const float l0 = clamp_action_f(a0_look), l1 = clamp_action_f(a1_look);
+  const double rn0 = e.rot[0] + (double)l0 * c.look;  // == move_look_s
+  const double rn1 = e.rot[1] + (double)l1 * c.look;
+  const bool f0 = e.qcd[0] <= 0, f1 = e.qcd[1] <= 0;  // fires this tick (Player.py:80)
+  const float lk = (float)c.look;
+  const sktrig::SinCosF t0 = f0 ? sktrig::sincos_add(m0, l0 * lk) : tq0;
+  const sktrig::SinCosF t1 = f1 ? sktrig::sincos_add(m1, l1 * lk) : tq1;
+  const float sp = (float)c.pspeed, qs = (float)c.qspeed;
+  const float em = 1e-6f * sp, eq = 2e-6f * qs;
+  const float s0 = clamp_action_f(a0_move), s1 = clamp_action_f(a1_move);
+  const float dx0 = (m0.s * sp) * s0, dy0 = (m0.c * sp) * s0;
+  const float dx1 = (m1.s * sp) * s1, dy1 = (m1.c * sp) * s1;
+  const float ex0 = t0.s * qs, ey0 = t0.c * qs;
+  const float ex1 = t1.s * qs, ey1 = t1.c * qs;
+  const bool v0 = (e.qvalid[0] != 0) || f0, v1 = (e.qvalid[1] != 0) || f1;  // valid after shoot
+  const int safe = (int)okm & ((int)f0 | (int)okq0) & ((int)f1 | (int)okq1) & (int)round_safe(dx0, em) &
+                   (int)round_safe(dy0, em) & (int)round_safe(dx1, em) & (int)round_safe(dy1, em) &
+                   ((int)!v0 | ((int)round_safe(ex0, eq) & (int)round_safe(ey0, eq))) &
+                   ((int)!v1 | ((int)round_safe(ex1, eq) & (int)round_safe(ey1, eq)));
+  if (__builtin_expect(!safe, 0)) {  // laid out after the hot path
+    tick_env(c, e, (double)a0_move, (double)a0_look, (double)a1_move, (double)a1_look);
+    return;
+  }
+  // do_actions(1, ...), do_actions(2, ...)  SkillshotLearner.py:206-213
+  {
+    const int nx = e.px[0] - (int)rintf(dx0), ny = e.py[0] - (int)rintf(dy0);
+    if (player_pos_valid(c, nx, ny)) { e.px[0] = nx; e.py[0] = ny; }
+  }
+  e.rot[0] = rn0;
+  shoot(c, e, 0);
+  {
+    const int nx = e.px[1] - (int)rintf(dx1), ny = e.py[1] - (int)rintf(dy1);
+    if (player_pos_valid(c, nx, ny)) { e.px[1] = nx; e.py[1] = ny; }
+  }
+  e.rot[1] = rn1;
+  shoot(c, e, 1);
+  // game_tick  SkillshotGame.py:115-122 (Projectile.py:38-53)
+  if (e.live) {
+    e.ticks += 1;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      if (e.qvalid[p]) {
+        const float ex = p ? ex1 : ex0, ey = p ? ey1 : ey0;
+        const int nx = e.qx[p] - (int)rintf(ex), ny = e.qy[p] - (int)rintf(ey);
+        bool ok = (nx + c.qsize <= c.W) & (nx >= 0) & (ny + c.qsize <= c.H) & (ny >= 0);
+        if (ok) { e.qx[p] = nx; e.qy[p] = ny; } else { e.qvalid[p] = 0; }
+      }
+      e.qcd[p] -= 1;
+      e.qage[p] += 1;
+    }
+    collide_s(c, e.px[0], e.py[0], e.qx[0], e.qy[0], e.qvalid[0], e.px[1], e.py[1], e.qx[1], e.qy[1],
+              e.qvalid[1], e.live, e.winner);
+  }
+}
+
+// the fast tick from the state alone (all four reductions inline)
+__device__ __forceinline__ void tick_env_fast(const Cfg& c, Env& e, float a0_move, float a0_look, float a1_move,
+                                              float a1_look) {
+  bool k0, k1, k2, k3;
+  const sktrig::SinCosF m0 = sktrig::sincos_fast(e.rot[0], &k0);
+  const sktrig::SinCosF m1 = sktrig::sincos_fast(e.rot[1], &k1);
+  const sktrig::SinCosF tq0 = sktrig::sincos_fast(e.qrot[0], &k2);
+  const sktrig::SinCosF tq1 = sktrig::sincos_fast(e.qrot[1], &k3);
+  tick_env_fast(c, e, m0, m1, tq0, tq1, k0 & k1, k2, k3, a0_move, a0_look, a1_move, a1_look);
 }
 
 // ---------------------------------------------------------------- features

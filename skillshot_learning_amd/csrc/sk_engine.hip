@@ -40,7 +40,10 @@ struct sk_env {
   // slots[1-parity] = value + advance, then the host flips parity.
   uint64_t* d_step;
   int parity;
-  int step_variant;  // 0 = one lane per env, 1 = player-split (SK_STEP_VARIANT)
+  // fused-step kernel: 0 = k_step (one lane per env, fp64 trig), 1 = k_step_split
+  // (player per lane), 2 = k_step_fast (fp32 trig + exact fallback); -1 = auto
+  // (SK_STEP_VARIANT overrides)
+  int step_variant;
 };
 
 static thread_local std::string g_err;
@@ -58,6 +61,7 @@ static int fail(int code, const std::string& msg) {
   } while (0)
 
 static constexpr int kBlock = 256;
+static constexpr int64_t kFastStepMinEnvs = 196608;
 static constexpr size_t kAuxBytes = 256 + SK_COUNTER_SLOTS * sizeof(sk_counters);
 
 static inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
@@ -185,6 +189,74 @@ __global__ void __launch_bounds__(kBlock) k_step(StepArgs a, Cfg c) {
   if (!in) return;
   if (d && a.auto_reset) {
     if (a.random_positions) reset_random(c, e, a.seed, (uint64_t)(a.env_offset + i), step);
+    else reset_fixed(c, e);
+  }
+  if (a.obs_reset) {
+    float o0[12], o1[12];
+    double pd0, pd1;
+    obs_env(c, e, o0, o1, &pd0, &pd1);
+    store_obs(a.obs_reset, a.n, 0, i, o0);
+    store_obs(a.obs_reset, a.n, 1, i, o1);
+  }
+  store_env(a.v, i, e);
+}
+
+// Fused step, fp32-trig variant (SK_STEP_VARIANT=2; the default from 196,608
+// games): the same tick through tick_env_fast (exact by construction: fp32
+// deltas decide the rounding unless within their error bound of a tie, then
+// the lane redoes the tick in fp64), with the loads issued by inline asm in
+// arrival order (issue_step_loads).  ~35 % fewer VALU instructions; faster
+// where several waves share a SIMD (8.9 vs 9.4 us per launch at 262,144
+// games), slower than k_step at one wave per SIMD (65,536 games: 5.3 vs 4.7
+// us), where the per-wave dependency chain, not issue, sets the time
+// (profiles/r01g_step_variants.jsonl).
+__global__ void __launch_bounds__(kBlock) k_step_fast(StepArgs a, Cfg c) {
+  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  bool in = i < a.n;
+  // every load issued back to back before anything else touches memory,
+  // then the tick works through the data in arrival order
+  // (issue_step_loads: rotations -> players' sincos, projectile rotations ->
+  // theirs, rest of the state -> decode, actions -> the tick)
+  StepLoads L;
+  if (in) issue_step_loads(a.v, a.actions, a.n, i, L);
+  bool d = false;
+  Env e;
+  if (in) {
+    wait_rot(L);
+    bool k0, k1, k2, k3;
+    sktrig::SinCosF m0 = sktrig::sincos_fast(L.r.x, &k0);
+    sktrig::SinCosF m1 = sktrig::sincos_fast(L.r.y, &k1);
+    wait_qrot(L, m0, m1);
+    sktrig::SinCosF tq0 = sktrig::sincos_fast(L.qr.x, &k2);
+    sktrig::SinCosF tq1 = sktrig::sincos_fast(L.qr.y, &k3);
+    wait_state(L, tq0, tq1);
+    decode_env(step_loads_env(L), e);
+    wait_actions(L);
+    tick_env_fast(c, e, m0, m1, tq0, tq1, k0 & k1, k2, k3, L.a0.x, L.a0.y, L.a1.x, L.a1.y);
+    if (a.obs || a.reward) {
+      float o0[12], o1[12];
+      double pd0, pd1;
+      obs_env(c, e, o0, o1, &pd0, &pd1);
+      if (a.obs) {
+        store_obs(a.obs, a.n, 0, i, o0);
+        store_obs(a.obs, a.n, 1, i, o1);
+      }
+      if (a.reward) {
+        a.reward[i] = reward_of(c, e, 0, a.reward_kind, pd0);
+        a.reward[a.n + i] = reward_of(c, e, 1, a.reward_kind, pd1);
+      }
+    }
+    d = (!e.live) || (e.ticks >= a.tick_limit);  // SkillshotLearner.py:302
+    if (a.done) a.done[i] = (uint8_t)d;
+    if (a.winner) a.winner[i] = (uint8_t)e.winner;
+  }
+  if (a.ctr) wave_count(a.ctr, d, in ? e.winner : 0, in ? e.ticks : 0);
+  if (!in) return;
+  // the RNG step slot is read only by the waves that need it (all lanes
+  // reading one line every launch made that line's L2 channel a hot spot)
+  if (blockIdx.x == 0 && threadIdx.x == 0) step_advance(a.step, step_read(a.step), 1);
+  if (d && a.auto_reset) {
+    if (a.random_positions) reset_random(c, e, a.seed, (uint64_t)(a.env_offset + i), step_read(a.step));
     else reset_fixed(c, e);
   }
   if (a.obs_reset) {
@@ -336,8 +408,7 @@ __global__ void __launch_bounds__(kBlock) k_rollout_random(RolloutArgs a, Cfg c)
     for (int t = 0; t < a.n_ticks; ++t) {
       uint64_t step = step0 + (uint64_t)t;
       U4 u = draw4(a.seed, genv, step, 0u);
-      tick_env(c, e, (double)u32_to_action(u.x), (double)u32_to_action(u.y), (double)u32_to_action(u.z),
-               (double)u32_to_action(u.w));
+      tick_env_fast(c, e, u32_to_action(u.x), u32_to_action(u.y), u32_to_action(u.z), u32_to_action(u.w));
       if ((!e.live) || (e.ticks >= a.tick_limit)) {
         dones += 1;
         w1 += (e.winner == 1);
@@ -576,7 +647,7 @@ static int make_env(sk_env** out, const sk_state_view* view, int32_t n, int64_t 
   if ((rc = validate_cfg(e->cfg))) { delete e; return rc; }
   e->dcfg = to_dcfg(e->cfg);
   e->parity = 0;
-  e->step_variant = 0;
+  e->step_variant = -1;
   if (const char* sv = std::getenv("SK_STEP_VARIANT")) e->step_variant = std::atoi(sv);
   if (view) {
     if (view->n_envs != n || !view->pos || !view->rot || !view->qpos || !view->qrot || !view->qcdage ||
@@ -829,8 +900,13 @@ int sk_env_step(sk_env* e, const float* actions, float* obs, float* reward, int3
   a.env_offset = e->env_offset;
   a.step = StepRef{e->d_step, e->parity};
   a.ctr = e->d_counters;
-  if (e->step_variant == 1)
+  // auto: k_step_fast once several waves share a SIMD (>= 2 per SIMD on 256
+  // CUs), k_step below (profiles/r01g_step_variants.jsonl)
+  const int variant = e->step_variant >= 0 ? e->step_variant : (e->n >= kFastStepMinEnvs ? 2 : 0);
+  if (variant == 1)
     k_step_split<<<grid_for(2 * (int64_t)e->n), kBlock, 0, (hipStream_t)stream>>>(a, e->dcfg);
+  else if (variant == 2)
+    k_step_fast<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(a, e->dcfg);
   else
     k_step<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(a, e->dcfg);
   SK_LAUNCH_CHECK();

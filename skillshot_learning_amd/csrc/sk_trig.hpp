@@ -95,3 +95,80 @@ SKT_HD SinCos sincos_bf(double x, bool* ok) {
 }
 
 }  // namespace sktrig
+
+namespace sktrig {
+
+// ---------------------------------------------------------------- fast path
+// The step only needs int(round(p - sin(r)*k)) for small k (3 or 5), so the
+// sin/cos values themselves never reach the state: an fp32 sin/cos of the
+// fp64-reduced argument decides the rounding whenever the fp32 delta is
+// farther than its error bound from a half-integer; the rare lanes within
+// the bound redo the move with the fp64 sincos_bf above (callers do that).
+//
+// Reduction: fn = rint(x*2/pi); y = (x - fn*pio2_1) - fn*pio2_2 in fp64 (both
+// products exact for |fn| < 2^20; the dropped tail fn*(pi/2 - pio2_1 -
+// pio2_2) is below 2.1e-21*2^20 = 2.2e-15).  Then y -> fp32 (|err| <= 4.7e-8
+// on |y| <= pi/4) and the Cephes sinf/cosf minimax polynomials in fp32 FMAs.
+// SKT_FAST_ERR bounds |sin_f - sin(x)| and |cos_f - cos(x)| for every x with
+// ok = true; tests/trig_check.cpp measures the maximum against long-double
+// sinl/cosl (about 1.3e-7) and checks it stays below half this bound.
+#define SKT_FAST_ERR 3.0e-7f
+
+struct SinCosF {
+  float s, c;
+};
+
+// Cephes sinf / cosf minimax polynomials on [-pi/4, pi/4] (fp32 FMAs)
+SKT_HD SinCosF sincos_poly(float yf) {
+  const float z = yf * yf;
+  const float ps = fmaf(fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f);
+  const float pc = fmaf(fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z, 4.166664568298827e-2f);
+  SinCosF o;
+  o.s = fmaf(yf * z, ps, yf);
+  o.c = fmaf(z * z, pc, fmaf(-0.5f, z, 1.0f));
+  return o;
+}
+
+SKT_HD SinCosF sincos_fast(double x, bool* ok) {
+  const double invpio2 = 6.36619772367581382433e-01;
+  const double pio2_1 = 1.57079632673412561417e+00;  // sincos_bf's constants
+  const double pio2_2 = 6.07710050630396597660e-11;
+  *ok = fabs(x) < 1647099.3291652855;  // false for NaN / inf too
+  const double fn = rint(x * invpio2);
+  const double y = (x - fn * pio2_1) - fn * pio2_2;
+  const SinCosF k = sincos_poly((float)y);
+  const int n = (int)(*ok ? fn : 0.0) & 3;  // |fn| < 2^20 when ok
+  SinCosF o;
+  o.s = (n & 1) ? k.c : k.s;
+  o.c = (n & 1) ? k.s : k.c;
+  if (n == 1 || n == 2) o.c = -o.c;
+  if (n >= 2) o.s = -o.s;
+  return o;
+}
+
+// sin/cos of r + d from fp32 sin/cos of r (|error| <= SKT_FAST_ERR) and a
+// small exact fp32 d (|d| <= pi/4): the angle-addition formulas.  The fast
+// tick uses it for a projectile fired this tick, whose rotation is the
+// player's rotation plus the look action times 0.25 (Player.py:33-39; the
+// fp64 sum's own rounding, <= 3e-14 at |r| <= 500, is far below the bound).
+// |error| <= 1.25*SKT_FAST_ERR + 2e-7 =: SKT_ADD_ERR (tests/trig_check.cpp
+// measures the maximum against sinl/cosl and checks it stays below half).
+#define SKT_ADD_ERR 6.0e-7f
+
+SKT_HD SinCosF sincos_add(SinCosF r, float d) {
+  const SinCosF k = sincos_poly(d);
+  SinCosF o;
+  o.s = fmaf(r.s, k.c, r.c * k.s);
+  o.c = fmaf(r.c, k.c, -(r.s * k.s));
+  return o;
+}
+
+// true iff d is provably not within `eps` of a half-integer, so that
+// rint(p - d_exact) == p - rintf(d) for every integer p and every d_exact with
+// |d_exact - d| <= eps (false for NaN / inf: the caller takes the exact path)
+SKT_HD bool round_safe(float d, float eps) {
+  const float t = d - floorf(d);  // exact for |d| < 2^23
+  return fabsf(t - 0.5f) > eps;
+}
+
+}  // namespace sktrig

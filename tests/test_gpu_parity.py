@@ -67,9 +67,9 @@ class GpuEngine:
         return o.cpu().numpy(), r.cpu().numpy()
 
 
-@pytest.fixture(params=[0, 1], ids=["lane_per_env", "player_split"])
+@pytest.fixture(params=[0, 1, 2], ids=["lane_per_env", "player_split", "fp32_fast"])
 def step_variant(request, monkeypatch):
-    """Both fused-step kernels (k_step, k_step_split) must meet the same bar."""
+    """Every fused-step kernel (k_step, k_step_split, k_step_fast) must meet the same bar."""
     monkeypatch.setenv("SK_STEP_VARIANT", str(request.param))
     return request.param
 
