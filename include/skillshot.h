@@ -256,6 +256,49 @@ int sk_critic_forward(const void* packed, const float* obs, const float* actions
 int sk_target_q(const void* actor_packed, const void* critic_packed, const float* obs, float* q, float* actions,
                 int64_t rows, void* stream);
 
+/* --- the DDPG update (A16, F1) ------------------------------------------- */
+
+/* One replay update as three launches per net instead of the ~100 small
+ * kernels of autograd + optimiser (DDPG.critic_step / model_actor_fit_step /
+ * soft_update, the rule of SkillshotLearner.py:386-443):
+ *   sk_grad_pack    torch Linear fp32 weights of one net (W2 [128][ld2]:
+ *                   ld2 = 258 critic, 256 actor; W3 [n_out][128]) -> a device
+ *                   buffer of sk_grad_packed_bytes() bytes (16-byte aligned)
+ *   sk_critic_grad  critic forward in training mode (Dropout(0.2) masks from
+ *                   Philox keyed by (seed, *call_counter, row, unit)), loss
+ *                   sum_b (q_b - y_b)^2 * grad_scale / 2 (grad_scale = 2/B is
+ *                   F.mse_loss), backward: per-workgroup gradient partials
+ *                   float[sk_update_partials(batch)][36,609] in torch
+ *                   parameters() order; loss_sum (nullable, device float,
+ *                   accumulated) += sum (q - y)^2; dropout_mask (nullable)
+ *                   receives uint8[batch][256] keep flags (tests)
+ *   sk_actor_grad   actor forward, critic forward at inference, backward of
+ *                   -loss_scale * sum_b Q(s_b, mu(s_b)) to the actor:
+ *                   partials float[sk_update_partials(batch)][36,482];
+ *                   q_sum (nullable) += sum_b Q
+ *   sk_adam_flat    g = grad_in (nullable) + sum of n_partials partials ->
+ *                   grad_out (nullable); if apply: torch.optim.Adam (fused
+ *                   formulation) on flat param / exp_avg / exp_avg_sq with
+ *                   the step count *step_counter (advanced by the grad
+ *                   kernels: step_counters[0 .. n_steps) += 1), then
+ *                   target (nullable) += tau (param - target).
+ * MFMA with bf16 operands and fp32 accumulation; batch-major rows; obs
+ * float[batch][12], actions float[batch][2], targets float[batch]. */
+size_t sk_grad_packed_bytes(void);
+int64_t sk_update_partials(int64_t batch);
+int sk_grad_pack(const float* W1, const float* b1, const float* W2, int32_t ld2, const float* b2, const float* W3,
+                 const float* b3, int32_t n_out, void* packed, void* stream);
+int sk_critic_grad(const void* critic_gpack, const float* obs, const float* actions, const float* targets,
+                   int64_t batch, float grad_scale, uint64_t seed, const int64_t* call_counter, float* partials,
+                   float* step_counters, int32_t n_steps, float* loss_sum, uint8_t* dropout_mask, void* stream);
+int sk_actor_grad(const void* actor_gpack, const void* critic_gpack, const float* obs, int64_t batch,
+                  float loss_scale, float* partials, float* step_counters, int32_t n_steps, float* q_sum,
+                  void* stream);
+int sk_adam_flat(const float* partials, int32_t n_partials, int32_t n_params, const float* grad_in,
+                 float* grad_out, int32_t apply, float* param, float* exp_avg, float* exp_avg_sq,
+                 const float* step_counter, float lr, float beta1, float beta2, float eps, float* target, float tau,
+                 void* stream);
+
 #ifdef __cplusplus
 }
 #endif

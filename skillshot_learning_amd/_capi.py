@@ -28,6 +28,7 @@ EXPORTS = (
     "sk_env_step", "sk_gen_random_actions", "sk_env_rollout_random",
     "sk_actor_packed_bytes", "sk_actor_pack", "sk_actor_forward", "sk_actor_forward_dev",
     "sk_critic_packed_bytes", "sk_critic_pack", "sk_critic_forward", "sk_target_q",
+    "sk_grad_packed_bytes", "sk_update_partials", "sk_grad_pack", "sk_critic_grad", "sk_actor_grad", "sk_adam_flat",
 )
 
 
@@ -75,6 +76,7 @@ def load(build_if_missing=True):
         raise SkillshotError(f"libskillshot not built ({path}); run python -m skillshot_learning_amd.build")
     L = ctypes.CDLL(path)
     P, i32, i64, u64, f64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double
+    f32 = ctypes.c_float
     PP = ctypes.POINTER(ctypes.c_void_p)
     sig = {
         "sk_last_error": ([], ctypes.c_char_p),
@@ -111,6 +113,12 @@ def load(build_if_missing=True):
         "sk_critic_pack": ([P, P, P, P, P, P, P, P], ctypes.c_int),
         "sk_critic_forward": ([P, P, P, P, i64, P], ctypes.c_int),
         "sk_target_q": ([P, P, P, P, P, i64, P], ctypes.c_int),
+        "sk_grad_packed_bytes": ([], ctypes.c_size_t),
+        "sk_update_partials": ([i64], ctypes.c_int64),
+        "sk_grad_pack": ([P, P, P, i32, P, P, P, i32, P, P], ctypes.c_int),
+        "sk_critic_grad": ([P, P, P, P, i64, f32, u64, P, P, P, i32, P, P, P], ctypes.c_int),
+        "sk_actor_grad": ([P, P, P, i64, f32, P, P, i32, P, P], ctypes.c_int),
+        "sk_adam_flat": ([P, i32, i32, P, P, i32, P, P, P, P, f32, f32, f32, f32, P, f32, P], ctypes.c_int),
     }
     for name, (argt, rest) in sig.items():
         fn = getattr(L, name)

@@ -25,6 +25,7 @@ all-reduced (RCCL over xGMI; gloo on CPU) as one flat bucket per update, and
 each rank's sampled minibatch all-gathered into a shared batch.
 """
 import math
+import os
 
 import torch
 import torch.distributed as dist
@@ -251,7 +252,7 @@ class DDPG:
     and gloo multi-process tests drive it without a GPU)."""
 
     def __init__(self, device="cpu", seed=0, batch_size=16, gamma=0.0, tau=None, replay_capacity=0,
-                 process_group=None, rank_seed_offset=0):
+                 process_group=None, rank_seed_offset=0, fused_update=None):
         self.device = torch.device(device)
         torch.manual_seed(seed)
         self.model_actor = Actor().to(self.device)
@@ -272,6 +273,14 @@ class DDPG:
         self._tq = None  # fused target-Q kernel (GPU), created at first use
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(seed * 7919 + rank_seed_offset + 17)
+        # the update on MFMA kernels (update_kernel.FusedUpdate) on the GPU;
+        # SK_FUSED_UPDATE=0 / fused_update=False keeps the autograd path
+        if fused_update is None:
+            fused_update = self.device.type == "cuda" and os.environ.get("SK_FUSED_UPDATE", "1") != "0"
+        self._fused = None
+        if fused_update:
+            from .update_kernel import FusedUpdate
+            self._fused = FusedUpdate(self, seed=seed * 1000033 + rank_seed_offset + 5)
 
     # ------------------------------------------------------------ distributed
     def world(self):
@@ -317,6 +326,8 @@ class DDPG:
 
     # ------------------------------------------------------------ updates
     def critic_step(self, s, a, target):
+        if self._fused is not None:  # one MFMA gradient launch + one Adam launch
+            return self._fused.critic_step(s, a, target)
         self.model_critic.train()  # Dropout active, as in critic.fit (:434)
         q = self.model_critic(s, a).squeeze(-1)
         loss = F.mse_loss(q, target)
@@ -329,6 +340,8 @@ class DDPG:
     def model_actor_fit_step(self, s):
         """model_actor_fit_step (:386-417): actor grads with output_gradients =
         -dQ/da, i.e. descent on -sum_batch Q(s, mu(s)); critic in inference mode."""
+        if self._fused is not None:
+            return self._fused.actor_step(s)
         self.model_critic.eval()
         for p in self.model_critic.parameters():
             p.requires_grad_(False)
@@ -371,7 +384,11 @@ class DDPG:
         lc = self.critic_step(s, a, target)
         la = self.model_actor_fit_step(s)
         if self.tau is not None:
-            self.soft_update()
+            if self._fused is not None:  # the Adam kernels already moved the targets
+                if self._tq is not None:
+                    self._tq.refresh()
+            else:
+                self.soft_update()
         return lc, la
 
     @torch.no_grad()

@@ -1,0 +1,205 @@
+"""The DDPG update on MFMA (csrc/sk_update.hip) bound to the torch nets of a
+`learner.DDPG`.
+
+Per update and net: one gradient launch (forward + backward over the whole
+minibatch, per-workgroup weight-gradient partials) and one Adam launch (sum
+of the partials, torch Adam, soft target update); the weight packs the
+gradient kernels read are refreshed after each step.  This replaces the
+~100 small torch kernels of `DDPG.critic_step` / `model_actor_fit_step` /
+`soft_update` (SkillshotLearner.py:386-443 rule).
+
+The torch modules stay the model: their parameters are rebound as views of
+one flat fp32 buffer per net (`.data` swap, so optimiser and state-dict
+references stay valid), and the torch Adam state (`exp_avg`, `exp_avg_sq`,
+`step`) is rebound as views of flat buffers too, so the kernel path and the
+torch path step the same numbers and `state_dict()` sees the kernel's Adam
+moments.  Multi-rank: the gradient is written flat, all-reduced (mean) over
+RCCL, then applied (two Adam launches).
+"""
+import ctypes
+
+import torch
+import torch.distributed as dist
+
+from . import _capi
+from ._capi import SkillshotError
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def flatten_module(module):
+    """Rebind every parameter of `module` as a view of one flat fp32 buffer
+    (idempotent); returns the buffer."""
+    flat = getattr(module, "_sk_flat", None)
+    params = list(module.parameters())
+    if flat is not None and all(p.data.data_ptr() == flat[o:o + p.numel()].data_ptr()
+                                for p, o in zip(params, _offsets(params))):
+        return flat
+    n = sum(p.numel() for p in params)
+    flat = torch.empty(n, dtype=torch.float32, device=params[0].device)
+    off = 0
+    for p in params:
+        k = p.numel()
+        flat[off:off + k].copy_(p.data.reshape(-1))
+        p.data = flat[off:off + k].view_as(p)
+        off += k
+    module._sk_flat = flat
+    return flat
+
+
+def _offsets(params):
+    out, off = [], 0
+    for p in params:
+        out.append(off)
+        off += p.numel()
+    return out
+
+
+class _AdamState:
+    """torch Adam state of one net as flat buffers (views rebound into the
+    optimiser's per-parameter state)."""
+
+    def __init__(self, opt, module, flat):
+        params = list(module.parameters())
+        dev = flat.device
+        self.m = torch.zeros_like(flat)
+        self.v = torch.zeros_like(flat)
+        self.steps = torch.zeros(len(params), dtype=torch.float32, device=dev)
+        g = opt.param_groups[0]
+        self.lr, (self.b1, self.b2), self.eps = float(g["lr"]), g["betas"], float(g["eps"])
+        for i, (p, off) in enumerate(zip(params, _offsets(params))):
+            k = p.numel()
+            st = opt.state[p]
+            if "exp_avg" in st:
+                self.m[off:off + k].copy_(st["exp_avg"].reshape(-1))
+                self.v[off:off + k].copy_(st["exp_avg_sq"].reshape(-1))
+                self.steps[i].copy_(torch.as_tensor(st["step"], dtype=torch.float32))
+            st["exp_avg"] = self.m[off:off + k].view_as(p)
+            st["exp_avg_sq"] = self.v[off:off + k].view_as(p)
+            st["step"] = self.steps[i]
+
+
+class FusedUpdate:
+    """Kernel path of DDPG.critic_step / model_actor_fit_step (+ soft update)."""
+
+    def __init__(self, ddpg, seed=0):
+        self.d = ddpg
+        self.L = _capi.load()
+        dev = ddpg.device
+        if dev.type != "cuda":
+            raise SkillshotError("FusedUpdate needs the nets on a gfx950 GPU")
+        self.dev = dev
+        self.fa = flatten_module(ddpg.model_actor)
+        self.fc = flatten_module(ddpg.model_critic)
+        self.ta = flatten_module(ddpg.target_actor) if ddpg.tau is not None else None
+        self.tc = flatten_module(ddpg.target_critic) if ddpg.tau is not None else None
+        self.sa = _AdamState(ddpg.optimiser, ddpg.model_actor, self.fa)
+        self.sc = _AdamState(ddpg.critic_optimiser, ddpg.model_critic, self.fc)
+        nb = int(self.L.sk_grad_packed_bytes())
+        self.gpa = torch.empty(nb, dtype=torch.uint8, device=dev)
+        self.gpc = torch.empty(nb, dtype=torch.uint8, device=dev)
+        self.seed = int(seed) & ((1 << 64) - 1)
+        self.calls = torch.zeros(1, dtype=torch.int64, device=dev)  # dropout call number (device, capturable)
+        self.stats = torch.zeros(2, dtype=torch.float32, device=dev)  # [sum (q-y)^2, sum Q]
+        self._partials = {}
+        self.grad_flat = None
+        self.pack()
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
+
+    def _partial(self, batch, n_params):
+        key = (batch, n_params)
+        t = self._partials.get(key)
+        if t is None:
+            g = int(self.L.sk_update_partials(batch))
+            t = self._partials[key] = torch.empty((g, n_params), dtype=torch.float32, device=self.dev)
+        return t
+
+    def _pack(self, m, buf, ld2, n_out):
+        rc = self.L.sk_grad_pack(_p(m.l1.weight), _p(m.l1.bias), _p(m.l2.weight), ld2, _p(m.l2.bias),
+                                 _p(m.l3.weight), _p(m.l3.bias), n_out, _p(buf), self._stream())
+        _capi.check(rc)
+
+    @torch.no_grad()
+    def pack(self):
+        self._pack(self.d.model_actor, self.gpa, 256, 2)
+        self._pack(self.d.model_critic, self.gpc, 258, 1)
+
+    def _adam(self, part, flat, st, target):
+        P = flat.numel()
+        tau = float(self.d.tau) if target is not None else 0.0
+        world = self.d.world()
+        if world > 1:  # sum partials -> flat grad -> RCCL mean -> apply
+            if self.grad_flat is None or self.grad_flat.numel() < P:
+                self.grad_flat = torch.empty(max(36609, P), dtype=torch.float32, device=self.dev)
+            g = self.grad_flat[:P]
+            _capi.check(self.L.sk_adam_flat(_p(part), part.shape[0], P, None, _p(g), 0, None, None, None, None,
+                                            0.0, 0.0, 0.0, 0.0, None, 0.0, self._stream()))
+            dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.d.group)
+            g /= world
+            _capi.check(self.L.sk_adam_flat(None, 0, P, _p(g), None, 1, _p(flat), _p(st.m), _p(st.v), _p(st.steps),
+                                            st.lr, st.b1, st.b2, st.eps, _p(target), tau, self._stream()))
+        else:
+            _capi.check(self.L.sk_adam_flat(_p(part), part.shape[0], P, None, None, 1, _p(flat), _p(st.m), _p(st.v),
+                                            _p(st.steps), st.lr, st.b1, st.b2, st.eps, _p(target), tau,
+                                            self._stream()))
+
+    @torch.no_grad()
+    def critic_step(self, s, a, target, mask_out=None):
+        """One critic Adam step on MSE(Q(s, a), target), Dropout active; returns
+        the loss (device scalar)."""
+        s, a, y = s.float().contiguous(), a.float().contiguous(), target.float().contiguous()
+        B = s.shape[0]
+        part = self._partial(B, self.fc.numel())
+        self.calls.add_(1)
+        self.stats.zero_()
+        st = self.sc
+        rc = self.L.sk_critic_grad(_p(self.gpc), _p(s), _p(a), _p(y), B, 2.0 / B, self.seed, _p(self.calls),
+                                   _p(part), _p(st.steps), st.steps.numel(), _p(self.stats), _p(mask_out),
+                                   self._stream())
+        _capi.check(rc)
+        self._adam(part, self.fc, st, self.tc)
+        self._pack(self.d.model_critic, self.gpc, 258, 1)
+        return self.stats[0] / B
+
+    @torch.no_grad()
+    def actor_step(self, s):
+        """One actor Adam step on -sum_b Q(s_b, mu(s_b)) (critic at inference);
+        returns that loss (device scalar)."""
+        s = s.float().contiguous()
+        B = s.shape[0]
+        part = self._partial(B, self.fa.numel())
+        self.stats.zero_()
+        st = self.sa
+        rc = self.L.sk_actor_grad(_p(self.gpa), _p(self.gpc), _p(s), B, 1.0, _p(part), _p(st.steps),
+                                  st.steps.numel(), _p(self.stats[1:]), self._stream())
+        _capi.check(rc)
+        self._adam(part, self.fa, st, self.ta)
+        self._pack(self.d.model_actor, self.gpa, 256, 2)
+        return -self.stats[1]
+
+    @torch.no_grad()
+    def grads(self, which, s, a=None, target=None, mask_out=None):
+        """Test hook: the flat gradient the kernels compute, without stepping
+        (the Adam step counters are restored)."""
+        B = s.shape[0]
+        if which == "critic":
+            flat, st = self.fc, self.sc
+            part = self._partial(B, flat.numel())
+            self.calls.add_(1)
+            rc = self.L.sk_critic_grad(_p(self.gpc), _p(s.contiguous()), _p(a.contiguous()),
+                                       _p(target.contiguous()), B, 2.0 / B, self.seed, _p(self.calls), _p(part),
+                                       None, 0, None, _p(mask_out), self._stream())
+        else:
+            flat, st = self.fa, self.sa
+            part = self._partial(B, flat.numel())
+            rc = self.L.sk_actor_grad(_p(self.gpa), _p(self.gpc), _p(s.contiguous()), B, 1.0, _p(part), None, 0,
+                                      None, self._stream())
+        _capi.check(rc)
+        g = torch.empty_like(flat)
+        _capi.check(self.L.sk_adam_flat(_p(part), part.shape[0], flat.numel(), None, _p(g), 0, None, None, None, None,
+                                        0.0, 0.0, 0.0, 0.0, None, 0.0, self._stream()))
+        return g

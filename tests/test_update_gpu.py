@@ -1,0 +1,211 @@
+"""A16/F1 on the GPU: the DDPG update kernels (csrc/sk_update.hip) against
+PyTorch references of the same losses (learner.DDPG's autograd path).
+
+The gradient GEMMs run with bf16 operands and fp32 accumulation.  Each
+parameter tensor's kernel gradient is held to a relative Frobenius error
+REL_EMU against a torch emulation of exactly those roundings (fp64
+accumulation), and to REL_FP32 against plain fp32 autograd (with the signs
+of large components agreeing); Adam and the soft update are fp32 and held
+to 1e-6."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+REL_EMU = 5e-3
+REL_FP32 = 6e-2
+
+
+def _bf(t):
+    return t.detach().to(torch.bfloat16).double()
+
+
+@pytest.fixture(scope="module")
+def mods():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from skillshot_learning_amd import learner
+    return learner
+
+
+def _ddpg(learner, seed=0, scale=2.0, tau=None):
+    d = learner.DDPG("cuda", seed=seed, tau=tau, fused_update=True)
+    with torch.no_grad():  # non-trivial weights and biases
+        for m in (d.model_actor, d.model_critic):
+            for l in (m.l1, m.l2, m.l3):
+                l.weight.mul_(scale)
+                l.bias.normal_(0, 0.1)
+    d._fused.pack()
+    return d
+
+
+def _obs(rows):
+    return torch.rand(rows, 12, device="cuda") * torch.tensor([1, 1, 1, 1, 9.8, 1, 1, 1, 1, 9.8, 1, 1.0],
+                                                             device="cuda")
+
+
+def _check_grads(flat_kernel, module, ref_grads, rel, sign=True):
+    off = 0
+    for (name, p), g in zip(module.named_parameters(), ref_grads):
+        k = p.numel()
+        got = flat_kernel[off:off + k].view_as(p).double()
+        g = g.double()
+        off += k
+        den = g.norm().item()
+        err = (got - g).norm().item()
+        assert err <= rel * den + 1e-6, (name, err, den)
+        if sign:
+            big = g.abs() > 0.1 * g.abs().max()
+            assert bool((torch.sign(got[big]) == torch.sign(g[big])).all()), name
+
+
+def _critic_emu(c, s, a, y, mask):
+    """the kernel's critic backward: bf16 operands at its rounding points, fp64 sums"""
+    W1, b1, W2, b2, W3, b3 = [t.detach().double() for t in (c.l1.weight, c.l1.bias, c.l2.weight, c.l2.bias,
+                                                            c.l3.weight, c.l3.bias)]
+    s, a, y = s.double(), a.double(), y.double()
+    B = s.shape[0]
+    Sb = _bf(s)
+    hd = torch.relu(Sb @ _bf(W1).t() + b1) * mask.double() * 1.25
+    Hb = _bf(hd)
+    h2 = torch.relu(Hb @ _bf(W2[:, :256]).t() + b2 + a @ W2[:, 256:].t())
+    q = (h2 @ W3.t() + b3).squeeze(-1)
+    dq = 2.0 * (q - y) / B
+    dz2 = dq[:, None] * W3 * (h2 > 0)
+    gW2 = torch.cat([_bf(dz2).t() @ Hb, dz2.t() @ a], 1)
+    dz1 = (_bf(dz2) @ _bf(W2[:, :256])) * 1.25 * (Hb > 0)
+    return [_bf(dz1).t() @ Sb, dz1.sum(0), gW2, dz2.sum(0), dq[None, :] @ h2, dq.sum(0, keepdim=True)]
+
+
+def _actor_emu(am, c, s):
+    aW1, ab1, aW2, ab2, aW3, ab3 = [t.detach().double() for t in (am.l1.weight, am.l1.bias, am.l2.weight,
+                                                                  am.l2.bias, am.l3.weight, am.l3.bias)]
+    cW1, cb1, cW2, cb2, cW3, cb3 = [t.detach().double() for t in (c.l1.weight, c.l1.bias, c.l2.weight, c.l2.bias,
+                                                                  c.l3.weight, c.l3.bias)]
+    s = s.double()
+    Sb = _bf(s)
+    H1 = _bf(torch.relu(Sb @ _bf(aW1).t() + ab1))
+    H1c = _bf(torch.relu(Sb @ _bf(cW1).t() + cb1))
+    h2 = torch.relu(H1 @ _bf(aW2).t() + ab2)
+    act = torch.tanh(h2 @ aW3.t() + ab3)
+    z2c = H1c @ _bf(cW2[:, :256]).t() + cb2 + act @ cW2[:, 256:].t()
+    dzc = (z2c > 0) * cW3
+    dz3 = -(dzc @ cW2[:, 256:]) * (1 - act * act)
+    dz2 = (dz3 @ aW3) * (h2 > 0)
+    dz1 = (_bf(dz2) @ _bf(aW2)) * (H1 > 0)
+    return [_bf(dz1).t() @ Sb, dz1.sum(0), _bf(dz2).t() @ H1, dz2.sum(0), dz3.t() @ h2, dz3.sum(0)]
+
+
+@pytest.mark.parametrize("rows", [1, 37, 256, 4096 + 17])
+def test_critic_grad_matches_autograd(mods, rows):
+    learner = mods
+    d = _ddpg(learner, seed=1)
+    s, a = _obs(rows), torch.rand(rows, 2, device="cuda") * 2 - 1
+    y = torch.randn(rows, device="cuda")
+    mask = torch.zeros(rows, 256, dtype=torch.uint8, device="cuda")
+    g = d._fused.grads("critic", s, a, y, mask_out=mask)
+    torch.cuda.synchronize()
+    keep = mask.float().mean().item()
+    if rows >= 256:
+        assert abs(keep - 0.8) < 0.02, keep  # Dropout(0.2)
+    c = d.model_critic
+    _check_grads(g, c, _critic_emu(c, s, a, y, mask), REL_EMU, sign=False)
+    params = list(c.parameters())
+    for p in params:
+        p.grad = None
+    h = torch.relu(c.l1(s)) * mask.float() * 1.25  # the kernel's mask, torch's scaling
+    q = c.l3(torch.relu(c.l2(torch.cat([h, a], -1)))).squeeze(-1)
+    torch.nn.functional.mse_loss(q, y).backward()
+    _check_grads(g, c, [p.grad for p in params], REL_FP32)
+
+
+@pytest.mark.parametrize("rows", [1, 37, 256, 4096 + 17])
+def test_actor_grad_matches_autograd(mods, rows):
+    learner = mods
+    d = _ddpg(learner, seed=2)
+    s = _obs(rows)
+    g = d._fused.grads("actor", s)
+    a_mod, c = d.model_actor, d.model_critic
+    _check_grads(g, a_mod, _actor_emu(a_mod, c, s), REL_EMU, sign=False)
+    params = list(a_mod.parameters())
+    for p in params:
+        p.grad = None
+    c.eval()
+    for p in c.parameters():
+        p.requires_grad_(False)
+    (-c(s, a_mod(s)).sum()).backward()
+    for p in c.parameters():
+        p.requires_grad_(True)
+    _check_grads(g, a_mod, [p.grad for p in params], REL_FP32)
+
+
+def test_adam_and_soft_update_match_torch(mods):
+    learner = mods
+    torch.manual_seed(0)
+    d = _ddpg(learner, seed=3, tau=0.05)
+    ref = learner.DDPG("cuda", seed=3, tau=0.05, fused_update=False)
+    ref.model_critic.load_state_dict(d.model_critic.state_dict())
+    ref.target_critic.load_state_dict(d.target_critic.state_dict())
+    st = d._fused.sc
+    P = d._fused.fc.numel()
+    for step in range(3):
+        g = torch.randn(P, device="cuda") * 0.01
+        # kernel: partial = g, one Adam launch (with the soft update); the
+        # gradient kernel normally advances the step counters
+        st.steps += 1
+        d._fused._adam(g.view(1, -1), d._fused.fc, st, d._fused.tc)
+        # torch: the same gradient through torch.optim.Adam + lerp
+        off = 0
+        for p in ref.model_critic.parameters():
+            p.grad = g[off:off + p.numel()].view_as(p).clone()
+            off += p.numel()
+        ref.critic_optimiser.step()
+        with torch.no_grad():
+            torch._foreach_lerp_(list(ref.target_critic.parameters()), list(ref.model_critic.parameters()), 0.05)
+    for a, b in zip(d.model_critic.parameters(), ref.model_critic.parameters()):
+        assert torch.allclose(a, b, rtol=1e-5, atol=1e-6)
+    for a, b in zip(d.target_critic.parameters(), ref.target_critic.parameters()):
+        assert torch.allclose(a, b, rtol=1e-5, atol=1e-6)
+    # the optimiser's own state is the kernel's (views of the flat buffers)
+    p0 = next(d.model_critic.parameters())
+    assert float(d.critic_optimiser.state[p0]["step"]) == 3.0
+    assert torch.allclose(d.critic_optimiser.state[p0]["exp_avg"],
+                          ref.critic_optimiser.state[next(ref.model_critic.parameters())]["exp_avg"], atol=1e-7)
+
+
+def test_fused_replay_update_trains(mods):
+    """End to end on a fixed replay: the fused path's critic fits the rewards
+    like the autograd path, targets track by tau, actor moves."""
+    learner = mods
+    losses = {}
+    for fused in (True, False):
+        torch.manual_seed(5)
+        d = learner.DDPG("cuda", seed=5, tau=0.01, gamma=0.0, replay_capacity=4096, fused_update=fused)
+        s = _obs(4096)
+        a = torch.rand(4096, 2, device="cuda") * 2 - 1
+        r = -(s[:, 0] - 0.5).abs() - 0.3 * a[:, 0]  # a learnable immediate reward
+        d.replay.add(s, a, r, s, torch.zeros(4096, device="cuda"))
+        t0 = [p.clone() for p in d.target_critic.parameters()]
+        a0 = [p.clone() for p in d.model_actor.parameters()]
+        out = [d.replay_update(256) for _ in range(300)]
+        lc = torch.stack([o[0] for o in out]).float().cpu()
+        losses[fused] = (lc[:20].mean().item(), lc[-20:].mean().item())
+        assert any((p - q).abs().max() > 0 for p, q in zip(d.target_critic.parameters(), t0))
+        assert any((p - q).abs().max() > 0 for p, q in zip(d.model_actor.parameters(), a0))
+    (f0, f1), (t0_, t1) = losses[True], losses[False]
+    assert f1 < 0.5 * f0 and t1 < 0.5 * t0_, losses
+    assert f1 < 2.0 * t1 + 1e-3, losses
+
+
+def test_fused_tick_graph(mods):
+    """The learner tick (act, step, insert, fused update) still captures and
+    replays as one hipGraph."""
+    learner = mods
+    L = learner.SkillshotLearner(n_envs=256, device="cuda", seed=9, gamma=0.9, tau=0.01, replay_capacity=1 << 14)
+    assert L.ddpg._fused is not None
+    g = L.tick_graph(batch=256, ticks_per_graph=2, warmup=2)
+    w0 = [p.clone() for p in L.model_actor.parameters()]
+    g.run(5)
+    torch.cuda.synchronize()
+    assert all(torch.isfinite(p).all() for p in L.model_actor.parameters())
+    assert any((p - q).abs().max() > 0 for p, q in zip(L.model_actor.parameters(), w0))
