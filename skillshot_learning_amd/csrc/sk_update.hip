@@ -73,6 +73,29 @@ __device__ __forceinline__ bf16x8 lfrag(const short* X, int ld, int row0, int k0
 __device__ __forceinline__ int drow(int v, int lane) { return 8 * (v >> 2) + 4 * (lane >> 5) + (v & 3); }
 __device__ __forceinline__ float bf2f(short s) { return __uint_as_float(((uint32_t)(uint16_t)s) << 16); }
 
+// sum over the 128 layer-2 units of X[i][k] * w[k * ws] for the row
+// i = threadIdx.x / 16 of this thread (all 512 threads: 32 rows x 16
+// 8-unit chunks, then a 4-step butterfly inside each 16-lane group; every
+// lane of the group returns the row sum)
+__device__ __forceinline__ float row_dot128(const float* X, int ld, const float* w, int ws) {
+  const int i = threadIdx.x >> 4, c = threadIdx.x & 15;
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s += X[i * ld + 8 * c + k] * w[(8 * c + k) * ws];
+#pragma unroll
+  for (int off = 1; off < 16; off <<= 1) s += __shfl_xor(s, off, 64);
+  return s;
+}
+__device__ __forceinline__ float row_sum128(const float* X, int ld) {
+  const int i = threadIdx.x >> 4, c = threadIdx.x & 15;
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s += X[i * ld + 8 * c + k];
+#pragma unroll
+  for (int off = 1; off < 16; off <<= 1) s += __shfl_xor(s, off, 64);
+  return s;
+}
+
 // D registers 4g..4g+3 of a lane are 4 consecutive rows: store them to a
 // transposed [col][row] bf16 array with one 8-byte write
 __device__ __forceinline__ void store_t4(short* XT, int ld, int col, int row, float a, float b, float c, float d) {
@@ -121,7 +144,7 @@ constexpr int kPackThreads = 8 * 64 + 2 * 64 * 64 + 1024;
 // ---------------------------------------------------------------- shared pieces
 struct Lds {
   short *Sr, *ST, *H1, *H1T, *DZ2, *DZ2T, *DZ1T, *H1C;
-  float *H2f, *DZC, *A, *Y, *DQ, *DZ3;
+  float *H2f, *DZC, *A, *Y, *DQ, *DZ3, *RED;
 };
 
 __device__ __forceinline__ Lds carve(char* smem, bool actor) {
@@ -139,6 +162,7 @@ __device__ __forceinline__ Lds carve(char* smem, bool actor) {
   L.Y = (float*)p;    p += 32 * 4;
   L.DQ = (float*)p;   p += 32 * 4;
   L.DZ3 = (float*)p;  p += 64 * 4;
+  L.RED = (float*)p;  p += 4 * 4;
   L.H1C = nullptr;
   L.DZC = nullptr;
   if (actor) {
@@ -148,7 +172,7 @@ __device__ __forceinline__ Lds carve(char* smem, bool actor) {
   return L;
 }
 constexpr size_t kLdsBase = 32 * kLdS * 2 + 32 * kLdT * 2 + 32 * kLdH1 * 2 + kH1 * kLdT * 2 + 32 * kLdZ2 * 2 +
-                            kH2 * kLdT * 2 + kH1 * kLdT * 2 + 32 * kLdH2f * 4 + (64 + 32 + 32 + 64) * 4;
+                            kH2 * kLdT * 2 + kH1 * kLdT * 2 + 32 * kLdH2f * 4 + (64 + 32 + 32 + 64 + 4) * 4;
 constexpr size_t kLdsCritic = kLdsBase;
 constexpr size_t kLdsActor = kLdsBase + 32 * kLdH1 * 2 + 32 * kLdH2f * 4;
 
@@ -198,17 +222,14 @@ __device__ __forceinline__ void layer1(const Lds& L, const bf16x8* gW1, const fl
 }
 
 // layer 2 MFMA of one net for out n-tile nt over the 256 hidden inputs
-// (k-steps in groups of 4 behind scheduling fences: the compiler otherwise
-// hoists all 32 fragment loads and spills the gradient accumulators)
+// (all 16 weight fragments issued up front: one memory round trip)
 __device__ __forceinline__ f32x16 layer2(const short* H, const bf16x8* gW2, int nt, int lane) {
+  bf16x8 wf[16];
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk) wf[kk] = gW2[(nt * 16 + kk) * 64 + lane];
   f32x16 acc = {0};
 #pragma unroll
-  for (int k4 = 0; k4 < 4; ++k4) {
-#pragma unroll
-    for (int kk = 4 * k4; kk < 4 * k4 + 4; ++kk)
-      acc = mfma(lfrag(H, kLdH1, 0, 16 * kk, lane), gW2[(nt * 16 + kk) * 64 + lane], acc);
-    __builtin_amdgcn_sched_barrier(0);
-  }
+  for (int kk = 0; kk < 16; ++kk) acc = mfma(lfrag(H, kLdH1, 0, 16 * kk, lane), wf[kk], acc);
   return acc;
 }
 
@@ -229,14 +250,12 @@ __device__ __forceinline__ void backward_12(const Lds& L, const bf16x8* gW2T, in
     __builtin_amdgcn_sched_barrier(0);
   }
   {
+    bf16x8 wf[8];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) wf[kk] = gW2T[(w * 8 + kk) * 64 + lane];
     f32x16 acc = {0};
 #pragma unroll
-    for (int k4 = 0; k4 < 2; ++k4) {
-#pragma unroll
-      for (int kk = 4 * k4; kk < 4 * k4 + 4; ++kk)
-        acc = mfma(lfrag(L.DZ2, kLdZ2, 0, 16 * kk, lane), gW2T[(w * 8 + kk) * 64 + lane], acc);
-      __builtin_amdgcn_sched_barrier(0);
-    }
+    for (int kk = 0; kk < 8; ++kk) acc = mfma(lfrag(L.DZ2, kLdZ2, 0, 16 * kk, lane), wf[kk], acc);
     const int n = 32 * w + (lane & 31);
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -301,6 +320,7 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad(const float* __restric
   float gb1 = 0.f, gb2 = 0.f, gw2a0 = 0.f, gw2a1 = 0.f, gw3 = 0.f, gb3 = 0.f, lsum = 0.f;
   const bool l2 = w < 4;               // layer-2 waves
   const int u = 32 * (w & 3) + (lane & 31);  // their layer-2 unit
+  if (threadIdx.x < 4) L.RED[threadIdx.x] = 0.f;
   __syncthreads();
   for (int sub = 0; sub < sub_per_wg; ++sub) {
     const int64_t row0 = ((int64_t)blockIdx.x * sub_per_wg + sub) * 32;
@@ -330,15 +350,15 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad(const float* __restric
       }
     }
     __syncthreads();
-    if (threadIdx.x < 32) {  // q and dL/dq per row
-      const int i = threadIdx.x;
-      float q = tail[kTB3];
-      for (int k = 0; k < kH2; ++k) q += L.H2f[i * kLdH2f + k] * tail[kTW3 + k];
-      const bool valid = row0 + i < B;
-      const float e = valid ? q - L.Y[i] : 0.f;
-      L.DQ[i] = grad_scale * e;
-      gb3 += grad_scale * e;
-      lsum += e * e;
+    {  // q and dL/dq per row (all threads: row_dot128)
+      const int i = threadIdx.x >> 4;
+      const float q = tail[kTB3] + row_dot128(L.H2f, kLdH2f, tail + kTW3, 1);
+      if ((threadIdx.x & 15) == 0) {
+        const float e = row0 + i < B ? q - L.Y[i] : 0.f;
+        L.DQ[i] = grad_scale * e;
+        gb3 += grad_scale * e;
+        lsum += e * e;
+      }
     }
     __syncthreads();
     if (l2) {
@@ -376,16 +396,14 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad(const float* __restric
     P[kPW2 + u * kCPW2ld + kH1 + 1] = gw2a1;
     P[kCPW3 + u] = gw3;
   }
-  if (w == 0) {  // lanes 0..31 hold db3 / loss partials
-#pragma unroll
-    for (int off = 16; off > 0; off >>= 1) {
-      gb3 += __shfl_xor(gb3, off, 64);
-      lsum += __shfl_xor(lsum, off, 64);
-    }
-    if (lane == 0) {
-      P[kCPB3] = gb3;
-      if (loss_out) atomicAdd(loss_out, lsum);
-    }
+  if ((threadIdx.x & 15) == 0) {  // the row-owner threads hold db3 / loss partials
+    atomicAdd(&L.RED[0], gb3);
+    atomicAdd(&L.RED[1], lsum);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    P[kCPB3] = L.RED[0];
+    if (loss_out) atomicAdd(loss_out, L.RED[1]);
   }
 }
 
@@ -409,6 +427,7 @@ __global__ void __launch_bounds__(kThreads) k_actor_grad(const float* __restrict
   float gb1 = 0.f, gb2 = 0.f, gw30 = 0.f, gw31 = 0.f, gb3 = 0.f, qsum = 0.f;
   const bool l2 = w < 4;                     // layer-2 waves
   const int u = 32 * (w & 3) + (lane & 31);  // their layer-2 unit
+  if (threadIdx.x < 4) L.RED[threadIdx.x] = 0.f;
   __syncthreads();
   for (int sub = 0; sub < sub_per_wg; ++sub) {
     const int64_t row0 = ((int64_t)blockIdx.x * sub_per_wg + sub) * 32;
@@ -424,7 +443,6 @@ __global__ void __launch_bounds__(kThreads) k_actor_grad(const float* __restrict
     const bf16x8* cW2 = (const bf16x8*)(cp + kGW2);
     const float* ct = (const float*)(cp + kGTail);
     load_states(L, S, row0, B);
-    if (threadIdx.x < 32) L.DQ[threadIdx.x] = 0.f;  // per-row Q accumulators (q_out)
     __syncthreads();
     layer1<false>(L, aW1, at, w, lane, L.H1, L.H1T, 0, 0, 0, nullptr, B);
     layer1<false>(L, cW1, ct, w, lane, L.H1C, nullptr, 0, 0, 0, nullptr, B);
@@ -436,36 +454,41 @@ __global__ void __launch_bounds__(kThreads) k_actor_grad(const float* __restrict
       for (int v = 0; v < 16; ++v) L.H2f[drow(v, lane) * kLdH2f + u] = fmaxf(acc[v] + b2, 0.f);
     }
     __syncthreads();
-    if (threadIdx.x < 64) {  // mu(s) = tanh(W3 h2 + b3)
-      const int i = threadIdx.x >> 1, j = threadIdx.x & 1;
-      float z = at[kTB3 + j];
-      for (int k = 0; k < kH2; ++k) z += L.H2f[i * kLdH2f + k] * at[kTW3 + j * kH2 + k];
-      L.A[2 * i + j] = tanhf(z);
+    {  // mu(s) = tanh(W3 h2 + b3) (all threads: row_dot128)
+      const int i = threadIdx.x >> 4, c = threadIdx.x & 15;
+      const float z0 = row_dot128(L.H2f, kLdH2f, at + kTW3, 1);
+      const float z1 = row_dot128(L.H2f, kLdH2f, at + kTW3 + kH2, 1);
+      if (c < 2) L.A[2 * i + c] = tanhf((c ? z1 : z0) + at[kTB3 + c]);
     }
     __syncthreads();
-    if (l2) {  // critic layer 2 at (s, mu(s)): dQ/dz2 = W3 relu'(z2) (rows beyond B: 0)
-      const f32x16 acc = layer2(L.H1C, cW2, w, lane);
-      const float b2 = ct[kTB2 + u], wa0 = ct[kTW2a + 2 * u], wa1 = ct[kTW2a + 2 * u + 1], w3 = ct[kTW3 + u];
+    {  // critic layer 2 at (s, mu(s)): dQ/dz2 = W3 relu'(z2) (rows beyond B: 0)
+      f32x16 acc = {0};
+      if (l2) acc = layer2(L.H1C, cW2, w, lane);
+      __syncthreads();  // every wave is done reading H1C: its space takes the Q terms
+      float* QZ = (float*)L.H1C;  // [32][kLdH2f] fp32 relu(z2) W3 (q_out)
+      if (l2) {
+        const float b2 = ct[kTB2 + u], wa0 = ct[kTW2a + 2 * u], wa1 = ct[kTW2a + 2 * u + 1], w3 = ct[kTW3 + u];
 #pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const int i = drow(v, lane);
-        const float z = acc[v] + b2 + L.A[2 * i] * wa0 + L.A[2 * i + 1] * wa1;
-        L.DZC[i * kLdH2f + u] = (z > 0.f && row0 + i < B) ? w3 : 0.f;
-        if (q_out) atomicAdd(&L.DQ[i], fmaxf(z, 0.f) * w3);
+        for (int v = 0; v < 16; ++v) {
+          const int i = drow(v, lane);
+          const float z = acc[v] + b2 + L.A[2 * i] * wa0 + L.A[2 * i + 1] * wa1;
+          L.DZC[i * kLdH2f + u] = (z > 0.f && row0 + i < B) ? w3 : 0.f;
+          if (q_out) QZ[i * kLdH2f + u] = fmaxf(z, 0.f) * w3;
+        }
       }
-    }
-    __syncthreads();
-    if (threadIdx.x < 64) {  // dL/dz3 = -loss_scale * dQ/da * (1 - a^2)
-      const int i = threadIdx.x >> 1, j = threadIdx.x & 1;
-      float da = 0.f;
-      for (int k = 0; k < kH2; ++k) da += L.DZC[i * kLdH2f + k] * ct[kTW2a + 2 * k + j];
-      const float a = L.A[2 * i + j];
-      const float d = -loss_scale * da * (1.f - a * a);
-      L.DZ3[2 * i + j] = d;
-      gb3 += d;
-      if (q_out && j == 0 && row0 + i < B) {
-        qsum += ct[kTB3] + L.DQ[i];
+      __syncthreads();
+      // dL/dz3 = -loss_scale * dQ/da * (1 - a^2), dQ/da = sum_u dQ/dz2 W2[u][256 + j]
+      const int i = threadIdx.x >> 4, c = threadIdx.x & 15;
+      const float da0 = row_dot128(L.DZC, kLdH2f, ct + kTW2a, 2);
+      const float da1 = row_dot128(L.DZC, kLdH2f, ct + kTW2a + 1, 2);
+      const float qrow = q_out ? row_sum128(QZ, kLdH2f) : 0.f;
+      if (c < 2) {
+        const float a = L.A[2 * i + c];
+        const float d = -loss_scale * (c ? da1 : da0) * (1.f - a * a);
+        L.DZ3[2 * i + c] = d;
+        gb3 += d;  // db3[c] partial (threads with c < 2)
       }
+      if (c == 0 && q_out && row0 + i < B) qsum += ct[kTB3] + qrow;
     }
     __syncthreads();
     if (l2) {  // dZ2 = (dz3 W3) relu'(h2);  dW3[j][u] += sum_i dz3[i][j] h2[i][u]
@@ -501,15 +524,14 @@ __global__ void __launch_bounds__(kThreads) k_actor_grad(const float* __restrict
     P[kAPW3 + u] = gw30;
     P[kAPW3 + kH2 + u] = gw31;
   }
-  if (w == 0) {  // lanes (i, j) of wave 0: db3[j] and sum Q over i
-#pragma unroll
-    for (int off = 2; off < 64; off <<= 1) {
-      gb3 += __shfl_xor(gb3, off, 64);
-      qsum += __shfl_xor(qsum, off, 64);
-    }
-    if (lane < 2) P[kAPB3 + lane] = gb3;
-    if (lane == 0 && q_out) atomicAdd(q_out, qsum);
+  {  // db3[j]: threads with c == j; sum Q: threads with c == 0
+    const int c = threadIdx.x & 15;
+    if (c < 2) atomicAdd(&L.RED[c], gb3);
+    if (c == 0) atomicAdd(&L.RED[2], qsum);
   }
+  __syncthreads();
+  if (threadIdx.x < 2) P[kAPB3 + threadIdx.x] = L.RED[threadIdx.x];
+  if (threadIdx.x == 0 && q_out) atomicAdd(q_out, L.RED[2]);
 }
 
 // ---------------------------------------------------------------- Adam
@@ -526,7 +548,14 @@ __global__ void k_adam_flat(const float* __restrict__ partial, int G, int P, con
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P) return;
   float g = grad_in ? grad_in[p] : 0.f;
-  for (int k = 0; k < G; ++k) g += partial[(int64_t)k * P + p];
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // 8 independent loads in flight
+  int k = 0;
+  for (; k + 8 <= G; k += 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += partial[(int64_t)(k + j) * P + p];
+  }
+  for (; k < G; ++k) acc[0] += partial[(int64_t)k * P + p];
+  g += ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   if (grad_out) grad_out[p] = g;
   if (!apply) return;
   const float t = step_ctr[0];

@@ -24,11 +24,14 @@ PEAK_GBS = 8000.0
 ACTOR_FLOP = 2 * (12 * 256 + 256 * 128 + 128 * 2)
 ACTOR_NOISE_FLOP = ACTOR_FLOP + 2 * (12 * 256 + 256 * 128)
 CRITIC_FLOP = 2 * (12 * 256 + (256 + 2) * 128 + 128)
+BWD_FLOP = 2 * (2 * 256 * 128 + 256 * 12)  # dW2, dH1, dW1 (the MFMA GEMMs of a backward)
+CRITIC_GRAD_FLOP = CRITIC_FLOP + BWD_FLOP
+ACTOR_GRAD_FLOP = ACTOR_FLOP + CRITIC_FLOP + BWD_FLOP
 
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--rows", default="8192,131072,1048576")
+    p.add_argument("--rows", default="256,4096,8192,131072,1048576")
     p.add_argument("--reps", type=int, default=200)
     p.add_argument("--only", default="")
     p.add_argument("--eager", action="store_true", help="plain launches (rocprofv3 --pmc attribution)")
@@ -36,10 +39,13 @@ def main():
     from skillshot_learning_amd import learner
     from skillshot_learning_amd.actor_kernel import ActorKernel
     from skillshot_learning_amd.critic_kernel import CriticKernel, TargetQKernel
+    from skillshot_learning_amd.update_kernel import FusedUpdate
 
     torch.manual_seed(0)
     actor, critic = learner.Actor().cuda(), learner.Critic().cuda().eval()
     ak, ck, tk = ActorKernel(actor, seed=1), CriticKernel(critic), TargetQKernel(actor, critic)
+    ddpg = learner.DDPG("cuda", seed=0, fused_update=True)
+    fu = ddpg._fused
     st = torch.cuda.Stream()
     for rows in [int(r) for r in a.rows.split(",")]:
         s = torch.rand(rows, 12, device="cuda")
@@ -51,6 +57,8 @@ def main():
             "actor_noise": (lambda: ak(s, 0.5, out=y), ACTOR_NOISE_FLOP, 56),
             "critic": (lambda: ck(s, act, out=q), CRITIC_FLOP, 60),
             "target_q": (lambda: tk(s, out=q), ACTOR_FLOP + CRITIC_FLOP, 52),
+            "critic_grad": (lambda: fu.grads("critic", s, act, q), CRITIC_GRAD_FLOP, 60),
+            "actor_grad": (lambda: fu.grads("actor", s), ACTOR_GRAD_FLOP, 48),
         }
         for name, (fn, flop, byts) in cases.items():
             if a.only and name != a.only:
