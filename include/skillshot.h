@@ -255,6 +255,30 @@ int sk_critic_forward(const void* packed, const float* obs, const float* actions
  * bit-identical to sk_actor_forward with noise_sd = 0. */
 int sk_target_q(const void* actor_packed, const void* critic_packed, const float* obs, float* q, float* actions,
                 int64_t rows, void* stream);
+/* The DDPG critic target in the same launch: y = r + gamma (1 - done) Q'(s',
+ * mu'(s')) (DDPG.replay_update); next_obs float[rows][12], rewards / done /
+ * y float[rows]. */
+int sk_target_y(const void* actor_packed, const void* critic_packed, const float* next_obs, const float* rewards,
+                const float* done, float gamma, float* y, int64_t rows, void* stream);
+
+/* --- the replay ring in HBM (F1) ------------------------------------------ */
+
+/* ring float[capacity][28] (s 12, a 2, r 1, s' 12, done 1: 112-byte rows,
+ * 16-byte aligned); *total (int64, device) = rows ever inserted (head =
+ * total % capacity, size = min(total, capacity)); arrivals: a zeroed device
+ * uint32 the insert uses to let its last workgroup advance *total.
+ * sk_replay_insert writes `rows` (<= capacity) transitions: obs / next_obs
+ * float[rows][12], actions float[rows][2], rewards float[rows], done
+ * uint8[n_games] with row r taking done[r % n_games] (the [2N] player-major
+ * order of the actor and the engine).  sk_replay_sample gathers `batch`
+ * uniformly drawn rows (Philox4x32-10 keyed by (seed; row, draw, *total))
+ * into contiguous s float[batch][12], a [batch][2], r [batch], s2
+ * [batch][12], d [batch].  Both are stream-ordered and graph-capturable. */
+int sk_replay_insert(float* ring, int64_t capacity, int64_t* total, uint32_t* arrivals, const float* obs,
+                     const float* actions, const float* rewards, const float* next_obs, const uint8_t* done,
+                     int64_t n_games, int64_t rows, void* stream);
+int sk_replay_sample(const float* ring, int64_t capacity, const int64_t* total, uint64_t seed, int32_t draw,
+                     int64_t batch, float* s, float* a, float* r, float* s2, float* d, void* stream);
 
 /* --- the DDPG update (A16, F1) ------------------------------------------- */
 

@@ -82,3 +82,15 @@ class TargetQKernel:
         if rc != 0:
             raise SkillshotError(f"sk_target_q failed ({rc})")
         return q
+
+    @torch.no_grad()
+    def target(self, next_obs, reward, done, gamma, out=None):
+        """y = r + gamma (1 - done) Q'(s', mu'(s')) in the same launch."""
+        x = next_obs.float().contiguous()
+        r, d = reward.float().contiguous(), done.float().contiguous()
+        y = out if out is not None else torch.empty(x.shape[0], dtype=torch.float32, device=self.device)
+        rc = self.L.sk_target_y(_p(self.actor_k.buf), _p(self.critic_k.buf), _p(x), _p(r), _p(d), float(gamma),
+                                _p(y), x.shape[0], self.critic_k._stream())
+        if rc != 0:
+            raise SkillshotError(f"sk_target_y failed ({rc})")
+        return y

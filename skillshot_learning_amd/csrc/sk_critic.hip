@@ -191,10 +191,13 @@ __global__ void __launch_bounds__(kCThreads) k_critic_fwd(const float* __restric
 }
 
 // Q'(s, mu'(s)): the actor then the critic on the same tile
+// With R given, Q receives the bootstrapped target R + gamma (1 - D) Q'
+// (DDPG.replay_update) instead of Q'.
 __global__ void __launch_bounds__(kCThreads) k_target_q(const float* __restrict__ S, float* __restrict__ Q,
                                                         float* __restrict__ A_out, int64_t M,
                                                         const char* __restrict__ apacked,
-                                                        const char* __restrict__ cpacked) {
+                                                        const char* __restrict__ cpacked, const float* __restrict__ R,
+                                                        const float* __restrict__ D, float gamma) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* sAW2 = smem;
   float* sATail = (float*)(smem + kW2Frag);            // actor b1 b2 b3 (512), W3 (256), W3^2 (256)
@@ -245,7 +248,7 @@ __global__ void __launch_bounds__(kCThreads) k_target_q(const float* __restrict_
     layer1((const bf16x8*)(cp + kCOffW1), sCTail + toff, xb, lane, h, h1);
     const float q = critic_q((const bf16x8*)sCW2, sCTail + toff, sCTail + toff + 512, sCTail + toff + 768, h1, a0,
                              a1, lane, h);
-    if (h == 0 && valid) Q[row] = q;
+    if (h == 0 && valid) Q[row] = R ? R[row] + gamma * (1.f - D[row]) * q : q;
   }
 }
 
@@ -314,7 +317,24 @@ int sk_target_q(const void* actor_packed, const void* critic_packed, const float
     attr = true;
   }
   k_target_q<<<(unsigned)grid_for(rows), kCThreads, lds, (hipStream_t)stream>>>(
-      obs, q, actions, rows, (const char*)actor_packed, (const char*)critic_packed);
+      obs, q, actions, rows, (const char*)actor_packed, (const char*)critic_packed, nullptr, nullptr, 0.f);
+  return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
+}
+
+int sk_target_y(const void* actor_packed, const void* critic_packed, const float* next_obs, const float* rewards,
+                const float* done, float gamma, float* y, int64_t rows, void* stream) {
+  if (!actor_packed || !critic_packed || !next_obs || !rewards || !done || !y || rows < 0) return SK_EINVAL;
+  if ((((uintptr_t)next_obs) & 15) || (((uintptr_t)actor_packed) & 15) || (((uintptr_t)critic_packed) & 15))
+    return SK_EINVAL;
+  if (rows == 0) return SK_OK;
+  const size_t lds = 2 * (kW2Frag + 1024 * 4);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_target_q, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr = true;
+  }
+  k_target_q<<<(unsigned)grid_for(rows), kCThreads, lds, (hipStream_t)stream>>>(
+      next_obs, y, nullptr, rows, (const char*)actor_packed, (const char*)critic_packed, rewards, done, gamma);
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
 }
 

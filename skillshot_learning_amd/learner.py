@@ -24,6 +24,7 @@ multi-GPU path: one process per GPU, games sharded by global id, gradients
 all-reduced (RCCL over xGMI; gloo on CPU) as one flat bucket per update, and
 each rank's sampled minibatch all-gathered into a shared batch.
 """
+import ctypes
 import math
 import os
 
@@ -170,27 +171,41 @@ def keras_adam(params):
 
 class ReplayRing:
     """Transitions (s 12f, a 2f, r 1f, s' 12f, done 1f = 112 B) in HBM, packed
-    as one [capacity, 28] float32 row per transition so an insert is one
-    scatter and a minibatch one gather (`s`, `a`, `r`, `s2`, `d` are column
-    views).
+    as one [capacity, 28] float32 row per transition (`s`, `a`, `r`, `s2`, `d`
+    are column views).  `total` counts the rows ever inserted: head = total %
+    capacity, size = min(total, capacity); the host keeps `total`, the device
+    `total_t`.
 
-    Two insert/sample paths: `add`/`sample` keep head and size on the host
-    (slice copies, Python-int range); `add_dev`/`sample_dev` keep them in
-    device scalars (`head_t`, `size_t`) so a captured hipGraph inserts at the
-    right slot and samples the right range on every replay.  Both paths keep
-    both copies in step (`sync_host` reads the device copy back)."""
+    Two insert/sample paths: `add`/`sample` use the host count (slice copies,
+    Python-int range); `add_dev`/`sample_dev` use the device count so a
+    captured hipGraph inserts at the right row and samples the right range on
+    every replay.  On the GPU those are one launch each (csrc/sk_replay.hip:
+    `sk_replay_insert`, whose last workgroup advances `total_t`, and
+    `sk_replay_sample`, a Philox gather into persistent contiguous batch
+    buffers, which the next `sample_dev` of the same size overwrites)."""
 
     WIDTH = 2 * STATE_DIM + ACTION_DIM + 2
 
-    def __init__(self, capacity, device):
+    def __init__(self, capacity, device, seed=0):
         self.cap = int(capacity)
         self.buf = torch.zeros(self.cap, self.WIDTH, device=device)
         self.s, self.a, self.r, self.s2, self.d = self._split(self.buf)
-        self.head = 0
-        self.size = 0
-        self.head_t = torch.zeros((), dtype=torch.int64, device=device)
-        self.size_t = torch.zeros((), dtype=torch.int64, device=device)
+        self.total = 0
+        self.total_t = torch.zeros((), dtype=torch.int64, device=device)
         self._ar = {}
+        self.seed = int(seed) & ((1 << 64) - 1)
+        self._k = None
+        if self.buf.is_cuda:
+            from . import _capi
+            self._k = _capi.load()
+            self._arrivals = torch.zeros(1, dtype=torch.int32, device=device)
+            self._draws = 0
+            self._batches = {}
+
+    head = property(lambda self: self.total % self.cap)
+    size = property(lambda self: min(self.total, self.cap))
+    head_t = property(lambda self: torch.remainder(self.total_t, self.cap))
+    size_t = property(lambda self: torch.clamp(self.total_t, max=self.cap))
 
     @staticmethod
     def _split(rows):
@@ -201,6 +216,8 @@ class ReplayRing:
     @staticmethod
     def _pack(s, a, r, s2, d):
         n = s.shape[0]
+        if d.numel() != n:  # per-game done for player-major rows (row r -> game r % N)
+            d = d.reshape(1, -1).expand(n // d.numel(), -1)
         # one kernel: cat promotes (e.g. a uint8 done column) to float32
         return torch.cat([s.reshape(n, STATE_DIM), a.reshape(n, ACTION_DIM), r.reshape(n, 1),
                           s2.reshape(n, STATE_DIM), d.reshape(n, 1)], 1).float()
@@ -210,41 +227,65 @@ class ReplayRing:
         rows = self._pack(s, a, r, s2, d)
         if n > self.cap:
             rows, n = rows[-self.cap:], self.cap
-        first = min(n, self.cap - self.head)  # contiguous copies, at most two
-        self.buf[self.head:self.head + first].copy_(rows[:first])
+        head = self.head
+        first = min(n, self.cap - head)  # contiguous copies, at most two
+        self.buf[head:head + first].copy_(rows[:first])
         if first < n:
             self.buf[:n - first].copy_(rows[first:])
-        self.head = (self.head + n) % self.cap
-        self.size = min(self.cap, self.size + n)
-        self.head_t.fill_(self.head)
-        self.size_t.fill_(self.size)
+        self.total += n
+        self.total_t.fill_(self.total)
 
     def sample(self, b, generator=None):
         idx = torch.randint(0, self.size, (b,), device=self.buf.device, generator=generator)
         return self._split(self.buf[idx])
 
     def add_dev(self, s, a, r, s2, d):
-        """Capturable insert of n <= capacity rows at the device-side head."""
+        """Capturable insert of n <= capacity rows at the device-side head; d is
+        per row or per game (uint8 [n / 2] for the engine's [2, N] rows)."""
         n = s.shape[0]
         if n > self.cap:
             raise ValueError("add_dev: more rows than capacity")
-        ar = self._ar.get(n)
-        if ar is None:
-            ar = self._ar[n] = torch.arange(n, dtype=torch.int64, device=self.buf.device)
-        self.buf.index_copy_(0, torch.remainder(ar + self.head_t, self.cap), self._pack(s, a, r, s2, d))
-        self.head_t.copy_(torch.remainder(self.head_t + n, self.cap))
-        self.size_t.copy_(torch.clamp(self.size_t + n, max=self.cap))
-        self.head = (self.head + n) % self.cap  # host mirror (exact while n is fixed)
-        self.size = min(self.cap, self.size + n)
+        if self._k is not None:
+            from . import _capi
+            p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+            sc, ac = s.float().contiguous(), a.float().contiguous()
+            rc, s2c = r.float().contiguous(), s2.float().contiguous()
+            dc = d.contiguous() if d.dtype == torch.uint8 else (d != 0).to(torch.uint8).contiguous()
+            _capi.check(self._k.sk_replay_insert(
+                p(self.buf), self.cap, p(self.total_t), p(self._arrivals), p(sc), p(ac), p(rc), p(s2c), p(dc),
+                dc.numel(), n, ctypes.c_void_p(torch.cuda.current_stream(self.buf.device).cuda_stream)))
+        else:
+            ar = self._ar.get(n)
+            if ar is None:
+                ar = self._ar[n] = torch.arange(n, dtype=torch.int64, device=self.buf.device)
+            self.buf.index_copy_(0, torch.remainder(ar + self.total_t, self.cap), self._pack(s, a, r, s2, d))
+            self.total_t.add_(n)
+        self.total += n  # host mirror (exact while n is fixed)
 
     def sample_dev(self, b, generator=None):
         """Capturable uniform sample over the device-side size."""
+        if self._k is not None:
+            from . import _capi
+            out = self._batches.get(b)
+            if out is None:
+                dev = self.buf.device
+                out = self._batches[b] = (torch.empty(b, STATE_DIM, device=dev), torch.empty(b, ACTION_DIM, device=dev),
+                                          torch.empty(b, device=dev), torch.empty(b, STATE_DIM, device=dev),
+                                          torch.empty(b, device=dev))
+            p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+            draw = self._draws
+            self._draws = (self._draws + 1) & 0x7FFFFFFF
+            _capi.check(self._k.sk_replay_sample(
+                p(self.buf), self.cap, p(self.total_t), self.seed, draw, b, *[p(t) for t in out],
+                ctypes.c_void_p(torch.cuda.current_stream(self.buf.device).cuda_stream)))
+            return out
         u = torch.rand(b, dtype=torch.float64, device=self.buf.device, generator=generator)
-        idx = torch.minimum((u * self.size_t).long(), self.size_t - 1)
+        size_t = self.size_t
+        idx = torch.minimum((u * size_t).long(), size_t - 1)
         return self._split(self.buf[idx])
 
     def sync_host(self):
-        self.head, self.size = int(self.head_t), int(self.size_t)
+        self.total = int(self.total_t)
 
 
 class DDPG:
@@ -269,7 +310,8 @@ class DDPG:
             self.target_critic = Critic().to(self.device)
             self.target_actor.load_state_dict(self.model_actor.state_dict())
             self.target_critic.load_state_dict(self.model_critic.state_dict())
-        self.replay = ReplayRing(replay_capacity, self.device) if replay_capacity else None
+        self.replay = (ReplayRing(replay_capacity, self.device, seed=seed * 7919 + rank_seed_offset + 29)
+                       if replay_capacity else None)
         self._tq = None  # fused target-Q kernel (GPU), created at first use
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(seed * 7919 + rank_seed_offset + 17)
@@ -380,7 +422,10 @@ class DDPG:
         target = r
         if self.gamma > 0.0:
             with torch.no_grad():
-                target = r + self.gamma * (1.0 - d) * self.target_q(s2)
+                if self.device.type == "cuda":  # r + gamma (1 - d) Q' in the target kernel's epilogue
+                    target = self._target_kernel().target(s2, r, d, self.gamma)
+                else:
+                    target = r + self.gamma * (1.0 - d) * self.target_q(s2)
         lc = self.critic_step(s, a, target)
         la = self.model_actor_fit_step(s)
         if self.tau is not None:
@@ -401,12 +446,19 @@ class DDPG:
         if self.device.type != "cuda":
             critic_t.eval()
             return critic_t(s2, actor_t(s2)).squeeze(-1)
+        return self._target_kernel()(s2)
+
+    def _target_kernel(self):
+        """The fused target kernel (critic_kernel.TargetQKernel) on packs that
+        are current for the nets it reads."""
         if self._tq is None:
             from .critic_kernel import TargetQKernel
+            actor_t = self.target_actor if self.tau is not None else self.model_actor
+            critic_t = self.target_critic if self.tau is not None else self.model_critic
             self._tq = TargetQKernel(actor_t, critic_t)
         elif self.tau is None:
             self._tq.refresh()  # online nets moved since the last call
-        return self._tq(s2)
+        return self._tq
 
     @torch.no_grad()
     def soft_update(self):
@@ -644,12 +696,12 @@ class TickGraph:
         self.stream.synchronize()
         self.graph = torch.cuda.CUDAGraph()
         self.graph.register_generator_state(L.gen)
-        mirror = (L.replay.head, L.replay.size)  # capture records the inserts without running them
+        mirror = L.replay.total  # capture records the inserts without running them
         with torch.cuda.graph(self.graph, stream=self.stream):
             for _ in range(self.ticks):
                 self._tick(update=True)
         self.stream.synchronize()
-        L.replay.head, L.replay.size = mirror
+        L.replay.total = mirror
         self.replays = 0
 
     def _tick(self, update):
@@ -666,7 +718,7 @@ class TickGraph:
         o = L.game_environment.step(self.act, obs=True, reward="looking", auto_reset=True, reset_obs=True,
                                     out=self.out)
         L.replay.add_dev(x, a, o["reward"].view(-1), o["obs"].view(-1, STATE_DIM),
-                         o["done"].view(1, -1).expand(2, -1))  # done per (player, game) row
+                         o["done"])  # per game: row r of the [2N] rows takes game r % N
         self.obs.copy_(o["obs_reset"])
         if update:
             for _ in range(self.updates):
@@ -685,5 +737,4 @@ class TickGraph:
         self.replays += n
         # host mirrors of the ring (2N rows per tick)
         r, rows = self.L.replay, n * self.ticks * 2 * self.obs.shape[1]
-        r.head = (r.head + rows) % r.cap
-        r.size = min(r.cap, r.size + rows)
+        r.total += rows
