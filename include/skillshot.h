@@ -305,23 +305,41 @@ int sk_replay_sample(const float* ring, int64_t capacity, const int64_t* total, 
  *                   formulation) on flat param / exp_avg / exp_avg_sq with
  *                   the step count *step_counter (advanced by the grad
  *                   kernels: step_counters[0 .. n_steps) += 1), then
- *                   target (nullable) += tau (param - target).
+ *                   target (nullable) += tau (param - target); and, when
+ *                   applying, *stat_out = *stat_acc * stat_scale, *stat_acc
+ *                   = 0 (the gradient kernel's loss accumulator) and
+ *                   ++*counter (its dropout call number), each nullable.
  * MFMA with bf16 operands and fp32 accumulation; batch-major rows; obs
  * float[batch][12], actions float[batch][2], targets float[batch]. */
 size_t sk_grad_packed_bytes(void);
 int64_t sk_update_partials(int64_t batch);
 int sk_grad_pack(const float* W1, const float* b1, const float* W2, int32_t ld2, const float* b2, const float* W3,
                  const float* b3, int32_t n_out, void* packed, void* stream);
+/* sk_grad_pack for up to 4 nets in one launch, each given as its flat fp32
+ * parameter vector in torch parameters() order (W1, b1, W2, b2, W3, b3);
+ * flats / ld2s / n_outs / outs are host arrays of n_nets entries. */
+int sk_grad_pack_flat(const float* const* flats, const int32_t* ld2s, const int32_t* n_outs, void* const* outs,
+                      int32_t n_nets, void* stream);
 int sk_critic_grad(const void* critic_gpack, const float* obs, const float* actions, const float* targets,
                    int64_t batch, float grad_scale, uint64_t seed, const int64_t* call_counter, float* partials,
                    float* step_counters, int32_t n_steps, float* loss_sum, uint8_t* dropout_mask, void* stream);
+/* sk_critic_grad with the DDPG target computed in the same launch: targets
+ * = rewards + gamma (1 - done) Q'(next_obs, mu'(next_obs)) with the target
+ * nets given as grad packs (targets may be NULL; next_obs float[batch][12],
+ * rewards / done float[batch]). */
+int sk_critic_grad_bootstrap(const void* critic_gpack, const float* obs, const float* actions, const float* targets,
+                             const float* next_obs, const float* rewards, const float* done, float gamma,
+                             const void* target_actor_gpack, const void* target_critic_gpack, int64_t batch,
+                             float grad_scale, uint64_t seed, const int64_t* call_counter, float* partials,
+                             float* step_counters, int32_t n_steps, float* loss_sum, uint8_t* dropout_mask,
+                             void* stream);
 int sk_actor_grad(const void* actor_gpack, const void* critic_gpack, const float* obs, int64_t batch,
                   float loss_scale, float* partials, float* step_counters, int32_t n_steps, float* q_sum,
                   void* stream);
 int sk_adam_flat(const float* partials, int32_t n_partials, int32_t n_params, const float* grad_in,
                  float* grad_out, int32_t apply, float* param, float* exp_avg, float* exp_avg_sq,
                  const float* step_counter, float lr, float beta1, float beta2, float eps, float* target, float tau,
-                 void* stream);
+                 float* stat_acc, float stat_scale, float* stat_out, int64_t* counter, void* stream);
 
 #ifdef __cplusplus
 }

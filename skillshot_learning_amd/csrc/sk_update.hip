@@ -107,9 +107,9 @@ __device__ __forceinline__ void store_t4(short* XT, int ld, int col, int row, fl
 // ---------------------------------------------------------------- pack
 // W1 [256][12], W2 [128][ld2] (first 256 columns on MFMA; critic: columns
 // 256, 257 are the action), W3 [n_out][128]
-__global__ void k_grad_pack(const float* W1, const float* b1, const float* W2, int ld2, const float* b2,
-                            const float* W3, const float* b3, int n_out, char* out) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void grad_pack_body(int t, const float* W1, const float* b1, const float* W2, int ld2,
+                                               const float* b2, const float* W3, const float* b3, int n_out,
+                                               char* out) {
   if (t < 8 * 64) {  // W1: B operand of layer 1 (n = hidden unit, k = input)
     short* o = (short*)(out + kGW1) + t * 8;
     const int nt = t >> 6, lane = t & 63;
@@ -141,10 +141,35 @@ __global__ void k_grad_pack(const float* W1, const float* b1, const float* W2, i
 }
 constexpr int kPackThreads = 8 * 64 + 2 * 64 * 64 + 1024;
 
+__global__ void k_grad_pack(const float* W1, const float* b1, const float* W2, int ld2, const float* b2,
+                            const float* W3, const float* b3, int n_out, char* out) {
+  grad_pack_body(blockIdx.x * blockDim.x + threadIdx.x, W1, b1, W2, ld2, b2, W3, b3, n_out, out);
+}
+
+// up to 4 nets stored flat in torch parameters() order (W1 [256][12], b1,
+// W2 [128][ld2], b2, W3 [n_out][128], b3), one per blockIdx.y
+struct PackJobs {
+  const float* flat[4];
+  char* out[4];
+  int ld2[4];
+  int n_out[4];
+};
+
+__global__ void k_grad_pack_flat(PackJobs j) {
+  const int y = blockIdx.y;
+  const float* f = j.flat[y];
+  const int ld2 = j.ld2[y];
+  const float* W2 = f + kPW2;
+  const float* b2 = W2 + kH2 * ld2;
+  const float* W3 = b2 + kH2;
+  grad_pack_body(blockIdx.x * blockDim.x + threadIdx.x, f + kPW1, f + kPB1, W2, ld2, b2, W3, W3 + j.n_out[y] * kH2,
+                 j.n_out[y], j.out[y]);
+}
+
 // ---------------------------------------------------------------- shared pieces
 struct Lds {
-  short *Sr, *ST, *H1, *H1T, *DZ2, *DZ2T, *DZ1T, *H1C;
-  float *H2f, *DZC, *A, *Y, *DQ, *DZ3, *RED;
+  short *Sr, *ST, *H1, *H1T, *DZ2, *DZ2T, *DZ1T, *H1C, *S2r;
+  float *H2f, *DZC, *A, *Y, *DQ, *DZ3, *RED, *A2, *RB, *DB;
 };
 
 __device__ __forceinline__ Lds carve(char* smem, bool actor) {
@@ -163,6 +188,10 @@ __device__ __forceinline__ Lds carve(char* smem, bool actor) {
   L.DQ = (float*)p;   p += 32 * 4;
   L.DZ3 = (float*)p;  p += 64 * 4;
   L.RED = (float*)p;  p += 4 * 4;
+  L.S2r = (short*)p;  p += 32 * kLdS * 2;  // bootstrap target: s', mu'(s'), r, done
+  L.A2 = (float*)p;   p += 64 * 4;
+  L.RB = (float*)p;   p += 32 * 4;
+  L.DB = (float*)p;   p += 32 * 4;
   L.H1C = nullptr;
   L.DZC = nullptr;
   if (actor) {
@@ -172,7 +201,8 @@ __device__ __forceinline__ Lds carve(char* smem, bool actor) {
   return L;
 }
 constexpr size_t kLdsBase = 32 * kLdS * 2 + 32 * kLdT * 2 + 32 * kLdH1 * 2 + kH1 * kLdT * 2 + 32 * kLdZ2 * 2 +
-                            kH2 * kLdT * 2 + kH1 * kLdT * 2 + 32 * kLdH2f * 4 + (64 + 32 + 32 + 64 + 4) * 4;
+                            kH2 * kLdT * 2 + kH1 * kLdT * 2 + 32 * kLdH2f * 4 + (64 + 32 + 32 + 64 + 4) * 4 +
+                            32 * kLdS * 2 + (64 + 32 + 32) * 4;
 constexpr size_t kLdsCritic = kLdsBase;
 constexpr size_t kLdsActor = kLdsBase + 32 * kLdH1 * 2 + 32 * kLdH2f * 4;
 
@@ -191,11 +221,11 @@ __device__ __forceinline__ void load_states(const Lds& L, const float* S, int64_
 // layer 1 of one net for n-tile nt: relu(S W1^T + b1) -> batch-major (and,
 // if HT, transposed) bf16; `drop` applies the critic's training Dropout
 template <bool DROP>
-__device__ __forceinline__ void layer1(const Lds& L, const bf16x8* gW1, const float* tail, int nt, int lane,
+__device__ __forceinline__ void layer1(const short* Sx, const bf16x8* gW1, const float* tail, int nt, int lane,
                                        short* H, short* HT, uint64_t seed, uint64_t call, int64_t row0,
                                        uint8_t* mask_out, int64_t B) {
   f32x16 acc = {0};
-  acc = mfma(lfrag(L.Sr, kLdS, 0, 0, lane), gW1[nt * 64 + lane], acc);
+  acc = mfma(lfrag(Sx, kLdS, 0, 0, lane), gW1[nt * 64 + lane], acc);
   const int n = 32 * nt + (lane & 31);
   const float b = tail[kTB1 + n];
 #pragma unroll
@@ -293,6 +323,60 @@ __device__ __forceinline__ void store_w12(float* P, int ld2, int w, int lane, co
   if (lane < 32) P[kPB1 + 32 * w + lane] = b;
 }
 
+// ---------------------------------------------------------------- bootstrap target
+// y = r + gamma (1 - done) Q'(s', mu'(s')) for the sub-tile's rows with the
+// target nets' grad packs (the same batch-major layers as the steps), into
+// L.Y; uses H1 / H2f as scratch (they are rewritten by the step after it).
+// Inputs in L.S2r, L.RB, L.DB; all threads of the workgroup call it.
+__device__ __forceinline__ void bootstrap_target(const Lds& L, const char* tap, const char* tcp, float gamma, int w,
+                                                 int lane) {
+  asm volatile("" : "+s"(tap), "+s"(tcp));  // no LICM of the fragment loads out of the sub-tile loop
+  const bf16x8* aW1 = (const bf16x8*)(tap + kGW1);
+  const bf16x8* aW2 = (const bf16x8*)(tap + kGW2);
+  const float* at = (const float*)(tap + kGTail);
+  const bf16x8* cW1 = (const bf16x8*)(tcp + kGW1);
+  const bf16x8* cW2 = (const bf16x8*)(tcp + kGW2);
+  const float* ct = (const float*)(tcp + kGTail);
+  const bool l2 = w < 4;
+  const int u = 32 * (w & 3) + (lane & 31);
+  __syncthreads();  // S2r in
+  layer1<false>(L.S2r, aW1, at, w, lane, L.H1, nullptr, 0, 0, 0, nullptr, 0);
+  __syncthreads();
+  if (l2) {
+    const f32x16 acc = layer2(L.H1, aW2, w, lane);
+    const float b2 = at[kTB2 + u];
+#pragma unroll
+    for (int v = 0; v < 16; ++v) L.H2f[drow(v, lane) * kLdH2f + u] = fmaxf(acc[v] + b2, 0.f);
+  }
+  __syncthreads();
+  {  // mu'(s')
+    const int i = threadIdx.x >> 4, c = threadIdx.x & 15;
+    const float z0 = row_dot128(L.H2f, kLdH2f, at + kTW3, 1);
+    const float z1 = row_dot128(L.H2f, kLdH2f, at + kTW3 + kH2, 1);
+    if (c < 2) L.A2[2 * i + c] = tanhf((c ? z1 : z0) + at[kTB3 + c]);
+  }
+  __syncthreads();
+  layer1<false>(L.S2r, cW1, ct, w, lane, L.H1, nullptr, 0, 0, 0, nullptr, 0);
+  __syncthreads();
+  if (l2) {  // Q' terms relu(z2) W3 per (row, unit)
+    const f32x16 acc = layer2(L.H1, cW2, w, lane);
+    const float b2 = ct[kTB2 + u], wa0 = ct[kTW2a + 2 * u], wa1 = ct[kTW2a + 2 * u + 1], w3 = ct[kTW3 + u];
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const int i = drow(v, lane);
+      const float z = acc[v] + b2 + L.A2[2 * i] * wa0 + L.A2[2 * i + 1] * wa1;
+      L.H2f[i * kLdH2f + u] = fmaxf(z, 0.f) * w3;
+    }
+  }
+  __syncthreads();
+  {
+    const int i = threadIdx.x >> 4;
+    const float q = ct[kTB3] + row_sum128(L.H2f, kLdH2f);
+    if ((threadIdx.x & 15) == 0) L.Y[i] = L.RB[i] + gamma * (1.f - L.DB[i]) * q;
+  }
+  __syncthreads();
+}
+
 // ---------------------------------------------------------------- critic step
 // Critic.forward in train mode + F.mse_loss(q, y) backward
 // (DDPG.critic_step; critic.fit, SkillshotLearner.py:434): dL/dq =
@@ -303,7 +387,10 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad(const float* __restric
                                                           const int64_t* __restrict__ call_ctr,
                                                           const char* __restrict__ gpack, float* __restrict__ partial,
                                                           float* step_ctr, int n_steps, float* __restrict__ loss_out,
-                                                          uint8_t* __restrict__ mask_out) {
+                                                          uint8_t* __restrict__ mask_out, const float* __restrict__ S2,
+                                                          const float* __restrict__ R, const float* __restrict__ D,
+                                                          float gamma, const char* __restrict__ tapack,
+                                                          const char* __restrict__ tcpack) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const Lds L = carve(smem, false);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5;
@@ -334,9 +421,22 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad(const float* __restric
     asm volatile("" : "+s"(fW1), "+s"(fW2), "+s"(fW2T), "+s"(tail));
     load_states(L, S, row0, B);
     if (threadIdx.x < 64) L.A[threadIdx.x] = row0 + (threadIdx.x >> 1) < B ? A[row0 * 2 + threadIdx.x] : 0.f;
-    if (threadIdx.x < 32) L.Y[threadIdx.x] = row0 + threadIdx.x < B ? Y[row0 + threadIdx.x] : 0.f;
+    if (tapack) {  // the DDPG target y = r + gamma (1 - done) Q'(s', mu'(s')) of this sub-tile, in LDS
+      for (int t = threadIdx.x; t < 32 * 16; t += kThreads) {
+        const int i = t >> 4, k = t & 15;
+        L.S2r[i * kLdS + k] = f2bf((k < kIn && row0 + i < B) ? S2[(row0 + i) * kIn + k] : 0.f);
+      }
+      if (threadIdx.x < 32) {
+        const bool ok = row0 + threadIdx.x < B;
+        L.RB[threadIdx.x] = ok ? R[row0 + threadIdx.x] : 0.f;
+        L.DB[threadIdx.x] = ok ? D[row0 + threadIdx.x] : 0.f;
+      }
+      bootstrap_target(L, tapack, tcpack, gamma, w, lane);
+    } else if (threadIdx.x < 32) {
+      L.Y[threadIdx.x] = row0 + threadIdx.x < B ? Y[row0 + threadIdx.x] : 0.f;
+    }
     __syncthreads();
-    layer1<true>(L, fW1, tail, w, lane, L.H1, L.H1T, seed, call, row0, mask_out, B);
+    layer1<true>(L.Sr, fW1, tail, w, lane, L.H1, L.H1T, seed, call, row0, mask_out, B);
     __syncthreads();
     float h2v[16];
     if (l2) {
@@ -444,8 +544,8 @@ __global__ void __launch_bounds__(kThreads) k_actor_grad(const float* __restrict
     const float* ct = (const float*)(cp + kGTail);
     load_states(L, S, row0, B);
     __syncthreads();
-    layer1<false>(L, aW1, at, w, lane, L.H1, L.H1T, 0, 0, 0, nullptr, B);
-    layer1<false>(L, cW1, ct, w, lane, L.H1C, nullptr, 0, 0, 0, nullptr, B);
+    layer1<false>(L.Sr, aW1, at, w, lane, L.H1, L.H1T, 0, 0, 0, nullptr, B);
+    layer1<false>(L.Sr, cW1, ct, w, lane, L.H1C, nullptr, 0, 0, 0, nullptr, B);
     __syncthreads();
     if (l2) {  // actor h2 -> H2f (fp32, kept for the backward)
       const f32x16 acc = layer2(L.H1, aW2, w, lane);
@@ -541,11 +641,23 @@ __global__ void __launch_bounds__(kThreads) k_actor_grad(const float* __restrict
 // (1-b2) g^2, p -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps), t = the
 // step counter (advanced by the grad kernel).  Then target += tau (p -
 // target) (torch._foreach_lerp_, DDPG.soft_update) when a target is given.
+// Housekeeping of the step, by thread 0 when applying (after the gradient
+// kernel consumed them, before the next one): stat_out = stat_acc * scale and
+// stat_acc = 0 (the loss accumulator of the gradient kernel), ++*counter (its
+// dropout call number) — one launch fewer each than torch ops would cost.
 __global__ void k_adam_flat(const float* __restrict__ partial, int G, int P, const float* __restrict__ grad_in,
                             float* __restrict__ grad_out, int apply, float* __restrict__ param, float* __restrict__ m,
                             float* __restrict__ v, const float* __restrict__ step_ctr, float lr, float beta1,
-                            float beta2, float eps, float* __restrict__ target, float tau) {
+                            float beta2, float eps, float* __restrict__ target, float tau, float* stat_acc,
+                            float stat_scale, float* stat_out, int64_t* counter) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (apply && p == 0) {
+    if (stat_acc) {
+      if (stat_out) *stat_out = *stat_acc * stat_scale;
+      *stat_acc = 0.f;
+    }
+    if (counter) *counter += 1;
+  }
   if (p >= P) return;
   float g = grad_in ? grad_in[p] : 0.f;
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // 8 independent loads in flight
@@ -587,6 +699,22 @@ extern "C" {
 
 size_t sk_grad_packed_bytes(void) { return kGPackBytes; }
 
+int sk_grad_pack_flat(const float* const* flats, const int32_t* ld2s, const int32_t* n_outs, void* const* outs,
+                      int32_t n_nets, void* stream) {
+  if (!flats || !ld2s || !n_outs || !outs || n_nets < 1 || n_nets > 4) return SK_EINVAL;
+  PackJobs j = {};
+  for (int k = 0; k < n_nets; ++k) {
+    if (!flats[k] || !outs[k] || (((uintptr_t)outs[k]) & 15)) return SK_EINVAL;
+    if ((ld2s[k] != kH1 && ld2s[k] != kH1 + 2) || (n_outs[k] != 1 && n_outs[k] != 2)) return SK_EINVAL;
+    j.flat[k] = flats[k];
+    j.out[k] = (char*)outs[k];
+    j.ld2[k] = ld2s[k];
+    j.n_out[k] = n_outs[k];
+  }
+  k_grad_pack_flat<<<dim3((kPackThreads + 255) / 256, n_nets), 256, 0, (hipStream_t)stream>>>(j);
+  return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
+}
+
 int64_t sk_update_partials(int64_t batch) {
   if (batch <= 0) return 0;
   const int64_t spw = subtiles_per_wg(batch);
@@ -605,7 +733,22 @@ int sk_grad_pack(const float* W1, const float* b1, const float* W2, int32_t ld2,
 int sk_critic_grad(const void* cpack, const float* obs, const float* actions, const float* targets, int64_t batch,
                    float grad_scale, uint64_t seed, const int64_t* call_counter, float* partial, float* step_counters,
                    int32_t n_steps, float* loss_sum, uint8_t* dropout_mask, void* stream) {
-  if (!cpack || !obs || !actions || !targets || !call_counter || !partial || batch <= 0) return SK_EINVAL;
+  return sk_critic_grad_bootstrap(cpack, obs, actions, targets, nullptr, nullptr, nullptr, 0.f, nullptr, nullptr,
+                                  batch, grad_scale, seed, call_counter, partial, step_counters, n_steps, loss_sum,
+                                  dropout_mask, stream);
+}
+
+int sk_critic_grad_bootstrap(const void* cpack, const float* obs, const float* actions, const float* targets,
+                             const float* next_obs, const float* rewards, const float* done, float gamma,
+                             const void* target_actor_gpack, const void* target_critic_gpack, int64_t batch,
+                             float grad_scale, uint64_t seed, const int64_t* call_counter, float* partial,
+                             float* step_counters, int32_t n_steps, float* loss_sum, uint8_t* dropout_mask,
+                             void* stream) {
+  const bool boot = target_actor_gpack != nullptr;
+  if (boot && (!target_critic_gpack || !next_obs || !rewards || !done)) return SK_EINVAL;
+  if (!boot && !targets) return SK_EINVAL;
+  if (boot && ((((uintptr_t)target_actor_gpack) & 15) || (((uintptr_t)target_critic_gpack) & 15))) return SK_EINVAL;
+  if (!cpack || !obs || !actions || !call_counter || !partial || batch <= 0) return SK_EINVAL;
   if ((n_steps > 0 && !step_counters) || n_steps < 0 || n_steps > 64) return SK_EINVAL;
   if ((((uintptr_t)cpack) & 15) || (((uintptr_t)obs) & 3) || (((uintptr_t)actions) & 3)) return SK_EINVAL;
   static bool attr = false;
@@ -615,9 +758,10 @@ int sk_critic_grad(const void* cpack, const float* obs, const float* actions, co
   }
   const int64_t spw = subtiles_per_wg(batch);
   const unsigned G = (unsigned)sk_update_partials(batch);
-  k_critic_grad<<<G, kThreads, kLdsCritic, (hipStream_t)stream>>>(obs, actions, targets, batch, (int)spw, grad_scale,
-                                                                   seed, call_counter, (const char*)cpack, partial,
-                                                                   step_counters, n_steps, loss_sum, dropout_mask);
+  k_critic_grad<<<G, kThreads, kLdsCritic, (hipStream_t)stream>>>(
+      obs, actions, targets, batch, (int)spw, grad_scale, seed, call_counter, (const char*)cpack, partial,
+      step_counters, n_steps, loss_sum, dropout_mask, next_obs, rewards, done, gamma,
+      (const char*)target_actor_gpack, (const char*)target_critic_gpack);
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
 }
 
@@ -641,13 +785,14 @@ int sk_actor_grad(const void* apack, const void* cpack, const float* obs, int64_
 
 int sk_adam_flat(const float* partial, int32_t n_partials, int32_t n_params, const float* grad_in, float* grad_out,
                  int32_t apply, float* param, float* exp_avg, float* exp_avg_sq, const float* step_counter, float lr,
-                 float beta1, float beta2, float eps, float* target, float tau, void* stream) {
+                 float beta1, float beta2, float eps, float* target, float tau, float* stat_acc, float stat_scale,
+                 float* stat_out, int64_t* counter, void* stream) {
   if (n_params <= 0 || n_partials < 0 || (n_partials > 0 && !partial)) return SK_EINVAL;
   if (apply && (!param || !exp_avg || !exp_avg_sq || !step_counter)) return SK_EINVAL;
   k_adam_flat<<<(n_params + 255) / 256, 256, 0, (hipStream_t)stream>>>(partial, n_partials, n_params, grad_in,
                                                                        grad_out, apply, param, exp_avg, exp_avg_sq,
                                                                        step_counter, lr, beta1, beta2, eps, target,
-                                                                       tau);
+                                                                       tau, stat_acc, stat_scale, stat_out, counter);
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
 }
 

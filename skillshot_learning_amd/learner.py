@@ -419,6 +419,12 @@ class DDPG:
         else:
             s, a, r, s2, d = self.replay.sample(batch, generator=self.gen)
         s, a, r, s2, d = self._allgather_batch(s, a, r, s2, d)
+        if self._fused is not None:  # target, critic step, actor step, soft updates: 4 launches + 2 pack launches
+            if self.gamma > 0.0:
+                lc = self._fused.critic_step(s, a, s2=s2, r=r, d=d, gamma=self.gamma)
+            else:
+                lc = self._fused.critic_step(s, a, r)
+            return lc, self._fused.actor_step(s)
         target = r
         if self.gamma > 0.0:
             with torch.no_grad():
@@ -429,11 +435,7 @@ class DDPG:
         lc = self.critic_step(s, a, target)
         la = self.model_actor_fit_step(s)
         if self.tau is not None:
-            if self._fused is not None:  # the Adam kernels already moved the targets
-                if self._tq is not None:
-                    self._tq.refresh()
-            else:
-                self.soft_update()
+            self.soft_update()
         return lc, la
 
     @torch.no_grad()
@@ -456,8 +458,8 @@ class DDPG:
             actor_t = self.target_actor if self.tau is not None else self.model_actor
             critic_t = self.target_critic if self.tau is not None else self.model_critic
             self._tq = TargetQKernel(actor_t, critic_t)
-        elif self.tau is None:
-            self._tq.refresh()  # online nets moved since the last call
+        elif self.tau is None or self._fused is not None:
+            self._tq.refresh()  # the nets it reads moved since the last call
         return self._tq
 
     @torch.no_grad()
@@ -679,11 +681,15 @@ class TickGraph:
         g = L.game_environment
         n = L.n_envs
         dev = L.device
-        self.obs = L.prepare_states().clone()
+        # the acting observation alternates between two buffers: tick t reads
+        # one and the step writes its reset observations into the other (no
+        # copy); a replay has an even number of ticks, so it ends where it began
+        self._obs = [L.prepare_states().clone(), g.new_obs()]
+        self._cur = 0
         self.act = torch.empty((2, n, ACTION_DIM), dtype=torch.float32, device=dev)
         self.out = dict(obs=g.new_obs(), reward=torch.empty((2, n), dtype=torch.float32, device=dev),
                         done=torch.empty(n, dtype=torch.uint8, device=dev),
-                        winner=torch.empty(n, dtype=torch.uint8, device=dev), obs_reset=g.new_obs())
+                        winner=torch.empty(n, dtype=torch.uint8, device=dev), obs_reset=self._obs[1])
         self.stream = torch.cuda.Stream(device=dev)
         self.stream.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(self.stream):
@@ -693,6 +699,9 @@ class TickGraph:
                 self._tick(update=False)
             for _ in range(max(warmup, 1)):
                 self._tick(update=True)
+            if self._cur:  # start the captured ticks from buffer 0
+                self._obs[0].copy_(self._obs[1])
+                self._cur = 0
         self.stream.synchronize()
         self.graph = torch.cuda.CUDAGraph()
         self.graph.register_generator_state(L.gen)
@@ -704,9 +713,16 @@ class TickGraph:
         L.replay.total = mirror
         self.replays = 0
 
+    @property
+    def obs(self):
+        """the observation the next tick acts on"""
+        return self._obs[self._cur]
+
     def _tick(self, update):
         L = self.L
-        x = self.obs.view(-1, STATE_DIM)
+        obs = self._obs[self._cur]
+        self.out["obs_reset"] = self._obs[1 - self._cur]
+        x = obs.view(-1, STATE_DIM)
         a = self.act.view(-1, ACTION_DIM)
         mode = L.exploration
         if L.actor_kernel is not None:
@@ -714,12 +730,12 @@ class TickGraph:
             if mode == "action_noise":
                 a.add_(L.action_noise_sd * torch.randn(a.shape, device=a.device, generator=L.gen))
         else:
-            a.copy_(L.model_act(self.obs).view(-1, ACTION_DIM))
+            a.copy_(L.model_act(obs).view(-1, ACTION_DIM))
         o = L.game_environment.step(self.act, obs=True, reward="looking", auto_reset=True, reset_obs=True,
                                     out=self.out)
         L.replay.add_dev(x, a, o["reward"].view(-1), o["obs"].view(-1, STATE_DIM),
                          o["done"])  # per game: row r of the [2N] rows takes game r % N
-        self.obs.copy_(o["obs_reset"])
+        self._cur ^= 1
         if update:
             for _ in range(self.updates):
                 L.ddpg.replay_update(self.batch, device_sampling=True)

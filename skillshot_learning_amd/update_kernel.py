@@ -84,6 +84,8 @@ class _AdamState:
 class FusedUpdate:
     """Kernel path of DDPG.critic_step / model_actor_fit_step (+ soft update)."""
 
+    LOSS_HIST = 1024
+
     def __init__(self, ddpg, seed=0):
         self.d = ddpg
         self.L = _capi.load()
@@ -100,9 +102,18 @@ class FusedUpdate:
         nb = int(self.L.sk_grad_packed_bytes())
         self.gpa = torch.empty(nb, dtype=torch.uint8, device=dev)
         self.gpc = torch.empty(nb, dtype=torch.uint8, device=dev)
+        # target nets' packs (the bootstrap target inside the critic step)
+        self.gpta = torch.empty(nb, dtype=torch.uint8, device=dev) if self.ta is not None else self.gpa
+        self.gptc = torch.empty(nb, dtype=torch.uint8, device=dev) if self.tc is not None else self.gpc
         self.seed = int(seed) & ((1 << 64) - 1)
-        self.calls = torch.zeros(1, dtype=torch.int64, device=dev)  # dropout call number (device, capturable)
-        self.stats = torch.zeros(2, dtype=torch.float32, device=dev)  # [sum (q-y)^2, sum Q]
+        # dropout call number and loss accumulators [sum (q-y)^2, sum Q] on
+        # device; the Adam launch advances / reads-and-clears them, and writes
+        # the step's loss into a history slot (the returned device scalar
+        # stays valid for LOSS_HIST further steps)
+        self.calls = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.stats = torch.zeros(2, dtype=torch.float32, device=dev)
+        self.loss_hist = torch.zeros(2, self.LOSS_HIST, dtype=torch.float32, device=dev)
+        self._li = [0, 0]
         self._partials = {}
         self.grad_flat = None
         self.pack()
@@ -123,12 +134,33 @@ class FusedUpdate:
                                  _p(m.l3.weight), _p(m.l3.bias), n_out, _p(buf), self._stream())
         _capi.check(rc)
 
+    def _pack_flat(self, jobs):
+        """one launch packing [(flat params, ld2, n_out, out buffer)]"""
+        k = len(jobs)
+        flats = (ctypes.c_void_p * k)(*[f.data_ptr() for f, _, _, _ in jobs])
+        ld2s = (ctypes.c_int32 * k)(*[l for _, l, _, _ in jobs])
+        nouts = (ctypes.c_int32 * k)(*[n for _, _, n, _ in jobs])
+        outs = (ctypes.c_void_p * k)(*[o.data_ptr() for _, _, _, o in jobs])
+        _capi.check(self.L.sk_grad_pack_flat(flats, ld2s, nouts, outs, k, self._stream()))
+
+    def _after_actor_jobs(self):
+        """the packs that change with the actor step (actor) and the soft updates
+        of both targets, packed in one launch after the actor's Adam"""
+        jobs = [(self.fa, 256, 2, self.gpa)]
+        if self.ta is not None:
+            jobs += [(self.ta, 256, 2, self.gpta), (self.tc, 258, 1, self.gptc)]
+        return jobs
+
     @torch.no_grad()
     def pack(self):
-        self._pack(self.d.model_actor, self.gpa, 256, 2)
-        self._pack(self.d.model_critic, self.gpc, 258, 1)
+        self._pack_flat(self._after_actor_jobs() + [(self.fc, 258, 1, self.gpc)])
 
-    def _adam(self, part, flat, st, target):
+    def _loss_slot(self, k):
+        i = self._li[k]
+        self._li[k] = (i + 1) % self.LOSS_HIST
+        return self.loss_hist[k, i]
+
+    def _adam(self, part, flat, st, target, stat=None, scale=1.0, out=None, counter=None):
         P = flat.numel()
         tau = float(self.d.tau) if target is not None else 0.0
         world = self.d.world()
@@ -137,33 +169,43 @@ class FusedUpdate:
                 self.grad_flat = torch.empty(max(36609, P), dtype=torch.float32, device=self.dev)
             g = self.grad_flat[:P]
             _capi.check(self.L.sk_adam_flat(_p(part), part.shape[0], P, None, _p(g), 0, None, None, None, None,
-                                            0.0, 0.0, 0.0, 0.0, None, 0.0, self._stream()))
+                                            0.0, 0.0, 0.0, 0.0, None, 0.0, None, 0.0, None, None, self._stream()))
             dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.d.group)
             g /= world
             _capi.check(self.L.sk_adam_flat(None, 0, P, _p(g), None, 1, _p(flat), _p(st.m), _p(st.v), _p(st.steps),
-                                            st.lr, st.b1, st.b2, st.eps, _p(target), tau, self._stream()))
+                                            st.lr, st.b1, st.b2, st.eps, _p(target), tau, _p(stat), float(scale),
+                                            _p(out), _p(counter), self._stream()))
         else:
             _capi.check(self.L.sk_adam_flat(_p(part), part.shape[0], P, None, None, 1, _p(flat), _p(st.m), _p(st.v),
-                                            _p(st.steps), st.lr, st.b1, st.b2, st.eps, _p(target), tau,
-                                            self._stream()))
+                                            _p(st.steps), st.lr, st.b1, st.b2, st.eps, _p(target), tau, _p(stat),
+                                            float(scale), _p(out), _p(counter), self._stream()))
 
     @torch.no_grad()
-    def critic_step(self, s, a, target, mask_out=None):
-        """One critic Adam step on MSE(Q(s, a), target), Dropout active; returns
-        the loss (device scalar)."""
-        s, a, y = s.float().contiguous(), a.float().contiguous(), target.float().contiguous()
+    def critic_step(self, s, a, target=None, mask_out=None, s2=None, r=None, d=None, gamma=0.0):
+        """One critic Adam step on MSE(Q(s, a), y), Dropout active; y = target,
+        or, given s2 / r / d, the bootstrap y = r + gamma (1 - d) Q'(s2,
+        mu'(s2)) computed inside the same launch from the target nets.
+        Returns the loss (device scalar)."""
+        s, a = s.float().contiguous(), a.float().contiguous()
         B = s.shape[0]
         part = self._partial(B, self.fc.numel())
-        self.calls.add_(1)
-        self.stats.zero_()
         st = self.sc
-        rc = self.L.sk_critic_grad(_p(self.gpc), _p(s), _p(a), _p(y), B, 2.0 / B, self.seed, _p(self.calls),
-                                   _p(part), _p(st.steps), st.steps.numel(), _p(self.stats), _p(mask_out),
-                                   self._stream())
+        if s2 is not None:
+            s2c, rc_, dc = s2.float().contiguous(), r.float().contiguous(), d.float().contiguous()
+            rc = self.L.sk_critic_grad_bootstrap(
+                _p(self.gpc), _p(s), _p(a), None, _p(s2c), _p(rc_), _p(dc), float(gamma), _p(self.gpta),
+                _p(self.gptc), B, 2.0 / B, self.seed, _p(self.calls), _p(part), _p(st.steps), st.steps.numel(),
+                _p(self.stats[0:1]), _p(mask_out), self._stream())
+        else:
+            y = target.float().contiguous()
+            rc = self.L.sk_critic_grad(_p(self.gpc), _p(s), _p(a), _p(y), B, 2.0 / B, self.seed, _p(self.calls),
+                                       _p(part), _p(st.steps), st.steps.numel(), _p(self.stats[0:1]), _p(mask_out),
+                                       self._stream())
         _capi.check(rc)
-        self._adam(part, self.fc, st, self.tc)
+        loss = self._loss_slot(0)
+        self._adam(part, self.fc, st, self.tc, stat=self.stats[0:1], scale=1.0 / B, out=loss, counter=self.calls)
         self._pack(self.d.model_critic, self.gpc, 258, 1)
-        return self.stats[0] / B
+        return loss
 
     @torch.no_grad()
     def actor_step(self, s):
@@ -172,27 +214,33 @@ class FusedUpdate:
         s = s.float().contiguous()
         B = s.shape[0]
         part = self._partial(B, self.fa.numel())
-        self.stats.zero_()
         st = self.sa
         rc = self.L.sk_actor_grad(_p(self.gpa), _p(self.gpc), _p(s), B, 1.0, _p(part), _p(st.steps),
                                   st.steps.numel(), _p(self.stats[1:]), self._stream())
         _capi.check(rc)
-        self._adam(part, self.fa, st, self.ta)
-        self._pack(self.d.model_actor, self.gpa, 256, 2)
-        return -self.stats[1]
+        loss = self._loss_slot(1)
+        self._adam(part, self.fa, st, self.ta, stat=self.stats[1:], scale=-1.0, out=loss)
+        self._pack_flat(self._after_actor_jobs())
+        return loss
 
     @torch.no_grad()
-    def grads(self, which, s, a=None, target=None, mask_out=None):
+    def grads(self, which, s, a=None, target=None, mask_out=None, s2=None, r=None, d=None, gamma=0.0):
         """Test hook: the flat gradient the kernels compute, without stepping
-        (the Adam step counters are restored)."""
+        (the Adam step counters are not touched)."""
         B = s.shape[0]
         if which == "critic":
             flat, st = self.fc, self.sc
             part = self._partial(B, flat.numel())
             self.calls.add_(1)
-            rc = self.L.sk_critic_grad(_p(self.gpc), _p(s.contiguous()), _p(a.contiguous()),
-                                       _p(target.contiguous()), B, 2.0 / B, self.seed, _p(self.calls), _p(part),
-                                       None, 0, None, _p(mask_out), self._stream())
+            if s2 is not None:
+                rc = self.L.sk_critic_grad_bootstrap(
+                    _p(self.gpc), _p(s.contiguous()), _p(a.contiguous()), None, _p(s2.contiguous()),
+                    _p(r.contiguous()), _p(d.contiguous()), float(gamma), _p(self.gpta), _p(self.gptc), B, 2.0 / B,
+                    self.seed, _p(self.calls), _p(part), None, 0, None, _p(mask_out), self._stream())
+            else:
+                rc = self.L.sk_critic_grad(_p(self.gpc), _p(s.contiguous()), _p(a.contiguous()),
+                                           _p(target.contiguous()), B, 2.0 / B, self.seed, _p(self.calls), _p(part),
+                                           None, 0, None, _p(mask_out), self._stream())
         else:
             flat, st = self.fa, self.sa
             part = self._partial(B, flat.numel())
@@ -201,5 +249,5 @@ class FusedUpdate:
         _capi.check(rc)
         g = torch.empty_like(flat)
         _capi.check(self.L.sk_adam_flat(_p(part), part.shape[0], flat.numel(), None, _p(g), 0, None, None, None, None,
-                                        0.0, 0.0, 0.0, 0.0, None, 0.0, self._stream()))
+                                        0.0, 0.0, 0.0, 0.0, None, 0.0, None, 0.0, None, None, self._stream()))
         return g

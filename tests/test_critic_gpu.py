@@ -109,19 +109,22 @@ def test_critic_refresh_tracks_weights(mods):
     assert emu.max().item() < EMU_MAX
 
 
-def test_ddpg_target_uses_fused_kernel(mods):
+@pytest.mark.parametrize("fused_update", [False, True])
+def test_ddpg_target_uses_fused_kernel(mods, fused_update):
     """DDPG.target_q on the GPU (sk_target_q on the packed target nets, kept in
-    step by soft_update) against the torch target nets."""
+    step by soft_update, or repacked on demand after MFMA-update steps that
+    moved the targets inside their Adam launches) against the torch target
+    nets."""
     learner, _, _ = mods
-    d = learner.DDPG("cuda", seed=4, gamma=0.9, tau=0.05, replay_capacity=4096)
+    d = learner.DDPG("cuda", seed=4, gamma=0.9, tau=0.05, replay_capacity=4096, fused_update=fused_update)
     g = torch.Generator(device="cuda").manual_seed(0)
     for _ in range(4):
         d.replay.add(torch.rand(512, 12, device="cuda", generator=g), torch.rand(512, 2, device="cuda") * 2 - 1,
                      torch.randn(512, device="cuda", generator=g), torch.rand(512, 12, device="cuda", generator=g),
                      torch.zeros(512, device="cuda"))
     for _ in range(3):
-        d.replay_update(256)  # creates the kernel, soft-updates and repacks
-    assert d._tq is not None
+        d.replay_update(256)  # autograd path: creates the kernel, soft-updates and repacks
+    assert (d._tq is None) == fused_update  # the MFMA update computes its target in the critic launch
     s2 = _obs(2048)
     got = d.target_q(s2)
     d.target_critic.eval()

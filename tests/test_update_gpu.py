@@ -139,6 +139,36 @@ def test_actor_grad_matches_autograd(mods, rows):
     _check_grads(g, a_mod, [p.grad for p in params], REL_FP32)
 
 
+@pytest.mark.parametrize("rows", [37, 4096 + 17])
+def test_critic_bootstrap_grad_matches_explicit_target(mods, rows):
+    """The in-launch target y = r + gamma (1 - d) Q'(s', mu'(s')) gives the
+    gradient of the step with that target precomputed by fp32 target nets
+    (same Dropout masks)."""
+    learner = mods
+    d = _ddpg(learner, seed=4, tau=0.05)
+    with torch.no_grad():  # targets differ from the online nets
+        for m in (d.target_actor, d.target_critic):
+            for p in m.parameters():
+                p.mul_(1.3)
+    d._fused.pack()
+    s, a = _obs(rows), torch.rand(rows, 2, device="cuda") * 2 - 1
+    s2, r = _obs(rows), torch.randn(rows, device="cuda")
+    done = (torch.rand(rows, device="cuda") < 0.2).float()
+    calls0 = d._fused.calls.clone()
+    g_boot = d._fused.grads("critic", s, a, s2=s2, r=r, d=done, gamma=0.9)
+    with torch.no_grad():
+        d.target_critic.eval()
+        y = r + 0.9 * (1 - done) * d.target_critic(s2, d.target_actor(s2)).squeeze(-1)
+    d._fused.calls.copy_(calls0)  # same Dropout masks
+    g_ref = d._fused.grads("critic", s, a, y)
+    off = 0
+    for name, p in d.model_critic.named_parameters():
+        k = p.numel()
+        e = (g_boot[off:off + k] - g_ref[off:off + k]).norm().item()
+        assert e <= 3e-2 * g_ref[off:off + k].norm().item() + 1e-6, (name, e)
+        off += k
+
+
 def test_adam_and_soft_update_match_torch(mods):
     learner = mods
     torch.manual_seed(0)
