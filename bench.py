@@ -51,6 +51,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-rollout", action="store_true")
+    p.add_argument("--no-large", action="store_true", help="skip the 4 M-game HBM-bound secondary measurement")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_k_step.json"))
     return p.parse_args()
 
@@ -78,6 +79,49 @@ def cpu_baseline(n_envs, seconds, tick_limit, seed):
                 sample=f"C oracle (oracle/skillshot_oracle.c, restatement of the reference step) "
                        f"{n_envs} envs x {steps} ticks ({el:.1f} s, 1 thread); reference Python on the "
                        f"survey host: 59.2k env-steps/s per core (BASELINE.md)")
+
+
+def large_batch_rate(dev, args, rank, n=1 << 22, launches=60, ring=8):
+    """k_step at n games per GPU, graph-replayed, HIP-event timed (HBM-bound
+    regime: 193 B x n per launch)."""
+    import ctypes
+    from skillshot_learning_amd import VecSkillshotGame
+    env = VecSkillshotGame(n, device=dev, seed=args.seed + 1, env_offset=rank * n, tick_limit=args.tick_limit,
+                           random_positions=True)
+    st = torch.cuda.Stream(device=dev)
+    with torch.cuda.stream(st):
+        env.reset(random_positions=True)
+        acts = env.gen_random_actions(ring)
+        done = torch.empty(n, dtype=torch.uint8, device=dev)
+    st.synchronize()
+    slab, sp = 16 * n, ctypes.c_void_p(st.cuda_stream)
+
+    def launch(t):
+        env.step_raw(ctypes.c_void_p(acts.data_ptr() + (t % ring) * slab), ctypes.c_void_p(done.data_ptr()), stream=sp)
+
+    with torch.cuda.stream(st):
+        for t in range(2):
+            launch(t)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=st):
+        for t in range(launches):
+            launch(t)
+    with torch.cuda.stream(st):
+        g.replay()
+    st.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(st):
+        e0.record()
+        g.replay()
+        e1.record()
+    st.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / launches
+    gbs = BYTES_PER_ENV_STEP * n / (us * 1e-6) / 1e9
+    env.close()
+    del acts, done
+    return dict(envs_per_gpu=n, kernel="k_step (auto variant)", us_per_launch=us, env_steps_per_s_per_gpu=n / (us * 1e-6),
+                achieved_gbs=gbs, frac=gbs / HBM_PEAK_GBS,
+                note="state 369 MB > Infinity Cache: the HBM-bound regime; reported beside, not as, the headline")
 
 
 def main():
@@ -197,6 +241,13 @@ def main():
                        env_steps_per_s_per_gpu=n * ticks * reps / (rms * 1e-3),
                        note="state held in registers across ticks; reported beside, not as, the headline")
 
+    # ---- secondary: the same k_step tick at 4 M games per GPU (369 MB of
+    # state: past the 256 MB Infinity Cache, so truly HBM-bound, not
+    # launch-bound) — SURVEY §7 hard part 3; reported beside the headline
+    large = None
+    if not args.no_large:
+        large = large_batch_rate(dev, args, rank)
+
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline(n, args.cpu_seconds, args.tick_limit, args.seed)
@@ -240,6 +291,7 @@ def main():
             "cpu_baseline": cpu,
             "episodes": counters,
             "rollout_random": rollout,
+            "large_batch": large,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

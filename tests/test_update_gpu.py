@@ -239,3 +239,61 @@ def test_fused_tick_graph(mods):
     torch.cuda.synchronize()
     assert all(torch.isfinite(p).all() for p in L.model_actor.parameters())
     assert any((p - q).abs().max() > 0 for p, q in zip(L.model_actor.parameters(), w0))
+
+
+# ------------------------------------------------- 2 ranks on one GPU (gloo)
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_worker(rank, world, port, q):
+    import os
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from skillshot_learning_amd import learner
+        d = learner.DDPG("cuda", seed=200 + rank, tau=0.05, rank_seed_offset=rank, fused_update=True)
+        w0 = torch.cat([p.detach().reshape(-1) for p in d.model_critic.parameters()]).cpu()
+        g = torch.Generator(device="cuda").manual_seed(rank)  # different data per rank
+        for _ in range(3):
+            s = torch.rand(256, 12, device="cuda", generator=g)
+            a = torch.rand(256, 2, device="cuda", generator=g) * 2 - 1
+            y = torch.randn(256, device="cuda", generator=g)
+            d.critic_step(s, a, y)        # gradient all-reduced (mean) over gloo between two Adam launches
+            d.model_actor_fit_step(s)
+        torch.cuda.synchronize()
+        flat = torch.cat([p.detach().reshape(-1) for m in (d.model_actor, d.model_critic, d.target_critic)
+                          for p in m.parameters()]).cpu()
+        q.put((rank, w0.numpy(), flat.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_fused_update_two_ranks_gloo():
+    """The multi-rank branch of the MFMA update (reduce-only Adam launch,
+    all-reduce, apply launch): ranks with different data end with identical
+    weights and targets."""
+    import multiprocessing as mp
+    import numpy as np
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(world):
+        rank, w0, flat = q.get(timeout=240)
+        out[rank] = (w0, flat)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert np.array_equal(out[0][0], out[1][0])  # rank 0's init broadcast
+    assert np.array_equal(out[0][1], out[1][1])  # all-reduced gradients: identical steps
+    assert np.isfinite(out[0][1]).all()
+    assert not np.array_equal(out[0][1][-36609:], out[0][0])  # the target critic moved (soft update)

@@ -20,7 +20,7 @@ rocm-smi --showproductname > $OUT/rocm_smi.txt 2>&1 || true
 python -c "import skillshot_learning_amd as s; s.load_library(); print('lib ok')" || exit 3
 
 if [[ "$STEPS" == all || "$STEPS" == *tests* ]]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > $OUT/pytest_gpu_$TAG.log 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 240 --timeout-method thread > $OUT/pytest_gpu_$TAG.log 2>&1
   rc=$?; tail -25 $OUT/pytest_gpu_$TAG.log; stop_if_fault $rc pytest
 fi
 if [[ "$STEPS" == all || "$STEPS" == *smoke* ]]; then
@@ -33,7 +33,7 @@ if [[ "$STEPS" == all || "$STEPS" == *bench* ]]; then
 fi
 if [[ "$STEPS" == all || "$STEPS" == *prof* ]]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run \
-    -- python3 bench.py --steps 2000 --warmup 200 --no-cpu-baseline > $OUT/prof_bench_$TAG.json 2> $OUT/prof_$TAG.err
+    -- python3 bench.py --steps 2000 --warmup 200 --no-cpu-baseline --no-large > $OUT/prof_bench_$TAG.json 2> $OUT/prof_$TAG.err
   rc=$?; tail -3 $OUT/prof_$TAG.err; stop_if_fault $rc rocprof
   find $OUT/prof_$TAG -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats_$TAG.csv \; 2>/dev/null
   head -20 $OUT/kernel_stats_$TAG.csv 2>/dev/null
