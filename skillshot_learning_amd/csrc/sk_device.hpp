@@ -169,38 +169,6 @@ __device__ __forceinline__ void store_env(const View& v, int64_t i, const Env& e
   v.misc[i] = make_int2(e.ticks, (int)f);
 }
 
-// The per-tick state store of the fused step kernels, write-through: `sc1`
-// stores leave no dirty line in the XCD's L2, so the release that ends every
-// dispatch (the next tick's launch reads this state, possibly on another
-// XCD) has nothing to write back.  With plain stores ~22 KB per workgroup is
-// dirty at kernel end and that write-back is serialised after the last wave
-// (MI355X_MICROARCH.md: release ~1.7 us clean, ~6.5 us with 16 KB dirty per
-// block; write-through publish 3.0 vs 8.2 us).  16-byte sc1 stores cost the
-// same as plain ones.
-__device__ __forceinline__ void store_wt16(void* p, uint4 u) {
-  const skv4i v = {(int)u.x, (int)u.y, (int)u.z, (int)u.w};  // native vector: asm cannot bind HIP's structs
-  // s_nop: the data VGPRs of a >8-byte VMEM store need 1 wait state before a
-  // VALU may overwrite them (gfx9 hazard the compiler cannot see in asm)
-  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 0" ::"v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ void store_wt8(void* p, uint2 u) {
-  const skv2i v = {(int)u.x, (int)u.y};
-  asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-}
-
-__device__ __forceinline__ void store_env_wt(const View& v, int64_t i, const Env& e) {
-  store_wt16(v.pos + i, make_uint4(e.px[0], e.py[0], e.px[1], e.py[1]));
-  store_wt16(v.rot + i, make_uint4(__double2loint(e.rot[0]), __double2hiint(e.rot[0]), __double2loint(e.rot[1]),
-                                   __double2hiint(e.rot[1])));
-  store_wt16(v.qpos + i, make_uint4(e.qx[0], e.qy[0], e.qx[1], e.qy[1]));
-  store_wt16(v.qrot + i, make_uint4(__double2loint(e.qrot[0]), __double2hiint(e.qrot[0]),
-                                    __double2loint(e.qrot[1]), __double2hiint(e.qrot[1])));
-  store_wt16(v.qcdage + i, make_uint4(e.qcd[0], e.qage[0], e.qcd[1], e.qage[1]));
-  const unsigned f = (unsigned)(e.qvalid[0] & 0xff) | ((unsigned)(e.qvalid[1] & 0xff) << 8) |
-                     ((unsigned)(e.live & 0xff) << 16) | ((unsigned)(e.winner & 0xff) << 24);
-  store_wt8(v.misc + i, make_uint2((unsigned)e.ticks, f));
-}
-
 // ---------------------------------------------------------------- Philox4x32-10
 struct U4 { uint32_t x, y, z, w; };
 

@@ -198,7 +198,7 @@ __global__ void __launch_bounds__(kBlock) k_step(StepArgs a, Cfg c) {
     store_obs(a.obs_reset, a.n, 0, i, o0);
     store_obs(a.obs_reset, a.n, 1, i, o1);
   }
-  store_env_wt(a.v, i, e);  // write-through: nothing dirty for the end-of-dispatch release
+  store_env(a.v, i, e);
 }
 
 // Fused step, fp32-trig variant (SK_STEP_VARIANT=2; the default from 196,608
@@ -266,7 +266,7 @@ __global__ void __launch_bounds__(kBlock) k_step_fast(StepArgs a, Cfg c) {
     store_obs(a.obs_reset, a.n, 0, i, o0);
     store_obs(a.obs_reset, a.n, 1, i, o1);
   }
-  store_env_wt(a.v, i, e);  // write-through: nothing dirty for the end-of-dispatch release
+  store_env(a.v, i, e);
 }
 
 // Player-split fused step: lanes (2i, 2i+1) own players 1 and 2 of env i.
