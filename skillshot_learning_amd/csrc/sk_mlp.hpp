@@ -58,9 +58,10 @@ __host__ __device__ __forceinline__ int w2_k(int kk, int h, int j) {
 }
 
 // ---------------------------------------------------------------- noise
+template <int ROUNDS = 10>
 __device__ __forceinline__ uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
-  for (int i = 0; i < 10; ++i) {
+  for (int i = 0; i < ROUNDS; ++i) {
     uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
     uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
     c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
