@@ -52,6 +52,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-rollout", action="store_true")
     p.add_argument("--no-large", action="store_true", help="skip the 4 M-game HBM-bound secondary measurement")
+    p.add_argument("--no-strong", action="store_true", help="skip the fixed-65,536-total secondary measurement")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_k_step.json"))
     return p.parse_args()
 
@@ -124,14 +125,75 @@ def large_batch_rate(dev, args, rank, n=1 << 22, launches=60, ring=8):
                 note="state 369 MB > Infinity Cache: the HBM-bound regime; reported beside, not as, the headline")
 
 
+def strong_scaling_rate(dev, args, rank, world, total=65536, launches=2000, G=400):
+    """BASELINE config-5 reading of the metric: 65,536 games in total split
+    over the ranks (65,536 / world per GPU), same fused tick; aggregate
+    env-steps/s over max-over-ranks wall time (barriers around)."""
+    import ctypes
+    from skillshot_learning_amd import VecSkillshotGame
+    n = total // world
+    env = VecSkillshotGame(n, device=dev, seed=args.seed + 2, env_offset=rank * n, tick_limit=args.tick_limit,
+                           random_positions=True)
+    st = torch.cuda.Stream(device=dev)
+    ring = G
+    with torch.cuda.stream(st):
+        env.reset(random_positions=True)
+        acts = env.gen_random_actions(ring)
+        done = torch.empty(n, dtype=torch.uint8, device=dev)
+    st.synchronize()
+    slab, sp = 16 * n, ctypes.c_void_p(st.cuda_stream)
+
+    def launch(t):
+        env.step_raw(ctypes.c_void_p(acts.data_ptr() + (t % ring) * slab), ctypes.c_void_p(done.data_ptr()), stream=sp)
+
+    with torch.cuda.stream(st):
+        for t in range(2):
+            launch(t)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=st):
+        for t in range(G):
+            launch(t)
+    with torch.cuda.stream(st):
+        g.replay()
+    st.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with torch.cuda.stream(st):
+        for _ in range(launches // G):
+            g.replay()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    steps = (launches // G) * G
+    env.close()
+    return dict(total_envs=total, envs_per_gpu=n, n_gpus=world, env_steps_per_s=total * steps / el,
+                us_per_tick=el * 1e6 / steps, scaling="strong",
+                note="fixed 65,536 games over all GPUs (launch-bound per GPU at 8,192); reported beside the "
+                     "weak-scaling headline")
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
+        # one rank per GPU over RCCL; SK_BENCH_BACKEND=gloo rehearses the
+        # multi-rank path with several ranks sharing the GPUs there are
+        backend = os.environ.get("SK_BENCH_BACKEND", "nccl")
+        local = local % max(torch.cuda.device_count(), 1) if backend == "gloo" else local
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -247,6 +309,9 @@ def main():
     large = None
     if not args.no_large:
         large = large_batch_rate(dev, args, rank)
+    strong = None
+    if world > 1 and not args.no_strong:
+        strong = strong_scaling_rate(dev, args, rank, world)
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
@@ -292,6 +357,9 @@ def main():
             "episodes": counters,
             "rollout_random": rollout,
             "large_batch": large,
+            "strong_scaling": strong if strong is not None else (
+                {"total_envs": n, "n_gpus": 1, "env_steps_per_s": value, "scaling": "strong",
+                 "note": "N=1: the headline itself"} if world == 1 and n == 65536 else None),
         }
         print(json.dumps(line), flush=True)
     if world > 1:
