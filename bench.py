@@ -49,6 +49,7 @@ def parse():
     p.add_argument("--graph-len", type=int, default=400, help="launches per captured hipGraph")
     p.add_argument("--action-ring", type=int, default=400, help="distinct per-tick action slabs in HBM")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--cpu-cores", type=int, default=16, help="host cores for the CPU baseline (the box's share)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-rollout", action="store_true")
     p.add_argument("--no-large", action="store_true", help="skip the 4 M-game HBM-bound secondary measurement")
@@ -57,29 +58,29 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(n_envs, seconds, tick_limit, seed):
-    """C oracle (port of the reference step, oracle/skillshot_oracle.c) on one
-    core: the same workload (random policy, fused step, auto-reset), bounded
-    to about `seconds` of CPU work."""
-    from oracle import oracle
-    s = oracle.OracleState(n_envs, seed=seed)
-    s.reset(random_positions=True)
-    chunk = 8
-    acts = s.gen_random_actions(chunk)  # pre-generated, untimed (as on the GPU)
-    steps = 0
-    t0 = time.perf_counter()
-    while True:
-        for t in range(chunk):
-            s.step(acts[t], tick_limit=tick_limit, auto_reset=True, random_positions=True, want_obs=False)
-        steps += chunk
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    rate = n_envs * steps / el
-    return dict(value=rate, unit="env-steps/s", cores=1, kind="port",
-                sample=f"C oracle (oracle/skillshot_oracle.c, restatement of the reference step) "
-                       f"{n_envs} envs x {steps} ticks ({el:.1f} s, 1 thread); reference Python on the "
-                       f"survey host: 59.2k env-steps/s per core (BASELINE.md)")
+def cpu_baseline(n_envs, seconds, tick_limit, seed, cores):
+    """C oracle (port of the reference step, oracle/skillshot_oracle.c): the
+    same workload (random policy, fused step, auto-reset) on `cores` host
+    cores, one process per core on its own slice of the games
+    (oracle/cpu_bench.py), each bounded to about `seconds` of CPU work; the
+    one-core rate is measured first on the full batch."""
+    import subprocess
+    root = os.path.dirname(os.path.abspath(__file__))
+    from oracle import cpu_bench
+    one = cpu_bench.run(n_envs, seconds / 2, seed=seed, tick_limit=tick_limit)
+    per = n_envs // cores
+    procs = [subprocess.Popen([sys.executable, "-m", "oracle.cpu_bench", "--envs", str(per), "--env-offset",
+                               str(c * per), "--seconds", str(seconds), "--seed", str(seed), "--tick-limit",
+                               str(tick_limit)], cwd=root, stdout=subprocess.PIPE, text=True)
+             for c in range(cores)]
+    outs = [json.loads(p.communicate()[0].strip().splitlines()[-1]) for p in procs]
+    rate = sum(o["env_steps_per_s"] for o in outs)
+    return dict(value=rate, unit="env-steps/s", cores=cores, kind="port",
+                sample=f"C oracle (oracle/skillshot_oracle.c, restatement of the reference step): {cores} processes "
+                       f"x {per} games for {seconds:.0f} s each ({sum(o['ticks'] for o in outs) // cores} ticks "
+                       f"per process on average); one core on all {n_envs} games: "
+                       f"{one['env_steps_per_s']:.4g} env-steps/s; reference Python on the survey host: "
+                       f"59.2k env-steps/s per core (BASELINE.md)")
 
 
 def large_batch_rate(dev, args, rank, n=1 << 22, launches=60, ring=8):
@@ -315,7 +316,8 @@ def main():
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(n, args.cpu_seconds, args.tick_limit, args.seed)
+        cpu = cpu_baseline(n, args.cpu_seconds, args.tick_limit, args.seed,
+                           max(1, min(args.cpu_cores, os.cpu_count() or 1)))
 
     if rank == 0:
         line = {
