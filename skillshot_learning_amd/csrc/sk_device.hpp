@@ -16,6 +16,7 @@
 #include <stdint.h>
 
 #include "../../include/skillshot.h"
+#include "sk_tan_cr.hpp"
 #include "sk_trig.hpp"
 
 namespace sk {
@@ -527,10 +528,6 @@ __device__ __forceinline__ void tick_env_fast(const Cfg& c, Env& e, float a0_mov
 }
 
 // ---------------------------------------------------------------- features
-__device__ __forceinline__ double grad_of(double rot) {  // Player.py:94, Projectile.py:58
-  return tan(-rot + kPi2);
-}
-
 // SkillshotGame.get_dist_line_point (SkillshotGame.py:124-130); g**2 as g*g
 __device__ __forceinline__ double dist_line_point(double g, int lx, int ly, int cx, int cy) {
   double cc = (double)ly - g * (double)lx;
@@ -547,10 +544,9 @@ __device__ __forceinline__ double dist_point_point(int ax, int ay, int bx, int b
 // SkillshotGame.check_future_collision (SkillshotGame.py:96-113) for a
 // projectile against an opponent at (ox, oy): the x_dir gate (:109) is always
 // true for the first projectile x bound, so the test reduces to
-// valid && exists X in {Ox, Ox+5}: Oy <= g*X + (qy - g*qx) <= Oy+5.
-__device__ __forceinline__ bool future_collision_s(const Cfg& c, int qx, int qy, int qvalid, int ox, int oy,
-                                                   double g) {
-  if (!qvalid) return false;
+// valid && exists X in {Ox, Ox+5}: Oy <= g*X + (qy - g*qx) <= Oy+5,
+// evaluated in the reference's order (contraction off).
+__device__ __forceinline__ bool future_collision_g(const Cfg& c, int qx, int qy, int ox, int oy, double g) {
   double yi = (double)qy - g * (double)qx;
   double lo = (double)oy, hi = (double)(oy + c.psize);
   double v0 = g * (double)ox + yi;
@@ -558,9 +554,41 @@ __device__ __forceinline__ bool future_collision_s(const Cfg& c, int qx, int qy,
   return ((lo <= v0) & (v0 <= hi)) | ((lo <= v1) & (v1 <= hi));
 }
 
-__device__ __forceinline__ bool future_collision(const Cfg& c, const Env& e, int p, double g) {
-  int o = 1 - p;
-  return future_collision_s(c, e.qx[p], e.qy[p], e.qvalid[p], e.px[o], e.py[o], g);
+// The flag from a fast gradient g (a few ulp from the correctly rounded
+// tan(-qrot + pi/2)): decided from g unless some g*X + yi lies within
+// kFutureMargin (relative to the magnitudes summed, >> the few-ulp gradient
+// and rounding differences) of a span edge; such lanes report *amb and the
+// kernel redoes the flag with the correctly rounded gradient
+// (fix_future_flag, sk_tan_cr.hpp) after its obs rows are stored, so the
+// rare slow path keeps no obs registers live.
+constexpr double kFutureMargin = 0x1p-40;
+
+__device__ __forceinline__ bool future_collision_s(const Cfg& c, int qx, int qy, int qvalid, int ox, int oy,
+                                                   double g, bool* amb) {
+  *amb = false;
+  if (!qvalid) return false;
+  double yi = (double)qy - g * (double)qx;
+  double lo = (double)oy, hi = (double)(oy + c.psize);
+  double v0 = g * (double)ox + yi;
+  double v1 = g * (double)(ox + c.psize) + yi;
+  double eps = kFutureMargin * (fabs(g) * (fabs((double)ox) + (double)c.psize + fabs((double)qx)) +
+                                fabs((double)qy) + fabs(yi) + hi + 1.0);
+  *amb = fabs(v0 - lo) <= eps || fabs(v0 - hi) <= eps || fabs(v1 - lo) <= eps || fabs(v1 - hi) <= eps;
+  return ((lo <= v0) & (v0 <= hi)) | ((lo <= v1) & (v1 <= hi));
+}
+
+// obs[11] of one player from the correctly rounded gradient (the *amb lanes)
+__device__ __attribute__((noinline)) void fix_future_flag(const Cfg& c, int qx, int qy, double qrot, int ox,
+                                                          int oy, float* slot) {
+  *slot = future_collision_g(c, qx, qy, ox, oy, sktan::tan_cr(-qrot + kPi2)) ? 1.0f : 0.0f;
+}
+
+// the obs rows [2][N][12] of env i were stored from env state e; amb bit p
+// marks player p's flag for redoing
+__device__ __forceinline__ void fix_future_flags(const Cfg& c, const Env& e, unsigned amb, float* obs, int64_t n,
+                                                 int64_t i) {
+  if (amb & 1u) fix_future_flag(c, e.qx[0], e.qy[0], e.qrot[0], e.px[1], e.py[1], obs + i * 12 + 11);
+  if (amb & 2u) fix_future_flag(c, e.qx[1], e.qy[1], e.qrot[1], e.px[0], e.py[0], obs + (n + i) * 12 + 11);
 }
 
 __device__ __forceinline__ double py_mod2(double r) {  // Python float % 2 (floored)
@@ -571,30 +599,6 @@ __device__ __forceinline__ double py_mod2(double r) {  // Python float % 2 (floo
     m = 0.0;
   }
   return m;
-}
-
-// prepare_states (SkillshotLearner.py:512-543) for one player (own player
-// and projectile state, opponent position); *path_dist receives the player's
-// line distance, the calculate_rewards_looking input (:584).
-__device__ __forceinline__ void obs12_s(const Cfg& c, int px, int py, double rot, int qx, int qy, double qrot,
-                                        int qcd, int qvalid, int ox, int oy, float out[12], double* path_dist) {
-  double gp = grad_of(rot);
-  double gq = grad_of(qrot);
-  double D = c.max_dist;
-  double pd = dist_line_point(gp, px, py, ox, oy);
-  *path_dist = pd;
-  out[0] = (float)(pd / D);
-  out[1] = (float)(dist_point_point(px, py, ox, oy) / D);
-  out[2] = (float)((double)px / (double)c.W);
-  out[3] = (float)((double)py / (double)c.H);
-  out[4] = (float)(((py_mod2(rot) * kPi) / 2.0) * kPi);  // `% 2 * np.pi) / 2 * np.pi`
-  out[5] = (float)((double)qcd / (double)c.cdmax);
-  out[6] = (float)(dist_point_point(qx, qy, ox, oy) / D);
-  out[7] = (float)((double)qx / (double)c.W);
-  out[8] = (float)((double)qy / (double)c.H);
-  out[9] = (float)(((py_mod2(qrot) * kPi) / 2.0) * kPi);
-  out[10] = (float)(dist_line_point(gq, qx, qy, ox, oy) / D);
-  out[11] = future_collision_s(c, qx, qy, qvalid, ox, oy, gq) ? 1.0f : 0.0f;
 }
 
 // Python's float r % 2 (floored, +0.0 for exact multiples): r - 2*floor(r/2)
@@ -619,7 +623,7 @@ __device__ __forceinline__ double grad_fast(double rot) {
 // gradients (fused step kernels: four grad_fast per game issued together).
 __device__ __forceinline__ void obs12_g(const Cfg& c, int px, int py, double rot, int qx, int qy, double qrot,
                                         int qcd, int qvalid, int ox, int oy, double gp, double gq, float out[12],
-                                        double* path_dist) {
+                                        double* path_dist, bool* amb) {
   double pd = dist_line_point(gp, px, py, ox, oy);
   *path_dist = pd;
   out[0] = (float)(pd * c.inv_max_dist);
@@ -633,31 +637,33 @@ __device__ __forceinline__ void obs12_g(const Cfg& c, int px, int py, double rot
   out[8] = (float)((double)qy * c.inv_H);
   out[9] = (float)(((py_mod2_fast(qrot) * kPi) / 2.0) * kPi);
   out[10] = (float)(dist_line_point(gq, qx, qy, ox, oy) * c.inv_max_dist);
-  out[11] = future_collision_s(c, qx, qy, qvalid, ox, oy, gq) ? 1.0f : 0.0f;
+  out[11] = future_collision_s(c, qx, qy, qvalid, ox, oy, gq, amb) ? 1.0f : 0.0f;
 }
 
-// both players' obs of one env (the fused step's obs/reward epilogue)
-__device__ __forceinline__ void obs_env(const Cfg& c, const Env& e, float o0[12], float o1[12], double* pd0,
-                                        double* pd1) {
+// both players' obs of one env (the fused step's obs/reward epilogue);
+// returns the fix_future_flags bits
+__device__ __forceinline__ unsigned obs_env(const Cfg& c, const Env& e, float o0[12], float o1[12], double* pd0,
+                                            double* pd1) {
+  bool m0, m1;
   const double gp0 = grad_fast(e.rot[0]), gq0 = grad_fast(e.qrot[0]);
   const double gp1 = grad_fast(e.rot[1]), gq1 = grad_fast(e.qrot[1]);
   obs12_g(c, e.px[0], e.py[0], e.rot[0], e.qx[0], e.qy[0], e.qrot[0], e.qcd[0], e.qvalid[0], e.px[1], e.py[1],
-          gp0, gq0, o0, pd0);
+          gp0, gq0, o0, pd0, &m0);
   obs12_g(c, e.px[1], e.py[1], e.rot[1], e.qx[1], e.qy[1], e.qrot[1], e.qcd[1], e.qvalid[1], e.px[0], e.py[0],
-          gp1, gq1, o1, pd1);
+          gp1, gq1, o1, pd1, &m1);
+  return (unsigned)m0 | ((unsigned)m1 << 1);
 }
 
-__device__ __forceinline__ void obs12(const Cfg& c, const Env& e, int p, float out[12], double* path_dist) {
-  int o = 1 - p;
-  obs12_s(c, e.px[p], e.py[p], e.rot[p], e.qx[p], e.qy[p], e.qrot[p], e.qcd[p], e.qvalid[p], e.px[o], e.py[o],
-          out, path_dist);
-}
+// tan(-rot + pi/2) correctly rounded (Player.py:94 / Projectile.py:58)
+__device__ __attribute__((noinline)) double grad_cr(double rot) { return sktan::tan_cr(-rot + kPi2); }
 
 // get_state per-player dict values (SkillshotGame.py:145-163 key order)
 __device__ __forceinline__ void features18(const Cfg& c, const Env& e, int p, double f[18]) {
+  // the get_state() path (not the step's hot loop): gradients correctly
+  // rounded, so f[0] / f[8] equal math.tan's wherever glibc's tan is
   int o = 1 - p;
-  double gp = grad_of(e.rot[p]);
-  double gq = grad_of(e.qrot[p]);
+  double gp = grad_cr(e.rot[p]);
+  double gq = grad_cr(e.qrot[p]);
   f[0] = gp;
   f[1] = (-sin(e.rot[p]) >= 0.0) ? 1.0 : -1.0;
   f[2] = dist_line_point(gp, e.px[p], e.py[p], e.px[o], e.py[o]);
@@ -675,7 +681,7 @@ __device__ __forceinline__ void features18(const Cfg& c, const Env& e, int p, do
   f[14] = e.qage[p];
   f[15] = e.qvalid[p];
   f[16] = dist_point_point(e.qx[p], e.qy[p], e.px[o], e.py[o]);
-  f[17] = future_collision(c, e, p, gq) ? 1.0 : 0.0;
+  f[17] = (e.qvalid[p] && future_collision_g(c, e.qx[p], e.qy[p], e.px[o], e.py[o], gq)) ? 1.0 : 0.0;
 }
 
 }  // namespace sk

@@ -171,10 +171,11 @@ __global__ void __launch_bounds__(kBlock) k_step(StepArgs a, Cfg c) {
     if (a.obs || a.reward) {
       float o0[12], o1[12];
       double pd0, pd1;
-      obs_env(c, e, o0, o1, &pd0, &pd1);
+      const unsigned amb = obs_env(c, e, o0, o1, &pd0, &pd1);
       if (a.obs) {
         store_obs(a.obs, a.n, 0, i, o0);
         store_obs(a.obs, a.n, 1, i, o1);
+        if (amb) fix_future_flags(c, e, amb, a.obs, a.n, i);
       }
       if (a.reward) {
         a.reward[i] = reward_of(c, e, 0, a.reward_kind, pd0);
@@ -194,9 +195,10 @@ __global__ void __launch_bounds__(kBlock) k_step(StepArgs a, Cfg c) {
   if (a.obs_reset) {
     float o0[12], o1[12];
     double pd0, pd1;
-    obs_env(c, e, o0, o1, &pd0, &pd1);
+    const unsigned amb = obs_env(c, e, o0, o1, &pd0, &pd1);
     store_obs(a.obs_reset, a.n, 0, i, o0);
     store_obs(a.obs_reset, a.n, 1, i, o1);
+    if (amb) fix_future_flags(c, e, amb, a.obs_reset, a.n, i);
   }
   store_env(a.v, i, e);
 }
@@ -236,10 +238,11 @@ __global__ void __launch_bounds__(kBlock) k_step_fast(StepArgs a, Cfg c) {
     if (a.obs || a.reward) {
       float o0[12], o1[12];
       double pd0, pd1;
-      obs_env(c, e, o0, o1, &pd0, &pd1);
+      const unsigned amb = obs_env(c, e, o0, o1, &pd0, &pd1);
       if (a.obs) {
         store_obs(a.obs, a.n, 0, i, o0);
         store_obs(a.obs, a.n, 1, i, o1);
+        if (amb) fix_future_flags(c, e, amb, a.obs, a.n, i);
       }
       if (a.reward) {
         a.reward[i] = reward_of(c, e, 0, a.reward_kind, pd0);
@@ -262,9 +265,10 @@ __global__ void __launch_bounds__(kBlock) k_step_fast(StepArgs a, Cfg c) {
   if (a.obs_reset) {
     float o0[12], o1[12];
     double pd0, pd1;
-    obs_env(c, e, o0, o1, &pd0, &pd1);
+    const unsigned amb = obs_env(c, e, o0, o1, &pd0, &pd1);
     store_obs(a.obs_reset, a.n, 0, i, o0);
     store_obs(a.obs_reset, a.n, 1, i, o1);
+    if (amb) fix_future_flags(c, e, amb, a.obs_reset, a.n, i);
   }
   store_env(a.v, i, e);
 }
@@ -330,8 +334,12 @@ __global__ void __launch_bounds__(kBlock) k_step_split(StepArgs a, Cfg c) {
     float o[12];
     double pd;
     const double gp = grad_fast(rot), gq = grad_fast(qrot);
-    obs12_g(c, px, py, rot, qx, qy, qrot, qcd, qvalid, opx, opy, gp, gq, o, &pd);
-    if (a.obs) store_obs(a.obs, a.n, p, i, o);
+    bool amb;
+    obs12_g(c, px, py, rot, qx, qy, qrot, qcd, qvalid, opx, opy, gp, gq, o, &pd, &amb);
+    if (a.obs) {
+      store_obs(a.obs, a.n, p, i, o);
+      if (amb) fix_future_flag(c, qx, qy, qrot, opx, opy, a.obs + ((int64_t)p * a.n + i) * 12 + 11);
+    }
     if (a.reward) {
       float r;
       if (a.reward_kind == SK_REWARD_SIMPLE) {
@@ -367,8 +375,10 @@ __global__ void __launch_bounds__(kBlock) k_step_split(StepArgs a, Cfg c) {
     float o[12];
     double pd;
     const double gp = grad_fast(rot), gq = grad_fast(qrot);
-    obs12_g(c, px, py, rot, qx, qy, qrot, qcd, qvalid, rpx, rpy, gp, gq, o, &pd);
+    bool amb;
+    obs12_g(c, px, py, rot, qx, qy, qrot, qcd, qvalid, rpx, rpy, gp, gq, o, &pd, &amb);
     store_obs(a.obs_reset, a.n, p, i, o);
+    if (amb) fix_future_flag(c, qx, qy, qrot, rpx, rpy, a.obs_reset + ((int64_t)p * a.n + i) * 12 + 11);
   }
   reinterpret_cast<int2*>(a.v.pos)[h] = make_int2(px, py);
   reinterpret_cast<double*>(a.v.rot)[h] = rot;
@@ -553,10 +563,11 @@ __global__ void __launch_bounds__(kBlock) k_observe(View v, int64_t n, float* ob
   load_env(v, i, e);
   float o0[12], o1[12];
   double pd0, pd1;
-  obs_env(c, e, o0, o1, &pd0, &pd1);
+  const unsigned amb = obs_env(c, e, o0, o1, &pd0, &pd1);
   if (obs) {
     store_obs(obs, n, 0, i, o0);
     store_obs(obs, n, 1, i, o1);
+    if (amb) fix_future_flags(c, e, amb, obs, n, i);
   }
   if (reward) {
     reward[i] = reward_of(c, e, 0, kind, pd0);

@@ -13,9 +13,22 @@ GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
 def fixture_names():
-    """Trajectory fixtures (boards.npz holds single states, see test_board_cpu)."""
+    """Trajectory fixtures (boards.npz and probes.npz hold single states, see
+    test_board_cpu / test_closed_forms_cpu)."""
     return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz"))
-                  if not p.endswith("boards.npz"))
+                  if os.path.basename(p) not in SINGLE_STATE)
+
+
+SINGLE_STATE = ("boards.npz", "probes.npz")
+
+
+def probe_state(d):
+    """Engine-layout arrays of the probe boards (probes.npz): live game, tick 0, no winner."""
+    n = d["pos"].shape[0]
+    zero = np.zeros(n, np.uint8)
+    return dict(pos=d["pos"].reshape(n, 4), rot=d["rot"], qpos=d["qpos"].reshape(n, 4), qrot=d["qrot"],
+                qcdage=np.stack([d["qcd"][:, 0], d["qage"][:, 0], d["qcd"][:, 1], d["qage"][:, 1]], -1),
+                misc=np.stack([np.zeros(n, np.int32), _flags(d["qvalid"], zero + 1, zero)], -1))
 
 
 def load(name):

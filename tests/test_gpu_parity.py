@@ -319,3 +319,83 @@ def test_full_reward_on_engine_features(ssa, name):
     m = ~np.isnan(want)
     assert np.array_equal(np.isnan(got), ~m)
     assert np.abs(got[m] - want[m]).max() <= 1e-12
+
+
+def _flag_mismatches_explained(state, got11, want11):
+    """obs[11] differences from the oracle (glibc tan) must all be projectiles
+    whose gradient glibc does not round correctly and whose flag the correctly
+    rounded tan decides the device's way (csrc/sk_tan_cr.hpp)."""
+    import math
+    from cr_tan import cr_tan
+    bad = np.argwhere(got11 != want11)
+    for p, i in bad:
+        qx, qy = (int(v) for v in state["qpos"][i, 2 * p:2 * p + 2])
+        ox, oy = (int(v) for v in state["pos"][i, 2 * (1 - p):2 * (1 - p) + 2])
+        x = -float(state["qrot"][i, p]) + math.pi / 2
+        g = cr_tan(x)
+        assert math.tan(x) != g, (p, i)
+        yi = float(qy) - g * float(qx)
+        fut = any(float(oy) <= g * float(X) + yi <= float(oy + 5) for X in (ox, ox + 5))
+        assert bool(got11[p, i]) == fut, (p, i)
+    return len(bad)
+
+
+def test_collision_probes_match_reference(ssa):
+    """A9 / A11 on the probe boards (tests/golden/make_probes.py: projectiles
+    a few pixels from the opponent, aimed corner shots, pi/4 multiples): the
+    HIP check_collision equals the reference's exactly; the get_state
+    future-collision feature and obs[11] equal the decision under the correctly
+    rounded gradient (future_cr), which differs from the reference's only where
+    glibc's tan is not correctly rounded; the get_state gradient is the
+    correctly rounded tan bit for bit."""
+    d = gr.load("probes")
+    n = d["pos"].shape[0]
+    g = ssa.VecSkillshotGame(n)
+    g.load_state_dict(gr.probe_state(d))
+    f = g.features().cpu().numpy()
+    assert np.array_equal(f[..., 8].view(np.int64), d["grad_cr"].view(np.int64))
+    assert np.array_equal(f[..., 17].astype(np.uint8), d["future_cr"])
+    o, _ = g.observe()
+    assert np.array_equal(o[..., 11].cpu().numpy().T.astype(np.uint8), d["future_cr"])
+    differ = d["future_cr"] != d["future"]
+    assert not (differ & (d["glibc_is_cr"] != 0)).any()
+    hit = g.check_collision().cpu().numpy()
+    assert np.array_equal(hit, d["hit"])
+    flags = g.state_dict()["misc"][:, 1].view(np.uint32)
+    assert np.array_equal(((flags >> 16) & 0xFF) == 0, d["hit"] != 0)
+    assert np.array_equal(flags >> 24, d["hit"])
+
+
+def test_fused_step_on_probe_boards(ssa, oracle_mod, step_variant):
+    """The fused learner step from the probe boards (16 seeded copies each,
+    96000 envs): projectiles start next to the opponent so most steps end in
+    a corner hit or a near miss; state bit-exact vs the oracle, obs[11] equal
+    except flags explained by glibc's tan rounding (see above)."""
+    d = gr.load("probes")
+    base = gr.probe_state(d)
+    reps = 16
+    arrays = {k: np.concatenate([v] * reps) for k, v in base.items()}
+    n = arrays["pos"].shape[0]
+    ref = oracle_mod.OracleState(n, seed=3)
+    ref.load(arrays)
+    g = ssa.VecSkillshotGame(n, seed=3, tick_limit=2000)
+    g.load_state_dict(arrays)
+    g.step_counter = ref.step_counter
+    hits = explained = 0
+    for t in range(4):
+        acts = g.gen_random_actions(1)[0]
+        ra = ref.gen_random_actions(1)[0]
+        out = g.step(acts, obs=True, auto_reset=False)
+        wo = ref.step(ra, tick_limit=2000, auto_reset=False)
+        torch.cuda.synchronize()
+        assert np.array_equal(out["done"].cpu().numpy(), wo["done"]), t
+        assert np.array_equal(out["winner"].cpu().numpy(), wo["winner"]), t
+        st = g.state_dict()
+        st.pop("step_counter")
+        _assert_state_equal(st, ref.arrays(), f"probe step {t}")
+        o = out["obs"].cpu().numpy().astype(np.float64)
+        explained += _flag_mismatches_explained(ref.arrays(), o[..., 11], wo["obs"][..., 11])
+        assert (np.abs(o - wo["obs"]) / np.maximum(1.0, np.abs(wo["obs"])))[..., :11].max() <= OBS_TOL
+        hits += int((wo["winner"] != 0).sum())
+    assert hits > 1000
+    assert explained <= 64
