@@ -54,6 +54,7 @@ def parse():
     p.add_argument("--no-rollout", action="store_true")
     p.add_argument("--no-large", action="store_true", help="skip the 4 M-game HBM-bound secondary measurement")
     p.add_argument("--no-strong", action="store_true", help="skip the fixed-65,536-total secondary measurement")
+    p.add_argument("--no-learner", action="store_true", help="skip the DDPG-in-the-loop secondary measurement (N=1)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_k_step.json"))
     return p.parse_args()
 
@@ -178,6 +179,35 @@ def strong_scaling_rate(dev, args, rank, world, total=65536, launches=2000, G=40
                 us_per_tick=el * 1e6 / steps, scaling="strong",
                 note="fixed 65,536 games over all GPUs (launch-bound per GPU at 8,192); reported beside the "
                      "weak-scaling headline")
+
+
+def learner_rate(envs, ticks=200, batch=4096):
+    """Configs 3 / 5 on one GPU: per tick the parameter-noise
+    actor forward for both players of every game, the fused env step with
+    obs/reward/auto-reset, 2N transitions into the HBM replay ring, one critic
+    + actor update (fused MFMA kernels, in-kernel bootstrap target) on a
+    `batch` sample, soft target update and actor repack — replayed as one
+    captured hipGraph per 2 ticks (SkillshotLearner.tick_graph)."""
+    from skillshot_learning_amd.learner import SkillshotLearner
+    L = SkillshotLearner(n_envs=envs, seed=0, exploration="param_noise", tick_limit=2000,
+                         replay_capacity=1 << 20, gamma=0.99, tau=0.005)
+    tg = L.tick_graph(batch=batch, updates_per_tick=1, ticks_per_graph=2)
+    tg.run(10)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(tg.stream)
+    tg.run(ticks // 2)
+    e1.record(tg.stream)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    n_ticks = (ticks // 2) * 2
+    out = dict(envs_per_gpu=envs, ticks=n_ticks, batch=batch, exploration="param_noise", updates_per_tick=1,
+               env_steps_per_s=envs * n_ticks / el, ms_per_tick=el * 1e3 / n_ticks,
+               gpu_ms_per_tick=e0.elapsed_time(e1) / n_ticks, episodes=L.game_environment.counters())
+    del tg, L
+    torch.cuda.empty_cache()
+    return out
 
 
 def main():
@@ -314,6 +344,13 @@ def main():
     if world > 1 and not args.no_strong:
         strong = strong_scaling_rate(dev, args, rank, world)
 
+    # ---- secondary: the DDPG learner in the loop (configs 3 and 5 on one GPU)
+    learner = None
+    if world == 1 and not args.no_learner:
+        learner = {"config3": learner_rate(4096), "config5_1gpu": learner_rate(65536),
+                   "note": "env step + param-noise actor + replay insert/sample + critic/actor update per tick; "
+                           "reported beside, not as, the headline"}
+
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline(n, args.cpu_seconds, args.tick_limit, args.seed,
@@ -359,6 +396,7 @@ def main():
             "episodes": counters,
             "rollout_random": rollout,
             "large_batch": large,
+            "learner": learner,
             "strong_scaling": strong if strong is not None else (
                 {"total_envs": n, "n_gpus": 1, "env_steps_per_s": value, "scaling": "strong",
                  "note": "N=1: the headline itself"} if world == 1 and n == 65536 else None),

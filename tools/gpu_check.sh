@@ -33,7 +33,7 @@ if [[ "$STEPS" == all || "$STEPS" == *bench* ]]; then
 fi
 if [[ "$STEPS" == all || "$STEPS" == *prof* ]]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run \
-    -- python3 bench.py --steps 2000 --warmup 200 --no-cpu-baseline --no-large > $OUT/prof_bench_$TAG.json 2> $OUT/prof_$TAG.err
+    -- python3 bench.py --steps 2000 --warmup 200 --no-cpu-baseline --no-large --no-learner > $OUT/prof_bench_$TAG.json 2> $OUT/prof_$TAG.err
   rc=$?; tail -3 $OUT/prof_$TAG.err; stop_if_fault $rc rocprof
   find $OUT/prof_$TAG -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats_$TAG.csv \; 2>/dev/null
   head -20 $OUT/kernel_stats_$TAG.csv 2>/dev/null
