@@ -340,6 +340,25 @@ int sk_adam_flat(const float* partials, int32_t n_partials, int32_t n_params, co
                  float* grad_out, int32_t apply, float* param, float* exp_avg, float* exp_avg_sq,
                  const float* step_counter, float lr, float beta1, float beta2, float eps, float* target, float tau,
                  float* stat_acc, float stat_scale, float* stat_out, int64_t* counter, void* stream);
+/* sk_adam_flat that also writes the packed copies of every parameter it
+ * produces, so no separate pack launch follows a step: param_gpack (the
+ * stepped net's sk_grad_pack layout), target_gpack (its soft-updated target's,
+ * needs target) and, for the actor (ld2 256, n_out 2), actor_fwd_pack (the
+ * sk_actor_pack layout).  Each pointer is nullable; the buffers must hold a
+ * full pack already (padding entries are not rewritten).  n_params must be
+ * the net's parameter count for (ld2, n_out).  Ignored when apply = 0. */
+typedef struct sk_pack_targets {
+  void* param_gpack;
+  void* target_gpack;
+  void* actor_fwd_pack;
+  int32_t ld2;   /* 256 (actor) or 258 (critic: W2 carries the 2 action columns) */
+  int32_t n_out; /* 2 (actor) or 1 (critic) */
+} sk_pack_targets;
+int sk_adam_flat_packed(const float* partials, int32_t n_partials, int32_t n_params, const float* grad_in,
+                        float* grad_out, int32_t apply, float* param, float* exp_avg, float* exp_avg_sq,
+                        const float* step_counter, float lr, float beta1, float beta2, float eps, float* target,
+                        float tau, float* stat_acc, float stat_scale, float* stat_out, int64_t* counter,
+                        const sk_pack_targets* packs, void* stream);
 
 #ifdef __cplusplus
 }

@@ -29,6 +29,7 @@ EXPORTS = (
     "sk_actor_packed_bytes", "sk_actor_pack", "sk_actor_forward", "sk_actor_forward_dev",
     "sk_critic_packed_bytes", "sk_critic_pack", "sk_critic_forward", "sk_target_q",
     "sk_grad_packed_bytes", "sk_update_partials", "sk_grad_pack", "sk_critic_grad", "sk_actor_grad", "sk_adam_flat",
+    "sk_adam_flat_packed",
     "sk_target_y", "sk_replay_insert", "sk_replay_sample", "sk_grad_pack_flat",
     "sk_critic_grad_bootstrap",
 )
@@ -120,6 +121,8 @@ def load(build_if_missing=True):
         "sk_grad_pack": ([P, P, P, i32, P, P, P, i32, P, P], ctypes.c_int),
         "sk_critic_grad": ([P, P, P, P, i64, f32, u64, P, P, P, i32, P, P, P], ctypes.c_int),
         "sk_actor_grad": ([P, P, P, i64, f32, P, P, i32, P, P], ctypes.c_int),
+        "sk_adam_flat_packed": ([P, i32, i32, P, P, i32, P, P, P, P, f32, f32, f32, f32, P, f32, P, f32, P, P, P, P],
+                                ctypes.c_int),
         "sk_adam_flat": ([P, i32, i32, P, P, i32, P, P, P, P, f32, f32, f32, f32, P, f32, P, f32, P, P, P],
                          ctypes.c_int),
         "sk_target_y": ([P, P, P, P, P, f32, P, i64, P], ctypes.c_int),

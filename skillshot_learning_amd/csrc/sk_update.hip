@@ -43,6 +43,24 @@ using namespace skmlp;
 
 constexpr int kThreads = 512;  // 8 waves
 
+// Phase timestamps of the first and last workgroup (diagnostic builds only:
+// -DSK_TRACE, read back with sk_debug_update_trace; tools/trace_update.py)
+#ifdef SK_TRACE
+__device__ unsigned long long g_sk_trace[2][32][2];
+#define SK_TP(k)                                                                             \
+  do {                                                                                       \
+    if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1)) {              \
+      const int wg_ = blockIdx.x == 0 ? 0 : 1;                                               \
+      g_sk_trace[wg_][k][0] = __builtin_amdgcn_s_memtime();                                  \
+      g_sk_trace[wg_][k][1] = wall_clock64();                                                \
+    }                                                                                        \
+  } while (0)
+#else
+#define SK_TP(k) \
+  do {           \
+  } while (0)
+#endif
+
 // grad pack layout (bytes)
 constexpr size_t kGW1 = 0;                        // 8 frags   (n-tile of 256 hidden)
 constexpr size_t kGW2 = kGW1 + 8 * 1024;          // 64 frags  (nt 0..3 of 128 out) x (kk 0..15 of 256 in)
@@ -393,6 +411,7 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad(const float* __restric
                                                           const char* __restrict__ tcpack) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const Lds L = carve(smem, false);
+  SK_TP(0);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5;
   const uint64_t call = (uint64_t)*call_ctr;
   const bf16x8* fW1_ = (const bf16x8*)(gpack + kGW1);
@@ -409,6 +428,7 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad(const float* __restric
   const int u = 32 * (w & 3) + (lane & 31);  // their layer-2 unit
   if (threadIdx.x < 4) L.RED[threadIdx.x] = 0.f;
   __syncthreads();
+  SK_TP(1);
   for (int sub = 0; sub < sub_per_wg; ++sub) {
     const int64_t row0 = ((int64_t)blockIdx.x * sub_per_wg + sub) * 32;
     if (row0 >= B) break;  // uniform across the workgroup
@@ -431,13 +451,17 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad(const float* __restric
         L.RB[threadIdx.x] = ok ? R[row0 + threadIdx.x] : 0.f;
         L.DB[threadIdx.x] = ok ? D[row0 + threadIdx.x] : 0.f;
       }
+      SK_TP(2);
       bootstrap_target(L, tapack, tcpack, gamma, w, lane);
+      SK_TP(3);
     } else if (threadIdx.x < 32) {
       L.Y[threadIdx.x] = row0 + threadIdx.x < B ? Y[row0 + threadIdx.x] : 0.f;
     }
     __syncthreads();
+    SK_TP(4);
     layer1<true>(L.Sr, fW1, tail, w, lane, L.H1, L.H1T, seed, call, row0, mask_out, B);
     __syncthreads();
+    SK_TP(5);
     float h2v[16];
     if (l2) {
       const f32x16 acc = layer2(L.H1, fW2, w, lane);
@@ -450,6 +474,7 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad(const float* __restric
       }
     }
     __syncthreads();
+    SK_TP(6);
     {  // q and dL/dq per row (all threads: row_dot128)
       const int i = threadIdx.x >> 4;
       const float q = tail[kTB3] + row_dot128(L.H2f, kLdH2f, tail + kTW3, 1);
@@ -461,6 +486,7 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad(const float* __restric
       }
     }
     __syncthreads();
+    SK_TP(7);
     if (l2) {
       const float w3 = tail[kTW3 + u];
 #pragma unroll
@@ -481,11 +507,14 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad(const float* __restric
       }
     }
     __syncthreads();
+    SK_TP(8);
     backward_12<true>(L, fW2T, w, lane, gW2, gW1, gb1);
     __syncthreads();
+    SK_TP(9);
   }
   float* P = partial + (int64_t)blockIdx.x * kCP;
   store_w12(P, kCPW2ld, w, lane, gW2, gW1, gb1);
+  SK_TP(10);
   gb2 += __shfl_xor(gb2, 32, 64);
   gw2a0 += __shfl_xor(gw2a0, 32, 64);
   gw2a1 += __shfl_xor(gw2a1, 32, 64);
@@ -505,6 +534,7 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad(const float* __restric
     P[kCPB3] = L.RED[0];
     if (loss_out) atomicAdd(loss_out, L.RED[1]);
   }
+  SK_TP(11);
 }
 
 // ---------------------------------------------------------------- actor step
@@ -517,6 +547,7 @@ __global__ void __launch_bounds__(kThreads) k_actor_grad(const float* __restrict
                                                          float* step_ctr, int n_steps, float* __restrict__ q_out) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const Lds L = carve(smem, true);
+  SK_TP(0);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5;
 
   if (blockIdx.x == 0 && threadIdx.x < n_steps) step_ctr[threadIdx.x] += 1.0f;  // Adam's step (read by k_adam_flat)
@@ -529,6 +560,7 @@ __global__ void __launch_bounds__(kThreads) k_actor_grad(const float* __restrict
   const int u = 32 * (w & 3) + (lane & 31);  // their layer-2 unit
   if (threadIdx.x < 4) L.RED[threadIdx.x] = 0.f;
   __syncthreads();
+  SK_TP(1);
   for (int sub = 0; sub < sub_per_wg; ++sub) {
     const int64_t row0 = ((int64_t)blockIdx.x * sub_per_wg + sub) * 32;
     if (row0 >= B) break;  // uniform across the workgroup
@@ -544,9 +576,11 @@ __global__ void __launch_bounds__(kThreads) k_actor_grad(const float* __restrict
     const float* ct = (const float*)(cp + kGTail);
     load_states(L, S, row0, B);
     __syncthreads();
+    SK_TP(2);
     layer1<false>(L.Sr, aW1, at, w, lane, L.H1, L.H1T, 0, 0, 0, nullptr, B);
     layer1<false>(L.Sr, cW1, ct, w, lane, L.H1C, nullptr, 0, 0, 0, nullptr, B);
     __syncthreads();
+    SK_TP(3);
     if (l2) {  // actor h2 -> H2f (fp32, kept for the backward)
       const f32x16 acc = layer2(L.H1, aW2, w, lane);
       const float b2 = at[kTB2 + u];
@@ -554,6 +588,7 @@ __global__ void __launch_bounds__(kThreads) k_actor_grad(const float* __restrict
       for (int v = 0; v < 16; ++v) L.H2f[drow(v, lane) * kLdH2f + u] = fmaxf(acc[v] + b2, 0.f);
     }
     __syncthreads();
+    SK_TP(4);
     {  // mu(s) = tanh(W3 h2 + b3) (all threads: row_dot128)
       const int i = threadIdx.x >> 4, c = threadIdx.x & 15;
       const float z0 = row_dot128(L.H2f, kLdH2f, at + kTW3, 1);
@@ -561,6 +596,7 @@ __global__ void __launch_bounds__(kThreads) k_actor_grad(const float* __restrict
       if (c < 2) L.A[2 * i + c] = tanhf((c ? z1 : z0) + at[kTB3 + c]);
     }
     __syncthreads();
+    SK_TP(5);
     {  // critic layer 2 at (s, mu(s)): dQ/dz2 = W3 relu'(z2) (rows beyond B: 0)
       f32x16 acc = {0};
       if (l2) acc = layer2(L.H1C, cW2, w, lane);
@@ -591,6 +627,7 @@ __global__ void __launch_bounds__(kThreads) k_actor_grad(const float* __restrict
       if (c == 0 && q_out && row0 + i < B) qsum += ct[kTB3] + qrow;
     }
     __syncthreads();
+    SK_TP(6);
     if (l2) {  // dZ2 = (dz3 W3) relu'(h2);  dW3[j][u] += sum_i dz3[i][j] h2[i][u]
       const float w30 = at[kTW3 + u], w31 = at[kTW3 + kH2 + u];
 #pragma unroll
@@ -611,11 +648,14 @@ __global__ void __launch_bounds__(kThreads) k_actor_grad(const float* __restrict
       }
     }
     __syncthreads();
+    SK_TP(7);
     backward_12<false>(L, aW2T, w, lane, gW2, gW1, gb1);
     __syncthreads();
+    SK_TP(8);
   }
   float* P = partial + (int64_t)blockIdx.x * kAP;
   store_w12(P, kH1, w, lane, gW2, gW1, gb1);
+  SK_TP(9);
   gb2 += __shfl_xor(gb2, 32, 64);
   gw30 += __shfl_xor(gw30, 32, 64);
   gw31 += __shfl_xor(gw31, 32, 64);
@@ -632,6 +672,7 @@ __global__ void __launch_bounds__(kThreads) k_actor_grad(const float* __restrict
   __syncthreads();
   if (threadIdx.x < 2) P[kAPB3 + threadIdx.x] = L.RED[threadIdx.x];
   if (threadIdx.x == 0 && q_out) atomicAdd(q_out, L.RED[2]);
+  SK_TP(10);
 }
 
 // ---------------------------------------------------------------- Adam
@@ -645,29 +686,127 @@ __global__ void __launch_bounds__(kThreads) k_actor_grad(const float* __restrict
 // kernel consumed them, before the next one): stat_out = stat_acc * scale and
 // stat_acc = 0 (the loss accumulator of the gradient kernel), ++*counter (its
 // dropout call number) — one launch fewer each than torch ops would cost.
-__global__ void k_adam_flat(const float* __restrict__ partial, int G, int P, const float* __restrict__ grad_in,
+// ---------------------------------------------------------------- packs from Adam
+// Every packed entry is a function of one parameter, so the Adam launch that
+// produces a parameter also writes its packed copies (replacing the separate
+// k_grad_pack / k_grad_pack_flat / k_actor_pack launches of a step):
+// scatter_grad_pack is the inverse of grad_pack_body's index map, and
+// scatter_fwd_pack of k_actor_pack's (sk_actor.hip).  Padding entries (W1 k
+// >= 12, unused tail slots) are never written: they keep the zeros of the
+// initial full pack.
+struct PackOut {
+  char* gp;   // grad pack of the stepped net (nullable)
+  char* tp;   // grad pack of its soft-updated target (nullable)
+  char* fp;   // actor forward pack (sk_actor_pack layout; nullable, actor only)
+  int ld2, n_out;
+};
+
+__device__ __forceinline__ void scatter_grad_pack(char* out, int p, float v, int ld2, int n_out) {
+  float* tail = (float*)(out + kGTail);
+  if (p < kPB1) {  // W1[n][k]
+    const int n = p / kIn, k = p - n * kIn;
+    const int lane = (n & 31) + 32 * (k >> 3);
+    ((short*)(out + kGW1))[((n >> 5) * 64 + lane) * 8 + (k & 7)] = f2bf(v);
+    return;
+  }
+  if (p < kPW2) {
+    tail[kTB1 + p - kPB1] = v;
+    return;
+  }
+  const int q = p - kPW2;
+  if (q < kH2 * ld2) {  // W2[o][i]
+    const int o = q / ld2, i = q - o * ld2;
+    if (i < kH1) {
+      const short b = f2bf(v);
+      const int l2 = (o & 31) + 32 * ((i >> 3) & 1);
+      ((short*)(out + kGW2))[(((o >> 5) * 16 + (i >> 4)) * 64 + l2) * 8 + (i & 7)] = b;
+      const int lt = (i & 31) + 32 * ((o >> 3) & 1);
+      ((short*)(out + kGW2T))[(((i >> 5) * 8 + (o >> 4)) * 64 + lt) * 8 + (o & 7)] = b;
+    } else {
+      tail[kTW2a + 2 * o + (i - kH1)] = v;
+    }
+    return;
+  }
+  const int r = q - kH2 * ld2;
+  if (r < kH2) tail[kTB2 + r] = v;
+  else if (r < kH2 + n_out * kH2) tail[kTW3 + r - kH2] = v;
+  else tail[kTB3 + r - kH2 - n_out * kH2] = v;
+}
+
+__device__ __forceinline__ void scatter_fwd_pack(char* out, int p, float v) {  // actor: ld2 = 256, n_out = 2
+  float* bias = (float*)(out + kOffB);
+  if (p < kPB1) {
+    const int n = p / kIn, k = p - n * kIn;
+    const int idx = ((n >> 5) * 64 + (n & 31) + 32 * (k >> 3)) * 8 + (k & 7);
+    ((short*)(out + kOffW1))[idx] = f2bf(v);
+    ((short*)(out + kOffW1s))[idx] = f2bf(v * v);
+    return;
+  }
+  if (p < kPW2) {
+    bias[p - kPB1] = v;
+    return;
+  }
+  const int q = p - kPW2;
+  if (q < kH2 * kH1) {
+    const int o = q / kH1, i = q - o * kH1;
+    const int kk = 2 * (i >> 5) + ((i >> 4) & 1), j = 4 * ((i >> 3) & 1) + (i & 3);
+    const int lane = (o & 31) + 32 * ((i >> 2) & 1);
+    const int idx = (((o >> 5) * 16 + kk) * 64 + lane) * 8 + j;
+    ((short*)(out + kOffW2))[idx] = f2bf(v);
+    ((short*)(out + kOffW2s))[idx] = f2bf(v * v);
+    return;
+  }
+  const int r = q - kH2 * kH1;
+  if (r < kH2) {
+    bias[kH1 + r] = v;
+  } else if (r < kH2 + kOut * kH2) {
+    float* w3f = (float*)(out + kOffW3f);
+    w3f[r - kH2] = v;
+    w3f[256 + r - kH2] = v * v;
+  } else {
+    bias[kH1 + kH2 + r - kH2 - kOut * kH2] = v;
+  }
+}
+
+constexpr int kAdamParams = 64, kAdamSlices = 4;
+
+__global__ void __launch_bounds__(kAdamParams * kAdamSlices) k_adam_flat(const float* __restrict__ partial, int G, int P, const float* __restrict__ grad_in,
                             float* __restrict__ grad_out, int apply, float* __restrict__ param, float* __restrict__ m,
                             float* __restrict__ v, const float* __restrict__ step_ctr, float lr, float beta1,
                             float beta2, float eps, float* __restrict__ target, float tau, float* stat_acc,
-                            float stat_scale, float* stat_out, int64_t* counter) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (apply && p == 0) {
+                            float stat_scale, float* stat_out, int64_t* counter, PackOut po) {
+  // a workgroup owns kAdamParams consecutive parameters; its kAdamSlices
+  // waves each sum every kAdamSlices-th partial of them (64-lane coalesced
+  // rows, 8 loads in flight per lane), then fold through LDS: 4x the waves
+  // of one-thread-per-parameter, for the latency of the partial reads
+  __shared__ float red[kAdamSlices - 1][kAdamParams];
+  const int lane = threadIdx.x % kAdamParams, slice = threadIdx.x / kAdamParams;
+  const int p = blockIdx.x * kAdamParams + lane;
+  if (apply && p == 0 && slice == 0) {
     if (stat_acc) {
       if (stat_out) *stat_out = *stat_acc * stat_scale;
       *stat_acc = 0.f;
     }
     if (counter) *counter += 1;
   }
-  if (p >= P) return;
-  float g = grad_in ? grad_in[p] : 0.f;
+  const bool in = p < P;
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // 8 independent loads in flight
-  int k = 0;
-  for (; k + 8 <= G; k += 8) {
+  if (in) {
+    int k = slice;
+    for (; k + 7 * kAdamSlices < G; k += 8 * kAdamSlices) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] += partial[(int64_t)(k + j) * P + p];
+      for (int j = 0; j < 8; ++j) acc[j] += partial[(int64_t)(k + j * kAdamSlices) * P + p];
+    }
+    for (; k < G; k += kAdamSlices) acc[0] += partial[(int64_t)k * P + p];
   }
-  for (; k < G; ++k) acc[0] += partial[(int64_t)k * P + p];
-  g += ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  const float part = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  if (slice > 0) red[slice - 1][lane] = part;
+  __syncthreads();
+  if (slice > 0 || !in) return;
+  float g = grad_in ? grad_in[p] : 0.f;
+  g += part;
+#pragma unroll
+  for (int j = 0; j < kAdamSlices - 1; ++j) g += red[j][lane];
   if (grad_out) grad_out[p] = g;
   if (!apply) return;
   const float t = step_ctr[0];
@@ -680,7 +819,13 @@ __global__ void k_adam_flat(const float* __restrict__ partial, int G, int P, con
   const float denom = sqrtf(vv) / sqrtf(bc2) + eps;
   const float w = param[p] - (lr / bc1) * mm / denom;
   param[p] = w;
-  if (target) target[p] = target[p] + tau * (w - target[p]);
+  if (po.gp) scatter_grad_pack(po.gp, p, w, po.ld2, po.n_out);
+  if (po.fp) scatter_fwd_pack(po.fp, p, w);
+  if (target) {
+    const float tw = target[p] + tau * (w - target[p]);
+    target[p] = tw;
+    if (po.tp) scatter_grad_pack(po.tp, p, tw, po.ld2, po.n_out);
+  }
 }
 
 int64_t subtiles_per_wg(int64_t B) {  // <= 128 workgroups, >= 1 sub-tile each
@@ -783,17 +928,44 @@ int sk_actor_grad(const void* apack, const void* cpack, const float* obs, int64_
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
 }
 
+int sk_adam_flat_packed(const float* partial, int32_t n_partials, int32_t n_params, const float* grad_in,
+                        float* grad_out, int32_t apply, float* param, float* exp_avg, float* exp_avg_sq,
+                        const float* step_counter, float lr, float beta1, float beta2, float eps, float* target,
+                        float tau, float* stat_acc, float stat_scale, float* stat_out, int64_t* counter,
+                        const sk_pack_targets* packs, void* stream) {
+  if (n_params <= 0 || n_partials < 0 || (n_partials > 0 && !partial)) return SK_EINVAL;
+  if (apply && (!param || !exp_avg || !exp_avg_sq || !step_counter)) return SK_EINVAL;
+  PackOut po = {nullptr, nullptr, nullptr, kH1, 1};
+  if (packs && apply) {
+    const int ld2 = packs->ld2, n_out = packs->n_out;
+    if ((ld2 != kH1 && ld2 != kH1 + 2) || (n_out != 1 && n_out != 2)) return SK_EINVAL;
+    if (n_params != kPW2 + kH2 * ld2 + kH2 + n_out * kH2 + n_out) return SK_EINVAL;
+    if (packs->actor_fwd_pack && (ld2 != kH1 || n_out != kOut)) return SK_EINVAL;
+    if (packs->target_gpack && !target) return SK_EINVAL;
+    for (const void* b : {packs->param_gpack, packs->target_gpack, packs->actor_fwd_pack})
+      if (((uintptr_t)b) & 15) return SK_EINVAL;
+    po = {(char*)packs->param_gpack, (char*)packs->target_gpack, (char*)packs->actor_fwd_pack, ld2, n_out};
+  }
+  k_adam_flat<<<(n_params + kAdamParams - 1) / kAdamParams, kAdamParams * kAdamSlices, 0, (hipStream_t)stream>>>(
+      partial, n_partials, n_params, grad_in, grad_out, apply, param, exp_avg, exp_avg_sq, step_counter, lr, beta1,
+      beta2, eps, target, tau, stat_acc, stat_scale, stat_out, counter, po);
+  return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
+}
+
 int sk_adam_flat(const float* partial, int32_t n_partials, int32_t n_params, const float* grad_in, float* grad_out,
                  int32_t apply, float* param, float* exp_avg, float* exp_avg_sq, const float* step_counter, float lr,
                  float beta1, float beta2, float eps, float* target, float tau, float* stat_acc, float stat_scale,
                  float* stat_out, int64_t* counter, void* stream) {
-  if (n_params <= 0 || n_partials < 0 || (n_partials > 0 && !partial)) return SK_EINVAL;
-  if (apply && (!param || !exp_avg || !exp_avg_sq || !step_counter)) return SK_EINVAL;
-  k_adam_flat<<<(n_params + 255) / 256, 256, 0, (hipStream_t)stream>>>(partial, n_partials, n_params, grad_in,
-                                                                       grad_out, apply, param, exp_avg, exp_avg_sq,
-                                                                       step_counter, lr, beta1, beta2, eps, target,
-                                                                       tau, stat_acc, stat_scale, stat_out, counter);
-  return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
+  return sk_adam_flat_packed(partial, n_partials, n_params, grad_in, grad_out, apply, param, exp_avg, exp_avg_sq,
+                             step_counter, lr, beta1, beta2, eps, target, tau, stat_acc, stat_scale, stat_out, counter,
+                             nullptr, stream);
 }
 
 }  // extern "C"
+
+#ifdef SK_TRACE
+// diagnostic builds only (not in include/skillshot.h): [2 wg][32 points][memtime, realtime]
+extern "C" int sk_debug_update_trace(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sk_trace), sizeof(g_sk_trace)) == hipSuccess ? SK_OK : SK_EHIP;
+}
+#endif

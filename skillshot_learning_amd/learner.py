@@ -419,7 +419,7 @@ class DDPG:
         else:
             s, a, r, s2, d = self.replay.sample(batch, generator=self.gen)
         s, a, r, s2, d = self._allgather_batch(s, a, r, s2, d)
-        if self._fused is not None:  # target, critic step, actor step, soft updates: 4 launches + 2 pack launches
+        if self._fused is not None:  # critic step (bootstrap inside) + actor step: 4 launches, Adam writes packs
             if self.gamma > 0.0:
                 lc = self._fused.critic_step(s, a, s2=s2, r=r, d=d, gamma=self.gamma)
             else:
@@ -506,6 +506,8 @@ class SkillshotLearner:
         if actor_kernel and self.device.type == "cuda":
             from .actor_kernel import ActorKernel
             self.actor_kernel = ActorKernel(self.model_actor, seed=seed * 1000003 + env_offset)
+            if self.ddpg._fused is not None:  # the actor's Adam launch writes the forward pack too
+                self.ddpg._fused.fwd_pack = self.actor_kernel.buf
         self.progress = dict(epoch_ticks=[], epoch_winner=[])
 
     # reference attribute names
@@ -517,8 +519,17 @@ class SkillshotLearner:
 
     def models_fit(self, states, actions, rewards):
         self.ddpg.models_fit(states, actions, rewards)
-        if self.actor_kernel is not None:
-            self.actor_kernel.refresh()
+        self._refresh_actor_pack()
+
+    def _refresh_actor_pack(self):
+        """repack the actor forward kernel's weights after an update, unless
+        the fused update's Adam launch already wrote them"""
+        if self.actor_kernel is None:
+            return
+        fu = self.ddpg._fused
+        if fu is not None and fu.fwd_pack is self.actor_kernel.buf:
+            return
+        self.actor_kernel.refresh()
 
     def replay_update(self, batch):
         return self.ddpg.replay_update(batch)
@@ -622,8 +633,7 @@ class SkillshotLearner:
             if self.replay.size >= warmup:
                 for _ in range(updates_per_tick):
                     stats.append(self.replay_update(batch))
-            if self.actor_kernel is not None:
-                self.actor_kernel.refresh()
+            self._refresh_actor_pack()
         return stats
 
     def tick_graph(self, batch=256, updates_per_tick=1, ticks_per_graph=2, warmup=3):
@@ -669,6 +679,8 @@ class SkillshotLearner:
             self.ddpg.target_critic.load_state_dict(d["target_critic"])
         if self.actor_kernel is not None:
             self.actor_kernel.refresh()
+        if self.ddpg._fused is not None:
+            self.ddpg._fused.pack()
         if self.ddpg._tq is not None:
             self.ddpg._tq.refresh()
 
@@ -739,8 +751,7 @@ class TickGraph:
         if update:
             for _ in range(self.updates):
                 L.ddpg.replay_update(self.batch, device_sampling=True)
-            if L.actor_kernel is not None:
-                L.actor_kernel.refresh()
+            L._refresh_actor_pack()
 
     def run(self, n=1):
         """n graph replays (n * ticks_per_graph ticks) on the graph's stream."""

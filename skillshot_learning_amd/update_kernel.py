@@ -29,6 +29,12 @@ def _p(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
+class PackTargets(ctypes.Structure):
+    """sk_pack_targets (include/skillshot.h): the packed copies an Adam launch writes."""
+    _fields_ = [("param_gpack", ctypes.c_void_p), ("target_gpack", ctypes.c_void_p),
+                ("actor_fwd_pack", ctypes.c_void_p), ("ld2", ctypes.c_int32), ("n_out", ctypes.c_int32)]
+
+
 def flatten_module(module):
     """Rebind every parameter of `module` as a view of one flat fp32 buffer
     (idempotent); returns the buffer."""
@@ -116,6 +122,9 @@ class FusedUpdate:
         self._li = [0, 0]
         self._partials = {}
         self.grad_flat = None
+        # the actor forward kernel's weight pack (ActorKernel.buf), written by
+        # the actor's Adam launch when bound (SkillshotLearner binds it)
+        self.fwd_pack = None
         self.pack()
 
     def _stream(self):
@@ -129,11 +138,6 @@ class FusedUpdate:
             t = self._partials[key] = torch.empty((g, n_params), dtype=torch.float32, device=self.dev)
         return t
 
-    def _pack(self, m, buf, ld2, n_out):
-        rc = self.L.sk_grad_pack(_p(m.l1.weight), _p(m.l1.bias), _p(m.l2.weight), ld2, _p(m.l2.bias),
-                                 _p(m.l3.weight), _p(m.l3.bias), n_out, _p(buf), self._stream())
-        _capi.check(rc)
-
     def _pack_flat(self, jobs):
         """one launch packing [(flat params, ld2, n_out, out buffer)]"""
         k = len(jobs)
@@ -143,25 +147,32 @@ class FusedUpdate:
         outs = (ctypes.c_void_p * k)(*[o.data_ptr() for _, _, _, o in jobs])
         _capi.check(self.L.sk_grad_pack_flat(flats, ld2s, nouts, outs, k, self._stream()))
 
-    def _after_actor_jobs(self):
-        """the packs that change with the actor step (actor) and the soft updates
-        of both targets, packed in one launch after the actor's Adam"""
-        jobs = [(self.fa, 256, 2, self.gpa)]
-        if self.ta is not None:
-            jobs += [(self.ta, 256, 2, self.gpta), (self.tc, 258, 1, self.gptc)]
-        return jobs
-
     @torch.no_grad()
     def pack(self):
-        self._pack_flat(self._after_actor_jobs() + [(self.fc, 258, 1, self.gpc)])
+        """full packs of every net from its parameters (at start, and after
+        parameters change outside the Adam launches, e.g. load_state_dict);
+        between steps each Adam launch rewrites the entries it produces"""
+        jobs = [(self.fa, 256, 2, self.gpa), (self.fc, 258, 1, self.gpc)]
+        if self.ta is not None:
+            jobs += [(self.ta, 256, 2, self.gpta), (self.tc, 258, 1, self.gptc)]
+        self._pack_flat(jobs)
 
     def _loss_slot(self, k):
         i = self._li[k]
         self._li[k] = (i + 1) % self.LOSS_HIST
         return self.loss_hist[k, i]
 
-    def _adam(self, part, flat, st, target, stat=None, scale=1.0, out=None, counter=None):
+    def _packs(self, critic):
+        """the packs the Adam launch of a step keeps current"""
+        if critic:
+            return PackTargets(self.gpc.data_ptr(), self.gptc.data_ptr() if self.tc is not None else None, None,
+                               258, 1)
+        return PackTargets(self.gpa.data_ptr(), self.gpta.data_ptr() if self.ta is not None else None,
+                           self.fwd_pack.data_ptr() if self.fwd_pack is not None else None, 256, 2)
+
+    def _adam(self, part, flat, st, target, stat=None, scale=1.0, out=None, counter=None, packs=None):
         P = flat.numel()
+        pk = ctypes.byref(packs) if packs is not None else None
         tau = float(self.d.tau) if target is not None else 0.0
         world = self.d.world()
         if world > 1:  # sum partials -> flat grad -> RCCL mean -> apply
@@ -172,13 +183,14 @@ class FusedUpdate:
                                             0.0, 0.0, 0.0, 0.0, None, 0.0, None, 0.0, None, None, self._stream()))
             dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.d.group)
             g /= world
-            _capi.check(self.L.sk_adam_flat(None, 0, P, _p(g), None, 1, _p(flat), _p(st.m), _p(st.v), _p(st.steps),
-                                            st.lr, st.b1, st.b2, st.eps, _p(target), tau, _p(stat), float(scale),
-                                            _p(out), _p(counter), self._stream()))
+            _capi.check(self.L.sk_adam_flat_packed(None, 0, P, _p(g), None, 1, _p(flat), _p(st.m), _p(st.v),
+                                                   _p(st.steps), st.lr, st.b1, st.b2, st.eps, _p(target), tau,
+                                                   _p(stat), float(scale), _p(out), _p(counter), pk, self._stream()))
         else:
-            _capi.check(self.L.sk_adam_flat(_p(part), part.shape[0], P, None, None, 1, _p(flat), _p(st.m), _p(st.v),
-                                            _p(st.steps), st.lr, st.b1, st.b2, st.eps, _p(target), tau, _p(stat),
-                                            float(scale), _p(out), _p(counter), self._stream()))
+            _capi.check(self.L.sk_adam_flat_packed(_p(part), part.shape[0], P, None, None, 1, _p(flat), _p(st.m),
+                                                   _p(st.v), _p(st.steps), st.lr, st.b1, st.b2, st.eps, _p(target),
+                                                   tau, _p(stat), float(scale), _p(out), _p(counter), pk,
+                                                   self._stream()))
 
     @torch.no_grad()
     def critic_step(self, s, a, target=None, mask_out=None, s2=None, r=None, d=None, gamma=0.0):
@@ -203,8 +215,8 @@ class FusedUpdate:
                                        self._stream())
         _capi.check(rc)
         loss = self._loss_slot(0)
-        self._adam(part, self.fc, st, self.tc, stat=self.stats[0:1], scale=1.0 / B, out=loss, counter=self.calls)
-        self._pack(self.d.model_critic, self.gpc, 258, 1)
+        self._adam(part, self.fc, st, self.tc, stat=self.stats[0:1], scale=1.0 / B, out=loss, counter=self.calls,
+                   packs=self._packs(critic=True))
         return loss
 
     @torch.no_grad()
@@ -219,8 +231,8 @@ class FusedUpdate:
                                   st.steps.numel(), _p(self.stats[1:]), self._stream())
         _capi.check(rc)
         loss = self._loss_slot(1)
-        self._adam(part, self.fa, st, self.ta, stat=self.stats[1:], scale=-1.0, out=loss)
-        self._pack_flat(self._after_actor_jobs())
+        self._adam(part, self.fa, st, self.ta, stat=self.stats[1:], scale=-1.0, out=loss,
+                   packs=self._packs(critic=False))
         return loss
 
     @torch.no_grad()

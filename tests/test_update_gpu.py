@@ -241,6 +241,30 @@ def test_fused_tick_graph(mods):
     assert any((p - q).abs().max() > 0 for p, q in zip(L.model_actor.parameters(), w0))
 
 
+def test_adam_launches_keep_every_pack_current(mods):
+    """The Adam launches write the packed copies of what they produce
+    (sk_adam_flat_packed): after training ticks, the critic / actor /
+    target grad packs and the actor forward pack equal, byte for byte, full
+    packs made from the parameters."""
+    learner = mods
+    L = learner.SkillshotLearner(n_envs=256, device="cuda", seed=4, gamma=0.9, tau=0.05, replay_capacity=1 << 14)
+    fu = L.ddpg._fused
+    assert fu.fwd_pack is L.actor_kernel.buf
+    w0 = [p.clone() for p in L.model_actor.parameters()]
+    L.train_ticks(6, batch=256)
+    torch.cuda.synchronize()
+    assert any((p - q).abs().max() > 0 for p, q in zip(L.model_actor.parameters(), w0))
+    names = ("gpa", "gpc", "gpta", "gptc")
+    kept = {k: getattr(fu, k).clone() for k in names}
+    kept_fwd = L.actor_kernel.buf.clone()
+    fu.pack()
+    L.actor_kernel.refresh()
+    torch.cuda.synchronize()
+    for k in names:
+        assert torch.equal(kept[k], getattr(fu, k)), k
+    assert torch.equal(kept_fwd, L.actor_kernel.buf)
+
+
 # ------------------------------------------------- 2 ranks on one GPU (gloo)
 def _free_port():
     import socket

@@ -64,8 +64,7 @@ def main():
             e[3].record()
         for _ in range(a.updates):
             L.replay_update(a.batch)
-        if L.actor_kernel is not None:
-            L.actor_kernel.refresh()
+        L._refresh_actor_pack()
         if timed:
             e[4].record()
             for k, name in enumerate(phases):

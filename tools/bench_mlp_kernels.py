@@ -52,12 +52,16 @@ def main():
         act = torch.rand(rows, 2, device="cuda") * 2 - 1
         y = torch.empty(rows, 2, device="cuda")
         q = torch.empty(rows, device="cuda")
+        rw = torch.rand(rows, device="cuda")
+        dn = torch.zeros(rows, device="cuda")
         cases = {
             "actor": (lambda: ak(s, 0.0, out=y), ACTOR_FLOP, 56),
             "actor_noise": (lambda: ak(s, 0.5, out=y), ACTOR_NOISE_FLOP, 56),
             "critic": (lambda: ck(s, act, out=q), CRITIC_FLOP, 60),
             "target_q": (lambda: tk(s, out=q), ACTOR_FLOP + CRITIC_FLOP, 52),
             "critic_grad": (lambda: fu.grads("critic", s, act, q), CRITIC_GRAD_FLOP, 60),
+            "critic_grad_boot": (lambda: fu.grads("critic", s, act, None, None, s, rw, dn, 0.99),
+                                 CRITIC_GRAD_FLOP + ACTOR_FLOP + CRITIC_FLOP, 116),
             "actor_grad": (lambda: fu.grads("actor", s), ACTOR_GRAD_FLOP, 48),
         }
         for name, (fn, flop, byts) in cases.items():
