@@ -233,6 +233,15 @@ int sk_actor_forward(const void* packed, const float* obs, float* actions, int64
  * the counter between calls (stream-ordered). */
 int sk_actor_forward_dev(const void* packed, const float* obs, float* actions, int64_t rows, float noise_sd,
                          uint64_t seed, const uint64_t* call_counter, void* stream);
+/* sk_actor_forward_dev that advances the counter itself: call_counter is
+ * uint64[2] = {call number, 0}; a noisy launch draws with call number
+ * call_counter[0] + 1 and stores that number back into call_counter[0] when
+ * its last workgroup finishes (call_counter[1] is its arrival slot: keep it
+ * 0 between launches).  No stream-ordered add is needed before the call, so
+ * a captured learner tick has one launch fewer.  noise_sd = 0 leaves the
+ * counter untouched. */
+int sk_actor_forward_advance(const void* packed, const float* obs, float* actions, int64_t rows, float noise_sd,
+                             uint64_t seed, uint64_t* call_counter, void* stream);
 
 /* --- critic forward and the DDPG bootstrap target (A16) ------------------- */
 

@@ -2,10 +2,11 @@
 
 The torch module stays the master copy (fp32, trained by autograd); after each
 optimiser step `refresh()` repacks its weights into the kernel's bf16 MFMA
-fragment layout on device (one small kernel, no host copy).  The noise call
-number lives on device (sk_actor_forward_dev) and is advanced by a stream-
-ordered add before each noisy call, so a captured hipGraph of the learner tick
-draws fresh parameter noise on every replay.
+fragment layout on device (one small kernel, no host copy) — unless the
+fused update's Adam launch writes that pack itself.  The noise call number
+lives on device and each noisy launch advances it (sk_actor_forward_advance),
+so a captured hipGraph of the learner tick draws fresh parameter noise on
+every replay with no extra launch.
 """
 import ctypes
 
@@ -26,7 +27,9 @@ class ActorKernel:
         self.buf = torch.empty(int(self.L.sk_actor_packed_bytes()), dtype=torch.uint8, device=self.device)
         self.seed = int(seed) & ((1 << 64) - 1)
         self.calls = 0
-        self.counter = torch.zeros(1, dtype=torch.int64, device=self.device)  # device noise-call number
+        # device noise-call number and the launch's arrival slot (sk_actor_forward_advance)
+        self._ctr = torch.zeros(2, dtype=torch.int64, device=self.device)
+        self.counter = self._ctr[:1]
         self.refresh()
 
     def _stream(self):
@@ -53,11 +56,9 @@ class ActorKernel:
         m = x.shape[0]
         y = out if out is not None else torch.empty((m, 2), dtype=torch.float32, device=self.device)
         self.calls += 1
-        if noise_sd != 0.0:
-            self.counter.add_(1)
-        rc = self.L.sk_actor_forward_dev(ctypes.c_void_p(self.buf.data_ptr()), ctypes.c_void_p(x.data_ptr()),
-                                         ctypes.c_void_p(y.data_ptr()), m, float(noise_sd), self.seed,
-                                         ctypes.c_void_p(self.counter.data_ptr()), self._stream())
+        rc = self.L.sk_actor_forward_advance(ctypes.c_void_p(self.buf.data_ptr()), ctypes.c_void_p(x.data_ptr()),
+                                             ctypes.c_void_p(y.data_ptr()), m, float(noise_sd), self.seed,
+                                             ctypes.c_void_p(self._ctr.data_ptr()), self._stream())
         if rc != 0:
             raise SkillshotError(f"sk_actor_forward failed ({rc})")
         return y

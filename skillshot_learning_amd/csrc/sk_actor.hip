@@ -93,15 +93,31 @@ __global__ void k_actor_pack(const float* W1, const float* b1, const float* W2, 
 // layer 2's pre-bias mean accumulator, variance accumulator and normal draw
 // (3 x 128).
 constexpr int kDbgCols = 386 + 3 * 128;
+// With a device call counter adv = {call number, arrivals}: every workgroup has
+// read adv[0] before its first barrier; the last to finish stores the number
+// it used, so the next launch draws fresh noise without a separate add.
+__device__ __forceinline__ void advance_call(uint64_t* adv, uint64_t call) {
+  if (threadIdx.x == 0) {
+    const unsigned long long prev = atomicAdd((unsigned long long*)&adv[1], 1ull);
+    if (prev == (unsigned long long)gridDim.x - 1) {
+      adv[1] = 0;
+      adv[0] = call;
+    }
+  }
+}
+
 template <bool NOISE, bool DBG = false>
 __global__ void __launch_bounds__(threads_for<NOISE>()) k_actor_fwd(const float* __restrict__ X, float* __restrict__ out,
                                                         int64_t M, const char* __restrict__ packed, float sd,
                                                         uint64_t seed, uint64_t call,
                                                         const uint64_t* __restrict__ call_dev = nullptr,
-                                                        float* dbg = nullptr) {
+                                                        float* dbg = nullptr, uint64_t* adv = nullptr) {
   // the noise call number comes from device memory when given (graph replays
-  // then draw fresh noise per replay; the caller advances the counter)
+  // then draw fresh noise per replay): *call_dev, advanced by the caller, or,
+  // with adv, adv[0] + 1, stored back by the last workgroup (advance_call)
   if (NOISE && call_dev) call = *call_dev;  // wave-uniform scalar load
+  if (NOISE && adv) call = adv[0] + 1;
+  asm volatile("" : "+s"(call));  // read before the staging barrier (advance_call relies on it)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16x8* sW2 = (bf16x8*)smem;                               // [4][16][64]
   bf16x8* sW2s = (bf16x8*)(smem + kW2Frag);                  // NOISE only
@@ -247,6 +263,7 @@ __global__ void __launch_bounds__(threads_for<NOISE>()) k_actor_fwd(const float*
       *(float2*)(out + row * kOut) = make_float2(o[0], o[1]);
     }
   }
+  if (NOISE && adv) advance_call(adv, call);
 }
 
 // One 32-row tile per WORKGROUP: for batches too small to give every SIMD its
@@ -264,7 +281,8 @@ template <bool NOISE>
 __global__ void __launch_bounds__(kWgThreads) k_actor_fwd_wg(const float* __restrict__ X, float* __restrict__ out,
                                                             int64_t M, const char* __restrict__ packed, float sd,
                                                             uint64_t seed, uint64_t call,
-                                                            const uint64_t* __restrict__ call_dev) {
+                                                            const uint64_t* __restrict__ call_dev,
+                                                            uint64_t* adv = nullptr) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16x8* sW2 = (bf16x8*)smem;
   bf16x8* sW2s = (bf16x8*)(smem + kW2Frag);
@@ -273,6 +291,8 @@ __global__ void __launch_bounds__(kWgThreads) k_actor_fwd_wg(const float* __rest
   bf16x8* sH1 = (bf16x8*)(sB + 1024);            // [16 k-steps][64 lanes]
   float4* sPart = (float4*)(sH1 + 16 * 64);      // [4 waves][32 rows]: m0 m1 q0 q1
   if (NOISE && call_dev) call = *call_dev;
+  if (NOISE && adv) call = adv[0] + 1;
+  asm volatile("" : "+s"(call));  // read before the staging barrier (advance_call)
   {
     const uint4* g = (const uint4*)(packed + kOffW2);
     uint4* sm = (uint4*)smem;
@@ -393,6 +413,7 @@ __global__ void __launch_bounds__(kWgThreads) k_actor_fwd_wg(const float* __rest
       *(float2*)(out + row * kOut) = make_float2(o2[0], o2[1]);
     }
   }
+  if (NOISE && adv) advance_call(adv, call);
 }
 
 // launch-mode override for tests and sweeps: 0 auto, 1 tile per wave, 2 tile per workgroup
@@ -414,10 +435,12 @@ int sk_actor_pack(const float* W1, const float* b1, const float* W2, const float
 }
 
 static int actor_forward(const void* packed, const float* obs, float* actions, int64_t rows, float noise_sd,
-                         uint64_t seed, uint64_t call, const uint64_t* call_dev, void* stream) {
+                         uint64_t seed, uint64_t call, const uint64_t* call_dev, void* stream,
+                         uint64_t* adv = nullptr) {
   if (!packed || !obs || !actions || rows < 0) return SK_EINVAL;
   if ((((uintptr_t)obs) & 15) || (((uintptr_t)actions) & 7) || (((uintptr_t)packed) & 15)) return SK_EINVAL;
   if (call_dev && (((uintptr_t)call_dev) & 7)) return SK_EINVAL;
+  if (adv && (((uintptr_t)adv) & 7)) return SK_EINVAL;
   if (rows == 0) return SK_OK;
   int dev = 0;
   (void)hipGetDevice(&dev);
@@ -457,7 +480,7 @@ static int actor_forward(const void* packed, const float* obs, float* actions, i
     const int64_t wgrid = tiles < cus ? tiles : cus;
     if (noise)
       k_actor_fwd_wg<true><<<(unsigned)wgrid, kWgThreads, lds + kWgExtra, (hipStream_t)stream>>>(
-          obs, actions, rows, (const char*)packed, noise_sd, seed, call, call_dev);
+          obs, actions, rows, (const char*)packed, noise_sd, seed, call, call_dev, adv);
     else
       k_actor_fwd_wg<false><<<(unsigned)wgrid, kWgThreads, lds + kWgExtra, (hipStream_t)stream>>>(
           obs, actions, rows, (const char*)packed, 0.f, seed, call, nullptr);
@@ -465,7 +488,8 @@ static int actor_forward(const void* packed, const float* obs, float* actions, i
   }
   if (noise) {
     k_actor_fwd<true><<<(unsigned)grid, threads, lds, (hipStream_t)stream>>>(obs, actions, rows, (const char*)packed,
-                                                                            noise_sd, seed, call, call_dev);
+                                                                            noise_sd, seed, call, call_dev, nullptr,
+                                                                            adv);
   } else {
     k_actor_fwd<false><<<(unsigned)grid, threads, lds, (hipStream_t)stream>>>(obs, actions, rows,
                                                                              (const char*)packed, 0.f, seed, call);
@@ -482,6 +506,13 @@ int sk_actor_forward_dev(const void* packed, const float* obs, float* actions, i
                          uint64_t seed, const uint64_t* call_counter, void* stream) {
   if (!call_counter) return SK_EINVAL;
   return actor_forward(packed, obs, actions, rows, noise_sd, seed, 0, call_counter, stream);
+}
+
+int sk_actor_forward_advance(const void* packed, const float* obs, float* actions, int64_t rows, float noise_sd,
+                             uint64_t seed, uint64_t* call_counter, void* stream) {
+  if (!call_counter) return SK_EINVAL;
+  if (noise_sd == 0.f) return actor_forward(packed, obs, actions, rows, 0.f, seed, 0, nullptr, stream);
+  return actor_forward(packed, obs, actions, rows, noise_sd, seed, 0, nullptr, stream, call_counter);
 }
 
 // diagnostics only (not in include/skillshot.h): force the launch mode

@@ -104,6 +104,28 @@ def test_param_noise_kernel_distribution(mods):
     assert got[:, 0].unique().numel() > n // 2
 
 
+@pytest.mark.parametrize("rows", [8192, 131072])  # tile-per-workgroup and tile-per-wave launch modes
+def test_noise_counter_advances_in_kernel(mods, rows):
+    """sk_actor_forward_advance: noisy call k draws with call number k (the
+    same noise as an explicit sk_actor_forward(call=k)), the counter holds k
+    afterwards with the arrival slot back at 0, deterministic calls leave it."""
+    import ctypes
+    learner, ActorKernel = mods
+    a = _actor(learner, seed=7)
+    k = ActorKernel(a, seed=13)
+    x = torch.rand(rows, 12, device="cuda")
+    ref = torch.empty(rows, 2, device="cuda")
+    for call in (1, 2, 3):
+        got = k(x, noise_sd=0.5)
+        rc = k.L.sk_actor_forward(ctypes.c_void_p(k.buf.data_ptr()), ctypes.c_void_p(x.data_ptr()),
+                                  ctypes.c_void_p(ref.data_ptr()), rows, 0.5, k.seed, call, k._stream())
+        assert rc == 0
+        assert torch.equal(got, ref), call
+        assert k._ctr.tolist() == [call, 0]
+    k(x)
+    assert k._ctr.tolist() == [3, 0]
+
+
 def test_learner_replay_training_runs(mods):
     learner, _ = mods
     L = learner.SkillshotLearner(n_envs=2048, seed=1, tick_limit=300, replay_capacity=1 << 16, gamma=0.9, tau=0.005)
