@@ -28,6 +28,7 @@ import ctypes
 import math
 import os
 
+import numpy as np
 import torch
 import torch.distributed as dist
 import torch.nn as nn
@@ -499,6 +500,10 @@ class SkillshotLearner:
         self.action_noise_sd = 0.15                            # :63
         self.param_noise_sd = 0.5                              # :64
         self.exploration = exploration
+        # on-disk locations (:46-51; formats in persist.py)
+        self.save_location = "training_models"
+        self.actor_dir_name, self.critic_dir_name = "actor", "critic"
+        self.training_progress_dir_name, self.training_boards_dir_name = "training_progress", "training_boards"
         self.ddpg = DDPG(self.device, seed=seed, batch_size=batch_size, gamma=gamma, tau=tau,
                          replay_capacity=replay_capacity, process_group=process_group, rank_seed_offset=env_offset)
         self.gen = self.ddpg.gen
@@ -562,7 +567,7 @@ class SkillshotLearner:
                                           reset_obs=reset_obs)
 
     # ------------------------------------------------------------ training loops
-    def model_train(self, epochs, save_progress=False, save_boards=False, reward="looking"):
+    def model_train(self, epochs, save_progress=False, save_boards=False, reward="looking", board_game=0):
         """model_train (:283-384) with the reference update rule: each epoch
         resets every game (random start), plays until every game has ended
         (hit or tick limit), then fits on all of the epoch's transitions of both
@@ -570,10 +575,12 @@ class SkillshotLearner:
         (:324-326): "looking" (the one it uses), "simple", or "full"
         (calculate_rewards, computed once the episode is complete; a game on
         which the reference would raise IndexError contributes no
-        transitions).  save_* flags are accepted for signature parity (on-disk
-        formats are out of scope)."""
+        transitions).  save_progress writes the models and the epochs' ticks /
+        winners, save_boards the board sequence of game `board_game` for
+        every epoch (:370-384; formats in persist.py)."""
         g = self.game_environment
         full = reward == "full"
+        call = dict(epoch_ticks=[], epoch_winner=[], epoch_board_sequences=[])
         for _ in range(epochs):
             g.reset(random_positions=self.use_random_start)
             obs = self.prepare_states()
@@ -582,6 +589,7 @@ class SkillshotLearner:
             ticks = torch.zeros(self.n_envs, dtype=torch.int32, device=self.device)
             lengths = torch.zeros(self.n_envs, dtype=torch.long, device=self.device)
             winner = torch.zeros(self.n_envs, dtype=torch.uint8, device=self.device)
+            boards = []
             while bool(alive.any()):
                 act = self.model_act(obs)
                 out = g.step(act, obs=True, reward="looking" if full else reward, auto_reset=False)
@@ -600,6 +608,8 @@ class SkillshotLearner:
                 ticks = torch.where(newly, g.ticks, ticks)
                 winner = torch.where(newly, out["winner"], winner)
                 lengths = lengths + alive.long()
+                if save_boards and bool(alive[board_game]):  # the board after each tick (:315-317)
+                    boards.append(g.get_board(board_game).astype(np.int8))
                 alive = alive & ~done
                 obs = out["obs"]
             if full:
@@ -610,9 +620,46 @@ class SkillshotLearner:
                 K = [k & ~raised.repeat(2) for k in K]
             K = torch.cat(K)
             self.models_fit(torch.cat(S)[K], torch.cat(A)[K], torch.cat(R)[K])
-            self.progress["epoch_ticks"].append(ticks.cpu())
-            self.progress["epoch_winner"].append(winner.cpu())
+            for d in (self.progress, call):
+                d["epoch_ticks"].append(ticks.cpu())
+                d["epoch_winner"].append(winner.cpu())
+            if save_boards:
+                call["epoch_board_sequences"].append(np.stack(boards) if boards else
+                                                     np.zeros((0, 250, 250), np.int8))
+        if save_progress:
+            self.save_actor_critic_models(epochs)
+            self.save_training_progress(call)
+        if save_boards:
+            self.save_training_boards(call["epoch_board_sequences"])
         return self.progress
+
+    # ------------------------------------------------------------ on-disk formats (persist.py)
+    def save_actor_critic_models(self, epochs):
+        from . import persist
+        return persist.save_actor_critic_models(self.save_location, self.model_actor, self.model_critic, epochs)
+
+    def load_actor_critic_models(self, load_index=-1):
+        from . import persist
+        ok = persist.load_actor_critic_models(self.save_location, self.model_actor, self.model_critic, load_index)
+        if ok:
+            self._params_changed()
+        return ok
+
+    def save_training_progress(self, total_progress):
+        from . import persist
+        return persist.save_training_progress(self.save_location, total_progress)
+
+    def load_training_progress(self):
+        from . import persist
+        return persist.load_training_progress(self.save_location)
+
+    def save_training_boards(self, epoch_board_list):
+        from . import persist
+        return persist.save_training_boards(self.save_location, epoch_board_list)
+
+    def load_training_boards(self):
+        from . import persist
+        return persist.load_training_boards(self.save_location)
 
     def train_ticks(self, n_ticks, batch=256, updates_per_tick=1, warmup=None):
         """Build-side replay training: each tick acts
@@ -677,6 +724,11 @@ class SkillshotLearner:
         if self.ddpg.tau is not None and "target_actor" in d:
             self.ddpg.target_actor.load_state_dict(d["target_actor"])
             self.ddpg.target_critic.load_state_dict(d["target_critic"])
+        self._params_changed()
+
+    def _params_changed(self):
+        """repack every kernel copy of the nets after their parameters were
+        replaced outside the update launches"""
         if self.actor_kernel is not None:
             self.actor_kernel.refresh()
         if self.ddpg._fused is not None:

@@ -120,6 +120,18 @@ class VecSkillshotGame:
             self.step_counter = int(d["step_counter"])
         torch.cuda.synchronize(self.device)
 
+    def get_board(self, index=0):
+        """SkillshotGame.get_board (SkillshotGame.py:36-56) of game `index`:
+        int64 [250, 250], [x, y] indexing (host rasteriser, visualisation only)."""
+        from .game import rasterize_board
+        i = int(index)
+        pos = self.pos[i].cpu().tolist()
+        qpos = self.qpos[i].cpu().tolist()
+        rot = self.rot[i].cpu().tolist()
+        flags = int(self.misc[i, 1].item()) & 0xFFFFFFFF
+        return rasterize_board(np.zeros((250, 250), dtype=np.int64), [pos[0:2], pos[2:4]], rot,
+                               [qpos[0:2], qpos[2:4]], [flags & 0xFF, (flags >> 8) & 0xFF])
+
     # convenience decoded views -------------------------------------------
     @property
     def ticks(self):

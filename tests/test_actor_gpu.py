@@ -157,6 +157,37 @@ def test_learner_reference_epochs(mods):
         assert act.shape == (2, 4, 2) and torch.isfinite(act).all()
 
 
+def test_model_train_saves_progress_boards_models(mods, tmp_path):
+    """model_train(save_progress, save_boards) (:370-384): the models, one
+    progress row per (epoch, game) and game 0's board after every tick it was
+    live, each board the rasterised engine state; models load back."""
+    import numpy as np
+    from skillshot_learning_amd.game import rasterize_board
+    learner, _ = mods
+    L = learner.SkillshotLearner(n_envs=1, seed=4, tick_limit=40)  # one game, as the reference plays
+    L.save_location = str(tmp_path / "training_models")
+    prog = L.model_train(epochs=2, save_progress=True, save_boards=True)
+    df = L.load_training_progress()
+    assert df.shape[0] == 2
+    assert df["epoch_ticks"].tolist() == [int(x) for t in prog["epoch_ticks"] for x in t]
+    boards = L.load_training_boards()
+    assert len(boards) == 2
+    for e in range(2):
+        assert boards[e].shape == (int(prog["epoch_ticks"][e][0]), 250, 250)
+    st = L.game_environment.state_dict()  # the final board of epoch 1 is the game's state now
+    pos, qpos, rot = st["pos"][0], st["qpos"][0], st["rot"][0]
+    flags = int(np.uint32(st["misc"][0, 1]))
+    want = rasterize_board(np.zeros((250, 250), dtype=np.int64), [pos[:2], pos[2:]], rot, [qpos[:2], qpos[2:]],
+                           [flags & 0xFF, (flags >> 8) & 0xFF])
+    assert np.array_equal(boards[1][-1], want)
+    w = [p.detach().clone() for p in L.model_actor.parameters()]
+    with torch.no_grad():
+        for p in L.model_actor.parameters():
+            p.add_(1.0)
+    assert L.load_actor_critic_models()
+    assert all(torch.equal(p, q) for p, q in zip(L.model_actor.parameters(), w))
+
+
 def test_learner_reference_epochs_full_reward(mods):
     """model_train with the alternative reward functions (:324-326)."""
     learner, _ = mods
