@@ -184,7 +184,7 @@ __global__ void __launch_bounds__(threads_for<NOISE>()) k_actor_fwd(const float*
         const int hid = 32 * c + (i & 3) + 8 * (i >> 2) + 4 * h;
         const float b = sB[hid];
         float y = acc[i] + b;
-        if (NOISE) y += sd * __builtin_sqrtf(fmaxf(var[i] + b * b, 0.f)) * z[i];
+        if (NOISE) y += sd * __builtin_amdgcn_sqrtf(fmaxf(var[i] + b * b, 0.f)) * z[i];
         y = fmaxf(y, 0.f);
         acc[i] = y;
         if (DBG && valid) dbg[row * kDbgCols + hid] = y;
@@ -222,7 +222,7 @@ __global__ void __launch_bounds__(threads_for<NOISE>()) k_actor_fwd(const float*
         const int hid = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
         const float b = sB[kH1 + hid];
         float y = acc[i] + b;
-        if (NOISE) y += sd * __builtin_sqrtf(fmaxf(var[i] + b * b, 0.f)) * z[i];
+        if (NOISE) y += sd * __builtin_amdgcn_sqrtf(fmaxf(var[i] + b * b, 0.f)) * z[i];
         y = fmaxf(y, 0.f);
         if (DBG && valid) {
           dbg[row * kDbgCols + kH1 + hid] = y;
@@ -256,7 +256,7 @@ __global__ void __launch_bounds__(threads_for<NOISE>()) k_actor_fwd(const float*
       for (int i = 0; i < 2; ++i) {
         const float b = sB[kH1 + kH2 + i];
         float y = mm[i] + b;
-        if (NOISE) y += sd * __builtin_sqrtf(fmaxf(qq[i] + b * b, 0.f)) * z[i];
+        if (NOISE) y += sd * __builtin_amdgcn_sqrtf(fmaxf(qq[i] + b * b, 0.f)) * z[i];
         if (DBG) dbg[row * kDbgCols + kH1 + kH2 + i] = y;
         o[i] = tanhf(y);
       }
@@ -342,7 +342,7 @@ __global__ void __launch_bounds__(kWgThreads) k_actor_fwd_wg(const float* __rest
         const int hid = 32 * c + (i & 3) + 8 * (i >> 2) + 4 * h;
         const float b = sB[hid];
         float y = acc[i] + b;
-        if (NOISE) y += sd * __builtin_sqrtf(fmaxf(var[i] + b * b, 0.f)) * z[i];
+        if (NOISE) y += sd * __builtin_amdgcn_sqrtf(fmaxf(var[i] + b * b, 0.f)) * z[i];
         acc[i] = fmaxf(y, 0.f);
       }
 #pragma unroll
@@ -373,7 +373,7 @@ __global__ void __launch_bounds__(kWgThreads) k_actor_fwd_wg(const float* __rest
         const int hid = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
         const float b = sB[kH1 + hid];
         float y = acc[i] + b;
-        if (NOISE) y += sd * __builtin_sqrtf(fmaxf(var[i] + b * b, 0.f)) * z[i];
+        if (NOISE) y += sd * __builtin_amdgcn_sqrtf(fmaxf(var[i] + b * b, 0.f)) * z[i];
         y = fmaxf(y, 0.f);
         m0 += sW3[hid] * y;
         m1 += sW3[kH2 + hid] * y;
@@ -407,7 +407,7 @@ __global__ void __launch_bounds__(kWgThreads) k_actor_fwd_wg(const float* __rest
       for (int i = 0; i < 2; ++i) {
         const float b = sB[kH1 + kH2 + i];
         float y = mm[i] + b;
-        if (NOISE) y += sd * __builtin_sqrtf(fmaxf(qq[i] + b * b, 0.f)) * z[i];
+        if (NOISE) y += sd * __builtin_amdgcn_sqrtf(fmaxf(qq[i] + b * b, 0.f)) * z[i];
         o2[i] = tanhf(y);
       }
       *(float2*)(out + row * kOut) = make_float2(o2[0], o2[1]);

@@ -71,25 +71,28 @@ __device__ __forceinline__ uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
   return c;
 }
 
-// 16 standard normals for (row, stream, lane half h): Box-Muller on 4 Philox
-// draws.  The two lane halves hold different hidden units of the same row,
-// so h is part of the counter (independent noise per unit).
+// 16 standard normals for (row, stream, lane half h): Box-Muller on 2 Philox
+// draws, each 32-bit word split into a 16-bit radius uniform and a 16-bit
+// angle uniform (one word per normal pair; radius truncated at 4.86 sigma,
+// P = 1.2e-6).  The two lane halves hold different hidden units of the same
+// row, so h is part of the counter (independent noise per unit).  The RNG
+// was half of the noisy actor's VALU instructions (PMC, profiles/r01t_*).
 __device__ __forceinline__ void normals16(uint64_t seed, uint64_t call, uint32_t row, uint32_t stream, int h,
                                           float z[16]) {
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    uint4 u = philox(make_uint4(row, (stream * 2 + (uint32_t)h) * 4 + q, (uint32_t)call, (uint32_t)(call >> 32)),
+  for (int q = 0; q < 2; ++q) {
+    uint4 u = philox(make_uint4(row, (stream * 2 + (uint32_t)h) * 2 + q, (uint32_t)call, (uint32_t)(call >> 32)),
                      (uint32_t)seed, (uint32_t)(seed >> 32));
     uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      float u1 = ((float)(w[2 * p] >> 8) + 0.5f) * 0x1p-24f;  // (0, 1)
-      float u2 = (float)(w[2 * p + 1] >> 8) * 0x1p-24f;       // [0, 1)
-      float rad = __builtin_sqrtf(-2.0f * __logf(u1));
+    for (int p = 0; p < 4; ++p) {
+      float u1 = ((float)(w[p] & 0xFFFFu) + 0.5f) * 0x1p-16f;  // (0, 1)
+      float u2 = (float)(w[p] >> 16) * 0x1p-16f;               // [0, 1)
+      float rad = __builtin_amdgcn_sqrtf(-2.0f * __logf(u1));  // v_sqrt_f32 (1 ulp): noise scale
       float sn, cs;
       __sincosf(6.283185307179586f * u2, &sn, &cs);
-      z[4 * q + 2 * p] = rad * cs;
-      z[4 * q + 2 * p + 1] = rad * sn;
+      z[8 * q + 2 * p] = rad * cs;
+      z[8 * q + 2 * p + 1] = rad * sn;
     }
   }
 }
