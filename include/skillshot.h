@@ -233,7 +233,9 @@ int sk_actor_forward(const void* packed, const float* obs, float* actions, int64
  * the counter between calls (stream-ordered). */
 int sk_actor_forward_dev(const void* packed, const float* obs, float* actions, int64_t rows, float noise_sd,
                          uint64_t seed, const uint64_t* call_counter, void* stream);
-/* sk_actor_forward_dev that advances the counter itself: call_counter is
+/* sk_actor_forward_dev that advances the counter itself (the fresh per-tick
+ * weight noise of model_act_param_noise, SkillshotLearner.py:245-281, drawn
+ * by every launch of a captured tick): call_counter is
  * uint64[2] = {call number, 0}; a noisy launch draws with call number
  * call_counter[0] + 1 and stores that number back into call_counter[0] when
  * its last workgroup finishes (call_counter[1] is its arrival slot: keep it
@@ -350,7 +352,9 @@ int sk_adam_flat(const float* partials, int32_t n_partials, int32_t n_params, co
                  const float* step_counter, float lr, float beta1, float beta2, float eps, float* target, float tau,
                  float* stat_acc, float stat_scale, float* stat_out, int64_t* counter, void* stream);
 /* sk_adam_flat that also writes the packed copies of every parameter it
- * produces, so no separate pack launch follows a step: param_gpack (the
+ * produces (the optimiser steps of SkillshotLearner.py:406-417, :434 and the
+ * north_star's soft target update), so no separate pack launch follows a
+ * step: param_gpack (the
  * stepped net's sk_grad_pack layout), target_gpack (its soft-updated target's,
  * needs target) and, for the actor (ld2 256, n_out 2), actor_fwd_pack (the
  * sk_actor_pack layout).  Each pointer is nullable; the buffers must hold a
