@@ -76,7 +76,18 @@ def cpu_baseline(n_envs, seconds, tick_limit, seed, cores):
              for c in range(cores)]
     outs = [json.loads(p.communicate()[0].strip().splitlines()[-1]) for p in procs]
     rate = sum(o["env_steps_per_s"] for o in outs)
-    return dict(value=rate, unit="env-steps/s", cores=cores, kind="port",
+    # the pure-Python restatement on config 1 (one game, one core), and the
+    # reference-equivalent rate through the ratio measured where the
+    # reference is importable (tools/ref_ratio.py -> profiles/ref_vs_pyoracle.json)
+    py = cpu_bench.run_python(min(5.0, seconds / 2), seed=seed, tick_limit=tick_limit)["env_steps_per_s"]
+    ratio_path = os.path.join(root, "profiles", "ref_vs_pyoracle.json")
+    ratio = json.load(open(ratio_path)) if os.path.exists(ratio_path) else None
+    python_leg = dict(pyoracle_env_steps_per_s_1core=py, procedure="SURVEY 8(d) config 1 (game_tick + actions)")
+    if ratio:
+        python_leg.update(ratio_pyoracle_over_reference=ratio["ratio_pyoracle_over_reference"],
+                          reference_equivalent_env_steps_per_s_1core=py / ratio["ratio_pyoracle_over_reference"],
+                          ratio_source="profiles/ref_vs_pyoracle.json")
+    return dict(value=rate, unit="env-steps/s", cores=cores, kind="port", python_restatement=python_leg,
                 sample=f"C oracle (oracle/skillshot_oracle.c, restatement of the reference step): {cores} processes "
                        f"x {per} games for {seconds:.0f} s each ({sum(o['ticks'] for o in outs) // cores} ticks "
                        f"per process on average); one core on all {n_envs} games: "
