@@ -61,10 +61,19 @@ static int fail(int code, const std::string& msg) {
   } while (0)
 
 static constexpr int kBlock = 256;
+// Step kernels (k_step*, k_rollout_random) launch one-wave workgroups: 64 vs
+// 256 lanes measured 4.66 vs 4.74 us (65,536 games) and 9.17 vs 9.48 us
+// (262,144) per k_step launch, never slower beyond noise
+// (profiles/r01v_step_block_ab.jsonl; -DSK_STEP_BLOCK=… rebuilds for A/B).
+#ifndef SK_STEP_BLOCK
+#define SK_STEP_BLOCK 64
+#endif
+static constexpr int kStepBlock = SK_STEP_BLOCK;
 static constexpr int64_t kFastStepMinEnvs = 196608;
 static constexpr size_t kAuxBytes = 256 + SK_COUNTER_SLOTS * sizeof(sk_counters);
 
 static inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+static inline unsigned step_grid(int64_t n) { return (unsigned)((n + kStepBlock - 1) / kStepBlock); }
 
 // ------------------------------------------------------------------ counters
 // Episode counters live in SK_COUNTER_SLOTS slots of 32 B; the host sums
@@ -73,7 +82,7 @@ static inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) 
 // index: no single hot line (a one-line counter serialises every wave's
 // atomics at the memory side and stalled 1M-env launches).
 __device__ __forceinline__ sk_counters* ctr_slot(sk_counters* base) {
-  unsigned wave = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  unsigned wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   return base + (wave & (SK_COUNTER_SLOTS - 1));
 }
 
@@ -148,8 +157,8 @@ struct StepArgs {
   sk_counters* ctr;
 };
 
-__global__ void __launch_bounds__(kBlock) k_step(StepArgs a, Cfg c) {
-  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+__global__ void __launch_bounds__(kStepBlock) k_step(StepArgs a, Cfg c) {
+  int64_t i = (int64_t)blockIdx.x * kStepBlock + threadIdx.x;
   const uint64_t step = step_read(a.step);
   step_advance(a.step, step, 1);
   bool in = i < a.n;
@@ -212,8 +221,8 @@ __global__ void __launch_bounds__(kBlock) k_step(StepArgs a, Cfg c) {
 // games), slower than k_step at one wave per SIMD (65,536 games: 5.3 vs 4.7
 // us), where the per-wave dependency chain, not issue, sets the time
 // (profiles/r01g_step_variants.jsonl).
-__global__ void __launch_bounds__(kBlock) k_step_fast(StepArgs a, Cfg c) {
-  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+__global__ void __launch_bounds__(kStepBlock) k_step_fast(StepArgs a, Cfg c) {
+  int64_t i = (int64_t)blockIdx.x * kStepBlock + threadIdx.x;
   bool in = i < a.n;
   // every load issued back to back before anything else touches memory,
   // then the tick works through the data in arrival order
@@ -280,8 +289,8 @@ __global__ void __launch_bounds__(kBlock) k_step_fast(StepArgs a, Cfg c) {
 // other player), then the pair swaps positions/projectiles with one
 // __shfl_xor(.,1) each for the collision test, which both lanes evaluate
 // identically.  Twice the waves of k_step, half the dependent chain per lane.
-__global__ void __launch_bounds__(kBlock) k_step_split(StepArgs a, Cfg c) {
-  const int64_t gt = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+__global__ void __launch_bounds__(kStepBlock) k_step_split(StepArgs a, Cfg c) {
+  const int64_t gt = (int64_t)blockIdx.x * kStepBlock + threadIdx.x;
   const int64_t i = gt >> 1;
   const int p = (int)(gt & 1);
   const uint64_t step = step_read(a.step);
@@ -404,8 +413,8 @@ struct RolloutArgs {
   sk_counters* ctr;
 };
 
-__global__ void __launch_bounds__(kBlock) k_rollout_random(RolloutArgs a, Cfg c) {
-  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+__global__ void __launch_bounds__(kStepBlock) k_rollout_random(RolloutArgs a, Cfg c) {
+  int64_t i = (int64_t)blockIdx.x * kStepBlock + threadIdx.x;
   bool in = i < a.n;
   const uint64_t step0 = step_read(a.step);
   step_advance(a.step, step0, (uint64_t)a.n_ticks);
@@ -912,14 +921,18 @@ int sk_env_step(sk_env* e, const float* actions, float* obs, float* reward, int3
   a.step = StepRef{e->d_step, e->parity};
   a.ctr = e->d_counters;
   // auto: k_step_fast once several waves share a SIMD (>= 2 per SIMD on 256
-  // CUs), k_step below (profiles/r01g_step_variants.jsonl)
-  const int variant = e->step_variant >= 0 ? e->step_variant : (e->n >= kFastStepMinEnvs ? 2 : 0);
+  // CUs); below that k_step, or k_step_split when observations are written
+  // (65,536 games with obs: 9.8 vs 10.5 us; profiles/r01g_step_variants.jsonl,
+  // profiles/r01v_step_block_ab.jsonl)
+  const int variant = e->step_variant >= 0 ? e->step_variant
+                      : e->n >= kFastStepMinEnvs ? 2
+                      : (obs || reward || obs_reset) ? 1 : 0;
   if (variant == 1)
-    k_step_split<<<grid_for(2 * (int64_t)e->n), kBlock, 0, (hipStream_t)stream>>>(a, e->dcfg);
+    k_step_split<<<step_grid(2 * (int64_t)e->n), kStepBlock, 0, (hipStream_t)stream>>>(a, e->dcfg);
   else if (variant == 2)
-    k_step_fast<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(a, e->dcfg);
+    k_step_fast<<<step_grid(e->n), kStepBlock, 0, (hipStream_t)stream>>>(a, e->dcfg);
   else
-    k_step<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(a, e->dcfg);
+    k_step<<<step_grid(e->n), kStepBlock, 0, (hipStream_t)stream>>>(a, e->dcfg);
   SK_LAUNCH_CHECK();
   e->parity ^= 1;
   return SK_OK;
@@ -947,7 +960,7 @@ int sk_env_rollout_random(sk_env* e, int32_t n_ticks, int32_t tick_limit, void* 
   a.env_offset = e->env_offset;
   a.step = StepRef{e->d_step, e->parity};
   a.ctr = e->d_counters;
-  k_rollout_random<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(a, e->dcfg);
+  k_rollout_random<<<step_grid(e->n), kStepBlock, 0, (hipStream_t)stream>>>(a, e->dcfg);
   SK_LAUNCH_CHECK();
   e->parity ^= 1;
   return SK_OK;
