@@ -363,7 +363,7 @@ def main():
                            "reported beside, not as, the headline"}
 
     cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline:  # N=1 only (the CPU baseline is a per-box figure)
         cpu = cpu_baseline(n, args.cpu_seconds, args.tick_limit, args.seed,
                            max(1, min(args.cpu_cores, os.cpu_count() or 1)))
 

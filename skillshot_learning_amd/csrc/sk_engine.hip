@@ -137,6 +137,19 @@ __device__ __forceinline__ void step_advance(const StepRef& s, uint64_t base, ui
   if (blockIdx.x == 0 && threadIdx.x == 0) s.slots[1 - s.parity] = base + inc;
 }
 
+// ------------------------------------------------------------------ step trace
+// Measurement build only (-DSK_TRACE_STEP; tools/trace_step.py): lane 0 of
+// every k_step wave records s_memrealtime (100 MHz) at entry, once the loads
+// have landed (a full s_waitcnt: perturbs the load/sincos overlap slightly),
+// after the tick, and once its stores have completed, plus HW_ID / XCC_ID,
+// into slot (step & 15) of sk_step_trace: [16][waves][8] u64.
+#ifdef SK_TRACE_STEP
+__device__ unsigned long long* sk_step_trace;
+#define SK_TS(var) const unsigned long long var = __builtin_amdgcn_s_memrealtime()
+#else
+#define SK_TS(var)
+#endif
+
 // ------------------------------------------------------------------ kernels
 struct StepArgs {
   View v;
@@ -159,11 +172,15 @@ struct StepArgs {
 
 __global__ void __launch_bounds__(kStepBlock) k_step(StepArgs a, Cfg c) {
   int64_t i = (int64_t)blockIdx.x * kStepBlock + threadIdx.x;
+  SK_TS(ts0);
   const uint64_t step = step_read(a.step);
   step_advance(a.step, step, 1);
   bool in = i < a.n;
   bool d = false;
   Env e;
+#ifdef SK_TRACE_STEP
+  unsigned long long ts1 = 0, ts2 = 0;
+#endif
   if (in) {
     // state first, actions last (in issue order, so the waits for the state
     // do not wait for the actions): the players' sincos of the old rotations
@@ -173,10 +190,20 @@ __global__ void __launch_bounds__(kStepBlock) k_step(StepArgs a, Cfg c) {
     const float2 a0 = a.actions[i];
     const float2 a1 = a.actions[a.n + i];
     __builtin_amdgcn_sched_barrier(0);
+#ifdef SK_TRACE_STEP
+    __builtin_amdgcn_s_waitcnt(0);
+    ts1 = __builtin_amdgcn_s_memrealtime();
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     bool k0, k1;
     const sktrig::SinCos m0 = sktrig::sincos_bf(e.rot[0], &k0);
     const sktrig::SinCos m1 = sktrig::sincos_bf(e.rot[1], &k1);
     tick_env_m(c, e, m0, m1, k0 & k1, (double)a0.x, (double)a0.y, (double)a1.x, (double)a1.y);
+#ifdef SK_TRACE_STEP
+    __builtin_amdgcn_sched_barrier(0);
+    ts2 = __builtin_amdgcn_s_memrealtime();
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     if (a.obs || a.reward) {
       float o0[12], o1[12];
       double pd0, pd1;
@@ -210,7 +237,25 @@ __global__ void __launch_bounds__(kStepBlock) k_step(StepArgs a, Cfg c) {
     if (amb) fix_future_flags(c, e, amb, a.obs_reset, a.n, i);
   }
   store_env(a.v, i, e);
+#ifdef SK_TRACE_STEP
+  __builtin_amdgcn_s_waitcnt(0);
+  const unsigned long long ts3 = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63) == 0 && sk_step_trace) {
+    const unsigned waves = gridDim.x * (blockDim.x >> 6);
+    const unsigned w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    unsigned long long* t = sk_step_trace + ((step & 15) * waves + w) * 8;
+    t[0] = ts0; t[1] = ts1; t[2] = ts2; t[3] = ts3;
+    t[4] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+    t[5] = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // XCC_ID
+  }
+#endif
 }
+
+#ifdef SK_TRACE_STEP
+extern "C" int skdiag_set_step_trace(void* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(sk_step_trace), &buf, sizeof(buf)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 // Fused step, fp32-trig variant (SK_STEP_VARIANT=2; the default from 196,608
 // games): the same tick through tick_env_fast (exact by construction: fp32
