@@ -103,6 +103,12 @@ typedef int skv2i __attribute__((ext_vector_type(2)));
 typedef double skv2d __attribute__((ext_vector_type(2)));
 typedef float skv2f __attribute__((ext_vector_type(2)));
 
+#ifdef SK_STATE_NT
+#define SK_STATE_LD "nt"
+#else
+#define SK_STATE_LD ""
+#endif
+
 struct StepLoads {  // native vector types: inline asm cannot bind HIP's struct vectors
   skv2d r, qr;
   skv4i p, q, ca;
@@ -117,14 +123,14 @@ __device__ __forceinline__ void issue_step_loads(const View& v, const float2* ac
   skv2i m;
   skv2f a0, a1;
   asm volatile(
-      "global_load_dwordx4 %0, %8, off\n\t"
-      "global_load_dwordx4 %1, %9, off\n\t"
-      "global_load_dwordx4 %2, %10, off\n\t"
-      "global_load_dwordx2 %3, %11, off\n\t"
-      "global_load_dwordx4 %4, %12, off\n\t"
-      "global_load_dwordx4 %5, %13, off\n\t"
-      "global_load_dwordx2 %6, %14, off\n\t"
-      "global_load_dwordx2 %7, %15, off"
+      "global_load_dwordx4 %0, %8, off " SK_STATE_LD "\n\t"
+      "global_load_dwordx4 %1, %9, off " SK_STATE_LD "\n\t"
+      "global_load_dwordx4 %2, %10, off " SK_STATE_LD "\n\t"
+      "global_load_dwordx2 %3, %11, off " SK_STATE_LD "\n\t"
+      "global_load_dwordx4 %4, %12, off " SK_STATE_LD "\n\t"
+      "global_load_dwordx4 %5, %13, off " SK_STATE_LD "\n\t"
+      "global_load_dwordx2 %6, %14, off nt\n\t"
+      "global_load_dwordx2 %7, %15, off nt"
       : "=&v"(r), "=&v"(qr), "=&v"(ca), "=&v"(m), "=&v"(p), "=&v"(q), "=&v"(a0), "=&v"(a1)
       : "v"(v.rot + i), "v"(v.qrot + i), "v"(v.qcdage + i), "v"(v.misc + i), "v"(v.pos + i), "v"(v.qpos + i),
         "v"(act + i), "v"(act + n + i)
@@ -160,14 +166,27 @@ __device__ __forceinline__ EnvRaw step_loads_env(const StepLoads& L) {
 }
 
 __device__ __forceinline__ void store_env(const View& v, int64_t i, const Env& e) {
+  unsigned f = (unsigned)(e.qvalid[0] & 0xff) | ((unsigned)(e.qvalid[1] & 0xff) << 8) |
+               ((unsigned)(e.live & 0xff) << 16) | ((unsigned)(e.winner & 0xff) << 24);
+#ifdef SK_STATE_NT
+  // A/B build: streaming state stores (for batches far past the Infinity Cache)
+  typedef int v4i __attribute__((ext_vector_type(4)));
+  typedef double v2d __attribute__((ext_vector_type(2)));
+  typedef int v2i __attribute__((ext_vector_type(2)));
+  __builtin_nontemporal_store((v4i){e.px[0], e.py[0], e.px[1], e.py[1]}, (v4i*)(v.pos + i));
+  __builtin_nontemporal_store((v2d){e.rot[0], e.rot[1]}, (v2d*)(v.rot + i));
+  __builtin_nontemporal_store((v4i){e.qx[0], e.qy[0], e.qx[1], e.qy[1]}, (v4i*)(v.qpos + i));
+  __builtin_nontemporal_store((v2d){e.qrot[0], e.qrot[1]}, (v2d*)(v.qrot + i));
+  __builtin_nontemporal_store((v4i){e.qcd[0], e.qage[0], e.qcd[1], e.qage[1]}, (v4i*)(v.qcdage + i));
+  __builtin_nontemporal_store((v2i){e.ticks, (int)f}, (v2i*)(v.misc + i));
+#else
   v.pos[i] = make_int4(e.px[0], e.py[0], e.px[1], e.py[1]);
   v.rot[i] = make_double2(e.rot[0], e.rot[1]);
   v.qpos[i] = make_int4(e.qx[0], e.qy[0], e.qx[1], e.qy[1]);
   v.qrot[i] = make_double2(e.qrot[0], e.qrot[1]);
   v.qcdage[i] = make_int4(e.qcd[0], e.qage[0], e.qcd[1], e.qage[1]);
-  unsigned f = (unsigned)(e.qvalid[0] & 0xff) | ((unsigned)(e.qvalid[1] & 0xff) << 8) |
-               ((unsigned)(e.live & 0xff) << 16) | ((unsigned)(e.winner & 0xff) << 24);
   v.misc[i] = make_int2(e.ticks, (int)f);
+#endif
 }
 
 // ---------------------------------------------------------------- Philox4x32-10
