@@ -70,6 +70,7 @@ static constexpr int kBlock = 256;
 #endif
 static constexpr int kStepBlock = SK_STEP_BLOCK;
 static constexpr int64_t kFastStepMinEnvs = 196608;
+static constexpr int64_t kFastStepMaxEnvs = 786432;
 static constexpr size_t kAuxBytes = 256 + SK_COUNTER_SLOTS * sizeof(sk_counters);
 
 static inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
@@ -190,6 +191,7 @@ __global__ void __launch_bounds__(kStepBlock) k_step(StepArgs a, Cfg c) {
   bool in = i < a.n;
   bool d = false;
   Env e;
+  double q_old0 = 0.0, q_old1 = 0.0;  // stored projectile rotations (store_env_q)
 #ifdef SK_TRACE_STEP
   unsigned long long ts1 = 0, ts2 = 0;
 #endif
@@ -198,6 +200,8 @@ __global__ void __launch_bounds__(kStepBlock) k_step(StepArgs a, Cfg c) {
     // do not wait for the actions): the players' sincos of the old rotations
     // then run while the actions arrive
     load_env(a.v, i, e);
+    q_old0 = e.qrot[0];
+    q_old1 = e.qrot[1];
     __builtin_amdgcn_sched_barrier(0);
     const float2 a0 = load_action(a.actions + i);
     const float2 a1 = load_action(a.actions + a.n + i);
@@ -253,7 +257,7 @@ __global__ void __launch_bounds__(kStepBlock) k_step(StepArgs a, Cfg c) {
     store_obs(a.obs_reset, a.n, 1, i, o1);
     if (amb) fix_future_flags(c, e, amb, a.obs_reset, a.n, i);
   }
-  store_env(a.v, i, e);
+  store_env_q(a.v, i, e, q_old0, q_old1);
 #ifdef SK_TRACE_STEP
   __builtin_amdgcn_s_waitcnt(0);
   const unsigned long long ts3 = __builtin_amdgcn_s_memrealtime();
@@ -346,7 +350,7 @@ __global__ void __launch_bounds__(kStepBlock) k_step_fast(StepArgs a, Cfg c) {
     store_obs(a.obs_reset, a.n, 1, i, o1);
     if (amb) fix_future_flags(c, e, amb, a.obs_reset, a.n, i);
   }
-  store_env(a.v, i, e);
+  store_env_q(a.v, i, e, L.qr.x, L.qr.y);
 }
 
 // Player-split fused step: lanes (2i, 2i+1) own players 1 and 2 of env i.
@@ -988,11 +992,14 @@ int sk_env_step(sk_env* e, const float* actions, float* obs, float* reward, int3
   a.step = StepRef{e->d_step, e->parity};
   a.ctr = e->d_counters;
   // auto: k_step_fast once several waves share a SIMD (>= 2 per SIMD on 256
-  // CUs); below that k_step, or k_step_split when observations are written
-  // (65,536 games with obs: 9.8 vs 10.5 us; profiles/r01g_step_variants.jsonl,
-  // profiles/r01v_step_block_ab.jsonl)
+  // CUs) up to ~3 per SIMD (262,144 games: 8.3 vs 9.1 us); k_step from
+  // 1 M games, where the step is HBM-bound (1 M: 30.1 vs 31.6 us, 4 M: 137
+  // vs 151 us; profiles/r01x_sweep_qskip.jsonl); below 196,608 k_step, or
+  // k_step_split when observations are written (65,536 games with obs: 9.8
+  // vs 10.5 us; profiles/r01g_step_variants.jsonl, r01v_step_block_ab.jsonl)
   const int variant = e->step_variant >= 0 ? e->step_variant
-                      : e->n >= kFastStepMinEnvs ? 2
+                      : (e->n >= kFastStepMinEnvs && e->n < kFastStepMaxEnvs) ? 2
+                      : e->n >= kFastStepMaxEnvs ? 0
                       : (obs || reward || obs_reset) ? 1 : 0;
   if (variant == 1)
     k_step_split<<<step_grid(2 * (int64_t)e->n), kStepBlock, 0, (hipStream_t)stream>>>(a, e->dcfg);
