@@ -6,26 +6,35 @@
         --master-port P bench.py --gpus N --steps K --warmup W
 
 Workload (BASELINE.json metric "env-steps/sec (whole node) at 65536 self-play
-envs"): every GPU steps 65,536 games (weak scaling:
-envs shard by global id, no data-path collective) with the random policy.
-One bench step = one k_step launch over all of a GPU's games: both players'
-do_actions (SkillshotLearner.py:206-213) + game_tick (SkillshotGame.py:115-122)
-+ done + random auto-reset.  Actions are Philox uniform(-1,1) float32
-pre-generated into HBM (K4, not timed), a distinct 1 MiB slab per tick, read
-from a ring larger than the 256 MiB Infinity Cache.  The K timed steps are
-replayed from hipGraphs of `--graph-len` captured launches (the engine's RNG
-step counter lives on device, so replays stay correctly keyed).
+envs; 1/2/4/8 GPU scaling", SURVEY.md §8(d) config 2 at the metric's size and
+§8(e)): 65,536 games IN TOTAL, split over the N ranks by contiguous global id
+(65,536 / 32,768 / 16,384 / 8,192 per GPU at N = 1 / 2 / 4 / 8: "scaling":
+"strong", no data-path collective), random policy.  One bench step = one
+k_step launch over all of a GPU's games: both players' do_actions
+(SkillshotLearner.py:206-213) + game_tick (SkillshotGame.py:115-122) + done
++ random auto-reset.  Actions are Philox uniform(-1,1) float32 pre-generated
+into HBM (K4, not timed), a distinct 1 MiB slab per tick, read from a ring
+larger than the 256 MiB Infinity Cache.  Whatever K and W are, the launches
+are replayed from hipGraphs (TickGraphs below: a chunk graph of --graph-len
+launches replayed K // len times plus one remainder graph), so the timed
+region never holds eager ctypes launches.  Weak scaling (65,536 games per GPU)
+is reported beside it for N > 1.
 
 Roofline: algorithmic bytes per env-step = 193 B (state 88 B read + 88 B
 written, actions 16 B, done 1 B: SURVEY.md §8(d)); average launch duration =
-HIP-event span of the timed region on the launch stream / K.  cpu_baseline: the C oracle (a port of the
-reference step) on one host core over a bounded sample of the same workload.
+HIP-event span of the timed region on the launch stream / K.  `traffic` comes
+from the committed PMC pass (profiles/traffic_k_step.json, rocprofv3 --pmc
+FETCH_SIZE / WRITE_SIZE), not from this run.  cpu_baseline: the
+C oracle (a port of the reference step) on the box's host cores over a
+bounded sample of the same workload.
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
 import time
+import traceback
 
 import torch
 import torch.distributed as dist
@@ -35,6 +44,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "env-steps/sec (whole node) at 65536 self-play envs; 1/2/4/8 GPU scaling"
 BYTES_PER_ENV_STEP = 193  # SURVEY.md §8(d) step-only contract
+BYTES_FULL_CONTRACT = 297  # + obs f32[2][12] + reward f32[2] (configs 3-5)
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
 
@@ -43,20 +53,92 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=4000)
     p.add_argument("--warmup", type=int, default=400)
-    p.add_argument("--envs", type=int, default=65536, help="games per GPU")
+    p.add_argument("--envs", type=int, default=65536, help="games in total over all GPUs (the metric's 65,536)")
     p.add_argument("--tick-limit", type=int, default=2000)
     p.add_argument("--seed", type=int, default=0)
-    p.add_argument("--graph-len", type=int, default=400, help="launches per captured hipGraph")
+    p.add_argument("--graph-len", type=int, default=400, help="launches per captured chunk hipGraph (even)")
     p.add_argument("--action-ring", type=int, default=400, help="distinct per-tick action slabs in HBM")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--cpu-cores", type=int, default=16, help="host cores for the CPU baseline (the box's share)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-rollout", action="store_true")
     p.add_argument("--no-large", action="store_true", help="skip the 4 M-game HBM-bound secondary measurement")
-    p.add_argument("--no-strong", action="store_true", help="skip the fixed-65,536-total secondary measurement")
-    p.add_argument("--no-learner", action="store_true", help="skip the DDPG-in-the-loop secondary measurement (N=1)")
+    p.add_argument("--no-weak", action="store_true", help="skip the 65,536-games-per-GPU weak-scaling leg (N>1)")
+    p.add_argument("--no-full", action="store_true", help="skip the full-contract (obs + reward) tick leg")
+    p.add_argument("--no-learner", action="store_true", help="skip the DDPG-in-the-loop legs")
+    p.add_argument("--learner-ticks", type=int, default=200)
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_k_step.json"))
     return p.parse_args()
+
+
+class TickGraphs:
+    """`k` launches of `launch(t)` on `stream` as hipGraph replays for any k.
+
+    The engine's RNG step counter lives on device in two ping-pong slots and a
+    captured launch bakes in the slot it reads.  Every graph is captured right
+    after `sync_step_counter` (both slots equal, host parity 0), and every
+    `run` starts with one: the chunk graph (even length) leaves the newest
+    value in slot 0, where the remainder graph (captured at the same parity)
+    reads it.  So any mix of run() sizes keeps the reference RNG keys."""
+
+    def __init__(self, env, stream, launch, chunk):
+        self.env, self.stream, self.launch = env, stream, launch
+        self.chunk = max(2, chunk - chunk % 2)
+        self.graphs = {}
+
+    def _graph(self, n):
+        g = self.graphs.get(n)
+        if g is None:
+            sp = ctypes.c_void_p(self.stream.cuda_stream)
+            with torch.cuda.stream(self.stream):
+                self.env.sync_step_counter(sp)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=self.stream):
+                for t in range(n):
+                    self.launch(t)
+            _upload(g, self.stream)
+            self.stream.synchronize()
+            self.graphs[n] = g
+        return g
+
+    def prepare(self, k):
+        """capture what run(k) replays (outside any timed region)"""
+        if k >= self.chunk:
+            self._graph(self.chunk)
+        if k % self.chunk:
+            self._graph(k % self.chunk)
+
+    def sync(self):
+        with torch.cuda.stream(self.stream):
+            self.env.sync_step_counter(ctypes.c_void_p(self.stream.cuda_stream))
+
+    def replay(self, k):
+        """the k launches (call sync() first, outside the timed region)"""
+        with torch.cuda.stream(self.stream):
+            for _ in range(k // self.chunk):
+                self._graph(self.chunk).replay()
+            if k % self.chunk:
+                self._graph(k % self.chunk).replay()
+
+
+_HIP = None
+
+
+def _upload(graph, stream):
+    """hipGraphUpload the instantiated graph now, so that its first replay
+    (possibly the timed one) does not pay for the upload"""
+    global _HIP
+    try:
+        if _HIP is None:
+            path = next(ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln)
+            _HIP = ctypes.CDLL(path)  # the runtime torch already loaded
+            _HIP.hipGraphUpload.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+            _HIP.hipGraphUpload.restype = ctypes.c_int
+        ex = graph.raw_cuda_graph_exec()
+        if ex:
+            _HIP.hipGraphUpload(ctypes.c_void_p(ex), ctypes.c_void_p(stream.cuda_stream))
+    except Exception:  # noqa: BLE001 (an optimisation only)
+        pass
 
 
 def cpu_baseline(n_envs, seconds, tick_limit, seed, cores):
@@ -66,13 +148,12 @@ def cpu_baseline(n_envs, seconds, tick_limit, seed, cores):
     (oracle/cpu_bench.py), each bounded to about `seconds` of CPU work; the
     one-core rate is measured first on the full batch."""
     import subprocess
-    root = os.path.dirname(os.path.abspath(__file__))
     from oracle import cpu_bench
     one = cpu_bench.run(n_envs, seconds / 2, seed=seed, tick_limit=tick_limit)
     per = n_envs // cores
     procs = [subprocess.Popen([sys.executable, "-m", "oracle.cpu_bench", "--envs", str(per), "--env-offset",
                                str(c * per), "--seconds", str(seconds), "--seed", str(seed), "--tick-limit",
-                               str(tick_limit)], cwd=root, stdout=subprocess.PIPE, text=True)
+                               str(tick_limit)], cwd=ROOT, stdout=subprocess.PIPE, text=True)
              for c in range(cores)]
     outs = [json.loads(p.communicate()[0].strip().splitlines()[-1]) for p in procs]
     rate = sum(o["env_steps_per_s"] for o in outs)
@@ -80,7 +161,7 @@ def cpu_baseline(n_envs, seconds, tick_limit, seed, cores):
     # reference-equivalent rate through the ratio measured where the
     # reference is importable (tools/ref_ratio.py -> profiles/ref_vs_pyoracle.json)
     py = cpu_bench.run_python(min(5.0, seconds / 2), seed=seed, tick_limit=tick_limit)["env_steps_per_s"]
-    ratio_path = os.path.join(root, "profiles", "ref_vs_pyoracle.json")
+    ratio_path = os.path.join(ROOT, "profiles", "ref_vs_pyoracle.json")
     ratio = json.load(open(ratio_path)) if os.path.exists(ratio_path) else None
     python_leg = dict(pyoracle_env_steps_per_s_1core=py, procedure="SURVEY 8(d) config 1 (game_tick + actions)")
     if ratio:
@@ -95,87 +176,56 @@ def cpu_baseline(n_envs, seconds, tick_limit, seed, cores):
                        f"59.2k env-steps/s per core (BASELINE.md)")
 
 
-def large_batch_rate(dev, args, rank, n=1 << 22, launches=60, ring=8):
-    """k_step at n games per GPU, graph-replayed, HIP-event timed (HBM-bound
-    regime: 193 B x n per launch)."""
-    import ctypes
+def _env_and_actions(dev, n, seed, env_offset, tick_limit, ring):
     from skillshot_learning_amd import VecSkillshotGame
-    env = VecSkillshotGame(n, device=dev, seed=args.seed + 1, env_offset=rank * n, tick_limit=args.tick_limit,
+    env = VecSkillshotGame(n, device=dev, seed=seed, env_offset=env_offset, tick_limit=tick_limit,
                            random_positions=True)
     st = torch.cuda.Stream(device=dev)
     with torch.cuda.stream(st):
         env.reset(random_positions=True)
-        acts = env.gen_random_actions(ring)
-        done = torch.empty(n, dtype=torch.uint8, device=dev)
+        acts = env.gen_random_actions(ring)  # [ring, 2, n, 2] f32, 16 B/env/tick
     st.synchronize()
+    return env, st, acts
+
+
+def timed_ticks(dev, n, seed, env_offset, tick_limit, k, warmup, ring, chunk, world, obs=False):
+    """k graph-replayed fused-step launches over n games: (wall s max over
+    ranks, HIP-event ms on the launch stream, env).  obs=True writes the
+    full contract (obs f32[2][n][12], reward f32[2][n], done) every tick."""
+    env, st, acts = _env_and_actions(dev, n, seed, env_offset, tick_limit, ring)
     slab, sp = 16 * n, ctypes.c_void_p(st.cuda_stream)
+    done = torch.empty(n, dtype=torch.uint8, device=dev)
+    ob = torch.empty((2, n, 12), dtype=torch.float32, device=dev) if obs else None
+    rw = torch.empty((2, n), dtype=torch.float32, device=dev) if obs else None
+    a0, dp = acts.data_ptr(), ctypes.c_void_p(done.data_ptr())
+    op = ctypes.c_void_p(ob.data_ptr()) if obs else None
+    rp = ctypes.c_void_p(rw.data_ptr()) if obs else None
 
     def launch(t):
-        env.step_raw(ctypes.c_void_p(acts.data_ptr() + (t % ring) * slab), ctypes.c_void_p(done.data_ptr()), stream=sp)
+        env.step_raw(ctypes.c_void_p(a0 + (t % ring) * slab), dp, obs_ptr=op, reward_ptr=rp, stream=sp)
 
-    with torch.cuda.stream(st):
-        for t in range(2):
+    with torch.cuda.stream(st):  # eager first launches load the code objects
+        for t in range(4):
             launch(t)
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, stream=st):
-        for t in range(launches):
-            launch(t)
-    with torch.cuda.stream(st):
-        g.replay()
+    st.synchronize()
+    tg = TickGraphs(env, st, launch, chunk)
+    tg.prepare(warmup)
+    tg.prepare(k)
+    tg.sync()
+    env.clear_counters()
+    tg.replay(warmup)
+    tg.sync()
     st.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    with torch.cuda.stream(st):
-        e0.record()
-        g.replay()
-        e1.record()
-    st.synchronize()
-    us = e0.elapsed_time(e1) * 1e3 / launches
-    gbs = BYTES_PER_ENV_STEP * n / (us * 1e-6) / 1e9
-    env.close()
-    del acts, done
-    return dict(envs_per_gpu=n, kernel="k_step (auto variant)", us_per_launch=us, env_steps_per_s_per_gpu=n / (us * 1e-6),
-                achieved_gbs=gbs, frac=gbs / HBM_PEAK_GBS,
-                note="state 369 MB > Infinity Cache: the HBM-bound regime; reported beside, not as, the headline")
-
-
-def strong_scaling_rate(dev, args, rank, world, total=65536, launches=2000, G=400):
-    """BASELINE config-5 reading of the metric: 65,536 games in total split
-    over the ranks (65,536 / world per GPU), same fused tick; aggregate
-    env-steps/s over max-over-ranks wall time (barriers around)."""
-    import ctypes
-    from skillshot_learning_amd import VecSkillshotGame
-    n = total // world
-    env = VecSkillshotGame(n, device=dev, seed=args.seed + 2, env_offset=rank * n, tick_limit=args.tick_limit,
-                           random_positions=True)
-    st = torch.cuda.Stream(device=dev)
-    ring = G
-    with torch.cuda.stream(st):
-        env.reset(random_positions=True)
-        acts = env.gen_random_actions(ring)
-        done = torch.empty(n, dtype=torch.uint8, device=dev)
-    st.synchronize()
-    slab, sp = 16 * n, ctypes.c_void_p(st.cuda_stream)
-
-    def launch(t):
-        env.step_raw(ctypes.c_void_p(acts.data_ptr() + (t % ring) * slab), ctypes.c_void_p(done.data_ptr()), stream=sp)
-
-    with torch.cuda.stream(st):
-        for t in range(2):
-            launch(t)
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, stream=st):
-        for t in range(G):
-            launch(t)
-    with torch.cuda.stream(st):
-        g.replay()
-    st.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     with torch.cuda.stream(st):
-        for _ in range(launches // G):
-            g.replay()
+        e0.record()
+    tg.replay(k)
+    with torch.cuda.stream(st):
+        e1.record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -184,41 +234,98 @@ def strong_scaling_rate(dev, args, rank, world, total=65536, launches=2000, G=40
         tt = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
-    steps = (launches // G) * G
+    ev = e0.elapsed_time(e1)
+    del tg
+    return el, ev, env
+
+
+def large_batch_rate(dev, args, rank, n=1 << 22, launches=60, ring=8):
+    """k_step at n games per GPU, graph-replayed, HIP-event timed (HBM-bound
+    regime: 193 B x n per launch)."""
+    el, ev, env = timed_ticks(dev, n, args.seed + 1, rank * n, args.tick_limit, launches, 2, ring, launches, 1)
     env.close()
-    return dict(total_envs=total, envs_per_gpu=n, n_gpus=world, env_steps_per_s=total * steps / el,
-                us_per_tick=el * 1e6 / steps, scaling="strong",
-                note="fixed 65,536 games over all GPUs (launch-bound per GPU at 8,192); reported beside the "
-                     "weak-scaling headline")
+    us = ev * 1e3 / launches
+    gbs = BYTES_PER_ENV_STEP * n / (us * 1e-6) / 1e9
+    torch.cuda.empty_cache()
+    return dict(envs_per_gpu=n, kernel="k_step (auto variant)", us_per_launch=us, env_steps_per_s_per_gpu=n / (us * 1e-6),
+                achieved_gbs=gbs, frac=gbs / HBM_PEAK_GBS,
+                note="state 369 MB > Infinity Cache: the HBM-bound regime; reported beside, not as, the headline")
 
 
-def learner_rate(envs, ticks=200, batch=4096):
-    """Configs 3 / 5 on one GPU: per tick the parameter-noise
-    actor forward for both players of every game, the fused env step with
+def full_contract_rate(dev, args, rank, n, launches=2000):
+    """The learner's env tick (SkillshotLearner.py:302-324): actions in, state
+    stepped, obs + reward of the post-tick state and done out, random
+    auto-reset — 297 B per env-step (SURVEY §8(d) full contract); the auto
+    variant picks k_step_split when observations are written."""
+    el, ev, env = timed_ticks(dev, n, args.seed + 3, rank * n, args.tick_limit, launches, 200, args.action_ring,
+                              args.graph_len, 1, obs=True)
+    env.close()
+    us = ev * 1e3 / launches
+    gbs = BYTES_FULL_CONTRACT * n / (us * 1e-6) / 1e9
+    return dict(envs_per_gpu=n, kernel="k_step_split (auto variant with obs)", launches=launches,
+                us_per_launch=us, env_steps_per_s_per_gpu=n / (us * 1e-6),
+                roofline=dict(bound="hbm", achieved=gbs, peak=HBM_PEAK_GBS, unit="GB/s", frac=gbs / HBM_PEAK_GBS,
+                              bytes_per_env_step=BYTES_FULL_CONTRACT,
+                              bytes="state 88 read + 88 written, actions 16, obs 96, reward 8, done 1"))
+
+
+def weak_rate(dev, args, rank, world, n=65536, launches=2000):
+    """65,536 games per GPU (weak scaling), same fused tick and timing."""
+    el, ev, env = timed_ticks(dev, n, args.seed + 2, rank * n, args.tick_limit, launches, 200, args.action_ring,
+                              args.graph_len, world)
+    env.close()
+    return dict(envs_per_gpu=n, total_envs=n * world, n_gpus=world, env_steps_per_s=n * world * launches / el,
+                us_per_tick=el * 1e6 / launches, event_us_per_tick=ev * 1e3 / launches, scaling="weak")
+
+
+def learner_rate(envs, world, rank, ticks, batch=256, exploration="param_noise", precision="bf16", group=None):
+    """per tick the actor forward (exploration
+    noise) for both players of every game, the fused env step with
     obs/reward/auto-reset, 2N transitions into the HBM replay ring, one critic
     + actor update (fused MFMA kernels, in-kernel bootstrap target) on a
     `batch` sample, soft target update and actor repack — replayed as one
-    captured hipGraph per 2 ticks (SkillshotLearner.tick_graph)."""
+    captured hipGraph per 2 ticks (SkillshotLearner.tick_graph).  envs = games
+    on this rank (global ids rank * envs ..)."""
     from skillshot_learning_amd.learner import SkillshotLearner
-    L = SkillshotLearner(n_envs=envs, seed=0, exploration="param_noise", tick_limit=2000,
-                         replay_capacity=1 << 20, gamma=0.99, tau=0.005)
+    L = SkillshotLearner(n_envs=envs, seed=0, env_offset=rank * envs, exploration=exploration, tick_limit=2000,
+                         replay_capacity=1 << 20, gamma=0.99, tau=0.005, precision=precision, process_group=group)
     tg = L.tick_graph(batch=batch, updates_per_tick=1, ticks_per_graph=2)
     tg.run(10)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     e0.record(tg.stream)
     tg.run(ticks // 2)
     e1.record(tg.stream)
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     el = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device=L.device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
     n_ticks = (ticks // 2) * 2
-    out = dict(envs_per_gpu=envs, ticks=n_ticks, batch=batch, exploration="param_noise", updates_per_tick=1,
-               env_steps_per_s=envs * n_ticks / el, ms_per_tick=el * 1e3 / n_ticks,
+    out = dict(envs_per_gpu=envs, total_envs=envs * world, n_gpus=world, ticks=n_ticks, batch_per_rank=batch,
+               exploration=exploration, updates_per_tick=1, dtype=precision, multi_rank=tg.multi_rank_mode,
+               env_steps_per_s=envs * world * n_ticks / el, ms_per_tick=el * 1e3 / n_ticks,
                gpu_ms_per_tick=e0.elapsed_time(e1) / n_ticks, episodes=L.game_environment.counters())
     del tg, L
     torch.cuda.empty_cache()
     return out
+
+
+def _guard(name, fn, errors):
+    """a secondary leg must never cost the headline line"""
+    try:
+        return fn()
+    except Exception as e:  # noqa: BLE001
+        errors[name] = f"{type(e).__name__}: {e}"
+        traceback.print_exc()
+        return None
 
 
 def main():
@@ -240,77 +347,17 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
-    from skillshot_learning_amd import VecSkillshotGame
-
-    n = args.envs
-    env = VecSkillshotGame(n, device=dev, seed=args.seed, env_offset=rank * n, tick_limit=args.tick_limit,
-                           random_positions=True)
-    stream = torch.cuda.Stream(device=dev)
-    G = max(2, args.graph_len - (args.graph_len % 2))  # even: keeps the step-slot parity invariant
-    ring = max(G, args.action_ring)
-    with torch.cuda.stream(stream):
-        env.reset(random_positions=True)
-        actions = env.gen_random_actions(ring)  # [ring, 2, N, 2] f32, 16 B/env/tick
-        done = torch.empty(n, dtype=torch.uint8, device=dev)
-    stream.synchronize()
-
-    a_ptr0 = actions.data_ptr()
-    slab = 2 * n * 2 * 4
-    d_ptr = done.data_ptr()
-    import ctypes
-    sp = ctypes.c_void_p(stream.cuda_stream)
-
-    def launch(t):
-        env.step_raw(ctypes.c_void_p(a_ptr0 + (t % ring) * slab), ctypes.c_void_p(d_ptr), stream=sp)
-
-    # capture one graph of G launches (eager warm-up first so code objects load)
-    with torch.cuda.stream(stream):
-        for t in range(4):
-            launch(t)
-    stream.synchronize()
-    graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph, stream=stream):
-        for t in range(G):
-            launch(t)
-    stream.synchronize()
-
-    def run(k):
-        """k launches: whole graph replays, remainder eager (parity-safe)."""
-        with torch.cuda.stream(stream):
-            for _ in range(k // G):
-                graph.replay()
-            for t in range(k % G):
-                launch(t)
-
-    env.clear_counters()
-    run(args.warmup)
-    stream.synchronize()
-
-    K = args.steps
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    with torch.cuda.stream(stream):
-        ev0.record()
-    run(K)
-    with torch.cuda.stream(stream):
-        ev1.record()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    ev_ms = ev0.elapsed_time(ev1)
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-    total_env_steps = n * world * K
-    value = total_env_steps / elapsed
+    total = args.envs
+    n = total // world  # strong scaling: the metric's fixed 65,536 games over the ranks
+    ring = max(args.graph_len, args.action_ring)
+    K, W = args.steps, args.warmup
+    elapsed, ev_ms, env = timed_ticks(dev, n, args.seed, rank * n, args.tick_limit, K, W, ring, args.graph_len, world)
+    value = n * world * K / elapsed
+    counters = env.counters()
+    env.close()
 
     # ---- roofline: the timed region is K back-to-back k_step launches on
-    # `stream` (graph replays), so the HIP-event span / K is the kernel's
+    # one stream (graph replays), so the HIP-event span / K is the kernel's
     # average launch duration (rocprofv3 --stats reports the same figure).
     kern_ms = ev_ms / K
     achieved = BYTES_PER_ENV_STEP * n / (kern_ms * 1e-3) / 1e9
@@ -323,49 +370,60 @@ def main():
         except Exception:
             traffic = None
 
-    counters = env.counters()
-
-    # ---- secondary: register-resident multi-tick random-policy kernel
+    errors = {}
     rollout = None
     if not args.no_rollout:
-        ticks = 200
-        with torch.cuda.stream(stream):
-            env.rollout_random(ticks)
-        stream.synchronize()
-        r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        reps = 10
-        with torch.cuda.stream(stream):
+        def _rollout():
+            from skillshot_learning_amd import VecSkillshotGame
+            g = VecSkillshotGame(n, device=dev, seed=args.seed, env_offset=rank * n, tick_limit=args.tick_limit,
+                                 random_positions=True)
+            g.reset(random_positions=True)
+            ticks, reps = 200, 10
+            g.rollout_random(ticks)
+            torch.cuda.synchronize()
+            r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             r0.record()
             for _ in range(reps):
-                env.rollout_random(ticks)
+                g.rollout_random(ticks)
             r1.record()
-        stream.synchronize()
-        rms = r0.elapsed_time(r1)
-        rollout = dict(kernel="k_rollout_random", ticks_per_launch=ticks,
-                       env_steps_per_s_per_gpu=n * ticks * reps / (rms * 1e-3),
-                       note="state held in registers across ticks; reported beside, not as, the headline")
+            torch.cuda.synchronize()
+            g.close()
+            return dict(kernel="k_rollout_random", ticks_per_launch=ticks, envs_per_gpu=n,
+                        env_steps_per_s_per_gpu=n * ticks * reps / (r0.elapsed_time(r1) * 1e-3),
+                        note="state held in registers across ticks; reported beside, not as, the headline")
+        rollout = _guard("rollout_random", _rollout, errors)
 
-    # ---- secondary: the same k_step tick at 4 M games per GPU (369 MB of
-    # state: past the 256 MB Infinity Cache, so truly HBM-bound, not
-    # launch-bound) — SURVEY §7 hard part 3; reported beside the headline
-    large = None
-    if not args.no_large:
-        large = large_batch_rate(dev, args, rank)
-    strong = None
-    if world > 1 and not args.no_strong:
-        strong = strong_scaling_rate(dev, args, rank, world)
+    full = None if args.no_full else _guard("full_contract_tick", lambda: full_contract_rate(dev, args, rank, n),
+                                            errors)
+    large = None if args.no_large else _guard("large_batch", lambda: large_batch_rate(dev, args, rank), errors)
+    weak = None
+    if world > 1 and not args.no_weak:
+        weak = _guard("weak_scaling", lambda: weak_rate(dev, args, rank, world), errors)
 
-    # ---- secondary: the DDPG learner in the loop (configs 3 and 5 on one GPU)
+    # ---- the DDPG learner in the loop: configs 3 / 5 on one GPU; configs 4
+    # (32,768 games over the ranks, gradient all-reduce) and 5 (65,536, param
+    # noise, shared-replay all-gather) at N > 1
     learner = None
-    if world == 1 and not args.no_learner:
-        learner = {"config3": learner_rate(4096), "config5_1gpu": learner_rate(65536),
-                   "note": "env step + param-noise actor + replay insert/sample + critic/actor update per tick; "
+    if not args.no_learner:
+        T = args.learner_ticks
+        learner = {"note": "actor + env step + replay insert/sample + critic/actor update per tick, graph-replayed; "
                            "reported beside, not as, the headline"}
+        if world == 1:
+            for prec in ("fp32", "bf16"):
+                learner[f"config3_{prec}"] = _guard(f"learner.config3_{prec}", lambda: learner_rate(
+                    4096, 1, 0, T, batch=256, exploration="action_noise", precision=prec), errors)
+            learner["config5_1gpu_bf16"] = _guard("learner.config5_1gpu", lambda: learner_rate(
+                65536, 1, 0, T, batch=256, exploration="param_noise", precision="bf16"), errors)
+        else:
+            learner["config4"] = _guard("learner.config4", lambda: learner_rate(
+                32768 // world, world, rank, T, batch=256, exploration="action_noise", precision="fp32"), errors)
+            learner["config5"] = _guard("learner.config5", lambda: learner_rate(
+                65536 // world, world, rank, T, batch=256, exploration="param_noise", precision="bf16"), errors)
 
     cpu = None
     if world == 1 and not args.no_cpu_baseline:  # N=1 only (the CPU baseline is a per-box figure)
-        cpu = cpu_baseline(n, args.cpu_seconds, args.tick_limit, args.seed,
-                           max(1, min(args.cpu_cores, os.cpu_count() or 1)))
+        cpu = _guard("cpu_baseline", lambda: cpu_baseline(n, args.cpu_seconds, args.tick_limit, args.seed,
+                                                          max(1, min(args.cpu_cores, os.cpu_count() or 1))), errors)
 
     if rank == 0:
         line = {
@@ -374,23 +432,23 @@ def main():
             "unit": "env-steps/s",
             "n_gpus": world,
             "steps": K,
-            "warmup": args.warmup,
+            "warmup": W,
             "ms_per_step": elapsed * 1e3 / K,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
             "config": {
-                "workload": f"config-2 step kernel: {n} games/GPU, random policy (Philox f32 actions pre-generated "
-                            f"in HBM), fused k_step per tick (do_actions x2 + game_tick + done + random "
-                            f"auto-reset), tick_limit {args.tick_limit}",
+                "workload": f"config-2 step kernel at the metric's size: {total} games in total, {n} per GPU, random "
+                            f"policy (Philox f32 actions pre-generated in HBM), fused k_step per tick (do_actions x2 + "
+                            f"game_tick + done + random auto-reset), tick_limit {args.tick_limit}, graph-replayed",
                 "envs_per_gpu": n,
-                "total_envs": n * world,
-                "global_batch": n * world,
+                "total_envs": total,
+                "global_batch": total,
                 "parallelism": f"env-shard dp{world}",
-                "graph_len": G,
-                "event_ms_per_step": ev_ms / K,
+                "graph_len": args.graph_len,
+                "event_ms_per_step": kern_ms,
             },
             "roofline": {
                 "bound": "hbm",
@@ -399,24 +457,25 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
+                "traffic_source": "profiles/traffic_k_step.json (rocprofv3 --pmc pass, not this run)",
                 "kernel": "k_step",
                 "bytes_per_env_step": BYTES_PER_ENV_STEP,
                 "kernel_us": kern_ms * 1e3,
             },
             "cpu_baseline": cpu,
             "episodes": counters,
+            "full_contract_tick": full,
             "rollout_random": rollout,
             "large_batch": large,
+            "weak_scaling": weak,
             "learner": learner,
-            "strong_scaling": strong if strong is not None else (
-                {"total_envs": n, "n_gpus": 1, "env_steps_per_s": value, "scaling": "strong",
-                 "note": "N=1: the headline itself"} if world == 1 and n == 65536 else None),
         }
+        if errors:
+            line["errors"] = errors
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-    env.close()
 
 
 if __name__ == "__main__":

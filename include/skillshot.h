@@ -128,6 +128,13 @@ int sk_env_clear_counters(sk_env* env, void* stream);
  * (seed, global env id, step counter)). */
 int sk_env_get_step_counter(const sk_env* env, uint64_t* out);
 int sk_env_set_step_counter(sk_env* env, uint64_t value);
+/* Stream-ordered, capturable: make both device step slots hold the current
+ * value (their maximum) and reset the host parity.  A hipGraph captured after
+ * this call reads the right value at its first node whatever launches ran
+ * between capture and replay, so eager launches and graph replays can be
+ * mixed (call it between them).  No reference equivalent (the reference's
+ * RNG is np.random's global state, SkillshotGame.py:15). */
+int sk_env_sync_step_counter(sk_env* env, void* stream);
 
 /* SkillshotGame.game_reset(random_positions) (SkillshotGame.py:168-169 ->
  * __init__ :10-25) for the envs whose mask byte is non-zero (mask NULL = all).

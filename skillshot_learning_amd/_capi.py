@@ -23,7 +23,7 @@ EXPORTS = (
     "sk_last_error", "sk_abi_version", "sk_config_default", "sk_env_create", "sk_env_attach",
     "sk_env_destroy", "sk_env_get_view", "sk_env_counters_ptr", "sk_env_read_counters",
     "sk_env_clear_counters", "sk_env_get_step_counter",
-    "sk_env_set_step_counter", "sk_env_reset", "sk_player_move_direction", "sk_player_move_look",
+    "sk_env_set_step_counter", "sk_env_sync_step_counter", "sk_env_reset", "sk_player_move_direction", "sk_player_move_look",
     "sk_player_move_discrete", "sk_player_shoot", "sk_projectile_move", "sk_game_check_collision", "sk_game_tick", "sk_env_features", "sk_env_observe",
     "sk_env_step", "sk_gen_random_actions", "sk_env_rollout_random",
     "sk_actor_packed_bytes", "sk_actor_pack", "sk_actor_forward", "sk_actor_forward_dev",
@@ -96,6 +96,7 @@ def load(build_if_missing=True):
         "sk_env_clear_counters": ([P, P], ctypes.c_int),
         "sk_env_get_step_counter": ([P, ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
         "sk_env_set_step_counter": ([P, u64], ctypes.c_int),
+        "sk_env_sync_step_counter": ([P, P], ctypes.c_int),
         "sk_env_reset": ([P, P, i32, P], ctypes.c_int),
         "sk_player_move_direction": ([P, i32, P, f64, P], ctypes.c_int),
         "sk_player_move_look": ([P, i32, P, f64, P], ctypes.c_int),

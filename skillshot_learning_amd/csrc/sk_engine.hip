@@ -856,11 +856,18 @@ int sk_env_clear_counters(sk_env* e, void* stream) {
   return SK_OK;
 }
 
+// The step counter only grows (every launch stores value + advance >= value
+// into the other slot), so the current value is the larger slot whatever
+// parity the host believes in: a graph captured at one parity and replayed
+// after an odd number of eager launches leaves the host parity stale, never
+// the maximum.
 int sk_env_get_step_counter(const sk_env* e, uint64_t* out) {
   if (!e || !out) return fail(SK_EINVAL, "NULL argument");
   HIP_TRY(hipSetDevice(e->device));
   HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpy(out, e->d_step + e->parity, sizeof(uint64_t), hipMemcpyDeviceToHost));
+  uint64_t s[2];
+  HIP_TRY(hipMemcpy(s, e->d_step, sizeof(s), hipMemcpyDeviceToHost));
+  *out = s[0] > s[1] ? s[0] : s[1];
   return SK_OK;
 }
 
@@ -868,7 +875,25 @@ int sk_env_set_step_counter(sk_env* e, uint64_t v) {
   if (!e) return fail(SK_EINVAL, "NULL handle");
   HIP_TRY(hipSetDevice(e->device));
   HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpy(e->d_step + e->parity, &v, sizeof(uint64_t), hipMemcpyHostToDevice));
+  const uint64_t s[2] = {v, v};
+  HIP_TRY(hipMemcpy(e->d_step, s, sizeof(s), hipMemcpyHostToDevice));
+  e->parity = 0;
+  return SK_OK;
+}
+
+__global__ void k_sync_step_slots(uint64_t* slots) {
+  if (threadIdx.x == 0) {
+    const uint64_t a = slots[0], b = slots[1], m = a > b ? a : b;
+    slots[0] = m;
+    slots[1] = m;
+  }
+}
+
+int sk_env_sync_step_counter(sk_env* e, void* stream) {
+  if (!e) return fail(SK_EINVAL, "NULL handle");
+  k_sync_step_slots<<<1, 64, 0, (hipStream_t)stream>>>(e->d_step);
+  HIP_TRY(hipGetLastError());
+  e->parity = 0;
   return SK_OK;
 }
 

@@ -483,8 +483,13 @@ class SkillshotLearner:
 
     def __init__(self, n_envs=1, device="cuda", seed=0, env_offset=0, exploration="param_noise",
                  tick_limit=2000, use_random_start=True, replay_capacity=1 << 20, batch_size=16,
-                 gamma=0.0, tau=None, actor_kernel=True, process_group=None):
+                 gamma=0.0, tau=None, actor_kernel=True, process_group=None, precision="bf16"):
         from .vec_env import VecSkillshotGame
+        if precision not in ("bf16", "fp32"):
+            raise ValueError("precision must be 'bf16' or 'fp32'")
+        if precision == "fp32":
+            raise NotImplementedError("fp32 learner kernels are not built yet")
+        self.precision = precision
         self.device = torch.device(device)
         self.game_environment = VecSkillshotGame(n_envs, device=self.device, seed=seed, env_offset=env_offset,
                                                  tick_limit=tick_limit, random_positions=use_random_start)
@@ -742,6 +747,7 @@ class TickGraph:
 
     def __init__(self, L, batch, updates_per_tick, ticks_per_graph, warmup):
         self.L, self.batch, self.updates, self.ticks = L, batch, updates_per_tick, ticks_per_graph
+        self.multi_rank_mode = None
         g = L.game_environment
         n = L.n_envs
         dev = L.device

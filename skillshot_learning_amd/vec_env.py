@@ -105,6 +105,12 @@ class VecSkillshotGame:
     def step_counter(self, value):
         check(self._L.sk_env_set_step_counter(self._h, int(value)))
 
+    def sync_step_counter(self, stream=None):
+        """Stream-ordered: both device step slots take the current value, so
+        graphs captured after this call replay with correct RNG keys after any
+        mix of eager launches (sk_env_sync_step_counter)."""
+        check(self._L.sk_env_sync_step_counter(self._h, stream if stream is not None else self._stream()))
+
     def state_dict(self):
         """Host copy of the state planes (engine layout) + RNG counter."""
         d = {name: getattr(self, name).cpu().numpy().copy() for name, _, _ in PLANES}
