@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define SK_ABI_VERSION 1
+#define SK_ABI_VERSION 2
 
 enum {
   SK_OK = 0,
@@ -307,7 +307,9 @@ int sk_replay_sample(const float* ring, int64_t capacity, const int64_t* total, 
  *                   ld2 = 258 critic, 256 actor; W3 [n_out][128]) -> a device
  *                   buffer of sk_grad_packed_bytes() bytes (16-byte aligned)
  *   sk_critic_grad  critic forward in training mode (Dropout(0.2) masks from
- *                   Philox keyed by (seed, *call_counter, row, unit)), loss
+ *                   Philox keyed by (seed, *call_counter, row_offset + row,
+ *                   unit): row_offset (a multiple of 4) numbers the rows of a
+ *                   batch split over ranks as in the 1-rank batch), loss
  *                   sum_b (q_b - y_b)^2 * grad_scale / 2 (grad_scale = 2/B is
  *                   F.mse_loss), backward: per-workgroup gradient partials
  *                   float[sk_update_partials(batch)][36,609] in torch
@@ -319,8 +321,9 @@ int sk_replay_sample(const float* ring, int64_t capacity, const int64_t* total, 
  *                   partials float[sk_update_partials(batch)][36,482];
  *                   q_sum (nullable) += sum_b Q
  *   sk_adam_flat    g = grad_in (nullable) + sum of n_partials partials ->
- *                   grad_out (nullable); if apply: torch.optim.Adam (fused
- *                   formulation) on flat param / exp_avg / exp_avg_sq with
+ *                   grad_out (nullable); if apply: Keras Adam (epsilon added
+ *                   to sqrt(v) before the bias correction, SkillshotLearner.py
+ *                   :68) on flat param / exp_avg / exp_avg_sq with
  *                   the step count *step_counter (advanced by the grad
  *                   kernels: step_counters[0 .. n_steps) += 1), then
  *                   target (nullable) += tau (param - target); and, when
@@ -339,8 +342,9 @@ int sk_grad_pack(const float* W1, const float* b1, const float* W2, int32_t ld2,
 int sk_grad_pack_flat(const float* const* flats, const int32_t* ld2s, const int32_t* n_outs, void* const* outs,
                       int32_t n_nets, void* stream);
 int sk_critic_grad(const void* critic_gpack, const float* obs, const float* actions, const float* targets,
-                   int64_t batch, float grad_scale, uint64_t seed, const int64_t* call_counter, float* partials,
-                   float* step_counters, int32_t n_steps, float* loss_sum, uint8_t* dropout_mask, void* stream);
+                   int64_t batch, int64_t row_offset, float grad_scale, uint64_t seed, const int64_t* call_counter,
+                   float* partials, float* step_counters, int32_t n_steps, float* loss_sum, uint8_t* dropout_mask,
+                   void* stream);
 /* sk_critic_grad with the DDPG target computed in the same launch: targets
  * = rewards + gamma (1 - done) Q'(next_obs, mu'(next_obs)) with the target
  * nets given as grad packs (targets may be NULL; next_obs float[batch][12],
@@ -348,9 +352,9 @@ int sk_critic_grad(const void* critic_gpack, const float* obs, const float* acti
 int sk_critic_grad_bootstrap(const void* critic_gpack, const float* obs, const float* actions, const float* targets,
                              const float* next_obs, const float* rewards, const float* done, float gamma,
                              const void* target_actor_gpack, const void* target_critic_gpack, int64_t batch,
-                             float grad_scale, uint64_t seed, const int64_t* call_counter, float* partials,
-                             float* step_counters, int32_t n_steps, float* loss_sum, uint8_t* dropout_mask,
-                             void* stream);
+                             int64_t row_offset, float grad_scale, uint64_t seed, const int64_t* call_counter,
+                             float* partials, float* step_counters, int32_t n_steps, float* loss_sum,
+                             uint8_t* dropout_mask, void* stream);
 int sk_actor_grad(const void* actor_gpack, const void* critic_gpack, const float* obs, int64_t batch,
                   float loss_scale, float* partials, float* step_counters, int32_t n_steps, float* q_sum,
                   void* stream);

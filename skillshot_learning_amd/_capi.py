@@ -16,7 +16,7 @@ from . import build as _build
 
 SK_OK, SK_EINVAL, SK_EHIP, SK_ENOMEM, SK_ENODEV = 0, -1, -2, -3, -4
 SK_REWARD_LOOKING, SK_REWARD_SIMPLE = 0, 1
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # every symbol include/skillshot.h declares
 EXPORTS = (
@@ -122,7 +122,7 @@ def load(build_if_missing=True):
         "sk_grad_packed_bytes": ([], ctypes.c_size_t),
         "sk_update_partials": ([i64], ctypes.c_int64),
         "sk_grad_pack": ([P, P, P, i32, P, P, P, i32, P, P], ctypes.c_int),
-        "sk_critic_grad": ([P, P, P, P, i64, f32, u64, P, P, P, i32, P, P, P], ctypes.c_int),
+        "sk_critic_grad": ([P, P, P, P, i64, i64, f32, u64, P, P, P, i32, P, P, P], ctypes.c_int),
         "sk_actor_grad": ([P, P, P, i64, f32, P, P, i32, P, P], ctypes.c_int),
         "sk_adam_flat_packed": ([P, i32, i32, P, P, i32, P, P, P, P, f32, f32, f32, f32, P, f32, P, f32, P, P, P, P],
                                 ctypes.c_int),
@@ -132,7 +132,7 @@ def load(build_if_missing=True):
         "sk_replay_insert": ([P, i64, P, P, P, P, P, P, P, i64, i64, P], ctypes.c_int),
         "sk_replay_sample": ([P, i64, P, u64, i32, i64, P, P, P, P, P, P], ctypes.c_int),
         "sk_grad_pack_flat": ([P, P, P, P, i32, P], ctypes.c_int),
-        "sk_critic_grad_bootstrap": ([P, P, P, P, P, P, P, f32, P, P, i64, f32, u64, P, P, P, i32, P, P, P],
+        "sk_critic_grad_bootstrap": ([P, P, P, P, P, P, P, f32, P, P, i64, i64, f32, u64, P, P, P, i32, P, P, P],
                                      ctypes.c_int),
     }
     for name, (argt, rest) in sig.items():

@@ -241,7 +241,7 @@ __device__ __forceinline__ void load_states(const Lds& L, const float* S, int64_
 template <bool DROP>
 __device__ __forceinline__ void layer1(const short* Sx, const bf16x8* gW1, const float* tail, int nt, int lane,
                                        short* H, short* HT, uint64_t seed, uint64_t call, int64_t row0,
-                                       uint8_t* mask_out, int64_t B) {
+                                       uint8_t* mask_out, int64_t B, int64_t key_row0 = 0) {
   f32x16 acc = {0};
   acc = mfma(lfrag(Sx, kLdS, 0, 0, lane), gW1[nt * 64 + lane], acc);
   const int n = 32 * nt + (lane & 31);
@@ -251,7 +251,10 @@ __device__ __forceinline__ void layer1(const short* Sx, const bf16x8* gW1, const
     float hv[4];
     uint4 u = make_uint4(0, 0, 0, 0);
     const int i0 = drow(4 * g, lane);
-    if (DROP) u = philox(make_uint4((uint32_t)((row0 + i0) >> 2), (uint32_t)n, (uint32_t)call, (uint32_t)(call >> 32)),
+    // the mask of GLOBAL batch row key_row0 + row0 + i (the 1-rank batch's
+    // row numbering; key_row0 is a multiple of 4): learner.DDPG, rng.dropout_keep
+    if (DROP) u = philox(make_uint4((uint32_t)((key_row0 + row0 + i0) >> 2), (uint32_t)n, (uint32_t)call,
+                                    (uint32_t)(call >> 32)),
                          (uint32_t)seed, (uint32_t)(seed >> 32));
     const uint32_t uw[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
@@ -400,7 +403,8 @@ __device__ __forceinline__ void bootstrap_target(const Lds& L, const char* tap, 
 // (DDPG.critic_step; critic.fit, SkillshotLearner.py:434): dL/dq =
 // grad_scale * (q - y) with grad_scale = 2 / (global batch).
 __global__ void __launch_bounds__(kThreads) k_critic_grad(const float* __restrict__ S, const float* __restrict__ A,
-                                                          const float* __restrict__ Y, int64_t B, int sub_per_wg,
+                                                          const float* __restrict__ Y, int64_t B, int64_t key_row0,
+                                                          int sub_per_wg,
                                                           float grad_scale, uint64_t seed,
                                                           const int64_t* __restrict__ call_ctr,
                                                           const char* __restrict__ gpack, float* __restrict__ partial,
@@ -459,7 +463,7 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad(const float* __restric
     }
     __syncthreads();
     SK_TP(4);
-    layer1<true>(L.Sr, fW1, tail, w, lane, L.H1, L.H1T, seed, call, row0, mask_out, B);
+    layer1<true>(L.Sr, fW1, tail, w, lane, L.H1, L.H1T, seed, call, row0, mask_out, B, key_row0);
     __syncthreads();
     SK_TP(5);
     float h2v[16];
@@ -678,10 +682,12 @@ __global__ void __launch_bounds__(kThreads) k_actor_grad(const float* __restrict
 // ---------------------------------------------------------------- Adam
 // g = sum of the G partials (+ written to grad_out, if given, e.g. for an
 // RCCL all-reduce between this kernel with apply=0 and a second with G=0).
-// torch.optim.Adam (fused) formulation: m = b1 m + (1-b1) g, v = b2 v +
-// (1-b2) g^2, p -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps), t = the
-// step counter (advanced by the grad kernel).  Then target += tau (p -
-// target) (torch._foreach_lerp_, DDPG.soft_update) when a target is given.
+// Keras Adam (tf.keras.optimizers.Adam of SkillshotLearner.py:68, :118;
+// learner.KerasAdam): m += (g - m)(1-b1), v += (g^2 - v)(1-b2),
+// p -= m alpha / (sqrt(v) + eps) with alpha = lr sqrt(1-b2^t) / (1-b1^t),
+// t = the step counter (advanced by the grad kernel).  Then target += tau
+// (p - target) (torch._foreach_lerp_, DDPG.soft_update) when a target is
+// given.
 // Housekeeping of the step, by thread 0 when applying (after the gradient
 // kernel consumed them, before the next one): stat_out = stat_acc * scale and
 // stat_acc = 0 (the loss accumulator of the gradient kernel), ++*counter (its
@@ -810,14 +816,13 @@ __global__ void __launch_bounds__(kAdamParams * kAdamSlices) k_adam_flat(const f
   if (grad_out) grad_out[p] = g;
   if (!apply) return;
   const float t = step_ctr[0];
-  const float bc1 = 1.f - powf(beta1, t), bc2 = 1.f - powf(beta2, t);
+  const float alpha = lr * sqrtf(1.f - powf(beta2, t)) / (1.f - powf(beta1, t));
   float mm = m[p], vv = v[p];
-  mm = mm + (1.f - beta1) * (g - mm);  // exp_avg.lerp_(grad, 1 - beta1)
-  vv = vv * beta2 + (1.f - beta2) * g * g;
+  mm = mm + (g - mm) * (1.f - beta1);
+  vv = vv + (g * g - vv) * (1.f - beta2);
   m[p] = mm;
   v[p] = vv;
-  const float denom = sqrtf(vv) / sqrtf(bc2) + eps;
-  const float w = param[p] - (lr / bc1) * mm / denom;
+  const float w = param[p] - (mm * alpha) / (sqrtf(vv) + eps);
   param[p] = w;
   if (po.gp) scatter_grad_pack(po.gp, p, w, po.ld2, po.n_out);
   if (po.fp) scatter_fwd_pack(po.fp, p, w);
@@ -876,20 +881,21 @@ int sk_grad_pack(const float* W1, const float* b1, const float* W2, int32_t ld2,
 }
 
 int sk_critic_grad(const void* cpack, const float* obs, const float* actions, const float* targets, int64_t batch,
-                   float grad_scale, uint64_t seed, const int64_t* call_counter, float* partial, float* step_counters,
-                   int32_t n_steps, float* loss_sum, uint8_t* dropout_mask, void* stream) {
+                   int64_t row_offset, float grad_scale, uint64_t seed, const int64_t* call_counter, float* partial,
+                   float* step_counters, int32_t n_steps, float* loss_sum, uint8_t* dropout_mask, void* stream) {
   return sk_critic_grad_bootstrap(cpack, obs, actions, targets, nullptr, nullptr, nullptr, 0.f, nullptr, nullptr,
-                                  batch, grad_scale, seed, call_counter, partial, step_counters, n_steps, loss_sum,
-                                  dropout_mask, stream);
+                                  batch, row_offset, grad_scale, seed, call_counter, partial, step_counters, n_steps,
+                                  loss_sum, dropout_mask, stream);
 }
 
 int sk_critic_grad_bootstrap(const void* cpack, const float* obs, const float* actions, const float* targets,
                              const float* next_obs, const float* rewards, const float* done, float gamma,
                              const void* target_actor_gpack, const void* target_critic_gpack, int64_t batch,
-                             float grad_scale, uint64_t seed, const int64_t* call_counter, float* partial,
-                             float* step_counters, int32_t n_steps, float* loss_sum, uint8_t* dropout_mask,
-                             void* stream) {
+                             int64_t row_offset, float grad_scale, uint64_t seed, const int64_t* call_counter,
+                             float* partial, float* step_counters, int32_t n_steps, float* loss_sum,
+                             uint8_t* dropout_mask, void* stream) {
   const bool boot = target_actor_gpack != nullptr;
+  if (row_offset < 0 || (row_offset & 3)) return SK_EINVAL;
   if (boot && (!target_critic_gpack || !next_obs || !rewards || !done)) return SK_EINVAL;
   if (!boot && !targets) return SK_EINVAL;
   if (boot && ((((uintptr_t)target_actor_gpack) & 15) || (((uintptr_t)target_critic_gpack) & 15))) return SK_EINVAL;
@@ -904,7 +910,7 @@ int sk_critic_grad_bootstrap(const void* cpack, const float* obs, const float* a
   const int64_t spw = subtiles_per_wg(batch);
   const unsigned G = (unsigned)sk_update_partials(batch);
   k_critic_grad<<<G, kThreads, kLdsCritic, (hipStream_t)stream>>>(
-      obs, actions, targets, batch, (int)spw, grad_scale, seed, call_counter, (const char*)cpack, partial,
+      obs, actions, targets, batch, row_offset, (int)spw, grad_scale, seed, call_counter, (const char*)cpack, partial,
       step_counters, n_steps, loss_sum, dropout_mask, next_obs, rewards, done, gamma,
       (const char*)target_actor_gpack, (const char*)target_critic_gpack);
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;

@@ -34,6 +34,8 @@ import torch.distributed as dist
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .rng import DROP_SCALE, dropout_keep
+
 STATE_DIM = 12   # SkillshotLearner.py:54
 ACTION_DIM = 2   # :55
 MAX_DIST = (2 * (250 ** 2)) ** 0.5  # max_dist_normaliser, :43
@@ -156,18 +158,63 @@ class Critic(nn.Module):
         for l in (self.l1, self.l2, self.l3):
             nn.init.zeros_(l.bias)
 
-    def forward(self, s, a):
-        h = self.drop(F.relu(self.l1(s)))
+    def forward(self, s, a, keep=None):
+        """keep (bool [rows, 256], optional): the Dropout(0.2) keep-mask of a
+        training step (rng.dropout_keep, the kernels' masks); without it
+        nn.Dropout applies in train mode and nothing in eval mode."""
+        h = F.relu(self.l1(s))
+        h = h * (keep.to(h.dtype) * DROP_SCALE) if keep is not None else self.drop(h)
         h = F.relu(self.l2(torch.cat([h, a], dim=-1)))
         return self.l3(h)
 
 
+class KerasAdam(torch.optim.Optimizer):
+    """tf.keras.optimizers.Adam() of the reference (SkillshotLearner.py:68; the
+    critic's compile("adam"), :118): lr 1e-3, beta_1 0.9, beta_2 0.999,
+    epsilon 1e-7, and Keras' update rule (keras.optimizers.Adam.update_step,
+    TensorFlow 2.x; the reference pins no version, and the older
+    ResourceApplyAdam kernel is the same formula):
+
+        m += (g - m) (1 - beta_1);   v += (g^2 - v) (1 - beta_2)
+        alpha = lr sqrt(1 - beta_2^t) / (1 - beta_1^t)
+        p -= m alpha / (sqrt(v) + epsilon)
+
+    i.e. epsilon is added to sqrt(v) BEFORE the bias correction, where
+    torch.optim.Adam adds it after.  Per-parameter state `exp_avg`,
+    `exp_avg_sq` and `step` (a float32 tensor on the parameter's device, so a
+    hipGraph capture replays it); k_adam_flat (csrc/sk_update.hip) computes
+    the same formula."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-7):
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        for group in self.param_groups:
+            b1, b2 = group["betas"]
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                st = self.state[p]
+                if not st:
+                    st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
+                    st["exp_avg"] = torch.zeros_like(p)
+                    st["exp_avg_sq"] = torch.zeros_like(p)
+                if st["step"].device != p.device or st["step"].dtype != torch.float32:  # e.g. after load_state_dict
+                    st["step"] = st["step"].to(device=p.device, dtype=torch.float32)
+                g, m, v = p.grad, st["exp_avg"], st["exp_avg_sq"]
+                st["step"].add_(1.0)
+                t = st["step"]
+                m.add_((g - m) * (1.0 - b1))
+                v.add_((g * g - v) * (1.0 - b2))
+                alpha = group["lr"] * torch.sqrt(1.0 - torch.pow(b2, t)) / (1.0 - torch.pow(b1, t))
+                p.sub_((m * alpha) / (torch.sqrt(v) + group["eps"]))
+        return None
+
+
 def keras_adam(params):
-    """Keras Adam defaults (lr 1e-3, eps 1e-7); on GPU one fused multi-tensor
-    kernel with the step count on device (capturable into a hipGraph)."""
-    params = list(params)
-    gpu = bool(params) and params[0].is_cuda
-    return torch.optim.Adam(params, lr=1e-3, betas=(0.9, 0.999), eps=1e-7, fused=gpu, capturable=gpu)
+    """Keras Adam defaults (SkillshotLearner.py:68, :118)."""
+    return KerasAdam(list(params), lr=1e-3, betas=(0.9, 0.999), eps=1e-7)
 
 
 class ReplayRing:
@@ -291,15 +338,38 @@ class ReplayRing:
 
 class DDPG:
     """Actor/critic, optimisers and update rules (device-agnostic: CPU tests
-    and gloo multi-process tests drive it without a GPU)."""
+    and gloo multi-process tests drive it without a GPU).
+
+    Dropout of a critic training step is keyed by (dropout seed, call number,
+    GLOBAL batch row, unit) on every path (rng.dropout_keep on the torch path,
+    the same Philox draw inside k_critic_grad), and every loss is normalised by
+    the global batch, so an update split over ranks equals, up to fp32
+    summation order, the 1-rank update on the concatenated batch.
+
+    Multi-rank (one process per GPU, games sharded by global id; the seed is
+    shared, rank_seed_offset separates the ranks' replay draws):
+      multi_rank="grad"    (BASELINE config 4) every rank samples `batch` rows
+                           of its own replay ring, computes the gradient of its
+                           rows (global rows rank*batch ..), and the gradients
+                           are summed by one all-reduce per net;
+      multi_rank="shared"  (config 5, shared replay) the ranks' samples are
+                           all-gathered into one [world*batch] batch and rank r
+                           takes the strided slice r::world of it (rows of
+                           every rank), global rows rank*batch .., then the
+                           same gradient all-reduce.
+    Per-rank update work is `batch` rows whatever the world size."""
 
     def __init__(self, device="cpu", seed=0, batch_size=16, gamma=0.0, tau=None, replay_capacity=0,
-                 process_group=None, rank_seed_offset=0, fused_update=None):
+                 process_group=None, rank_seed_offset=0, fused_update=None, multi_rank="grad", precision="bf16"):
         self.device = torch.device(device)
         torch.manual_seed(seed)
         self.model_actor = Actor().to(self.device)
         self.model_critic = Critic().to(self.device)
         self.group = process_group
+        if multi_rank not in ("grad", "shared"):
+            raise ValueError("multi_rank must be 'grad' or 'shared'")
+        self.multi_rank = multi_rank
+        self.precision = precision
         self._sync_params()
         self.optimiser = keras_adam(self.model_actor.parameters())         # SkillshotLearner.py:68
         self.critic_optimiser = keras_adam(self.model_critic.parameters())  # critic.compile("adam"), :118
@@ -316,6 +386,10 @@ class DDPG:
         self._tq = None  # fused target-Q kernel (GPU), created at first use
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(seed * 7919 + rank_seed_offset + 17)
+        # Dropout key: the same on every rank (masks are keyed by global row);
+        # the call number lives on device (advanced once per critic step)
+        self.drop_seed = (seed * 1000033 + 5) & ((1 << 64) - 1)
+        self.drop_calls = torch.zeros(1, dtype=torch.int64, device=self.device)
         # the update on MFMA kernels (update_kernel.FusedUpdate) on the GPU;
         # SK_FUSED_UPDATE=0 / fused_update=False keeps the autograd path
         if fused_update is None:
@@ -323,11 +397,14 @@ class DDPG:
         self._fused = None
         if fused_update:
             from .update_kernel import FusedUpdate
-            self._fused = FusedUpdate(self, seed=seed * 1000033 + rank_seed_offset + 5)
+            self._fused = FusedUpdate(self)
 
     # ------------------------------------------------------------ distributed
     def world(self):
         return dist.get_world_size(self.group) if dist.is_available() and dist.is_initialized() else 1
+
+    def rank(self):
+        return dist.get_rank(self.group) if self.world() > 1 else 0
 
     def _sync_params(self):
         """Start every rank from rank 0's weights (broadcast)."""
@@ -337,14 +414,14 @@ class DDPG:
                     dist.broadcast(p.data, src=0, group=self.group)
 
     def _allreduce_grads(self, module):
-        """Gradient all-reduce (mean) as ONE flat bucket per update:
-        36,482 actor / 36,609 critic fp32 parameters (RCCL over xGMI)."""
+        """Gradient all-reduce (sum: each rank's loss is already normalised
+        by the global batch) as ONE flat bucket per update: 36,482 actor /
+        36,609 critic fp32 parameters (RCCL over xGMI)."""
         if self.world() <= 1:
             return
         grads = [p.grad for p in module.parameters()]
         flat = torch.cat([g.reshape(-1) for g in grads])
         dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
-        flat /= self.world()
         off = 0
         for g in grads:
             n = g.numel()
@@ -352,8 +429,9 @@ class DDPG:
             off += n
 
     def _allgather_batch(self, *tensors):
-        """Shared replay sample: every rank contributes its local minibatch and
-        all ranks train on the concatenation (one all-gather of a packed buffer)."""
+        """Shared replay sample: every rank contributes its local minibatch,
+        one all-gather of a packed buffer; returns the [world*b] batch (rank
+        0's rows first)."""
         w = self.world()
         if w <= 1:
             return tensors
@@ -368,21 +446,29 @@ class DDPG:
         return tuple(res)
 
     # ------------------------------------------------------------ updates
-    def critic_step(self, s, a, target):
+    def critic_step(self, s, a, target, row_offset=0, global_batch=None):
+        """One critic Adam step on MSE(Q(s, a), target) with Dropout active
+        (critic.fit, SkillshotLearner.py:434): loss = sum over this rank's
+        rows of (Q - y)^2 / global_batch (= the batch mean on one rank)."""
+        B = s.shape[0]
+        gb = B if global_batch is None else int(global_batch)
         if self._fused is not None:  # one MFMA gradient launch + one Adam launch
-            return self._fused.critic_step(s, a, target)
-        self.model_critic.train()  # Dropout active, as in critic.fit (:434)
-        q = self.model_critic(s, a).squeeze(-1)
-        loss = F.mse_loss(q, target)
+            return self._fused.critic_step(s, a, target, row_offset=row_offset, global_batch=gb)
+        self.model_critic.train()
+        keep = dropout_keep(self.drop_seed, self.drop_calls, row_offset, B, device=s.device)
+        q = self.model_critic(s, a, keep=keep).squeeze(-1)
+        loss = ((q - target) ** 2).sum() / gb
         self.critic_optimiser.zero_grad(set_to_none=True)  # backward writes the grads (no accumulate)
         loss.backward()
+        self.drop_calls.add_(1)
         self._allreduce_grads(self.model_critic)
         self.critic_optimiser.step()
         return loss.detach()
 
     def model_actor_fit_step(self, s):
         """model_actor_fit_step (:386-417): actor grads with output_gradients =
-        -dQ/da, i.e. descent on -sum_batch Q(s, mu(s)); critic in inference mode."""
+        -dQ/da, i.e. descent on -sum_batch Q(s, mu(s)); critic in inference
+        mode.  Multi-rank: each rank's -sum over its rows, gradients summed."""
         if self._fused is not None:
             return self._fused.actor_step(s)
         self.model_critic.eval()
@@ -400,40 +486,61 @@ class DDPG:
 
     def models_fit(self, states, actions, rewards):
         """models_fit (:419-443): shuffle, critic one pass at batch 16, then the
-        actor per batch of 16 on the same shuffled states."""
+        actor per batch of 16 on the same shuffled states.  No target nets
+        or soft update here (the reference has none)."""
         assert states.shape[0] == actions.shape[0] == rewards.shape[0]
         idx = torch.randperm(states.shape[0], device=states.device, generator=self.gen)
         states, actions, rewards = states[idx], actions[idx], rewards[idx]
         b = self.model_param_batch_size
-        for k in range(0, states.shape[0], b):
-            self.critic_step(states[k:k + b], actions[k:k + b], rewards[k:k + b])
-        for k in range(0, states.shape[0], b):
-            self.model_actor_fit_step(states[k:k + b])
+        fu = self._fused
+        if fu is not None:
+            fu.soft_update_in_adam = False
+        try:
+            for k in range(0, states.shape[0], b):
+                self.critic_step(states[k:k + b], actions[k:k + b], rewards[k:k + b])
+            for k in range(0, states.shape[0], b):
+                self.model_actor_fit_step(states[k:k + b])
+        finally:
+            if fu is not None:
+                fu.soft_update_in_adam = True
+
+    def sample_local(self, batch, device_sampling=False):
+        """this rank's minibatch of the replay ring"""
+        if device_sampling:
+            return self.replay.sample_dev(batch, generator=self.gen)
+        return self.replay.sample(batch, generator=self.gen)
 
     def replay_update(self, batch, device_sampling=False):
         """Build-side extension: one critic + one actor step on a replay
-        minibatch (shared across ranks by all-gather), optional bootstrapped
-        target with target nets and soft update tau.  device_sampling draws
-        the minibatch over the ring's device-side size (hipGraph capture)."""
-        if device_sampling:
-            s, a, r, s2, d = self.replay.sample_dev(batch, generator=self.gen)
-        else:
-            s, a, r, s2, d = self.replay.sample(batch, generator=self.gen)
-        s, a, r, s2, d = self._allgather_batch(s, a, r, s2, d)
+        minibatch (see the class doc for the multi-rank schemes), optional
+        bootstrapped target with target nets and soft update tau.
+        device_sampling draws the minibatch over the ring's device-side size
+        (hipGraph capture)."""
+        return self.update_batch(*self.sample_local(batch, device_sampling))
+
+    def update_batch(self, s, a, r, s2, d):
+        """replay_update on this rank's sampled rows s, a, r, s2, d."""
+        w, rk, b = self.world(), self.rank(), s.shape[0]
+        if w > 1 and self.multi_rank == "shared":
+            s, a, r, s2, d = [t[rk::w] for t in self._allgather_batch(s, a, r, s2, d)]
+        row0, gb = rk * b, w * b
+        if w > 1 and b % 4:
+            raise ValueError("multi-rank batches must be a multiple of 4 rows (Dropout key groups)")
         if self._fused is not None:  # critic step (bootstrap inside) + actor step: 4 launches, Adam writes packs
             if self.gamma > 0.0:
-                lc = self._fused.critic_step(s, a, s2=s2, r=r, d=d, gamma=self.gamma)
+                lc = self._fused.critic_step(s, a, s2=s2, r=r, d=d, gamma=self.gamma, row_offset=row0,
+                                             global_batch=gb)
             else:
-                lc = self._fused.critic_step(s, a, r)
+                lc = self._fused.critic_step(s, a, r, row_offset=row0, global_batch=gb)
             return lc, self._fused.actor_step(s)
         target = r
         if self.gamma > 0.0:
             with torch.no_grad():
-                if self.device.type == "cuda":  # r + gamma (1 - d) Q' in the target kernel's epilogue
+                if self.device.type == "cuda" and self.precision == "bf16":  # r + gamma (1 - d) Q' in one launch
                     target = self._target_kernel().target(s2, r, d, self.gamma)
                 else:
                     target = r + self.gamma * (1.0 - d) * self.target_q(s2)
-        lc = self.critic_step(s, a, target)
+        lc = self.critic_step(s, a, target, row_offset=row0, global_batch=gb)
         la = self.model_actor_fit_step(s)
         if self.tau is not None:
             self.soft_update()
@@ -442,11 +549,12 @@ class DDPG:
     @torch.no_grad()
     def target_q(self, s2):
         """Q'(s', mu'(s')) with the target nets (the online nets when tau is
-        None).  On the GPU one fused MFMA launch (sk_target_q) on weights
-        packed after every change of the nets; on CPU the torch modules."""
+        None).  On the GPU (bf16 kernels) one fused MFMA launch (sk_target_q)
+        on weights packed after every change of the nets; otherwise the torch
+        modules."""
         actor_t = self.target_actor if self.tau is not None else self.model_actor
         critic_t = self.target_critic if self.tau is not None else self.model_critic
-        if self.device.type != "cuda":
+        if self.device.type != "cuda" or self.precision != "bf16":
             critic_t.eval()
             return critic_t(s2, actor_t(s2)).squeeze(-1)
         return self._target_kernel()(s2)
@@ -471,6 +579,12 @@ class DDPG:
         if self._tq is not None:
             self._tq.refresh()
 
+    def optimisers_loaded(self):
+        """after Optimizer.load_state_dict replaced the Adam state tensors:
+        the fused path copies them into its flat buffers and rebinds the views"""
+        if self._fused is not None:
+            self._fused.rebind_optimisers()
+
 
 class SkillshotLearner:
     """Batched self-play DDPG learner (SkillshotLearner.py:13-682 API shape).
@@ -483,7 +597,8 @@ class SkillshotLearner:
 
     def __init__(self, n_envs=1, device="cuda", seed=0, env_offset=0, exploration="param_noise",
                  tick_limit=2000, use_random_start=True, replay_capacity=1 << 20, batch_size=16,
-                 gamma=0.0, tau=None, actor_kernel=True, process_group=None, precision="bf16"):
+                 gamma=0.0, tau=None, actor_kernel=True, process_group=None, precision="bf16",
+                 multi_rank="grad"):
         from .vec_env import VecSkillshotGame
         if precision not in ("bf16", "fp32"):
             raise ValueError("precision must be 'bf16' or 'fp32'")
@@ -510,7 +625,8 @@ class SkillshotLearner:
         self.actor_dir_name, self.critic_dir_name = "actor", "critic"
         self.training_progress_dir_name, self.training_boards_dir_name = "training_progress", "training_boards"
         self.ddpg = DDPG(self.device, seed=seed, batch_size=batch_size, gamma=gamma, tau=tau,
-                         replay_capacity=replay_capacity, process_group=process_group, rank_seed_offset=env_offset)
+                         replay_capacity=replay_capacity, process_group=process_group, rank_seed_offset=env_offset,
+                         multi_rank=multi_rank, precision=precision)
         self.gen = self.ddpg.gen
         self.actor_kernel = None
         if actor_kernel and self.device.type == "cuda":
@@ -684,7 +800,8 @@ class SkillshotLearner:
             obs = out["obs_reset"]
             if self.replay.size >= warmup:
                 for _ in range(updates_per_tick):
-                    stats.append(self.replay_update(batch))
+                    # the fused path returns slots of a loss ring: keep copies
+                    stats.append(tuple(x.detach().clone() for x in self.replay_update(batch)))
             self._refresh_actor_pack()
         return stats
 
@@ -725,6 +842,7 @@ class SkillshotLearner:
         self.model_critic.load_state_dict(d["critic"])
         self.ddpg.optimiser.load_state_dict(d["actor_opt"])
         self.ddpg.critic_optimiser.load_state_dict(d["critic_opt"])
+        self.ddpg.optimisers_loaded()
         self.game_environment.load_state_dict(d["env"])
         if self.ddpg.tau is not None and "target_actor" in d:
             self.ddpg.target_actor.load_state_dict(d["target_actor"])

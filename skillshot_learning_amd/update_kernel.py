@@ -64,8 +64,8 @@ def _offsets(params):
 
 
 class _AdamState:
-    """torch Adam state of one net as flat buffers (views rebound into the
-    optimiser's per-parameter state)."""
+    """Adam state (learner.KerasAdam) of one net as flat buffers (views
+    rebound into the optimiser's per-parameter state)."""
 
     def __init__(self, opt, module, flat):
         params = list(module.parameters())
@@ -75,6 +75,14 @@ class _AdamState:
         self.steps = torch.zeros(len(params), dtype=torch.float32, device=dev)
         g = opt.param_groups[0]
         self.lr, (self.b1, self.b2), self.eps = float(g["lr"]), g["betas"], float(g["eps"])
+        self.bind(opt, module)
+
+    @torch.no_grad()
+    def bind(self, opt, module):
+        """copy whatever state the optimiser holds (e.g. just loaded by
+        Optimizer.load_state_dict) into the flat buffers, then make the
+        optimiser's state views of them again"""
+        params = list(module.parameters())
         for i, (p, off) in enumerate(zip(params, _offsets(params))):
             k = p.numel()
             st = opt.state[p]
@@ -92,7 +100,7 @@ class FusedUpdate:
 
     LOSS_HIST = 1024
 
-    def __init__(self, ddpg, seed=0):
+    def __init__(self, ddpg):
         self.d = ddpg
         self.L = _capi.load()
         dev = ddpg.device
@@ -105,18 +113,22 @@ class FusedUpdate:
         self.tc = flatten_module(ddpg.target_critic) if ddpg.tau is not None else None
         self.sa = _AdamState(ddpg.optimiser, ddpg.model_actor, self.fa)
         self.sc = _AdamState(ddpg.critic_optimiser, ddpg.model_critic, self.fc)
+        # models_fit (the reference rule) has no target nets: it clears this
+        self.soft_update_in_adam = True
         nb = int(self.L.sk_grad_packed_bytes())
         self.gpa = torch.empty(nb, dtype=torch.uint8, device=dev)
         self.gpc = torch.empty(nb, dtype=torch.uint8, device=dev)
         # target nets' packs (the bootstrap target inside the critic step)
         self.gpta = torch.empty(nb, dtype=torch.uint8, device=dev) if self.ta is not None else self.gpa
         self.gptc = torch.empty(nb, dtype=torch.uint8, device=dev) if self.tc is not None else self.gpc
-        self.seed = int(seed) & ((1 << 64) - 1)
-        # dropout call number and loss accumulators [sum (q-y)^2, sum Q] on
-        # device; the Adam launch advances / reads-and-clears them, and writes
-        # the step's loss into a history slot (the returned device scalar
-        # stays valid for LOSS_HIST further steps)
-        self.calls = torch.zeros(1, dtype=torch.int64, device=dev)
+        # Dropout key and call number: the DDPG's (shared with the torch
+        # path; masks keyed by global batch row).  Loss accumulators [sum
+        # (q-y)^2, sum Q] on device; the Adam launch advances the call number,
+        # reads-and-clears the accumulators and writes the step's loss into a
+        # history slot (the returned device scalar stays valid for LOSS_HIST
+        # further steps)
+        self.seed = ddpg.drop_seed
+        self.calls = ddpg.drop_calls
         self.stats = torch.zeros(2, dtype=torch.float32, device=dev)
         self.loss_hist = torch.zeros(2, self.LOSS_HIST, dtype=torch.float32, device=dev)
         self._li = [0, 0]
@@ -126,6 +138,13 @@ class FusedUpdate:
         # the actor's Adam launch when bound (SkillshotLearner binds it)
         self.fwd_pack = None
         self.pack()
+
+    def rebind_optimisers(self):
+        """after the optimisers' state was replaced (load_state_dict): the
+        loaded moments and step counts into the flat buffers the Adam launches
+        read, and the optimiser state views of them again"""
+        self.sa.bind(self.d.optimiser, self.d.model_actor)
+        self.sc.bind(self.d.critic_optimiser, self.d.model_critic)
 
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
@@ -172,17 +191,20 @@ class FusedUpdate:
 
     def _adam(self, part, flat, st, target, stat=None, scale=1.0, out=None, counter=None, packs=None):
         P = flat.numel()
+        if not self.soft_update_in_adam:
+            target = None
+            if packs is not None:
+                packs = PackTargets(packs.param_gpack, None, packs.actor_fwd_pack, packs.ld2, packs.n_out)
         pk = ctypes.byref(packs) if packs is not None else None
         tau = float(self.d.tau) if target is not None else 0.0
         world = self.d.world()
-        if world > 1:  # sum partials -> flat grad -> RCCL mean -> apply
+        if world > 1:  # sum partials -> flat grad -> RCCL sum (losses are global-batch normalised) -> apply
             if self.grad_flat is None or self.grad_flat.numel() < P:
                 self.grad_flat = torch.empty(max(36609, P), dtype=torch.float32, device=self.dev)
             g = self.grad_flat[:P]
             _capi.check(self.L.sk_adam_flat(_p(part), part.shape[0], P, None, _p(g), 0, None, None, None, None,
                                             0.0, 0.0, 0.0, 0.0, None, 0.0, None, 0.0, None, None, self._stream()))
             dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.d.group)
-            g /= world
             _capi.check(self.L.sk_adam_flat_packed(None, 0, P, _p(g), None, 1, _p(flat), _p(st.m), _p(st.v),
                                                    _p(st.steps), st.lr, st.b1, st.b2, st.eps, _p(target), tau,
                                                    _p(stat), float(scale), _p(out), _p(counter), pk, self._stream()))
@@ -193,31 +215,39 @@ class FusedUpdate:
                                                    self._stream()))
 
     @torch.no_grad()
-    def critic_step(self, s, a, target=None, mask_out=None, s2=None, r=None, d=None, gamma=0.0):
+    def critic_step(self, s, a, target=None, mask_out=None, s2=None, r=None, d=None, gamma=0.0, row_offset=0,
+                    global_batch=None):
         """One critic Adam step on MSE(Q(s, a), y), Dropout active; y = target,
         or, given s2 / r / d, the bootstrap y = r + gamma (1 - d) Q'(s2,
-        mu'(s2)) computed inside the same launch from the target nets.
-        Returns the loss (device scalar)."""
+        mu'(s2)) computed inside the same launch from the target nets.  The
+        rows are global batch rows row_offset .. (their Dropout keys) of a
+        global batch of global_batch rows (the loss normaliser; default this
+        batch).  Returns the loss (device scalar; this rank's share)."""
         s, a = s.float().contiguous(), a.float().contiguous()
         B = s.shape[0]
+        gb = B if global_batch is None else int(global_batch)
         part = self._partial(B, self.fc.numel())
         st = self.sc
-        if s2 is not None:
-            s2c, rc_, dc = s2.float().contiguous(), r.float().contiguous(), d.float().contiguous()
-            rc = self.L.sk_critic_grad_bootstrap(
-                _p(self.gpc), _p(s), _p(a), None, _p(s2c), _p(rc_), _p(dc), float(gamma), _p(self.gpta),
-                _p(self.gptc), B, 2.0 / B, self.seed, _p(self.calls), _p(part), _p(st.steps), st.steps.numel(),
-                _p(self.stats[0:1]), _p(mask_out), self._stream())
-        else:
-            y = target.float().contiguous()
-            rc = self.L.sk_critic_grad(_p(self.gpc), _p(s), _p(a), _p(y), B, 2.0 / B, self.seed, _p(self.calls),
-                                       _p(part), _p(st.steps), st.steps.numel(), _p(self.stats[0:1]), _p(mask_out),
-                                       self._stream())
+        rc = self._critic_grad(s, a, target, s2, r, d, gamma, row_offset, gb, part, st.steps, mask_out)
         _capi.check(rc)
         loss = self._loss_slot(0)
-        self._adam(part, self.fc, st, self.tc, stat=self.stats[0:1], scale=1.0 / B, out=loss, counter=self.calls,
+        self._adam(part, self.fc, st, self.tc, stat=self.stats[0:1], scale=1.0 / gb, out=loss, counter=self.calls,
                    packs=self._packs(critic=True))
         return loss
+
+    def _critic_grad(self, s, a, target, s2, r, d, gamma, row_offset, gb, part, steps, mask_out, stat=True):
+        n_steps = steps.numel() if steps is not None else 0
+        statp = _p(self.stats[0:1]) if stat else None
+        if s2 is not None:
+            s2c, rc_, dc = s2.float().contiguous(), r.float().contiguous(), d.float().contiguous()
+            return self.L.sk_critic_grad_bootstrap(
+                _p(self.gpc), _p(s), _p(a), None, _p(s2c), _p(rc_), _p(dc), float(gamma), _p(self.gpta),
+                _p(self.gptc), s.shape[0], int(row_offset), 2.0 / gb, self.seed, _p(self.calls), _p(part), _p(steps),
+                n_steps, statp, _p(mask_out), self._stream())
+        y = target.float().contiguous()
+        return self.L.sk_critic_grad(_p(self.gpc), _p(s), _p(a), _p(y), s.shape[0], int(row_offset), 2.0 / gb,
+                                     self.seed, _p(self.calls), _p(part), _p(steps), n_steps, statp, _p(mask_out),
+                                     self._stream())
 
     @torch.no_grad()
     def actor_step(self, s):
@@ -236,29 +266,26 @@ class FusedUpdate:
         return loss
 
     @torch.no_grad()
-    def grads(self, which, s, a=None, target=None, mask_out=None, s2=None, r=None, d=None, gamma=0.0):
+    def grads(self, which, s, a=None, target=None, mask_out=None, s2=None, r=None, d=None, gamma=0.0, row_offset=0,
+              global_batch=None):
         """Test hook: the flat gradient the kernels compute, without stepping
-        (the Adam step counters are not touched)."""
+        (the Adam step counters are not touched; the critic's Dropout call
+        number advances as a step would)."""
         B = s.shape[0]
         if which == "critic":
-            flat, st = self.fc, self.sc
+            flat = self.fc
             part = self._partial(B, flat.numel())
+            gb = B if global_batch is None else int(global_batch)
+            rc = self._critic_grad(s.float().contiguous(), a.float().contiguous(), target, s2, r, d, gamma,
+                                   row_offset, gb, part, None, mask_out, stat=False)
+            _capi.check(rc)
             self.calls.add_(1)
-            if s2 is not None:
-                rc = self.L.sk_critic_grad_bootstrap(
-                    _p(self.gpc), _p(s.contiguous()), _p(a.contiguous()), None, _p(s2.contiguous()),
-                    _p(r.contiguous()), _p(d.contiguous()), float(gamma), _p(self.gpta), _p(self.gptc), B, 2.0 / B,
-                    self.seed, _p(self.calls), _p(part), None, 0, None, _p(mask_out), self._stream())
-            else:
-                rc = self.L.sk_critic_grad(_p(self.gpc), _p(s.contiguous()), _p(a.contiguous()),
-                                           _p(target.contiguous()), B, 2.0 / B, self.seed, _p(self.calls), _p(part),
-                                           None, 0, None, _p(mask_out), self._stream())
         else:
-            flat, st = self.fa, self.sa
+            flat = self.fa
             part = self._partial(B, flat.numel())
             rc = self.L.sk_actor_grad(_p(self.gpa), _p(self.gpc), _p(s.contiguous()), B, 1.0, _p(part), None, 0,
                                       None, self._stream())
-        _capi.check(rc)
+            _capi.check(rc)
         g = torch.empty_like(flat)
         _capi.check(self.L.sk_adam_flat(_p(part), part.shape[0], flat.numel(), None, _p(g), 0, None, None, None, None,
                                         0.0, 0.0, 0.0, 0.0, None, 0.0, None, 0.0, None, None, self._stream()))

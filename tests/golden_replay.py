@@ -103,7 +103,10 @@ def replay(engine, d, obs_tol=OBS_TOL, check_every=1):
     engine: object with load(state_arrays), arrays() -> state arrays (host numpy),
     step(actions[2,E,2], tick_limit) -> dict(obs[2,E,12], reward[2,E], done[E], winner[E]),
     move_direction(pid, speeds[E]), move_look(pid, angles[E]), shoot(pid, mask[E]),
-    game_tick(), observe() -> (obs[2,E,12], reward[2,E]).
+    game_tick(), observe() -> (obs[2,E,12], reward[2,E]); optionally
+    reward_simple() -> reward[2,E] of calculate_rewards_simple
+    (SkillshotLearner.py:590-603) on the current state, held to the fixture's
+    `reward_simple` series (the reference's own values) at every checked tick.
     Returns the number of env-ticks compared.
     """
     E = d["pos"].shape[0]
@@ -114,6 +117,9 @@ def replay(engine, d, obs_tol=OBS_TOL, check_every=1):
     act0 = np.ones(E, bool)
     compare_obs(obs0, d["obs"][:, 0], act0, "t=0", obs_tol)
     compare_reward(rew0, d["reward"][:, 0], act0, "t=0", obs_tol)
+    simple = hasattr(engine, "reward_simple") and "reward_simple" in d
+    if simple:
+        compare_reward(engine.reward_simple(), d["reward_simple"][:, 0], act0, "simple t=0", obs_tol)
     protocol = str(d["protocol"])
     compared = 0
     for t in range(T):
@@ -133,6 +139,9 @@ def replay(engine, d, obs_tol=OBS_TOL, check_every=1):
             compare_state(engine.arrays(), state_at(d, t + 1), active, f"{d['scenario']} t={t + 1}")
             compare_obs(obs, d["obs"][:, t + 1], active, f"{d['scenario']} t={t + 1}", obs_tol)
             compare_reward(rew, d["reward"][:, t + 1], active, f"{d['scenario']} t={t + 1}", obs_tol)
+            if simple:
+                compare_reward(engine.reward_simple(), d["reward_simple"][:, t + 1], active,
+                               f"{d['scenario']} simple t={t + 1}", obs_tol)
             if protocol == "learner":
                 live = d["live"][:, t + 1].astype(bool)
                 ticks = d["ticks"][:, t + 1]

@@ -66,6 +66,9 @@ class GpuEngine:
         o, r = self.g.observe()
         return o.cpu().numpy(), r.cpu().numpy()
 
+    def reward_simple(self):
+        return self.g.observe(reward="simple")[1].cpu().numpy()
+
 
 @pytest.fixture(params=[0, 1, 2], ids=["lane_per_env", "player_split", "fp32_fast"])
 def step_variant(request, monkeypatch):

@@ -44,12 +44,14 @@ def test_actor_step_is_minus_sum_q():
     q = d.model_critic(s, ref(s)).sum()
     grads = torch.autograd.grad(-q, list(ref.parameters()))
     d.model_actor_fit_step(s)
-    # first Adam step moves every parameter with a non-zero grad by ~lr*sign(g)
+    # first Keras Adam step: m = 0.1 g, v = 0.001 g^2, alpha = lr sqrt(0.001) / 0.1,
+    # so |delta| = lr |g| / (|g| + eps / sqrt(0.001)) (epsilon-hat, not torch's)
     for (name, p), g in zip(d.model_actor.named_parameters(), grads):
         delta = p.detach() - ref.state_dict()[name]
-        nz = g.abs() > 1e-5
+        nz = g.abs() > 1e-6
         assert torch.all(torch.sign(delta[nz]) == -torch.sign(g[nz]))
-        assert torch.allclose(delta[nz].abs(), torch.full_like(delta[nz], 1e-3), rtol=0.02)
+        want = 1e-3 * g[nz].abs() / (g[nz].abs() + 1e-7 / math.sqrt(1e-3))
+        assert torch.allclose(delta[nz].abs(), want, rtol=2e-3, atol=1e-9)
     for p, b in zip(d.model_critic.parameters(), crit_before):
         assert torch.equal(p.detach(), b)
     assert d.optimiser.defaults["eps"] == 1e-7 and d.optimiser.defaults["lr"] == 1e-3

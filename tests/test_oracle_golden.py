@@ -34,6 +34,9 @@ class OracleEngine:
     def observe(self):
         return self.s.observe()
 
+    def reward_simple(self):
+        return self.s.observe(reward_kind=1)[1]
+
 
 @pytest.mark.parametrize("name", gr.fixture_names())
 def test_oracle_matches_reference(oracle_mod, name):
