@@ -891,6 +891,10 @@ class TickGraph:
                 self._obs[0].copy_(self._obs[1])
                 self._cur = 0
         self.stream.synchronize()
+        # capture at a synced step counter (both device slots current, host
+        # parity 0): run() syncs before replaying, so eager steps between
+        # replays cannot leave the captured slot stale
+        g.sync_step_counter(ctypes.c_void_p(self.stream.cuda_stream))
         self.graph = torch.cuda.CUDAGraph()
         self.graph.register_generator_state(L.gen)
         mirror = L.replay.total  # capture records the inserts without running them
@@ -934,6 +938,7 @@ class TickGraph:
         cur = torch.cuda.current_stream(self.L.device)
         self.stream.wait_stream(cur)
         with torch.cuda.stream(self.stream):  # replay() launches on the current stream
+            self.L.game_environment.sync_step_counter(ctypes.c_void_p(self.stream.cuda_stream))
             for _ in range(n):
                 self.graph.replay()
         cur.wait_stream(self.stream)

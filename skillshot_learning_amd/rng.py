@@ -47,7 +47,10 @@ def dropout_keep(seed, call, row0, rows, units=256, device="cpu"):
     r = torch.arange(row0, row0 + rows, dtype=torch.int64, device=device).view(-1, 1)
     u = torch.arange(units, dtype=torch.int64, device=device).view(1, -1)
     grp = (r >> 2).expand(rows, units)
-    call, seed = int(call), int(seed)
+    seed = int(seed)
+    if not torch.is_tensor(call):
+        call = torch.tensor(int(call), dtype=torch.int64)
+    call = call.to(device=device, dtype=torch.int64).reshape(())  # device counter: no host sync, capturable
     w = philox4x32_10(grp, u.expand(rows, units), call & _U32, (call >> 32) & _U32, seed & _U32, (seed >> 32) & _U32)
     words = torch.stack(w, -1)  # [rows, units, 4]
     pick = (r & 3).expand(rows, units).unsqueeze(-1)

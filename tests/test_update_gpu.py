@@ -321,3 +321,55 @@ def test_fused_update_two_ranks_gloo():
     assert np.array_equal(out[0][1], out[1][1])  # all-reduced gradients: identical steps
     assert np.isfinite(out[0][1]).all()
     assert not np.array_equal(out[0][1][-36609:], out[0][0])  # the target critic moved (soft update)
+
+
+def test_critic_grad_split_rows_equal_whole_batch(mods):
+    """Dropout keyed by global row (row_offset) and the loss normalised by the
+    global batch: the gradients of two row ranges sum to the whole batch's
+    (what the multi-rank all-reduce relies on)."""
+    learner = mods
+    d = _ddpg(learner, seed=6)
+    s, a = _obs(512), torch.rand(512, 2, device="cuda") * 2 - 1
+    y = torch.randn(512, device="cuda")
+    c0 = d._fused.calls.clone()
+    whole = d._fused.grads("critic", s, a, y)
+    parts = []
+    for lo, hi in ((0, 192), (192, 512)):
+        d._fused.calls.copy_(c0)
+        parts.append(d._fused.grads("critic", s[lo:hi], a[lo:hi], y[lo:hi], row_offset=lo, global_batch=512))
+    tot = parts[0] + parts[1]
+    assert (tot - whole).norm() <= 1e-5 * whole.norm(), float((tot - whole).norm() / whole.norm())
+
+
+def test_load_state_dict_rebinds_fused_adam(mods):
+    """after load_state_dict the fused Adam launches continue from
+    the LOADED moments and step counts (the optimiser's state tensors are
+    views of the flat buffers the kernels read)."""
+    learner = mods
+    L = learner.SkillshotLearner(n_envs=256, device="cuda", seed=12, gamma=0.9, tau=0.05, replay_capacity=1 << 14)
+    L.train_ticks(6, batch=256)
+    sd = {k: ({kk: (vv.cpu().clone() if torch.is_tensor(vv) else vv) for kk, vv in v.items()}
+              if isinstance(v, dict) and k not in ("actor_opt", "critic_opt") else v)
+          for k, v in L.state_dict().items()}
+    import copy
+    sd["actor_opt"] = copy.deepcopy(L.ddpg.optimiser.state_dict())
+    sd["critic_opt"] = copy.deepcopy(L.ddpg.critic_optimiser.state_dict())
+    saved_m = L.ddpg._fused.sc.m.clone()
+    saved_steps = L.ddpg._fused.sc.steps.clone()
+    L.train_ticks(3, batch=256)
+    torch.cuda.synchronize()
+    assert not torch.equal(L.ddpg._fused.sc.m, saved_m)
+    L.load_state_dict(sd)
+    fu = L.ddpg._fused
+    assert torch.equal(fu.sc.m, saved_m) and torch.equal(fu.sc.steps, saved_steps)
+    p0 = next(L.model_critic.parameters())
+    assert L.ddpg.critic_optimiser.state[p0]["exp_avg"].data_ptr() == fu.sc.m.data_ptr()
+    # the next fused step continues from the loaded state: m' = m + (g - m)(1 - b1), t' = t + 1
+    s, a, y = _obs(256), torch.rand(256, 2, device="cuda") * 2 - 1, torch.randn(256, device="cuda")
+    c0 = fu.calls.clone()
+    g = fu.grads("critic", s, a, y)
+    fu.calls.copy_(c0)
+    L.ddpg.critic_step(s, a, y)
+    torch.cuda.synchronize()
+    assert torch.allclose(fu.sc.m, saved_m + (g - saved_m) * 0.1, rtol=1e-5, atol=1e-8)
+    assert torch.equal(fu.sc.steps, saved_steps + 1)
