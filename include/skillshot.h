@@ -384,6 +384,39 @@ int sk_adam_flat_packed(const float* partials, int32_t n_partials, int32_t n_par
                         float tau, float* stat_acc, float stat_scale, float* stat_out, int64_t* counter,
                         const sk_pack_targets* packs, void* stream);
 
+/* --- the learner at the reference's precision (A13, A16, F1, F2) ----------
+ * The same nets and update as above with fp32 operands and fp32 accumulation
+ * (v_mfma_f32_32x32x2_f32: exact f32 products), i.e. Keras' fp32 Dense math
+ * (SkillshotLearner.py:70-121, 386-443).  No packing: every kernel reads a
+ * net's flat fp32 parameter vector in torch parameters() order (W1 [256][12],
+ * b1 [256], W2 [128][ld2], b2 [128], W3 [n_out][128], b3 [n_out]; actor ld2 =
+ * 256, n_out = 2; critic ld2 = 258, n_out = 1).  Gradients leave as
+ * float[sk_update_partials_f32(batch)][n_params] partials summed (and Adam
+ * applied) by sk_adam_flat with packs = NULL.
+ *   sk_actor_forward_f32  obs float[rows][12] -> actions float[rows][2]
+ *                         (model_act*, :215-281); noise_sd != 0 samples the
+ *                         parameter noise w -> w (1 + noise_sd N(0,1)) per row
+ *                         by local reparameterisation, keyed by (seed, row,
+ *                         unit, call); call_counter (nullable; uint64[2] =
+ *                         {call, 0}) is read and advanced on device as by
+ *                         sk_actor_forward_advance.
+ *   sk_critic_grad_f32    as sk_critic_grad_bootstrap (target_actor_flat NULL:
+ *                         y = targets; else y = rewards + gamma (1 - done)
+ *                         Q'(next_obs, mu'(next_obs)) from the target nets).
+ *   sk_actor_grad_f32     as sk_actor_grad. */
+int64_t sk_update_partials_f32(int64_t batch);
+int sk_actor_forward_f32(const float* actor_flat, const float* obs, float* actions, int64_t rows, float noise_sd,
+                         uint64_t seed, uint64_t* call_counter, void* stream);
+int sk_critic_grad_f32(const float* critic_flat, const float* obs, const float* actions, const float* targets,
+                       const float* next_obs, const float* rewards, const float* done, float gamma,
+                       const float* target_actor_flat, const float* target_critic_flat, int64_t batch,
+                       int64_t row_offset, float grad_scale, uint64_t seed, const int64_t* call_counter,
+                       float* partials, float* step_counters, int32_t n_steps, float* loss_sum,
+                       uint8_t* dropout_mask, void* stream);
+int sk_actor_grad_f32(const float* actor_flat, const float* critic_flat, const float* obs, int64_t batch,
+                      float loss_scale, float* partials, float* step_counters, int32_t n_steps, float* q_sum,
+                      void* stream);
+
 #ifdef __cplusplus
 }
 #endif

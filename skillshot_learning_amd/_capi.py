@@ -33,6 +33,7 @@ EXPORTS = (
     "sk_adam_flat_packed",
     "sk_target_y", "sk_replay_insert", "sk_replay_sample", "sk_grad_pack_flat",
     "sk_critic_grad_bootstrap",
+    "sk_update_partials_f32", "sk_actor_forward_f32", "sk_critic_grad_f32", "sk_actor_grad_f32",
 )
 
 
@@ -134,6 +135,11 @@ def load(build_if_missing=True):
         "sk_grad_pack_flat": ([P, P, P, P, i32, P], ctypes.c_int),
         "sk_critic_grad_bootstrap": ([P, P, P, P, P, P, P, f32, P, P, i64, i64, f32, u64, P, P, P, i32, P, P, P],
                                      ctypes.c_int),
+        "sk_update_partials_f32": ([i64], ctypes.c_int64),
+        "sk_actor_forward_f32": ([P, P, P, i64, f32, u64, P, P], ctypes.c_int),
+        "sk_critic_grad_f32": ([P, P, P, P, P, P, P, f32, P, P, i64, i64, f32, u64, P, P, P, i32, P, P, P],
+                               ctypes.c_int),
+        "sk_actor_grad_f32": ([P, P, P, i64, f32, P, P, i32, P, P], ctypes.c_int),
     }
     for name, (argt, rest) in sig.items():
         fn = getattr(L, name)

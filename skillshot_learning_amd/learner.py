@@ -602,8 +602,6 @@ class SkillshotLearner:
         from .vec_env import VecSkillshotGame
         if precision not in ("bf16", "fp32"):
             raise ValueError("precision must be 'bf16' or 'fp32'")
-        if precision == "fp32":
-            raise NotImplementedError("fp32 learner kernels are not built yet")
         self.precision = precision
         self.device = torch.device(device)
         self.game_environment = VecSkillshotGame(n_envs, device=self.device, seed=seed, env_offset=env_offset,
@@ -630,10 +628,13 @@ class SkillshotLearner:
         self.gen = self.ddpg.gen
         self.actor_kernel = None
         if actor_kernel and self.device.type == "cuda":
-            from .actor_kernel import ActorKernel
-            self.actor_kernel = ActorKernel(self.model_actor, seed=seed * 1000003 + env_offset)
-            if self.ddpg._fused is not None:  # the actor's Adam launch writes the forward pack too
-                self.ddpg._fused.fwd_pack = self.actor_kernel.buf
+            from .actor_kernel import ActorKernel, ActorKernel32
+            if precision == "fp32":  # reads the actor's flat fp32 parameters: nothing to repack
+                self.actor_kernel = ActorKernel32(self.model_actor, seed=seed * 1000003 + env_offset)
+            else:
+                self.actor_kernel = ActorKernel(self.model_actor, seed=seed * 1000003 + env_offset)
+                if self.ddpg._fused is not None:  # the actor's Adam launch writes the forward pack too
+                    self.ddpg._fused.fwd_pack = self.actor_kernel.buf
         self.progress = dict(epoch_ticks=[], epoch_winner=[])
 
     # reference attribute names

@@ -111,6 +111,9 @@ class FusedUpdate:
         self.fc = flatten_module(ddpg.model_critic)
         self.ta = flatten_module(ddpg.target_actor) if ddpg.tau is not None else None
         self.tc = flatten_module(ddpg.target_critic) if ddpg.tau is not None else None
+        # fp32: the kernels of csrc/sk_learn32.hip read the flat parameter
+        # vectors themselves (no packs); bf16: sk_update.hip's MFMA packs
+        self.f32 = getattr(ddpg, "precision", "bf16") == "fp32"
         self.sa = _AdamState(ddpg.optimiser, ddpg.model_actor, self.fa)
         self.sc = _AdamState(ddpg.critic_optimiser, ddpg.model_critic, self.fc)
         # models_fit (the reference rule) has no target nets: it clears this
@@ -153,7 +156,7 @@ class FusedUpdate:
         key = (batch, n_params)
         t = self._partials.get(key)
         if t is None:
-            g = int(self.L.sk_update_partials(batch))
+            g = int(self.L.sk_update_partials_f32(batch) if self.f32 else self.L.sk_update_partials(batch))
             t = self._partials[key] = torch.empty((g, n_params), dtype=torch.float32, device=self.dev)
         return t
 
@@ -171,6 +174,8 @@ class FusedUpdate:
         """full packs of every net from its parameters (at start, and after
         parameters change outside the Adam launches, e.g. load_state_dict);
         between steps each Adam launch rewrites the entries it produces"""
+        if self.f32:
+            return
         jobs = [(self.fa, 256, 2, self.gpa), (self.fc, 258, 1, self.gpc)]
         if self.ta is not None:
             jobs += [(self.ta, 256, 2, self.gpta), (self.tc, 258, 1, self.gptc)]
@@ -183,6 +188,8 @@ class FusedUpdate:
 
     def _packs(self, critic):
         """the packs the Adam launch of a step keeps current"""
+        if self.f32:
+            return None
         if critic:
             return PackTargets(self.gpc.data_ptr(), self.gptc.data_ptr() if self.tc is not None else None, None,
                                258, 1)
@@ -238,6 +245,18 @@ class FusedUpdate:
     def _critic_grad(self, s, a, target, s2, r, d, gamma, row_offset, gb, part, steps, mask_out, stat=True):
         n_steps = steps.numel() if steps is not None else 0
         statp = _p(self.stats[0:1]) if stat else None
+        if self.f32:
+            boot = s2 is not None
+            ta = (self.ta if self.ta is not None else self.fa) if boot else None
+            tc = (self.tc if self.tc is not None else self.fc) if boot else None
+            s2c = s2.float().contiguous() if boot else None
+            rc_ = r.float().contiguous() if boot else None
+            dc = d.float().contiguous() if boot else None
+            y = None if boot else target.float().contiguous()
+            return self.L.sk_critic_grad_f32(
+                _p(self.fc), _p(s), _p(a), _p(y), _p(s2c), _p(rc_), _p(dc), float(gamma), _p(ta), _p(tc), s.shape[0],
+                int(row_offset), 2.0 / gb, self.seed, _p(self.calls), _p(part), _p(steps), n_steps, statp,
+                _p(mask_out), self._stream())
         if s2 is not None:
             s2c, rc_, dc = s2.float().contiguous(), r.float().contiguous(), d.float().contiguous()
             return self.L.sk_critic_grad_bootstrap(
@@ -257,13 +276,20 @@ class FusedUpdate:
         B = s.shape[0]
         part = self._partial(B, self.fa.numel())
         st = self.sa
-        rc = self.L.sk_actor_grad(_p(self.gpa), _p(self.gpc), _p(s), B, 1.0, _p(part), _p(st.steps),
-                                  st.steps.numel(), _p(self.stats[1:]), self._stream())
+        rc = self._actor_grad(s, part, st.steps, self.stats[1:])
         _capi.check(rc)
         loss = self._loss_slot(1)
         self._adam(part, self.fa, st, self.ta, stat=self.stats[1:], scale=-1.0, out=loss,
                    packs=self._packs(critic=False))
         return loss
+
+    def _actor_grad(self, s, part, steps, stat):
+        n = steps.numel() if steps is not None else 0
+        if self.f32:
+            return self.L.sk_actor_grad_f32(_p(self.fa), _p(self.fc), _p(s), s.shape[0], 1.0, _p(part), _p(steps), n,
+                                            _p(stat), self._stream())
+        return self.L.sk_actor_grad(_p(self.gpa), _p(self.gpc), _p(s), s.shape[0], 1.0, _p(part), _p(steps), n,
+                                    _p(stat), self._stream())
 
     @torch.no_grad()
     def grads(self, which, s, a=None, target=None, mask_out=None, s2=None, r=None, d=None, gamma=0.0, row_offset=0,
@@ -283,9 +309,7 @@ class FusedUpdate:
         else:
             flat = self.fa
             part = self._partial(B, flat.numel())
-            rc = self.L.sk_actor_grad(_p(self.gpa), _p(self.gpc), _p(s.contiguous()), B, 1.0, _p(part), None, 0,
-                                      None, self._stream())
-            _capi.check(rc)
+            _capi.check(self._actor_grad(s.float().contiguous(), part, None, None))
         g = torch.empty_like(flat)
         _capi.check(self.L.sk_adam_flat(_p(part), part.shape[0], flat.numel(), None, _p(g), 0, None, None, None, None,
                                         0.0, 0.0, 0.0, 0.0, None, 0.0, None, 0.0, None, None, self._stream()))

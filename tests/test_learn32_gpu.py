@@ -1,0 +1,222 @@
+"""The learner at the reference's precision on the GPU (csrc/sk_learn32.hip,
+fp32 operands on v_mfma_f32_32x32x2_f32) against the numpy fp64 restatement
+of the reference's Keras arithmetic (oracle/keras_ref.py): critic and actor
+gradients (SkillshotLearner.py:386-443), the bootstrap target, the actor
+forward (:70-96) and its parameter noise (:245-281), and whole updates with
+Keras Adam.
+
+Bars: gradients within GRAD_REL = 1e-5 relative Frobenius per parameter
+tensor; actor outputs within 1e-5 absolute; parameters after Adam steps within
+PARAM_ABS = 1e-5 (1 % of one lr-sized Adam step).  Parity with Keras itself
+stays unpinned (TensorFlow is absent)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+GRAD_REL = 1e-5
+PARAM_ABS = 1e-5
+
+
+@pytest.fixture(scope="module")
+def mods():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from oracle import keras_ref
+    from skillshot_learning_amd import learner
+    return learner, keras_ref
+
+
+def _ddpg(learner, seed=0, scale=2.0, tau=None, gamma=0.0):
+    d = learner.DDPG("cuda", seed=seed, tau=tau, gamma=gamma, fused_update=True, precision="fp32")
+    with torch.no_grad():
+        for m in (d.model_actor, d.model_critic):
+            for l in (m.l1, m.l2, m.l3):
+                l.weight.mul_(scale)
+                l.bias.normal_(0, 0.1)
+        if tau is not None:
+            for dst, src in ((d.target_actor, d.model_actor), (d.target_critic, d.model_critic)):
+                for pd, ps in zip(dst.parameters(), src.parameters()):
+                    pd.copy_(ps * 1.1)
+    return d
+
+
+def _obs(rows, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    return torch.rand(rows, 12, device="cuda", generator=g) * torch.tensor(
+        [1, 1, 1, 1, 9.8, 1, 1, 1, 1, 9.8, 1, 1.0], device="cuda")
+
+
+def _np(t):
+    return t.detach().double().cpu().numpy()
+
+
+def _check_flat(flat, module, want, rel=GRAD_REL):
+    off = 0
+    for name, p in module.named_parameters():
+        k = p.numel()
+        got = flat[off:off + k].view_as(p).double().cpu().numpy()
+        off += k
+        err, den = np.linalg.norm(got - want[name]), np.linalg.norm(want[name])
+        assert err <= rel * den + 1e-9, (name, err, den, err / max(den, 1e-30))
+
+
+@pytest.mark.parametrize("rows", [1, 37, 256, 4096 + 17])
+def test_critic_grad_f32_matches_keras(mods, rows):
+    learner, kr = mods
+    d = _ddpg(learner, seed=1)
+    s, a = _obs(rows, 1), torch.rand(rows, 2, device="cuda") * 2 - 1
+    y = torch.randn(rows, device="cuda")
+    mask = torch.zeros(rows, 256, dtype=torch.uint8, device="cuda")
+    g = d._fused.grads("critic", s, a, y, mask_out=mask)
+    torch.cuda.synchronize()
+    if rows >= 256:
+        assert abs(mask.float().mean().item() - 0.8) < 0.02
+    want, _ = kr.critic_grads(kr.from_module(d.model_critic), _np(s), _np(a), _np(y), _np(mask))
+    _check_flat(g, d.model_critic, want)
+
+
+@pytest.mark.parametrize("rows", [37, 4096 + 17])
+def test_critic_grad_f32_bootstrap_matches_keras(mods, rows):
+    learner, kr = mods
+    d = _ddpg(learner, seed=4, tau=0.05, gamma=0.9)
+    s, a = _obs(rows, 2), torch.rand(rows, 2, device="cuda") * 2 - 1
+    s2, r = _obs(rows, 3), torch.randn(rows, device="cuda")
+    done = (torch.rand(rows, device="cuda") < 0.2).float()
+    mask = torch.zeros(rows, 256, dtype=torch.uint8, device="cuda")
+    g = d._fused.grads("critic", s, a, s2=s2, r=r, d=done, gamma=0.9, mask_out=mask)
+    y = kr.target_y(kr.from_module(d.target_actor), kr.from_module(d.target_critic), _np(s2), _np(r), _np(done), 0.9)
+    want, _ = kr.critic_grads(kr.from_module(d.model_critic), _np(s), _np(a), y, _np(mask))
+    # the target adds an fp32 forward of two nets ahead of the gradient: 2e-5
+    _check_flat(g, d.model_critic, want, rel=2e-5)
+
+
+@pytest.mark.parametrize("rows", [1, 37, 256, 4096 + 17])
+def test_actor_grad_f32_matches_keras(mods, rows):
+    learner, kr = mods
+    d = _ddpg(learner, seed=2)
+    s = _obs(rows, 4)
+    g = d._fused.grads("actor", s)
+    want, _ = kr.actor_grads(kr.from_module(d.model_actor), kr.from_module(d.model_critic), _np(s))
+    _check_flat(g, d.model_actor, want)
+
+
+def test_critic_grad_f32_split_rows_equal_whole(mods):
+    learner, _ = mods
+    d = _ddpg(learner, seed=6)
+    s, a, y = _obs(512, 5), torch.rand(512, 2, device="cuda") * 2 - 1, torch.randn(512, device="cuda")
+    c0 = d._fused.calls.clone()
+    whole = d._fused.grads("critic", s, a, y)
+    tot = torch.zeros_like(whole)
+    for lo, hi in ((0, 200), (200, 512)):
+        d._fused.calls.copy_(c0)
+        tot += d._fused.grads("critic", s[lo:hi], a[lo:hi], y[lo:hi], row_offset=lo, global_batch=512)
+    assert (tot - whole).norm() <= 1e-6 * whole.norm()
+
+
+@pytest.mark.parametrize("rows", [1, 33, 8192])
+def test_actor_forward_f32_matches_keras(mods, rows):
+    learner, kr = mods
+    from skillshot_learning_amd.actor_kernel import ActorKernel32
+    d = _ddpg(learner, seed=7)
+    k = ActorKernel32(d.model_actor, seed=3)
+    s = _obs(rows, 6)
+    out = k(s)
+    want, _ = kr.actor_forward(kr.from_module(d.model_actor), _np(s))
+    assert np.abs(_np(out) - want).max() <= 1e-5
+
+
+def test_actor_forward_f32_param_noise_distribution(mods):
+    """model_act_param_noise (:245-281) per row: the kernel's outputs for one
+    state repeated over 32,768 rows against explicit weight noise w (1 +
+    0.5 N(0,1)) drawn per sample in fp64 (two-sample KS, moments); the device
+    call counter advances once per launch and changes the draw."""
+    learner, _ = mods
+    from skillshot_learning_amd.actor_kernel import ActorKernel32
+    d = _ddpg(learner, seed=8, scale=4.0)
+    k = ActorKernel32(d.model_actor, seed=11)
+    n = 32768
+    x = _obs(1, 7).expand(n, 12).contiguous()
+    got = k(x, noise_sd=0.5)
+    got2 = k(x, noise_sd=0.5)
+    torch.cuda.synchronize()
+    assert int(k._ctr[0]) == 2 and int(k._ctr[1]) == 0
+    assert not torch.equal(got, got2)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    a = d.model_actor
+    outs = []
+    with torch.no_grad():
+        for _ in range(n // 2048):
+            h = x[:2048].double()
+            for j, l in enumerate((a.l1, a.l2, a.l3)):
+                W = l.weight.double().unsqueeze(0) * (1 + 0.5 * torch.randn((2048,) + tuple(l.weight.shape),
+                                                                             device="cuda", generator=g,
+                                                                             dtype=torch.float64))
+                b = l.bias.double().unsqueeze(0) * (1 + 0.5 * torch.randn((2048,) + tuple(l.bias.shape),
+                                                                           device="cuda", generator=g,
+                                                                           dtype=torch.float64))
+                h = torch.einsum("boi,bi->bo", W, h) + b
+                h = torch.tanh(h) if j == 2 else torch.relu(h)
+            outs.append(h)
+    ex = torch.cat(outs).float().double().cpu()  # rounded like the kernel's: tanh saturates to exactly +-1 in fp32
+    got = got.double().cpu()
+    for j in range(2):
+        m1, m2 = float(got[:, j].mean()), float(ex[:, j].mean())
+        s1, s2 = float(got[:, j].std()), float(ex[:, j].std())
+        assert abs(m1 - m2) < 5 * max(s1, s2) / math.sqrt(n) + 1e-3, (j, m1, m2)
+        assert abs(s1 - s2) / max(s1, s2) < 0.04, (j, s1, s2)
+        a_s, b_s = torch.sort(got[:, j]).values, torch.sort(ex[:, j]).values
+        grid = torch.linspace(float(min(a_s[0], b_s[0])), float(max(a_s[-1], b_s[-1])), 400, dtype=torch.float64)
+        fa = torch.searchsorted(a_s, grid).double() / n
+        fb = torch.searchsorted(b_s, grid).double() / n
+        assert float((fa - fb).abs().max()) < 1.95 * math.sqrt(2 / n) * 1.3
+
+
+def test_f32_replay_updates_match_keras(mods):
+    """three fused fp32 replay updates (bootstrap target, critic step, actor
+    step, Keras Adam, soft update) against the restatement step by step"""
+    learner, kr = mods
+    from skillshot_learning_amd import rng
+    d = _ddpg(learner, seed=5, tau=0.05, gamma=0.9)
+    A, C = kr.from_module(d.model_actor), kr.from_module(d.model_critic)
+    TA, TC = kr.from_module(d.target_actor), kr.from_module(d.target_critic)
+    oa, oc = kr.Adam(A), kr.Adam(C)
+    for it in range(3):
+        s, a = _obs(256, 20 + it), torch.rand(256, 2, device="cuda") * 2 - 1
+        r, s2 = torch.randn(256, device="cuda"), _obs(256, 30 + it)
+        dn = (torch.rand(256, device="cuda") < 0.2).float()
+        keep = rng.dropout_keep(d.drop_seed, int(d.drop_calls), 0, 256).double().numpy()
+        y = kr.target_y(TA, TC, _np(s2), _np(r), _np(dn), 0.9)
+        gc, _ = kr.critic_grads(C, _np(s), _np(a), y, keep)
+        C = oc.step(C, gc)
+        ga, _ = kr.actor_grads(A, C, _np(s))
+        A = oa.step(A, ga)
+        TA, TC = kr.soft_update(TA, A, 0.05), kr.soft_update(TC, C, 0.05)
+        d.update_batch(s, a, r, s2, dn)
+        torch.cuda.synchronize()
+        for mod, ref in ((d.model_critic, C), (d.model_actor, A), (d.target_critic, TC), (d.target_actor, TA)):
+            for name, p in mod.named_parameters():
+                err = np.abs(_np(p) - ref[name]).max()
+                assert err <= PARAM_ABS, (it, name, err)
+
+
+def test_f32_learner_tick_graph(mods):
+    """config 3 at the reference's precision: the captured learner tick with
+    the fp32 kernels (actor forward with parameter noise, fused step, replay,
+    fp32 critic / actor steps) runs, trains and stays finite"""
+    learner, _ = mods
+    L = learner.SkillshotLearner(n_envs=4096, device="cuda", seed=23, exploration="param_noise", gamma=0.99,
+                                 tau=0.005, replay_capacity=1 << 20, precision="fp32")
+    assert L.ddpg._fused.f32
+    tg = L.tick_graph(batch=256, ticks_per_graph=2, warmup=2)
+    w0 = [p.clone() for p in L.model_actor.parameters()]
+    c0 = int(L.actor_kernel._ctr[0])
+    tg.run(50)
+    torch.cuda.synchronize()
+    assert int(L.actor_kernel._ctr[0]) == c0 + 100  # one noise draw per tick
+    assert all(bool(torch.isfinite(p).all()) for m in (L.model_actor, L.model_critic) for p in m.parameters())
+    assert any((p - q).abs().max() > 0 for p, q in zip(L.model_actor.parameters(), w0))
+    assert bool(torch.isfinite(tg.act).all()) and float(tg.act.abs().max()) <= 1.0
