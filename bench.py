@@ -67,6 +67,9 @@ def parse():
     p.add_argument("--no-full", action="store_true", help="skip the full-contract (obs + reward) tick leg")
     p.add_argument("--no-learner", action="store_true", help="skip the DDPG-in-the-loop legs")
     p.add_argument("--learner-ticks", type=int, default=200)
+    p.add_argument("--learner-timeout", type=float, default=240.0,
+                   help="seconds per multi-rank learner leg (run in child processes)")
+    p.add_argument("--learner-child", default=None, help=argparse.SUPPRESS)
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_k_step.json"))
     return p.parse_args()
 
@@ -278,7 +281,8 @@ def weak_rate(dev, args, rank, world, n=65536, launches=2000):
                 us_per_tick=el * 1e6 / launches, event_us_per_tick=ev * 1e3 / launches, scaling="weak")
 
 
-def learner_rate(envs, world, rank, ticks, batch=256, exploration="param_noise", precision="bf16", group=None):
+def learner_rate(envs, world, rank, ticks, batch=256, exploration="param_noise", precision="bf16", group=None,
+                 multi_rank="grad"):
     """per tick the actor forward (exploration
     noise) for both players of every game, the fused env step with
     obs/reward/auto-reset, 2N transitions into the HBM replay ring, one critic
@@ -288,7 +292,8 @@ def learner_rate(envs, world, rank, ticks, batch=256, exploration="param_noise",
     on this rank (global ids rank * envs ..)."""
     from skillshot_learning_amd.learner import SkillshotLearner
     L = SkillshotLearner(n_envs=envs, seed=0, env_offset=rank * envs, exploration=exploration, tick_limit=2000,
-                         replay_capacity=1 << 20, gamma=0.99, tau=0.005, precision=precision, process_group=group)
+                         replay_capacity=1 << 20, gamma=0.99, tau=0.005, precision=precision, process_group=group,
+                         multi_rank=multi_rank)
     tg = L.tick_graph(batch=batch, updates_per_tick=1, ticks_per_graph=2)
     tg.run(10)
     torch.cuda.synchronize()
@@ -318,6 +323,66 @@ def learner_rate(envs, world, rank, ticks, batch=256, exploration="param_noise",
     return out
 
 
+def learner_child_main(cfg):
+    """one rank of a multi-rank learner leg, in a child process of the bench
+    rank (its own process group on MASTER_PORT, so a failed or hung learner
+    leg cannot take the bench's headline down with it)"""
+    import datetime
+    world, rank = int(os.environ["WORLD_SIZE"]), int(os.environ["RANK"])
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("SK_BENCH_BACKEND", "nccl")
+    local = local % max(torch.cuda.device_count(), 1) if backend == "gloo" else local
+    torch.cuda.set_device(local)
+    kw = dict(timeout=datetime.timedelta(seconds=cfg["timeout"]))
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local), **kw)
+    else:
+        dist.init_process_group(backend, **kw)
+    if cfg.get("mode"):
+        os.environ["SK_TICKGRAPH_MODE"] = cfg["mode"]
+    out = learner_rate(cfg["envs"], world, rank, cfg["ticks"], batch=cfg["batch"], exploration=cfg["exploration"],
+                       precision=cfg["precision"], multi_rank=cfg["multi_rank"])
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def learner_leg_ranks(cfg, world, timeout, leg):
+    """run a multi-rank learner leg as one child process per rank; returns
+    rank 0's result (None elsewhere) or raises.  "full" capture (RCCL inside
+    the graph) first; if any rank's child fails, every rank retries with the
+    segmented capture (collectives between graph segments)."""
+    import subprocess
+    base = int(os.environ.get("MASTER_PORT", "29500"))
+    tried = []
+    for attempt, mode in enumerate(("", "segmented")):
+        env = os.environ.copy()
+        env["MASTER_PORT"] = str(base + 11 + 2 * leg + attempt)
+        c = dict(cfg, mode=mode, timeout=timeout)
+        p = subprocess.Popen([sys.executable, os.path.abspath(__file__), "--learner-child", json.dumps(c)],
+                             env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        try:
+            out, err = p.communicate(timeout=timeout)
+            ok = p.returncode == 0
+        except subprocess.TimeoutExpired:
+            p.kill()
+            out, err = p.communicate()
+            ok = False
+        flag = torch.tensor([1.0 if ok else 0.0], device=torch.device("cuda", torch.cuda.current_device()))
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        tried.append(mode or "auto")
+        if float(flag.item()) == 1.0:
+            if int(os.environ.get("RANK", "0")) == 0:
+                res = json.loads(out.strip().splitlines()[-1])
+                res["capture_attempts"] = tried
+                return res
+            return None
+        if ok is False:
+            sys.stderr.write(f"learner leg {cfg} ({mode or 'auto'}) failed rc={p.returncode}:\n{err[-3000:]}\n")
+    raise RuntimeError(f"learner leg failed in modes {tried}")
+
+
 def _guard(name, fn, errors):
     """a secondary leg must never cost the headline line"""
     try:
@@ -330,6 +395,9 @@ def _guard(name, fn, errors):
 
 def main():
     args = parse()
+    if args.learner_child:
+        learner_child_main(json.loads(args.learner_child))
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -412,13 +480,18 @@ def main():
             for prec in ("fp32", "bf16"):
                 learner[f"config3_{prec}"] = _guard(f"learner.config3_{prec}", lambda: learner_rate(
                     4096, 1, 0, T, batch=256, exploration="action_noise", precision=prec), errors)
-            learner["config5_1gpu_bf16"] = _guard("learner.config5_1gpu", lambda: learner_rate(
-                65536, 1, 0, T, batch=256, exploration="param_noise", precision="bf16"), errors)
+            for prec in ("fp32", "bf16"):
+                learner[f"config5_1gpu_{prec}"] = _guard(f"learner.config5_1gpu_{prec}", lambda: learner_rate(
+                    65536, 1, 0, T, batch=256, exploration="param_noise", precision=prec), errors)
         else:
-            learner["config4"] = _guard("learner.config4", lambda: learner_rate(
-                32768 // world, world, rank, T, batch=256, exploration="action_noise", precision="fp32"), errors)
-            learner["config5"] = _guard("learner.config5", lambda: learner_rate(
-                65536 // world, world, rank, T, batch=256, exploration="param_noise", precision="bf16"), errors)
+            legs = (("config4", dict(envs=32768 // world, batch=256, exploration="action_noise", precision="fp32",
+                                     multi_rank="grad", ticks=T)),
+                    ("config5", dict(envs=65536 // world, batch=256, exploration="param_noise", precision="bf16",
+                                     multi_rank="shared", ticks=T)))
+            for k, (name, cfg) in enumerate(legs):
+                dist.barrier()
+                learner[name] = _guard(f"learner.{name}", lambda: learner_leg_ranks(cfg, world, args.learner_timeout,
+                                                                                    k), errors)
 
     cpu = None
     if world == 1 and not args.no_cpu_baseline:  # N=1 only (the CPU baseline is a per-box figure)

@@ -20,6 +20,7 @@
 #include <string>
 
 #include "sk_device.hpp"
+#include "sk_host.hpp"
 
 using namespace sk;
 
@@ -44,6 +45,9 @@ struct sk_env {
   // (player per lane), 2 = k_step_fast (fp32 trig + exact fallback); -1 = auto
   // (SK_STEP_VARIANT overrides)
   int step_variant;
+  // device = -1: the CPU backend (sk_host.cpp) owns the games; every entry
+  // point below forwards to it and takes host pointers
+  skh::Host* host;
 };
 
 static thread_local std::string g_err;
@@ -726,6 +730,27 @@ static int make_env(sk_env** out, const sk_state_view* view, int32_t n, int64_t 
   if (!out) return fail(SK_EINVAL, "out is NULL");
   *out = nullptr;
   if (n <= 0) return fail(SK_EINVAL, "n_envs must be > 0");
+  if (device == -1) {  // CPU backend
+    sk_env* e = new sk_env();
+    e->n = n;
+    e->env_offset = env_offset;
+    e->seed = seed;
+    e->device = -1;
+    if (cfg) e->cfg = *cfg; else sk_config_default(&e->cfg);
+    int rc0 = validate_cfg(e->cfg);
+    if (rc0) { delete e; return rc0; }
+    if (view && (view->n_envs != n || !view->pos || !view->rot || !view->qpos || !view->qrot || !view->qcdage ||
+                 !view->misc)) {
+      delete e;
+      return fail(SK_EINVAL, "incomplete sk_state_view");
+    }
+    e->host = skh::create(n, env_offset, seed, e->cfg, view);
+    if (!e->host) { delete e; return fail(SK_ENOMEM, "host state allocation"); }
+    e->hview = skh::view_of(*e->host);
+    e->owned = view == nullptr;
+    *out = e;
+    return SK_OK;
+  }
   int rc = check_device(device);
   if (rc) return rc;
   HIP_TRY(hipSetDevice(device));
@@ -815,6 +840,11 @@ int sk_env_attach(sk_env** out, const sk_state_view* view, int64_t env_offset, u
 
 int sk_env_destroy(sk_env* e) {
   if (!e) return fail(SK_EINVAL, "NULL handle");
+  if (e->host) {
+    skh::destroy(e->host);
+    delete e;
+    return SK_OK;
+  }
   (void)hipSetDevice(e->device);
   if (e->owned) (void)hipFree(e->hview.pos);
   (void)hipFree(e->d_aux);
@@ -830,12 +860,20 @@ int sk_env_get_view(const sk_env* e, sk_state_view* out) {
 
 int sk_env_counters_ptr(const sk_env* e, sk_counters** out) {
   if (!e || !out) return fail(SK_EINVAL, "NULL argument");
+  if (e->host) {  // one host slot
+    *out = &e->host->ctr;
+    return SK_OK;
+  }
   *out = e->d_counters;
   return SK_OK;
 }
 
 int sk_env_read_counters(sk_env* e, sk_counters* out, void* stream) {
   if (!e || !out) return fail(SK_EINVAL, "NULL argument");
+  if (e->host) {
+    *out = e->host->ctr;
+    return SK_OK;
+  }
   sk_counters slots[SK_COUNTER_SLOTS];
   HIP_TRY(hipMemcpyAsync(slots, e->d_counters, sizeof(slots), hipMemcpyDeviceToHost, (hipStream_t)stream));
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
@@ -852,6 +890,10 @@ int sk_env_read_counters(sk_env* e, sk_counters* out, void* stream) {
 
 int sk_env_clear_counters(sk_env* e, void* stream) {
   if (!e) return fail(SK_EINVAL, "NULL handle");
+  if (e->host) {
+    e->host->ctr = sk_counters{0, 0, 0, 0};
+    return SK_OK;
+  }
   HIP_TRY(hipMemsetAsync(e->d_counters, 0, SK_COUNTER_SLOTS * sizeof(sk_counters), (hipStream_t)stream));
   return SK_OK;
 }
@@ -863,6 +905,10 @@ int sk_env_clear_counters(sk_env* e, void* stream) {
 // the maximum.
 int sk_env_get_step_counter(const sk_env* e, uint64_t* out) {
   if (!e || !out) return fail(SK_EINVAL, "NULL argument");
+  if (e->host) {
+    *out = e->host->step;
+    return SK_OK;
+  }
   HIP_TRY(hipSetDevice(e->device));
   HIP_TRY(hipDeviceSynchronize());
   uint64_t s[2];
@@ -873,6 +919,10 @@ int sk_env_get_step_counter(const sk_env* e, uint64_t* out) {
 
 int sk_env_set_step_counter(sk_env* e, uint64_t v) {
   if (!e) return fail(SK_EINVAL, "NULL handle");
+  if (e->host) {
+    e->host->step = v;
+    return SK_OK;
+  }
   HIP_TRY(hipSetDevice(e->device));
   HIP_TRY(hipDeviceSynchronize());
   const uint64_t s[2] = {v, v};
@@ -891,6 +941,7 @@ __global__ void k_sync_step_slots(uint64_t* slots) {
 
 int sk_env_sync_step_counter(sk_env* e, void* stream) {
   if (!e) return fail(SK_EINVAL, "NULL handle");
+  if (e->host) return SK_OK;  // one host counter: nothing to sync
   k_sync_step_slots<<<1, 64, 0, (hipStream_t)stream>>>(e->d_step);
   HIP_TRY(hipGetLastError());
   e->parity = 0;
@@ -905,6 +956,7 @@ int sk_env_sync_step_counter(sk_env* e, void* stream) {
 
 int sk_env_reset(sk_env* e, const uint8_t* mask, int32_t random_positions, void* stream) {
   SK_CHECK_ENV(e);
+  if (e->host) return skh::reset(*e->host, mask, random_positions), SK_OK;
   k_reset<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(e->view, e->n, mask, random_positions, e->seed,
                                                                e->env_offset, StepRef{e->d_step, e->parity}, e->dcfg);
   SK_LAUNCH_CHECK();
@@ -915,6 +967,7 @@ int sk_env_reset(sk_env* e, const uint8_t* mask, int32_t random_positions, void*
 int sk_player_move_direction(sk_env* e, int32_t pid, const double* speeds, double scalar, void* stream) {
   SK_CHECK_ENV(e);
   SK_CHECK_PID(pid);
+  if (e->host) return skh::move_direction(*e->host, pid - 1, speeds, scalar), SK_OK;
   k_move_direction<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(e->view, e->n, pid - 1, speeds, scalar,
                                                                         e->dcfg);
   SK_LAUNCH_CHECK();
@@ -924,6 +977,7 @@ int sk_player_move_direction(sk_env* e, int32_t pid, const double* speeds, doubl
 int sk_player_move_look(sk_env* e, int32_t pid, const double* angles, double scalar, void* stream) {
   SK_CHECK_ENV(e);
   SK_CHECK_PID(pid);
+  if (e->host) return skh::move_look(*e->host, pid - 1, angles, scalar), SK_OK;
   k_move_look<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(e->view, e->n, pid - 1, angles, scalar,
                                                                    e->dcfg);
   SK_LAUNCH_CHECK();
@@ -934,6 +988,7 @@ int sk_player_move_discrete(sk_env* e, int32_t pid, int32_t kind, const uint8_t*
   SK_CHECK_ENV(e);
   SK_CHECK_PID(pid);
   if (kind < 0 || kind > 3) return fail(SK_EINVAL, "kind must be 0..3");
+  if (e->host) return skh::move_discrete(*e->host, pid - 1, kind, mask), SK_OK;
   k_move_discrete<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(e->view, e->n, pid - 1, kind, mask,
                                                                        e->dcfg);
   SK_LAUNCH_CHECK();
@@ -943,6 +998,7 @@ int sk_player_move_discrete(sk_env* e, int32_t pid, int32_t kind, const uint8_t*
 int sk_player_shoot(sk_env* e, int32_t pid, const uint8_t* mask, void* stream) {
   SK_CHECK_ENV(e);
   SK_CHECK_PID(pid);
+  if (e->host) return skh::shoot(*e->host, pid - 1, mask), SK_OK;
   k_shoot<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(e->view, e->n, pid - 1, mask, e->dcfg);
   SK_LAUNCH_CHECK();
   return SK_OK;
@@ -951,6 +1007,7 @@ int sk_player_shoot(sk_env* e, int32_t pid, const uint8_t* mask, void* stream) {
 int sk_projectile_move(sk_env* e, int32_t pid, int32_t tick, const uint8_t* mask, void* stream) {
   SK_CHECK_ENV(e);
   SK_CHECK_PID(pid);
+  if (e->host) return skh::projectile_move(*e->host, pid - 1, tick, mask), SK_OK;
   k_projectile_move<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(e->view, e->n, pid - 1, tick, mask,
                                                                          e->dcfg);
   SK_LAUNCH_CHECK();
@@ -959,6 +1016,7 @@ int sk_projectile_move(sk_env* e, int32_t pid, int32_t tick, const uint8_t* mask
 
 int sk_game_check_collision(sk_env* e, uint8_t* hit_out, void* stream) {
   SK_CHECK_ENV(e);
+  if (e->host) return skh::check_collision(*e->host, hit_out), SK_OK;
   k_check_collision<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(e->view, e->n, hit_out, e->dcfg);
   SK_LAUNCH_CHECK();
   return SK_OK;
@@ -966,6 +1024,7 @@ int sk_game_check_collision(sk_env* e, uint8_t* hit_out, void* stream) {
 
 int sk_game_tick(sk_env* e, void* stream) {
   SK_CHECK_ENV(e);
+  if (e->host) return skh::game_tick(*e->host), SK_OK;
   k_game_tick<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(e->view, e->n, e->dcfg);
   SK_LAUNCH_CHECK();
   return SK_OK;
@@ -974,6 +1033,7 @@ int sk_game_tick(sk_env* e, void* stream) {
 int sk_env_features(sk_env* e, double* feat, void* stream) {
   SK_CHECK_ENV(e);
   if (!feat) return fail(SK_EINVAL, "feat is NULL");
+  if (e->host) return skh::features(*e->host, feat), SK_OK;
   k_features<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(e->view, e->n, feat, e->dcfg);
   SK_LAUNCH_CHECK();
   return SK_OK;
@@ -984,6 +1044,7 @@ int sk_env_observe(sk_env* e, float* obs, float* reward, int32_t kind, void* str
   if (kind != SK_REWARD_LOOKING && kind != SK_REWARD_SIMPLE) return fail(SK_EINVAL, "bad reward_kind");
   if (((uintptr_t)obs) & 15) return fail(SK_EINVAL, "obs must be 16-byte aligned");
   if (!obs && !reward) return SK_OK;
+  if (e->host) return skh::observe(*e->host, obs, reward, kind), SK_OK;
   k_observe<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(e->view, e->n, obs, reward, kind, e->dcfg);
   SK_LAUNCH_CHECK();
   return SK_OK;
@@ -999,6 +1060,11 @@ int sk_env_step(sk_env* e, const float* actions, float* obs, float* reward, int3
     return fail(SK_EINVAL, "obs buffers must be 16-byte aligned");
   if (reward_kind != SK_REWARD_LOOKING && reward_kind != SK_REWARD_SIMPLE)
     return fail(SK_EINVAL, "bad reward_kind");
+  if (e->host) {
+    skh::step(*e->host, actions, obs, reward, reward_kind, done, winner, tick_limit, auto_reset, random_positions,
+              obs_reset);
+    return SK_OK;
+  }
   StepArgs a;
   a.v = e->view;
   a.n = e->n;
@@ -1041,6 +1107,7 @@ int sk_gen_random_actions(sk_env* e, float* actions, int32_t n_ticks, void* stre
   SK_CHECK_ENV(e);
   if (!actions || n_ticks <= 0) return fail(SK_EINVAL, "bad actions / n_ticks");
   if (((uintptr_t)actions) & 7) return fail(SK_EINVAL, "actions must be 8-byte aligned");
+  if (e->host) return skh::gen_random_actions(*e->host, actions, n_ticks), SK_OK;
   k_gen_actions<<<grid_for(e->n), kBlock, 0, (hipStream_t)stream>>>(
       reinterpret_cast<float4*>(actions), e->n, n_ticks, e->seed, e->env_offset, StepRef{e->d_step, e->parity});
   SK_LAUNCH_CHECK();
@@ -1050,6 +1117,7 @@ int sk_gen_random_actions(sk_env* e, float* actions, int32_t n_ticks, void* stre
 int sk_env_rollout_random(sk_env* e, int32_t n_ticks, int32_t tick_limit, void* stream) {
   SK_CHECK_ENV(e);
   if (n_ticks <= 0) return fail(SK_EINVAL, "n_ticks must be > 0");
+  if (e->host) return skh::rollout_random(*e->host, n_ticks, tick_limit), SK_OK;
   RolloutArgs a;
   a.v = e->view;
   a.n = e->n;

@@ -1,17 +1,19 @@
-"""Reference-shaped class API over the GPU engine: SkillshotGame, Player,
+"""Reference-shaped class API over libskillshot: SkillshotGame, Player,
 Projectile with the constructors, attributes and methods of
 SkillshotGame.py:8-169, Player.py:8-100 and Projectile.py:4-64.
 
-Each SkillshotGame is a one-game VecSkillshotGame on the GPU; every mutating
-method is one libskillshot launch (the batched kernels with N=1) and
-attribute reads come from a host snapshot refreshed after mutations.  Pure
+Each SkillshotGame is a one-game VecSkillshotGame: by default on
+libskillshot's CPU backend (device="cpu", csrc/sk_host.cpp: one C call per
+method, no device round trip), or on the GPU (device="cuda": every mutating
+method one launch of the batched kernels with N=1).  Attribute reads come
+from a snapshot of the state planes refreshed after mutations.  Pure
 helpers the reference computes from attributes alone (get_gradient_dir,
 check_pos_valid, the static distance helpers, check_future_collision,
 get_board) are evaluated on the host exactly as the reference writes them.
 
 Random starts keep the reference's numpy global RNG draw
 (np.random.randint(25, 225, (2, 2)), SkillshotGame.py:15) so np.random.seed
-keeps its meaning.  This layer needs a gfx950 GPU: there is no CPU fallback.
+keeps its meaning.
 """
 import math
 
@@ -19,6 +21,12 @@ import numpy as np
 import torch
 
 from .vec_env import FEATURE_KEYS, VecSkillshotGame
+
+# get_state value types (SkillshotGame.py:145-163): Python ints, bools and floats
+_INTS = {"player_x_dir", "player_pos_x", "player_pos_y", "projectile_cooldown", "projectile_x_dir",
+         "projectile_pos_x", "projectile_pos_y", "projectile_age"}
+_BOOLS = {"projectile_valid", "projectile_future_collision_opponent"}
+_CASTS = tuple(int if k in _INTS else (bool if k in _BOOLS else float) for k in FEATURE_KEYS)
 
 _PLAYER_SHAPE = [[0, 0, 0, 0, 0], [0, 1, 1, 1, 0], [0, 1, 1, 1, 0], [0, 1, 1, 1, 0], [0, 0, 0, 0, 0]]
 _PROJECTILE_SHAPE = [[1, 0, 1], [0, 1, 0], [1, 0, 1]]
@@ -148,13 +156,11 @@ class Projectile(object):
 
     def move_forwards(self):  # Projectile.py:38-47
         _trig_check(self.rotation)
-        self._g._eng.projectile_move(self._i + 1, tick=False)
-        self._g._dirty()
+        self._g._projectile_move(self._i + 1, 0)
 
     def tick(self):  # Projectile.py:49-53
         _trig_check(self.rotation)
-        self._g._eng.projectile_move(self._i + 1, tick=True)
-        self._g._dirty()
+        self._g._projectile_move(self._i + 1, 1)
 
     def get_gradient_dir(self):
         return _gradient_dir(self.rotation, self.pos)
@@ -192,63 +198,63 @@ class Player(object):
     def rotation(self):
         return float(self._g._snap()["rot_p"][self._i])
 
+    def _rotation_checked(self):
+        """the rotation, raising where the reference's math.sin/cos would"""
+        r = float(self._g._snap()["rot_p"][self._i])
+        if r != r or r in (math.inf, -math.inf):
+            _trig_check(r)
+        return r
+
     @rotation.setter
     def rotation(self, value):
         self._g._write("rot", (0, self._i), float(value))
 
     def move_look_left(self):  # Player.py:27-28
-        self._g._eng.move_discrete(self.id, 2)
-        self._g._dirty()
+        self._g._move_discrete(self.id, 2)
 
     def move_look_right(self):  # Player.py:30-31
-        self._g._eng.move_discrete(self.id, 3)
-        self._g._dirty()
+        self._g._move_discrete(self.id, 3)
 
     def move_look_float(self, angle):  # Player.py:33-39
-        self._g._eng.move_look(self.id, float(angle))
-        self._g._dirty()
+        self._g._move_look(self.id, float(angle))
 
     def move_forwards(self):  # Player.py:41-47
-        _trig_check(self.rotation)
-        self._g._eng.move_discrete(self.id, 0)
-        self._g._dirty()
+        self._rotation_checked()
+        self._g._move_discrete(self.id, 0)
 
     def move_backwards(self):  # Player.py:49-55
-        _trig_check(self.rotation)
-        self._g._eng.move_discrete(self.id, 1)
-        self._g._dirty()
+        self._rotation_checked()
+        self._g._move_discrete(self.id, 1)
 
     def move_direction_float(self, speed):  # Player.py:57-68
         speed = float(speed)
-        clamped = 1.0 if speed >= 1 else speed
-        clamped = -1.0 if clamped <= -1 else clamped
-        _trig_check(self.rotation)
-        _nan_check(clamped)
-        self._g._eng.move_direction(self.id, speed)
-        self._g._dirty()
+        self._rotation_checked()
+        if speed != speed:  # int(round(nan)) raises in the reference
+            _nan_check(speed)
+        self._g._move_direction(self.id, speed)
 
     def check_pos_valid(self, check_x, check_y):  # Player.py:70-76
         return (check_x + self.shape_size[0] <= self.board_dim[0] and check_x >= 0 and
                 check_y + self.shape_size[1] <= self.board_dim[1] and check_y >= 0)
 
     def move_shoot_projectile(self):  # Player.py:78-89
-        self._g._eng.shoot(self.id)
-        self._g._dirty()
+        self._g._shoot(self.id)
 
     def get_gradient_dir(self):  # Player.py:91-100
         return _gradient_dir(self.rotation, self.pos)
 
 
 class SkillshotGame(object):
-    """SkillshotGame.py:8-169 over a one-game GPU batch."""
+    """SkillshotGame.py:8-169 over a one-game libskillshot batch (CPU backend or GPU)."""
 
-    def __init__(self, random_positions=False, device="cuda"):
+    def __init__(self, random_positions=False, device="cpu"):
         self.board_size = (250, 250)
         self.board = np.zeros(self.board_size, dtype=int)
         if getattr(self, "_eng", None) is None:
             self._eng = VecSkillshotGame(1, device=device, tick_limit=2 ** 31 - 1, random_positions=False)
+            self._bind()
         self._eng.reset(random_positions=False)
-        self._cache = None
+        self._dirty()
         if random_positions:
             pos_player1, pos_player2 = np.random.randint(25, 225, (2, 2))  # SkillshotGame.py:15
             self._write("pos", (0, 0), int(pos_player1[0]))
@@ -259,13 +265,51 @@ class SkillshotGame(object):
         self.player2 = Player(self, 1)
 
     # -- state plumbing
-    def _dirty(self):
+    def _bind(self):
+        """the per-method entry points: direct C calls on the CPU backend
+        (host pointers, no stream; the state planes are live numpy views, so
+        the snapshot never goes stale), the VecSkillshotGame methods on the
+        GPU (snapshot refreshed after each mutation)"""
+        e = self._eng
+        self._cpu = e.is_cpu
         self._cache = None
+        if self._cpu:
+            L, h = e._L, e._h
+            views = {k: getattr(e, k).numpy() for k in ("pos", "rot", "qpos", "qrot", "qcdage", "misc")}
+            views["rot_p"] = views["rot"][0]
+            views["rot_q"] = views["qrot"][0]
+            self._cache = views
+            self._move_direction = lambda pid, v: L.sk_player_move_direction(h, pid, None, v, None)
+            self._move_look = lambda pid, v: L.sk_player_move_look(h, pid, None, v, None)
+            self._move_discrete = lambda pid, k: L.sk_player_move_discrete(h, pid, k, None, None)
+            self._shoot = lambda pid: L.sk_player_shoot(h, pid, None, None)
+            self._projectile_move = lambda pid, t: L.sk_projectile_move(h, pid, t, None, None)
+            self._game_tick_c = lambda: L.sk_game_tick(h, None)
+        else:
+            def mut(f):
+                def g(*a):
+                    f(*a)
+                    self._cache = None
+                return g
+            self._move_direction = mut(e.move_direction)
+            self._move_look = mut(e.move_look)
+            self._move_discrete = mut(e.move_discrete)
+            self._shoot = mut(e.shoot)
+            self._projectile_move = mut(lambda pid, t: e.projectile_move(pid, tick=bool(t)))
+            self._game_tick_c = mut(e.game_tick)
+
+    def _dirty(self):
+        if not self._cpu:
+            self._cache = None
 
     def _snap(self):
         if self._cache is None:
-            torch.cuda.current_stream(self._eng.device).synchronize()
-            d = {k: getattr(self._eng, k).cpu().numpy() for k in ("pos", "rot", "qpos", "qrot", "qcdage", "misc")}
+            if self._eng.is_cpu:  # the planes are host memory: views, no copies
+                d = {k: getattr(self._eng, k).numpy() for k in ("pos", "rot", "qpos", "qrot", "qcdage", "misc")}
+            else:
+                torch.cuda.current_stream(self._eng.device).synchronize()
+                d = {k: getattr(self._eng, k).cpu().numpy() for k in ("pos", "rot", "qpos", "qrot", "qcdage",
+                                                                      "misc")}
             d["rot_p"] = d["rot"][0]
             d["rot_q"] = d["qrot"][0]
             self._cache = d
@@ -347,10 +391,11 @@ class SkillshotGame(object):
     def game_tick(self):  # SkillshotGame.py:115-122
         was_live = self.game_live
         if was_live:  # Projectile.move_forwards evaluates sin/cos before testing valid
-            for q in (self.player1.projectile, self.player2.projectile):
-                _trig_check(q.rotation)
-        self._eng.game_tick()
-        self._dirty()
+            qr = self._snap()["rot_q"]
+            for r in (float(qr[0]), float(qr[1])):
+                if r != r or r in (math.inf, -math.inf):
+                    _trig_check(r)
+        self._game_tick_c()
         if was_live and not self.game_live:
             print("Player", self.winner_id, "loss")
 
@@ -363,18 +408,21 @@ class SkillshotGame(object):
     def get_dist_point_point(point1, point2):  # SkillshotGame.py:132-134
         return ((point1[0] - point2[0]) ** 2 + (point1[1] - point2[1]) ** 2) ** 0.5
 
-    def get_state(self):  # SkillshotGame.py:136-166, numerics from the k_features kernel
-        f = self._eng.features().cpu().numpy()[0]
+    def get_state(self):  # SkillshotGame.py:136-166, numerics from sk_env_features
+        if self._cpu:
+            fb = getattr(self, "_featbuf", None)
+            if fb is None:
+                fb = self._featbuf = torch.empty((1, 2, 18), dtype=torch.float64)
+                self._featnp = fb.numpy()
+            self._eng.features(out=fb)
+            f = self._featnp[0].tolist()
+        else:
+            f = self._eng.features().cpu().numpy()[0].tolist()
         feature_dict = dict(game_live=self.game_live, ticks=self.ticks, game_winner=self.winner_id)
-        ints = {"player_x_dir", "player_pos_x", "player_pos_y", "projectile_cooldown", "projectile_x_dir",
-                "projectile_pos_x", "projectile_pos_y", "projectile_age"}
-        bools = {"projectile_valid", "projectile_future_collision_opponent"}
+        casts = _CASTS
         for p, pid in ((0, 1), (1, 2)):
-            d = {}
-            for k, key in enumerate(FEATURE_KEYS):
-                v = float(f[p, k])
-                d[key] = int(v) if key in ints else (bool(v) if key in bools else v)
-            feature_dict[pid] = d
+            row = f[p]
+            feature_dict[pid] = {key: casts[k](row[k]) for k, key in enumerate(FEATURE_KEYS)}
         return feature_dict
 
     def game_reset(self, random_positions=False):  # SkillshotGame.py:168-169

@@ -413,6 +413,21 @@ class DDPG:
                 for p in m.parameters():
                     dist.broadcast(p.data, src=0, group=self.group)
 
+    # every collective of an update goes through _collective: eager it runs
+    # at once; while a TickGraph captures in segments it cuts the capture
+    # there and is replayed between the graph segments (collective_hook)
+    collective_hook = None
+
+    def _collective(self, fn):
+        if self.collective_hook is not None:
+            self.collective_hook(fn)
+        else:
+            fn()
+
+    def allreduce_sum(self, flat):
+        """in-place SUM all-reduce of one flat device buffer (RCCL over xGMI)"""
+        self._collective(lambda: dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group))
+
     def _allreduce_grads(self, module):
         """Gradient all-reduce (sum: each rank's loss is already normalised
         by the global batch) as ONE flat bucket per update: 36,482 actor /
@@ -421,7 +436,7 @@ class DDPG:
             return
         grads = [p.grad for p in module.parameters()]
         flat = torch.cat([g.reshape(-1) for g in grads])
-        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+        self.allreduce_sum(flat)
         off = 0
         for g in grads:
             n = g.numel()
@@ -437,7 +452,10 @@ class DDPG:
             return tensors
         flat = torch.cat([t.reshape(t.shape[0], -1) for t in tensors], dim=1).contiguous()
         out = torch.empty((w * flat.shape[0], flat.shape[1]), device=flat.device, dtype=flat.dtype)
-        dist.all_gather_into_tensor(out, flat, group=self.group)
+        if flat.is_cuda and dist.get_backend(self.group) == "gloo":  # gloo: the list form on device tensors
+            self._collective(lambda: dist.all_gather(list(out.chunk(w)), flat, group=self.group))
+        else:
+            self._collective(lambda: dist.all_gather_into_tensor(out, flat, group=self.group))
         res, off = [], 0
         for t in tensors:
             k = t[0].numel()
@@ -817,13 +835,18 @@ class SkillshotLearner:
         device-side samples (capturable fused Adam), the soft target update and
         the actor repack.  Every per-tick quantity (ring head and size, step
         and noise counters, RNG offsets) lives on device, so replays continue
-        the eager trajectory's semantics.  Single-GPU only: collectives stay
-        on the eager path.  Returns a TickGraph; `.run(n)` replays n times.
+        the eager trajectory's semantics.  Returns a TickGraph; `.run(n)`
+        replays n times.
+
+        Several ranks (multi_rank "grad" / "shared"): mode "full" captures the
+        RCCL collectives (gradient all-reduce, shared-sample all-gather) inside
+        the graph (backend nccl); mode "segmented" cuts the capture at every
+        collective and replays graph segments with the collectives issued
+        between them (any backend, e.g. gloo).  Default: "full" for nccl,
+        "segmented" otherwise; SK_TICKGRAPH_MODE overrides.
         """
         if self.device.type != "cuda":
             raise RuntimeError("tick_graph needs the GPU engine")
-        if self.ddpg.world() > 1:
-            raise RuntimeError("tick_graph is single-GPU (the multi-rank update stays eager)")
         if ticks_per_graph % 2:
             raise ValueError("ticks_per_graph must be even (step-counter ping-pong slots)")
         return TickGraph(self, batch, updates_per_tick, ticks_per_graph, warmup)
@@ -866,7 +889,15 @@ class TickGraph:
 
     def __init__(self, L, batch, updates_per_tick, ticks_per_graph, warmup):
         self.L, self.batch, self.updates, self.ticks = L, batch, updates_per_tick, ticks_per_graph
+        world = L.ddpg.world()
         self.multi_rank_mode = None
+        if world > 1:
+            mode = os.environ.get("SK_TICKGRAPH_MODE") or (
+                "full" if dist.get_backend(L.ddpg.group) == "nccl" else "segmented")
+            if mode not in ("full", "segmented"):
+                raise ValueError("SK_TICKGRAPH_MODE must be 'full' or 'segmented'")
+            self.multi_rank_mode = f"{L.ddpg.multi_rank}/{mode}"
+        self._segments = None
         g = L.game_environment
         n = L.n_envs
         dev = L.device
@@ -896,15 +927,52 @@ class TickGraph:
         # parity 0): run() syncs before replaying, so eager steps between
         # replays cannot leave the captured slot stale
         g.sync_step_counter(ctypes.c_void_p(self.stream.cuda_stream))
-        self.graph = torch.cuda.CUDAGraph()
-        self.graph.register_generator_state(L.gen)
         mirror = L.replay.total  # capture records the inserts without running them
-        with torch.cuda.graph(self.graph, stream=self.stream):
-            for _ in range(self.ticks):
-                self._tick(update=True)
+        if self.multi_rank_mode and self.multi_rank_mode.endswith("segmented"):
+            self.graph = None
+            self._segments = self._capture_segments()
+        else:
+            self.graph = torch.cuda.CUDAGraph()
+            self.graph.register_generator_state(L.gen)
+            with torch.cuda.graph(self.graph, stream=self.stream):
+                for _ in range(self.ticks):
+                    self._tick(update=True)
         self.stream.synchronize()
         L.replay.total = mirror
         self.replays = 0
+
+    def _capture_segments(self):
+        """capture the ticks as graph segments cut at every collective:
+        returns [graph, fn, graph, fn, ..., graph] (fn = the collective,
+        issued eagerly on replay between the segments it separates)"""
+        L = self.L
+        pool = torch.cuda.graph_pool_handle()
+        items = []
+        cur = []
+
+        def begin():
+            g = torch.cuda.CUDAGraph()
+            g.register_generator_state(L.gen)
+            g.capture_begin(pool=pool)
+            cur[:] = [g]
+
+        def cut(fn):
+            cur[0].capture_end()
+            items.append(cur[0])
+            items.append(fn)
+            begin()
+
+        with torch.cuda.stream(self.stream):
+            L.ddpg.collective_hook = cut
+            try:
+                begin()
+                for _ in range(self.ticks):
+                    self._tick(update=True)
+                cur[0].capture_end()
+                items.append(cur[0])
+            finally:
+                L.ddpg.collective_hook = None
+        return items
 
     @property
     def obs(self):
@@ -941,7 +1009,14 @@ class TickGraph:
         with torch.cuda.stream(self.stream):  # replay() launches on the current stream
             self.L.game_environment.sync_step_counter(ctypes.c_void_p(self.stream.cuda_stream))
             for _ in range(n):
-                self.graph.replay()
+                if self._segments is None:
+                    self.graph.replay()
+                    continue
+                for it in self._segments:
+                    if callable(it) and not isinstance(it, torch.cuda.CUDAGraph):
+                        it()
+                    else:
+                        it.replay()
         cur.wait_stream(self.stream)
         self.replays += n
         # host mirrors of the ring (2N rows per tick)

@@ -211,7 +211,7 @@ class FusedUpdate:
             g = self.grad_flat[:P]
             _capi.check(self.L.sk_adam_flat(_p(part), part.shape[0], P, None, _p(g), 0, None, None, None, None,
                                             0.0, 0.0, 0.0, 0.0, None, 0.0, None, 0.0, None, None, self._stream()))
-            dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.d.group)
+            self.d.allreduce_sum(g)
             _capi.check(self.L.sk_adam_flat_packed(None, 0, P, _p(g), None, 1, _p(flat), _p(st.m), _p(st.v),
                                                    _p(st.steps), st.lr, st.b1, st.b2, st.eps, _p(target), tau,
                                                    _p(stat), float(scale), _p(out), _p(counter), pk, self._stream()))

@@ -32,12 +32,17 @@ def _ptr(t):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
-def _require_gpu(device):
+def _resolve_device(device):
+    """cuda[:i] -> the gfx950 engine on that device; cpu -> libskillshot's CPU
+    backend (device = -1, csrc/sk_host.cpp), chosen explicitly, never as a
+    fallback: a cuda request without a GPU raises."""
     dev = torch.device(device)
+    if dev.type == "cpu":
+        return dev
     if dev.type != "cuda":
-        raise SkillshotError("VecSkillshotGame runs on a gfx950 GPU only (no CPU fallback)")
+        raise SkillshotError(f"VecSkillshotGame runs on a gfx950 GPU or the CPU backend, not {dev}")
     if not torch.cuda.is_available():
-        raise SkillshotError("no GPU visible: libskillshot has no CPU fallback")
+        raise SkillshotError("no GPU visible (use device='cpu' for libskillshot's CPU backend)")
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     return torch.device("cuda", idx)
 
@@ -54,7 +59,8 @@ class VecSkillshotGame:
 
     def __init__(self, n_envs, device="cuda", seed=0, env_offset=0, tick_limit=2000,
                  random_positions=True, config=None):
-        self.device = _require_gpu(device)
+        self.device = _resolve_device(device)
+        self.is_cpu = self.device.type == "cpu"
         self.n = int(n_envs)
         if self.n <= 0:
             raise ValueError("n_envs must be > 0")
@@ -63,16 +69,15 @@ class VecSkillshotGame:
         self.tick_limit = int(tick_limit)
         self.random_positions = bool(random_positions)
         self._L = _capi.load()
-        with torch.cuda.device(self.device):
-            for name, dt, w in PLANES:
-                setattr(self, name, torch.zeros((self.n, w), dtype=dt, device=self.device))
+        for name, dt, w in PLANES:
+            setattr(self, name, torch.zeros((self.n, w), dtype=dt, device=self.device))
         view = _capi.SkStateView(self.n, *[getattr(self, name).data_ptr() for name, _, _ in PLANES])
         cfg = config if config is not None else _capi.default_config()
         self.config = cfg
         h = ctypes.c_void_p()
-        torch.cuda.synchronize(self.device)
+        self._sync()
         check(self._L.sk_env_attach(ctypes.byref(h), ctypes.byref(view), self.env_offset, self.seed,
-                                    self.device.index, ctypes.byref(cfg)))
+                                    -1 if self.is_cpu else self.device.index, ctypes.byref(cfg)))
         self._h = h
         cp = ctypes.c_void_p()
         check(self._L.sk_env_counters_ptr(self._h, ctypes.byref(cp)))
@@ -81,11 +86,17 @@ class VecSkillshotGame:
 
     # ------------------------------------------------------------------ utils
     def _stream(self):
+        if self.is_cpu:
+            return None
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _sync(self):
+        if not self.is_cpu:
+            torch.cuda.synchronize(self.device)
 
     def close(self):
         if getattr(self, "_h", None):
-            torch.cuda.synchronize(self.device)
+            self._sync()
             self._L.sk_env_destroy(self._h)
             self._h = None
 
@@ -118,13 +129,13 @@ class VecSkillshotGame:
         return d
 
     def load_state_dict(self, d):
-        torch.cuda.synchronize(self.device)
+        self._sync()
         for name, dt, w in PLANES:
             src = torch.as_tensor(np.asarray(d[name]).reshape(self.n, w)).to(dt)
             getattr(self, name).copy_(src)
         if "step_counter" in d:
             self.step_counter = int(d["step_counter"])
-        torch.cuda.synchronize(self.device)
+        self._sync()
 
     def get_board(self, index=0):
         """SkillshotGame.get_board (SkillshotGame.py:36-56) of game `index`:

@@ -1,5 +1,7 @@
 """The reference-shaped class API (skillshot_learning_amd.game) driven exactly
-like the reference and compared with the reference fixtures (GPU)."""
+like the reference and compared with the reference fixtures, on both
+libskillshot backends: the CPU backend (device="cpu", csrc/sk_host.cpp; runs
+in the CPU suite) and the GPU engine (device="cuda", marked gpu)."""
 import contextlib
 import io
 import math
@@ -10,15 +12,23 @@ import torch
 
 import golden_replay as gr
 
-pytestmark = pytest.mark.gpu
+class _Game:
+    """the game module with SkillshotGame bound to one backend"""
+
+    def __init__(self, mod, device):
+        self._m, self.device = mod, device
+        self.FEATURE_KEYS = mod.FEATURE_KEYS
+
+    def SkillshotGame(self, random_positions=False):
+        return self._m.SkillshotGame(random_positions=random_positions, device=self.device)
 
 
-@pytest.fixture(scope="module")
-def game_mod():
-    if not torch.cuda.is_available():
+@pytest.fixture(scope="module", params=["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def game_mod(request):
+    if request.param == "cuda" and not torch.cuda.is_available():
         pytest.skip("no GPU")
     from skillshot_learning_amd import game
-    return game
+    return _Game(game, request.param)
 
 
 def _set(g, d, e, t):
