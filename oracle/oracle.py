@@ -19,7 +19,8 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "_build", "libskillshot_oracle.so")
+# SK_ORACLE_LIB: a differently built copy (the sanitizer run, tools/sanitize.sh)
+_LIB_PATH = os.environ.get("SK_ORACLE_LIB") or os.path.join(_HERE, "_build", "libskillshot_oracle.so")
 _lib = None
 
 FIELDS = (("pos", np.int32, 4), ("rot", np.float64, 2), ("qpos", np.int32, 4),
@@ -33,8 +34,8 @@ def build():
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(_LIB_PATH) or (
-                os.path.getmtime(_LIB_PATH) < os.path.getmtime(os.path.join(_HERE, "skillshot_oracle.c"))):
+        if not os.environ.get("SK_ORACLE_LIB") and (not os.path.exists(_LIB_PATH) or (
+                os.path.getmtime(_LIB_PATH) < os.path.getmtime(os.path.join(_HERE, "skillshot_oracle.c")))):
             build()
         L = ctypes.CDLL(_LIB_PATH)
         P = ctypes.c_void_p

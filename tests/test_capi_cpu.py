@@ -1,6 +1,7 @@
 """CPU-side checks of the drop-in boundary: libskillshot builds, loads, exports
-every symbol include/skillshot.h declares, and fails loudly without a GPU
-(no CPU fallback)."""
+every symbol include/skillshot.h declares, fails loudly when a GPU is asked
+for and absent (no CPU fallback), and serves device = -1 with its CPU
+backend."""
 import ctypes
 import os
 import re
@@ -70,7 +71,29 @@ def test_abi_errors_without_device():
 
 @pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU failure path")
 def test_no_cpu_fallback():
+    """a GPU request without a GPU fails loudly; the CPU backend is only ever
+    the one asked for (device = -1 / "cpu"), never a silent substitute"""
     with pytest.raises(ssa.SkillshotError):
         ssa.VecSkillshotGame(8, device="cuda")
     with pytest.raises(ssa.SkillshotError):
-        ssa.VecSkillshotGame(8, device="cpu")
+        ssa.VecSkillshotGame(8, device="meta")
+    g = ssa.VecSkillshotGame(8, device="cpu")
+    assert g.is_cpu and g.pos.device.type == "cpu"
+
+
+def test_cpu_backend_through_the_abi():
+    """sk_env_create(device = -1): engine-owned host state, the fixed start,
+    host-pointer calls (device -1 = CPU)"""
+    L = ssa.load_library()
+    h = ctypes.c_void_p()
+    assert L.sk_env_create(ctypes.byref(h), 3, 0, 7, -1, None) == _capi.SK_OK
+    v = _capi.SkStateView()
+    assert L.sk_env_get_view(h, ctypes.byref(v)) == _capi.SK_OK
+    pos = (ctypes.c_int32 * 12).from_address(v.pos)
+    assert list(pos[:4]) == [50, 50, 200, 200]  # SkillshotGame.py:17-18
+    acts = (ctypes.c_float * 12)(*([0.5, 0.25] * 6))
+    done = (ctypes.c_uint8 * 3)()
+    assert L.sk_env_step(h, acts, None, None, 0, done, None, 2000, 1, 1, None, None) == _capi.SK_OK
+    step = ctypes.c_uint64()
+    assert L.sk_env_get_step_counter(h, ctypes.byref(step)) == _capi.SK_OK and step.value == 1
+    assert L.sk_env_destroy(h) == _capi.SK_OK
