@@ -294,7 +294,12 @@ def learner_rate(envs, world, rank, ticks, batch=256, exploration="param_noise",
     L = SkillshotLearner(n_envs=envs, seed=0, env_offset=rank * envs, exploration=exploration, tick_limit=2000,
                          replay_capacity=1 << 20, gamma=0.99, tau=0.005, precision=precision, process_group=group,
                          multi_rank=multi_rank)
+    verbose = os.environ.get("SK_BENCH_VERBOSE") == "1"
+    if verbose:
+        _log(f"learner {envs} games: capturing")
     tg = L.tick_graph(batch=batch, updates_per_tick=1, ticks_per_graph=2)
+    if verbose:
+        _log(f"learner {envs} games: captured ({tg.multi_rank_mode})")
     tg.run(10)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -323,6 +328,12 @@ def learner_rate(envs, world, rank, ticks, batch=256, exploration="param_noise",
     return out
 
 
+def _log(msg):
+    """progress on stderr (SK_BENCH_VERBOSE=1 or the multi-rank heartbeat)"""
+    sys.stderr.write(f"[bench rank {os.environ.get('RANK', '0')}] {msg}\n")
+    sys.stderr.flush()
+
+
 def learner_child_main(cfg):
     """one rank of a multi-rank learner leg, in a child process of the bench
     rank (its own process group on MASTER_PORT, so a failed or hung learner
@@ -340,6 +351,8 @@ def learner_child_main(cfg):
         dist.init_process_group(backend, **kw)
     if cfg.get("mode"):
         os.environ["SK_TICKGRAPH_MODE"] = cfg["mode"]
+    if os.environ.get("SK_BENCH_VERBOSE") == "1":
+        _log(f"learner child up: {cfg}")
     out = learner_rate(cfg["envs"], world, rank, cfg["ticks"], batch=cfg["batch"], exploration=cfg["exploration"],
                        precision=cfg["precision"], multi_rank=cfg["multi_rank"])
     if rank == 0:
@@ -357,18 +370,25 @@ def learner_leg_ranks(cfg, world, timeout, leg):
     base = int(os.environ.get("MASTER_PORT", "29500"))
     tried = []
     for attempt, mode in enumerate(("", "segmented")):
-        env = os.environ.copy()
+        env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC")}
+        env["TORCHELASTIC_USE_AGENT_STORE"] = "False"  # the children's rank 0 hosts their own TCPStore
         env["MASTER_PORT"] = str(base + 11 + 2 * leg + attempt)
         c = dict(cfg, mode=mode, timeout=timeout)
         p = subprocess.Popen([sys.executable, os.path.abspath(__file__), "--learner-child", json.dumps(c)],
-                             env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
-        try:
-            out, err = p.communicate(timeout=timeout)
-            ok = p.returncode == 0
-        except subprocess.TimeoutExpired:
-            p.kill()
-            out, err = p.communicate()
-            ok = False
+                             env=env, stdout=subprocess.PIPE, text=True,
+                             stderr=None if os.environ.get("SK_BENCH_VERBOSE") == "1" else subprocess.PIPE)
+        t0, ok = time.time(), False
+        while True:  # a heartbeat on stderr while the child runs
+            try:
+                out, err = p.communicate(timeout=20)
+                ok = p.returncode == 0
+                break
+            except subprocess.TimeoutExpired:
+                if time.time() - t0 > timeout:
+                    p.kill()
+                    out, err = p.communicate()
+                    break
+                _log(f"learner leg {leg} ({mode or 'auto'}) running {time.time() - t0:.0f} s")
         flag = torch.tensor([1.0 if ok else 0.0], device=torch.device("cuda", torch.cuda.current_device()))
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         tried.append(mode or "auto")
@@ -379,7 +399,7 @@ def learner_leg_ranks(cfg, world, timeout, leg):
                 return res
             return None
         if ok is False:
-            sys.stderr.write(f"learner leg {cfg} ({mode or 'auto'}) failed rc={p.returncode}:\n{err[-3000:]}\n")
+            sys.stderr.write(f"learner leg {cfg} ({mode or 'auto'}) failed rc={p.returncode}:\n{(err or '')[-3000:]}\n")
     raise RuntimeError(f"learner leg failed in modes {tried}")
 
 
@@ -419,6 +439,9 @@ def main():
     n = total // world  # strong scaling: the metric's fixed 65,536 games over the ranks
     ring = max(args.graph_len, args.action_ring)
     K, W = args.steps, args.warmup
+    verbose = os.environ.get("SK_BENCH_VERBOSE") == "1"
+    if verbose:
+        _log(f"headline: {n} games per GPU, K={K}, W={W}")
     elapsed, ev_ms, env = timed_ticks(dev, n, args.seed, rank * n, args.tick_limit, K, W, ring, args.graph_len, world)
     value = n * world * K / elapsed
     counters = env.counters()
@@ -461,6 +484,8 @@ def main():
                         note="state held in registers across ticks; reported beside, not as, the headline")
         rollout = _guard("rollout_random", _rollout, errors)
 
+    if verbose:
+        _log("secondary legs")
     full = None if args.no_full else _guard("full_contract_tick", lambda: full_contract_rate(dev, args, rank, n),
                                             errors)
     large = None if args.no_large else _guard("large_batch", lambda: large_batch_rate(dev, args, rank), errors)
@@ -490,6 +515,8 @@ def main():
                                      multi_rank="shared", ticks=T)))
             for k, (name, cfg) in enumerate(legs):
                 dist.barrier()
+                if verbose:
+                    _log(f"learner {name}")
                 learner[name] = _guard(f"learner.{name}", lambda: learner_leg_ranks(cfg, world, args.learner_timeout,
                                                                                     k), errors)
 

@@ -402,3 +402,35 @@ def test_fused_step_on_probe_boards(ssa, oracle_mod, step_variant):
         hits += int((wo["winner"] != 0).sum())
     assert hits > 1000
     assert explained <= 64
+
+
+def test_cpu_backend_equals_gpu_engine(ssa):
+    """The two libskillshot backends on one workload: the CPU backend
+    (device = -1, csrc/sk_host.cpp) and the gfx950 engine, same start, same
+    random-policy actions, random auto-reset: state / done / winner bit-exact,
+    obs within 1e-5 with the future-collision flag exact, counters equal."""
+    n, T = 4096, 900
+    g = ssa.VecSkillshotGame(n, seed=5, tick_limit=400)
+    g.reset(random_positions=True)
+    c = ssa.VecSkillshotGame(n, device="cpu", seed=5, tick_limit=400)
+    c.load_state_dict(g.state_dict())
+    g.clear_counters()
+    c.clear_counters()
+    for t in range(T):
+        a = g.gen_random_actions(1)[0]
+        want = t % 89 == 0
+        og = g.step(a, obs=want, auto_reset=True, reset_obs=want)
+        oc = c.step(a.cpu(), obs=want, auto_reset=True, reset_obs=want)
+        if want:
+            torch.cuda.synchronize()
+            assert np.array_equal(og["done"].cpu().numpy(), oc["done"].numpy()), t
+            assert np.array_equal(og["winner"].cpu().numpy(), oc["winner"].numpy()), t
+            for k in ("obs", "reward", "obs_reset"):
+                x, y = og[k].cpu().numpy().astype(np.float64), oc[k].numpy().astype(np.float64)
+                assert (np.abs(x - y) / np.maximum(1.0, np.abs(y))).max() <= OBS_TOL, (t, k)
+            assert np.array_equal(og["obs"].cpu().numpy()[..., 11], oc["obs"].numpy()[..., 11]), t
+    sg, sc = g.state_dict(), c.state_dict()
+    _assert_state_equal({k: v for k, v in sg.items() if k != "step_counter"},
+                        {k: v for k, v in sc.items() if k != "step_counter"}, "end")
+    assert sg["step_counter"] == sc["step_counter"]
+    assert g.counters() == c.counters()
