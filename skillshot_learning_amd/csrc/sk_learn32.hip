@@ -65,9 +65,9 @@ __device__ __forceinline__ Net net_of(const float* f, int ld2, int n_out) {
 // Re-derive a net's bases (and the lane id) inside a sub-tile loop: without
 // this LICM hoists every per-lane load address out of the loop and spills
 // them (the same trap as sk_update.hip's fragment loads)
-__device__ __forceinline__ Net launder(Net n) {
-  asm volatile("" : "+s"(n.W1), "+s"(n.b1), "+s"(n.W2), "+s"(n.b2), "+s"(n.W3), "+s"(n.b3));
-  return n;
+__device__ __forceinline__ const float* launder(const float* base) {
+  asm volatile("" : "+s"(base));  // one SGPR pair per net; the parameter offsets are immediates
+  return base;
 }
 __device__ __forceinline__ int launder_lane(int lane) {
   asm volatile("" : "+v"(lane));
@@ -291,7 +291,6 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad32(
   L.S2 = p;  p += kFS;
   carve_small(L, p);
   const int lane0 = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const Net C0 = net_of(cflat, kCLd, 1);
   const uint64_t call = (uint64_t)*call_ctr;
   if (blockIdx.x == 0 && threadIdx.x < n_steps) step_ctr[threadIdx.x] += 1.0f;  // Adam's step (read by k_adam_flat)
   f32x16 gW2[4], gW1 = {0};
@@ -304,7 +303,7 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad32(
     const int64_t row0 = ((int64_t)blockIdx.x * sub_per_wg + sub) * 32;
     if (row0 >= B) break;  // uniform across the workgroup
     const int lane = launder_lane(lane0);
-    const Net C = launder(C0);
+    const Net C = net_of(launder(cflat), kCLd, 1);
     stage_states(L.S, Sg, row0, B);
     if (threadIdx.x < 64) L.A[threadIdx.x] = row0 + (threadIdx.x >> 1) < B ? Ag[row0 * 2 + threadIdx.x] : 0.f;
     if (taflat) {
@@ -316,7 +315,7 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad32(
       }
       __syncthreads();
       // ---- bootstrap target: mu'(s') then Q'(s', mu'(s')), inference
-      const Net TA = launder(net_of(taflat, kALd, 2)), TC = launder(net_of(tcflat, kCLd, 1));
+      const Net TA = net_of(launder(taflat), kALd, 2), TC = net_of(launder(tcflat), kCLd, 1);
       layer1_relu(L.S2, TA, L.H1, w, lane);
       __syncthreads();
       {
@@ -502,7 +501,6 @@ __global__ void __launch_bounds__(kThreads) k_actor_grad32(const float* __restri
   L.XCH = p; p += kFX;
   carve_small(L, p);
   const int lane0 = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const Net A0 = net_of(aflat, kALd, 2), C0 = net_of(cflat, kCLd, 1);
   if (blockIdx.x == 0 && threadIdx.x < n_steps) step_ctr[threadIdx.x] += 1.0f;
   f32x16 gW2[4], gW1 = {0};
 #pragma unroll
@@ -513,7 +511,7 @@ __global__ void __launch_bounds__(kThreads) k_actor_grad32(const float* __restri
     const int64_t row0 = ((int64_t)blockIdx.x * sub_per_wg + sub) * 32;
     if (row0 >= B) break;
     const int lane = launder_lane(lane0);
-    const Net A = launder(A0), C = launder(C0);
+    const Net A = net_of(launder(aflat), kALd, 2), C = net_of(launder(cflat), kCLd, 1);
     stage_states(L.S, Sg, row0, B);
     __syncthreads();
     layer1_relu(L.S, A, L.H1, w, lane);
