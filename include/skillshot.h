@@ -397,16 +397,18 @@ int sk_adam_flat_packed(const float* partials, int32_t n_partials, int32_t n_par
  *                         (model_act*, :215-281); noise_sd != 0 samples the
  *                         parameter noise w -> w (1 + noise_sd N(0,1)) per row
  *                         by local reparameterisation, keyed by (seed, row,
- *                         unit, call); call_counter (nullable; uint64[2] =
- *                         {call, 0}) is read and advanced on device as by
- *                         sk_actor_forward_advance.
+ *                         unit, call); action_sd != 0 adds N(0, action_sd) to
+ *                         the tanh outputs (model_act_action_noise, :229-243);
+ *                         call_counter (nullable; uint64[2] = {call, 0}) is
+ *                         read and advanced on device by every noisy launch,
+ *                         as by sk_actor_forward_advance.
  *   sk_critic_grad_f32    as sk_critic_grad_bootstrap (target_actor_flat NULL:
  *                         y = targets; else y = rewards + gamma (1 - done)
  *                         Q'(next_obs, mu'(next_obs)) from the target nets).
  *   sk_actor_grad_f32     as sk_actor_grad. */
 int64_t sk_update_partials_f32(int64_t batch);
 int sk_actor_forward_f32(const float* actor_flat, const float* obs, float* actions, int64_t rows, float noise_sd,
-                         uint64_t seed, uint64_t* call_counter, void* stream);
+                         float action_sd, uint64_t seed, uint64_t* call_counter, void* stream);
 int sk_critic_grad_f32(const float* critic_flat, const float* obs, const float* actions, const float* targets,
                        const float* next_obs, const float* rewards, const float* done, float gamma,
                        const float* target_actor_flat, const float* target_critic_flat, int64_t batch,

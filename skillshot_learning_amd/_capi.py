@@ -136,7 +136,7 @@ def load(build_if_missing=True):
         "sk_critic_grad_bootstrap": ([P, P, P, P, P, P, P, f32, P, P, i64, i64, f32, u64, P, P, P, i32, P, P, P],
                                      ctypes.c_int),
         "sk_update_partials_f32": ([i64], ctypes.c_int64),
-        "sk_actor_forward_f32": ([P, P, P, i64, f32, u64, P, P], ctypes.c_int),
+        "sk_actor_forward_f32": ([P, P, P, i64, f32, f32, u64, P, P], ctypes.c_int),
         "sk_critic_grad_f32": ([P, P, P, P, P, P, P, f32, P, P, i64, i64, f32, u64, P, P, P, i32, P, P, P],
                                ctypes.c_int),
         "sk_actor_grad_f32": ([P, P, P, i64, f32, P, P, i32, P, P], ctypes.c_int),

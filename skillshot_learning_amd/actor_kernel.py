@@ -90,9 +90,12 @@ class ActorKernel32:
         from .update_kernel import flatten_module
         self.flat = flatten_module(self.actor)  # idempotent: the parameters stay views of it
 
+    fused_action_noise = True  # model_act_action_noise's N(0, sd) is drawn in the kernel
+
     @torch.no_grad()
-    def __call__(self, obs, noise_sd=0.0, generator=None, out=None):
-        """obs float32 [M, 12] -> actions float32 [M, 2]."""
+    def __call__(self, obs, noise_sd=0.0, generator=None, out=None, action_sd=0.0):
+        """obs float32 [M, 12] -> actions float32 [M, 2]; noise_sd: parameter
+        noise, action_sd: action noise on the tanh outputs."""
         x = obs if obs.dtype == torch.float32 else obs.float()
         x = x.contiguous()
         if x.dim() != 2 or x.shape[1] != 12:
@@ -101,8 +104,8 @@ class ActorKernel32:
         y = out if out is not None else torch.empty((m, 2), dtype=torch.float32, device=self.device)
         self.calls += 1
         rc = self.L.sk_actor_forward_f32(ctypes.c_void_p(self.flat.data_ptr()), ctypes.c_void_p(x.data_ptr()),
-                                         ctypes.c_void_p(y.data_ptr()), m, float(noise_sd), self.seed,
-                                         ctypes.c_void_p(self._ctr.data_ptr()), self._stream())
+                                         ctypes.c_void_p(y.data_ptr()), m, float(noise_sd), float(action_sd),
+                                         self.seed, ctypes.c_void_p(self._ctr.data_ptr()), self._stream())
         if rc != 0:
             raise SkillshotError(f"sk_actor_forward_f32 failed ({rc})")
         return y

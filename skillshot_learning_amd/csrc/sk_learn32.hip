@@ -100,8 +100,37 @@ __device__ __forceinline__ uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
 // ------------------------------------------------------------------ GEMM tiles
 // acc[i][j] += sum_{k0 <= k < k0+kc} X[i][k] W[n0 + j][k]: X in LDS row-major,
 // W global row-major (ldw); kc a multiple of 8
+// Software-pipelined: the weight loads of the next 4 steps (32 k) are in
+// flight while the MFMAs of the current 4 run (the weights come from L2 and
+// would otherwise stall both waves of a SIMD at every batch).
+template <int KC>
+__device__ __forceinline__ f32x16 gemm_xwT_p(f32x16 acc, const float* X, int ldx, const float* W, int ldw, int n0,
+                                             int k0, int lane) {
+  static_assert(KC % 32 == 0, "KC: multiple of 32");
+  const int i = lane & 31, h = lane >> 5;
+  const float* xr = X + i * ldx + k0 + 4 * h;
+  const float* wr = W + (size_t)(n0 + i) * ldw + k0 + 4 * h;
+  f4 wn[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) wn[t] = *(const f4u*)(wr + 8 * t);
+#pragma unroll
+  for (int k = 0; k < KC; k += 32) {
+    f4 wc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) wc[t] = wn[t];
+    if (k + 32 < KC) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) wn[t] = *(const f4u*)(wr + k + 32 + 8 * t);
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc = mf4(*(const f4*)(xr + k + 8 * t), wc[t], acc);
+  }
+  return acc;
+}
 __device__ __forceinline__ f32x16 gemm_xwT(f32x16 acc, const float* X, int ldx, const float* W, int ldw, int n0,
                                            int k0, int kc, int lane) {
+  if (kc == 128) return gemm_xwT_p<128>(acc, X, ldx, W, ldw, n0, k0, lane);
+  if (kc == 256) return gemm_xwT_p<256>(acc, X, ldx, W, ldw, n0, k0, lane);
   const int i = lane & 31, h = lane >> 5;
   const float* xr = X + i * ldx + k0 + 4 * h;
   const float* wr = W + (size_t)(n0 + i) * ldw + k0 + 4 * h;
@@ -109,19 +138,20 @@ __device__ __forceinline__ f32x16 gemm_xwT(f32x16 acc, const float* X, int ldx, 
   for (int k = 0; k < kc; k += 8) acc = mf4(*(const f4*)(xr + k), *(const f4u*)(wr + k), acc);
   return acc;
 }
-// the same with squared operands: the variance GEMM of parameter noise
-__device__ __forceinline__ f32x16 gemm_xwT_sq(f32x16 acc, const float* X, int ldx, const float* W, int ldw, int n0,
-                                              int k0, int kc, int lane) {
+// mean and variance GEMMs of parameter noise in one pass: every operand load
+// feeds both (x w and x^2 w^2: two independent accumulator chains per wave)
+__device__ __forceinline__ void gemm_xwT_mv(f32x16& m, f32x16& v, const float* X, int ldx, const float* W, int ldw,
+                                            int n0, int k0, int kc, int lane) {
   const int i = lane & 31, h = lane >> 5;
   const float* xr = X + i * ldx + k0 + 4 * h;
   const float* wr = W + (size_t)(n0 + i) * ldw + k0 + 4 * h;
-#pragma unroll 8
+#pragma unroll 4
   for (int k = 0; k < kc; k += 8) {
     const f4 x = *(const f4*)(xr + k);
     const f4 w = *(const f4u*)(wr + k);
-    acc = mf4(x * x, w * w, acc);
+    m = mf4(x, w, m);
+    v = mf4(x * x, w * w, v);
   }
-  return acc;
 }
 // layer 1 (K = 12): k 0..7 by both halves, k 8..11 by half 0 (half 1's
 // 12..15 are zero operands, never loaded)
@@ -152,10 +182,24 @@ __device__ __forceinline__ f32x16 gemm_xw(f32x16 acc, const float* DZ, int ldz, 
   const int i = lane & 31, h = lane >> 5;
   const float* zr = DZ + i * ldz + k0 + 4 * h;
   const float* wc = W + (size_t)(k0 + 4 * h) * ldw + n0 + i;
-#pragma unroll 4
-  for (int k = 0; k < kc; k += 8) {
-    const f4 b = {wc[(k + 0) * ldw], wc[(k + 1) * ldw], wc[(k + 2) * ldw], wc[(k + 3) * ldw]};
-    acc = mf4(*(const f4*)(zr + k), b, acc);
+  // pipelined as gemm_xwT_p: 4 steps (16 column loads) in flight ahead
+  f4 bn[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+    bn[t] = f4{wc[(8 * t + 0) * ldw], wc[(8 * t + 1) * ldw], wc[(8 * t + 2) * ldw], wc[(8 * t + 3) * ldw]};
+  for (int k = 0; k < kc; k += 32) {
+    f4 bc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) bc[t] = bn[t];
+    if (k + 32 < kc) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int r = k + 32 + 8 * t;
+        bn[t] = f4{wc[(r + 0) * ldw], wc[(r + 1) * ldw], wc[(r + 2) * ldw], wc[(r + 3) * ldw]};
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc = mf4(*(const f4*)(zr + k + 8 * t), bc[t], acc);
   }
   return acc;
 }
@@ -658,7 +702,7 @@ __device__ __forceinline__ void normals4(uint64_t seed, uint64_t call, uint32_t 
 template <bool NOISE>
 __global__ void __launch_bounds__(kFwdThreads) k_actor_fwd32(const float* __restrict__ aflat,
                                                              const float* __restrict__ X, float* __restrict__ out,
-                                                             int64_t rows, float sd, uint64_t seed,
+                                                             int64_t rows, float sd, float action_sd, uint64_t seed,
                                                              uint64_t* __restrict__ call_ctr) {
   __shared__ __attribute__((aligned(16))) float S[32 * kLdS];
   __shared__ __attribute__((aligned(16))) float H1[32 * kLdH1];
@@ -666,7 +710,10 @@ __global__ void __launch_bounds__(kFwdThreads) k_actor_fwd32(const float* __rest
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const Net A = net_of(aflat, kALd, 2);
   const int64_t row0 = (int64_t)blockIdx.x * 32;
-  const uint64_t call = NOISE && call_ctr ? call_ctr[0] + 1 : 0;
+  // a launch that draws noise (parameter or action) uses call number
+  // counter + 1 and its last workgroup stores that number back
+  const bool draws = (NOISE || action_sd != 0.f) && call_ctr;
+  const uint64_t call = draws ? call_ctr[0] + 1 : 0;
   stage_states(S, X, row0, rows);
   __syncthreads();
 #pragma unroll
@@ -695,12 +742,11 @@ __global__ void __launch_bounds__(kFwdThreads) k_actor_fwd32(const float* __rest
   __syncthreads();
   {
     const int u = 32 * w + (lane & 31);
-    f32x16 m = {0};
-    m = gemm_xwT(m, H1, kLdH1, A.W2, kALd, 32 * w, 0, kH1, lane);
+    f32x16 m = {0}, var = {0};
+    if (NOISE) gemm_xwT_mv(m, var, H1, kLdH1, A.W2, kALd, 32 * w, 0, kH1, lane);
+    else m = gemm_xwT(m, H1, kLdH1, A.W2, kALd, 32 * w, 0, kH1, lane);
     const float b = A.b2[u];
     if (NOISE) {
-      f32x16 var = {0};
-      var = gemm_xwT_sq(var, H1, kLdH1, A.W2, kALd, 32 * w, 0, kH1, lane);
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         float z[4];
@@ -749,10 +795,17 @@ __global__ void __launch_bounds__(kFwdThreads) k_actor_fwd32(const float* __rest
         y0 += sd * __builtin_amdgcn_sqrtf(v0 + A.b3[0] * A.b3[0]) * z[0];
         y1 += sd * __builtin_amdgcn_sqrtf(v1 + A.b3[1] * A.b3[1]) * z[1];
       }
-      *(float2*)(out + (row0 + i) * 2) = make_float2(tanhf(y0), tanhf(y1));
+      float o0 = tanhf(y0), o1 = tanhf(y1);
+      if (action_sd != 0.f) {  // model_act_action_noise (:229-243): tanh output + N(0, sd), unclipped
+        float z[4];
+        normals4(seed, call, (uint32_t)(row0 + i), (uint32_t)(kH1 + kH2 + 1), z);
+        o0 += action_sd * z[0];
+        o1 += action_sd * z[1];
+      }
+      *(float2*)(out + (row0 + i) * 2) = make_float2(o0, o1);
     }
   }
-  if (NOISE && call_ctr) {  // the last workgroup to finish stores the call number it drew with
+  if (draws) {  // the last workgroup to finish stores the call number it drew with
     __syncthreads();
     if (threadIdx.x == 0) {
       const unsigned long long prev =
@@ -830,16 +883,16 @@ int sk_actor_grad_f32(const float* actor_flat, const float* critic_flat, const f
 }
 
 int sk_actor_forward_f32(const float* actor_flat, const float* obs, float* actions, int64_t rows, float noise_sd,
-                         uint64_t seed, uint64_t* call_counter, void* stream) {
+                         float action_sd, uint64_t seed, uint64_t* call_counter, void* stream) {
   if (!actor_flat || !obs || !actions || rows <= 0) return SK_EINVAL;
   if ((((uintptr_t)actions) & 7)) return SK_EINVAL;
   const unsigned G = (unsigned)((rows + 31) / 32);
   if (noise_sd != 0.f)
-    k_actor_fwd32<true><<<G, kFwdThreads, 0, (hipStream_t)stream>>>(actor_flat, obs, actions, rows, noise_sd, seed,
-                                                                      call_counter);
+    k_actor_fwd32<true><<<G, kFwdThreads, 0, (hipStream_t)stream>>>(actor_flat, obs, actions, rows, noise_sd,
+                                                                      action_sd, seed, call_counter);
   else
-    k_actor_fwd32<false><<<G, kFwdThreads, 0, (hipStream_t)stream>>>(actor_flat, obs, actions, rows, 0.f, seed,
-                                                                       nullptr);
+    k_actor_fwd32<false><<<G, kFwdThreads, 0, (hipStream_t)stream>>>(actor_flat, obs, actions, rows, 0.f, action_sd,
+                                                                       seed, call_counter);
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
 }
 

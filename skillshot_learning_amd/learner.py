@@ -695,6 +695,8 @@ class SkillshotLearner:
                 a = self.actor_kernel(x, noise_sd=self.param_noise_sd, generator=self.gen)
             else:
                 a = self.model_actor.forward_param_noise(x, self.param_noise_sd, generator=self.gen)
+        elif mode == "action_noise" and getattr(self.actor_kernel, "fused_action_noise", False):
+            a = self.actor_kernel(x, action_sd=self.action_noise_sd)
         else:
             a = self.actor_kernel(x) if self.actor_kernel is not None else self.model_actor(x)
             if mode == "action_noise":
@@ -986,7 +988,10 @@ class TickGraph:
         x = obs.view(-1, STATE_DIM)
         a = self.act.view(-1, ACTION_DIM)
         mode = L.exploration
-        if L.actor_kernel is not None:
+        if L.actor_kernel is not None and mode == "action_noise" and getattr(L.actor_kernel, "fused_action_noise",
+                                                                               False):
+            L.actor_kernel(x, out=a, action_sd=L.action_noise_sd)
+        elif L.actor_kernel is not None:
             L.actor_kernel(x, noise_sd=L.param_noise_sd if mode == "param_noise" else 0.0, out=a)
             if mode == "action_noise":
                 a.add_(L.action_noise_sd * torch.randn(a.shape, device=a.device, generator=L.gen))

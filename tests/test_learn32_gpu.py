@@ -220,3 +220,23 @@ def test_f32_learner_tick_graph(mods):
     assert all(bool(torch.isfinite(p).all()) for m in (L.model_actor, L.model_critic) for p in m.parameters())
     assert any((p - q).abs().max() > 0 for p, q in zip(L.model_actor.parameters(), w0))
     assert bool(torch.isfinite(tg.act).all()) and float(tg.act.abs().max()) <= 1.0
+
+
+def test_actor_forward_f32_action_noise(mods):
+    """model_act_action_noise (:229-243): the tanh outputs + N(0, 0.15) drawn
+    in the kernel; the call counter advances per launch (fresh draws on every
+    replay of a captured tick)"""
+    learner, _ = mods
+    from skillshot_learning_amd.actor_kernel import ActorKernel32
+    d = _ddpg(learner, seed=9)
+    k = ActorKernel32(d.model_actor, seed=5)
+    x = _obs(65536, 9)
+    clean = k(x)
+    a1 = k(x, action_sd=0.15)
+    a2 = k(x, action_sd=0.15)
+    torch.cuda.synchronize()
+    assert int(k._ctr[0]) == 2
+    z = ((a1 - clean) / 0.15).double().cpu().flatten()
+    assert abs(float(z.mean())) < 0.01 and abs(float(z.std()) - 1.0) < 0.01
+    assert abs(float((z.abs() < 1).double().mean()) - 0.6827) < 0.01  # normal, not uniform
+    assert not torch.equal(a1, a2)
