@@ -1,0 +1,44 @@
+"""Device time of the actor forward kernels (fp32 sk_actor_forward_f32, bf16
+sk_actor_forward_advance) with and without parameter noise, per row count
+(rows = 2 x games: both players), HIP events over --iters launches."""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from skillshot_learning_amd.actor_kernel import ActorKernel, ActorKernel32  # noqa: E402
+from skillshot_learning_amd.learner import Actor  # noqa: E402
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--rows", default="8192,131072")
+    p.add_argument("--iters", type=int, default=50)
+    a = p.parse_args()
+    torch.manual_seed(0)
+    actor = Actor().cuda()
+    kernels = {"fp32": ActorKernel32(actor, seed=1), "bf16": ActorKernel(actor, seed=1)}
+    for rows in [int(r) for r in a.rows.split(",")]:
+        x = torch.rand(rows, 12, device="cuda")
+        out = torch.empty(rows, 2, device="cuda")
+        for prec, k in kernels.items():
+            for sd in (0.0, 0.5):
+                for _ in range(3):
+                    k(x, noise_sd=sd, out=out)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.iters):
+                    k(x, noise_sd=sd, out=out)
+                e1.record()
+                torch.cuda.synchronize()
+                us = e0.elapsed_time(e1) * 1e3 / a.iters
+                flop = 72192 * rows * (2 if sd else 1)  # 2 x MACs of 12x256 + 256x128 + 128x2; noise doubles
+                print(json.dumps(dict(precision=prec, rows=rows, param_noise=sd, us=us,
+                                      tflops=flop / (us * 1e-6) / 1e12)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
