@@ -118,6 +118,7 @@ __global__ void __launch_bounds__(threads_for<NOISE>()) k_actor_fwd(const float*
   if (NOISE && call_dev) call = *call_dev;  // wave-uniform scalar load
   if (NOISE && adv) call = adv[0] + 1;
   asm volatile("" : "+s"(call));  // read before the staging barrier (advance_call relies on it)
+  const float k2 = noise_k2(sd);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16x8* sW2 = (bf16x8*)smem;                               // [4][16][64]
   bf16x8* sW2s = (bf16x8*)(smem + kW2Frag);                  // NOISE only
@@ -178,13 +179,12 @@ __global__ void __launch_bounds__(threads_for<NOISE>()) k_actor_fwd(const float*
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gW1[c * 64 + lane], xb, acc, 0, 0, 0);
       if (NOISE) var = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gW1s[c * 64 + lane], xs, var, 0, 0, 0);
       float z[16];
-      if (NOISE) normals16(seed, call, (uint32_t)row, (uint32_t)c, h, z);
+      if (NOISE) normals16(seed, call, (uint32_t)row, (uint32_t)c, h, k2, z);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int hid = 32 * c + (i & 3) + 8 * (i >> 2) + 4 * h;
         const float b = sB[hid];
-        float y = acc[i] + b;
-        if (NOISE) y += sd * __builtin_amdgcn_sqrtf(fmaxf(var[i] + b * b, 0.f)) * z[i];
+        float y = NOISE ? noisy_pre(acc[i], b, var[i], z[i]) : acc[i] + b;
         y = fmaxf(y, 0.f);
         acc[i] = y;
         if (DBG && valid) dbg[row * kDbgCols + hid] = y;
@@ -216,25 +216,25 @@ __global__ void __launch_bounds__(threads_for<NOISE>()) k_actor_fwd(const float*
         if (NOISE && (kk & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // cap hoisted LDS fragments
       }
       float z[16];
-      if (NOISE) normals16(seed, call, (uint32_t)row, (uint32_t)(8 + t), h, z);
+      if (NOISE) normals16(seed, call, (uint32_t)row, (uint32_t)(8 + t), h, k2, z);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int hid = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
         const float b = sB[kH1 + hid];
-        float y = acc[i] + b;
-        if (NOISE) y += sd * __builtin_amdgcn_sqrtf(fmaxf(var[i] + b * b, 0.f)) * z[i];
+        float y = NOISE ? noisy_pre(acc[i], b, var[i], z[i]) : acc[i] + b;
         y = fmaxf(y, 0.f);
         if (DBG && valid) {
           dbg[row * kDbgCols + kH1 + hid] = y;
           dbg[row * kDbgCols + 386 + hid] = acc[i];
           dbg[row * kDbgCols + 386 + kH2 + hid] = NOISE ? var[i] : 0.f;
-          dbg[row * kDbgCols + 386 + 2 * kH2 + hid] = NOISE ? z[i] : 0.f;
+          dbg[row * kDbgCols + 386 + 2 * kH2 + hid] = NOISE ? z[i] / sd : 0.f;
         }
-        m0 += sW3[hid] * y;
-        m1 += sW3[kH2 + hid] * y;
+        m0 = __builtin_fmaf(sW3[hid], y, m0);
+        m1 = __builtin_fmaf(sW3[kH2 + hid], y, m1);
         if (NOISE) {
-          q0 += sW3[2 * kH2 + hid] * (y * y);
-          q1 += sW3[3 * kH2 + hid] * (y * y);
+          const float yy = y * y;
+          q0 = __builtin_fmaf(sW3[2 * kH2 + hid], yy, q0);
+          q1 = __builtin_fmaf(sW3[3 * kH2 + hid], yy, q1);
         }
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -249,14 +249,13 @@ __global__ void __launch_bounds__(threads_for<NOISE>()) k_actor_fwd(const float*
     // ---- layer 3 epilogue: a = tanh(W3 h2 + b3 [+ noise]) for this lane's row
     if (h == 0 && valid) {
       float z[16];
-      if (NOISE) normals16(seed, call, (uint32_t)row, 12u, h, z);
+      if (NOISE) normals16(seed, call, (uint32_t)row, 12u, h, k2, z);
       const float mm[2] = {m0, m1}, qq[2] = {q0, q1};
       float o[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const float b = sB[kH1 + kH2 + i];
-        float y = mm[i] + b;
-        if (NOISE) y += sd * __builtin_amdgcn_sqrtf(fmaxf(qq[i] + b * b, 0.f)) * z[i];
+        const float y = NOISE ? noisy_pre(mm[i], b, qq[i], z[i]) : mm[i] + b;
         if (DBG) dbg[row * kDbgCols + kH1 + kH2 + i] = y;
         o[i] = tanhf(y);
       }
@@ -293,6 +292,7 @@ __global__ void __launch_bounds__(kWgThreads) k_actor_fwd_wg(const float* __rest
   if (NOISE && call_dev) call = *call_dev;
   if (NOISE && adv) call = adv[0] + 1;
   asm volatile("" : "+s"(call));  // read before the staging barrier (advance_call)
+  const float k2 = noise_k2(sd);
   {
     const uint4* g = (const uint4*)(packed + kOffW2);
     uint4* sm = (uint4*)smem;
@@ -336,13 +336,12 @@ __global__ void __launch_bounds__(kWgThreads) k_actor_fwd_wg(const float* __rest
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gW1[c * 64 + lane], xb, acc, 0, 0, 0);
       if (NOISE) var = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gW1s[c * 64 + lane], xs, var, 0, 0, 0);
       float z[16];
-      if (NOISE) normals16(seed, call, (uint32_t)row, (uint32_t)c, h, z);
+      if (NOISE) normals16(seed, call, (uint32_t)row, (uint32_t)c, h, k2, z);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int hid = 32 * c + (i & 3) + 8 * (i >> 2) + 4 * h;
         const float b = sB[hid];
-        float y = acc[i] + b;
-        if (NOISE) y += sd * __builtin_amdgcn_sqrtf(fmaxf(var[i] + b * b, 0.f)) * z[i];
+        float y = NOISE ? noisy_pre(acc[i], b, var[i], z[i]) : acc[i] + b;
         acc[i] = fmaxf(y, 0.f);
       }
 #pragma unroll
@@ -367,19 +366,19 @@ __global__ void __launch_bounds__(kWgThreads) k_actor_fwd_wg(const float* __rest
           var = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sW2s[(t * 16 + kk) * 64 + lane], sq_bf16(hb), var, 0, 0, 0);
       }
       float z[16];
-      if (NOISE) normals16(seed, call, (uint32_t)row, (uint32_t)(8 + t), h, z);
+      if (NOISE) normals16(seed, call, (uint32_t)row, (uint32_t)(8 + t), h, k2, z);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int hid = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
         const float b = sB[kH1 + hid];
-        float y = acc[i] + b;
-        if (NOISE) y += sd * __builtin_amdgcn_sqrtf(fmaxf(var[i] + b * b, 0.f)) * z[i];
+        float y = NOISE ? noisy_pre(acc[i], b, var[i], z[i]) : acc[i] + b;
         y = fmaxf(y, 0.f);
-        m0 += sW3[hid] * y;
-        m1 += sW3[kH2 + hid] * y;
+        m0 = __builtin_fmaf(sW3[hid], y, m0);
+        m1 = __builtin_fmaf(sW3[kH2 + hid], y, m1);
         if (NOISE) {
-          q0 += sW3[2 * kH2 + hid] * (y * y);
-          q1 += sW3[3 * kH2 + hid] * (y * y);
+          const float yy = y * y;
+          q0 = __builtin_fmaf(sW3[2 * kH2 + hid], yy, q0);
+          q1 = __builtin_fmaf(sW3[3 * kH2 + hid], yy, q1);
         }
       }
     }
@@ -400,14 +399,13 @@ __global__ void __launch_bounds__(kWgThreads) k_actor_fwd_wg(const float* __rest
         p.x += o.x; p.y += o.y; p.z += o.z; p.w += o.w;
       }
       float z[16];
-      if (NOISE) normals16(seed, call, (uint32_t)row, 12u, 0, z);
+      if (NOISE) normals16(seed, call, (uint32_t)row, 12u, 0, k2, z);
       const float mm[2] = {p.x, p.y}, qq[2] = {p.z, p.w};
       float o2[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const float b = sB[kH1 + kH2 + i];
-        float y = mm[i] + b;
-        if (NOISE) y += sd * __builtin_amdgcn_sqrtf(fmaxf(qq[i] + b * b, 0.f)) * z[i];
+        const float y = NOISE ? noisy_pre(mm[i], b, qq[i], z[i]) : mm[i] + b;
         o2[i] = tanhf(y);
       }
       *(float2*)(out + row * kOut) = make_float2(o2[0], o2[1]);

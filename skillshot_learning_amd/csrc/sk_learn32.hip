@@ -88,14 +88,32 @@ __device__ __forceinline__ int drow(int v, int lane) { return 8 * (v >> 2) + 4 *
 __device__ __forceinline__ uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
-    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
-    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
-    c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+    const uint64_t p0 = (uint64_t)c.x * 0xD2511F53u, p1 = (uint64_t)c.z * 0xCD9E8D57u;  // v_mad_u64_u32
+    c = make_uint4(__builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c.y, k0, 0x96), (uint32_t)p1,
+                   __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c.w, k1, 0x96), (uint32_t)p0);
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
   }
   return c;
 }
+
+// Phase timestamps of the first and last workgroup (diagnostic builds only:
+// -DSK_TRACE32, read back with sk_debug_trace32; tools/trace_learn32.py)
+#ifdef SK_TRACE32
+__device__ unsigned long long g_sk_trace32[2][32][2];
+#define TP32(k)                                                                              \
+  do {                                                                                       \
+    if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1)) {              \
+      const int wg_ = blockIdx.x == 0 ? 0 : 1;                                               \
+      g_sk_trace32[wg_][k][0] = __builtin_amdgcn_s_memtime();                                \
+      g_sk_trace32[wg_][k][1] = wall_clock64();                                              \
+    }                                                                                        \
+  } while (0)
+#else
+#define TP32(k) \
+  do {          \
+  } while (0)
+#endif
 
 // ------------------------------------------------------------------ GEMM tiles
 // acc[i][j] += sum_{k0 <= k < k0+kc} X[i][k] W[n0 + j][k]: X in LDS row-major,
@@ -343,6 +361,7 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad32(
   // per-unit sums over rows: thread t < 256 owns b1[t]; t < 128 b2, W2 action columns, W3
   float gb1 = 0.f, gb2 = 0.f, gwa0 = 0.f, gwa1 = 0.f, gw3 = 0.f, gb3 = 0.f, lsum = 0.f;
   const int u2 = w & 3;  // layer-2 n-tile of this wave (waves 0..3 hold the sums)
+  TP32(0);
   for (int sub = 0; sub < sub_per_wg; ++sub) {
     const int64_t row0 = ((int64_t)blockIdx.x * sub_per_wg + sub) * 32;
     if (row0 >= B) break;  // uniform across the workgroup
@@ -358,6 +377,7 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad32(
         L.D[threadIdx.x] = ok ? Dg[row0 + threadIdx.x] : 0.f;
       }
       __syncthreads();
+      TP32(1);
       // ---- bootstrap target: mu'(s') then Q'(s', mu'(s')), inference
       const Net TA = net_of(launder(taflat), kALd, 2), TC = net_of(launder(tcflat), kCLd, 1);
       layer1_relu(L.S2, TA, L.H1, w, lane);
@@ -372,6 +392,7 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad32(
         }
       }
       __syncthreads();
+      TP32(2);
       actor_out(L.H2, TA, L.A2);
       layer1_relu(L.S2, TC, L.H1, w, lane);  // H1 was last read before the previous barrier
       __syncthreads();
@@ -393,6 +414,7 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad32(
         const int i = threadIdx.x >> 4;
         if ((threadIdx.x & 15) == 0) L.Y[i] = L.R[i] + gamma * (1.f - L.D[i]) * q2;
       }
+      TP32(3);
     } else if (threadIdx.x < 32) {
       L.Y[threadIdx.x] = row0 + threadIdx.x < B ? Yg[row0 + threadIdx.x] : 0.f;
     }
@@ -419,6 +441,7 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad32(
       }
     }
     __syncthreads();
+    TP32(4);
     // ---- layer 2 (+ the two action columns) -> h2
     {
       const f32x16 acc = layer2_split(L.H1, C, L.XCH, w, lane);
@@ -433,6 +456,7 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad32(
       }
     }
     __syncthreads();
+    TP32(5);
     // ---- q, dL/dq (rows beyond B: 0)
     {
       const float q = C.b3[0] + row_dot128(L.H2, kLdH2, C.W3, 1);
@@ -452,6 +476,7 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad32(
       L.DZ2[i * kLdH2 + u] = h > 0.f ? L.DQ[i] * C.W3[u] : 0.f;
     }
     __syncthreads();
+    TP32(6);
     if (threadIdx.x < kH2) {  // per-unit sums: b2, the action columns of W2, W3
       const int u = threadIdx.x;
       for (int i = 0; i < 32; ++i) {
@@ -480,12 +505,14 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad32(
       }
     }
     __syncthreads();
+    TP32(7);
     if (threadIdx.x < kH1) {
       for (int i = 0; i < 32; ++i) gb1 += L.DZ1[i * kLdH1 + threadIdx.x];
     }
     // ---- dW1[u][c] += sum_i dz1[i][u] s[i][c]: wave w, u-tile w (columns c >= 12 discarded)
     gW1 = gemm_wgrad(gW1, L.DZ1, kLdH1, 32 * w, L.S, kLdS, 0, lane);
     __syncthreads();  // the next sub-tile restages S / H1
+    TP32(8);
   }
   // ---- this workgroup's partial gradient (torch parameters() order)
   float* P = partial + (int64_t)blockIdx.x * kCP;
@@ -522,6 +549,7 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad32(
     P[pB3(kCLd, 1)] = L.RED[0];
     if (loss_out) atomicAdd(loss_out, L.RED[1]);
   }
+  TP32(9);
 }
 
 // ---------------------------------------------------------------- actor step
@@ -686,11 +714,9 @@ __device__ __forceinline__ void normals4(uint64_t seed, uint64_t call, uint32_t 
   for (int q = 0; q < 2; ++q) {
     const float u1 = ((float)(wd[2 * q] >> 8) + 0.5f) * 0x1p-24f;  // (0, 1)
     const float u2 = (float)(wd[2 * q + 1] >> 8) * 0x1p-24f;       // [0, 1)
-    const float rad = __builtin_amdgcn_sqrtf(-2.0f * __logf(u1));
-    float sn, cs;
-    __sincosf(6.283185307179586f * u2, &sn, &cs);
-    z[2 * q] = rad * cs;
-    z[2 * q + 1] = rad * sn;
+    const float rad = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));  // -2 ln u1
+    z[2 * q] = rad * __builtin_amdgcn_cosf(u2);  // v_cos_f32 / v_sin_f32 take revolutions
+    z[2 * q + 1] = rad * __builtin_amdgcn_sinf(u2);
   }
 }
 
@@ -730,7 +756,7 @@ __global__ void __launch_bounds__(kFwdThreads) k_actor_fwd32(const float* __rest
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int v = 4 * g + q;
-          const float y = m[v] + b + sd * __builtin_amdgcn_sqrtf(var[v] + b * b) * z[q];
+          const float y = __builtin_fmaf(sd * __builtin_amdgcn_sqrtf(__builtin_fmaf(b, b, var[v])), z[q], m[v] + b);
           H1[drow(v, lane) * kLdH1 + u] = fmaxf(y, 0.f);
         }
       }
@@ -754,7 +780,7 @@ __global__ void __launch_bounds__(kFwdThreads) k_actor_fwd32(const float* __rest
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int v = 4 * g + q;
-          const float y = m[v] + b + sd * __builtin_amdgcn_sqrtf(var[v] + b * b) * z[q];
+          const float y = __builtin_fmaf(sd * __builtin_amdgcn_sqrtf(__builtin_fmaf(b, b, var[v])), z[q], m[v] + b);
           H2[drow(v, lane) * kLdH2 + u] = fmaxf(y, 0.f);
         }
       }
@@ -897,3 +923,10 @@ int sk_actor_forward_f32(const float* actor_flat, const float* obs, float* actio
 }
 
 }  // extern "C"
+
+#ifdef SK_TRACE32
+// diagnostic builds only (not in include/skillshot.h): [2 wg][32 points][memtime, realtime]
+extern "C" int sk_debug_trace32(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sk_trace32), sizeof(g_sk_trace32)) == hipSuccess ? SK_OK : SK_EHIP;
+}
+#endif

@@ -62,23 +62,31 @@ template <int ROUNDS = 10>
 __device__ __forceinline__ uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int i = 0; i < ROUNDS; ++i) {
-    uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
-    uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
-    c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+    // one v_mad_u64_u32 gives both halves of each product (instead of a
+    // v_mul_lo_u32 + v_mul_hi_u32 pair), one v_bitop3_b32 (0x96: a^b^c) each xor
+    const uint64_t p0 = (uint64_t)c.x * 0xD2511F53u, p1 = (uint64_t)c.z * 0xCD9E8D57u;
+    c = make_uint4(__builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c.y, k0, 0x96), (uint32_t)p1,
+                   __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c.w, k1, 0x96), (uint32_t)p0);
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
   }
   return c;
 }
 
-// 16 standard normals for (row, stream, lane half h): Box-Muller on 2 Philox
-// draws, each 32-bit word split into a 16-bit radius uniform and a 16-bit
-// angle uniform (one word per normal pair; radius truncated at 4.86 sigma,
-// P = 1.2e-6).  The two lane halves hold different hidden units of the same
-// row, so h is part of the counter (independent noise per unit).  The RNG
-// was half of the noisy actor's VALU instructions (PMC, profiles/r01t_*).
+// 16 normals of standard deviation sd for (row, stream, lane half h):
+// Box-Muller on 2 Philox draws, each 32-bit word split into a 16-bit radius
+// uniform and a 16-bit angle uniform (one word per normal pair; radius
+// truncated at 4.86 sigma, P = 1.2e-6).  The two lane halves hold different
+// hidden units of the same row, so h is part of the counter (independent noise
+// per unit).  k2 = noise_k2(sd) = -2 ln2 sd^2 folds sd and ln -> log2 into the
+// radius: rad = sqrt(k2 log2 u1) on v_log_f32 (u1 >= 2^-17: no denormal
+// scaling), and the angle goes to v_sin_f32 / v_cos_f32 in revolutions, so a
+// pair costs ~10 VALU instructions.  The RNG was half of the noisy actor's
+// VALU instructions (PMC, profiles/r01t_*, r02_pmc_mfma_learner.json).
+__host__ __device__ __forceinline__ float noise_k2(float sd) { return -1.3862943611198906f * sd * sd; }
+
 __device__ __forceinline__ void normals16(uint64_t seed, uint64_t call, uint32_t row, uint32_t stream, int h,
-                                          float z[16]) {
+                                          float k2, float z[16]) {
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     uint4 u = philox(make_uint4(row, (stream * 2 + (uint32_t)h) * 2 + q, (uint32_t)call, (uint32_t)(call >> 32)),
@@ -86,15 +94,19 @@ __device__ __forceinline__ void normals16(uint64_t seed, uint64_t call, uint32_t
     uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-      float u1 = ((float)(w[p] & 0xFFFFu) + 0.5f) * 0x1p-16f;  // (0, 1)
-      float u2 = (float)(w[p] >> 16) * 0x1p-16f;               // [0, 1)
-      float rad = __builtin_amdgcn_sqrtf(-2.0f * __logf(u1));  // v_sqrt_f32 (1 ulp): noise scale
-      float sn, cs;
-      __sincosf(6.283185307179586f * u2, &sn, &cs);
-      z[8 * q + 2 * p] = rad * cs;
-      z[8 * q + 2 * p + 1] = rad * sn;
+      const float u1 = ((float)(w[p] & 0xFFFFu) + 0.5f) * 0x1p-16f;  // (0, 1)
+      const float rev = (float)(w[p] >> 16) * 0x1p-16f;               // [0, 1) revolutions
+      const float rad = __builtin_amdgcn_sqrtf(k2 * __builtin_amdgcn_logf(u1));
+      z[8 * q + 2 * p] = rad * __builtin_amdgcn_cosf(rev);
+      z[8 * q + 2 * p + 1] = rad * __builtin_amdgcn_sinf(rev);
     }
   }
+}
+
+// noisy pre-activation y = m + b + sqrt(v + b^2) * zs (zs already scaled by
+// sd).  v is a sum of products of squares (>= 0), so v + b^2 needs no clamp.
+__device__ __forceinline__ float noisy_pre(float m, float b, float v, float zs) {
+  return __builtin_fmaf(__builtin_amdgcn_sqrtf(__builtin_fmaf(b, b, v)), zs, m + b);
 }
 
 }  // namespace skmlp
