@@ -312,15 +312,20 @@ int sk_replay_sample(const float* ring, int64_t capacity, const int64_t* total, 
  *                   batch split over ranks as in the 1-rank batch), loss
  *                   sum_b (q_b - y_b)^2 * grad_scale / 2 (grad_scale = 2/B is
  *                   F.mse_loss), backward: per-workgroup gradient partials
- *                   float[sk_update_partials(batch)][36,609] in torch
- *                   parameters() order; loss_sum (nullable, device float,
+ *                   float[sk_update_partials(batch)][36,609] in the PARTIAL
+ *                   LAYOUT: torch parameters() order except W2 [128][258],
+ *                   stored as its 256 main columns [128][256] then the two
+ *                   action columns [128][2] (16-byte-aligned rows for the
+ *                   stores; csrc/sk_partial.hpp); loss_sum (nullable, device float,
  *                   accumulated) += sum (q - y)^2; dropout_mask (nullable)
  *                   receives uint8[batch][256] keep flags (tests)
  *   sk_actor_grad   actor forward, critic forward at inference, backward of
  *                   -loss_scale * sum_b Q(s_b, mu(s_b)) to the actor:
  *                   partials float[sk_update_partials(batch)][36,482];
  *                   q_sum (nullable) += sum_b Q
- *   sk_adam_flat    g = grad_in (nullable) + sum of n_partials partials ->
+ *   sk_adam_flat    g = grad_in (nullable) + sum of n_partials partials (in
+ *                   the partial layout when n_params is the critic's 36,609;
+ *                   grad_in, grad_out and the rest are flat parameter order) ->
  *                   grad_out (nullable); if apply: Keras Adam (epsilon added
  *                   to sqrt(v) before the bias correction, SkillshotLearner.py
  *                   :68) on flat param / exp_avg / exp_avg_sq with

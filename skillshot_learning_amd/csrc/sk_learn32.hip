@@ -30,6 +30,7 @@
 #include <stdint.h>
 
 #include "../../include/skillshot.h"
+#include "sk_partial.hpp"
 
 namespace {
 
@@ -52,14 +53,20 @@ __host__ __device__ constexpr int pW3(int ld2) { return pB2(ld2) + kH2; }
 __host__ __device__ constexpr int pB3(int ld2, int n_out) { return pW3(ld2) + n_out * kH2; }
 constexpr int kCLd = kH1 + 2, kALd = kH1;
 constexpr int kCP = pB3(kCLd, 1) + 1, kAP = pB3(kALd, 2) + 2;
-static_assert(kCP == 36609 && kAP == 36482, "parameter counts");
+static_assert(kCP == 36609 && kAP == 36482 && kCP == skpart::kCriticParams && kPW2 == skpart::kPW2, "parameter counts");
 
+// Weights are read through GLOBAL-address-space pointers: laundered (below)
+// generic pointers would become FLAT loads, which count on lgkmcnt too, so
+// every LDS wait would also wait for the in-flight weight loads
+typedef const __attribute__((address_space(1))) float* gfp;
+typedef const __attribute__((address_space(1))) f4u* gf4u;
 struct Net {  // views into one flat parameter vector
-  const float *W1, *b1, *W2, *b2, *W3, *b3;
+  gfp W1, b1, W2, b2, W3, b3;
   int ld2;
 };
 __device__ __forceinline__ Net net_of(const float* f, int ld2, int n_out) {
-  return Net{f + kPW1, f + kPB1, f + kPW2, f + pB2(ld2), f + pW3(ld2), f + pB3(ld2, n_out), ld2};
+  const gfp g = (gfp)f;
+  return Net{g + kPW1, g + kPB1, g + kPW2, g + pB2(ld2), g + pW3(ld2), g + pB3(ld2, n_out), ld2};
 }
 
 // Re-derive a net's bases (and the lane id) inside a sub-tile loop: without
@@ -122,15 +129,15 @@ __device__ unsigned long long g_sk_trace32[2][32][2];
 // flight while the MFMAs of the current 4 run (the weights come from L2 and
 // would otherwise stall both waves of a SIMD at every batch).
 template <int KC>
-__device__ __forceinline__ f32x16 gemm_xwT_p(f32x16 acc, const float* X, int ldx, const float* W, int ldw, int n0,
+__device__ __forceinline__ f32x16 gemm_xwT_p(f32x16 acc, const float* X, int ldx, gfp W, int ldw, int n0,
                                              int k0, int lane) {
   static_assert(KC % 32 == 0, "KC: multiple of 32");
   const int i = lane & 31, h = lane >> 5;
   const float* xr = X + i * ldx + k0 + 4 * h;
-  const float* wr = W + (size_t)(n0 + i) * ldw + k0 + 4 * h;
+  const gfp wr = W + (size_t)(n0 + i) * ldw + k0 + 4 * h;
   f4 wn[4];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) wn[t] = *(const f4u*)(wr + 8 * t);
+  for (int t = 0; t < 4; ++t) wn[t] = *(gf4u)(wr + 8 * t);
 #pragma unroll
   for (int k = 0; k < KC; k += 32) {
     f4 wc[4];
@@ -138,35 +145,35 @@ __device__ __forceinline__ f32x16 gemm_xwT_p(f32x16 acc, const float* X, int ldx
     for (int t = 0; t < 4; ++t) wc[t] = wn[t];
     if (k + 32 < KC) {
 #pragma unroll
-      for (int t = 0; t < 4; ++t) wn[t] = *(const f4u*)(wr + k + 32 + 8 * t);
+      for (int t = 0; t < 4; ++t) wn[t] = *(gf4u)(wr + k + 32 + 8 * t);
     }
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc = mf4(*(const f4*)(xr + k + 8 * t), wc[t], acc);
   }
   return acc;
 }
-__device__ __forceinline__ f32x16 gemm_xwT(f32x16 acc, const float* X, int ldx, const float* W, int ldw, int n0,
+__device__ __forceinline__ f32x16 gemm_xwT(f32x16 acc, const float* X, int ldx, gfp W, int ldw, int n0,
                                            int k0, int kc, int lane) {
   if (kc == 128) return gemm_xwT_p<128>(acc, X, ldx, W, ldw, n0, k0, lane);
   if (kc == 256) return gemm_xwT_p<256>(acc, X, ldx, W, ldw, n0, k0, lane);
   const int i = lane & 31, h = lane >> 5;
   const float* xr = X + i * ldx + k0 + 4 * h;
-  const float* wr = W + (size_t)(n0 + i) * ldw + k0 + 4 * h;
+  const gfp wr = W + (size_t)(n0 + i) * ldw + k0 + 4 * h;
 #pragma unroll UNROLL_XW
-  for (int k = 0; k < kc; k += 8) acc = mf4(*(const f4*)(xr + k), *(const f4u*)(wr + k), acc);
+  for (int k = 0; k < kc; k += 8) acc = mf4(*(const f4*)(xr + k), *(gf4u)(wr + k), acc);
   return acc;
 }
 // mean and variance GEMMs of parameter noise in one pass: every operand load
 // feeds both (x w and x^2 w^2: two independent accumulator chains per wave)
-__device__ __forceinline__ void gemm_xwT_mv(f32x16& m, f32x16& v, const float* X, int ldx, const float* W, int ldw,
+__device__ __forceinline__ void gemm_xwT_mv(f32x16& m, f32x16& v, const float* X, int ldx, gfp W, int ldw,
                                             int n0, int k0, int kc, int lane) {
   const int i = lane & 31, h = lane >> 5;
   const float* xr = X + i * ldx + k0 + 4 * h;
-  const float* wr = W + (size_t)(n0 + i) * ldw + k0 + 4 * h;
+  const gfp wr = W + (size_t)(n0 + i) * ldw + k0 + 4 * h;
 #pragma unroll 4
   for (int k = 0; k < kc; k += 8) {
     const f4 x = *(const f4*)(xr + k);
-    const f4 w = *(const f4u*)(wr + k);
+    const f4 w = *(gf4u)(wr + k);
     m = mf4(x, w, m);
     v = mf4(x * x, w * w, v);
   }
@@ -174,14 +181,14 @@ __device__ __forceinline__ void gemm_xwT_mv(f32x16& m, f32x16& v, const float* X
 // layer 1 (K = 12): k 0..7 by both halves, k 8..11 by half 0 (half 1's
 // 12..15 are zero operands, never loaded)
 template <bool SQ>
-__device__ __forceinline__ f32x16 gemm_l1(const float* S, const float* W1, int n0, int lane) {
+__device__ __forceinline__ f32x16 gemm_l1(const float* S, gfp W1, int n0, int lane) {
   const int i = lane & 31, h = lane >> 5;
   f4 x0 = *(const f4*)(S + i * kLdS + 4 * h);
-  f4 w0 = *(const f4u*)(W1 + (n0 + i) * kIn + 4 * h);
+  f4 w0 = *(gf4u)(W1 + (n0 + i) * kIn + 4 * h);
   f4 x1 = {0.f, 0.f, 0.f, 0.f}, w1 = {0.f, 0.f, 0.f, 0.f};
   if (h == 0) {
     x1 = *(const f4*)(S + i * kLdS + 8);
-    w1 = *(const f4u*)(W1 + (n0 + i) * kIn + 8);
+    w1 = *(gf4u)(W1 + (n0 + i) * kIn + 8);
   }
   if (SQ) {
     x0 *= x0;
@@ -195,11 +202,11 @@ __device__ __forceinline__ f32x16 gemm_l1(const float* S, const float* W1, int n
 }
 // acc[i][j] += sum_{k0 <= u < k0+kc} DZ[i][u] W[u][n0 + j]: DZ in LDS
 // row-major, W global row-major (ldw), read down its columns (coalesced)
-__device__ __forceinline__ f32x16 gemm_xw(f32x16 acc, const float* DZ, int ldz, const float* W, int ldw, int n0,
+__device__ __forceinline__ f32x16 gemm_xw(f32x16 acc, const float* DZ, int ldz, gfp W, int ldw, int n0,
                                           int k0, int kc, int lane) {
   const int i = lane & 31, h = lane >> 5;
   const float* zr = DZ + i * ldz + k0 + 4 * h;
-  const float* wc = W + (size_t)(k0 + 4 * h) * ldw + n0 + i;
+  const gfp wc = W + (size_t)(k0 + 4 * h) * ldw + n0 + i;
   // pipelined as gemm_xwT_p: 4 steps (16 column loads) in flight ahead
   f4 bn[4];
 #pragma unroll
@@ -240,7 +247,7 @@ __device__ __forceinline__ f32x16 gemm_wgrad(f32x16 acc, const float* DZ, int ld
 
 // row reductions: thread t owns row t/16 and 8 of its 128 units; every lane
 // of the 16-lane group returns the row's sum
-__device__ __forceinline__ float row_dot128(const float* X, int ldx, const float* w, int ws) {
+__device__ __forceinline__ float row_dot128(const float* X, int ldx, gfp w, int ws) {
   const int i = threadIdx.x >> 4, c = threadIdx.x & 15;
   float s = 0.f;
 #pragma unroll
@@ -523,7 +530,7 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad32(
     for (int t = 0; t < 4; ++t) {
       const int k = 32 * (4 * (w >> 2) + t) + j;
 #pragma unroll
-      for (int v = 0; v < 16; ++v) P[kPW2 + (32 * u2 + drow(v, lane)) * kCLd + k] = gW2[t][v];
+      for (int v = 0; v < 16; ++v) P[skpart::critic_w2_main(32 * u2 + drow(v, lane), k)] = gW2[t][v];
     }
     if (j < kIn) {
 #pragma unroll
@@ -534,8 +541,8 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad32(
   if (threadIdx.x < kH2) {
     const int u = threadIdx.x;
     P[pB2(kCLd) + u] = gb2;
-    P[kPW2 + u * kCLd + kH1] = gwa0;
-    P[kPW2 + u * kCLd + kH1 + 1] = gwa1;
+    P[skpart::critic_w2_action(u, 0)] = gwa0;
+    P[skpart::critic_w2_action(u, 1)] = gwa1;
     P[pW3(kCLd) + u] = gw3;
   }
   if (threadIdx.x < 2) L.RED[threadIdx.x] = 0.f;

@@ -25,23 +25,26 @@
 // weight-gradient GEMMs contract over the batch, so the activations they
 // need are written to LDS twice, batch-major and transposed.
 //
-// A workgroup (8 waves) owns a contiguous range of 32-row sub-tiles and
-// keeps its weight-gradient accumulators in registers across them: wave w
-// holds dW2 rows 32(w%4).. x columns 128(w/4).. (4 MFMA tiles) and dW1 rows
-// 32w..32w+31 (1 tile); layer 1 / dH1 use one 32-unit tile per wave, layer
-// 2 (128 units) waves 0-3.  Operands are bf16, accumulation fp32; biases, the critic's action
-// columns, layer 3 and the losses are fp32 VALU.
+// A workgroup of 8 waves (two per SIMD: one wave's VALU epilogue overlaps the
+// other's MFMA chain) owns a contiguous range of 32-row sub-tiles and keeps
+// its weight-gradient accumulators (AGPRs) across them: wave w holds dW2 rows
+// 32(w%4).. x columns 128(w/4).. (4 MFMA tiles) and dW1 rows 32w.. (1 tile);
+// layer 1 / dH1 use the 32-unit tile w.  Layer 2 (128 units) takes four
+// waves per net, so waves 0-3 and 4-7 run two nets' layer 2 side by side.
+// Operands are bf16, accumulation fp32; biases, the critic's action columns,
+// layer 3 and the losses are fp32 VALU.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "../../include/skillshot.h"
 #include "sk_mlp.hpp"
+#include "sk_partial.hpp"
 
 namespace {
 
 using namespace skmlp;
 
-constexpr int kThreads = 512;  // 8 waves
+constexpr int kThreads = 512;  // 8 waves, two per SIMD
 
 // Phase timestamps of the first and last workgroup (diagnostic builds only:
 // -DSK_TRACE, read back with sk_debug_update_trace; tools/trace_update.py)
@@ -75,7 +78,7 @@ constexpr int kPW1 = 0, kPB1 = kPW1 + kH1 * kIn, kPW2 = kPB1 + kH1;
 constexpr int kCPW2ld = kH1 + 2;  // critic W2 row length (h1 then the action)
 constexpr int kCPB2 = kPW2 + kH2 * kCPW2ld, kCPW3 = kCPB2 + kH2, kCPB3 = kCPW3 + kH2, kCP = kCPB3 + 1;
 constexpr int kAPB2 = kPW2 + kH2 * kH1, kAPW3 = kAPB2 + kH2, kAPB3 = kAPW3 + kOut * kH2, kAP = kAPB3 + kOut;
-static_assert(kCP == 36609 && kAP == 36482, "parameter counts");
+static_assert(kCP == 36609 && kAP == 36482 && kCP == skpart::kCriticParams && kPW2 == skpart::kPW2, "parameter counts");
 
 // LDS leading dimensions (bf16 elements unless noted): +8 (16 B) per row
 // rotates the banks of successive rows for the 16-byte fragment reads
@@ -90,29 +93,6 @@ __device__ __forceinline__ bf16x8 lfrag(const short* X, int ld, int row0, int k0
 }
 __device__ __forceinline__ int drow(int v, int lane) { return 8 * (v >> 2) + 4 * (lane >> 5) + (v & 3); }
 __device__ __forceinline__ float bf2f(short s) { return __uint_as_float(((uint32_t)(uint16_t)s) << 16); }
-
-// sum over the 128 layer-2 units of X[i][k] * w[k * ws] for the row
-// i = threadIdx.x / 16 of this thread (all 512 threads: 32 rows x 16
-// 8-unit chunks, then a 4-step butterfly inside each 16-lane group; every
-// lane of the group returns the row sum)
-__device__ __forceinline__ float row_dot128(const float* X, int ld, const float* w, int ws) {
-  const int i = threadIdx.x >> 4, c = threadIdx.x & 15;
-  float s = 0.f;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) s += X[i * ld + 8 * c + k] * w[(8 * c + k) * ws];
-#pragma unroll
-  for (int off = 1; off < 16; off <<= 1) s += __shfl_xor(s, off, 64);
-  return s;
-}
-__device__ __forceinline__ float row_sum128(const float* X, int ld) {
-  const int i = threadIdx.x >> 4, c = threadIdx.x & 15;
-  float s = 0.f;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) s += X[i * ld + 8 * c + k];
-#pragma unroll
-  for (int off = 1; off < 16; off <<= 1) s += __shfl_xor(s, off, 64);
-  return s;
-}
 
 // D registers 4g..4g+3 of a lane are 4 consecutive rows: store them to a
 // transposed [col][row] bf16 array with one 8-byte write
@@ -185,85 +165,161 @@ __global__ void k_grad_pack_flat(PackJobs j) {
 }
 
 // ---------------------------------------------------------------- shared pieces
-struct Lds {
-  short *Sr, *ST, *H1, *H1T, *DZ2, *DZ2T, *DZ1T, *H1C, *S2r;
-  float *H2f, *DZC, *A, *Y, *DQ, *DZ3, *RED, *A2, *RB, *DB;
-};
+// LDS-only workgroup barrier: waits for this wave's LDS traffic but not its
+// global loads, so the weight fragments prefetched for the next phase stay
+// in flight across it (the waves of these kernels exchange data through LDS
+// only; global results are written after the last barrier)
+__device__ __forceinline__ void lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+// Pointers laundered through inline asm (against LICM, below) lose their
+// address space, and a FLAT load counts on lgkmcnt too, so every LDS wait
+// (lds_sync) would also wait for the weight prefetches: loads through these
+// casts stay GLOBAL loads
+typedef const __attribute__((address_space(1))) bf16x8* gfrag_t;
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) f4v* gf4_t;
 
-__device__ __forceinline__ Lds carve(char* smem, bool actor) {
+// Re-derive the lane id inside a sub-tile loop: without this LICM hoists every
+// lane-dependent LDS / tail address of the loop body out of it and spills them
+__device__ __forceinline__ int launder_lane(int lane) {
+  asm volatile("" : "+v"(lane));
+  return lane;
+}
+// a wave's LDS write, then its read of another lane's value: LDS operations of
+// one wave complete in order, this only keeps the compiler from reordering
+__device__ __forceinline__ void wave_lds_order() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront", "local"); }
+
+// LDS of both gradient kernels.  Regions with disjoint lifetimes alias (the
+// phase numbers of the kernels below):
+//   DZ2 + DZ2T   critic: target actor h2 H2a (phases 2-3), then dz2 (4-5)
+//   DZ1T         critic: target actor h1 H1a (1-2), target critic Q terms QT
+//                (3-4); actor: Q terms QZ (3-4); then dz1 (5)
+//   H1B          critic: target critic h1 (1-3); actor: critic h1 (1-2),
+//                then dQ/dz2 DZC (3-4)
+struct Lds {
+  short *Sr, *S2r, *ST, *H1, *H1B, *H1T, *DZ2, *DZ2T, *DZ1T, *H1a;
+  float *H2a, *QT, *QZ, *DZC, *H2f, *TL, *A, *Y, *QV, *RB, *DB, *RED, *AW, *DW;
+};
+constexpr size_t kSzS = 32 * kLdS * 2, kSzT = 32 * kLdT * 2, kSzH1 = 32 * kLdH1 * 2, kSzH1T = kH1 * kLdT * 2;
+constexpr size_t kSzZ2 = 32 * kLdZ2 * 2, kSzZ2T = kH2 * kLdT * 2, kSzH2f = 32 * kLdH2f * 4;
+constexpr int kSmallF = 64 + 32 + 32 + 32 + 32 + 4 + 8 * 64 + 8 * 64;
+constexpr size_t kLdsGrad = 2 * kSzS + kSzT + 2 * kSzH1 + kSzH1T + kSzZ2 + kSzZ2T + kSzH1T + kSzH2f +
+                            3 * 1024 * 4 + kSmallF * 4;
+static_assert(kSzH2f <= kSzZ2 + kSzZ2T && kSzH2f <= kSzH1T && kSzH1 <= kSzH1T && kSzH2f == kSzH1, "LDS aliases");
+static_assert(kLdsGrad <= 160 * 1024, "LDS budget of one CU");
+
+__device__ __forceinline__ Lds carve(char* smem) {
   Lds L;
   char* p = smem;
-  L.Sr = (short*)p;   p += 32 * kLdS * 2;
-  L.ST = (short*)p;   p += 32 * kLdT * 2;
-  L.H1 = (short*)p;   p += 32 * kLdH1 * 2;
-  L.H1T = (short*)p;  p += kH1 * kLdT * 2;
-  L.DZ2 = (short*)p;  p += 32 * kLdZ2 * 2;
-  L.DZ2T = (short*)p; p += kH2 * kLdT * 2;
-  L.DZ1T = (short*)p; p += kH1 * kLdT * 2;
-  L.H2f = (float*)p;  p += 32 * kLdH2f * 4;
-  L.A = (float*)p;    p += 64 * 4;
-  L.Y = (float*)p;    p += 32 * 4;
-  L.DQ = (float*)p;   p += 32 * 4;
-  L.DZ3 = (float*)p;  p += 64 * 4;
-  L.RED = (float*)p;  p += 4 * 4;
-  L.S2r = (short*)p;  p += 32 * kLdS * 2;  // bootstrap target: s', mu'(s'), r, done
-  L.A2 = (float*)p;   p += 64 * 4;
-  L.RB = (float*)p;   p += 32 * 4;
-  L.DB = (float*)p;   p += 32 * 4;
-  L.H1C = nullptr;
-  L.DZC = nullptr;
-  if (actor) {
-    L.H1C = (short*)p; p += 32 * kLdH1 * 2;
-    L.DZC = (float*)p; p += 32 * kLdH2f * 4;
-  }
+  L.Sr = (short*)p;   p += kSzS;
+  L.S2r = (short*)p;  p += kSzS;
+  L.ST = (short*)p;   p += kSzT;
+  L.H1 = (short*)p;   p += kSzH1;
+  L.H1B = (short*)p;  p += kSzH1;
+  L.H1T = (short*)p;  p += kSzH1T;
+  L.DZ2 = (short*)p;  p += kSzZ2;
+  L.DZ2T = (short*)p; p += kSzZ2T;
+  L.DZ1T = (short*)p; p += kSzH1T;
+  L.H2f = (float*)p;  p += kSzH2f;
+  L.TL = (float*)p;   p += 3 * 1024 * 4;
+  float* f = (float*)p;
+  L.A = f;   f += 64;
+  L.Y = f;   f += 32;
+  L.QV = f;  f += 32;
+  L.RB = f;  f += 32;
+  L.DB = f;  f += 32;
+  L.RED = f; f += 4;
+  L.AW = f;  f += 8 * 64;
+  L.DW = f;
+  L.H2a = (float*)L.DZ2;
+  L.H1a = L.DZ1T;
+  L.QT = (float*)L.DZ1T;
+  L.QZ = (float*)L.DZ1T;
+  L.DZC = (float*)L.H1B;
   return L;
 }
-constexpr size_t kLdsBase = 32 * kLdS * 2 + 32 * kLdT * 2 + 32 * kLdH1 * 2 + kH1 * kLdT * 2 + 32 * kLdZ2 * 2 +
-                            kH2 * kLdT * 2 + kH1 * kLdT * 2 + 32 * kLdH2f * 4 + (64 + 32 + 32 + 64 + 4) * 4 +
-                            32 * kLdS * 2 + (64 + 32 + 32) * 4;
-constexpr size_t kLdsCritic = kLdsBase;
-constexpr size_t kLdsActor = kLdsBase + 32 * kLdH1 * 2 + 32 * kLdH2f * 4;
 
-// this sub-tile's states into Sr (batch-major) and ST (transposed, inputs
-// padded to 32 rows; rows 12..31 stay zero from the kernel start)
-__device__ __forceinline__ void load_states(const Lds& L, const float* S, int64_t row0, int64_t B) {
-  for (int t = threadIdx.x; t < 32 * 16; t += kThreads) {
-    const int i = t >> 4, k = t & 15;
-    const float v = (k < kIn && row0 + i < B) ? S[(row0 + i) * kIn + k] : 0.f;
-    const short b = f2bf(v);
-    L.Sr[i * kLdS + k] = b;
-    if (k < kIn) L.ST[k * kLdT + i] = b;
-  }
+// Phase 0 of a sub-tile issues every global load first (states, actions or
+// targets, s', r, done; on the first sub-tile also the nets' fp32 tails) so
+// that their latencies overlap, then writes LDS.  Thread t < 512 owns state
+// element (row t / 16, input t % 16) and tail float4s t and t + 512.
+__device__ __forceinline__ float load_state(const float* S, int64_t row0, int64_t B, int tid) {
+  const int i = tid >> 4, k = tid & 15;
+  return (k < kIn && row0 + i < B) ? S[(row0 + i) * kIn + k] : 0.f;
+}
+__device__ __forceinline__ void put_state(short* Xr, short* XT, float v, int tid) {
+  const int i = tid >> 4, k = tid & 15;
+  const short b = f2bf(v);
+  Xr[i * kLdS + k] = b;
+  if (XT && k < kIn) XT[k * kLdT + i] = b;  // rows 12..31 of XT stay zero from the kernel start
+}
+// tails of n <= 3 nets: waves 0-3 load net 0's 256 float4s, waves 4-7 net 1's,
+// and waves 0-3 also net 2's (wave-uniform pointer choice: global loads)
+__device__ __forceinline__ void load_tails(f4v& a, f4v& b, const char* p0, const char* p1, const char* p2, int n,
+                                           int w, int tid) {
+  if (w < 4 || n > 1) a = ((gf4_t)((w < 4 ? p0 : p1) + kGTail))[tid & 255];
+  if (n > 2 && w < 4) b = ((gf4_t)(p2 + kGTail))[tid];
+}
+__device__ __forceinline__ void put_tails(float* TL, f4v a, f4v b, int n, int w, int tid) {
+  if (w < 4 || n > 1) ((f4v*)TL)[tid] = a;
+  if (n > 2 && w < 4) ((f4v*)TL)[512 + tid] = b;
 }
 
-// layer 1 of one net for n-tile nt: relu(S W1^T + b1) -> batch-major (and,
-// if HT, transposed) bf16; `drop` applies the critic's training Dropout
+// keep bits of the critic's training Dropout for n-tile nt: bit 4g + q is row
+// drow(4g, lane) + q of the sub-tile, unit 32 nt + lane % 32.  The mask of
+// GLOBAL batch row key + i (the 1-rank batch's row numbering; key is a
+// multiple of 4: learner.DDPG, rng.dropout_keep), P(drop) = 0.2 (Dropout(0.2),
+// SkillshotLearner.py:110).  Data-independent: computed while phase 0's loads fly.
+__device__ __forceinline__ uint32_t dropout_bits(uint64_t seed, uint64_t call, int64_t key, int nt, int lane) {
+  const uint32_t n = 32 * nt + (lane & 31);
+  uint32_t bits = 0;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const uint4 u = philox(make_uint4((uint32_t)((key + drow(4 * g, lane)) >> 2), n, (uint32_t)call,
+                                      (uint32_t)(call >> 32)),
+                           (uint32_t)seed, (uint32_t)(seed >> 32));
+    bits |= ((uint32_t)(u.x >= 858993460u) | ((uint32_t)(u.y >= 858993460u) << 1) |
+             ((uint32_t)(u.z >= 858993460u) << 2) | ((uint32_t)(u.w >= 858993460u) << 3)) << (4 * g);
+  }
+  return bits;
+}
+
+// per-row LDS values for the 4 consecutive rows i0 .. i0 + 3 of an
+// accumulator register group (i0 a multiple of 4): X[i], and X[2i], X[2i+1]
+__device__ __forceinline__ float4 rows4(const float* X, int i0) { return *(const float4*)(X + i0); }
+__device__ __forceinline__ void pairs4(const float* X, int i0, float x0[4], float x1[4]) {
+  const float4 p = *(const float4*)(X + 2 * i0), q = *(const float4*)(X + 2 * i0 + 4);
+  x0[0] = p.x; x1[0] = p.y; x0[1] = p.z; x1[1] = p.w;
+  x0[2] = q.x; x1[2] = q.y; x0[3] = q.z; x1[3] = q.w;
+}
+
+// layer-1 fragment of n-tile w
+__device__ __forceinline__ bf16x8 load_l1(const char* pack, int w, int lane) {
+  return ((gfrag_t)(pack + kGW1))[w * 64 + lane];
+}
+
+// layer 1 of one net for n-tile nt (its fragment prefetched): relu(S W1^T +
+// b1) -> batch-major (and, if HT, transposed) bf16; DROP applies the
+// critic's training Dropout with the precomputed keep bits
 template <bool DROP>
-__device__ __forceinline__ void layer1(const short* Sx, const bf16x8* gW1, const float* tail, int nt, int lane,
-                                       short* H, short* HT, uint64_t seed, uint64_t call, int64_t row0,
-                                       uint8_t* mask_out, int64_t B, int64_t key_row0 = 0) {
+__device__ __forceinline__ void layer1(const short* Sx, bf16x8 wfrag, const float* tail, int nt, int lane, short* H,
+                                       short* HT, uint32_t keep_bits) {
   f32x16 acc = {0};
-  acc = mfma(lfrag(Sx, kLdS, 0, 0, lane), gW1[nt * 64 + lane], acc);
+  acc = mfma(lfrag(Sx, kLdS, 0, 0, lane), wfrag, acc);
   const int n = 32 * nt + (lane & 31);
   const float b = tail[kTB1 + n];
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     float hv[4];
-    uint4 u = make_uint4(0, 0, 0, 0);
     const int i0 = drow(4 * g, lane);
-    // the mask of GLOBAL batch row key_row0 + row0 + i (the 1-rank batch's
-    // row numbering; key_row0 is a multiple of 4): learner.DDPG, rng.dropout_keep
-    if (DROP) u = philox(make_uint4((uint32_t)((key_row0 + row0 + i0) >> 2), (uint32_t)n, (uint32_t)call,
-                                    (uint32_t)(call >> 32)),
-                         (uint32_t)seed, (uint32_t)(seed >> 32));
-    const uint32_t uw[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       float z = fmaxf(acc[4 * g + q] + b, 0.f);
       if (DROP) {
-        const bool keep = uw[q] >= 858993460u;  // P(drop) = 0.2 (Dropout(0.2), SkillshotLearner.py:110)
-        z = keep ? z * 1.25f : 0.f;
-        if (mask_out && row0 + i0 + q < B) mask_out[(row0 + i0 + q) * kH1 + n] = keep;
+        z = (keep_bits >> (4 * g + q)) & 1u ? z * 1.25f : 0.f;
       }
       hv[q] = z;
       H[(i0 + q) * kLdH1 + n] = f2bf(z);
@@ -272,25 +328,93 @@ __device__ __forceinline__ void layer1(const short* Sx, const bf16x8* gW1, const
   }
 }
 
-// layer 2 MFMA of one net for out n-tile nt over the 256 hidden inputs
-// (all 16 weight fragments issued up front: one memory round trip)
-__device__ __forceinline__ f32x16 layer2(const short* H, const bf16x8* gW2, int nt, int lane) {
-  bf16x8 wf[16];
+// layer 2: the 16 weight fragments of out n-tile nt (issued a phase ahead),
+// then the MFMA chain over the 256 hidden inputs; l2_mfma2 runs two nets'
+// chains interleaved (independent accumulators keep the MFMA pipe full)
+__device__ __forceinline__ void load_l2(bf16x8 wf[16], const char* pack, int nt, int lane) {
+  const gfrag_t g = (gfrag_t)(pack + kGW2);
 #pragma unroll
-  for (int kk = 0; kk < 16; ++kk) wf[kk] = gW2[(nt * 16 + kk) * 64 + lane];
+  for (int kk = 0; kk < 16; ++kk) wf[kk] = g[(nt * 16 + kk) * 64 + lane];
+}
+__device__ __forceinline__ f32x16 l2_mfma(const short* H, const bf16x8 wf[16], int lane) {
   f32x16 acc = {0};
 #pragma unroll
-  for (int kk = 0; kk < 16; ++kk) acc = mfma(lfrag(H, kLdH1, 0, 16 * kk, lane), wf[kk], acc);
+  for (int kk = 0; kk < 16; ++kk) {
+    acc = mfma(lfrag(H, kLdH1, 0, 16 * kk, lane), wf[kk], acc);
+    if ((kk & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // cap the hoisted LDS fragments (VGPRs)
+  }
   return acc;
+}
+__device__ __forceinline__ void l2_mfma2(f32x16& a0, f32x16& a1, const short* H0, const short* H1, const bf16x8 w0[16],
+                                         const bf16x8 w1[16], int lane) {
+  a0 = f32x16{0};
+  a1 = f32x16{0};
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk) {
+    a0 = mfma(lfrag(H0, kLdH1, 0, 16 * kk, lane), w0[kk], a0);
+    a1 = mfma(lfrag(H1, kLdH1, 0, 16 * kk, lane), w1[kk], a1);
+    if ((kk & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+  }
+}
+// W2^T fragments of the dH1 n-tile w (phase 5)
+__device__ __forceinline__ void load_w2t(bf16x8 wt[8], const char* pack, int w, int lane) {
+  const gfrag_t g = (gfrag_t)(pack + kGW2T);
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) wt[kk] = g[(w * 8 + kk) * 64 + lane];
+}
+
+// Row reductions done by ONE wave for all 32 rows of the sub-tile (each wave
+// that needs them computes them itself: no barrier between producer and
+// consumer).  Lane l takes row l % 32 and j = l / 32.
+// actor output a[row][j] = tanh(b3[j] + W3[j] . h2[row]) (tail of the actor)
+__device__ __forceinline__ float wave_mu(const float* H2, const float* tl, int lane) {
+  const int r = lane & 31, j = lane >> 5;
+  const float4* h = (const float4*)(H2 + r * kLdH2f);
+  const float4* wv = (const float4*)(tl + kTW3 + j * kH2);
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    const float4 a = h[k], b = wv[k];
+    s[k & 3] += (a.x * b.x + a.y * b.y) + (a.z * b.z + a.w * b.w);
+  }
+  return tanhf(tl[kTB3 + j] + ((s[0] + s[1]) + (s[2] + s[3])));
+}
+// sum over the 128 units of X[row] (both lane halves return it)
+__device__ __forceinline__ float wave_rowsum(const float* X, int lane) {
+  const int r = lane & 31, hh = lane >> 5;
+  const float4* x = (const float4*)(X + r * kLdH2f + 64 * hh);
+  float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; k += 2) {
+    const float4 a = x[k], c = x[k + 1];
+    s0 += (a.x + a.y) + (a.z + a.w);
+    s1 += (c.x + c.y) + (c.z + c.w);
+  }
+  const float s = s0 + s1;
+  return s + __shfl_xor(s, 32, 64);
+}
+// dQ/da[row][j] = sum_u X[row][u] W2[u][256 + j] (the critic's action columns, tail layout [u][2])
+__device__ __forceinline__ float wave_dot_action_cols(const float* X, const float* tl, int lane) {
+  const int r = lane & 31, j = lane >> 5;
+  const float4* x = (const float4*)(X + r * kLdH2f);
+  const float4* wa = (const float4*)(tl + kTW2a);  // [u][2]: float4 k/2 holds units 2k', 2k'+1
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    const float4 a = x[k], w0 = wa[2 * k], w1 = wa[2 * k + 1];
+    const float c0 = j ? w0.y : w0.x, c1 = j ? w0.w : w0.z, c2 = j ? w1.y : w1.x, c3 = j ? w1.w : w1.z;
+    s[k & 3] += (a.x * c0 + a.y * c1) + (a.z * c2 + a.w * c3);
+  }
+  return (s[0] + s[1]) + (s[2] + s[3]);
 }
 
 // the backward GEMMs shared by both kernels, given dZ2 (batch-major and
-// transposed) in LDS:
+// transposed) in LDS and the W2^T fragments wt (prefetched):
 //   dW2 tiles (w%4, 4(w/4)..+3) += dZ2^T H1     (accumulators gW2[4])
 //   dZ1 = (dZ2 W2) * d relu1 (* 1.25 under Dropout) -> DZ1T; db1 partial
 //   dW1 tile w += dZ1^T S                       (accumulator gW1)
 template <bool DROP>
-__device__ __forceinline__ void backward_12(const Lds& L, const bf16x8* gW2T, int w, int lane, f32x16 gW2[4],
+__device__ __forceinline__ void backward_12(const Lds& L, const bf16x8 wt[8], int w, int lane, f32x16 gW2[4],
                                             f32x16& gW1, float& gb1) {
   const int mt = w & 3, nt0 = 4 * (w >> 2);
   const bf16x8 a0 = lfrag(L.DZ2T, kLdT, 32 * mt, 0, lane), a1 = lfrag(L.DZ2T, kLdT, 32 * mt, 16, lane);
@@ -301,12 +425,9 @@ __device__ __forceinline__ void backward_12(const Lds& L, const bf16x8* gW2T, in
     __builtin_amdgcn_sched_barrier(0);
   }
   {
-    bf16x8 wf[8];
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) wf[kk] = gW2T[(w * 8 + kk) * 64 + lane];
     f32x16 acc = {0};
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) acc = mfma(lfrag(L.DZ2, kLdZ2, 0, 16 * kk, lane), wf[kk], acc);
+    for (int kk = 0; kk < 8; ++kk) acc = mfma(lfrag(L.DZ2, kLdZ2, 0, 16 * kk, lane), wt[kk], acc);
     const int n = 32 * w + (lane & 31);
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -321,20 +442,22 @@ __device__ __forceinline__ void backward_12(const Lds& L, const bf16x8* gW2T, in
       store_t4(L.DZ1T, kLdT, n, i0, d[0], d[1], d[2], d[3]);
     }
   }
-  __syncthreads();
+  lds_sync();
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) gW1 = mfma(lfrag(L.DZ1T, kLdT, 32 * w, 16 * kk, lane), lfrag(L.ST, kLdT, 0, 16 * kk, lane), gW1);
 }
 
-// write the register-held gradients of W1 / W2 (main 256 columns) / b1
-__device__ __forceinline__ void store_w12(float* P, int ld2, int w, int lane, const f32x16 gW2[4], const f32x16& gW1,
+// write the register-held gradients of W1 / W2 (main 256 columns, the
+// partial layout's 256-float rows: kPartW2) / b1; 32 lanes of a register write
+// 128 contiguous bytes
+__device__ __forceinline__ void store_w12(float* P, int w, int lane, const f32x16 gW2[4], const f32x16& gW1,
                                           float gb1) {
   const int mt = w & 3, nt0 = 4 * (w >> 2);
 #pragma unroll
   for (int t = 0; t < 4; ++t)
 #pragma unroll
     for (int v = 0; v < 16; ++v)
-      P[kPW2 + (32 * mt + drow(v, lane)) * ld2 + 32 * (nt0 + t) + (lane & 31)] = gW2[t][v];
+      P[kPW2 + (32 * mt + drow(v, lane)) * kH1 + 32 * (nt0 + t) + (lane & 31)] = gW2[t][v];
   const int k = lane & 31;
   if (k < kIn) {
 #pragma unroll
@@ -344,68 +467,25 @@ __device__ __forceinline__ void store_w12(float* P, int ld2, int w, int lane, co
   if (lane < 32) P[kPB1 + 32 * w + lane] = b;
 }
 
-// ---------------------------------------------------------------- bootstrap target
-// y = r + gamma (1 - done) Q'(s', mu'(s')) for the sub-tile's rows with the
-// target nets' grad packs (the same batch-major layers as the steps), into
-// L.Y; uses H1 / H2f as scratch (they are rewritten by the step after it).
-// Inputs in L.S2r, L.RB, L.DB; all threads of the workgroup call it.
-__device__ __forceinline__ void bootstrap_target(const Lds& L, const char* tap, const char* tcp, float gamma, int w,
-                                                 int lane) {
-  asm volatile("" : "+s"(tap), "+s"(tcp));  // no LICM of the fragment loads out of the sub-tile loop
-  const bf16x8* aW1 = (const bf16x8*)(tap + kGW1);
-  const bf16x8* aW2 = (const bf16x8*)(tap + kGW2);
-  const float* at = (const float*)(tap + kGTail);
-  const bf16x8* cW1 = (const bf16x8*)(tcp + kGW1);
-  const bf16x8* cW2 = (const bf16x8*)(tcp + kGW2);
-  const float* ct = (const float*)(tcp + kGTail);
-  const bool l2 = w < 4;
-  const int u = 32 * (w & 3) + (lane & 31);
-  __syncthreads();  // S2r in
-  layer1<false>(L.S2r, aW1, at, w, lane, L.H1, nullptr, 0, 0, 0, nullptr, 0);
-  __syncthreads();
-  if (l2) {
-    const f32x16 acc = layer2(L.H1, aW2, w, lane);
-    const float b2 = at[kTB2 + u];
-#pragma unroll
-    for (int v = 0; v < 16; ++v) L.H2f[drow(v, lane) * kLdH2f + u] = fmaxf(acc[v] + b2, 0.f);
-  }
-  __syncthreads();
-  {  // mu'(s')
-    const int i = threadIdx.x >> 4, c = threadIdx.x & 15;
-    const float z0 = row_dot128(L.H2f, kLdH2f, at + kTW3, 1);
-    const float z1 = row_dot128(L.H2f, kLdH2f, at + kTW3 + kH2, 1);
-    if (c < 2) L.A2[2 * i + c] = tanhf((c ? z1 : z0) + at[kTB3 + c]);
-  }
-  __syncthreads();
-  layer1<false>(L.S2r, cW1, ct, w, lane, L.H1, nullptr, 0, 0, 0, nullptr, 0);
-  __syncthreads();
-  if (l2) {  // Q' terms relu(z2) W3 per (row, unit)
-    const f32x16 acc = layer2(L.H1, cW2, w, lane);
-    const float b2 = ct[kTB2 + u], wa0 = ct[kTW2a + 2 * u], wa1 = ct[kTW2a + 2 * u + 1], w3 = ct[kTW3 + u];
-#pragma unroll
-    for (int v = 0; v < 16; ++v) {
-      const int i = drow(v, lane);
-      const float z = acc[v] + b2 + L.A2[2 * i] * wa0 + L.A2[2 * i + 1] * wa1;
-      L.H2f[i * kLdH2f + u] = fmaxf(z, 0.f) * w3;
-    }
-  }
-  __syncthreads();
-  {
-    const int i = threadIdx.x >> 4;
-    const float q = ct[kTB3] + row_sum128(L.H2f, kLdH2f);
-    if ((threadIdx.x & 15) == 0) L.Y[i] = L.RB[i] + gamma * (1.f - L.DB[i]) * q;
-  }
-  __syncthreads();
-}
-
 // ---------------------------------------------------------------- critic step
 // Critic.forward in train mode + F.mse_loss(q, y) backward
 // (DDPG.critic_step; critic.fit, SkillshotLearner.py:434): dL/dq =
-// grad_scale * (q - y) with grad_scale = 2 / (global batch).
+// grad_scale * (q - y) with grad_scale = 2 / (global batch).  BOOT: y = r +
+// gamma (1 - done) Q'(s', mu'(s')) from the target nets' packs, computed in
+// the same phases as the training forward:
+//   0  stage s, a (s', r, done); layer-1 fragments in flight
+//   1  layer 1 (n-tile w) of the critic (Dropout), target actor, target critic
+//   2  waves 0-3: critic layer 2 -> h2;  waves 4-7: target actor layer 2
+//   3  waves 0-3: q = W3 h2 + b3;  waves 4-7: mu'(s') (each wave, all rows)
+//      and the target critic's layer 2 at (s', mu'(s')) -> Q' terms
+//   4  waves 0-3: y and dL/dq (each wave, all rows), dz2 of its units
+//   5  dW2, dz1;  6  dW1
+// Weight fragments are loaded one phase ahead of their MFMAs and the
+// barriers are LDS-only (lds_sync), so no phase waits on a global load.
+template <bool BOOT>
 __global__ void __launch_bounds__(kThreads) k_critic_grad(const float* __restrict__ S, const float* __restrict__ A,
                                                           const float* __restrict__ Y, int64_t B, int64_t key_row0,
-                                                          int sub_per_wg,
-                                                          float grad_scale, uint64_t seed,
+                                                          int sub_per_wg, float grad_scale, uint64_t seed,
                                                           const int64_t* __restrict__ call_ctr,
                                                           const char* __restrict__ gpack, float* __restrict__ partial,
                                                           float* step_ctr, int n_steps, float* __restrict__ loss_out,
@@ -414,252 +494,350 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad(const float* __restric
                                                           float gamma, const char* __restrict__ tapack,
                                                           const char* __restrict__ tcpack) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const Lds L = carve(smem, false);
+  const Lds L = carve(smem);
   SK_TP(0);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5;
+  const int lane0 = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool l2 = w < 4;  // waves of the critic's own layer 2 (4-7: the target nets')
   const uint64_t call = (uint64_t)*call_ctr;
-  const bf16x8* fW1_ = (const bf16x8*)(gpack + kGW1);
-  const bf16x8* fW2_ = (const bf16x8*)(gpack + kGW2);
-  const bf16x8* fW2T_ = (const bf16x8*)(gpack + kGW2T);
-  const float* tail_ = (const float*)(gpack + kGTail);
   if (blockIdx.x == 0 && threadIdx.x < n_steps) step_ctr[threadIdx.x] += 1.0f;  // Adam's step (read by k_adam_flat)
   for (int t = threadIdx.x; t < 32 * kLdT; t += kThreads) L.ST[t] = 0;
+  const float* TLc = L.TL;
+  const float* TLa = L.TL + 1024;
+  const float* TLt = L.TL + 2048;
   f32x16 gW2[4], gW1 = {0};
 #pragma unroll
   for (int k = 0; k < 4; ++k) gW2[k] = f32x16{0};
   float gb1 = 0.f, gb2 = 0.f, gw2a0 = 0.f, gw2a1 = 0.f, gw3 = 0.f, gb3 = 0.f, lsum = 0.f;
-  const bool l2 = w < 4;               // layer-2 waves
-  const int u = 32 * (w & 3) + (lane & 31);  // their layer-2 unit
   if (threadIdx.x < 4) L.RED[threadIdx.x] = 0.f;
-  __syncthreads();
   SK_TP(1);
   for (int sub = 0; sub < sub_per_wg; ++sub) {
     const int64_t row0 = ((int64_t)blockIdx.x * sub_per_wg + sub) * 32;
     if (row0 >= B) break;  // uniform across the workgroup
-    // launder the weight bases every sub-tile: otherwise LICM hoists every
+    const int tid = launder_lane(threadIdx.x), lane = tid & 63, hh = lane >> 5, col = lane & 31;
+    const int u = 32 * (w & 3) + col;  // the lane's layer-2 unit (of the critic or a target net)
+    // launder the pack bases every sub-tile: otherwise LICM hoists every
     // (loop-invariant) fragment load out of the loop and spills
-    const bf16x8* fW1 = fW1_;
-    const bf16x8* fW2 = fW2_;
-    const bf16x8* fW2T = fW2T_;
-    const float* tail = tail_;
-    asm volatile("" : "+s"(fW1), "+s"(fW2), "+s"(fW2T), "+s"(tail));
-    load_states(L, S, row0, B);
-    if (threadIdx.x < 64) L.A[threadIdx.x] = row0 + (threadIdx.x >> 1) < B ? A[row0 * 2 + threadIdx.x] : 0.f;
-    if (tapack) {  // the DDPG target y = r + gamma (1 - done) Q'(s', mu'(s')) of this sub-tile, in LDS
-      for (int t = threadIdx.x; t < 32 * 16; t += kThreads) {
-        const int i = t >> 4, k = t & 15;
-        L.S2r[i * kLdS + k] = f2bf((k < kIn && row0 + i < B) ? S2[(row0 + i) * kIn + k] : 0.f);
-      }
-      if (threadIdx.x < 32) {
-        const bool ok = row0 + threadIdx.x < B;
-        L.RB[threadIdx.x] = ok ? R[row0 + threadIdx.x] : 0.f;
-        L.DB[threadIdx.x] = ok ? D[row0 + threadIdx.x] : 0.f;
-      }
-      SK_TP(2);
-      bootstrap_target(L, tapack, tcpack, gamma, w, lane);
-      SK_TP(3);
-    } else if (threadIdx.x < 32) {
-      L.Y[threadIdx.x] = row0 + threadIdx.x < B ? Y[row0 + threadIdx.x] : 0.f;
+    const char* cp = gpack;
+    const char* ap = tapack;
+    const char* tp = tcpack;
+    asm volatile("" : "+s"(cp), "+s"(ap), "+s"(tp));
+    const bf16x8 f1c = load_l1(cp, w, lane);
+    bf16x8 f1a = {}, f1t = {};
+    if (BOOT) {
+      f1a = load_l1(ap, w, lane);
+      f1t = load_l1(tp, w, lane);
     }
-    __syncthreads();
-    SK_TP(4);
-    layer1<true>(L.Sr, fW1, tail, w, lane, L.H1, L.H1T, seed, call, row0, mask_out, B, key_row0);
-    __syncthreads();
-    SK_TP(5);
-    float h2v[16];
-    if (l2) {
-      const f32x16 acc = layer2(L.H1, fW2, w, lane);
-      const float b2 = tail[kTB2 + u], wa0 = tail[kTW2a + 2 * u], wa1 = tail[kTW2a + 2 * u + 1];
+    // ---- phase 0: every global load of the sub-tile, the Dropout bits while they fly, then LDS
+    const float sv = load_state(S, row0, B, tid);
+    const float s2v = BOOT ? load_state(S2, row0, B, tid) : 0.f;
+    const float av = tid < 64 && row0 + (tid >> 1) < B ? A[row0 * 2 + tid] : 0.f;
+    const bool rok = tid < 32 && row0 + tid < B;
+    const float rv = rok ? (BOOT ? R[row0 + tid] : Y[row0 + tid]) : 0.f;
+    const float dv = BOOT && rok ? D[row0 + tid] : 0.f;
+    f4v tla = {}, tlb = {};
+    if (sub == 0) load_tails(tla, tlb, cp, ap, tp, BOOT ? 3 : 1, w, tid);
+    uint32_t keep = dropout_bits(seed, call, key_row0 + row0, w, lane);
+    asm volatile("" : "+v"(keep));  // computed here, under the loads' latency (not sunk into phase 1)
+    if (mask_out) {  // the Dropout mask (tests): byte per (row, unit)
+      const int n = 32 * w + col;
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
         const int i = drow(v, lane);
-        h2v[v] = fmaxf(acc[v] + b2 + L.A[2 * i] * wa0 + L.A[2 * i + 1] * wa1, 0.f);
-        L.H2f[i * kLdH2f + u] = h2v[v];
+        if (row0 + i < B) mask_out[(row0 + i) * kH1 + n] = (keep >> v) & 1u;
       }
     }
-    __syncthreads();
-    SK_TP(6);
-    {  // q and dL/dq per row (all threads: row_dot128)
-      const int i = threadIdx.x >> 4;
-      const float q = tail[kTB3] + row_dot128(L.H2f, kLdH2f, tail + kTW3, 1);
-      if ((threadIdx.x & 15) == 0) {
-        const float e = row0 + i < B ? q - L.Y[i] : 0.f;
-        L.DQ[i] = grad_scale * e;
+    put_state(L.Sr, L.ST, sv, tid);
+    if (BOOT) put_state(L.S2r, nullptr, s2v, tid);
+    if (tid < 64) L.A[tid] = av;
+    if (tid < 32) {
+      if (BOOT) {
+        L.RB[tid] = rv;
+        L.DB[tid] = dv;
+      } else {
+        L.Y[tid] = rv;
+      }
+    }
+    if (sub == 0) put_tails(L.TL, tla, tlb, BOOT ? 3 : 1, w, tid);
+    lds_sync();
+    SK_TP(2);
+    // ---- phase 1: layer 1 (n-tile w) of the critic with Dropout, the target actor, the target critic
+    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch in phase 1 (hoisted into phase 0 it spills)
+    bf16x8 wf[16];
+    if (l2) load_l2(wf, cp, w, lane);
+    else if (BOOT) load_l2(wf, ap, w - 4, lane);
+    SK_TP(12);
+    layer1<true>(L.Sr, f1c, TLc, w, lane, L.H1, L.H1T, keep);
+    SK_TP(13);
+    if (BOOT) {
+      layer1<false>(L.S2r, f1a, TLa, w, lane, L.H1a, nullptr, 0);
+      SK_TP(14);
+      layer1<false>(L.S2r, f1t, TLt, w, lane, L.H1B, nullptr, 0);
+    }
+    SK_TP(15);
+    lds_sync();
+    SK_TP(3);
+    // ---- phase 2
+    if (l2) {  // critic h2 = relu(W2 [h1; a] + b2) -> fp32 LDS (q, dz2)
+      const f32x16 acc = l2_mfma(L.H1, wf, lane);
+      const float b2 = TLc[kTB2 + u], wa0 = TLc[kTW2a + 2 * u], wa1 = TLc[kTW2a + 2 * u + 1];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int i0 = drow(4 * g, lane);
+        float a0[4], a1[4];
+        pairs4(L.A, i0, a0, a1);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          L.H2f[(i0 + q) * kLdH2f + u] = fmaxf(acc[4 * g + q] + b2 + a0[q] * wa0 + a1[q] * wa1, 0.f);
+      }
+    } else if (BOOT) {  // target actor h2; then the target critic's layer-2 fragments for phase 3
+      const f32x16 acc = l2_mfma(L.H1a, wf, lane);
+      __builtin_amdgcn_sched_barrier(0);
+      load_l2(wf, tp, w - 4, lane);
+      const float b2 = TLa[kTB2 + u];
+#pragma unroll
+      for (int v = 0; v < 16; ++v) L.H2a[drow(v, lane) * kLdH2f + u] = fmaxf(acc[v] + b2, 0.f);
+    }
+    lds_sync();
+    SK_TP(4);
+    // ---- phase 3
+    bf16x8 wt[8];  // W2^T fragments of phase 5 (waves 4-7: after the target critic's fragments are consumed)
+    if (l2 || !BOOT) load_w2t(wt, cp, w, lane);
+    if (l2) {  // q per row: 8 threads per row, 16 units each
+      const int i = tid >> 3, c = tid & 7;
+      const float4* h = (const float4*)(L.H2f + i * kLdH2f + 16 * c);
+      const float4* w3 = (const float4*)(TLc + kTW3 + 16 * c);
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float4 a = h[k], b = w3[k];
+        s += (a.x * b.x + a.y * b.y) + (a.z * b.z + a.w * b.w);
+      }
+      s += __shfl_xor(s, 1, 64);
+      s += __shfl_xor(s, 2, 64);
+      s += __shfl_xor(s, 4, 64);
+      if (c == 0) L.QV[i] = TLc[kTB3] + s;
+    } else if (BOOT) {  // mu'(s') for all rows, then the Q' terms relu(z2') W3' of the wave's units
+      const f32x16 acc = l2_mfma(L.H1B, wf, lane);
+      __builtin_amdgcn_sched_barrier(0);
+      load_w2t(wt, cp, w, lane);
+      float* aw = L.AW + 64 * w;
+      aw[2 * col + hh] = wave_mu(L.H2a, TLa, lane);
+      wave_lds_order();
+      const float b2 = TLt[kTB2 + u], wa0 = TLt[kTW2a + 2 * u], wa1 = TLt[kTW2a + 2 * u + 1], w3 = TLt[kTW3 + u];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int i0 = drow(4 * g, lane);
+        float a0[4], a1[4];
+        pairs4(aw, i0, a0, a1);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          L.QT[(i0 + q) * kLdH2f + u] = fmaxf(acc[4 * g + q] + b2 + a0[q] * wa0 + a1[q] * wa1, 0.f) * w3;
+      }
+    }
+    lds_sync();
+    SK_TP(5);
+    // ---- phase 4 (waves 0-3): y and dL/dq for all rows (each wave), then dz2 = dL/dq W3 relu'(h2) of its units
+    if (l2) {
+      const float yv = BOOT ? L.RB[col] + gamma * (1.f - L.DB[col]) * (TLt[kTB3] + wave_rowsum(L.QT, lane))
+                            : L.Y[col];
+      const float e = row0 + col < B ? L.QV[col] - yv : 0.f;
+      float* dw = L.DW + 64 * w;
+      if (hh == 0) dw[col] = grad_scale * e;
+      if (w == 0 && hh == 0) {
         gb3 += grad_scale * e;
         lsum += e * e;
       }
-    }
-    __syncthreads();
-    SK_TP(7);
-    if (l2) {
-      const float w3 = tail[kTW3 + u];
+      wave_lds_order();
+      const float w3 = TLc[kTW3 + u];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        float d[4];
+        const int i0 = drow(4 * g, lane);
+        const float4 dq4 = rows4(dw, i0);
+        const float dqs[4] = {dq4.x, dq4.y, dq4.z, dq4.w};
+        float a0[4], a1[4], d[4];
+        pairs4(L.A, i0, a0, a1);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int i = drow(4 * g + q, lane);
-          const float dq = L.DQ[i];
-          d[q] = h2v[4 * g + q] > 0.f ? dq * w3 : 0.f;
-          L.DZ2[i * kLdZ2 + u] = f2bf(d[q]);
+          const float h = L.H2f[(i0 + q) * kLdH2f + u];
+          d[q] = h > 0.f ? dqs[q] * w3 : 0.f;
+          L.DZ2[(i0 + q) * kLdZ2 + u] = f2bf(d[q]);
           gb2 += d[q];
-          gw2a0 += d[q] * L.A[2 * i];
-          gw2a1 += d[q] * L.A[2 * i + 1];
-          gw3 += dq * h2v[4 * g + q];
+          gw2a0 += d[q] * a0[q];
+          gw2a1 += d[q] * a1[q];
+          gw3 += dqs[q] * h;
         }
-        store_t4(L.DZ2T, kLdT, u, drow(4 * g, lane), d[0], d[1], d[2], d[3]);
+        store_t4(L.DZ2T, kLdT, u, i0, d[0], d[1], d[2], d[3]);
       }
     }
-    __syncthreads();
-    SK_TP(8);
-    backward_12<true>(L, fW2T, w, lane, gW2, gW1, gb1);
-    __syncthreads();
-    SK_TP(9);
+    lds_sync();
+    SK_TP(6);
+    // ---- phases 5, 6
+    backward_12<true>(L, wt, w, lane, gW2, gW1, gb1);
+    lds_sync();  // the next sub-tile restages
+    SK_TP(7);
   }
+  const int lane = lane0, hh = lane >> 5;
+  const int u = 32 * (w & 3) + (lane & 31);
   float* P = partial + (int64_t)blockIdx.x * kCP;
-  store_w12(P, kCPW2ld, w, lane, gW2, gW1, gb1);
-  SK_TP(10);
+  store_w12(P, w, lane, gW2, gW1, gb1);
+  SK_TP(8);
   gb2 += __shfl_xor(gb2, 32, 64);
   gw2a0 += __shfl_xor(gw2a0, 32, 64);
   gw2a1 += __shfl_xor(gw2a1, 32, 64);
   gw3 += __shfl_xor(gw3, 32, 64);
   if (l2 && hh == 0) {
     P[kCPB2 + u] = gb2;
-    P[kPW2 + u * kCPW2ld + kH1] = gw2a0;
-    P[kPW2 + u * kCPW2ld + kH1 + 1] = gw2a1;
+    P[skpart::critic_w2_action(u, 0)] = gw2a0;
+    P[skpart::critic_w2_action(u, 1)] = gw2a1;
     P[kCPW3 + u] = gw3;
   }
-  if ((threadIdx.x & 15) == 0) {  // the row-owner threads hold db3 / loss partials
+  if (w == 0 && hh == 0) {  // wave 0's row lanes hold the db3 / loss partials
     atomicAdd(&L.RED[0], gb3);
     atomicAdd(&L.RED[1], lsum);
   }
-  __syncthreads();
+  lds_sync();
   if (threadIdx.x == 0) {
     P[kCPB3] = L.RED[0];
     if (loss_out) atomicAdd(loss_out, L.RED[1]);
   }
-  SK_TP(11);
+  SK_TP(9);
 }
 
 // ---------------------------------------------------------------- actor step
 // model_actor_fit_step (SkillshotLearner.py:386-417; DDPG.model_actor_fit_step):
 // gradient of -loss_scale * sum_b Q(s_b, mu(s_b)) w.r.t. the actor, critic in
-// inference mode (no Dropout).  q_out (optional) receives sum_b Q.
+// inference mode (no Dropout).  q_out (optional) receives sum_b Q.  Phases:
+//   0  stage s; layer-1 fragments in flight
+//   1  layer 1 (n-tile w) of the actor and of the critic (both read s)
+//   2  waves 0-3: actor layer 2 -> h2;  waves 4-7: the critic's layer-2 MFMA
+//      (its action columns join in phase 3)
+//   3  mu(s) (each wave, all rows); waves 4-7: critic z2 at (s, mu(s)),
+//      dQ/dz2 = W3 relu'(z2), Q terms
+//   4  waves 0-3: dL/dz3 = -loss_scale dQ/da (1 - a^2) (each wave, all rows),
+//      dz2 of its units; wave 4: sum Q
+//   5  dW2, dz1;  6  dW1
 __global__ void __launch_bounds__(kThreads) k_actor_grad(const float* __restrict__ S, int64_t B, int sub_per_wg,
                                                          float loss_scale, const char* __restrict__ apack,
                                                          const char* __restrict__ cpack, float* __restrict__ partial,
                                                          float* step_ctr, int n_steps, float* __restrict__ q_out) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const Lds L = carve(smem, true);
+  const Lds L = carve(smem);
   SK_TP(0);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5;
-
+  const int lane0 = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool l2 = w < 4;  // waves of the actor's layer 2 (4-7: the critic's)
   if (blockIdx.x == 0 && threadIdx.x < n_steps) step_ctr[threadIdx.x] += 1.0f;  // Adam's step (read by k_adam_flat)
   for (int t = threadIdx.x; t < 32 * kLdT; t += kThreads) L.ST[t] = 0;
+  const float* TLa = L.TL;
+  const float* TLc = L.TL + 1024;
   f32x16 gW2[4], gW1 = {0};
 #pragma unroll
   for (int k = 0; k < 4; ++k) gW2[k] = f32x16{0};
   float gb1 = 0.f, gb2 = 0.f, gw30 = 0.f, gw31 = 0.f, gb3 = 0.f, qsum = 0.f;
-  const bool l2 = w < 4;                     // layer-2 waves
-  const int u = 32 * (w & 3) + (lane & 31);  // their layer-2 unit
   if (threadIdx.x < 4) L.RED[threadIdx.x] = 0.f;
-  __syncthreads();
   SK_TP(1);
   for (int sub = 0; sub < sub_per_wg; ++sub) {
     const int64_t row0 = ((int64_t)blockIdx.x * sub_per_wg + sub) * 32;
     if (row0 >= B) break;  // uniform across the workgroup
+    const int tid = launder_lane(threadIdx.x), lane = tid & 63, hh = lane >> 5, col = lane & 31;
+    const int u = 32 * (w & 3) + col;  // the lane's layer-2 unit (actor: waves 0-3, critic: 4-7)
     const char* ap = apack;
     const char* cp = cpack;
     asm volatile("" : "+s"(ap), "+s"(cp));  // no LICM of the fragment loads (see k_critic_grad)
-    const bf16x8* aW1 = (const bf16x8*)(ap + kGW1);
-    const bf16x8* aW2 = (const bf16x8*)(ap + kGW2);
-    const bf16x8* aW2T = (const bf16x8*)(ap + kGW2T);
-    const float* at = (const float*)(ap + kGTail);
-    const bf16x8* cW1 = (const bf16x8*)(cp + kGW1);
-    const bf16x8* cW2 = (const bf16x8*)(cp + kGW2);
-    const float* ct = (const float*)(cp + kGTail);
-    load_states(L, S, row0, B);
-    __syncthreads();
+    const bf16x8 f1a = load_l1(ap, w, lane), f1c = load_l1(cp, w, lane);
+    // ---- phase 0: states (and, first sub-tile, the tails) loaded together, then LDS
+    const float sv = load_state(S, row0, B, tid);
+    f4v tla = {}, tlb = {};
+    if (sub == 0) load_tails(tla, tlb, ap, cp, nullptr, 2, w, tid);
+    put_state(L.Sr, L.ST, sv, tid);
+    if (sub == 0) put_tails(L.TL, tla, tlb, 2, w, tid);
+    lds_sync();
     SK_TP(2);
-    layer1<false>(L.Sr, aW1, at, w, lane, L.H1, L.H1T, 0, 0, 0, nullptr, B);
-    layer1<false>(L.Sr, cW1, ct, w, lane, L.H1C, nullptr, 0, 0, 0, nullptr, B);
-    __syncthreads();
+    // ---- phase 1: layer 1 (n-tile w) of the actor and of the critic
+    bf16x8 wf[16];
+    if (l2) load_l2(wf, ap, w, lane);
+    else load_l2(wf, cp, w - 4, lane);
+    layer1<false>(L.Sr, f1a, TLa, w, lane, L.H1, L.H1T, 0);
+    layer1<false>(L.Sr, f1c, TLc, w, lane, L.H1B, nullptr, 0);
+    lds_sync();
     SK_TP(3);
-    if (l2) {  // actor h2 -> H2f (fp32, kept for the backward)
-      const f32x16 acc = layer2(L.H1, aW2, w, lane);
-      const float b2 = at[kTB2 + u];
+    // ---- phase 2
+    f32x16 zc = {0};
+    if (l2) {  // actor h2 -> fp32 LDS (mu, dz2)
+      const f32x16 acc = l2_mfma(L.H1, wf, lane);
+      const float b2 = TLa[kTB2 + u];
 #pragma unroll
       for (int v = 0; v < 16; ++v) L.H2f[drow(v, lane) * kLdH2f + u] = fmaxf(acc[v] + b2, 0.f);
+    } else {
+      zc = l2_mfma(L.H1B, wf, lane);
     }
-    __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);
+    bf16x8 wt[8];  // W2^T fragments of phase 5
+    load_w2t(wt, ap, w, lane);
+    lds_sync();
     SK_TP(4);
-    {  // mu(s) = tanh(W3 h2 + b3) (all threads: row_dot128)
-      const int i = threadIdx.x >> 4, c = threadIdx.x & 15;
-      const float z0 = row_dot128(L.H2f, kLdH2f, at + kTW3, 1);
-      const float z1 = row_dot128(L.H2f, kLdH2f, at + kTW3 + kH2, 1);
-      if (c < 2) L.A[2 * i + c] = tanhf((c ? z1 : z0) + at[kTB3 + c]);
-    }
-    __syncthreads();
-    SK_TP(5);
-    {  // critic layer 2 at (s, mu(s)): dQ/dz2 = W3 relu'(z2) (rows beyond B: 0)
-      f32x16 acc = {0};
-      if (l2) acc = layer2(L.H1C, cW2, w, lane);
-      __syncthreads();  // every wave is done reading H1C: its space takes the Q terms
-      float* QZ = (float*)L.H1C;  // [32][kLdH2f] fp32 relu(z2) W3 (q_out)
-      if (l2) {
-        const float b2 = ct[kTB2 + u], wa0 = ct[kTW2a + 2 * u], wa1 = ct[kTW2a + 2 * u + 1], w3 = ct[kTW3 + u];
-#pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const int i = drow(v, lane);
-          const float z = acc[v] + b2 + L.A[2 * i] * wa0 + L.A[2 * i + 1] * wa1;
-          L.DZC[i * kLdH2f + u] = (z > 0.f && row0 + i < B) ? w3 : 0.f;
-          if (q_out) QZ[i * kLdH2f + u] = fmaxf(z, 0.f) * w3;
-        }
-      }
-      __syncthreads();
-      // dL/dz3 = -loss_scale * dQ/da * (1 - a^2), dQ/da = sum_u dQ/dz2 W2[u][256 + j]
-      const int i = threadIdx.x >> 4, c = threadIdx.x & 15;
-      const float da0 = row_dot128(L.DZC, kLdH2f, ct + kTW2a, 2);
-      const float da1 = row_dot128(L.DZC, kLdH2f, ct + kTW2a + 1, 2);
-      const float qrow = q_out ? row_sum128(QZ, kLdH2f) : 0.f;
-      if (c < 2) {
-        const float a = L.A[2 * i + c];
-        const float d = -loss_scale * (c ? da1 : da0) * (1.f - a * a);
-        L.DZ3[2 * i + c] = d;
-        gb3 += d;  // db3[c] partial (threads with c < 2)
-      }
-      if (c == 0 && q_out && row0 + i < B) qsum += ct[kTB3] + qrow;
-    }
-    __syncthreads();
-    SK_TP(6);
-    if (l2) {  // dZ2 = (dz3 W3) relu'(h2);  dW3[j][u] += sum_i dz3[i][j] h2[i][u]
-      const float w30 = at[kTW3 + u], w31 = at[kTW3 + kH2 + u];
+    // ---- phase 3: mu(s) = tanh(W3 h2 + b3), lane (row col, output hh), every wave
+    const float a = wave_mu(L.H2f, TLa, lane);
+    if (!l2) {  // the critic at (s, mu(s)): dQ/dz2 = W3 relu'(z2) (rows beyond B: 0), Q terms relu(z2) W3
+      float* aw = L.AW + 64 * w;
+      aw[2 * col + hh] = a;
+      wave_lds_order();
+      const float b2 = TLc[kTB2 + u], wa0 = TLc[kTW2a + 2 * u], wa1 = TLc[kTW2a + 2 * u + 1], w3 = TLc[kTW3 + u];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        float d[4];
+        const int i0 = drow(4 * g, lane);
+        float a0[4], a1[4];
+        pairs4(aw, i0, a0, a1);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int i = drow(4 * g + q, lane);
-          const float z0 = L.DZ3[2 * i], z1 = L.DZ3[2 * i + 1];
-          const float h = L.H2f[i * kLdH2f + u];
-          d[q] = h > 0.f ? z0 * w30 + z1 * w31 : 0.f;
-          L.DZ2[i * kLdZ2 + u] = f2bf(d[q]);
-          gb2 += d[q];
-          gw30 += z0 * h;
-          gw31 += z1 * h;
+          const int i = i0 + q;
+          const float z = zc[4 * g + q] + b2 + a0[q] * wa0 + a1[q] * wa1;
+          L.DZC[i * kLdH2f + u] = (z > 0.f && row0 + i < B) ? w3 : 0.f;
+          if (q_out) L.QZ[i * kLdH2f + u] = fmaxf(z, 0.f) * w3;
         }
-        store_t4(L.DZ2T, kLdT, u, drow(4 * g, lane), d[0], d[1], d[2], d[3]);
       }
     }
-    __syncthreads();
+    lds_sync();
+    SK_TP(5);
+    // ---- phase 4
+    if (l2) {  // dL/dz3[row col][hh], then dz2 = (dz3 W3) relu'(h2) of its units
+      const float dz3 = -loss_scale * wave_dot_action_cols(L.DZC, TLc, lane) * (1.f - a * a);
+      float* dw = L.DW + 64 * w;
+      dw[2 * col + hh] = dz3;
+      if (w == 0) gb3 += dz3;  // db3[hh] partial of row col
+      wave_lds_order();
+      const float w30 = TLa[kTW3 + u], w31 = TLa[kTW3 + kH2 + u];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int i0 = drow(4 * g, lane);
+        float z0[4], z1[4], d[4];
+        pairs4(dw, i0, z0, z1);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float h = L.H2f[(i0 + q) * kLdH2f + u];
+          d[q] = h > 0.f ? z0[q] * w30 + z1[q] * w31 : 0.f;
+          L.DZ2[(i0 + q) * kLdZ2 + u] = f2bf(d[q]);
+          gb2 += d[q];
+          gw30 += z0[q] * h;
+          gw31 += z1[q] * h;
+        }
+        store_t4(L.DZ2T, kLdT, u, i0, d[0], d[1], d[2], d[3]);
+      }
+    } else if (w == 4 && q_out) {
+      const float s = wave_rowsum(L.QZ, lane);
+      if (hh == 0 && row0 + col < B) qsum += TLc[kTB3] + s;
+    }
+    lds_sync();
+    SK_TP(6);
+    // ---- phases 5, 6
+    backward_12<false>(L, wt, w, lane, gW2, gW1, gb1);
+    lds_sync();
     SK_TP(7);
-    backward_12<false>(L, aW2T, w, lane, gW2, gW1, gb1);
-    __syncthreads();
-    SK_TP(8);
   }
+  const int lane = lane0, hh = lane >> 5;
+  const int u = 32 * (w & 3) + (lane & 31);
   float* P = partial + (int64_t)blockIdx.x * kAP;
-  store_w12(P, kH1, w, lane, gW2, gW1, gb1);
-  SK_TP(9);
+  store_w12(P, w, lane, gW2, gW1, gb1);
+  SK_TP(8);
   gb2 += __shfl_xor(gb2, 32, 64);
   gw30 += __shfl_xor(gw30, 32, 64);
   gw31 += __shfl_xor(gw31, 32, 64);
@@ -668,15 +846,12 @@ __global__ void __launch_bounds__(kThreads) k_actor_grad(const float* __restrict
     P[kAPW3 + u] = gw30;
     P[kAPW3 + kH2 + u] = gw31;
   }
-  {  // db3[j]: threads with c == j; sum Q: threads with c == 0
-    const int c = threadIdx.x & 15;
-    if (c < 2) atomicAdd(&L.RED[c], gb3);
-    if (c == 0) atomicAdd(&L.RED[2], qsum);
-  }
-  __syncthreads();
+  if (w == 0) atomicAdd(&L.RED[hh], gb3);  // db3[hh]: wave 0, lane (row, hh)
+  if (w == 4 && hh == 0 && q_out) atomicAdd(&L.RED[2], qsum);
+  lds_sync();
   if (threadIdx.x < 2) P[kAPB3 + threadIdx.x] = L.RED[threadIdx.x];
   if (threadIdx.x == 0 && q_out) atomicAdd(q_out, L.RED[2]);
-  SK_TP(10);
+  SK_TP(9);
 }
 
 // ---------------------------------------------------------------- Adam
@@ -796,14 +971,15 @@ __global__ void __launch_bounds__(kAdamParams * kAdamSlices) k_adam_flat(const f
     if (counter) *counter += 1;
   }
   const bool in = p < P;
+  const int pp = skpart::index(p, P);  // the partial layout (sk_partial.hpp)
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // 8 independent loads in flight
   if (in) {
     int k = slice;
     for (; k + 7 * kAdamSlices < G; k += 8 * kAdamSlices) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += partial[(int64_t)(k + j * kAdamSlices) * P + p];
+      for (int j = 0; j < 8; ++j) acc[j] += partial[(int64_t)(k + j * kAdamSlices) * P + pp];
     }
-    for (; k < G; k += kAdamSlices) acc[0] += partial[(int64_t)k * P + p];
+    for (; k < G; k += kAdamSlices) acc[0] += partial[(int64_t)k * P + pp];
   }
   const float part = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   if (slice > 0) red[slice - 1][lane] = part;
@@ -904,12 +1080,14 @@ int sk_critic_grad_bootstrap(const void* cpack, const float* obs, const float* a
   if ((((uintptr_t)cpack) & 15) || (((uintptr_t)obs) & 3) || (((uintptr_t)actions) & 3)) return SK_EINVAL;
   static bool attr = false;
   if (!attr) {
-    set_lds(k_critic_grad, kLdsCritic);
+    set_lds(k_critic_grad<true>, kLdsGrad);
+    set_lds(k_critic_grad<false>, kLdsGrad);
     attr = true;
   }
   const int64_t spw = subtiles_per_wg(batch);
   const unsigned G = (unsigned)sk_update_partials(batch);
-  k_critic_grad<<<G, kThreads, kLdsCritic, (hipStream_t)stream>>>(
+  auto kern = boot ? k_critic_grad<true> : k_critic_grad<false>;
+  kern<<<G, kThreads, kLdsGrad, (hipStream_t)stream>>>(
       obs, actions, targets, batch, row_offset, (int)spw, grad_scale, seed, call_counter, (const char*)cpack, partial,
       step_counters, n_steps, loss_sum, dropout_mask, next_obs, rewards, done, gamma,
       (const char*)target_actor_gpack, (const char*)target_critic_gpack);
@@ -923,12 +1101,12 @@ int sk_actor_grad(const void* apack, const void* cpack, const float* obs, int64_
   if ((((uintptr_t)apack) & 15) || (((uintptr_t)cpack) & 15) || (((uintptr_t)obs) & 3)) return SK_EINVAL;
   static bool attr = false;
   if (!attr) {
-    set_lds(k_actor_grad, kLdsActor);
+    set_lds(k_actor_grad, kLdsGrad);
     attr = true;
   }
   const int64_t spw = subtiles_per_wg(batch);
   const unsigned G = (unsigned)sk_update_partials(batch);
-  k_actor_grad<<<G, kThreads, kLdsActor, (hipStream_t)stream>>>(obs, batch, (int)spw, loss_scale, (const char*)apack,
+  k_actor_grad<<<G, kThreads, kLdsGrad, (hipStream_t)stream>>>(obs, batch, (int)spw, loss_scale, (const char*)apack,
                                                                 (const char*)cpack, partial, step_counters, n_steps,
                                                                 q_sum);
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;

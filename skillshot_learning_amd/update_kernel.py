@@ -55,6 +55,21 @@ def flatten_module(module):
     return flat
 
 
+def partial_index(n_params, device=None):
+    """Offset of each flat parameter in a gradient-partial row (the layout the
+    gradient kernels write and sk_adam_flat sums; csrc/sk_partial.hpp): flat
+    order, except the critic's (36,609 parameters) W2 [128][258] as [128][256]
+    main columns followed by its [128][2] action columns."""
+    idx = torch.arange(n_params, dtype=torch.int64, device=device)
+    if n_params != 36609:
+        return idx
+    w2 = 256 * 12 + 256
+    q = idx[w2:w2 + 128 * 258] - w2
+    o, i = q // 258, q % 258
+    idx[w2:w2 + 128 * 258] = torch.where(i < 256, w2 + o * 256 + i, w2 + 128 * 256 + 2 * o + (i - 256))
+    return idx
+
+
 def _offsets(params):
     out, off = [], 0
     for p in params:

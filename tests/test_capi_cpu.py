@@ -97,3 +97,18 @@ def test_cpu_backend_through_the_abi():
     step = ctypes.c_uint64()
     assert L.sk_env_get_step_counter(h, ctypes.byref(step)) == _capi.SK_OK and step.value == 1
     assert L.sk_env_destroy(h) == _capi.SK_OK
+
+
+def test_partial_layout_index_is_a_permutation():
+    """the gradient-partial layout (csrc/sk_partial.hpp): a permutation of the
+    critic's flat parameters that moves W2's action columns behind its
+    256-column rows; identity for the actor"""
+    import torch
+    from skillshot_learning_amd.update_kernel import partial_index
+    c = partial_index(36609)
+    assert torch.equal(torch.sort(c).values, torch.arange(36609))
+    w2 = 256 * 12 + 256
+    assert int(c[w2 + 258 + 5]) == w2 + 256 + 5          # W2[1][5]
+    assert int(c[w2 + 258 + 257]) == w2 + 128 * 256 + 3  # W2[1][257] (action column 1)
+    assert torch.equal(c[:w2], torch.arange(w2)) and torch.equal(c[w2 + 128 * 258:], torch.arange(w2 + 128 * 258, 36609))
+    assert torch.equal(partial_index(36482), torch.arange(36482))

@@ -170,6 +170,7 @@ def test_critic_bootstrap_grad_matches_explicit_target(mods, rows):
 
 
 def test_adam_and_soft_update_match_torch(mods):
+    from skillshot_learning_amd.update_kernel import partial_index
     learner = mods
     torch.manual_seed(0)
     d = _ddpg(learner, seed=3, tau=0.05)
@@ -180,10 +181,12 @@ def test_adam_and_soft_update_match_torch(mods):
     P = d._fused.fc.numel()
     for step in range(3):
         g = torch.randn(P, device="cuda") * 0.01
-        # kernel: partial = g, one Adam launch (with the soft update); the
-        # gradient kernel normally advances the step counters
+        # kernel: partial = g (in the partial layout), one Adam launch (with
+        # the soft update); the gradient kernel normally advances the step counters
         st.steps += 1
-        d._fused._adam(g.view(1, -1), d._fused.fc, st, d._fused.tc)
+        part = torch.empty_like(g)
+        part[partial_index(P, g.device)] = g
+        d._fused._adam(part.view(1, -1), d._fused.fc, st, d._fused.tc)
         # torch: the same gradient through torch.optim.Adam + lerp
         off = 0
         for p in ref.model_critic.parameters():

@@ -20,9 +20,9 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-CRITIC = ["start", "init", "staged", "bootstrap", "y_ready", "layer1", "layer2", "q", "dz2", "backward",
-          "store_partials", "end"]
-ACTOR = ["start", "init", "staged", "layer1x2", "layer2", "mu", "critic_dq", "dz2", "backward", "store_partials",
+CRITIC = ["start", "init", "staged", "layer1x3", "layer2x2", "q_mu_targetQ", "y_dz2", "backward", "store_partials",
+          "end"]
+ACTOR = ["start", "init", "staged", "layer1x2", "layer2x2", "mu_critic_dq", "dz3_dz2", "backward", "store_partials",
          "end"]
 
 
@@ -38,7 +38,12 @@ def timeline(t, names):
         mt, rt = t[wg, :len(names), 0], t[wg, :len(names), 1]
         rate = (mt[-1] - mt[0]) / max(rt[-1] - rt[0], 1)  # memtime ticks per 10 ns
         us = (mt - mt[0]) / rate / 100.0 if rate > 0 else (rt - rt[0]) / 100.0
-        out["first" if wg == 0 else "last"] = {n: round(float(u), 2) for n, u in zip(names, us)}
+        d = {n: round(float(u), 2) for n, u in zip(names, us)}
+        # optional sub-phase points 12..15 (diagnostic builds that set them)
+        extra = t[wg, 12:16, 0]
+        if rate > 0 and (extra > 0).all():
+            d.update({f"tp{12 + k}": round(float((x - mt[0]) / rate / 100.0), 2) for k, x in enumerate(extra)})
+        out["first" if wg == 0 else "last"] = d
     return out
 
 
