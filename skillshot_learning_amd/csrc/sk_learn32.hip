@@ -200,133 +200,6 @@ __device__ __forceinline__ f32x16 gemm_l1(const float* S, gfp W1, int n0, int la
   acc = mf4(x0, w0, acc);
   return mf4(x1, w1, acc);
 }
-// acc[i][j] += sum_{k0 <= u < k0+kc} DZ[i][u] W[u][n0 + j]: DZ in LDS
-// row-major, W global row-major (ldw), read down its columns (coalesced)
-__device__ __forceinline__ f32x16 gemm_xw(f32x16 acc, const float* DZ, int ldz, gfp W, int ldw, int n0,
-                                          int k0, int kc, int lane) {
-  const int i = lane & 31, h = lane >> 5;
-  const float* zr = DZ + i * ldz + k0 + 4 * h;
-  const gfp wc = W + (size_t)(k0 + 4 * h) * ldw + n0 + i;
-  // pipelined as gemm_xwT_p: 4 steps (16 column loads) in flight ahead
-  f4 bn[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-    bn[t] = f4{wc[(8 * t + 0) * ldw], wc[(8 * t + 1) * ldw], wc[(8 * t + 2) * ldw], wc[(8 * t + 3) * ldw]};
-  for (int k = 0; k < kc; k += 32) {
-    f4 bc[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) bc[t] = bn[t];
-    if (k + 32 < kc) {
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int r = k + 32 + 8 * t;
-        bn[t] = f4{wc[(r + 0) * ldw], wc[(r + 1) * ldw], wc[(r + 2) * ldw], wc[(r + 3) * ldw]};
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc = mf4(*(const f4*)(zr + k + 8 * t), bc[t], acc);
-  }
-  return acc;
-}
-// weight gradient over the 32 rows of a sub-tile:
-// acc[m][n] += sum_i DZ[i][m0 + m] X[i][n0 + n] (both in LDS)
-__device__ __forceinline__ f32x16 gemm_wgrad(f32x16 acc, const float* DZ, int ldz, int m0, const float* X, int ldx,
-                                             int n0, int lane) {
-  const int j = lane & 31, h = lane >> 5;
-#pragma unroll
-  for (int k = 0; k < 32; k += 8) {
-    const int r = k + 4 * h;
-    const f4 a = {DZ[(r + 0) * ldz + m0 + j], DZ[(r + 1) * ldz + m0 + j], DZ[(r + 2) * ldz + m0 + j],
-                  DZ[(r + 3) * ldz + m0 + j]};
-    const f4 b = {X[(r + 0) * ldx + n0 + j], X[(r + 1) * ldx + n0 + j], X[(r + 2) * ldx + n0 + j],
-                  X[(r + 3) * ldx + n0 + j]};
-    acc = mf4(a, b, acc);
-  }
-  return acc;
-}
-
-// row reductions: thread t owns row t/16 and 8 of its 128 units; every lane
-// of the 16-lane group returns the row's sum
-__device__ __forceinline__ float row_dot128(const float* X, int ldx, gfp w, int ws) {
-  const int i = threadIdx.x >> 4, c = threadIdx.x & 15;
-  float s = 0.f;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) s += X[i * ldx + 8 * c + k] * w[(8 * c + k) * ws];
-#pragma unroll
-  for (int off = 1; off < 16; off <<= 1) s += __shfl_xor(s, off, 64);
-  return s;
-}
-__device__ __forceinline__ float row_sum128(const float* X, int ldx) {
-  const int i = threadIdx.x >> 4, c = threadIdx.x & 15;
-  float s = 0.f;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) s += X[i * ldx + 8 * c + k];
-#pragma unroll
-  for (int off = 1; off < 16; off <<= 1) s += __shfl_xor(s, off, 64);
-  return s;
-}
-
-// ------------------------------------------------------------ shared layers
-// relu(S W1^T + b1) of n-tile w into H (inference; no Dropout)
-__device__ __forceinline__ void layer1_relu(const float* S, const Net& n, float* H, int w, int lane) {
-  const f32x16 acc = gemm_l1<false>(S, n.W1, 32 * w, lane);
-  const int u = 32 * w + (lane & 31);
-  const float b = n.b1[u];
-#pragma unroll
-  for (int v = 0; v < 16; ++v) H[drow(v, lane) * kLdH1 + u] = fmaxf(acc[v] + b, 0.f);
-}
-
-// layer 2 pre-activation over the 256 hidden inputs, split over the 8 waves:
-// wave w computes n-tile w & 3 over inputs 128 (w >> 2) ..; the upper half's
-// partial goes through XCH.  Returns the full sum in waves 0..3.
-__device__ __forceinline__ f32x16 layer2_split(const float* H, const Net& n, float* XCH, int w, int lane) {
-  const int nt = w & 3, kh = w >> 2;
-  f32x16 acc = {0};
-  acc = gemm_xwT(acc, H, kLdH1, n.W2, n.ld2, 32 * nt, 128 * kh, 128, lane);
-  if (kh) {
-#pragma unroll
-    for (int v = 0; v < 16; ++v) XCH[(nt * 16 + v) * 64 + lane] = acc[v];
-  }
-  __syncthreads();
-  if (!kh) {
-#pragma unroll
-    for (int v = 0; v < 16; ++v) acc[v] += XCH[(nt * 16 + v) * 64 + lane];
-  }
-  return acc;
-}
-
-// actor layer 3: a = tanh(W3 h2 + b3) per row into ACT[32][2] (all threads)
-__device__ __forceinline__ void actor_out(const float* H2, const Net& n, float* ACT) {
-  const int i = threadIdx.x >> 4, c = threadIdx.x & 15;
-  const float z0 = row_dot128(H2, kLdH2, n.W3, 1);
-  const float z1 = row_dot128(H2, kLdH2, n.W3 + kH2, 1);
-  if (c < 2) ACT[2 * i + c] = tanhf((c ? z1 : z0) + n.b3[c]);
-}
-
-// ---------------------------------------------------------------- LDS layout
-struct L32 {
-  float *S, *H1, *H2, *DZ2, *DZ1, *XCH, *H1C, *QZ, *S2, *A, *Y, *DQ, *A2, *R, *D, *DZ3, *RED;
-};
-constexpr int kFS = 32 * kLdS, kFH1 = 32 * kLdH1, kFH2 = 32 * kLdH2, kFX = 4 * 16 * 64;
-constexpr int kSmall = 64 + 32 + 32 + 64 + 32 + 32 + 64 + 8;
-// critic: S, H1 (the dropped-out h1), H2, DZ2, DZ1 (aliases XCH), S2, small
-constexpr size_t kLdsCritic = (size_t)(kFS + kFH1 + kFH2 + kFH2 + kFH1 + kFS + kSmall) * 4;
-// actor: S, H1 (actor), H1C (critic h1; DZ1 aliases it), H2 (actor h2),
-// DZ2 (also the critic's dQ/dz2), QZ, XCH, small
-constexpr size_t kLdsActor = (size_t)(kFS + kFH1 + kFH1 + kFH2 + kFH2 + kFH2 + kFX + kSmall) * 4;
-static_assert(kFX <= kFH1, "XCH aliases DZ1 in the critic kernel");
-
-__device__ __forceinline__ void carve_small(L32& L, float* p) {
-  L.A = p;   p += 64;
-  L.Y = p;   p += 32;
-  L.DQ = p;  p += 32;
-  L.A2 = p;  p += 64;
-  L.R = p;   p += 32;
-  L.D = p;   p += 32;
-  L.DZ3 = p; p += 64;
-  L.RED = p;
-}
-
 // stage a sub-tile's states: S[i][k] = obs (k < 12, row < B), else 0
 __device__ __forceinline__ void stage_states(float* S, const float* X, int64_t row0, int64_t B) {
   for (int t = threadIdx.x; t < 32 * kLdS; t += blockDim.x) {
@@ -335,12 +208,246 @@ __device__ __forceinline__ void stage_states(float* S, const float* X, int64_t r
   }
 }
 
+// ================================================================ gradient kernels
+// 16-row sub-tiles on v_mfma_f32_16x16x4_f32 (the fp32 MFMA rate is the
+// bound: a 16-row sub-tile per workgroup spreads a minibatch over twice the
+// CUs of 32-row tiles).  Lane l = (i = l % 16, g = l / 16): A[i][k = g],
+// B[k = g][i], D register r = D[4g + r][i] (4 consecutive rows of column i).
+// The float4 trick of the 32x32 GEMMs: lane (i, g) loads k0 + 4g .. + 3 and
+// MFMA t contracts {k0 + t, k0 + 4 + t, k0 + 8 + t, k0 + 12 + t}.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int kR = 16;                         // rows per sub-tile
+constexpr int kLdS16 = 20, kLdT16 = 20;        // [16][20] states; transposed [unit][16 rows (+4)]
+
+__device__ __forceinline__ f32x4 m16(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 m16x4(f4 a, f4 b, f32x4 c) {
+  c = m16(a.x, b.x, c);
+  c = m16(a.y, b.y, c);
+  c = m16(a.z, b.z, c);
+  return m16(a.w, b.w, c);
+}
+
+// layer 1 (K = 12): k 0..11 by lane groups 0-2 (group 3's 12..15 are zero
+// operands: S is zero-padded, W1 is not read)
+__device__ __forceinline__ f32x4 g16_l1(const float* S, gfp W1, int n0, int lane) {
+  const int i = lane & 15, g = lane >> 4;
+  const f4 x = *(const f4*)(S + i * kLdS16 + 4 * g);
+  f4 w = {0.f, 0.f, 0.f, 0.f};
+  if (g < 3) w = *(gf4u)(W1 + (n0 + i) * kIn + 4 * g);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  return m16x4(x, w, acc);
+}
+// D[row][n0 + j] = sum_k X[row][k] W[n0 + j][k] over the 256 inputs (X in
+// LDS [16][ldx], W global row-major), for one net (a) or two nets' chains
+// interleaved (b); the weight loads of the next 4 steps are in flight
+__device__ __forceinline__ f32x4 g16_xwT256(const float* X, int ldx, gfp W, int ldw, int n0, int lane) {
+  const int i = lane & 15, g = lane >> 4;
+  const float* xr = X + i * ldx + 4 * g;
+  const gfp wr = W + (size_t)(n0 + i) * ldw + 4 * g;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  f4 wn[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) wn[t] = *(gf4u)(wr + 16 * t);
+#pragma unroll
+  for (int k = 0; k < 256; k += 64) {
+    f4 wc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) wc[t] = wn[t];
+    if (k + 64 < 256) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) wn[t] = *(gf4u)(wr + k + 64 + 16 * t);
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc = m16x4(*(const f4*)(xr + k + 16 * t), wc[t], acc);
+  }
+  return acc;
+}
+__device__ __forceinline__ void g16_xwT256x2(f32x4& a0, f32x4& a1, const float* X0, gfp W0, int ldw0, const float* X1,
+                                             gfp W1, int ldw1, int n0, int lane) {
+  const int i = lane & 15, g = lane >> 4;
+  const float* x0 = X0 + i * kLdH1 + 4 * g;
+  const float* x1 = X1 + i * kLdH1 + 4 * g;
+  const gfp w0 = W0 + (size_t)(n0 + i) * ldw0 + 4 * g;
+  const gfp w1 = W1 + (size_t)(n0 + i) * ldw1 + 4 * g;
+  a0 = f32x4{0.f, 0.f, 0.f, 0.f};
+  a1 = f32x4{0.f, 0.f, 0.f, 0.f};
+  f4 n0w[2], n1w[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    n0w[t] = *(gf4u)(w0 + 16 * t);
+    n1w[t] = *(gf4u)(w1 + 16 * t);
+  }
+#pragma unroll
+  for (int k = 0; k < 256; k += 32) {
+    f4 c0[2], c1[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      c0[t] = n0w[t];
+      c1[t] = n1w[t];
+    }
+    if (k + 32 < 256) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        n0w[t] = *(gf4u)(w0 + k + 32 + 16 * t);
+        n1w[t] = *(gf4u)(w1 + k + 32 + 16 * t);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      a0 = m16x4(*(const f4*)(x0 + k + 16 * t), c0[t], a0);
+      a1 = m16x4(*(const f4*)(x1 + k + 16 * t), c1[t], a1);
+    }
+  }
+}
+// D[row][n0 + j] = sum_{u < 128} DZ[row][u] W[u][n0 + j]: DZ in LDS [16][ldz],
+// W global row-major read down its columns (16 lanes: 64 contiguous bytes)
+__device__ __forceinline__ f32x4 g16_xw128(const float* DZ, int ldz, gfp W, int ldw, int n0, int lane) {
+  const int i = lane & 15, g = lane >> 4;
+  const float* zr = DZ + i * ldz + 4 * g;
+  const gfp wc = W + (size_t)(4 * g) * ldw + n0 + i;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  f4 bn[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+    bn[t] = f4{wc[(16 * t + 0) * ldw], wc[(16 * t + 1) * ldw], wc[(16 * t + 2) * ldw], wc[(16 * t + 3) * ldw]};
+#pragma unroll
+  for (int k = 0; k < 128; k += 64) {
+    f4 bc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) bc[t] = bn[t];
+    if (k + 64 < 128) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int r = k + 64 + 16 * t;
+        bn[t] = f4{wc[(r + 0) * ldw], wc[(r + 1) * ldw], wc[(r + 2) * ldw], wc[(r + 3) * ldw]};
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc = m16x4(*(const f4*)(zr + k + 16 * t), bc[t], acc);
+  }
+  return acc;
+}
+// weight gradient of one 16 x 16 tile over the sub-tile's 16 rows: acc[m][n]
+// += sum_row AT[m0 + m][row] BT[n0 + n][row] (both transposed in LDS)
+__device__ __forceinline__ f32x4 g16_wgrad(f32x4 acc, const float* AT, int m0, const float* BT, int n0, int lane) {
+  const int i = lane & 15, g = lane >> 4;
+  return m16x4(*(const f4*)(AT + (m0 + i) * kLdT16 + 4 * g), *(const f4*)(BT + (n0 + i) * kLdT16 + 4 * g), acc);
+}
+
+// inclusive prefix sum over the 16 lanes of a DPP row (row_shr 1, 2, 4, 8,
+// zero fill): lane 15 of each row holds the row's total
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, true));
+}
+__device__ __forceinline__ float rowsum16(float v) {
+  v += dpp_f<0x111>(v);
+  v += dpp_f<0x112>(v);
+  v += dpp_f<0x114>(v);
+  v += dpp_f<0x118>(v);
+  return v;
+}
+
+// LDS-only workgroup barrier (outstanding global loads stay in flight)
+__device__ __forceinline__ void lds_sync32() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// fp32 tails of a net staged in LDS (1024 floats, the bf16 grad-pack tail
+// layout): b1 [256], b2 [128], critic action columns W2[u][256 + j] as [128][2],
+// W3 [n_out][128], b3
+constexpr int kT1 = 0, kT2 = 256, kTA = 384, kT3 = 640, kTB = 896;
+__device__ __forceinline__ float tail_src(gfp f, int ld2, int n_out, int e) {
+  if (e < kT2) return f[kPB1 + e];
+  if (e < kTA) return f[pB2(ld2) + e - kT2];
+  if (e < kT3) return ld2 == kH1 ? 0.f : f[kPW2 + ((e - kTA) >> 1) * ld2 + kH1 + ((e - kTA) & 1)];
+  if (e < kTB) return e - kT3 < n_out * kH2 ? f[pW3(ld2) + e - kT3] : 0.f;
+  return e - kTB < n_out ? f[pB3(ld2, n_out) + e - kTB] : 0.f;
+}
+
+struct G32 {
+  float *S, *S2, *ST, *H1, *H1a, *H1c, *H1T, *DZ2, *DZ2T, *DZ1T, *TL, *A, *R, *D, *Y, *QP, *MP, *YP, *DP, *RED;
+};
+constexpr int kG32Floats = 3 * kR * kLdS16 + 3 * kR * kLdH1 + kH1 * kLdT16 + kR * kLdH2 + kH2 * kLdT16 +
+                           kH1 * kLdT16 + 3 * 1024 + 32 + 16 + 16 + 16 + 8 * 16 + 8 * 32 + 8 * 16 + 8 * 32 + 4;
+constexpr size_t kLdsGrad32 = (size_t)kG32Floats * 4;
+static_assert(kLdsGrad32 <= 160 * 1024, "LDS budget of one CU");
+__device__ __forceinline__ G32 carve32(float* p) {
+  G32 L;
+  L.S = p;    p += kR * kLdS16;
+  L.S2 = p;   p += kR * kLdS16;
+  L.ST = p;   p += kR * kLdS16;
+  L.H1 = p;   p += kR * kLdH1;
+  L.H1a = p;  p += kR * kLdH1;
+  L.H1c = p;  p += kR * kLdH1;
+  L.H1T = p;  p += kH1 * kLdT16;
+  L.DZ2 = p;  p += kR * kLdH2;
+  L.DZ2T = p; p += kH2 * kLdT16;
+  L.DZ1T = p; p += kH1 * kLdT16;
+  L.TL = p;   p += 3 * 1024;
+  L.A = p;    p += 32;
+  L.R = p;    p += 16;
+  L.D = p;    p += 16;
+  L.Y = p;    p += 16;
+  L.QP = p;   p += 8 * 16;  // per-wave partial row sums: [wave][row]
+  L.MP = p;   p += 8 * 32;  //                             [wave][row][2]
+  L.YP = p;   p += 8 * 16;
+  L.DP = p;   p += 8 * 32;
+  L.RED = p;
+  return L;
+}
+// Dropout keep bits of n-tiles w and w + 8 (16 units each): bit 4j + r is
+// row 4g + r of the sub-tile, unit 16 (w + 8j) + i (rng.dropout_keep: the mask
+// of global row key + row, Philox word row % 4 of counter (row / 4, unit))
+__device__ __forceinline__ uint32_t dropout_bits16(uint64_t seed, uint64_t call, int64_t key, int w, int lane) {
+  const int i = lane & 15, g = lane >> 4;
+  uint32_t bits = 0;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const uint4 u = philox(make_uint4((uint32_t)((key + 4 * g) >> 2), (uint32_t)(16 * (w + 8 * j) + i), (uint32_t)call,
+                                      (uint32_t)(call >> 32)),
+                           (uint32_t)seed, (uint32_t)(seed >> 32));
+    bits |= ((uint32_t)(u.x >= 858993460u) | ((uint32_t)(u.y >= 858993460u) << 1) |
+             ((uint32_t)(u.z >= 858993460u) << 2) | ((uint32_t)(u.w >= 858993460u) << 3)) << (4 * j);
+  }
+  return bits;
+}
+// layer-1 epilogue of n-tile nt: relu(acc + b1) (x Dropout keep bits) ->
+// H [row][unit] and, if HT, HT [unit][rows] (one 16-byte write)
+__device__ __forceinline__ void l1_out(f32x4 acc, const float* tl, int nt, int lane, float* H, float* HT, bool drop,
+                                       uint32_t bits4) {
+  const int i = lane & 15, g = lane >> 4, n = 16 * nt + i;
+  const float b = tl[kT1 + n];
+  f4 z;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float v = fmaxf(acc[r] + b, 0.f);
+    if (drop) v = (bits4 >> r) & 1u ? v * 1.25f : 0.f;
+    z[r] = v;
+    H[(4 * g + r) * kLdH1 + n] = v;
+  }
+  if (HT) *(f4*)(HT + n * kLdT16 + 4 * g) = z;
+}
+
 // ---------------------------------------------------------------- critic step
 // Critic.forward in training mode + MSE backward (critic.fit,
 // SkillshotLearner.py:434; DDPG.critic_step): dL/dq = grad_scale (q - y),
 // grad_scale = 2 / global batch; Dropout keep-mask of global row key_row0 +
-// row (rng.dropout_keep), keep -> x 1.25.  With tap (target actor): y = r +
-// gamma (1 - done) Q'(s', mu'(s')) from the target nets first.
+// row (rng.dropout_keep), keep -> x 1.25.  BOOT: y = r + gamma (1 - done)
+// Q'(s', mu'(s')) from the target nets, in the same phases (wave w: layer-2
+// unit tile w, layer-1 / dz1 tiles w and w + 8):
+//   0  stage s, a (s', r, done), the nets' tails; Dropout bits meanwhile
+//   1  layer 1 of the critic (Dropout), the target actor, the target critic
+//   2  layer 2 of the critic and of the target actor (chains interleaved);
+//      per-wave partial row sums of q and mu'
+//   3  mu'(s') from the partials; the target critic's layer 2 -> Q' partials
+//   4  y, dL/dq per row; dz2 of the wave's units
+//   5  dW2 (16 tiles per wave), dz1;  6  dW1
+template <bool BOOT>
 __global__ void __launch_bounds__(kThreads) k_critic_grad32(
     const float* __restrict__ cflat, const float* __restrict__ Sg, const float* __restrict__ Ag,
     const float* __restrict__ Yg, int64_t B, int64_t key_row0, int sub_per_wg, float grad_scale, uint64_t seed,
@@ -349,209 +456,241 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad32(
     const float* __restrict__ Rg, const float* __restrict__ Dg, float gamma, const float* __restrict__ taflat,
     const float* __restrict__ tcflat) {
   extern __shared__ __attribute__((aligned(16))) float smem32[];
-  L32 L;
-  float* p = smem32;
-  L.S = p;   p += kFS;
-  L.H1 = p;  p += kFH1;
-  L.H2 = p;  p += kFH2;
-  L.DZ2 = p; p += kFH2;
-  L.DZ1 = p; p += kFH1;
-  L.XCH = L.DZ1;
-  L.S2 = p;  p += kFS;
-  carve_small(L, p);
-  const int lane0 = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const G32 L = carve32(smem32);
+  TP32(0);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t call = (uint64_t)*call_ctr;
   if (blockIdx.x == 0 && threadIdx.x < n_steps) step_ctr[threadIdx.x] += 1.0f;  // Adam's step (read by k_adam_flat)
-  f32x16 gW2[4], gW1 = {0};
+  const float* TLc = L.TL;
+  const float* TLa = L.TL + 1024;
+  const float* TLt = L.TL + 2048;
+  f32x4 gW2[16], gW1[2];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) gW2[t] = f32x16{0};
-  // per-unit sums over rows: thread t < 256 owns b1[t]; t < 128 b2, W2 action columns, W3
-  float gb1 = 0.f, gb2 = 0.f, gwa0 = 0.f, gwa1 = 0.f, gw3 = 0.f, gb3 = 0.f, lsum = 0.f;
-  const int u2 = w & 3;  // layer-2 n-tile of this wave (waves 0..3 hold the sums)
-  TP32(0);
+  for (int t = 0; t < 16; ++t) gW2[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  gW1[0] = gW1[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // per-lane partial sums: b1 of units 16(w + 8j) + i, b2 / W2 action
+  // columns / W3 of unit 16w + i (over the lane's rows), db3 and the loss
+  float gb1[2] = {0.f, 0.f}, gb2 = 0.f, gwa0 = 0.f, gwa1 = 0.f, gw3 = 0.f, gb3 = 0.f, lsum = 0.f;
+  if (threadIdx.x < 4) L.RED[threadIdx.x] = 0.f;
   for (int sub = 0; sub < sub_per_wg; ++sub) {
-    const int64_t row0 = ((int64_t)blockIdx.x * sub_per_wg + sub) * 32;
+    const int64_t row0 = ((int64_t)blockIdx.x * sub_per_wg + sub) * kR;
     if (row0 >= B) break;  // uniform across the workgroup
-    const int lane = launder_lane(lane0);
+    const int tid = launder_lane(threadIdx.x), lane = tid & 63, i = lane & 15, g = lane >> 4;
+    const int u = 16 * w + i;  // the lane's layer-2 unit
     const Net C = net_of(launder(cflat), kCLd, 1);
-    stage_states(L.S, Sg, row0, B);
-    if (threadIdx.x < 64) L.A[threadIdx.x] = row0 + (threadIdx.x >> 1) < B ? Ag[row0 * 2 + threadIdx.x] : 0.f;
-    if (taflat) {
-      stage_states(L.S2, S2g, row0, B);
-      if (threadIdx.x < 32) {
-        const bool ok = row0 + threadIdx.x < B;
-        L.R[threadIdx.x] = ok ? Rg[row0 + threadIdx.x] : 0.f;
-        L.D[threadIdx.x] = ok ? Dg[row0 + threadIdx.x] : 0.f;
-      }
-      __syncthreads();
-      TP32(1);
-      // ---- bootstrap target: mu'(s') then Q'(s', mu'(s')), inference
-      const Net TA = net_of(launder(taflat), kALd, 2), TC = net_of(launder(tcflat), kCLd, 1);
-      layer1_relu(L.S2, TA, L.H1, w, lane);
-      __syncthreads();
-      {
-        const f32x16 acc = layer2_split(L.H1, TA, L.XCH, w, lane);
-        if (w < 4) {
-          const int u = 32 * u2 + (lane & 31);
-          const float b = TA.b2[u];
+    // ---- phase 0: every global load, the Dropout bits while they fly, then LDS
+    const int si = (tid & 255) >> 4, sk = tid & 15;
+    const float* src = tid < 256 ? Sg : S2g;
+    const bool want_s = tid < 256 || BOOT;
+    const float sv = want_s && sk < kIn && row0 + si < B ? src[(row0 + si) * kIn + sk] : 0.f;
+    const float av = tid < 32 && row0 + (tid >> 1) < B ? Ag[row0 * 2 + tid] : 0.f;
+    const bool rok = tid < kR && row0 + tid < B;
+    const float rv = rok ? (BOOT ? Rg[row0 + tid] : Yg[row0 + tid]) : 0.f;
+    const float dv = BOOT && rok ? Dg[row0 + tid] : 0.f;
+    float tv[6];
+    if (sub == 0) {
 #pragma unroll
-          for (int v = 0; v < 16; ++v) L.H2[drow(v, lane) * kLdH2 + u] = fmaxf(acc[v] + b, 0.f);
-        }
+      for (int k = 0; k < 6; ++k) {
+        const int net = k >> 1, e = tid + kThreads * (k & 1);
+        tv[k] = net == 0 ? tail_src(C.W1, kCLd, 1, e)
+                         : (BOOT ? (net == 1 ? tail_src((gfp)launder(taflat), kALd, 2, e)
+                                             : tail_src((gfp)launder(tcflat), kCLd, 1, e))
+                                 : 0.f);
       }
-      __syncthreads();
-      TP32(2);
-      actor_out(L.H2, TA, L.A2);
-      layer1_relu(L.S2, TC, L.H1, w, lane);  // H1 was last read before the previous barrier
-      __syncthreads();
-      {
-        const f32x16 acc = layer2_split(L.H1, TC, L.XCH, w, lane);
-        if (w < 4) {
-          const int u = 32 * u2 + (lane & 31);
-          const float b = TC.b2[u], wa0 = TC.W2[u * kCLd + kH1], wa1 = TC.W2[u * kCLd + kH1 + 1];
-#pragma unroll
-          for (int v = 0; v < 16; ++v) {
-            const int i = drow(v, lane);
-            L.H2[i * kLdH2 + u] = fmaxf(acc[v] + b + L.A2[2 * i] * wa0 + L.A2[2 * i + 1] * wa1, 0.f);
-          }
-        }
-      }
-      __syncthreads();
-      {
-        const float q2 = TC.b3[0] + row_dot128(L.H2, kLdH2, TC.W3, 1);
-        const int i = threadIdx.x >> 4;
-        if ((threadIdx.x & 15) == 0) L.Y[i] = L.R[i] + gamma * (1.f - L.D[i]) * q2;
-      }
-      TP32(3);
-    } else if (threadIdx.x < 32) {
-      L.Y[threadIdx.x] = row0 + threadIdx.x < B ? Yg[row0 + threadIdx.x] : 0.f;
     }
-    __syncthreads();
-    // ---- layer 1 with Dropout: wave w -> units 32w ..
+    uint32_t keep = dropout_bits16(seed, call, key_row0 + row0, w, lane);
+    asm volatile("" : "+v"(keep));  // computed here, under the loads' latency
+    if (mask_out) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (row0 + 4 * g + r < B) mask_out[(row0 + 4 * g + r) * kH1 + 16 * (w + 8 * j) + i] = (keep >> (4 * j + r)) & 1u;
+    }
+    if (tid < 256) {
+      L.S[si * kLdS16 + sk] = sv;
+      L.ST[sk * kLdT16 + si] = sv;  // feature rows 12..15 get zeros
+    } else if (BOOT) {
+      L.S2[si * kLdS16 + sk] = sv;
+    }
+    if (tid < 32) L.A[tid] = av;
+    if (tid < kR) {
+      if (BOOT) {
+        L.R[tid] = rv;
+        L.D[tid] = dv;
+      } else {
+        L.Y[tid] = rv;
+      }
+    }
+    if (sub == 0) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k)
+        if (k < 2 || BOOT) L.TL[(k >> 1) * 1024 + tid + kThreads * (k & 1)] = tv[k];
+    }
+    lds_sync32();
+    TP32(1);
+    // ---- phase 1: layer 1, n-tiles w and w + 8, of the critic (Dropout), target actor, target critic
+    const Net TA = net_of(launder(BOOT ? taflat : cflat), kALd, 2), TC = net_of(launder(BOOT ? tcflat : cflat), kCLd, 1);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int nt = w + 8 * j;
+      l1_out(g16_l1(L.S, C.W1, 16 * nt, lane), TLc, nt, lane, L.H1, L.H1T, true, keep >> (4 * j));
+      if (BOOT) {
+        l1_out(g16_l1(L.S2, TA.W1, 16 * nt, lane), TLa, nt, lane, L.H1a, nullptr, false, 0);
+        l1_out(g16_l1(L.S2, TC.W1, 16 * nt, lane), TLt, nt, lane, L.H1c, nullptr, false, 0);
+      }
+    }
+    lds_sync32();
+    TP32(2);
+    // ---- phase 2: critic h2 (registers) and per-wave q partials; target actor mu' partials
+    float h2[4];
     {
-      const f32x16 acc = gemm_l1<false>(L.S, C.W1, 32 * w, lane);
-      const int u = 32 * w + (lane & 31);
-      const float b = C.b1[u];
+      f32x4 acc, acca;
+      if (BOOT) g16_xwT256x2(acc, acca, L.H1, C.W2, kCLd, L.H1a, TA.W2, kALd, 16 * w, lane);
+      else acc = g16_xwT256(L.H1, kLdH1, C.W2, kCLd, 16 * w, lane);
+      const float b2 = TLc[kT2 + u], wa0 = TLc[kTA + 2 * u], wa1 = TLc[kTA + 2 * u + 1], w3 = TLc[kT3 + u];
+      const f4 a01 = *(const f4*)(L.A + 8 * g), a23 = *(const f4*)(L.A + 8 * g + 4);  // a[4g + r][0..1]
+      const float a0[4] = {a01.x, a01.z, a23.x, a23.z}, a1[4] = {a01.y, a01.w, a23.y, a23.w};
+      f4 qp;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int i0 = drow(4 * g, lane);
-        const uint4 r = philox(make_uint4((uint32_t)((key_row0 + row0 + i0) >> 2), (uint32_t)u, (uint32_t)call,
-                                          (uint32_t)(call >> 32)),
-                               (uint32_t)seed, (uint32_t)(seed >> 32));
-        const uint32_t wd[4] = {r.x, r.y, r.z, r.w};
+      for (int r = 0; r < 4; ++r) {
+        h2[r] = fmaxf(acc[r] + b2 + a0[r] * wa0 + a1[r] * wa1, 0.f);
+        qp[r] = rowsum16(h2[r] * w3);
+      }
+      if (i == 15) *(f4*)(L.QP + 16 * w + 4 * g) = qp;
+      if (BOOT) {
+        const float b2a = TLa[kT2 + u], w30 = TLa[kT3 + u], w31 = TLa[kT3 + kH2 + u];
+        f4 m0, m1;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const bool keep = wd[q] >= 858993460u;  // P(drop) = 0.2 (Dropout(0.2), SkillshotLearner.py:105)
-          const float z = fmaxf(acc[4 * g + q] + b, 0.f);
-          L.H1[(i0 + q) * kLdH1 + u] = keep ? z * 1.25f : 0.f;
-          if (mask_out && row0 + i0 + q < B) mask_out[(row0 + i0 + q) * kH1 + u] = keep;
+        for (int r = 0; r < 4; ++r) {
+          const float h = fmaxf(acca[r] + b2a, 0.f);
+          m0[r] = rowsum16(h * w30);
+          m1[r] = rowsum16(h * w31);
+        }
+        if (i == 15) {
+          *(f4*)(L.MP + 32 * w + 8 * g) = f4{m0.x, m1.x, m0.y, m1.y};
+          *(f4*)(L.MP + 32 * w + 8 * g + 4) = f4{m0.z, m1.z, m0.w, m1.w};
         }
       }
     }
-    __syncthreads();
+    lds_sync32();
+    TP32(3);
+    // ---- phase 3 (BOOT): mu'(s') of the lane's rows, the target critic's layer 2 -> Q' partials
+    if (BOOT) {
+      f4 s01 = {0.f, 0.f, 0.f, 0.f}, s23 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int v = 0; v < 8; ++v) {
+        s01 += *(const f4*)(L.MP + 32 * v + 8 * g);
+        s23 += *(const f4*)(L.MP + 32 * v + 8 * g + 4);
+      }
+      const float ap0[4] = {tanhf(s01.x + TLa[kTB]), tanhf(s01.z + TLa[kTB]), tanhf(s23.x + TLa[kTB]),
+                            tanhf(s23.z + TLa[kTB])};
+      const float ap1[4] = {tanhf(s01.y + TLa[kTB + 1]), tanhf(s01.w + TLa[kTB + 1]), tanhf(s23.y + TLa[kTB + 1]),
+                            tanhf(s23.w + TLa[kTB + 1])};
+      const f32x4 acc = g16_xwT256(L.H1c, kLdH1, TC.W2, kCLd, 16 * w, lane);
+      const float b2 = TLt[kT2 + u], wa0 = TLt[kTA + 2 * u], wa1 = TLt[kTA + 2 * u + 1], w3 = TLt[kT3 + u];
+      f4 yp;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) yp[r] = rowsum16(fmaxf(acc[r] + b2 + ap0[r] * wa0 + ap1[r] * wa1, 0.f) * w3);
+      if (i == 15) *(f4*)(L.YP + 16 * w + 4 * g) = yp;
+      lds_sync32();
+    }
     TP32(4);
-    // ---- layer 2 (+ the two action columns) -> h2
+    // ---- phase 4: y and dL/dq of the lane's rows; dz2 = dL/dq W3 relu'(h2) of unit u
     {
-      const f32x16 acc = layer2_split(L.H1, C, L.XCH, w, lane);
-      if (w < 4) {
-        const int u = 32 * u2 + (lane & 31);
-        const float b = C.b2[u], wa0 = C.W2[u * kCLd + kH1], wa1 = C.W2[u * kCLd + kH1 + 1];
+      f4 q = {TLc[kTB], TLc[kTB], TLc[kTB], TLc[kTB]}, yq = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const int i = drow(v, lane);
-          L.H2[i * kLdH2 + u] = fmaxf(acc[v] + b + L.A[2 * i] * wa0 + L.A[2 * i + 1] * wa1, 0.f);
+      for (int v = 0; v < 8; ++v) {
+        q += *(const f4*)(L.QP + 16 * v + 4 * g);
+        if (BOOT) yq += *(const f4*)(L.YP + 16 * v + 4 * g);
+      }
+      const f4 rr = *(const f4*)((BOOT ? L.R : L.Y) + 4 * g);
+      const f4 dd = BOOT ? *(const f4*)(L.D + 4 * g) : f4{0.f, 0.f, 0.f, 0.f};
+      const float w3 = TLc[kT3 + u];
+      const f4 a01 = *(const f4*)(L.A + 8 * g), a23 = *(const f4*)(L.A + 8 * g + 4);
+      const float a0[4] = {a01.x, a01.z, a23.x, a23.z}, a1[4] = {a01.y, a01.w, a23.y, a23.w};
+      f4 dz;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float y = BOOT ? rr[r] + gamma * (1.f - dd[r]) * (TLt[kTB] + yq[r]) : rr[r];
+        const float e = row0 + 4 * g + r < B ? q[r] - y : 0.f;
+        const float dq = grad_scale * e;
+        if (w == 0 && i == 0) {
+          gb3 += dq;
+          lsum += e * e;
         }
-      }
-    }
-    __syncthreads();
-    TP32(5);
-    // ---- q, dL/dq (rows beyond B: 0)
-    {
-      const float q = C.b3[0] + row_dot128(L.H2, kLdH2, C.W3, 1);
-      const int i = threadIdx.x >> 4;
-      if ((threadIdx.x & 15) == 0) {
-        const float e = row0 + i < B ? q - L.Y[i] : 0.f;
-        L.DQ[i] = grad_scale * e;
-        gb3 += grad_scale * e;
-        lsum += e * e;
-      }
-    }
-    __syncthreads();
-    // ---- dz2 = dq W3 relu'(h2)
-    for (int t = threadIdx.x; t < 32 * kH2; t += kThreads) {
-      const int i = t >> 7, u = t & 127;
-      const float h = L.H2[i * kLdH2 + u];
-      L.DZ2[i * kLdH2 + u] = h > 0.f ? L.DQ[i] * C.W3[u] : 0.f;
-    }
-    __syncthreads();
-    TP32(6);
-    if (threadIdx.x < kH2) {  // per-unit sums: b2, the action columns of W2, W3
-      const int u = threadIdx.x;
-      for (int i = 0; i < 32; ++i) {
-        const float d = L.DZ2[i * kLdH2 + u];
+        const float d = h2[r] > 0.f ? dq * w3 : 0.f;
+        dz[r] = d;
+        L.DZ2[(4 * g + r) * kLdH2 + u] = d;
         gb2 += d;
-        gwa0 += d * L.A[2 * i];
-        gwa1 += d * L.A[2 * i + 1];
-        gw3 += L.DQ[i] * L.H2[i * kLdH2 + u];
+        gwa0 += d * a0[r];
+        gwa1 += d * a1[r];
+        gw3 += dq * h2[r];
       }
+      *(f4*)(L.DZ2T + u * kLdT16 + 4 * g) = dz;
     }
-    // ---- dW2[u][k] += sum_i dz2[i][u] h1d[i][k]: wave w, u-tile w & 3, k-tiles 4 (w >> 2) ..
+    lds_sync32();
+    TP32(5);
+    // ---- phase 5: dW2 (unit tile w x 16 input tiles), dz1 of n-tiles w, w + 8
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      __builtin_amdgcn_sched_barrier(0); gW2[t] = gemm_wgrad(gW2[t], L.DZ2, kLdH2, 32 * u2, L.H1, kLdH1, 32 * (4 * (w >> 2) + t), lane);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    // ---- dz1 = (dz2 W2) x 1.25 relu'(kept h1): wave w -> units 32w ..
-    {
-      f32x16 acc = {0};
-      acc = gemm_xw(acc, L.DZ2, kLdH2, C.W2, kCLd, 32 * w, 0, kH2, lane);
-      const int u = 32 * w + (lane & 31);
+    for (int kt = 0; kt < 16; ++kt) gW2[kt] = g16_wgrad(gW2[kt], L.DZ2T, 16 * w, L.H1T, 16 * kt, lane);
 #pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const int i = drow(v, lane);
-        L.DZ1[i * kLdH1 + u] = L.H1[i * kLdH1 + u] > 0.f ? acc[v] * 1.25f : 0.f;
+    for (int j = 0; j < 2; ++j) {
+      const int n = 16 * (w + 8 * j) + i;
+      const f32x4 acc = g16_xw128(L.DZ2, kLdH2, C.W2, kCLd, 16 * (w + 8 * j), lane);
+      f4 d;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        d[r] = L.H1[(4 * g + r) * kLdH1 + n] > 0.f ? acc[r] * 1.25f : 0.f;
+        gb1[j] += d[r];
       }
+      *(f4*)(L.DZ1T + n * kLdT16 + 4 * g) = d;
     }
-    __syncthreads();
+    lds_sync32();
+    TP32(6);
+    // ---- phase 6: dW1 of unit tiles w, w + 8 (input columns 12..15 discarded)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) gW1[j] = g16_wgrad(gW1[j], L.DZ1T, 16 * (w + 8 * j), L.ST, 0, lane);
+    lds_sync32();  // the next sub-tile restages
     TP32(7);
-    if (threadIdx.x < kH1) {
-      for (int i = 0; i < 32; ++i) gb1 += L.DZ1[i * kLdH1 + threadIdx.x];
-    }
-    // ---- dW1[u][c] += sum_i dz1[i][u] s[i][c]: wave w, u-tile w (columns c >= 12 discarded)
-    gW1 = gemm_wgrad(gW1, L.DZ1, kLdH1, 32 * w, L.S, kLdS, 0, lane);
-    __syncthreads();  // the next sub-tile restages S / H1
-    TP32(8);
   }
-  // ---- this workgroup's partial gradient (torch parameters() order)
+  // ---- this workgroup's partial gradient (sk_partial.hpp layout)
   float* P = partial + (int64_t)blockIdx.x * kCP;
-  const int lane = lane0;
-  {
-    const int j = lane & 31;
+  const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4, u = 16 * w + i;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int k = 32 * (4 * (w >> 2) + t) + j;
+  for (int kt = 0; kt < 16; ++kt)
 #pragma unroll
-      for (int v = 0; v < 16; ++v) P[skpart::critic_w2_main(32 * u2 + drow(v, lane), k)] = gW2[t][v];
+    for (int r = 0; r < 4; ++r) P[skpart::critic_w2_main(16 * w + 4 * g + r, 16 * kt + i)] = gW2[kt][r];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    if (i < kIn) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) P[kPW1 + (16 * (w + 8 * j) + 4 * g + r) * kIn + i] = gW1[j][r];
     }
-    if (j < kIn) {
-#pragma unroll
-      for (int v = 0; v < 16; ++v) P[kPW1 + (32 * w + drow(v, lane)) * kIn + j] = gW1[v];
-    }
+    float b = gb1[j] + __shfl_xor(gb1[j], 16, 64);
+    b += __shfl_xor(b, 32, 64);
+    if (g == 0) P[kPB1 + 16 * (w + 8 * j) + i] = b;
   }
-  if (threadIdx.x < kH1) P[kPB1 + threadIdx.x] = gb1;
-  if (threadIdx.x < kH2) {
-    const int u = threadIdx.x;
+  TP32(8);
+  gb2 += __shfl_xor(gb2, 16, 64);
+  gb2 += __shfl_xor(gb2, 32, 64);
+  gwa0 += __shfl_xor(gwa0, 16, 64);
+  gwa0 += __shfl_xor(gwa0, 32, 64);
+  gwa1 += __shfl_xor(gwa1, 16, 64);
+  gwa1 += __shfl_xor(gwa1, 32, 64);
+  gw3 += __shfl_xor(gw3, 16, 64);
+  gw3 += __shfl_xor(gw3, 32, 64);
+  if (g == 0) {
     P[pB2(kCLd) + u] = gb2;
     P[skpart::critic_w2_action(u, 0)] = gwa0;
     P[skpart::critic_w2_action(u, 1)] = gwa1;
     P[pW3(kCLd) + u] = gw3;
   }
-  if (threadIdx.x < 2) L.RED[threadIdx.x] = 0.f;
-  __syncthreads();
-  if ((threadIdx.x & 15) == 0) {
+  if (w == 0 && i == 0) {  // wave 0, one lane per row group: db3 and loss partials
     atomicAdd(&L.RED[0], gb3);
     atomicAdd(&L.RED[1], lsum);
   }
-  __syncthreads();
+  lds_sync32();
   if (threadIdx.x == 0) {
     P[pB3(kCLd, 1)] = L.RED[0];
     if (loss_out) atomicAdd(loss_out, L.RED[1]);
@@ -562,150 +701,203 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad32(
 // ---------------------------------------------------------------- actor step
 // model_actor_fit_step (SkillshotLearner.py:386-417): gradient of
 // -loss_scale * sum_b Q(s_b, mu(s_b)) w.r.t. the actor, critic at inference.
+//   0  stage s, the nets' tails
+//   1  layer 1 of the actor (-> H1, H1T) and of the critic (-> H1c)
+//   2  the actor's layer 2 (-> h2 registers, mu partials) and the critic's
+//      layer-2 MFMA (held; its action columns join in phase 3), interleaved
+//   3  mu per row; critic z2 at (s, mu): dQ/da and Q partials
+//   4  dL/dz3 = -loss_scale dQ/da (1 - a^2) per row; dz2 of unit 16w + i
+//   5  dW2, dz1;  6  dW1
 __global__ void __launch_bounds__(kThreads) k_actor_grad32(const float* __restrict__ aflat,
                                                            const float* __restrict__ cflat,
                                                            const float* __restrict__ Sg, int64_t B, int sub_per_wg,
                                                            float loss_scale, float* __restrict__ partial,
                                                            float* step_ctr, int n_steps, float* __restrict__ q_out) {
   extern __shared__ __attribute__((aligned(16))) float smem32[];
-  L32 L;
-  float* p = smem32;
-  L.S = p;   p += kFS;
-  L.H1 = p;  p += kFH1;
-  L.H1C = p; p += kFH1;
-  L.DZ1 = L.H1C;
-  L.H2 = p;  p += kFH2;
-  L.DZ2 = p; p += kFH2;
-  L.QZ = p;  p += kFH2;
-  L.XCH = p; p += kFX;
-  carve_small(L, p);
-  const int lane0 = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const G32 L = carve32(smem32);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (blockIdx.x == 0 && threadIdx.x < n_steps) step_ctr[threadIdx.x] += 1.0f;
-  f32x16 gW2[4], gW1 = {0};
+  const float* TLa = L.TL;
+  const float* TLc = L.TL + 1024;
+  f32x4 gW2[16], gW1[2];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) gW2[t] = f32x16{0};
-  float gb1 = 0.f, gb2 = 0.f, gw30 = 0.f, gw31 = 0.f, gb3 = 0.f, qsum = 0.f;
-  const int u2 = w & 3;
+  for (int t = 0; t < 16; ++t) gW2[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  gW1[0] = gW1[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float gb1[2] = {0.f, 0.f}, gb2 = 0.f, gw30 = 0.f, gw31 = 0.f, gb30 = 0.f, gb31 = 0.f, qsum = 0.f;
+  if (threadIdx.x < 4) L.RED[threadIdx.x] = 0.f;
   for (int sub = 0; sub < sub_per_wg; ++sub) {
-    const int64_t row0 = ((int64_t)blockIdx.x * sub_per_wg + sub) * 32;
+    const int64_t row0 = ((int64_t)blockIdx.x * sub_per_wg + sub) * kR;
     if (row0 >= B) break;
-    const int lane = launder_lane(lane0);
+    const int tid = launder_lane(threadIdx.x), lane = tid & 63, i = lane & 15, g = lane >> 4;
+    const int u = 16 * w + i;
     const Net A = net_of(launder(aflat), kALd, 2), C = net_of(launder(cflat), kCLd, 1);
-    stage_states(L.S, Sg, row0, B);
-    __syncthreads();
-    layer1_relu(L.S, A, L.H1, w, lane);
-    layer1_relu(L.S, C, L.H1C, w, lane);
-    __syncthreads();
-    {  // actor h2
-      const f32x16 acc = layer2_split(L.H1, A, L.XCH, w, lane);
-      if (w < 4) {
-        const int u = 32 * u2 + (lane & 31);
-        const float b = A.b2[u];
+    // ---- phase 0
+    const int si = tid >> 4, sk = tid & 15;
+    const float sv = tid < 256 && sk < kIn && row0 + si < B ? Sg[(row0 + si) * kIn + sk] : 0.f;
+    float tv[4];
+    if (sub == 0) {
 #pragma unroll
-        for (int v = 0; v < 16; ++v) L.H2[drow(v, lane) * kLdH2 + u] = fmaxf(acc[v] + b, 0.f);
+      for (int k = 0; k < 4; ++k) {
+        const int e = tid + kThreads * (k & 1);
+        tv[k] = k < 2 ? tail_src(A.W1, kALd, 2, e) : tail_src(C.W1, kCLd, 1, e);
       }
     }
-    __syncthreads();
-    actor_out(L.H2, A, L.A);  // mu(s)
-    __syncthreads();
-    {  // critic layer 2 at (s, mu(s)): dQ/dz2 = W3 relu'(z2) into DZ2 (rows beyond B: 0), Q terms into QZ
-      const f32x16 acc = layer2_split(L.H1C, C, L.XCH, w, lane);
-      if (w < 4) {
-        const int u = 32 * u2 + (lane & 31);
-        const float b = C.b2[u], wa0 = C.W2[u * kCLd + kH1], wa1 = C.W2[u * kCLd + kH1 + 1], w3 = C.W3[u];
+    if (tid < 256) {
+      L.S[si * kLdS16 + sk] = sv;
+      L.ST[sk * kLdT16 + si] = sv;
+    }
+    if (sub == 0) {
 #pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const int i = drow(v, lane);
-          const float z = acc[v] + b + L.A[2 * i] * wa0 + L.A[2 * i + 1] * wa1;
-          L.DZ2[i * kLdH2 + u] = (z > 0.f && row0 + i < B) ? w3 : 0.f;
-          L.QZ[i * kLdH2 + u] = fmaxf(z, 0.f) * w3;
+      for (int k = 0; k < 4; ++k) L.TL[(k >> 1) * 1024 + tid + kThreads * (k & 1)] = tv[k];
+    }
+    lds_sync32();
+    // ---- phase 1
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int nt = w + 8 * j;
+      l1_out(g16_l1(L.S, A.W1, 16 * nt, lane), TLa, nt, lane, L.H1, L.H1T, false, 0);
+      l1_out(g16_l1(L.S, C.W1, 16 * nt, lane), TLc, nt, lane, L.H1c, nullptr, false, 0);
+    }
+    lds_sync32();
+    // ---- phase 2
+    float h2[4];
+    f32x4 zc;
+    {
+      f32x4 acc;
+      g16_xwT256x2(acc, zc, L.H1, A.W2, kALd, L.H1c, C.W2, kCLd, 16 * w, lane);
+      const float b2 = TLa[kT2 + u], w30 = TLa[kT3 + u], w31 = TLa[kT3 + kH2 + u];
+      f4 m0, m1;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        h2[r] = fmaxf(acc[r] + b2, 0.f);
+        m0[r] = rowsum16(h2[r] * w30);
+        m1[r] = rowsum16(h2[r] * w31);
+      }
+      if (i == 15) {
+        *(f4*)(L.MP + 32 * w + 8 * g) = f4{m0.x, m1.x, m0.y, m1.y};
+        *(f4*)(L.MP + 32 * w + 8 * g + 4) = f4{m0.z, m1.z, m0.w, m1.w};
+      }
+    }
+    lds_sync32();
+    // ---- phase 3: mu of the lane's rows; the critic at (s, mu)
+    float a0[4], a1[4];
+    {
+      f4 s01 = {0.f, 0.f, 0.f, 0.f}, s23 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int v = 0; v < 8; ++v) {
+        s01 += *(const f4*)(L.MP + 32 * v + 8 * g);
+        s23 += *(const f4*)(L.MP + 32 * v + 8 * g + 4);
+      }
+      a0[0] = tanhf(s01.x + TLa[kTB]);
+      a1[0] = tanhf(s01.y + TLa[kTB + 1]);
+      a0[1] = tanhf(s01.z + TLa[kTB]);
+      a1[1] = tanhf(s01.w + TLa[kTB + 1]);
+      a0[2] = tanhf(s23.x + TLa[kTB]);
+      a1[2] = tanhf(s23.y + TLa[kTB + 1]);
+      a0[3] = tanhf(s23.z + TLa[kTB]);
+      a1[3] = tanhf(s23.w + TLa[kTB + 1]);
+      const float b2 = TLc[kT2 + u], wa0 = TLc[kTA + 2 * u], wa1 = TLc[kTA + 2 * u + 1], w3 = TLc[kT3 + u];
+      f4 d0, d1, qp;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float z = zc[r] + b2 + a0[r] * wa0 + a1[r] * wa1;
+        const float dqdz = (z > 0.f && row0 + 4 * g + r < B) ? w3 : 0.f;  // dQ/dz2 (rows beyond B: 0)
+        d0[r] = rowsum16(dqdz * wa0);
+        d1[r] = rowsum16(dqdz * wa1);
+        qp[r] = rowsum16(fmaxf(z, 0.f) * w3);
+      }
+      if (i == 15) {
+        *(f4*)(L.DP + 32 * w + 8 * g) = f4{d0.x, d1.x, d0.y, d1.y};
+        *(f4*)(L.DP + 32 * w + 8 * g + 4) = f4{d0.z, d1.z, d0.w, d1.w};
+        *(f4*)(L.QP + 16 * w + 4 * g) = qp;
+      }
+    }
+    lds_sync32();
+    // ---- phase 4: dL/dz3 of the lane's rows, dz2 = (dz3 W3) relu'(h2) of unit u
+    {
+      f4 s01 = {0.f, 0.f, 0.f, 0.f}, s23 = {0.f, 0.f, 0.f, 0.f}, qs = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int v = 0; v < 8; ++v) {
+        s01 += *(const f4*)(L.DP + 32 * v + 8 * g);
+        s23 += *(const f4*)(L.DP + 32 * v + 8 * g + 4);
+        qs += *(const f4*)(L.QP + 16 * v + 4 * g);
+      }
+      const float da0[4] = {s01.x, s01.z, s23.x, s23.z}, da1[4] = {s01.y, s01.w, s23.y, s23.w};
+      const float w30 = TLa[kT3 + u], w31 = TLa[kT3 + kH2 + u];
+      f4 dz;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float z0 = -loss_scale * da0[r] * (1.f - a0[r] * a0[r]);
+        const float z1 = -loss_scale * da1[r] * (1.f - a1[r] * a1[r]);
+        if (w == 0 && i == 0) {
+          gb30 += z0;
+          gb31 += z1;
+          if (row0 + 4 * g + r < B) qsum += TLc[kTB] + qs[r];
         }
+        const float d = h2[r] > 0.f ? z0 * w30 + z1 * w31 : 0.f;
+        dz[r] = d;
+        L.DZ2[(4 * g + r) * kLdH2 + u] = d;
+        gb2 += d;
+        gw30 += z0 * h2[r];
+        gw31 += z1 * h2[r];
       }
+      *(f4*)(L.DZ2T + u * kLdT16 + 4 * g) = dz;
     }
-    __syncthreads();
-    {  // dL/dz3 = -loss_scale dQ/da (1 - a^2), dQ/da = sum_u dQ/dz2 W2[u][256 + c]
-      const int i = threadIdx.x >> 4, c = threadIdx.x & 15;
-      const float da0 = row_dot128(L.DZ2, kLdH2, C.W2 + kH1, kCLd);
-      const float da1 = row_dot128(L.DZ2, kLdH2, C.W2 + kH1 + 1, kCLd);
-      const float qrow = row_sum128(L.QZ, kLdH2);
-      if (c < 2) {
-        const float a = L.A[2 * i + c];
-        const float d = -loss_scale * (c ? da1 : da0) * (1.f - a * a);
-        L.DZ3[2 * i + c] = d;
-        gb3 += d;
-      }
-      if (c == 0 && row0 + i < B) qsum += C.b3[0] + qrow;
-    }
-    __syncthreads();
-    // dz2 = (dz3 W3) relu'(h2) (DZ2 is free again)
-    for (int t = threadIdx.x; t < 32 * kH2; t += kThreads) {
-      const int i = t >> 7, u = t & 127;
-      const float h = L.H2[i * kLdH2 + u];
-      L.DZ2[i * kLdH2 + u] = h > 0.f ? L.DZ3[2 * i] * A.W3[u] + L.DZ3[2 * i + 1] * A.W3[kH2 + u] : 0.f;
-    }
-    __syncthreads();
-    if (threadIdx.x < kH2) {
-      const int u = threadIdx.x;
-      for (int i = 0; i < 32; ++i) {
-        const float h = L.H2[i * kLdH2 + u];
-        gb2 += L.DZ2[i * kLdH2 + u];
-        gw30 += L.DZ3[2 * i] * h;
-        gw31 += L.DZ3[2 * i + 1] * h;
-      }
-    }
+    lds_sync32();
+    // ---- phase 5
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      __builtin_amdgcn_sched_barrier(0);
-      gW2[t] = gemm_wgrad(gW2[t], L.DZ2, kLdH2, 32 * u2, L.H1, kLdH1, 32 * (4 * (w >> 2) + t), lane);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    {  // dz1 = (dz2 W2) relu'(h1) into DZ1 (aliases H1C: last read before the barrier above)
-      f32x16 acc = {0};
-      acc = gemm_xw(acc, L.DZ2, kLdH2, A.W2, kALd, 32 * w, 0, kH2, lane);
-      const int u = 32 * w + (lane & 31);
+    for (int kt = 0; kt < 16; ++kt) gW2[kt] = g16_wgrad(gW2[kt], L.DZ2T, 16 * w, L.H1T, 16 * kt, lane);
 #pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const int i = drow(v, lane);
-        L.DZ1[i * kLdH1 + u] = L.H1[i * kLdH1 + u] > 0.f ? acc[v] : 0.f;
+    for (int j = 0; j < 2; ++j) {
+      const int n = 16 * (w + 8 * j) + i;
+      const f32x4 acc = g16_xw128(L.DZ2, kLdH2, A.W2, kALd, 16 * (w + 8 * j), lane);
+      f4 d;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        d[r] = L.H1[(4 * g + r) * kLdH1 + n] > 0.f ? acc[r] : 0.f;
+        gb1[j] += d[r];
       }
+      *(f4*)(L.DZ1T + n * kLdT16 + 4 * g) = d;
     }
-    __syncthreads();
-    if (threadIdx.x < kH1) {
-      for (int i = 0; i < 32; ++i) gb1 += L.DZ1[i * kLdH1 + threadIdx.x];
-    }
-    gW1 = gemm_wgrad(gW1, L.DZ1, kLdH1, 32 * w, L.S, kLdS, 0, lane);
-    __syncthreads();
+    lds_sync32();
+    // ---- phase 6
+#pragma unroll
+    for (int j = 0; j < 2; ++j) gW1[j] = g16_wgrad(gW1[j], L.DZ1T, 16 * (w + 8 * j), L.ST, 0, lane);
+    lds_sync32();
   }
   float* P = partial + (int64_t)blockIdx.x * kAP;
-  const int lane = lane0;
-  {
-    const int j = lane & 31;
+  const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4, u = 16 * w + i;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int k = 32 * (4 * (w >> 2) + t) + j;
+  for (int kt = 0; kt < 16; ++kt)
 #pragma unroll
-      for (int v = 0; v < 16; ++v) P[kPW2 + (32 * u2 + drow(v, lane)) * kALd + k] = gW2[t][v];
+    for (int r = 0; r < 4; ++r) P[kPW2 + (16 * w + 4 * g + r) * kALd + 16 * kt + i] = gW2[kt][r];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    if (i < kIn) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) P[kPW1 + (16 * (w + 8 * j) + 4 * g + r) * kIn + i] = gW1[j][r];
     }
-    if (j < kIn) {
-#pragma unroll
-      for (int v = 0; v < 16; ++v) P[kPW1 + (32 * w + drow(v, lane)) * kIn + j] = gW1[v];
-    }
+    float b = gb1[j] + __shfl_xor(gb1[j], 16, 64);
+    b += __shfl_xor(b, 32, 64);
+    if (g == 0) P[kPB1 + 16 * (w + 8 * j) + i] = b;
   }
-  if (threadIdx.x < kH1) P[kPB1 + threadIdx.x] = gb1;
-  if (threadIdx.x < kH2) {
-    const int u = threadIdx.x;
+  gb2 += __shfl_xor(gb2, 16, 64);
+  gb2 += __shfl_xor(gb2, 32, 64);
+  gw30 += __shfl_xor(gw30, 16, 64);
+  gw30 += __shfl_xor(gw30, 32, 64);
+  gw31 += __shfl_xor(gw31, 16, 64);
+  gw31 += __shfl_xor(gw31, 32, 64);
+  if (g == 0) {
     P[pB2(kALd) + u] = gb2;
     P[pW3(kALd) + u] = gw30;
     P[pW3(kALd) + kH2 + u] = gw31;
   }
-  if (threadIdx.x < 4) L.RED[threadIdx.x] = 0.f;
-  __syncthreads();
-  {
-    const int c = threadIdx.x & 15;
-    if (c < 2) atomicAdd(&L.RED[c], gb3);
-    if (c == 0) atomicAdd(&L.RED[2], qsum);
+  if (w == 0 && i == 0) {
+    atomicAdd(&L.RED[0], gb30);
+    atomicAdd(&L.RED[1], gb31);
+    atomicAdd(&L.RED[2], qsum);
   }
-  __syncthreads();
+  lds_sync32();
   if (threadIdx.x < 2) P[pB3(kALd, 2) + threadIdx.x] = L.RED[threadIdx.x];
   if (threadIdx.x == 0 && q_out) atomicAdd(q_out, L.RED[2]);
 }
@@ -851,8 +1043,8 @@ __global__ void __launch_bounds__(kFwdThreads) k_actor_fwd32(const float* __rest
   }
 }
 
-int64_t subtiles_per_wg32(int64_t B) {  // <= 256 workgroups, >= 1 sub-tile each
-  const int64_t tiles = (B + 31) / 32;
+int64_t subtiles_per_wg32(int64_t B) {  // 16-row sub-tiles; <= 256 workgroups, >= 1 sub-tile each
+  const int64_t tiles = (B + kR - 1) / kR;
   return (tiles + 255) / 256;
 }
 
@@ -868,7 +1060,7 @@ extern "C" {
 int64_t sk_update_partials_f32(int64_t batch) {
   if (batch <= 0) return 0;
   const int64_t spw = subtiles_per_wg32(batch);
-  return ((batch + 31) / 32 + spw - 1) / spw;
+  return ((batch + kR - 1) / kR + spw - 1) / spw;
 }
 
 int sk_critic_grad_f32(const float* critic_flat, const float* obs, const float* actions, const float* targets,
@@ -885,12 +1077,14 @@ int sk_critic_grad_f32(const float* critic_flat, const float* obs, const float* 
   if ((n_steps > 0 && !step_counters) || n_steps < 0 || n_steps > 64) return SK_EINVAL;
   static bool attr = false;
   if (!attr) {
-    set_lds32(k_critic_grad32, kLdsCritic);
+    set_lds32(k_critic_grad32<true>, kLdsGrad32);
+    set_lds32(k_critic_grad32<false>, kLdsGrad32);
     attr = true;
   }
   const int64_t spw = subtiles_per_wg32(batch);
   const unsigned G = (unsigned)sk_update_partials_f32(batch);
-  k_critic_grad32<<<G, kThreads, kLdsCritic, (hipStream_t)stream>>>(
+  auto kern = boot ? k_critic_grad32<true> : k_critic_grad32<false>;
+  kern<<<G, kThreads, kLdsGrad32, (hipStream_t)stream>>>(
       critic_flat, obs, actions, targets, batch, row_offset, (int)spw, grad_scale, seed, call_counter, partials,
       step_counters, n_steps, loss_sum, dropout_mask, next_obs, rewards, done, gamma, target_actor_flat,
       target_critic_flat);
@@ -904,12 +1098,12 @@ int sk_actor_grad_f32(const float* actor_flat, const float* critic_flat, const f
   if ((n_steps > 0 && !step_counters) || n_steps < 0 || n_steps > 64) return SK_EINVAL;
   static bool attr = false;
   if (!attr) {
-    set_lds32(k_actor_grad32, kLdsActor);
+    set_lds32(k_actor_grad32, kLdsGrad32);
     attr = true;
   }
   const int64_t spw = subtiles_per_wg32(batch);
   const unsigned G = (unsigned)sk_update_partials_f32(batch);
-  k_actor_grad32<<<G, kThreads, kLdsActor, (hipStream_t)stream>>>(actor_flat, critic_flat, obs, batch, (int)spw,
+  k_actor_grad32<<<G, kThreads, kLdsGrad32, (hipStream_t)stream>>>(actor_flat, critic_flat, obs, batch, (int)spw,
                                                                   loss_scale, partials, step_counters, n_steps,
                                                                   q_sum);
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;

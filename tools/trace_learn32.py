@@ -17,7 +17,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-CRITIC = ["start", "staged", "boot_actor_l2", "y_ready", "layer1", "layer2", "dq_dz2", "wgrad_dx", "subtile_end",
+CRITIC = ["start", "staged", "layer1x3", "layer2x2", "targetQ", "y_dz2", "dW2_dz1", "dW1", "store_partials",
           "end"]
 
 
