@@ -235,8 +235,8 @@ __global__ void __launch_bounds__(kCThreads) k_target_q(const float* __restrict_
       for (int i = 0; i < 16; ++i) {
         const int u = 32 * t + (i & 3) + 8 * (i >> 2);  // hidden unit - 4h
         const float y = fmaxf(acc[i] + ab2h[u], 0.f);
-        m0 += aw3h[u] * y;
-        m1 += aw3h[kH2 + u] * y;
+        m0 = __builtin_fmaf(aw3h[u], y, m0);  // the actor kernel's layer-3 order (sk_actor.hip): same bits
+        m1 = __builtin_fmaf(aw3h[kH2 + u], y, m1);
       }
     }
     m0 += __shfl_xor(m0, 32, 64);

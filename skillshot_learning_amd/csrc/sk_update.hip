@@ -192,23 +192,20 @@ __device__ __forceinline__ int launder_lane(int lane) {
 // one wave complete in order, this only keeps the compiler from reordering
 __device__ __forceinline__ void wave_lds_order() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront", "local"); }
 
-// LDS of both gradient kernels.  Regions with disjoint lifetimes alias (the
-// phase numbers of the kernels below):
-//   DZ2 + DZ2T   critic: target actor h2 H2a (phases 2-3), then dz2 (4-5)
-//   DZ1T         critic: target actor h1 H1a (1-2), target critic Q terms QT
-//                (3-4); actor: Q terms QZ (3-4); then dz1 (5)
-//   H1B          critic: target critic h1 (1-3); actor: critic h1 (1-2),
-//                then dQ/dz2 DZC (3-4)
+// LDS of both gradient kernels.  H1a (the critic kernel's target-actor h1,
+// phases 1-2) aliases DZ1T (dz1, phase 5); H1B holds the second net's h1
+// (critic: target critic, actor: critic).  QP / MP / YP / DP are per-wave
+// partial row sums (halfsum32) of the layer-2 epilogues.
 struct Lds {
   short *Sr, *S2r, *ST, *H1, *H1B, *H1T, *DZ2, *DZ2T, *DZ1T, *H1a;
-  float *H2a, *QT, *QZ, *DZC, *H2f, *TL, *A, *Y, *QV, *RB, *DB, *RED, *AW, *DW;
+  float *H2f, *TL, *A, *Y, *RB, *DB, *RED, *AW, *DW, *QP, *MP, *YP, *DP;
 };
 constexpr size_t kSzS = 32 * kLdS * 2, kSzT = 32 * kLdT * 2, kSzH1 = 32 * kLdH1 * 2, kSzH1T = kH1 * kLdT * 2;
 constexpr size_t kSzZ2 = 32 * kLdZ2 * 2, kSzZ2T = kH2 * kLdT * 2, kSzH2f = 32 * kLdH2f * 4;
-constexpr int kSmallF = 64 + 32 + 32 + 32 + 32 + 4 + 8 * 64 + 8 * 64;
+constexpr int kSmallF = 64 + 32 + 32 + 32 + 4 + 8 * 64 + 8 * 64 + 4 * 32 + 4 * 64 + 4 * 32 + 4 * 64;
 constexpr size_t kLdsGrad = 2 * kSzS + kSzT + 2 * kSzH1 + kSzH1T + kSzZ2 + kSzZ2T + kSzH1T + kSzH2f +
                             3 * 1024 * 4 + kSmallF * 4;
-static_assert(kSzH2f <= kSzZ2 + kSzZ2T && kSzH2f <= kSzH1T && kSzH1 <= kSzH1T && kSzH2f == kSzH1, "LDS aliases");
+static_assert(kSzH1 <= kSzH1T, "LDS alias");
 static_assert(kLdsGrad <= 160 * 1024, "LDS budget of one CU");
 
 __device__ __forceinline__ Lds carve(char* smem) {
@@ -228,17 +225,16 @@ __device__ __forceinline__ Lds carve(char* smem) {
   float* f = (float*)p;
   L.A = f;   f += 64;
   L.Y = f;   f += 32;
-  L.QV = f;  f += 32;
   L.RB = f;  f += 32;
   L.DB = f;  f += 32;
   L.RED = f; f += 4;
   L.AW = f;  f += 8 * 64;
-  L.DW = f;
-  L.H2a = (float*)L.DZ2;
+  L.DW = f;  f += 8 * 64;
+  L.QP = f;  f += 4 * 32;  // per-wave partial row sums over a wave's 32 units: [wave][row]
+  L.MP = f;  f += 4 * 64;  //                                                  [wave][row][2]
+  L.YP = f;  f += 4 * 32;
+  L.DP = f;
   L.H1a = L.DZ1T;
-  L.QT = (float*)L.DZ1T;
-  L.QZ = (float*)L.DZ1T;
-  L.DZC = (float*)L.H1B;
   return L;
 }
 
@@ -363,49 +359,30 @@ __device__ __forceinline__ void load_w2t(bf16x8 wt[8], const char* pack, int w, 
   for (int kk = 0; kk < 8; ++kk) wt[kk] = g[(w * 8 + kk) * 64 + lane];
 }
 
-// Row reductions done by ONE wave for all 32 rows of the sub-tile (each wave
-// that needs them computes them itself: no barrier between producer and
-// consumer).  Lane l takes row l % 32 and j = l / 32.
-// actor output a[row][j] = tanh(b3[j] + W3[j] . h2[row]) (tail of the actor)
-__device__ __forceinline__ float wave_mu(const float* H2, const float* tl, int lane) {
-  const int r = lane & 31, j = lane >> 5;
-  const float4* h = (const float4*)(H2 + r * kLdH2f);
-  const float4* wv = (const float4*)(tl + kTW3 + j * kH2);
-  float s[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int k = 0; k < 32; ++k) {
-    const float4 a = h[k], b = wv[k];
-    s[k & 3] += (a.x * b.x + a.y * b.y) + (a.z * b.z + a.w * b.w);
-  }
-  return tanhf(tl[kTB3 + j] + ((s[0] + s[1]) + (s[2] + s[3])));
+// sum over the 32 lanes of each wave half (the 32 units of a layer-2 tile,
+// per register = per row): DPP row_shr 1, 2, 4, 8 (16-lane inclusive scan,
+// zero fill), then row_bcast:15 into rows 1 and 3; lanes 31 and 63 return
+// their half's total
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWS, 0xf, true));
 }
-// sum over the 128 units of X[row] (both lane halves return it)
-__device__ __forceinline__ float wave_rowsum(const float* X, int lane) {
-  const int r = lane & 31, hh = lane >> 5;
-  const float4* x = (const float4*)(X + r * kLdH2f + 64 * hh);
-  float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-  for (int k = 0; k < 16; k += 2) {
-    const float4 a = x[k], c = x[k + 1];
-    s0 += (a.x + a.y) + (a.z + a.w);
-    s1 += (c.x + c.y) + (c.z + c.w);
-  }
-  const float s = s0 + s1;
-  return s + __shfl_xor(s, 32, 64);
+__device__ __forceinline__ float halfsum32(float v) {
+  v += dpp_f<0x111, 0xf>(v);
+  v += dpp_f<0x112, 0xf>(v);
+  v += dpp_f<0x114, 0xf>(v);
+  v += dpp_f<0x118, 0xf>(v);
+  v += dpp_f<0x142, 0xa>(v);
+  return v;
 }
-// dQ/da[row][j] = sum_u X[row][u] W2[u][256 + j] (the critic's action columns, tail layout [u][2])
-__device__ __forceinline__ float wave_dot_action_cols(const float* X, const float* tl, int lane) {
-  const int r = lane & 31, j = lane >> 5;
-  const float4* x = (const float4*)(X + r * kLdH2f);
-  const float4* wa = (const float4*)(tl + kTW2a);  // [u][2]: float4 k/2 holds units 2k', 2k'+1
-  float s[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int k = 0; k < 32; ++k) {
-    const float4 a = x[k], w0 = wa[2 * k], w1 = wa[2 * k + 1];
-    const float c0 = j ? w0.y : w0.x, c1 = j ? w0.w : w0.z, c2 = j ? w1.y : w1.x, c3 = j ? w1.w : w1.z;
-    s[k & 3] += (a.x * c0 + a.y * c1) + (a.z * c2 + a.w * c3);
-  }
-  return (s[0] + s[1]) + (s[2] + s[3]);
+// a lane-31 / lane-63 register group's row totals (4 consecutive rows from
+// i0) into X[row], or interleaved as X[2 row + j]
+__device__ __forceinline__ void put_rows4(float* X, const float v[4], int i0) {
+  *(float4*)(X + i0) = make_float4(v[0], v[1], v[2], v[3]);
+}
+__device__ __forceinline__ void put_rows4x2(float* X, const float v0[4], const float v1[4], int i0) {
+  *(float4*)(X + 2 * i0) = make_float4(v0[0], v1[0], v0[1], v1[1]);
+  *(float4*)(X + 2 * i0 + 4) = make_float4(v0[2], v1[2], v0[3], v1[3]);
 }
 
 // the backward GEMMs shared by both kernels, given dZ2 (batch-major and
@@ -577,70 +554,80 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad(const float* __restric
     lds_sync();
     SK_TP(3);
     // ---- phase 2
-    if (l2) {  // critic h2 = relu(W2 [h1; a] + b2) -> fp32 LDS (q, dz2)
+    if (l2) {  // critic h2 = relu(W2 [h1; a] + b2) -> fp32 LDS (dz2); q partial row sums
       const f32x16 acc = l2_mfma(L.H1, wf, lane);
-      const float b2 = TLc[kTB2 + u], wa0 = TLc[kTW2a + 2 * u], wa1 = TLc[kTW2a + 2 * u + 1];
+      const float b2 = TLc[kTB2 + u], wa0 = TLc[kTW2a + 2 * u], wa1 = TLc[kTW2a + 2 * u + 1], w3 = TLc[kTW3 + u];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int i0 = drow(4 * g, lane);
-        float a0[4], a1[4];
+        float a0[4], a1[4], qv[4];
         pairs4(L.A, i0, a0, a1);
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          L.H2f[(i0 + q) * kLdH2f + u] = fmaxf(acc[4 * g + q] + b2 + a0[q] * wa0 + a1[q] * wa1, 0.f);
+        for (int q = 0; q < 4; ++q) {
+          const float h = fmaxf(acc[4 * g + q] + b2 + a0[q] * wa0 + a1[q] * wa1, 0.f);
+          L.H2f[(i0 + q) * kLdH2f + u] = h;
+          qv[q] = halfsum32(h * w3);
+        }
+        if (col == 31) put_rows4(L.QP + 32 * w, qv, i0);
       }
-    } else if (BOOT) {  // target actor h2; then the target critic's layer-2 fragments for phase 3
+    } else if (BOOT) {  // target actor h2 -> mu' partial row sums; then the target critic's layer-2 fragments
       const f32x16 acc = l2_mfma(L.H1a, wf, lane);
       __builtin_amdgcn_sched_barrier(0);
       load_l2(wf, tp, w - 4, lane);
-      const float b2 = TLa[kTB2 + u];
+      const float b2 = TLa[kTB2 + u], w30 = TLa[kTW3 + u], w31 = TLa[kTW3 + kH2 + u];
 #pragma unroll
-      for (int v = 0; v < 16; ++v) L.H2a[drow(v, lane) * kLdH2f + u] = fmaxf(acc[v] + b2, 0.f);
+      for (int g = 0; g < 4; ++g) {
+        float m0[4], m1[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float h = fmaxf(acc[4 * g + q] + b2, 0.f);
+          m0[q] = halfsum32(h * w30);
+          m1[q] = halfsum32(h * w31);
+        }
+        if (col == 31) put_rows4x2(L.MP + 64 * (w - 4), m0, m1, drow(4 * g, lane));
+      }
     }
     lds_sync();
     SK_TP(4);
     // ---- phase 3
     bf16x8 wt[8];  // W2^T fragments of phase 5 (waves 4-7: after the target critic's fragments are consumed)
     if (l2 || !BOOT) load_w2t(wt, cp, w, lane);
-    if (l2) {  // q per row: 8 threads per row, 16 units each
-      const int i = tid >> 3, c = tid & 7;
-      const float4* h = (const float4*)(L.H2f + i * kLdH2f + 16 * c);
-      const float4* w3 = (const float4*)(TLc + kTW3 + 16 * c);
-      float s = 0.f;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float4 a = h[k], b = w3[k];
-        s += (a.x * b.x + a.y * b.y) + (a.z * b.z + a.w * b.w);
-      }
-      s += __shfl_xor(s, 1, 64);
-      s += __shfl_xor(s, 2, 64);
-      s += __shfl_xor(s, 4, 64);
-      if (c == 0) L.QV[i] = TLc[kTB3] + s;
-    } else if (BOOT) {  // mu'(s') for all rows, then the Q' terms relu(z2') W3' of the wave's units
+    if (!l2 && BOOT) {  // mu'(s') per row from the partials, then Q' partial row sums of the wave's units
       const f32x16 acc = l2_mfma(L.H1B, wf, lane);
       __builtin_amdgcn_sched_barrier(0);
       load_w2t(wt, cp, w, lane);
       float* aw = L.AW + 64 * w;
-      aw[2 * col + hh] = wave_mu(L.H2a, TLa, lane);
+      {  // lane (row col, output hh)
+        float sm = TLa[kTB3 + hh];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) sm += L.MP[64 * v + 2 * col + hh];
+        aw[2 * col + hh] = tanhf(sm);
+      }
       wave_lds_order();
       const float b2 = TLt[kTB2 + u], wa0 = TLt[kTW2a + 2 * u], wa1 = TLt[kTW2a + 2 * u + 1], w3 = TLt[kTW3 + u];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int i0 = drow(4 * g, lane);
-        float a0[4], a1[4];
+        float a0[4], a1[4], yq[4];
         pairs4(aw, i0, a0, a1);
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          L.QT[(i0 + q) * kLdH2f + u] = fmaxf(acc[4 * g + q] + b2 + a0[q] * wa0 + a1[q] * wa1, 0.f) * w3;
+          yq[q] = halfsum32(fmaxf(acc[4 * g + q] + b2 + a0[q] * wa0 + a1[q] * wa1, 0.f) * w3);
+        if (col == 31) put_rows4(L.YP + 32 * (w - 4), yq, i0);
       }
     }
-    lds_sync();
+    if (BOOT) lds_sync();
     SK_TP(5);
     // ---- phase 4 (waves 0-3): y and dL/dq for all rows (each wave), then dz2 = dL/dq W3 relu'(h2) of its units
     if (l2) {
-      const float yv = BOOT ? L.RB[col] + gamma * (1.f - L.DB[col]) * (TLt[kTB3] + wave_rowsum(L.QT, lane))
-                            : L.Y[col];
-      const float e = row0 + col < B ? L.QV[col] - yv : 0.f;
+      float q = TLc[kTB3], yq = TLt[kTB3];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        q += L.QP[32 * v + col];
+        if (BOOT) yq += L.YP[32 * v + col];
+      }
+      const float yv = BOOT ? L.RB[col] + gamma * (1.f - L.DB[col]) * yq : L.Y[col];
+      const float e = row0 + col < B ? q - yv : 0.f;
       float* dw = L.DW + 64 * w;
       if (hh == 0) dw[col] = grad_scale * e;
       if (w == 0 && hh == 0) {
@@ -762,11 +749,22 @@ __global__ void __launch_bounds__(kThreads) k_actor_grad(const float* __restrict
     SK_TP(3);
     // ---- phase 2
     f32x16 zc = {0};
-    if (l2) {  // actor h2 -> fp32 LDS (mu, dz2)
+    if (l2) {  // actor h2 -> fp32 LDS (dz2); mu partial row sums
       const f32x16 acc = l2_mfma(L.H1, wf, lane);
-      const float b2 = TLa[kTB2 + u];
+      const float b2 = TLa[kTB2 + u], w30 = TLa[kTW3 + u], w31 = TLa[kTW3 + kH2 + u];
 #pragma unroll
-      for (int v = 0; v < 16; ++v) L.H2f[drow(v, lane) * kLdH2f + u] = fmaxf(acc[v] + b2, 0.f);
+      for (int g = 0; g < 4; ++g) {
+        const int i0 = drow(4 * g, lane);
+        float m0[4], m1[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float h = fmaxf(acc[4 * g + q] + b2, 0.f);
+          L.H2f[(i0 + q) * kLdH2f + u] = h;
+          m0[q] = halfsum32(h * w30);
+          m1[q] = halfsum32(h * w31);
+        }
+        if (col == 31) put_rows4x2(L.MP + 64 * w, m0, m1, i0);
+      }
     } else {
       zc = l2_mfma(L.H1B, wf, lane);
     }
@@ -775,9 +773,15 @@ __global__ void __launch_bounds__(kThreads) k_actor_grad(const float* __restrict
     load_w2t(wt, ap, w, lane);
     lds_sync();
     SK_TP(4);
-    // ---- phase 3: mu(s) = tanh(W3 h2 + b3), lane (row col, output hh), every wave
-    const float a = wave_mu(L.H2f, TLa, lane);
-    if (!l2) {  // the critic at (s, mu(s)): dQ/dz2 = W3 relu'(z2) (rows beyond B: 0), Q terms relu(z2) W3
+    // ---- phase 3: mu(s) = tanh(W3 h2 + b3) from the partials, lane (row col, output hh), every wave
+    float a;
+    {
+      float sm = TLa[kTB3 + hh];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) sm += L.MP[64 * v + 2 * col + hh];
+      a = tanhf(sm);
+    }
+    if (!l2) {  // the critic at (s, mu(s)): partial row sums of dQ/da = W3 relu'(z2) W2a (rows beyond B: 0) and Q
       float* aw = L.AW + 64 * w;
       aw[2 * col + hh] = a;
       wave_lds_order();
@@ -785,14 +789,19 @@ __global__ void __launch_bounds__(kThreads) k_actor_grad(const float* __restrict
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int i0 = drow(4 * g, lane);
-        float a0[4], a1[4];
+        float a0[4], a1[4], d0[4], d1[4], qz[4];
         pairs4(aw, i0, a0, a1);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int i = i0 + q;
           const float z = zc[4 * g + q] + b2 + a0[q] * wa0 + a1[q] * wa1;
-          L.DZC[i * kLdH2f + u] = (z > 0.f && row0 + i < B) ? w3 : 0.f;
-          if (q_out) L.QZ[i * kLdH2f + u] = fmaxf(z, 0.f) * w3;
+          const float dqdz = (z > 0.f && row0 + i0 + q < B) ? w3 : 0.f;
+          d0[q] = halfsum32(dqdz * wa0);
+          d1[q] = halfsum32(dqdz * wa1);
+          qz[q] = q_out ? halfsum32(fmaxf(z, 0.f) * w3) : 0.f;
+        }
+        if (col == 31) {
+          put_rows4x2(L.DP + 64 * (w - 4), d0, d1, i0);
+          if (q_out) put_rows4(L.QP + 32 * (w - 4), qz, i0);
         }
       }
     }
@@ -800,10 +809,21 @@ __global__ void __launch_bounds__(kThreads) k_actor_grad(const float* __restrict
     SK_TP(5);
     // ---- phase 4
     if (l2) {  // dL/dz3[row col][hh], then dz2 = (dz3 W3) relu'(h2) of its units
-      const float dz3 = -loss_scale * wave_dot_action_cols(L.DZC, TLc, lane) * (1.f - a * a);
+      float da = 0.f;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) da += L.DP[64 * v + 2 * col + hh];
+      const float dz3 = -loss_scale * da * (1.f - a * a);
       float* dw = L.DW + 64 * w;
       dw[2 * col + hh] = dz3;
-      if (w == 0) gb3 += dz3;  // db3[hh] partial of row col
+      if (w == 0) {
+        gb3 += dz3;  // db3[hh] partial of row col
+        if (q_out && hh == 0 && row0 + col < B) {
+          float sq = TLc[kTB3];
+#pragma unroll
+          for (int v = 0; v < 4; ++v) sq += L.QP[32 * v + col];
+          qsum += sq;
+        }
+      }
       wave_lds_order();
       const float w30 = TLa[kTW3 + u], w31 = TLa[kTW3 + kH2 + u];
 #pragma unroll
@@ -822,9 +842,6 @@ __global__ void __launch_bounds__(kThreads) k_actor_grad(const float* __restrict
         }
         store_t4(L.DZ2T, kLdT, u, i0, d[0], d[1], d[2], d[3]);
       }
-    } else if (w == 4 && q_out) {
-      const float s = wave_rowsum(L.QZ, lane);
-      if (hh == 0 && row0 + col < B) qsum += TLc[kTB3] + s;
     }
     lds_sync();
     SK_TP(6);
@@ -847,7 +864,7 @@ __global__ void __launch_bounds__(kThreads) k_actor_grad(const float* __restrict
     P[kAPW3 + kH2 + u] = gw31;
   }
   if (w == 0) atomicAdd(&L.RED[hh], gb3);  // db3[hh]: wave 0, lane (row, hh)
-  if (w == 4 && hh == 0 && q_out) atomicAdd(&L.RED[2], qsum);
+  if (w == 0 && hh == 0 && q_out) atomicAdd(&L.RED[2], qsum);
   lds_sync();
   if (threadIdx.x < 2) P[kAPB3 + threadIdx.x] = L.RED[threadIdx.x];
   if (threadIdx.x == 0 && q_out) atomicAdd(q_out, L.RED[2]);
