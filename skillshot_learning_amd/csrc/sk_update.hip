@@ -424,22 +424,31 @@ __device__ __forceinline__ void backward_12(const Lds& L, const bf16x8 wt[8], in
   for (int kk = 0; kk < 2; ++kk) gW1 = mfma(lfrag(L.DZ1T, kLdT, 32 * w, 16 * kk, lane), lfrag(L.ST, kLdT, 0, 16 * kk, lane), gW1);
 }
 
-// write the register-held gradients of W1 / W2 (main 256 columns, the
-// partial layout's 256-float rows: kPartW2) / b1; 32 lanes of a register write
-// 128 contiguous bytes
+// write a sub-tile's W1 / W2 gradients (W2: main 256 columns, the partial
+// layout's 256-float rows) into the workgroup's partial row, or add them to it
+// (later sub-tiles: each lane re-reads only what it wrote).  Storing per
+// sub-tile keeps the 80 accumulator registers out of phases 0-4.  32 lanes of
+// a register write 128 contiguous bytes.
 __device__ __forceinline__ void store_w12(float* P, int w, int lane, const f32x16 gW2[4], const f32x16& gW1,
-                                          float gb1) {
+                                          bool add) {
   const int mt = w & 3, nt0 = 4 * (w >> 2);
 #pragma unroll
   for (int t = 0; t < 4; ++t)
 #pragma unroll
-    for (int v = 0; v < 16; ++v)
-      P[kPW2 + (32 * mt + drow(v, lane)) * kH1 + 32 * (nt0 + t) + (lane & 31)] = gW2[t][v];
+    for (int v = 0; v < 16; ++v) {
+      float* d = P + kPW2 + (32 * mt + drow(v, lane)) * kH1 + 32 * (nt0 + t) + (lane & 31);
+      *d = add ? *d + gW2[t][v] : gW2[t][v];
+    }
   const int k = lane & 31;
   if (k < kIn) {
 #pragma unroll
-    for (int v = 0; v < 16; ++v) P[kPW1 + (32 * w + drow(v, lane)) * kIn + k] = gW1[v];
+    for (int v = 0; v < 16; ++v) {
+      float* d = P + kPW1 + (32 * w + drow(v, lane)) * kIn + k;
+      *d = add ? *d + gW1[v] : gW1[v];
+    }
   }
+}
+__device__ __forceinline__ void store_b1(float* P, int w, int lane, float gb1) {
   const float b = gb1 + __shfl_xor(gb1, 32, 64);
   if (lane < 32) P[kPB1 + 32 * w + lane] = b;
 }
@@ -481,9 +490,7 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad(const float* __restric
   const float* TLc = L.TL;
   const float* TLa = L.TL + 1024;
   const float* TLt = L.TL + 2048;
-  f32x16 gW2[4], gW1 = {0};
-#pragma unroll
-  for (int k = 0; k < 4; ++k) gW2[k] = f32x16{0};
+  float* P = partial + (int64_t)blockIdx.x * kCP;
   float gb1 = 0.f, gb2 = 0.f, gw2a0 = 0.f, gw2a1 = 0.f, gw3 = 0.f, gb3 = 0.f, lsum = 0.f;
   if (threadIdx.x < 4) L.RED[threadIdx.x] = 0.f;
   SK_TP(1);
@@ -659,14 +666,19 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad(const float* __restric
     lds_sync();
     SK_TP(6);
     // ---- phases 5, 6
-    backward_12<true>(L, wt, w, lane, gW2, gW1, gb1);
+    {
+      f32x16 gW2[4], gW1 = {0};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) gW2[k] = f32x16{0};
+      backward_12<true>(L, wt, w, lane, gW2, gW1, gb1);
+      store_w12(P, w, lane, gW2, gW1, sub > 0);
+    }
     lds_sync();  // the next sub-tile restages
     SK_TP(7);
   }
   const int lane = lane0, hh = lane >> 5;
   const int u = 32 * (w & 3) + (lane & 31);
-  float* P = partial + (int64_t)blockIdx.x * kCP;
-  store_w12(P, w, lane, gW2, gW1, gb1);
+  store_b1(P, w, lane, gb1);
   SK_TP(8);
   gb2 += __shfl_xor(gb2, 32, 64);
   gw2a0 += __shfl_xor(gw2a0, 32, 64);
@@ -716,6 +728,9 @@ __global__ void __launch_bounds__(kThreads) k_actor_grad(const float* __restrict
   for (int t = threadIdx.x; t < 32 * kLdT; t += kThreads) L.ST[t] = 0;
   const float* TLa = L.TL;
   const float* TLc = L.TL + 1024;
+  float* P = partial + (int64_t)blockIdx.x * kAP;
+  // the actor kernel has the registers to keep its weight-gradient
+  // accumulators across sub-tiles (the critic stores per sub-tile)
   f32x16 gW2[4], gW1 = {0};
 #pragma unroll
   for (int k = 0; k < 4; ++k) gW2[k] = f32x16{0};
@@ -852,8 +867,8 @@ __global__ void __launch_bounds__(kThreads) k_actor_grad(const float* __restrict
   }
   const int lane = lane0, hh = lane >> 5;
   const int u = 32 * (w & 3) + (lane & 31);
-  float* P = partial + (int64_t)blockIdx.x * kAP;
-  store_w12(P, w, lane, gW2, gW1, gb1);
+  store_w12(P, w, lane, gW2, gW1, false);
+  store_b1(P, w, lane, gb1);
   SK_TP(8);
   gb2 += __shfl_xor(gb2, 32, 64);
   gw30 += __shfl_xor(gw30, 32, 64);
