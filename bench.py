@@ -100,6 +100,15 @@ class TickGraphs:
                 for t in range(n):
                     self.launch(t)
             _upload(g, self.stream)
+            # launch the new executable once, untimed (setup, like the eager
+            # launches that load the code objects): its first launch costs
+            # ~0.4 us more GPU time per node than later ones, which the
+            # driver's 20-step timed region would otherwise count
+            # (tools/short_run_warm.py, profiles/r02_short_run_warm.jsonl:
+            # 5.2-5.3 -> 4.8 us per step on the HIP events at K = 20)
+            if not _launch_direct(g, self.stream):
+                with torch.cuda.stream(self.stream):
+                    g.replay()
             self.stream.synchronize()
             self.graphs[n] = g
         return g

@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define SK_ABI_VERSION 2
+#define SK_ABI_VERSION 3
 
 enum {
   SK_OK = 0,
@@ -88,9 +88,10 @@ typedef struct sk_state_view {
 typedef struct sk_env sk_env;
 
 /* Episode counters accumulated on device by the step kernels (wavefront
- * ballot + popcount, one atomic per wave and counter).  On device they are
- * spread over SK_COUNTER_SLOTS slots (no hot line); the totals are the sums
- * (sk_env_read_counters returns the sums). */
+ * ballot + popcount).  On device every step-kernel wave owns one 128-B line of
+ * slots (read at kernel entry, written once by the wave: no atomics), so there
+ * are sk_env_counter_slots (>= SK_COUNTER_SLOTS) slots; the totals are their
+ * sums (sk_env_read_counters returns the sums). */
 #define SK_COUNTER_SLOTS 256
 typedef struct sk_counters {
   uint64_t dones;          /* episodes finished (hit or tick limit) */
@@ -116,9 +117,11 @@ int sk_env_attach(sk_env** out, const sk_state_view* view, int64_t env_offset, u
                   int32_t device, const sk_config* cfg);
 int sk_env_destroy(sk_env* env);
 int sk_env_get_view(const sk_env* env, sk_state_view* out);
-/* Device counter slots (SK_COUNTER_SLOTS x sk_counters, device memory) the
- * step kernels accumulate into. */
+/* Device counter slots (sk_env_counter_slots x sk_counters, device memory)
+ * the step kernels accumulate into. */
 int sk_env_counters_ptr(const sk_env* env, sk_counters** out);
+/* Number of counter slots at sk_env_counters_ptr (1 for the CPU backend). */
+int sk_env_counter_slots(const sk_env* env, int64_t* out);
 /* Copy the episode counters to host memory (synchronises `stream`), and
  * zero them (stream-ordered). */
 int sk_env_read_counters(sk_env* env, sk_counters* host_out, void* stream);

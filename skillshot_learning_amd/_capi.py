@@ -16,12 +16,12 @@ from . import build as _build
 
 SK_OK, SK_EINVAL, SK_EHIP, SK_ENOMEM, SK_ENODEV = 0, -1, -2, -3, -4
 SK_REWARD_LOOKING, SK_REWARD_SIMPLE = 0, 1
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # every symbol include/skillshot.h declares
 EXPORTS = (
     "sk_last_error", "sk_abi_version", "sk_config_default", "sk_env_create", "sk_env_attach",
-    "sk_env_destroy", "sk_env_get_view", "sk_env_counters_ptr", "sk_env_read_counters",
+    "sk_env_destroy", "sk_env_get_view", "sk_env_counters_ptr", "sk_env_counter_slots", "sk_env_read_counters",
     "sk_env_clear_counters", "sk_env_get_step_counter",
     "sk_env_set_step_counter", "sk_env_sync_step_counter", "sk_env_reset", "sk_player_move_direction", "sk_player_move_look",
     "sk_player_move_discrete", "sk_player_shoot", "sk_projectile_move", "sk_game_check_collision", "sk_game_tick", "sk_env_features", "sk_env_observe",
@@ -93,6 +93,7 @@ def load(build_if_missing=True):
         "sk_env_destroy": ([P], ctypes.c_int),
         "sk_env_get_view": ([P, ctypes.POINTER(SkStateView)], ctypes.c_int),
         "sk_env_counters_ptr": ([P, PP], ctypes.c_int),
+        "sk_env_counter_slots": ([P, ctypes.POINTER(ctypes.c_int64)], ctypes.c_int),
         "sk_env_read_counters": ([P, ctypes.POINTER(SkCounters), P], ctypes.c_int),
         "sk_env_clear_counters": ([P, P], ctypes.c_int),
         "sk_env_get_step_counter": ([P, ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),

@@ -199,12 +199,24 @@ __device__ __forceinline__ void store_env_q(const View& v, int64_t i, const Env&
                ((unsigned)(e.live & 0xff) << 16) | ((unsigned)(e.winner & 0xff) << 24);
   const bool qrot_changed = (int)(__double_as_longlong(e.qrot[0]) != __double_as_longlong(q_old0)) |
                             (int)(__double_as_longlong(e.qrot[1]) != __double_as_longlong(q_old1));
+#ifdef SK_STATE_NT
+  typedef int v4i __attribute__((ext_vector_type(4)));
+  typedef double v2d __attribute__((ext_vector_type(2)));
+  typedef int v2i __attribute__((ext_vector_type(2)));
+  __builtin_nontemporal_store((v4i){e.px[0], e.py[0], e.px[1], e.py[1]}, (v4i*)(v.pos + i));
+  __builtin_nontemporal_store((v2d){e.rot[0], e.rot[1]}, (v2d*)(v.rot + i));
+  __builtin_nontemporal_store((v4i){e.qx[0], e.qy[0], e.qx[1], e.qy[1]}, (v4i*)(v.qpos + i));
+  if (qrot_changed) __builtin_nontemporal_store((v2d){e.qrot[0], e.qrot[1]}, (v2d*)(v.qrot + i));
+  __builtin_nontemporal_store((v4i){e.qcd[0], e.qage[0], e.qcd[1], e.qage[1]}, (v4i*)(v.qcdage + i));
+  __builtin_nontemporal_store((v2i){e.ticks, (int)f}, (v2i*)(v.misc + i));
+#else
   v.pos[i] = make_int4(e.px[0], e.py[0], e.px[1], e.py[1]);
   v.rot[i] = make_double2(e.rot[0], e.rot[1]);
   v.qpos[i] = make_int4(e.qx[0], e.qy[0], e.qx[1], e.qy[1]);
   if (qrot_changed) v.qrot[i] = make_double2(e.qrot[0], e.qrot[1]);
   v.qcdage[i] = make_int4(e.qcd[0], e.qage[0], e.qcd[1], e.qage[1]);
   v.misc[i] = make_int2(e.ticks, (int)f);
+#endif
 }
 
 // ---------------------------------------------------------------- Philox4x32-10

@@ -10,7 +10,8 @@
 //   k_gen_actions     random-policy actions into HBM (K4)
 //   k_reset / k_move_* / k_shoot / k_game_tick / k_observe / k_features:
 //                     the reference's per-method API, batched
-// Episode counters use a wavefront ballot + popcount and one atomic per wave.
+// Episode counters: wavefront ballots + popcount into one 128-B slot line per
+// wave, read-modify-written without atomics (see "counters" below).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -18,6 +19,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "sk_device.hpp"
 #include "sk_host.hpp"
@@ -35,7 +37,7 @@ struct sk_env {
   sk_state_view hview;
   bool owned;
   char* d_aux;               // [step slots: 256 B][counter slots]
-  sk_counters* d_counters;   // SK_COUNTER_SLOTS slots
+  sk_counters* d_counters;   // counter_slots(n) slots: one per step-kernel wave
   // RNG step counter, device-resident so every call is hipGraph-capturable:
   // two slots ping-pong; a kernel reads slots[parity] and block 0 writes
   // slots[1-parity] = value + advance, then the host flips parity.
@@ -75,37 +77,94 @@ static constexpr int kBlock = 256;
 static constexpr int kStepBlock = SK_STEP_BLOCK;
 static constexpr int64_t kFastStepMinEnvs = 196608;
 static constexpr int64_t kFastStepMaxEnvs = 786432;
-static constexpr size_t kAuxBytes = 256 + SK_COUNTER_SLOTS * sizeof(sk_counters);
+// Counter slots per wave: 4 x 32 B = one 128-B line, so no two waves (on
+// different XCDs, whose L2s write partial lines back at the end of the
+// dispatch) share a line: 0.27 us less per 65,536-game k_step than packed
+// 32-B slots (profiles/r02_step_ablation.jsonl).  Only the first slot of a
+// wave's line is written; the host sums them all.
+#ifndef SK_CTR_STRIDE
+#define SK_CTR_STRIDE 4
+#endif
+// SK_CTR_STRIDE slots per wave of the widest step grid (k_step_split: two
+// lanes per game), at least SK_COUNTER_SLOTS
+static inline int64_t counter_slots(int64_t n) {
+  const int64_t waves = (2 * n + 63) / 64;
+  return waves * SK_CTR_STRIDE > SK_COUNTER_SLOTS ? waves * SK_CTR_STRIDE : SK_COUNTER_SLOTS;
+}
+static inline size_t aux_bytes(int64_t n) { return 256 + (size_t)counter_slots(n) * sizeof(sk_counters); }
 
 static inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 static inline unsigned step_grid(int64_t n) { return (unsigned)((n + kStepBlock - 1) / kStepBlock); }
 
 // ------------------------------------------------------------------ counters
-// Episode counters live in SK_COUNTER_SLOTS slots of 32 B; the host sums
-// them.  Each wave ballots its done / hit-by-id lanes and sums final ticks
-// across lanes, then lane 0 adds into the slot picked by its global wave
-// index: no single hot line (a one-line counter serialises every wave's
-// atomics at the memory side and stalled 1M-env launches).
+// Episode counters: one slot line per wave of the launch (global wave index),
+// so no two waves of a launch share a slot and no atomics are needed.  A wave
+// loads its slot at entry (ctr_load, under the state loads' latency), ballots
+// its done / hit-by-id lanes, sums their final ticks, and lane 0 stores
+// slot + counts with one vector store after the state stores.  Launches on a
+// stream are ordered, so the read-modify-write is race-free; the host sums
+// the slots.  Round 1 added per-wave device atomics into 256 shared slots and
+// summed the ticks with a 64-bit shuffle tree; counting then cost 0.42 of a
+// 4.62 us 65,536-game k_step, now 0.04 us (profiles/r02_step_ablation.jsonl).
 __device__ __forceinline__ sk_counters* ctr_slot(sk_counters* base) {
-  unsigned wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  return base + (wave & (SK_COUNTER_SLOTS - 1));
+  // every kernel that counts launches kStepBlock-lane workgroups (a constant,
+  // not blockDim, whose dispatch-packet load would land on the wave's tail)
+  const unsigned wave = blockIdx.x * (kStepBlock >> 6) + (threadIdx.x >> 6);
+  return base + (size_t)wave * SK_CTR_STRIDE;
 }
 
-__device__ __forceinline__ void wave_count(sk_counters* ctr, bool done, int winner, int ticks) {
-  uint64_t m_done = __ballot(done);
-  if (m_done == 0) return;  // wave-uniform
-  uint64_t m_w1 = __ballot(done && winner == 1);
-  uint64_t m_w2 = __ballot(done && winner == 2);
-  uint64_t t = done ? (uint64_t)ticks : 0;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
-  if ((threadIdx.x & 63) == 0) {
-    sk_counters* c = ctr_slot(ctr);
-    atomicAdd((unsigned long long*)&c->dones, (unsigned long long)__popcll(m_done));
-    if (m_w1) atomicAdd((unsigned long long*)&c->hits_p1, (unsigned long long)__popcll(m_w1));
-    if (m_w2) atomicAdd((unsigned long long*)&c->hits_p2, (unsigned long long)__popcll(m_w2));
-    atomicAdd((unsigned long long*)&c->ticks_sum, (unsigned long long)t);
-  }
+struct WaveCtr {
+  ulonglong4 v;
+};
+
+__device__ __forceinline__ WaveCtr ctr_load(sk_counters* base) {
+  WaveCtr w;
+#ifdef SK_CTR_NOMEM  // timing ablation: counting without its memory traffic
+  w.v = make_ulonglong4(0, 0, 0, 0);
+#else
+  w.v = base ? *reinterpret_cast<const ulonglong4*>(ctr_slot(base)) : make_ulonglong4(0, 0, 0, 0);
+#endif
+  return w;
+}
+
+// Called once the wave's loads have all been consumed (the tick is done): an
+// empty asm that redefines the slot values, so the final counter store does
+// not depend on a load the waitcnt pass still sees pending.  Without it the
+// pass (its tracking lost across the tick's branches) put an s_waitcnt
+// vmcnt(0) before that store, i.e. made every wave wait for its own state
+// stores to be acknowledged before issuing one more: +0.5 us per 65,536-game
+// k_step (profiles/r02_step_ablation.jsonl).
+__device__ __forceinline__ void ctr_settle(WaveCtr& w) {
+  asm volatile("" : "+v"(w.v.x), "+v"(w.v.y), "+v"(w.v.z), "+v"(w.v.w));
+}
+
+__device__ __forceinline__ void ctr_store(sk_counters* base, const WaveCtr& w, uint64_t dones, uint64_t h1,
+                                          uint64_t h2, uint64_t tsum) {
+#ifdef SK_CTR_NOMEM
+  asm volatile("" ::"s"(dones + h1 + h2 + tsum));
+  return;
+#endif
+  if ((threadIdx.x & 63) == 0)
+    *reinterpret_cast<ulonglong4*>(ctr_slot(base)) =
+        make_ulonglong4(w.v.x + dones, w.v.y + h1, w.v.z + h2, w.v.w + tsum);
+}
+
+// The store is unconditional (32 B per wave per launch), so the slot's load
+// has a use on every path and stays at kernel entry instead of being sunk
+// into the rare done branch.  The finished games' ticks are summed by a
+// wave-uniform scalar loop of readlanes over the done lanes (almost always
+// one), not a 6-step 64-bit shuffle tree: a wave with a finished game is the
+// tick's slowest (it also draws the random restart), and the kernel ends with
+// it.  Callers count after their state stores, so this overlaps the stores'
+// drain.
+__device__ __forceinline__ void wave_count(sk_counters* ctr, const WaveCtr& w, bool done, int winner, int ticks) {
+  const uint64_t m_done = __ballot(done);
+  const uint64_t m_w1 = __ballot(done && winner == 1);
+  const uint64_t m_w2 = __ballot(done && winner == 2);
+  uint64_t t = 0;
+  for (uint64_t m = m_done; m; m &= m - 1)  // wave-uniform
+    t += (uint32_t)__builtin_amdgcn_readlane(ticks, (int)__builtin_ctzll(m));
+  ctr_store(ctr, w, __popcll(m_done), __popcll(m_w1), __popcll(m_w2), t);
 }
 
 __device__ __forceinline__ void store_obs(float* obs, int64_t n, int p, int64_t i, const float o[12]) {
@@ -190,6 +249,7 @@ struct StepArgs {
 __global__ void __launch_bounds__(kStepBlock) k_step(StepArgs a, Cfg c) {
   int64_t i = (int64_t)blockIdx.x * kStepBlock + threadIdx.x;
   SK_TS(ts0);
+  WaveCtr wc = ctr_load(a.ctr);
   const uint64_t step = step_read(a.step);
   step_advance(a.step, step, 1);
   bool in = i < a.n;
@@ -224,6 +284,9 @@ __global__ void __launch_bounds__(kStepBlock) k_step(StepArgs a, Cfg c) {
     ts2 = __builtin_amdgcn_s_memrealtime();
     __builtin_amdgcn_sched_barrier(0);
 #endif
+  }
+  ctr_settle(wc);  // every load consumed, no state store issued yet
+  if (in) {
     if (a.obs || a.reward) {
       float o0[12], o1[12];
       double pd0, pd1;
@@ -247,13 +310,13 @@ __global__ void __launch_bounds__(kStepBlock) k_step(StepArgs a, Cfg c) {
     if (a.winner) a.winner[i] = (uint8_t)e.winner;
 #endif
   }
-  if (a.ctr) wave_count(a.ctr, d, in ? e.winner : 0, in ? e.ticks : 0);
-  if (!in) return;
-  if (d && a.auto_reset) {
+  const int fin_winner = in ? e.winner : 0, fin_ticks = in ? e.ticks : 0;  // before the restart
+  (void)fin_winner; (void)fin_ticks; (void)wc;  // unused in the -DSK_ABL_NOCTR timing build
+  if (in && d && a.auto_reset) {
     if (a.random_positions) reset_random(c, e, a.seed, (uint64_t)(a.env_offset + i), step);
     else reset_fixed(c, e);
   }
-  if (a.obs_reset) {
+  if (in && a.obs_reset) {
     float o0[12], o1[12];
     double pd0, pd1;
     const unsigned amb = obs_env(c, e, o0, o1, &pd0, &pd1);
@@ -261,7 +324,11 @@ __global__ void __launch_bounds__(kStepBlock) k_step(StepArgs a, Cfg c) {
     store_obs(a.obs_reset, a.n, 1, i, o1);
     if (amb) fix_future_flags(c, e, amb, a.obs_reset, a.n, i);
   }
-  store_env_q(a.v, i, e, q_old0, q_old1);
+  if (in) store_env_q(a.v, i, e, q_old0, q_old1);
+#ifndef SK_ABL_NOCTR  // timing ablation only
+  if (a.ctr) wave_count(a.ctr, wc, d, fin_winner, fin_ticks);
+#endif
+  if (!in) return;
 #ifdef SK_TRACE_STEP
   __builtin_amdgcn_s_waitcnt(0);
   const unsigned long long ts3 = __builtin_amdgcn_s_memrealtime();
@@ -300,6 +367,7 @@ __global__ void __launch_bounds__(kStepBlock) k_step_fast(StepArgs a, Cfg c) {
   // theirs, rest of the state -> decode, actions -> the tick)
   StepLoads L;
   if (in) issue_step_loads(a.v, a.actions, a.n, i, L);
+  WaveCtr wc = ctr_load(a.ctr);
   bool d = false;
   Env e;
   if (in) {
@@ -314,6 +382,9 @@ __global__ void __launch_bounds__(kStepBlock) k_step_fast(StepArgs a, Cfg c) {
     decode_env(step_loads_env(L), e);
     wait_actions(L);
     tick_env_fast(c, e, m0, m1, tq0, tq1, k0 & k1, k2, k3, L.a0.x, L.a0.y, L.a1.x, L.a1.y);
+  }
+  ctr_settle(wc);  // every load consumed, no state store issued yet
+  if (in) {
     if (a.obs || a.reward) {
       float o0[12], o1[12];
       double pd0, pd1;
@@ -337,8 +408,8 @@ __global__ void __launch_bounds__(kStepBlock) k_step_fast(StepArgs a, Cfg c) {
     if (a.winner) a.winner[i] = (uint8_t)e.winner;
 #endif
   }
-  if (a.ctr) wave_count(a.ctr, d, in ? e.winner : 0, in ? e.ticks : 0);
   if (!in) return;
+  const int fin_winner = e.winner, fin_ticks = e.ticks;  // before the restart
   // the RNG step slot is read only by the waves that need it (all lanes
   // reading one line every launch made that line's L2 channel a hot spot)
   if (blockIdx.x == 0 && threadIdx.x == 0) step_advance(a.step, step_read(a.step), 1);
@@ -355,6 +426,7 @@ __global__ void __launch_bounds__(kStepBlock) k_step_fast(StepArgs a, Cfg c) {
     if (amb) fix_future_flags(c, e, amb, a.obs_reset, a.n, i);
   }
   store_env_q(a.v, i, e, L.qr.x, L.qr.y);
+  if (a.ctr) wave_count(a.ctr, wc, d, fin_winner, fin_ticks);  // after the stores (see wave_count)
 }
 
 // Player-split fused step: lanes (2i, 2i+1) own players 1 and 2 of env i.
@@ -372,6 +444,7 @@ __global__ void __launch_bounds__(kStepBlock) k_step_split(StepArgs a, Cfg c) {
   step_advance(a.step, step, 1);
   const bool in = i < a.n;
   const int64_t h = 2 * i + p;  // this lane's half-plane index
+  WaveCtr wc = ctr_load(a.ctr);
   int px = 0, py = 0, qx = 0, qy = 0, qcd = 0, qage = 0, ticks = 0, flags = 0;
   double rot = 0.0, qrot = 0.0;
   float2 act = make_float2(0.f, 0.f);
@@ -413,6 +486,7 @@ __global__ void __launch_bounds__(kStepBlock) k_step_split(StepArgs a, Cfg c) {
     if (p == 0) collide_s(c, px, py, qx, qy, qvalid, opx, opy, oqx, oqy, oqv, live, winner);
     else collide_s(c, opx, opy, oqx, oqy, oqv, px, py, qx, qy, qvalid, live, winner);
   }
+  ctr_settle(wc);  // every load consumed, no state store issued yet
   const bool d = in && ((!live) || (ticks >= a.tick_limit));  // SkillshotLearner.py:302
   if (in && (a.obs || a.reward)) {
     float o[12];
@@ -440,8 +514,8 @@ __global__ void __launch_bounds__(kStepBlock) k_step_split(StepArgs a, Cfg c) {
     if (a.done) a.done[i] = (uint8_t)d;
     if (a.winner) a.winner[i] = (uint8_t)winner;
   }
-  if (a.ctr) wave_count(a.ctr, d && p == 0, winner, ticks);
   if (!in) return;
+  const int fin_winner = winner, fin_ticks = ticks;  // before the restart
   if (d && a.auto_reset) {  // SkillshotGame.__init__ :10-25 for this lane's player
     if (a.random_positions) {
       U4 u = draw4(a.seed, (uint64_t)(a.env_offset + i), step, 1u);
@@ -475,6 +549,7 @@ __global__ void __launch_bounds__(kStepBlock) k_step_split(StepArgs a, Cfg c) {
                  ((unsigned)(winner & 0xff) << 24);
     a.v.misc[i] = make_int2(ticks, (int)f);
   }
+  if (a.ctr) wave_count(a.ctr, wc, d && p == 0, fin_winner, fin_ticks);  // after the stores (see wave_count)
 }
 
 struct RolloutArgs {
@@ -493,11 +568,13 @@ __global__ void __launch_bounds__(kStepBlock) k_rollout_random(RolloutArgs a, Cf
   bool in = i < a.n;
   const uint64_t step0 = step_read(a.step);
   step_advance(a.step, step0, (uint64_t)a.n_ticks);
+  WaveCtr wc = ctr_load(a.ctr);
   Env e;
   if (in) load_env(a.v, i, e);
   uint64_t genv = (uint64_t)(a.env_offset + i);
   unsigned dones = 0, w1 = 0, w2 = 0;
   uint64_t tsum = 0;
+  ctr_settle(wc);  // with the state loads, before any store
   if (in) {
     for (int t = 0; t < a.n_ticks; ++t) {
       uint64_t step = step0 + (uint64_t)t;
@@ -522,11 +599,7 @@ __global__ void __launch_bounds__(kStepBlock) k_rollout_random(RolloutArgs a, Cf
       for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
       vals[k] = x;
     }
-    if ((threadIdx.x & 63) == 0 && vals[0]) {
-      unsigned long long* base = (unsigned long long*)ctr_slot(a.ctr);
-      for (int k = 0; k < 4; ++k)
-        if (vals[k]) atomicAdd(base + k, (unsigned long long)vals[k]);
-    }
+    if (vals[0]) ctr_store(a.ctr, wc, vals[0], vals[1], vals[2], vals[3]);
   }
 }
 
@@ -806,12 +879,12 @@ static int make_env(sk_env** out, const sk_state_view* view, int32_t n, int64_t 
     delete e;
     return fail(SK_EINVAL, "misc plane must be 8-byte aligned");
   }
-  if (hipMalloc(&e->d_aux, kAuxBytes) != hipSuccess) {
+  if (hipMalloc(&e->d_aux, aux_bytes(n)) != hipSuccess) {
     if (e->owned) (void)hipFree(e->hview.pos);
     delete e;
     return fail(SK_ENOMEM, "hipMalloc counters");
   }
-  HIP_TRY(hipMemset(e->d_aux, 0, kAuxBytes));
+  HIP_TRY(hipMemset(e->d_aux, 0, aux_bytes(n)));
   e->d_step = reinterpret_cast<uint64_t*>(e->d_aux);
   e->d_counters = reinterpret_cast<sk_counters*>(e->d_aux + 256);
   if (e->owned) {
@@ -868,17 +941,25 @@ int sk_env_counters_ptr(const sk_env* e, sk_counters** out) {
   return SK_OK;
 }
 
+int sk_env_counter_slots(const sk_env* e, int64_t* out) {
+  if (!e || !out) return fail(SK_EINVAL, "NULL argument");
+  *out = e->host ? 1 : counter_slots(e->n);
+  return SK_OK;
+}
+
 int sk_env_read_counters(sk_env* e, sk_counters* out, void* stream) {
   if (!e || !out) return fail(SK_EINVAL, "NULL argument");
   if (e->host) {
     *out = e->host->ctr;
     return SK_OK;
   }
-  sk_counters slots[SK_COUNTER_SLOTS];
-  HIP_TRY(hipMemcpyAsync(slots, e->d_counters, sizeof(slots), hipMemcpyDeviceToHost, (hipStream_t)stream));
+  const int64_t ns = counter_slots(e->n);
+  std::vector<sk_counters> slots((size_t)ns);
+  HIP_TRY(hipMemcpyAsync(slots.data(), e->d_counters, (size_t)ns * sizeof(sk_counters), hipMemcpyDeviceToHost,
+                         (hipStream_t)stream));
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
   sk_counters sum = {0, 0, 0, 0};
-  for (int k = 0; k < SK_COUNTER_SLOTS; ++k) {
+  for (int64_t k = 0; k < ns; ++k) {
     sum.dones += slots[k].dones;
     sum.hits_p1 += slots[k].hits_p1;
     sum.hits_p2 += slots[k].hits_p2;
@@ -894,7 +975,8 @@ int sk_env_clear_counters(sk_env* e, void* stream) {
     e->host->ctr = sk_counters{0, 0, 0, 0};
     return SK_OK;
   }
-  HIP_TRY(hipMemsetAsync(e->d_counters, 0, SK_COUNTER_SLOTS * sizeof(sk_counters), (hipStream_t)stream));
+  HIP_TRY(hipMemsetAsync(e->d_counters, 0, (size_t)counter_slots(e->n) * sizeof(sk_counters),
+                         (hipStream_t)stream));
   return SK_OK;
 }
 

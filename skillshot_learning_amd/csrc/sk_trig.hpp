@@ -11,10 +11,12 @@
 // Algorithm: Cody-Waite reduction by pi/2 split in four parts (the fdlibm /
 // musl constants, public domain), every rounding error carried so the
 // reduction is branch-free, then musl's degree-13/14 minimax kernels on
-// [-pi/4, pi/4] with the reduced argument's tail.  Measured against glibc: |error| <= 1 ulp, exact
-// at +-0 (sin = +-0, cos = 1) — the only argument where the game's
-// int(round(x - sin(r)*3*s)) has exact ties.  Compile with -ffp-contract=off:
-// the reduction relies on separately rounded products.
+// [-pi/4, pi/4] with the reduced argument's tail, their polynomials evaluated
+// with explicit fmas (0.1 us less per 65,536-game k_step than separate
+// products, profiles/r02_step_ablation.jsonl).  Measured against glibc:
+// |error| <= 1 ulp, exact at +-0 (sin = +-0, cos = 1) — the only argument
+// where the game's int(round(x - sin(r)*3*s)) has exact ties.  Compile with
+// -ffp-contract=off: the reduction relies on separately rounded products.
 #pragma once
 #include <math.h>
 #include <stdint.h>
@@ -38,9 +40,15 @@ SKT_HD double ksin(double x, double y) {
                S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
   double z = x * x;
   double w = z * z;
+#ifndef SK_TRIG_NOFMA  // explicit fmas in the polynomial (A/B: -DSK_TRIG_NOFMA)
+  double r = fma(z * w, fma(z, S6, S5), fma(z, fma(z, S4, S3), S2));
+  double v = z * x;
+  return x - (fma(z, fma(-v, r, 0.5 * y), -y) - v * S1);
+#else
   double r = S2 + z * (S3 + z * S4) + z * w * (S5 + z * S6);
   double v = z * x;
   return x - ((z * (0.5 * y - v * r) - y) - v * S1);
+#endif
 }
 
 // musl __cos(x, y): cos(x + y) for |x| <= pi/4
@@ -50,15 +58,26 @@ SKT_HD double kcos(double x, double y) {
                C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
   double z = x * x;
   double w = z * z;
+#ifndef SK_TRIG_NOFMA
+  double r = fma(z, fma(z, fma(z, C3, C2), C1), w * w * fma(z, fma(z, C6, C5), C4));
+  double hz = 0.5 * z;
+  w = 1.0 - hz;
+  return w + (((1.0 - w) - hz) + fma(z, r, -x * y));
+#else
   double r = z * (C1 + z * (C2 + z * C3)) + w * w * (C4 + z * (C5 + z * C6));
   double hz = 0.5 * z;
   w = 1.0 - hz;
   return w + (((1.0 - w) - hz) + (z * r - x * y));
+#endif
 }
 
 // sin and cos of x; ok = false for |x| >= 2^20*pi/2 or non-finite x (result
 // then meaningless: recompute with the library routine)
 SKT_HD SinCos sincos_bf(double x, bool* ok) {
+#ifdef SK_ABL_NOTRIG  // timing ablation only: wrong values, same data flow
+  *ok = fabs(x) < 1647099.3291652855;
+  return SinCos{x * 0.125, 1.0 - x * 0.0625};
+#endif
   const double invpio2 = 6.36619772367581382433e-01;
   const double pio2_1 = 1.57079632673412561417e+00;  // first 33 bits of pi/2
   const double pio2_2 = 6.07710050630396597660e-11;  // next 33 bits

@@ -325,8 +325,7 @@ __device__ __forceinline__ void layer1(const short* Sx, bf16x8 wfrag, const floa
 }
 
 // layer 2: the 16 weight fragments of out n-tile nt (issued a phase ahead),
-// then the MFMA chain over the 256 hidden inputs; l2_mfma2 runs two nets'
-// chains interleaved (independent accumulators keep the MFMA pipe full)
+// then the MFMA chain over the 256 hidden inputs
 __device__ __forceinline__ void load_l2(bf16x8 wf[16], const char* pack, int nt, int lane) {
   const gfrag_t g = (gfrag_t)(pack + kGW2);
 #pragma unroll
@@ -340,17 +339,6 @@ __device__ __forceinline__ f32x16 l2_mfma(const short* H, const bf16x8 wf[16], i
     if ((kk & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // cap the hoisted LDS fragments (VGPRs)
   }
   return acc;
-}
-__device__ __forceinline__ void l2_mfma2(f32x16& a0, f32x16& a1, const short* H0, const short* H1, const bf16x8 w0[16],
-                                         const bf16x8 w1[16], int lane) {
-  a0 = f32x16{0};
-  a1 = f32x16{0};
-#pragma unroll
-  for (int kk = 0; kk < 16; ++kk) {
-    a0 = mfma(lfrag(H0, kLdH1, 0, 16 * kk, lane), w0[kk], a0);
-    a1 = mfma(lfrag(H1, kLdH1, 0, 16 * kk, lane), w1[kk], a1);
-    if ((kk & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-  }
 }
 // W2^T fragments of the dH1 n-tile w (phase 5)
 __device__ __forceinline__ void load_w2t(bf16x8 wt[8], const char* pack, int w, int lane) {

@@ -29,7 +29,12 @@ def main():
     p.add_argument("--k", type=int, default=20)
     p.add_argument("--reps", type=int, default=15)
     p.add_argument("--envs", type=int, default=65536)
+    p.add_argument("--spin", action="store_true", help="hipSetDeviceFlags(hipDeviceScheduleSpin) before the device is used")
     a = p.parse_args()
+    if a.spin:
+        hp = next(ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln)
+        rc = ctypes.CDLL(hp).hipSetDeviceFlags(ctypes.c_uint(1))
+        print(json.dumps(dict(spin_rc=rc)), flush=True)
     n, K = a.envs, a.k
     g = VecSkillshotGame(n, device="cuda:0", seed=0, random_positions=True)
     st = torch.cuda.Stream()
@@ -74,7 +79,8 @@ def main():
                 for t in range(K):
                     launch(t)
 
-    env = {k: v for k, v in os.environ.items() if k.startswith(("DEBUG_CLR", "HIP_", "GPU_"))}
+    env = {k: v for k, v in os.environ.items() if k.startswith(("DEBUG_CLR", "HIP_", "GPU_", "ROC_"))}
+    env["spin"] = a.spin
     for method in ("torch", "direct", "eager"):
         gr = torch.cuda.CUDAGraph()
         g.sync_step_counter(sp)
