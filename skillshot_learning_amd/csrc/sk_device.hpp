@@ -262,6 +262,15 @@ __device__ __forceinline__ void reset_fixed(const Cfg& c, Env& e) {  // Skillsho
   e.ticks = 0; e.live = 1; e.winner = 0;
 }
 
+// random start from a draw4(seed, genv, step, 1) the caller already made
+__device__ __forceinline__ void reset_random_u(const Cfg& c, Env& e, U4 u) {
+  reset_fixed(c, e);
+  e.px[0] = u32_to_pos(u.x, c.rlo, c.rhi);
+  e.py[0] = u32_to_pos(u.y, c.rlo, c.rhi);
+  e.px[1] = u32_to_pos(u.z, c.rlo, c.rhi);
+  e.py[1] = u32_to_pos(u.w, c.rlo, c.rhi);
+}
+
 __device__ __forceinline__ void reset_random(const Cfg& c, Env& e, uint64_t seed, uint64_t genv,
                                              uint64_t step) {
   U4 u = draw4(seed, genv, step, 1u);

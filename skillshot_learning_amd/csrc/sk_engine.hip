@@ -77,6 +77,7 @@ static constexpr int kBlock = 256;
 static constexpr int kStepBlock = SK_STEP_BLOCK;
 static constexpr int64_t kFastStepMinEnvs = 196608;
 static constexpr int64_t kFastStepMaxEnvs = 786432;
+static constexpr int64_t kEarlyDrawMinEnvs = 32768;  // k_step: restart draw under the loads
 // Counter slots per wave: 4 x 32 B = one 128-B line, so no two waves (on
 // different XCDs, whose L2s write partial lines back at the end of the
 // dispatch) share a line: 0.27 us less per 65,536-game k_step than packed
@@ -256,6 +257,7 @@ __global__ void __launch_bounds__(kStepBlock) k_step(StepArgs a, Cfg c) {
   bool d = false;
   Env e;
   double q_old0 = 0.0, q_old1 = 0.0;  // stored projectile rotations (store_env_q)
+  U4 ru = {0u, 0u, 0u, 0u};
 #ifdef SK_TRACE_STEP
   unsigned long long ts1 = 0, ts2 = 0;
 #endif
@@ -269,6 +271,18 @@ __global__ void __launch_bounds__(kStepBlock) k_step(StepArgs a, Cfg c) {
     __builtin_amdgcn_sched_barrier(0);
     const float2 a0 = load_action(a.actions + i);
     const float2 a1 = load_action(a.actions + a.n + i);
+    __builtin_amdgcn_sched_barrier(0);
+    // the random restart's Philox draw (SkillshotGame.py:15 via :168) while
+    // the state is in flight: the VALU is idle until it lands, whereas after
+    // the tick the draw would sit on the finishing waves' tail (the empty asm
+    // pins it here: it would otherwise be sunk into the restart branch).
+    // Only for large grids: 4.30 -> 4.24 us at 65,536 games, but 3.28 ->
+    // 3.34 us at 4,096, whose state lands before the draw is done
+    // (profiles/r02_step_ablation.jsonl, run ed1)
+    if (a.random_positions && a.n >= kEarlyDrawMinEnvs) {
+      ru = draw4(a.seed, (uint64_t)(a.env_offset + i), step, 1u);
+      asm volatile("" : "+v"(ru.x), "+v"(ru.y), "+v"(ru.z), "+v"(ru.w));
+    }
     __builtin_amdgcn_sched_barrier(0);
 #ifdef SK_TRACE_STEP
     __builtin_amdgcn_s_waitcnt(0);
@@ -313,7 +327,10 @@ __global__ void __launch_bounds__(kStepBlock) k_step(StepArgs a, Cfg c) {
   const int fin_winner = in ? e.winner : 0, fin_ticks = in ? e.ticks : 0;  // before the restart
   (void)fin_winner; (void)fin_ticks; (void)wc;  // unused in the -DSK_ABL_NOCTR timing build
   if (in && d && a.auto_reset) {
-    if (a.random_positions) reset_random(c, e, a.seed, (uint64_t)(a.env_offset + i), step);
+    if (a.random_positions) {
+      if (a.n >= kEarlyDrawMinEnvs) reset_random_u(c, e, ru);
+      else reset_random(c, e, a.seed, (uint64_t)(a.env_offset + i), step);
+    }
     else reset_fixed(c, e);
   }
   if (in && a.obs_reset) {
