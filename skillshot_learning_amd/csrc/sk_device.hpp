@@ -712,6 +712,59 @@ __device__ __forceinline__ unsigned obs_env(const Cfg& c, const Env& e, float o0
   return (unsigned)m0 | ((unsigned)m1 << 1);
 }
 
+// prepare_states (SkillshotLearner.py:512-543) of one player from sin/cos the
+// step already holds, with no tan, no fp64 division in the distances and no
+// fp64 sqrt (the player-split step's obs epilogue).
+//
+// * get_dist_line_point(g, l, c) (SkillshotGame.py:124-130) with
+//   g = tan(pi/2 - r) = cos r / sin r is |g*dx - dy| / sqrt(g*g + 1) =
+//   |cos r * dx - sin r * dy| (dx, dy = c - l: the numerator and the root both
+//   scale by |sin r|).  For the player, r is its post-look rotation, whose
+//   sin/cos `pr` the caller takes in fp32 (error <= SKT_FAST_ERR): the
+//   distance is then within 3e-7 * (|dx| + |dy|) < 2e-4 of the fp64 one, i.e.
+//   ~5e-7 of obs[0] (/ max_dist) and of the looking reward (/ W), far inside
+//   the 1e-5 obs bar.  For the projectile, r = qrot and `qt` is the fp64
+//   sincos the tick moved it with (its rotation after shoot, Player.py:80-84).
+// * get_dist_point_point (:132-134): sqrtf of the exact integer sum of
+//   squares (< 2^24), relative error 6e-8.
+// * check_future_collision (:96-113) needs g itself within a few ulp of
+//   math.tan(-qrot + pi/2): the argument y = fl(kPi2 - qrot) is pi/2 - (qrot +
+//   eta) with eta = (pi/2 - kPi2) + the sum's rounding error (TwoSum, exact),
+//   so tan(y) = cos(qrot + eta) / sin(qrot + eta) = (c - eta*s) / (s + eta*c)
+//   to first order (eta < 2^-52 * |qrot| + 6.2e-17; the second-order terms
+//   are below an ulp).  At qrot = 0 this is 1 / 6.123e-17 = 1.633e16 =
+//   math.tan(math.pi/2).  The flag then follows future_collision_s' margin
+//   rule (2^-40 relative >> these few ulp) and its correctly rounded redo.
+constexpr double kPi2Lo = 6.123233995736766e-17;  // pi/2 - kPi2
+
+__device__ __forceinline__ double grad_from_sincos(double qrot, sktrig::SinCos qt) {
+  const double y = -qrot + kPi2;  // TwoSum(kPi2, -qrot): kPi2 - qrot = y + err
+  const double bb = y - kPi2;
+  const double err = (kPi2 - (y - bb)) + (-qrot - bb);
+  const double eta = kPi2Lo + err;
+  return fma(-eta, qt.s, qt.c) / fma(eta, qt.c, qt.s);
+}
+
+__device__ __forceinline__ void obs12_sc(const Cfg& c, int px, int py, double rot, sktrig::SinCosF pr, int qx,
+                                         int qy, double qrot, sktrig::SinCos qt, int qcd, int qvalid, int ox, int oy,
+                                         float out[12], float* path_dist, bool* amb) {
+  const int dx = ox - px, dy = oy - py, ex = ox - qx, ey = oy - qy;
+  const float pd = fabsf(fmaf(pr.c, (float)dx, -(pr.s * (float)dy)));
+  *path_dist = pd;
+  out[0] = (float)((double)pd * c.inv_max_dist);
+  out[1] = (float)((double)sqrtf((float)(dx * dx + dy * dy)) * c.inv_max_dist);
+  out[2] = (float)((double)px * c.inv_W);
+  out[3] = (float)((double)py * c.inv_H);
+  out[4] = (float)(((py_mod2_fast(rot) * kPi) / 2.0) * kPi);  // `% 2 * np.pi) / 2 * np.pi`
+  out[5] = (float)((double)qcd * c.inv_cdmax);
+  out[6] = (float)((double)sqrtf((float)(ex * ex + ey * ey)) * c.inv_max_dist);
+  out[7] = (float)((double)qx * c.inv_W);
+  out[8] = (float)((double)qy * c.inv_H);
+  out[9] = (float)(((py_mod2_fast(qrot) * kPi) / 2.0) * kPi);
+  out[10] = (float)(fabs(fma(qt.c, (double)ex, -(qt.s * (double)ey))) * c.inv_max_dist);
+  out[11] = future_collision_s(c, qx, qy, qvalid, ox, oy, grad_from_sincos(qrot, qt), amb) ? 1.0f : 0.0f;
+}
+
 // tan(-rot + pi/2) correctly rounded (Player.py:94 / Projectile.py:58)
 __device__ __attribute__((noinline)) double grad_cr(double rot) { return sktan::tan_cr(-rot + kPi2); }
 

@@ -75,6 +75,51 @@ __global__ void __launch_bounds__(kDiagBlock) kd_copy_map(int4* pos, double2* ro
   done[i] = (uint8_t)t;
 }
 
+// kind 4 copy_full : the full-contract tick's traffic (k_step_split layout:
+//                    lanes 2i, 2i+1 own players 1, 2 of game i, 8-byte plane
+//                    halves) — state in/out, action in, obs row 48 B and
+//                    reward 4 B out per player, done per game; no game logic.
+//                    obs/reward go to `obs` = [2][n][12] f32 followed by
+//                    [2][n] f32 (one buffer the caller sizes 104 n bytes)
+__global__ void __launch_bounds__(kDiagBlock) kd_copy_full(int2* pos, double* rot, int2* qpos, double* qrot,
+                                                           int2* qcdage, int2* misc, const float2* act,
+                                                           uint8_t* done, float* obs, int64_t n) {
+  const int64_t gt = (int64_t)blockIdx.x * kDiagBlock + threadIdx.x;
+  const int64_t i = gt >> 1;
+  const int p = (int)(gt & 1);
+  if (i >= n) return;
+  const int64_t h = 2 * i + p;
+  int2 pp = pos[h], qq = qpos[h], ca = qcdage[h];
+  double r = rot[h], qr = qrot[h];
+  int2 m = misc[i];
+  float2 a = act[(int64_t)p * n + i];
+  int t = (a.x > 2.f) + (a.y > 2.f);
+  pos[h] = make_int2(pp.x + t, pp.y);
+  rot[h] = r;
+  qpos[h] = qq;
+  qrot[h] = qr;
+  qcdage[h] = ca;
+  if (p == 0) {
+    misc[i] = m;
+    done[i] = (uint8_t)t;
+  }
+  float4* o = reinterpret_cast<float4*>(obs + ((int64_t)p * n + i) * 12);
+  const float f = (float)pp.x;
+  o[0] = make_float4(f, f, f, f);
+  o[1] = make_float4(f, f, (float)r, f);
+  o[2] = make_float4(f, (float)qr, f, f);
+  obs[24 * n + (int64_t)p * n + i] = f;
+}
+
+extern "C" int skdiag_launch_full(void* const* planes, const float* actions, uint8_t* done, float* obs, int64_t n,
+                                  void* stream) {
+  unsigned grid = (unsigned)((2 * n + kDiagBlock - 1) / kDiagBlock);
+  kd_copy_full<<<grid, kDiagBlock, 0, (hipStream_t)stream>>>(
+      (int2*)planes[0], (double*)planes[1], (int2*)planes[2], (double*)planes[3], (int2*)planes[4],
+      (int2*)planes[5], (const float2*)actions, done, obs, n);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 extern "C" int skdiag_launch(int kind, void* const* planes, const float* actions, uint8_t* done, int64_t n,
                              void* stream) {
   unsigned grid = (unsigned)((n + kDiagBlock - 1) / kDiagBlock);

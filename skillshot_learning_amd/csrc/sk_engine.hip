@@ -482,12 +482,19 @@ __global__ void __launch_bounds__(kStepBlock) k_step_split(StepArgs a, Cfg c) {
   // do_actions(p+1, ...)  SkillshotLearner.py:206-213, both sincos up front (tick_env)
   const double rn = rot + clamp_action((double)act.y) * c.look;
   const double qn = (qcd <= 0) ? rn : qrot;
-  bool k0, k1;
+  bool k0, k1, k2;
   sktrig::SinCos m = sktrig::sincos_bf(rot, &k0);
   sktrig::SinCos t = sktrig::sincos_bf(qn, &k1);
-  if (!(k0 & k1)) {
+  // the post-look rotation's sin/cos for the obs epilogue (fp32: obs12_sc)
+  sktrig::SinCosF pr = sktrig::sincos_fast(rn, &k2);
+  if (!(k0 & k1 & k2)) {
     if (!k0) m = sincos_lib(rot);
     if (!k1) t = sincos_lib(qn);
+    if (!k2) {
+      const sktrig::SinCos r = sincos_lib(rn);
+      pr.s = (float)r.s;
+      pr.c = (float)r.c;
+    }
   }
   move_direction_sc(c, px, py, m, (double)act.x);
   rot = rn;
@@ -505,24 +512,29 @@ __global__ void __launch_bounds__(kStepBlock) k_step_split(StepArgs a, Cfg c) {
   }
   ctr_settle(wc);  // every load consumed, no state store issued yet
   const bool d = in && ((!live) || (ticks >= a.tick_limit));  // SkillshotLearner.py:302
-  if (in && (a.obs || a.reward)) {
-    float o[12];
-    double pd;
-    const double gp = grad_fast(rot), gq = grad_fast(qrot);
-    bool amb;
-    obs12_g(c, px, py, rot, qx, qy, qrot, qcd, qvalid, opx, opy, gp, gq, o, &pd, &amb);
+  const bool want_obs = a.obs || a.reward || a.obs_reset;     // launch-uniform
+  float o[12];
+  bool amb = false;
+  if (in && want_obs) {
+    float pd;
+#ifdef SK_ABL_NOOBS  // timing ablation only: obs values without their arithmetic
+    for (int k = 0; k < 12; ++k) o[k] = (float)(px + k * qx) + pr.s * (float)t.c;
+    pd = o[3];
+#else
+    obs12_sc(c, px, py, rot, pr, qx, qy, qrot, t, qcd, qvalid, opx, opy, o, &pd, &amb);
+#endif
     if (a.obs) {
       store_obs(a.obs, a.n, p, i, o);
       if (amb) fix_future_flag(c, qx, qy, qrot, opx, opy, a.obs + ((int64_t)p * a.n + i) * 12 + 11);
     }
     if (a.reward) {
       float r;
-      if (a.reward_kind == SK_REWARD_SIMPLE) {
+      if (a.reward_kind == SK_REWARD_SIMPLE) {  // a difference of distances: fp64 roots
         double mine = dist_point_point(qx, qy, opx, opy);
         double theirs = dist_point_point(oqx, oqy, px, py);
         r = (float)(mine - theirs);
       } else {
-        r = (float)(-pd / (double)c.W);
+        r = (float)(-(double)pd / (double)c.W);
       }
       a.reward[(int64_t)p * a.n + i] = r;
     }
@@ -533,7 +545,8 @@ __global__ void __launch_bounds__(kStepBlock) k_step_split(StepArgs a, Cfg c) {
   }
   if (!in) return;
   const int fin_winner = winner, fin_ticks = ticks;  // before the restart
-  if (d && a.auto_reset) {  // SkillshotGame.__init__ :10-25 for this lane's player
+  const bool reset = d && a.auto_reset;
+  if (reset) {  // SkillshotGame.__init__ :10-25 for this lane's player
     if (a.random_positions) {
       U4 u = draw4(a.seed, (uint64_t)(a.env_offset + i), step, 1u);
       px = u32_to_pos(p ? u.z : u.x, c.rlo, c.rhi);
@@ -546,12 +559,15 @@ __global__ void __launch_bounds__(kStepBlock) k_step_split(StepArgs a, Cfg c) {
     ticks = 0; live = 1; winner = 0;
   }
   if (a.obs_reset) {
+    // a game that did not restart acts next on the obs just computed; a
+    // restarted one (both lanes of the pair) on its fresh state's, whose
+    // rotations are 0 (sin 0, cos 1: no trig) and projectile invalid
     const int rpx = __shfl_xor(px, 1, 64), rpy = __shfl_xor(py, 1, 64);
-    float o[12];
-    double pd;
-    const double gp = grad_fast(rot), gq = grad_fast(qrot);
-    bool amb;
-    obs12_g(c, px, py, rot, qx, qy, qrot, qcd, qvalid, rpx, rpy, gp, gq, o, &pd, &amb);
+    if (reset) {
+      float pd;
+      obs12_sc(c, px, py, rot, sktrig::SinCosF{0.0f, 1.0f}, qx, qy, qrot, sktrig::SinCos{0.0, 1.0}, qcd, qvalid,
+               rpx, rpy, o, &pd, &amb);
+    }
     store_obs(a.obs_reset, a.n, p, i, o);
     if (amb) fix_future_flag(c, qx, qy, qrot, rpx, rpy, a.obs_reset + ((int64_t)p * a.n + i) * 12 + 11);
   }

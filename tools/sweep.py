@@ -34,7 +34,20 @@ def run(variant, n, steps, graph_len, ring, obs=False):
 
     planes = (ctypes.c_void_p * 6)(*[getattr(env, k).data_ptr() for k in ("pos", "rot", "qpos", "qrot", "qcdage", "misc")])
     diag = {"empty": 0, "copy": 1, "copy_xcc": 2, "copy_b8": 3}.get(variant)
-    if diag is not None:
+    if variant == "copy_full":  # the full contract's traffic, split layout, no logic
+        L = env._L
+        L.skdiag_launch_full.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_int64, ctypes.c_void_p]
+        with torch.cuda.stream(st):
+            ob = torch.empty(26 * n, dtype=torch.float32, device="cuda")
+        st.synchronize()
+        obs = True
+
+        def launch(t):
+            rc = L.skdiag_launch_full(planes, ctypes.c_void_p(a0 + (t % ring) * slab), ctypes.c_void_p(done.data_ptr()),
+                                      ctypes.c_void_p(ob.data_ptr()), n, sp)
+            assert rc == 0
+    elif diag is not None:
         L = env._L
         L.skdiag_launch.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                     ctypes.c_void_p]
