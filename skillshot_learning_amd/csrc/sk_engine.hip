@@ -169,10 +169,14 @@ __device__ __forceinline__ void wave_count(sk_counters* ctr, const WaveCtr& w, b
 }
 
 __device__ __forceinline__ void store_obs(float* obs, int64_t n, int p, int64_t i, const float o[12]) {
-  float4* d = reinterpret_cast<float4*>(obs + ((int64_t)p * n + i) * 12);
-  d[0] = make_float4(o[0], o[1], o[2], o[3]);
-  d[1] = make_float4(o[4], o[5], o[6], o[7]);
-  d[2] = make_float4(o[8], o[9], o[10], o[11]);
+  // the row is 48 B into a 16-B aligned buffer: say so, or the backend may
+  // re-split the three vector stores at 4-byte alignment (dwordx3 + x4 + x4
+  // + x1 at offsets 0/12/28/44 in k_step_split)
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  f4* d = reinterpret_cast<f4*>(__builtin_assume_aligned(obs + ((int64_t)p * n + i) * 12, 16));
+  d[0] = f4{o[0], o[1], o[2], o[3]};
+  d[1] = f4{o[4], o[5], o[6], o[7]};
+  d[2] = f4{o[8], o[9], o[10], o[11]};
 }
 
 __device__ __forceinline__ float reward_of(const Cfg& c, const Env& e, int p, int kind, double path_dist) {
@@ -462,28 +466,31 @@ __global__ void __launch_bounds__(kStepBlock) k_step_split(StepArgs a, Cfg c) {
   const bool in = i < a.n;
   const int64_t h = 2 * i + p;  // this lane's half-plane index
   WaveCtr wc = ctr_load(a.ctr);
-  int px = 0, py = 0, qx = 0, qy = 0, qcd = 0, qage = 0, ticks = 0, flags = 0;
-  double rot = 0.0, qrot = 0.0;
-  float2 act = make_float2(0.f, 0.f);
-  if (in) {
-    int2 pp = reinterpret_cast<const int2*>(a.v.pos)[h];
-    int2 qq = reinterpret_cast<const int2*>(a.v.qpos)[h];
-    int2 ca = reinterpret_cast<const int2*>(a.v.qcdage)[h];
-    int2 m = a.v.misc[i];
-    rot = reinterpret_cast<const double*>(a.v.rot)[h];
-    qrot = reinterpret_cast<const double*>(a.v.qrot)[h];
-    act = load_action(a.actions + (int64_t)p * a.n + i);
-    px = pp.x; py = pp.y; qx = qq.x; qy = qq.y; qcd = ca.x; qage = ca.y;
-    ticks = m.x; flags = m.y;
-  }
+  // Loads are unconditional (a lane past the end reads game 0 and stores
+  // nothing), so no exec-mask branch surrounds them and each value is waited
+  // for on its own: issued rotation first, action last, the player's sincos
+  // of its old rotation then runs while the rest arrives.  (Loads inside
+  // `if (in)` made the join wait for all of them, action included.)
+  const int64_t ic = in ? i : 0, hc = 2 * ic + p;
+  double rot = reinterpret_cast<const double*>(a.v.rot)[hc];
+  double qrot = reinterpret_cast<const double*>(a.v.qrot)[hc];
+  const int2 pp = reinterpret_cast<const int2*>(a.v.pos)[hc];
+  const int2 ca = reinterpret_cast<const int2*>(a.v.qcdage)[hc];
+  const int2 qq = reinterpret_cast<const int2*>(a.v.qpos)[hc];
+  const int2 mi = a.v.misc[ic];
+  __builtin_amdgcn_sched_barrier(0);
+  const float2 act = load_action(a.actions + (int64_t)p * a.n + ic);
+  __builtin_amdgcn_sched_barrier(0);
+  bool k0, k1, k2;
+  sktrig::SinCos m = sktrig::sincos_bf(rot, &k0);
+  int px = pp.x, py = pp.y, qx = qq.x, qy = qq.y, qcd = ca.x, qage = ca.y, ticks = mi.x;
+  const int flags = mi.y;
   int qvalid = ((unsigned)flags >> (8 * p)) & 0xff;
   int live = ((unsigned)flags >> 16) & 0xff;
   int winner = ((unsigned)flags >> 24) & 0xff;
   // do_actions(p+1, ...)  SkillshotLearner.py:206-213, both sincos up front (tick_env)
   const double rn = rot + clamp_action((double)act.y) * c.look;
   const double qn = (qcd <= 0) ? rn : qrot;
-  bool k0, k1, k2;
-  sktrig::SinCos m = sktrig::sincos_bf(rot, &k0);
   sktrig::SinCos t = sktrig::sincos_bf(qn, &k1);
   // the post-look rotation's sin/cos for the obs epilogue (fp32: obs12_sc)
   sktrig::SinCosF pr = sktrig::sincos_fast(rn, &k2);
