@@ -443,7 +443,8 @@ __device__ __attribute__((noinline)) sktrig::SinCos sincos_lib(double x) {  // |
 // action-independent) supplied by the caller, who can evaluate them while
 // the actions are still in flight from memory.  ok01: both were in range.
 __device__ __forceinline__ void tick_env_m(const Cfg& c, Env& e, sktrig::SinCos m0, sktrig::SinCos m1, bool ok01,
-                                           double a0_move, double a0_look, double a1_move, double a1_look) {
+                                           double a0_move, double a0_look, double a1_move, double a1_look,
+                                           sktrig::SinCos* tq0 = nullptr, sktrig::SinCos* tq1 = nullptr) {
   const double rn0 = e.rot[0] + clamp_action(a0_look) * c.look;  // == move_look_s
   const double rn1 = e.rot[1] + clamp_action(a1_look) * c.look;
   const double q0 = (e.qcd[0] <= 0) ? rn0 : e.qrot[0];
@@ -460,6 +461,8 @@ __device__ __forceinline__ void tick_env_m(const Cfg& c, Env& e, sktrig::SinCos 
     if (!k2) t0 = sincos_lib(q0);
     if (!k3) t1 = sincos_lib(q1);
   }
+  if (tq0) *tq0 = t0;  // the projectiles' rotations after shoot: the obs epilogue's (obs_env_sc)
+  if (tq1) *tq1 = t1;
   // do_actions(1, ...), do_actions(2, ...)  SkillshotLearner.py:206-213
   move_direction_sc(c, e.px[0], e.py[0], m0, a0_move);
   e.rot[0] = rn0;
@@ -763,6 +766,25 @@ __device__ __forceinline__ void obs12_sc(const Cfg& c, int px, int py, double ro
   out[9] = (float)(((py_mod2_fast(qrot) * kPi) / 2.0) * kPi);
   out[10] = (float)(fabs(fma(qt.c, (double)ex, -(qt.s * (double)ey))) * c.inv_max_dist);
   out[11] = future_collision_s(c, qx, qy, qvalid, ox, oy, grad_from_sincos(qrot, qt), amb) ? 1.0f : 0.0f;
+}
+
+// both players' obs of one env from the projectile sincos the tick used
+// (tick_env_m's tq0/tq1) and an fp32 sincos of each post-look rotation;
+// returns the fix_future_flags bits
+__device__ __forceinline__ unsigned obs_env_sc(const Cfg& c, const Env& e, sktrig::SinCos t0, sktrig::SinCos t1,
+                                               float o0[12], float o1[12], float* pd0, float* pd1) {
+  bool k0, k1, m0, m1;
+  sktrig::SinCosF r0 = sktrig::sincos_fast(e.rot[0], &k0);
+  sktrig::SinCosF r1 = sktrig::sincos_fast(e.rot[1], &k1);
+  if (!(k0 & k1)) {
+    if (!k0) { const sktrig::SinCos r = sincos_lib(e.rot[0]); r0.s = (float)r.s; r0.c = (float)r.c; }
+    if (!k1) { const sktrig::SinCos r = sincos_lib(e.rot[1]); r1.s = (float)r.s; r1.c = (float)r.c; }
+  }
+  obs12_sc(c, e.px[0], e.py[0], e.rot[0], r0, e.qx[0], e.qy[0], e.qrot[0], t0, e.qcd[0], e.qvalid[0], e.px[1],
+           e.py[1], o0, pd0, &m0);
+  obs12_sc(c, e.px[1], e.py[1], e.rot[1], r1, e.qx[1], e.qy[1], e.qrot[1], t1, e.qcd[1], e.qvalid[1], e.px[0],
+           e.py[0], o1, pd1, &m1);
+  return (unsigned)m0 | ((unsigned)m1 << 1);
 }
 
 // tan(-rot + pi/2) correctly rounded (Player.py:94 / Projectile.py:58)

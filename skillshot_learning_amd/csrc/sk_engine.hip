@@ -251,6 +251,10 @@ struct StepArgs {
   sk_counters* ctr;
 };
 
+// OBS: the launch writes obs / reward / obs_reset (instantiated apart so the
+// step-only tick keeps no obs state live: holding the projectiles' sincos for
+// the epilogue cost the headline tick 0.09 us, profiles/r02_step_obs_ab.jsonl)
+template <bool OBS>
 __global__ void __launch_bounds__(kStepBlock) k_step(StepArgs a, Cfg c) {
   int64_t i = (int64_t)blockIdx.x * kStepBlock + threadIdx.x;
   SK_TS(ts0);
@@ -261,6 +265,7 @@ __global__ void __launch_bounds__(kStepBlock) k_step(StepArgs a, Cfg c) {
   bool d = false;
   Env e;
   double q_old0 = 0.0, q_old1 = 0.0;  // stored projectile rotations (store_env_q)
+  sktrig::SinCos tq0 = {0.0, 1.0}, tq1 = {0.0, 1.0};  // the projectiles' sincos after shoot
   U4 ru = {0u, 0u, 0u, 0u};
 #ifdef SK_TRACE_STEP
   unsigned long long ts1 = 0, ts2 = 0;
@@ -296,7 +301,8 @@ __global__ void __launch_bounds__(kStepBlock) k_step(StepArgs a, Cfg c) {
     bool k0, k1;
     const sktrig::SinCos m0 = sktrig::sincos_bf(e.rot[0], &k0);
     const sktrig::SinCos m1 = sktrig::sincos_bf(e.rot[1], &k1);
-    tick_env_m(c, e, m0, m1, k0 & k1, (double)a0.x, (double)a0.y, (double)a1.x, (double)a1.y);
+    tick_env_m(c, e, m0, m1, k0 & k1, (double)a0.x, (double)a0.y, (double)a1.x, (double)a1.y, OBS ? &tq0 : nullptr,
+               OBS ? &tq1 : nullptr);
 #ifdef SK_TRACE_STEP
     __builtin_amdgcn_sched_barrier(0);
     ts2 = __builtin_amdgcn_s_memrealtime();
@@ -304,19 +310,20 @@ __global__ void __launch_bounds__(kStepBlock) k_step(StepArgs a, Cfg c) {
 #endif
   }
   ctr_settle(wc);  // every load consumed, no state store issued yet
+  float o0[12], o1[12];
+  unsigned amb = 0;
   if (in) {
-    if (a.obs || a.reward) {
-      float o0[12], o1[12];
-      double pd0, pd1;
-      const unsigned amb = obs_env(c, e, o0, o1, &pd0, &pd1);
+    if (OBS && (a.obs || a.reward || a.obs_reset)) {
+      float pd0, pd1;
+      amb = obs_env_sc(c, e, tq0, tq1, o0, o1, &pd0, &pd1);
       if (a.obs) {
         store_obs(a.obs, a.n, 0, i, o0);
         store_obs(a.obs, a.n, 1, i, o1);
         if (amb) fix_future_flags(c, e, amb, a.obs, a.n, i);
       }
       if (a.reward) {
-        a.reward[i] = reward_of(c, e, 0, a.reward_kind, pd0);
-        a.reward[a.n + i] = reward_of(c, e, 1, a.reward_kind, pd1);
+        a.reward[i] = reward_of(c, e, 0, a.reward_kind, (double)pd0);
+        a.reward[a.n + i] = reward_of(c, e, 1, a.reward_kind, (double)pd1);
       }
     }
     d = (!e.live) || (e.ticks >= a.tick_limit);  // SkillshotLearner.py:302
@@ -337,10 +344,13 @@ __global__ void __launch_bounds__(kStepBlock) k_step(StepArgs a, Cfg c) {
     }
     else reset_fixed(c, e);
   }
-  if (in && a.obs_reset) {
-    float o0[12], o1[12];
-    double pd0, pd1;
-    const unsigned amb = obs_env(c, e, o0, o1, &pd0, &pd1);
+  if (OBS && in && a.obs_reset) {
+    // a game that did not restart acts next on the obs just computed; a
+    // restarted one on its fresh state's (rotations 0: sin 0, cos 1)
+    if (d && a.auto_reset) {
+      float pd0, pd1;
+      amb = obs_env_sc(c, e, sktrig::SinCos{0.0, 1.0}, sktrig::SinCos{0.0, 1.0}, o0, o1, &pd0, &pd1);
+    }
     store_obs(a.obs_reset, a.n, 0, i, o0);
     store_obs(a.obs_reset, a.n, 1, i, o1);
     if (amb) fix_future_flags(c, e, amb, a.obs_reset, a.n, i);
@@ -1218,8 +1228,10 @@ int sk_env_step(sk_env* e, const float* actions, float* obs, float* reward, int3
     k_step_split<<<step_grid(2 * (int64_t)e->n), kStepBlock, 0, (hipStream_t)stream>>>(a, e->dcfg);
   else if (variant == 2)
     k_step_fast<<<step_grid(e->n), kStepBlock, 0, (hipStream_t)stream>>>(a, e->dcfg);
+  else if (a.obs || a.reward || a.obs_reset)
+    k_step<true><<<step_grid(e->n), kStepBlock, 0, (hipStream_t)stream>>>(a, e->dcfg);
   else
-    k_step<<<step_grid(e->n), kStepBlock, 0, (hipStream_t)stream>>>(a, e->dcfg);
+    k_step<false><<<step_grid(e->n), kStepBlock, 0, (hipStream_t)stream>>>(a, e->dcfg);
   SK_LAUNCH_CHECK();
   e->parity ^= 1;
   return SK_OK;
