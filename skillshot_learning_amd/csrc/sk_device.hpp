@@ -644,6 +644,11 @@ __device__ __attribute__((noinline)) void fix_future_flag(const Cfg& c, int qx, 
   *slot = future_collision_g(c, qx, qy, ox, oy, sktan::tan_cr(-qrot + kPi2)) ? 1.0f : 0.0f;
 }
 
+// the same flag as a value (callers that store it themselves)
+__device__ __attribute__((noinline)) float future_flag_cr(const Cfg& c, int qx, int qy, double qrot, int ox, int oy) {
+  return future_collision_g(c, qx, qy, ox, oy, sktan::tan_cr(-qrot + kPi2)) ? 1.0f : 0.0f;
+}
+
 // the obs rows [2][N][12] of env i were stored from env state e; amb bit p
 // marks player p's flag for redoing
 __device__ __forceinline__ void fix_future_flags(const Cfg& c, const Env& e, unsigned amb, float* obs, int64_t n,
@@ -745,6 +750,9 @@ __device__ __forceinline__ double grad_from_sincos(double qrot, sktrig::SinCos q
   const double bb = y - kPi2;
   const double err = (kPi2 - (y - bb)) + (-qrot - bb);
   const double eta = kPi2Lo + err;
+#ifdef SK_ABL_NODIV  // timing ablation only: wrong values, no fp64 division
+  return fma(-eta, qt.s, qt.c) * fma(eta, qt.c, qt.s);
+#endif
   return fma(-eta, qt.s, qt.c) / fma(eta, qt.c, qt.s);
 }
 
@@ -765,7 +773,15 @@ __device__ __forceinline__ void obs12_sc(const Cfg& c, int px, int py, double ro
   out[8] = (float)((double)qy * c.inv_H);
   out[9] = (float)(((py_mod2_fast(qrot) * kPi) / 2.0) * kPi);
   out[10] = (float)(fabs(fma(qt.c, (double)ex, -(qt.s * (double)ey))) * c.inv_max_dist);
+#ifdef SK_ABL_NOFLAG  // timing ablation only: the flag without its gradient / margin test
+  out[11] = (float)(qvalid & (qx > ox));
+  *amb = false;
+#else
   out[11] = future_collision_s(c, qx, qy, qvalid, ox, oy, grad_from_sincos(qrot, qt), amb) ? 1.0f : 0.0f;
+#ifdef SK_ABL_NOAMB  // timing ablation only: never take the correctly rounded redo
+  *amb = false;
+#endif
+#endif
 }
 
 // both players' obs of one env from the projectile sincos the tick used

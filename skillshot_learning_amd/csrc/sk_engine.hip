@@ -540,10 +540,7 @@ __global__ void __launch_bounds__(kStepBlock) k_step_split(StepArgs a, Cfg c) {
 #else
     obs12_sc(c, px, py, rot, pr, qx, qy, qrot, t, qcd, qvalid, opx, opy, o, &pd, &amb);
 #endif
-    if (a.obs) {
-      store_obs(a.obs, a.n, p, i, o);
-      if (amb) fix_future_flag(c, qx, qy, qrot, opx, opy, a.obs + ((int64_t)p * a.n + i) * 12 + 11);
-    }
+    if (a.obs) store_obs(a.obs, a.n, p, i, o);
     if (a.reward) {
       float r;
       if (a.reward_kind == SK_REWARD_SIMPLE) {  // a difference of distances: fp64 roots
@@ -562,6 +559,8 @@ __global__ void __launch_bounds__(kStepBlock) k_step_split(StepArgs a, Cfg c) {
   }
   if (!in) return;
   const int fin_winner = winner, fin_ticks = ticks;  // before the restart
+  const int aqx = qx, aqy = qy;  // the post-tick projectile, for the flag's redo
+  const double aqrot = qrot;
   const bool reset = d && a.auto_reset;
   if (reset) {  // SkillshotGame.__init__ :10-25 for this lane's player
     if (a.random_positions) {
@@ -580,13 +579,13 @@ __global__ void __launch_bounds__(kStepBlock) k_step_split(StepArgs a, Cfg c) {
     // restarted one (both lanes of the pair) on its fresh state's, whose
     // rotations are 0 (sin 0, cos 1: no trig) and projectile invalid
     const int rpx = __shfl_xor(px, 1, 64), rpy = __shfl_xor(py, 1, 64);
-    if (reset) {
+    if (reset) {  // (its projectile is invalid: the flag is 0, never ambiguous)
       float pd;
+      bool amb_r;
       obs12_sc(c, px, py, rot, sktrig::SinCosF{0.0f, 1.0f}, qx, qy, qrot, sktrig::SinCos{0.0, 1.0}, qcd, qvalid,
-               rpx, rpy, o, &pd, &amb);
+               rpx, rpy, o, &pd, &amb_r);
     }
     store_obs(a.obs_reset, a.n, p, i, o);
-    if (amb) fix_future_flag(c, qx, qy, qrot, rpx, rpy, a.obs_reset + ((int64_t)p * a.n + i) * 12 + 11);
   }
   reinterpret_cast<int2*>(a.v.pos)[h] = make_int2(px, py);
   reinterpret_cast<double*>(a.v.rot)[h] = rot;
@@ -600,6 +599,15 @@ __global__ void __launch_bounds__(kStepBlock) k_step_split(StepArgs a, Cfg c) {
     a.v.misc[i] = make_int2(ticks, (int)f);
   }
   if (a.ctr) wave_count(a.ctr, wc, d && p == 0, fin_winner, fin_ticks);  // after the stores (see wave_count)
+  // The future-collision flag within its margin of an edge (rare: none in
+  // 2.9 M random-policy projectiles) is redone correctly rounded here, after
+  // every other store.  A call site ahead of the stores, even never taken,
+  // cost 1.75 us per 65,536-game tick (profiles/r02_split_flag_ab.jsonl).
+  if (amb) {
+    const float f = future_flag_cr(c, aqx, aqy, aqrot, opx, opy);
+    if (a.obs) a.obs[((int64_t)p * a.n + i) * 12 + 11] = f;
+    if (a.obs_reset && !reset) a.obs_reset[((int64_t)p * a.n + i) * 12 + 11] = f;
+  }
 }
 
 struct RolloutArgs {

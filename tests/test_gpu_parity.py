@@ -388,9 +388,12 @@ def test_fused_step_on_probe_boards(ssa, oracle_mod, step_variant):
     for t in range(4):
         acts = g.gen_random_actions(1)[0]
         ra = ref.gen_random_actions(1)[0]
-        out = g.step(acts, obs=True, auto_reset=False)
+        out = g.step(acts, obs=True, auto_reset=False, reset_obs=True)
         wo = ref.step(ra, tick_limit=2000, auto_reset=False)
         torch.cuda.synchronize()
+        # no restart: the next tick's obs are this tick's, flags (and their
+        # correctly rounded redo on ambiguous lanes) included
+        assert torch.equal(out["obs_reset"], out["obs"]), t
         assert np.array_equal(out["done"].cpu().numpy(), wo["done"]), t
         assert np.array_equal(out["winner"].cpu().numpy(), wo["winner"]), t
         st = g.state_dict()
