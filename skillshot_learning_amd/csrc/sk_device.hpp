@@ -644,10 +644,48 @@ __device__ __attribute__((noinline)) void fix_future_flag(const Cfg& c, int qx, 
   *slot = future_collision_g(c, qx, qy, ox, oy, sktan::tan_cr(-qrot + kPi2)) ? 1.0f : 0.0f;
 }
 
+// The rare ambiguous flag (future_collision_s' *amb: a compare within its
+// margin of a span edge) without the correctly rounded tan in most cases: the
+// fast gradient g is within a few ulp of the correctly rounded one (sincos_bf
+// <= 1 ulp, the TwoSum-corrected quotient <= 2 ulp of glibc's tan, measured),
+// so if the reference's compare gives the same answer for every double within
+// kFlagUlps ulps of g, that answer is the correctly rounded tan's.  Returns
+// the flag, or -1 when it does depend on g's last bits (then tan_cr decides).
+// Most ambiguous lanes are hits, where the projectile sits on the opponent's
+// x and the compare is exact for every g; 17 compares replace tan_cr's ~700
+// dependent fp64 instructions on the slowest wave of the tick.
+constexpr int kFlagUlps = 8;
+
+__device__ __forceinline__ int future_flag_interval(const Cfg& c, int qx, int qy, int ox, int oy, double g) {
+  const long long b = __double_as_longlong(g);
+  const bool f0 = future_collision_g(c, qx, qy, ox, oy, g);
+  bool same = true;
+#pragma unroll
+  for (int k = 1; k <= kFlagUlps; ++k) {
+    same &= future_collision_g(c, qx, qy, ox, oy, __longlong_as_double(b + k)) == f0;
+    same &= future_collision_g(c, qx, qy, ox, oy, __longlong_as_double(b - k)) == f0;
+  }
+  return same ? (int)f0 : -1;
+}
+
 // the same flag as a value (callers that store it themselves)
+#if defined(SK_ABL_INLINEREDO)  // timing ablation: the redo inlined (no call)
+__device__ __forceinline__ float future_flag_cr(const Cfg& c, int qx, int qy, double qrot, int ox, int oy) {
+  return future_collision_g(c, qx, qy, ox, oy, sktan::tan_cr(-qrot + kPi2)) ? 1.0f : 0.0f;
+}
+#elif defined(SK_ABL_TRIVCALL)  // timing ablation only: a trivial out-of-line redo (wrong on ambiguous lanes)
+__device__ __attribute__((noinline)) float future_flag_cr(const Cfg& c, int qx, int qy, double qrot, int ox, int oy) {
+  return future_collision_g(c, qx, qy, ox, oy, qrot * 3.0) ? 1.0f : 0.0f;
+}
+#elif defined(SK_ABL_CHEAPREDO)  // timing ablation only: the redo without tan_cr (wrong on ambiguous lanes)
+__device__ __forceinline__ float future_flag_cr(const Cfg& c, int qx, int qy, double qrot, int ox, int oy) {
+  return future_collision_g(c, qx, qy, ox, oy, qrot * 3.0) ? 1.0f : 0.0f;
+}
+#else
 __device__ __attribute__((noinline)) float future_flag_cr(const Cfg& c, int qx, int qy, double qrot, int ox, int oy) {
   return future_collision_g(c, qx, qy, ox, oy, sktan::tan_cr(-qrot + kPi2)) ? 1.0f : 0.0f;
 }
+#endif
 
 // the obs rows [2][N][12] of env i were stored from env state e; amb bit p
 // marks player p's flag for redoing
@@ -655,6 +693,20 @@ __device__ __forceinline__ void fix_future_flags(const Cfg& c, const Env& e, uns
                                                  int64_t i) {
   if (amb & 1u) fix_future_flag(c, e.qx[0], e.qy[0], e.qrot[0], e.px[1], e.py[1], obs + i * 12 + 11);
   if (amb & 2u) fix_future_flag(c, e.qx[1], e.qy[1], e.qrot[1], e.px[0], e.py[0], obs + (n + i) * 12 + 11);
+}
+
+// the same with the interval check first (g0, g1: the fast gradients the
+// flags were decided from)
+__device__ __forceinline__ void fix_future_flags_g(const Cfg& c, const Env& e, unsigned amb, double g0, double g1,
+                                                   float* obs, int64_t n, int64_t i) {
+  if (amb & 1u) {
+    const int f = future_flag_interval(c, e.qx[0], e.qy[0], e.px[1], e.py[1], g0);
+    obs[i * 12 + 11] = f >= 0 ? (float)f : future_flag_cr(c, e.qx[0], e.qy[0], e.qrot[0], e.px[1], e.py[1]);
+  }
+  if (amb & 2u) {
+    const int f = future_flag_interval(c, e.qx[1], e.qy[1], e.px[0], e.py[0], g1);
+    obs[(n + i) * 12 + 11] = f >= 0 ? (float)f : future_flag_cr(c, e.qx[1], e.qy[1], e.qrot[1], e.px[0], e.py[0]);
+  }
 }
 
 __device__ __forceinline__ double py_mod2(double r) {  // Python float % 2 (floored)
@@ -758,7 +810,7 @@ __device__ __forceinline__ double grad_from_sincos(double qrot, sktrig::SinCos q
 
 __device__ __forceinline__ void obs12_sc(const Cfg& c, int px, int py, double rot, sktrig::SinCosF pr, int qx,
                                          int qy, double qrot, sktrig::SinCos qt, int qcd, int qvalid, int ox, int oy,
-                                         float out[12], float* path_dist, bool* amb) {
+                                         float out[12], float* path_dist, bool* amb, double* gq = nullptr) {
   const int dx = ox - px, dy = oy - py, ex = ox - qx, ey = oy - qy;
   const float pd = fabsf(fmaf(pr.c, (float)dx, -(pr.s * (float)dy)));
   *path_dist = pd;
@@ -777,7 +829,9 @@ __device__ __forceinline__ void obs12_sc(const Cfg& c, int px, int py, double ro
   out[11] = (float)(qvalid & (qx > ox));
   *amb = false;
 #else
-  out[11] = future_collision_s(c, qx, qy, qvalid, ox, oy, grad_from_sincos(qrot, qt), amb) ? 1.0f : 0.0f;
+  const double g = grad_from_sincos(qrot, qt);
+  if (gq) *gq = g;
+  out[11] = future_collision_s(c, qx, qy, qvalid, ox, oy, g, amb) ? 1.0f : 0.0f;
 #ifdef SK_ABL_NOAMB  // timing ablation only: never take the correctly rounded redo
   *amb = false;
 #endif
@@ -788,7 +842,8 @@ __device__ __forceinline__ void obs12_sc(const Cfg& c, int px, int py, double ro
 // (tick_env_m's tq0/tq1) and an fp32 sincos of each post-look rotation;
 // returns the fix_future_flags bits
 __device__ __forceinline__ unsigned obs_env_sc(const Cfg& c, const Env& e, sktrig::SinCos t0, sktrig::SinCos t1,
-                                               float o0[12], float o1[12], float* pd0, float* pd1) {
+                                               float o0[12], float o1[12], float* pd0, float* pd1,
+                                               double* g0 = nullptr, double* g1 = nullptr) {
   bool k0, k1, m0, m1;
   sktrig::SinCosF r0 = sktrig::sincos_fast(e.rot[0], &k0);
   sktrig::SinCosF r1 = sktrig::sincos_fast(e.rot[1], &k1);
@@ -797,9 +852,9 @@ __device__ __forceinline__ unsigned obs_env_sc(const Cfg& c, const Env& e, sktri
     if (!k1) { const sktrig::SinCos r = sincos_lib(e.rot[1]); r1.s = (float)r.s; r1.c = (float)r.c; }
   }
   obs12_sc(c, e.px[0], e.py[0], e.rot[0], r0, e.qx[0], e.qy[0], e.qrot[0], t0, e.qcd[0], e.qvalid[0], e.px[1],
-           e.py[1], o0, pd0, &m0);
+           e.py[1], o0, pd0, &m0, g0);
   obs12_sc(c, e.px[1], e.py[1], e.rot[1], r1, e.qx[1], e.qy[1], e.qrot[1], t1, e.qcd[1], e.qvalid[1], e.px[0],
-           e.py[0], o1, pd1, &m1);
+           e.py[0], o1, pd1, &m1, g1);
   return (unsigned)m0 | ((unsigned)m1 << 1);
 }
 

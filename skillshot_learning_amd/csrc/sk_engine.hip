@@ -312,14 +312,15 @@ __global__ void __launch_bounds__(kStepBlock) k_step(StepArgs a, Cfg c) {
   ctr_settle(wc);  // every load consumed, no state store issued yet
   float o0[12], o1[12];
   unsigned amb = 0;
+  double g0 = 0.0, g1 = 0.0;  // the fast projectile gradients (fix_future_flags_g)
   if (in) {
     if (OBS && (a.obs || a.reward || a.obs_reset)) {
       float pd0, pd1;
-      amb = obs_env_sc(c, e, tq0, tq1, o0, o1, &pd0, &pd1);
+      amb = obs_env_sc(c, e, tq0, tq1, o0, o1, &pd0, &pd1, &g0, &g1);
       if (a.obs) {
         store_obs(a.obs, a.n, 0, i, o0);
         store_obs(a.obs, a.n, 1, i, o1);
-        if (amb) fix_future_flags(c, e, amb, a.obs, a.n, i);
+        if (amb) fix_future_flags_g(c, e, amb, g0, g1, a.obs, a.n, i);
       }
       if (a.reward) {
         a.reward[i] = reward_of(c, e, 0, a.reward_kind, (double)pd0);
@@ -353,7 +354,7 @@ __global__ void __launch_bounds__(kStepBlock) k_step(StepArgs a, Cfg c) {
     }
     store_obs(a.obs_reset, a.n, 0, i, o0);
     store_obs(a.obs_reset, a.n, 1, i, o1);
-    if (amb) fix_future_flags(c, e, amb, a.obs_reset, a.n, i);
+    if (amb) fix_future_flags_g(c, e, amb, g0, g1, a.obs_reset, a.n, i);  // (restarted: amb = 0)
   }
   if (in) store_env_q(a.v, i, e, q_old0, q_old1);
 #ifndef SK_ABL_NOCTR  // timing ablation only
@@ -532,13 +533,14 @@ __global__ void __launch_bounds__(kStepBlock) k_step_split(StepArgs a, Cfg c) {
   const bool want_obs = a.obs || a.reward || a.obs_reset;     // launch-uniform
   float o[12];
   bool amb = false;
+  double gq = 0.0;  // the fast projectile gradient (the ambiguous flag's interval check)
   if (in && want_obs) {
     float pd;
 #ifdef SK_ABL_NOOBS  // timing ablation only: obs values without their arithmetic
     for (int k = 0; k < 12; ++k) o[k] = (float)(px + k * qx) + pr.s * (float)t.c;
     pd = o[3];
 #else
-    obs12_sc(c, px, py, rot, pr, qx, qy, qrot, t, qcd, qvalid, opx, opy, o, &pd, &amb);
+    obs12_sc(c, px, py, rot, pr, qx, qy, qrot, t, qcd, qvalid, opx, opy, o, &pd, &amb, &gq);
 #endif
     if (a.obs) store_obs(a.obs, a.n, p, i, o);
     if (a.reward) {
@@ -599,12 +601,14 @@ __global__ void __launch_bounds__(kStepBlock) k_step_split(StepArgs a, Cfg c) {
     a.v.misc[i] = make_int2(ticks, (int)f);
   }
   if (a.ctr) wave_count(a.ctr, wc, d && p == 0, fin_winner, fin_ticks);  // after the stores (see wave_count)
-  // The future-collision flag within its margin of an edge (rare: none in
-  // 2.9 M random-policy projectiles) is redone correctly rounded here, after
-  // every other store.  A call site ahead of the stores, even never taken,
-  // cost 1.75 us per 65,536-game tick (profiles/r02_split_flag_ab.jsonl).
+  // The future-collision flag within its margin of an edge is settled here,
+  // after every other store: ~3 lanes per 65,536-game tick, mostly hits
+  // (terminal states); by the interval check unless it depends on g's last
+  // bits (then the correctly rounded tan).  tan_cr on those lanes made their
+  // waves the tick's tail: 8.5 vs 6.9 us (profiles/r02_split_flag_ab.jsonl).
   if (amb) {
-    const float f = future_flag_cr(c, aqx, aqy, aqrot, opx, opy);
+    const int fi = future_flag_interval(c, aqx, aqy, opx, opy, gq);
+    const float f = fi >= 0 ? (float)fi : future_flag_cr(c, aqx, aqy, aqrot, opx, opy);
     if (a.obs) a.obs[((int64_t)p * a.n + i) * 12 + 11] = f;
     if (a.obs_reset && !reset) a.obs_reset[((int64_t)p * a.n + i) * 12 + 11] = f;
   }
