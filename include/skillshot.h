@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define SK_ABI_VERSION 3
+#define SK_ABI_VERSION 4
 
 enum {
   SK_OK = 0,
@@ -254,6 +254,14 @@ int sk_actor_forward_dev(const void* packed, const float* obs, float* actions, i
  * counter untouched. */
 int sk_actor_forward_advance(const void* packed, const float* obs, float* actions, int64_t rows, float noise_sd,
                              uint64_t seed, uint64_t* call_counter, void* stream);
+/* sk_actor_forward_advance with model_act_action_noise (SkillshotLearner.py:
+ * 229-243) drawn in the same launch: actions = tanh(...) + N(0, action_sd)
+ * per output, unclipped, keyed by (seed, row, call) on a counter stream of
+ * its own (parameter noise, noise_sd, may be drawn alongside).  A launch
+ * with either sd nonzero advances call_counter as above.  (ABI 4; replaces
+ * the learner's torch randn + add after the bf16 actor, 4 kernels a tick.) */
+int sk_actor_forward_noise(const void* packed, const float* obs, float* actions, int64_t rows, float noise_sd,
+                           float action_sd, uint64_t seed, uint64_t* call_counter, void* stream);
 
 /* --- critic forward and the DDPG bootstrap target (A16) ------------------- */
 

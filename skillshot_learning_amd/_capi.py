@@ -16,7 +16,7 @@ from . import build as _build
 
 SK_OK, SK_EINVAL, SK_EHIP, SK_ENOMEM, SK_ENODEV = 0, -1, -2, -3, -4
 SK_REWARD_LOOKING, SK_REWARD_SIMPLE = 0, 1
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # every symbol include/skillshot.h declares
 EXPORTS = (
@@ -27,7 +27,7 @@ EXPORTS = (
     "sk_player_move_discrete", "sk_player_shoot", "sk_projectile_move", "sk_game_check_collision", "sk_game_tick", "sk_env_features", "sk_env_observe",
     "sk_env_step", "sk_gen_random_actions", "sk_env_rollout_random",
     "sk_actor_packed_bytes", "sk_actor_pack", "sk_actor_forward", "sk_actor_forward_dev",
-    "sk_actor_forward_advance",
+    "sk_actor_forward_advance", "sk_actor_forward_noise",
     "sk_critic_packed_bytes", "sk_critic_pack", "sk_critic_forward", "sk_target_q",
     "sk_grad_packed_bytes", "sk_update_partials", "sk_grad_pack", "sk_critic_grad", "sk_actor_grad", "sk_adam_flat",
     "sk_adam_flat_packed",
@@ -117,6 +117,7 @@ def load(build_if_missing=True):
         "sk_actor_forward": ([P, P, P, i64, ctypes.c_float, u64, u64, P], ctypes.c_int),
         "sk_actor_forward_dev": ([P, P, P, i64, ctypes.c_float, u64, P, P], ctypes.c_int),
         "sk_actor_forward_advance": ([P, P, P, i64, ctypes.c_float, u64, P, P], ctypes.c_int),
+        "sk_actor_forward_noise": ([P, P, P, i64, ctypes.c_float, ctypes.c_float, u64, P, P], ctypes.c_int),
         "sk_critic_packed_bytes": ([], ctypes.c_size_t),
         "sk_critic_pack": ([P, P, P, P, P, P, P, P], ctypes.c_int),
         "sk_critic_forward": ([P, P, P, P, i64, P], ctypes.c_int),

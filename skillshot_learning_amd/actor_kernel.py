@@ -46,9 +46,12 @@ class ActorKernel:
         if rc != 0:
             raise SkillshotError(f"sk_actor_pack failed ({rc})")
 
+    fused_action_noise = True  # model_act_action_noise's N(0, sd) is drawn in the kernel (sk_actor_forward_noise)
+
     @torch.no_grad()
-    def __call__(self, obs, noise_sd=0.0, generator=None, out=None):
-        """obs float32 [M, 12] -> actions float32 [M, 2]."""
+    def __call__(self, obs, noise_sd=0.0, generator=None, out=None, action_sd=0.0):
+        """obs float32 [M, 12] -> actions float32 [M, 2]; noise_sd: parameter
+        noise, action_sd: action noise on the tanh outputs."""
         x = obs if obs.dtype == torch.float32 else obs.float()
         x = x.contiguous()
         if x.dim() != 2 or x.shape[1] != 12:
@@ -56,9 +59,9 @@ class ActorKernel:
         m = x.shape[0]
         y = out if out is not None else torch.empty((m, 2), dtype=torch.float32, device=self.device)
         self.calls += 1
-        rc = self.L.sk_actor_forward_advance(ctypes.c_void_p(self.buf.data_ptr()), ctypes.c_void_p(x.data_ptr()),
-                                             ctypes.c_void_p(y.data_ptr()), m, float(noise_sd), self.seed,
-                                             ctypes.c_void_p(self._ctr.data_ptr()), self._stream())
+        rc = self.L.sk_actor_forward_noise(ctypes.c_void_p(self.buf.data_ptr()), ctypes.c_void_p(x.data_ptr()),
+                                           ctypes.c_void_p(y.data_ptr()), m, float(noise_sd), float(action_sd),
+                                           self.seed, ctypes.c_void_p(self._ctr.data_ptr()), self._stream())
         if rc != 0:
             raise SkillshotError(f"sk_actor_forward failed ({rc})")
         return y

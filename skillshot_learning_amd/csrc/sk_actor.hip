@@ -111,12 +111,14 @@ __global__ void __launch_bounds__(threads_for<NOISE>()) k_actor_fwd(const float*
                                                         int64_t M, const char* __restrict__ packed, float sd,
                                                         uint64_t seed, uint64_t call,
                                                         const uint64_t* __restrict__ call_dev = nullptr,
-                                                        float* dbg = nullptr, uint64_t* adv = nullptr) {
+                                                        float* dbg = nullptr, uint64_t* adv = nullptr,
+                                                        float action_sd = 0.f) {
   // the noise call number comes from device memory when given (graph replays
   // then draw fresh noise per replay): *call_dev, advanced by the caller, or,
   // with adv, adv[0] + 1, stored back by the last workgroup (advance_call)
-  if (NOISE && call_dev) call = *call_dev;  // wave-uniform scalar load
-  if (NOISE && adv) call = adv[0] + 1;
+  const bool draws = NOISE || action_sd != 0.f;  // parameter and/or action noise
+  if (draws && call_dev) call = *call_dev;  // wave-uniform scalar load
+  if (draws && adv) call = adv[0] + 1;
   asm volatile("" : "+s"(call));  // read before the staging barrier (advance_call relies on it)
   const float k2 = noise_k2(sd);
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -259,10 +261,16 @@ __global__ void __launch_bounds__(threads_for<NOISE>()) k_actor_fwd(const float*
         if (DBG) dbg[row * kDbgCols + kH1 + kH2 + i] = y;
         o[i] = tanhf(y);
       }
+      if (action_sd != 0.f) {  // model_act_action_noise (:229-243): tanh output + N(0, sd), unclipped
+        float za[2];
+        normals2(seed, call, (uint32_t)row, 13u, noise_k2(action_sd), za);
+        o[0] += za[0];
+        o[1] += za[1];
+      }
       *(float2*)(out + row * kOut) = make_float2(o[0], o[1]);
     }
   }
-  if (NOISE && adv) advance_call(adv, call);
+  if (draws && adv) advance_call(adv, call);
 }
 
 // One 32-row tile per WORKGROUP: for batches too small to give every SIMD its
@@ -281,7 +289,7 @@ __global__ void __launch_bounds__(kWgThreads) k_actor_fwd_wg(const float* __rest
                                                             int64_t M, const char* __restrict__ packed, float sd,
                                                             uint64_t seed, uint64_t call,
                                                             const uint64_t* __restrict__ call_dev,
-                                                            uint64_t* adv = nullptr) {
+                                                            uint64_t* adv = nullptr, float action_sd = 0.f) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16x8* sW2 = (bf16x8*)smem;
   bf16x8* sW2s = (bf16x8*)(smem + kW2Frag);
@@ -289,8 +297,9 @@ __global__ void __launch_bounds__(kWgThreads) k_actor_fwd_wg(const float* __rest
   float* sW3 = sB + 512;
   bf16x8* sH1 = (bf16x8*)(sB + 1024);            // [16 k-steps][64 lanes]
   float4* sPart = (float4*)(sH1 + 16 * 64);      // [4 waves][32 rows]: m0 m1 q0 q1
-  if (NOISE && call_dev) call = *call_dev;
-  if (NOISE && adv) call = adv[0] + 1;
+  const bool draws = NOISE || action_sd != 0.f;  // parameter and/or action noise
+  if (draws && call_dev) call = *call_dev;
+  if (draws && adv) call = adv[0] + 1;
   asm volatile("" : "+s"(call));  // read before the staging barrier (advance_call)
   const float k2 = noise_k2(sd);
   {
@@ -408,10 +417,16 @@ __global__ void __launch_bounds__(kWgThreads) k_actor_fwd_wg(const float* __rest
         const float y = NOISE ? noisy_pre(mm[i], b, qq[i], z[i]) : mm[i] + b;
         o2[i] = tanhf(y);
       }
+      if (action_sd != 0.f) {  // model_act_action_noise (:229-243), as k_actor_fwd
+        float za[2];
+        normals2(seed, call, (uint32_t)row, 13u, noise_k2(action_sd), za);
+        o2[0] += za[0];
+        o2[1] += za[1];
+      }
       *(float2*)(out + row * kOut) = make_float2(o2[0], o2[1]);
     }
   }
-  if (NOISE && adv) advance_call(adv, call);
+  if (draws && adv) advance_call(adv, call);
 }
 
 // launch-mode override for tests and sweeps: 0 auto, 1 tile per wave, 2 tile per workgroup
@@ -434,7 +449,7 @@ int sk_actor_pack(const float* W1, const float* b1, const float* W2, const float
 
 static int actor_forward(const void* packed, const float* obs, float* actions, int64_t rows, float noise_sd,
                          uint64_t seed, uint64_t call, const uint64_t* call_dev, void* stream,
-                         uint64_t* adv = nullptr) {
+                         uint64_t* adv = nullptr, float action_sd = 0.f) {
   if (!packed || !obs || !actions || rows < 0) return SK_EINVAL;
   if ((((uintptr_t)obs) & 15) || (((uintptr_t)actions) & 7) || (((uintptr_t)packed) & 15)) return SK_EINVAL;
   if (call_dev && (((uintptr_t)call_dev) & 7)) return SK_EINVAL;
@@ -478,19 +493,19 @@ static int actor_forward(const void* packed, const float* obs, float* actions, i
     const int64_t wgrid = tiles < cus ? tiles : cus;
     if (noise)
       k_actor_fwd_wg<true><<<(unsigned)wgrid, kWgThreads, lds + kWgExtra, (hipStream_t)stream>>>(
-          obs, actions, rows, (const char*)packed, noise_sd, seed, call, call_dev, adv);
+          obs, actions, rows, (const char*)packed, noise_sd, seed, call, call_dev, adv, action_sd);
     else
       k_actor_fwd_wg<false><<<(unsigned)wgrid, kWgThreads, lds + kWgExtra, (hipStream_t)stream>>>(
-          obs, actions, rows, (const char*)packed, 0.f, seed, call, nullptr);
+          obs, actions, rows, (const char*)packed, 0.f, seed, call, call_dev, adv, action_sd);
     return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
   }
   if (noise) {
     k_actor_fwd<true><<<(unsigned)grid, threads, lds, (hipStream_t)stream>>>(obs, actions, rows, (const char*)packed,
                                                                             noise_sd, seed, call, call_dev, nullptr,
-                                                                            adv);
+                                                                            adv, action_sd);
   } else {
-    k_actor_fwd<false><<<(unsigned)grid, threads, lds, (hipStream_t)stream>>>(obs, actions, rows,
-                                                                             (const char*)packed, 0.f, seed, call);
+    k_actor_fwd<false><<<(unsigned)grid, threads, lds, (hipStream_t)stream>>>(
+        obs, actions, rows, (const char*)packed, 0.f, seed, call, call_dev, nullptr, adv, action_sd);
   }
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
 }
@@ -511,6 +526,13 @@ int sk_actor_forward_advance(const void* packed, const float* obs, float* action
   if (!call_counter) return SK_EINVAL;
   if (noise_sd == 0.f) return actor_forward(packed, obs, actions, rows, 0.f, seed, 0, nullptr, stream);
   return actor_forward(packed, obs, actions, rows, noise_sd, seed, 0, nullptr, stream, call_counter);
+}
+
+int sk_actor_forward_noise(const void* packed, const float* obs, float* actions, int64_t rows, float noise_sd,
+                           float action_sd, uint64_t seed, uint64_t* call_counter, void* stream) {
+  if (!call_counter || !(action_sd >= 0.f) || !(noise_sd >= 0.f)) return SK_EINVAL;
+  if (noise_sd == 0.f && action_sd == 0.f) return actor_forward(packed, obs, actions, rows, 0.f, seed, 0, nullptr, stream);
+  return actor_forward(packed, obs, actions, rows, noise_sd, seed, 0, nullptr, stream, call_counter, action_sd);
 }
 
 // diagnostics only (not in include/skillshot.h): force the launch mode

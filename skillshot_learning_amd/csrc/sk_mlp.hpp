@@ -103,6 +103,19 @@ __device__ __forceinline__ void normals16(uint64_t seed, uint64_t call, uint32_t
   }
 }
 
+// 2 normals of standard deviation sd (model_act_action_noise's N(0, sd) on
+// the two tanh outputs): one Philox draw, the first word as in normals16
+__device__ __forceinline__ void normals2(uint64_t seed, uint64_t call, uint32_t row, uint32_t stream, float k2,
+                                         float z[2]) {
+  const uint4 u = philox(make_uint4(row, stream * 4u, (uint32_t)call, (uint32_t)(call >> 32)), (uint32_t)seed,
+                         (uint32_t)(seed >> 32));
+  const float u1 = ((float)(u.x & 0xFFFFu) + 0.5f) * 0x1p-16f;
+  const float rev = (float)(u.x >> 16) * 0x1p-16f;
+  const float rad = __builtin_amdgcn_sqrtf(k2 * __builtin_amdgcn_logf(u1));
+  z[0] = rad * __builtin_amdgcn_cosf(rev);
+  z[1] = rad * __builtin_amdgcn_sinf(rev);
+}
+
 // noisy pre-activation y = m + b + sqrt(v + b^2) * zs (zs already scaled by
 // sd).  v is a sum of products of squares (>= 0), so v + b^2 needs no clamp.
 __device__ __forceinline__ float noisy_pre(float m, float b, float v, float zs) {

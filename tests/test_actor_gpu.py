@@ -126,6 +126,30 @@ def test_noise_counter_advances_in_kernel(mods, rows):
     assert k._ctr.tolist() == [3, 0]
 
 
+@pytest.mark.parametrize("rows", [8192, 65536])  # tile-per-workgroup and tile-per-wave launch modes
+def test_action_noise_in_kernel(mods, rows):
+    """model_act_action_noise (:229-243) in the bf16 kernel
+    (sk_actor_forward_noise): the clean tanh outputs + N(0, 0.15) per output,
+    unclipped; the call counter advances per launch, so repeated calls and
+    graph replays draw fresh noise; parameter noise alongside still works."""
+    learner, ActorKernel = mods
+    a = _actor(learner, seed=9)
+    k = ActorKernel(a, seed=5)
+    x = torch.rand(rows, 12, device="cuda")
+    clean = k(x)
+    a1 = k(x, action_sd=0.15)
+    a2 = k(x, action_sd=0.15)
+    torch.cuda.synchronize()
+    assert k._ctr.tolist() == [2, 0]
+    z = ((a1 - clean) / 0.15).double().cpu().flatten()
+    assert abs(float(z.mean())) < 0.03 and abs(float(z.std()) - 1.0) < 0.03
+    assert abs(float((z.abs() < 1).double().mean()) - 0.6827) < 0.02  # normal, not uniform
+    assert float(a1.abs().max()) > 1.0  # unclipped, as the reference adds after tanh
+    assert not torch.equal(a1, a2)
+    both = k(x, noise_sd=0.5, action_sd=0.15)
+    assert k._ctr.tolist() == [3, 0] and bool(torch.isfinite(both).all())
+
+
 def test_learner_replay_training_runs(mods):
     learner, _ = mods
     L = learner.SkillshotLearner(n_envs=2048, seed=1, tick_limit=300, replay_capacity=1 << 16, gamma=0.9, tau=0.005)
