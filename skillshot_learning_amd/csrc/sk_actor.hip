@@ -32,9 +32,14 @@ using namespace skmlp;
 
 // deterministic: 8 waves (two per SIMD, 141 VGPRs); noise: 4 waves (one per
 // SIMD) so the mean and variance chains' operands (h1, h1^2: 128 VGPRs) plus
-// both accumulators fit the 512-register budget without spilling
+// both accumulators fit the 512-register budget without spilling (332 VGPRs;
+// 8 waves force 256 and 77 spilled: 61 -> 72 us at 131,072 rows,
+// profiles/r02_actor_threads_ab.jsonl)
+#ifndef SK_NOISE_THREADS  // A/B builds only
+#define SK_NOISE_THREADS 256
+#endif
 template <bool NOISE>
-constexpr int threads_for() { return NOISE ? 256 : 512; }
+constexpr int threads_for() { return NOISE ? SK_NOISE_THREADS : 512; }
 
 
 // ---------------------------------------------------------------- packing
