@@ -293,9 +293,19 @@ def full_contract_rate(dev, args, rank, n, launches=2000):
     env.close()
     us = ev * 1e3 / launches
     gbs = BYTES_FULL_CONTRACT * n / (us * 1e-6) / 1e9
+    traffic = None
+    tj = os.path.join(ROOT, "profiles", "traffic_k_step_split.json")
+    if os.path.exists(tj):
+        try:
+            t = json.load(open(tj))
+            traffic = t.get("hbm_bytes_per_launch") if t.get("envs") == n else None
+        except Exception:
+            traffic = None
     return dict(envs_per_gpu=n, kernel="k_step_split (auto variant with obs)", launches=launches,
                 us_per_launch=us, env_steps_per_s_per_gpu=n / (us * 1e-6),
                 roofline=dict(bound="hbm", achieved=gbs, peak=HBM_PEAK_GBS, unit="GB/s", frac=gbs / HBM_PEAK_GBS,
+                              traffic=traffic,
+                              traffic_source="profiles/traffic_k_step_split.json (rocprofv3 --pmc pass, not this run)",
                               bytes_per_env_step=BYTES_FULL_CONTRACT,
                               bytes="state 88 read + 88 written, actions 16, obs 96, reward 8, done 1"))
 

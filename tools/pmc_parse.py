@@ -24,7 +24,9 @@ def load(dirs, kernel):
             with open(path) as f:
                 for row in csv.DictReader(f):
                     name = row.get("Kernel_Name", "")
-                    if not name.startswith(kernel + "(") and name != kernel:
+                    if name.startswith("void "):  # template instances: "void k_step<false>(...)"
+                        name = name[5:]
+                    if not (name.startswith(kernel + "(") or name.startswith(kernel + "<") or name == kernel):
                         continue
                     vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in vals.items()}, {k: len(v) for k, v in vals.items()}
