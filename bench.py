@@ -596,7 +596,7 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "traffic_source": "profiles/traffic_k_step.json (rocprofv3 --pmc pass, not this run)",
-                "kernel": "k_step",
+                "kernel": "k_step" if n > 8192 else "k_step_split (auto variant at <= 8,192 games per GPU)",
                 "bytes_per_env_step": BYTES_PER_ENV_STEP,
                 "kernel_us": kern_ms * 1e3,
             },

@@ -77,6 +77,12 @@ static constexpr int kBlock = 256;
 static constexpr int kStepBlock = SK_STEP_BLOCK;
 static constexpr int64_t kFastStepMinEnvs = 196608;
 static constexpr int64_t kFastStepMaxEnvs = 786432;
+// at or below this many games the step-only tick is latency-bound on a
+// fraction of the SIMDs, and two lanes per game (k_step_split, half the
+// dependent chain per lane) beat k_step: 8,192 games 3.25 vs 3.33 us, 16,384
+// 3.58 vs 3.51 (profiles/r02_step_small_ab.jsonl) -- the per-GPU size of the
+// metric's 65,536 games over 8 ranks
+static constexpr int64_t kSplitStepMaxEnvs = 8192;
 static constexpr int64_t kEarlyDrawMinEnvs = 32768;  // k_step: restart draw under the loads
 // Counter slots per wave: 4 x 32 B = one 128-B line, so no two waves (on
 // different XCDs, whose L2s write partial lines back at the end of the
@@ -1235,7 +1241,7 @@ int sk_env_step(sk_env* e, const float* actions, float* obs, float* reward, int3
   const int variant = e->step_variant >= 0 ? e->step_variant
                       : (e->n >= kFastStepMinEnvs && e->n < kFastStepMaxEnvs) ? 2
                       : e->n >= kFastStepMaxEnvs ? 0
-                      : (obs || reward || obs_reset) ? 1 : 0;
+                      : (obs || reward || obs_reset || e->n <= kSplitStepMaxEnvs) ? 1 : 0;
   if (variant == 1)
     k_step_split<<<step_grid(2 * (int64_t)e->n), kStepBlock, 0, (hipStream_t)stream>>>(a, e->dcfg);
   else if (variant == 2)
