@@ -308,6 +308,15 @@ int sk_replay_insert(float* ring, int64_t capacity, int64_t* total, uint32_t* ar
                      int64_t n_games, int64_t rows, void* stream);
 int sk_replay_sample(const float* ring, int64_t capacity, const int64_t* total, uint64_t seed, int32_t draw,
                      int64_t batch, float* s, float* a, float* r, float* s2, float* d, void* stream);
+/* sk_replay_insert followed by sk_replay_sample in ONE launch, bit for bit
+ * (same draw, key and range as a sample after the insert): a sampled row the
+ * launch is inserting is read from the insert's sources.  The learner tick's
+ * two ring launches (SkillshotLearner.py:302-324 + the north_star replay
+ * extension) become one.  (ABI 4.) */
+int sk_replay_insert_sample(float* ring, int64_t capacity, int64_t* total, uint32_t* arrivals, const float* obs,
+                            const float* actions, const float* rewards, const float* next_obs, const uint8_t* done,
+                            int64_t n_games, int64_t rows, uint64_t seed, int32_t draw, int64_t batch, float* s,
+                            float* a, float* r, float* s2, float* d, void* stream);
 
 /* --- the DDPG update (A16, F1) ------------------------------------------- */
 

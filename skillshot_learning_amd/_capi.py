@@ -31,7 +31,7 @@ EXPORTS = (
     "sk_critic_packed_bytes", "sk_critic_pack", "sk_critic_forward", "sk_target_q",
     "sk_grad_packed_bytes", "sk_update_partials", "sk_grad_pack", "sk_critic_grad", "sk_actor_grad", "sk_adam_flat",
     "sk_adam_flat_packed",
-    "sk_target_y", "sk_replay_insert", "sk_replay_sample", "sk_grad_pack_flat",
+    "sk_target_y", "sk_replay_insert", "sk_replay_sample", "sk_replay_insert_sample", "sk_grad_pack_flat",
     "sk_critic_grad_bootstrap",
     "sk_update_partials_f32", "sk_actor_forward_f32", "sk_critic_grad_f32", "sk_actor_grad_f32",
 )
@@ -134,6 +134,8 @@ def load(build_if_missing=True):
         "sk_target_y": ([P, P, P, P, P, f32, P, i64, P], ctypes.c_int),
         "sk_replay_insert": ([P, i64, P, P, P, P, P, P, P, i64, i64, P], ctypes.c_int),
         "sk_replay_sample": ([P, i64, P, u64, i32, i64, P, P, P, P, P, P], ctypes.c_int),
+        "sk_replay_insert_sample": ([P, i64, P, P, P, P, P, P, P, i64, i64, u64, i32, i64, P, P, P, P, P, P],
+                                    ctypes.c_int),
         "sk_grad_pack_flat": ([P, P, P, P, i32, P], ctypes.c_int),
         "sk_critic_grad_bootstrap": ([P, P, P, P, P, P, P, f32, P, P, i64, i64, f32, u64, P, P, P, i32, P, P, P],
                                      ctypes.c_int),

@@ -310,16 +310,45 @@ class ReplayRing:
             self.total_t.add_(n)
         self.total += n  # host mirror (exact while n is fixed)
 
+    def add_sample_dev(self, s, a, r, s2, d, b):
+        """add_dev followed by sample_dev(b) in one launch on the GPU
+        (sk_replay_insert_sample, bit-identical to the two); the pair
+        elsewhere."""
+        if self._k is None:
+            self.add_dev(s, a, r, s2, d)
+            return self.sample_dev(b)
+        from . import _capi
+        n = s.shape[0]
+        if n > self.cap:
+            raise ValueError("add_sample_dev: more rows than capacity")
+        out = self._batch_bufs(b)
+        p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        sc, ac = s.float().contiguous(), a.float().contiguous()
+        rc, s2c = r.float().contiguous(), s2.float().contiguous()
+        dc = d.contiguous() if d.dtype == torch.uint8 else (d != 0).to(torch.uint8).contiguous()
+        draw = self._draws
+        self._draws = (self._draws + 1) & 0x7FFFFFFF
+        _capi.check(self._k.sk_replay_insert_sample(
+            p(self.buf), self.cap, p(self.total_t), p(self._arrivals), p(sc), p(ac), p(rc), p(s2c), p(dc),
+            dc.numel(), n, self.seed, draw, b, *[p(t) for t in out],
+            ctypes.c_void_p(torch.cuda.current_stream(self.buf.device).cuda_stream)))
+        self.total += n
+        return out
+
+    def _batch_bufs(self, b):
+        out = self._batches.get(b)
+        if out is None:
+            dev = self.buf.device
+            out = self._batches[b] = (torch.empty(b, STATE_DIM, device=dev), torch.empty(b, ACTION_DIM, device=dev),
+                                      torch.empty(b, device=dev), torch.empty(b, STATE_DIM, device=dev),
+                                      torch.empty(b, device=dev))
+        return out
+
     def sample_dev(self, b, generator=None):
         """Capturable uniform sample over the device-side size."""
         if self._k is not None:
             from . import _capi
-            out = self._batches.get(b)
-            if out is None:
-                dev = self.buf.device
-                out = self._batches[b] = (torch.empty(b, STATE_DIM, device=dev), torch.empty(b, ACTION_DIM, device=dev),
-                                          torch.empty(b, device=dev), torch.empty(b, STATE_DIM, device=dev),
-                                          torch.empty(b, device=dev))
+            out = self._batch_bufs(b)
             p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
             draw = self._draws
             self._draws = (self._draws + 1) & 0x7FFFFFFF
@@ -999,13 +1028,17 @@ class TickGraph:
             a.copy_(L.model_act(obs).view(-1, ACTION_DIM))
         o = L.game_environment.step(self.act, obs=True, reward="looking", auto_reset=True, reset_obs=True,
                                     out=self.out)
-        L.replay.add_dev(x, a, o["reward"].view(-1), o["obs"].view(-1, STATE_DIM),
-                         o["done"])  # per game: row r of the [2N] rows takes game r % N
+        # per game: row r of the [2N] rows takes game r % N
+        rows = (x, a, o["reward"].view(-1), o["obs"].view(-1, STATE_DIM), o["done"])
         self._cur ^= 1
-        if update:
-            for _ in range(self.updates):
+        if update and self.updates > 0:
+            # the insert and the first update's minibatch in one launch
+            L.ddpg.update_batch(*L.replay.add_sample_dev(*rows, self.batch))
+            for _ in range(self.updates - 1):
                 L.ddpg.replay_update(self.batch, device_sampling=True)
             L._refresh_actor_pack()
+        else:
+            L.replay.add_dev(*rows)
 
     def run(self, n=1):
         """n graph replays (n * ticks_per_graph ticks) on the graph's stream."""

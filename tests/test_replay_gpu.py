@@ -78,3 +78,24 @@ def test_fused_target_matches_unfused(learner):
     y = d._target_kernel().target(s2, r, done, 0.9)
     ref = r + 0.9 * (1.0 - done) * d.target_q(s2)
     assert torch.allclose(y, ref, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("n,cap,B", [(5, 64, 256), (300, 1000, 4096), (4096, 1 << 15, 256), (256, 512, 1000)])
+def test_insert_sample_fused_equals_insert_then_sample(learner, n, cap, B):
+    """sk_replay_insert_sample (the learner tick's one ring launch) against
+    sk_replay_insert then sk_replay_sample on an identical ring: the same
+    ring, counters and minibatch bit for bit, through wrap-around and with
+    rows of the current tick among the sampled ones (cap = 2n: every row)."""
+    one = learner.ReplayRing(cap, "cuda", seed=3)
+    two = learner.ReplayRing(cap, "cuda", seed=3)
+    for t in range(2 * cap // (2 * n) + 3):
+        rows = _tick(n, t)
+        got = [x.clone() for x in one.add_sample_dev(*rows, B)]
+        two.add_dev(*rows)
+        want = [x.clone() for x in two.sample_dev(B)]
+        torch.cuda.synchronize()
+        for g, w in zip(got, want):
+            assert torch.equal(g, w), t
+        assert int(one.total_t) == int(two.total_t) == one.total == two.total
+        assert torch.equal(one.buf, two.buf)
+        assert int(one._arrivals) == 0
