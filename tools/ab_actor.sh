@@ -11,6 +11,6 @@ python3 - $OUT <<'PY'
 import json, sys, collections
 d = collections.defaultdict(list)
 for l in open(sys.argv[1]):
-    j = json.loads(l); r = j["r"]; d[(j["lib"], r["precision"], r["rows"], r["param_noise"])].append(r["us"])
+    j = json.loads(l); r = j["r"]; d[(j["lib"], r["precision"], r["rows"], r["param_noise"], r.get("action_noise", 0.0))].append(r["us"])
 for k, v in sorted(d.items()): print(k, [round(x, 2) for x in v])
 PY

@@ -25,18 +25,18 @@ def main():
         x = torch.rand(rows, 12, device="cuda")
         out = torch.empty(rows, 2, device="cuda")
         for prec, k in kernels.items():
-            for sd in (0.0, 0.5):
+            for sd, asd in ((0.0, 0.0), (0.5, 0.0), (0.0, 0.15)):
                 for _ in range(3):
-                    k(x, noise_sd=sd, out=out)
+                    k(x, noise_sd=sd, out=out, action_sd=asd)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(a.iters):
-                    k(x, noise_sd=sd, out=out)
+                    k(x, noise_sd=sd, out=out, action_sd=asd)
                 e1.record()
                 torch.cuda.synchronize()
                 us = e0.elapsed_time(e1) * 1e3 / a.iters
                 flop = 72192 * rows * (2 if sd else 1)  # 2 x MACs of 12x256 + 256x128 + 128x2; noise doubles
-                print(json.dumps(dict(precision=prec, rows=rows, param_noise=sd, us=us,
+                print(json.dumps(dict(precision=prec, rows=rows, param_noise=sd, action_noise=asd, us=us,
                                       tflops=flop / (us * 1e-6) / 1e12)), flush=True)
 
 
