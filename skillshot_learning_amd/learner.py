@@ -1031,14 +1031,19 @@ class TickGraph:
         # per game: row r of the [2N] rows takes game r % N
         rows = (x, a, o["reward"].view(-1), o["obs"].view(-1, STATE_DIM), o["done"])
         self._cur ^= 1
-        if update and self.updates > 0:
+        if update and self.updates > 0 and os.environ.get("SK_FUSED_REPLAY", "1") != "0":
             # the insert and the first update's minibatch in one launch
+            # (SK_FUSED_REPLAY=0: the two launches, for A/B)
             L.ddpg.update_batch(*L.replay.add_sample_dev(*rows, self.batch))
             for _ in range(self.updates - 1):
                 L.ddpg.replay_update(self.batch, device_sampling=True)
             L._refresh_actor_pack()
         else:
             L.replay.add_dev(*rows)
+            if update:
+                for _ in range(self.updates):
+                    L.ddpg.replay_update(self.batch, device_sampling=True)
+                L._refresh_actor_pack()
 
     def run(self, n=1):
         """n graph replays (n * ticks_per_graph ticks) on the graph's stream."""
