@@ -75,6 +75,12 @@ def run(n, obs, G=400, ring=400):
                last_entry_to_last_done_ns=ns(t3.max(1) - t0.max(1)),
                gap_ns=ns(t0.min(1)[1:] - t3.max(1)[:-1]),
                launch_period_ns=ns(np.diff(t0.min(1))),
+               # the tail: how much later than the median wave the last one finishes, and why
+               end_rel_med_ns=ns(np.median(t3 - t0.min(1)[:, None], axis=1)),
+               end_rel_max_ns=ns((t3 - t0.min(1)[:, None]).max(1)),
+               entry_of_last_done_ns=ns((t0 - t0.min(1)[:, None])[np.arange(16), (t3).argmax(1)]),
+               load_ns_max=ns((t1 - t0).max(1)), tick_ns_max=ns((t2 - t1).max(1)),
+               store_ns_max=ns((t3 - t2).max(1)),
                xcc_of_wave_0_15=[int(x) for x in xcc[:16]],
                cu_ids_distinct=int(len(np.unique(hw & ~np.int64(0xF)))))
     return res
