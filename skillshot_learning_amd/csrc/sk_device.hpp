@@ -656,16 +656,42 @@ __device__ __attribute__((noinline)) void fix_future_flag(const Cfg& c, int qx, 
 // dependent fp64 instructions on the slowest wave of the tick.
 constexpr int kFlagUlps = 8;
 
+// Only the compares within the margin are re-evaluated (the flag is an OR of
+// two span tests, X = ox and X = ox + psize): a test certainly inside the
+// span settles the flag at 1, and a certain test keeps its value for every g.
+__device__ __forceinline__ bool span_test(const Cfg& c, int qx, int qy, int X, int oy, double g) {
+  const double yi = (double)qy - g * (double)qx;  // SkillshotGame.py:105-111, reference order
+  const double v = g * (double)X + yi;
+  return ((double)oy <= v) & (v <= (double)(oy + c.psize));
+}
+
 __device__ __forceinline__ int future_flag_interval(const Cfg& c, int qx, int qy, int ox, int oy, double g) {
+  const double yi = (double)qy - g * (double)qx;
+  const double lo = (double)oy, hi = (double)(oy + c.psize);
+  const double v0 = g * (double)ox + yi, v1 = g * (double)(ox + c.psize) + yi;
+  const double eps = kFutureMargin * (fabs(g) * (fabs((double)ox) + (double)c.psize + fabs((double)qx)) +
+                                      fabs((double)qy) + fabs(yi) + hi + 1.0);  // future_collision_s' margin
+  const bool in0 = (lo <= v0) & (v0 <= hi), in1 = (lo <= v1) & (v1 <= hi);
+  const bool u0 = fabs(v0 - lo) <= eps || fabs(v0 - hi) <= eps;
+  const bool u1 = fabs(v1 - lo) <= eps || fabs(v1 - hi) <= eps;
+  if ((in0 && !u0) || (in1 && !u1)) return 1;
   const long long b = __double_as_longlong(g);
-  const bool f0 = future_collision_g(c, qx, qy, ox, oy, g);
   bool same = true;
+  if (u0) {
 #pragma unroll
-  for (int k = 1; k <= kFlagUlps; ++k) {
-    same &= future_collision_g(c, qx, qy, ox, oy, __longlong_as_double(b + k)) == f0;
-    same &= future_collision_g(c, qx, qy, ox, oy, __longlong_as_double(b - k)) == f0;
+    for (int k = 1; k <= kFlagUlps; ++k) {
+      same &= span_test(c, qx, qy, ox, oy, __longlong_as_double(b + k)) == in0;
+      same &= span_test(c, qx, qy, ox, oy, __longlong_as_double(b - k)) == in0;
+    }
   }
-  return same ? (int)f0 : -1;
+  if (u1) {
+#pragma unroll
+    for (int k = 1; k <= kFlagUlps; ++k) {
+      same &= span_test(c, qx, qy, ox + c.psize, oy, __longlong_as_double(b + k)) == in1;
+      same &= span_test(c, qx, qy, ox + c.psize, oy, __longlong_as_double(b - k)) == in1;
+    }
+  }
+  return same ? (int)(in0 | in1) : -1;
 }
 
 // the same flag as a value (callers that store it themselves)
