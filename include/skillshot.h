@@ -258,8 +258,13 @@ int sk_actor_forward_advance(const void* packed, const float* obs, float* action
  * 229-243) drawn in the same launch: actions = tanh(...) + N(0, action_sd)
  * per output, unclipped, keyed by (seed, row, call) on a counter stream of
  * its own (parameter noise, noise_sd, may be drawn alongside).  A launch
- * with either sd nonzero advances call_counter as above.  (ABI 4; replaces
- * the learner's torch randn + add after the bf16 actor, 4 kernels a tick.) */
+ * with either sd nonzero advances the call number as above, but
+ * call_counter is uint64[SK_ACTOR_COUNTER_WORDS] = {call number, 0, 0, ...}:
+ * the workgroups arrive in 8 groups on words 2 + 16g (one 128-byte line
+ * each) before word 1, which spreads the device-scope atomics (all zero
+ * again between launches).  (ABI 4; replaces the learner's torch randn + add
+ * after the bf16 actor, 4 kernels a tick.) */
+#define SK_ACTOR_COUNTER_WORDS 130
 int sk_actor_forward_noise(const void* packed, const float* obs, float* actions, int64_t rows, float noise_sd,
                            float action_sd, uint64_t seed, uint64_t* call_counter, void* stream);
 
@@ -424,9 +429,10 @@ int sk_adam_flat_packed(const float* partials, int32_t n_partials, int32_t n_par
  *                         by local reparameterisation, keyed by (seed, row,
  *                         unit, call); action_sd != 0 adds N(0, action_sd) to
  *                         the tanh outputs (model_act_action_noise, :229-243);
- *                         call_counter (nullable; uint64[2] = {call, 0}) is
- *                         read and advanced on device by every noisy launch,
- *                         as by sk_actor_forward_advance.
+ *                         call_counter (nullable; uint64[SK_ACTOR_COUNTER_
+ *                         WORDS] = {call, 0, ...}) is read and advanced on
+ *                         device by every noisy launch, as by
+ *                         sk_actor_forward_noise.
  *   sk_critic_grad_f32    as sk_critic_grad_bootstrap (target_actor_flat NULL:
  *                         y = targets; else y = rewards + gamma (1 - done)
  *                         Q'(next_obs, mu'(next_obs)) from the target nets).

@@ -27,8 +27,9 @@ class ActorKernel:
         self.buf = torch.empty(int(self.L.sk_actor_packed_bytes()), dtype=torch.uint8, device=self.device)
         self.seed = int(seed) & ((1 << 64) - 1)
         self.calls = 0
-        # device noise-call number and the launch's arrival slot (sk_actor_forward_advance)
-        self._ctr = torch.zeros(2, dtype=torch.int64, device=self.device)
+        # device noise-call number, the launch's arrival slot and its 8 group
+        # slots (sk_actor_forward_noise: SK_ACTOR_COUNTER_WORDS words)
+        self._ctr = torch.zeros(130, dtype=torch.int64, device=self.device)
         self.counter = self._ctr[:1]
         self.refresh()
 
@@ -86,7 +87,7 @@ class ActorKernel32:
         self.flat = flatten_module(actor)
         self.seed = int(seed) & ((1 << 64) - 1)
         self.calls = 0
-        self._ctr = torch.zeros(2, dtype=torch.int64, device=self.device)
+        self._ctr = torch.zeros(130, dtype=torch.int64, device=self.device)  # SK_ACTOR_COUNTER_WORDS
         self.counter = self._ctr[:1]
 
     def refresh(self):

@@ -101,13 +101,26 @@ constexpr int kDbgCols = 386 + 3 * 128;
 // With a device call counter adv = {call number, arrivals}: every workgroup has
 // read adv[0] before its first barrier; the last to finish stores the number
 // it used, so the next launch draws fresh noise without a separate add.
-__device__ __forceinline__ void advance_call(uint64_t* adv, uint64_t call) {
-  if (threadIdx.x == 0) {
-    const unsigned long long prev = atomicAdd((unsigned long long*)&adv[1], 1ull);
-    if (prev == (unsigned long long)gridDim.x - 1) {
-      adv[1] = 0;
-      adv[0] = call;
-    }
+// grouped (sk_actor_forward_noise, adv = uint64[SK_ACTOR_COUNTER_WORDS]):
+// workgroup b arrives first on group counter b % 8 (its own 128-byte line,
+// adv[2 + 16 (b % 8)]), the last of each group on adv[1]; device-scope
+// atomics on one address serialise, and 256 arrivals on adv[1] cost up to
+// 3 us of a bf16 launch (store-only ablation, profiles/r02_actor_arrival_ab.jsonl)
+__device__ __forceinline__ void advance_call(uint64_t* adv, uint64_t call, int grouped = 0) {
+  if (threadIdx.x != 0) return;
+  unsigned long long last = (unsigned long long)gridDim.x - 1;
+  if (grouped) {
+    const unsigned g = blockIdx.x & 7u;
+    const unsigned long long members = (gridDim.x - g + 7u) / 8u;  // workgroups b with b % 8 == g
+    unsigned long long* gc = (unsigned long long*)&adv[2 + 16 * g];
+    if (atomicAdd(gc, 1ull) != members - 1) return;
+    *gc = 0;  // every member of the group has arrived
+    last = (gridDim.x < 8u ? gridDim.x : 8u) - 1;
+  }
+  const unsigned long long prev = atomicAdd((unsigned long long*)&adv[1], 1ull);
+  if (prev == last) {
+    adv[1] = 0;
+    adv[0] = call;
   }
 }
 
@@ -117,7 +130,7 @@ __global__ void __launch_bounds__(threads_for<NOISE>()) k_actor_fwd(const float*
                                                         uint64_t seed, uint64_t call,
                                                         const uint64_t* __restrict__ call_dev = nullptr,
                                                         float* dbg = nullptr, uint64_t* adv = nullptr,
-                                                        float action_sd = 0.f) {
+                                                        float action_sd = 0.f, int grouped = 0) {
   // the noise call number comes from device memory when given (graph replays
   // then draw fresh noise per replay): *call_dev, advanced by the caller, or,
   // with adv, adv[0] + 1, stored back by the last workgroup (advance_call)
@@ -275,7 +288,7 @@ __global__ void __launch_bounds__(threads_for<NOISE>()) k_actor_fwd(const float*
       *(float2*)(out + row * kOut) = make_float2(o[0], o[1]);
     }
   }
-  if (draws && adv) advance_call(adv, call);
+  if (draws && adv) advance_call(adv, call, grouped);
 }
 
 // One 32-row tile per WORKGROUP: for batches too small to give every SIMD its
@@ -294,7 +307,8 @@ __global__ void __launch_bounds__(kWgThreads) k_actor_fwd_wg(const float* __rest
                                                             int64_t M, const char* __restrict__ packed, float sd,
                                                             uint64_t seed, uint64_t call,
                                                             const uint64_t* __restrict__ call_dev,
-                                                            uint64_t* adv = nullptr, float action_sd = 0.f) {
+                                                            uint64_t* adv = nullptr, float action_sd = 0.f,
+                                                            int grouped = 0) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16x8* sW2 = (bf16x8*)smem;
   bf16x8* sW2s = (bf16x8*)(smem + kW2Frag);
@@ -431,7 +445,7 @@ __global__ void __launch_bounds__(kWgThreads) k_actor_fwd_wg(const float* __rest
       *(float2*)(out + row * kOut) = make_float2(o2[0], o2[1]);
     }
   }
-  if (draws && adv) advance_call(adv, call);
+  if (draws && adv) advance_call(adv, call, grouped);
 }
 
 // launch-mode override for tests and sweeps: 0 auto, 1 tile per wave, 2 tile per workgroup
@@ -454,7 +468,7 @@ int sk_actor_pack(const float* W1, const float* b1, const float* W2, const float
 
 static int actor_forward(const void* packed, const float* obs, float* actions, int64_t rows, float noise_sd,
                          uint64_t seed, uint64_t call, const uint64_t* call_dev, void* stream,
-                         uint64_t* adv = nullptr, float action_sd = 0.f) {
+                         uint64_t* adv = nullptr, float action_sd = 0.f, int grouped = 0) {
   if (!packed || !obs || !actions || rows < 0) return SK_EINVAL;
   if ((((uintptr_t)obs) & 15) || (((uintptr_t)actions) & 7) || (((uintptr_t)packed) & 15)) return SK_EINVAL;
   if (call_dev && (((uintptr_t)call_dev) & 7)) return SK_EINVAL;
@@ -498,19 +512,19 @@ static int actor_forward(const void* packed, const float* obs, float* actions, i
     const int64_t wgrid = tiles < cus ? tiles : cus;
     if (noise)
       k_actor_fwd_wg<true><<<(unsigned)wgrid, kWgThreads, lds + kWgExtra, (hipStream_t)stream>>>(
-          obs, actions, rows, (const char*)packed, noise_sd, seed, call, call_dev, adv, action_sd);
+          obs, actions, rows, (const char*)packed, noise_sd, seed, call, call_dev, adv, action_sd, grouped);
     else
       k_actor_fwd_wg<false><<<(unsigned)wgrid, kWgThreads, lds + kWgExtra, (hipStream_t)stream>>>(
-          obs, actions, rows, (const char*)packed, 0.f, seed, call, call_dev, adv, action_sd);
+          obs, actions, rows, (const char*)packed, 0.f, seed, call, call_dev, adv, action_sd, grouped);
     return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
   }
   if (noise) {
     k_actor_fwd<true><<<(unsigned)grid, threads, lds, (hipStream_t)stream>>>(obs, actions, rows, (const char*)packed,
                                                                             noise_sd, seed, call, call_dev, nullptr,
-                                                                            adv, action_sd);
+                                                                            adv, action_sd, grouped);
   } else {
     k_actor_fwd<false><<<(unsigned)grid, threads, lds, (hipStream_t)stream>>>(
-        obs, actions, rows, (const char*)packed, 0.f, seed, call, call_dev, nullptr, adv, action_sd);
+        obs, actions, rows, (const char*)packed, 0.f, seed, call, call_dev, nullptr, adv, action_sd, grouped);
   }
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
 }
@@ -537,7 +551,7 @@ int sk_actor_forward_noise(const void* packed, const float* obs, float* actions,
                            float action_sd, uint64_t seed, uint64_t* call_counter, void* stream) {
   if (!call_counter || !(action_sd >= 0.f) || !(noise_sd >= 0.f)) return SK_EINVAL;
   if (noise_sd == 0.f && action_sd == 0.f) return actor_forward(packed, obs, actions, rows, 0.f, seed, 0, nullptr, stream);
-  return actor_forward(packed, obs, actions, rows, noise_sd, seed, 0, nullptr, stream, call_counter, action_sd);
+  return actor_forward(packed, obs, actions, rows, noise_sd, seed, 0, nullptr, stream, call_counter, action_sd, 1);
 }
 
 // diagnostics only (not in include/skillshot.h): force the launch mode

@@ -1032,12 +1032,20 @@ __global__ void __launch_bounds__(kFwdThreads) k_actor_fwd32(const float* __rest
   }
   if (draws) {  // the last workgroup to finish stores the call number it drew with
     __syncthreads();
+    // grouped arrival (as the bf16 actor's advance_call, csrc/sk_actor.hip):
+    // workgroup b on group line call_ctr[2 + 16 (b % 8)], the last of each
+    // group on call_ctr[1] (SK_ACTOR_COUNTER_WORDS)
     if (threadIdx.x == 0) {
-      const unsigned long long prev =
-          atomicAdd((unsigned long long*)&call_ctr[1], 1ull);
-      if (prev == gridDim.x - 1) {
-        call_ctr[0] = call;
-        call_ctr[1] = 0;
+      const unsigned g = blockIdx.x & 7u;
+      const unsigned long long members = (gridDim.x - g + 7u) / 8u;
+      unsigned long long* gc = (unsigned long long*)&call_ctr[2 + 16 * g];
+      if (atomicAdd(gc, 1ull) == members - 1) {
+        *gc = 0;
+        const unsigned long long groups = gridDim.x < 8u ? gridDim.x : 8u;
+        if (atomicAdd((unsigned long long*)&call_ctr[1], 1ull) == groups - 1) {
+          call_ctr[0] = call;
+          call_ctr[1] = 0;
+        }
       }
     }
   }

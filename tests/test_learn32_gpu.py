@@ -143,7 +143,7 @@ def test_actor_forward_f32_param_noise_distribution(mods):
     got = k(x, noise_sd=0.5)
     got2 = k(x, noise_sd=0.5)
     torch.cuda.synchronize()
-    assert int(k._ctr[0]) == 2 and int(k._ctr[1]) == 0
+    assert int(k._ctr[0]) == 2 and not k._ctr[1:].any()  # every arrival slot back at 0
     assert not torch.equal(got, got2)
     g = torch.Generator(device="cuda").manual_seed(1)
     a = d.model_actor
