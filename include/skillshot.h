@@ -317,7 +317,10 @@ int sk_replay_sample(const float* ring, int64_t capacity, const int64_t* total, 
  * (same draw, key and range as a sample after the insert): a sampled row the
  * launch is inserting is read from the insert's sources.  The learner tick's
  * two ring launches (SkillshotLearner.py:302-324 + the north_star replay
- * extension) become one.  (ABI 4.) */
+ * extension) become one.  arrivals: zeroed device
+ * uint32[SK_REPLAY_ARRIVAL_WORDS] (the workgroups arrive in 8 groups on
+ * separate 128-byte lines; all zero again between launches).  (ABI 4.) */
+#define SK_REPLAY_ARRIVAL_WORDS 288
 int sk_replay_insert_sample(float* ring, int64_t capacity, int64_t* total, uint32_t* arrivals, const float* obs,
                             const float* actions, const float* rewards, const float* next_obs, const uint8_t* done,
                             int64_t n_games, int64_t rows, uint64_t seed, int32_t draw, int64_t batch, float* s,

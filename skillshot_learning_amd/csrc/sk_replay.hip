@@ -175,11 +175,20 @@ __global__ void __launch_bounds__(kThreads) k_replay_insert_sample(
     }
   }
   __syncthreads();
+  // grouped arrival (arrivals = uint32[SK_REPLAY_ARRIVAL_WORDS]): workgroup b
+  // on group line arrivals[32 (1 + b % 8)], the last of each group on
+  // arrivals[0]; 500+ workgroups on one address serialise for microseconds
   if (threadIdx.x == 0) {
-    const unsigned prev = atomicAdd(arrivals, 1u);
-    if (prev == gridDim.x - 1) {  // the last workgroup: every other one has read total
-      *total = base + rows;
-      *arrivals = 0u;
+    const unsigned g = blockIdx.x & 7u;
+    const unsigned members = (gridDim.x - g + 7u) / 8u;
+    unsigned* gc = arrivals + 32u * (1u + g);
+    if (atomicAdd(gc, 1u) == members - 1u) {
+      *gc = 0u;
+      const unsigned groups = gridDim.x < 8u ? gridDim.x : 8u;
+      if (atomicAdd(arrivals, 1u) == groups - 1u) {  // the last workgroup: every other one has read total
+        *total = base + rows;
+        *arrivals = 0u;
+      }
     }
   }
 }

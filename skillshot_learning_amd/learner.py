@@ -246,7 +246,7 @@ class ReplayRing:
         if self.buf.is_cuda:
             from . import _capi
             self._k = _capi.load()
-            self._arrivals = torch.zeros(1, dtype=torch.int32, device=device)
+            self._arrivals = torch.zeros(288, dtype=torch.int32, device=device)  # SK_REPLAY_ARRIVAL_WORDS
             self._draws = 0
             self._batches = {}
 

@@ -98,4 +98,4 @@ def test_insert_sample_fused_equals_insert_then_sample(learner, n, cap, B):
             assert torch.equal(g, w), t
         assert int(one.total_t) == int(two.total_t) == one.total == two.total
         assert torch.equal(one.buf, two.buf)
-        assert int(one._arrivals) == 0
+        assert not one._arrivals.any()  # every arrival slot back at 0
