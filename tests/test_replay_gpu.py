@@ -99,3 +99,23 @@ def test_insert_sample_fused_equals_insert_then_sample(learner, n, cap, B):
         assert int(one.total_t) == int(two.total_t) == one.total == two.total
         assert torch.equal(one.buf, two.buf)
         assert not one._arrivals.any()  # every arrival slot back at 0
+
+
+def test_tick_graph_fused_replay_equals_two_launches(learner, monkeypatch):
+    """the captured learner tick with the ring's insert + minibatch in one
+    launch (default) and in two (SK_FUSED_REPLAY=0): identical nets, ring and
+    counters after the same ticks, bit for bit"""
+    out = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("SK_FUSED_REPLAY", fused)
+        L = learner.SkillshotLearner(n_envs=256, device="cuda", seed=5, exploration="action_noise", gamma=0.9,
+                                     tau=0.05, replay_capacity=4096)
+        tg = L.tick_graph(batch=128, ticks_per_graph=2, warmup=2)
+        tg.run(10)
+        torch.cuda.synchronize()
+        out.append((torch.cat([p.detach().flatten() for p in L.model_actor.parameters()]),
+                    torch.cat([p.detach().flatten() for p in L.model_critic.parameters()]),
+                    L.replay.buf.clone(), int(L.replay.total_t)))
+    (a1, c1, b1, t1), (a2, c2, b2, t2) = out
+    assert t1 == t2 and torch.equal(b1, b2)
+    assert torch.equal(a1, a2) and torch.equal(c1, c2)
