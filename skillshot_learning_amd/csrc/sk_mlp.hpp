@@ -58,6 +58,9 @@ __host__ __device__ __forceinline__ int w2_k(int kk, int h, int j) {
 }
 
 // ---------------------------------------------------------------- noise
+#ifndef SK_NOISE_ROUNDS  // Philox rounds of the actors' exploration noise (A/B builds)
+#define SK_NOISE_ROUNDS 10
+#endif
 template <int ROUNDS = 10>
 __device__ __forceinline__ uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
@@ -89,7 +92,8 @@ __device__ __forceinline__ void normals16(uint64_t seed, uint64_t call, uint32_t
                                           float k2, float z[16]) {
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
-    uint4 u = philox(make_uint4(row, (stream * 2 + (uint32_t)h) * 2 + q, (uint32_t)call, (uint32_t)(call >> 32)),
+    uint4 u = philox<SK_NOISE_ROUNDS>(make_uint4(row, (stream * 2 + (uint32_t)h) * 2 + q, (uint32_t)call,
+                                                 (uint32_t)(call >> 32)),
                      (uint32_t)seed, (uint32_t)(seed >> 32));
     uint32_t w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
