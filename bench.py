@@ -70,7 +70,10 @@ def parse():
     p.add_argument("--learner-timeout", type=float, default=240.0,
                    help="seconds per multi-rank learner leg (run in child processes)")
     p.add_argument("--learner-child", default=None, help=argparse.SUPPRESS)
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_k_step.json"))
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_k_step_multi.json"))
+    p.add_argument("--ticks-per-launch", type=int, default=400,
+                   help="k_step_multi: ticks per launch (the headline runs K ticks in ceil(K / this) launches)")
+    p.add_argument("--no-variants", action="store_true", help="skip the per-tick-launch / L2-resident legs")
     return p.parse_args()
 
 
@@ -84,10 +87,11 @@ class TickGraphs:
     value in slot 0, where the remainder graph (captured at the same parity)
     reads it.  So any mix of run() sizes keeps the reference RNG keys."""
 
-    def __init__(self, env, stream, launch, chunk):
+    def __init__(self, env, stream, launch, chunk, trace=None):
         self.env, self.stream, self.launch = env, stream, launch
         self.chunk = max(2, chunk - chunk % 2)
         self.graphs = {}
+        self.trace = trace  # optional list: ("run", m) per executed m-launch graph (launches 0..m-1)
 
     def _graph(self, n):
         g = self.graphs.get(n)
@@ -109,6 +113,8 @@ class TickGraphs:
             if not _launch_direct(g, self.stream):
                 with torch.cuda.stream(self.stream):
                     g.replay()
+            if self.trace is not None:
+                self.trace.append(("run", n))
             self.stream.synchronize()
             self.graphs[n] = g
         return g
@@ -137,6 +143,8 @@ class TickGraphs:
             if not _launch_direct(g, self.stream):
                 with torch.cuda.stream(self.stream):
                     g.replay()
+            if self.trace is not None:
+                self.trace.append(("run", m))
 
 
 _HIP = None
@@ -219,10 +227,14 @@ def _env_and_actions(dev, n, seed, env_offset, tick_limit, ring):
     return env, st, acts
 
 
-def timed_ticks(dev, n, seed, env_offset, tick_limit, k, warmup, ring, chunk, world, obs=False):
+def timed_ticks(dev, n, seed, env_offset, tick_limit, k, warmup, ring, chunk, world, obs=False, trace=None):
     """k graph-replayed fused-step launches over n games: (wall s max over
     ranks, HIP-event ms on the launch stream, env).  obs=True writes the
-    full contract (obs f32[2][n][12], reward f32[2][n], done) every tick."""
+    full contract (obs f32[2][n][12], reward f32[2][n], done) every tick.
+    trace (a list) receives the executed launches in order: ("run", m) = the
+    launches for slabs 0..m-1 (a graph, or the eager first launches) and
+    ("clear",) where the episode counters were zeroed (stream-ordered), so a
+    test can replay exactly what ran (tests/test_bench_path_gpu.py)."""
     env, st, acts = _env_and_actions(dev, n, seed, env_offset, tick_limit, ring)
     slab, sp = 16 * n, ctypes.c_void_p(st.cuda_stream)
     done = torch.empty(n, dtype=torch.uint8, device=dev)
@@ -238,12 +250,19 @@ def timed_ticks(dev, n, seed, env_offset, tick_limit, k, warmup, ring, chunk, wo
     with torch.cuda.stream(st):  # eager first launches load the code objects
         for t in range(4):
             launch(t)
+    if trace is not None:
+        trace.append(("run", 4))
     st.synchronize()
-    tg = TickGraphs(env, st, launch, chunk)
+    tg = TickGraphs(env, st, launch, chunk, trace)
     tg.prepare(warmup)
     tg.prepare(k)
     tg.sync()
-    env.clear_counters()
+    # on the launch stream: issued on torch's current (null) stream, the
+    # memset raced the pool stream's in-flight graph launches (VERDICT r02:
+    # the driver's episodes record counted dones from before the clear)
+    env.clear_counters(stream=sp)
+    if trace is not None:
+        trace.append(("clear",))
     tg.replay(warmup)
     tg.sync()
     st.synchronize()
@@ -267,7 +286,63 @@ def timed_ticks(dev, n, seed, env_offset, tick_limit, k, warmup, ring, chunk, wo
         el = float(tt.item())
     ev = e0.elapsed_time(e1)
     del tg
+    env.bench_actions = acts  # the ring (tests replay it)
+    env.bench_stream = st
     return el, ev, env
+
+
+def timed_multi(dev, n, seed, env_offset, tick_limit, k, warmup, ring, world, per_launch=500, trace=None):
+    """k ticks of the same step-only contract through k_step_multi
+    (sk_env_step_multi): launches of at most `per_launch` ticks, each tick
+    loading and storing every game's state (193 B per
+    env-step) and reading its own slab of the HBM action ring; the warm-up
+    runs the same way.  Returns (wall s max over ranks, HIP-event ms on the
+    launch stream, env).  trace receives ("slabs", first slab, ticks) per
+    launch and ("clear",), as timed_ticks'."""
+    env, st, acts = _env_and_actions(dev, n, seed, env_offset, tick_limit, ring)
+    sp = ctypes.c_void_p(st.cuda_stream)
+    done = torch.empty(n, dtype=torch.uint8, device=dev)
+    ap, dp = ctypes.c_void_p(acts.data_ptr()), ctypes.c_void_p(done.data_ptr())
+    slab = 0
+
+    def run(m):
+        nonlocal slab
+        while m > 0:
+            t = min(m, per_launch)
+            env.step_multi_raw(ap, ring, slab, t, dp, None, 0, stream=sp)
+            if trace is not None:
+                trace.append(("slabs", slab, t))
+            slab = (slab + t) % ring
+            m -= t
+
+    run(1)  # the first launch loads the code object
+    st.synchronize()
+    env.clear_counters(stream=sp)
+    if trace is not None:
+        trace.append(("clear",))
+    run(warmup)
+    st.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with torch.cuda.stream(st):
+        e0.record()
+    run(k)
+    with torch.cuda.stream(st):
+        e1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    env.bench_actions = acts
+    env.bench_stream = st
+    return el, e0.elapsed_time(e1), env
 
 
 def large_batch_rate(dev, args, rank, n=1 << 22, launches=60, ring=8):
@@ -310,13 +385,14 @@ def full_contract_rate(dev, args, rank, n, launches=2000):
                               bytes="state 88 read + 88 written, actions 16, obs 96, reward 8, done 1"))
 
 
-def weak_rate(dev, args, rank, world, n=65536, launches=2000):
-    """65,536 games per GPU (weak scaling), same fused tick and timing."""
-    el, ev, env = timed_ticks(dev, n, args.seed + 2, rank * n, args.tick_limit, launches, 200, args.action_ring,
-                              args.graph_len, world)
+def weak_rate(dev, args, rank, world, n=65536, ticks=4000):
+    """65,536 games per GPU (weak scaling), the headline's kernel and timing."""
+    el, ev, env = timed_multi(dev, n, args.seed + 2, rank * n, args.tick_limit, ticks, 200, args.action_ring, world,
+                              per_launch=args.ticks_per_launch)
     env.close()
-    return dict(envs_per_gpu=n, total_envs=n * world, n_gpus=world, env_steps_per_s=n * world * launches / el,
-                us_per_tick=el * 1e6 / launches, event_us_per_tick=ev * 1e3 / launches, scaling="weak")
+    return dict(envs_per_gpu=n, total_envs=n * world, n_gpus=world, env_steps_per_s=n * world * ticks / el,
+                us_per_tick=el * 1e6 / ticks, event_us_per_tick=ev * 1e3 / ticks, scaling="weak",
+                kernel="k_step_multi<1>")
 
 
 def learner_rate(envs, world, rank, ticks, batch=256, exploration="param_noise", precision="bf16", group=None,
@@ -480,14 +556,20 @@ def main():
     verbose = os.environ.get("SK_BENCH_VERBOSE") == "1"
     if verbose:
         _log(f"headline: {n} games per GPU, K={K}, W={W}")
-    elapsed, ev_ms, env = timed_ticks(dev, n, args.seed, rank * n, args.tick_limit, K, W, ring, args.graph_len, world)
+    # the headline: k_step_multi with the write-through state port (every
+    # tick's 176 state bytes leave L2: the contract bytes move; SK_MULTI_POLICY
+    # =0 is the L2-resident port, reported beside as step_variants.l2_resident)
+    os.environ["SK_MULTI_POLICY"] = "1"
+    elapsed, ev_ms, env = timed_multi(dev, n, args.seed, rank * n, args.tick_limit, K, W, ring, world,
+                                      per_launch=args.ticks_per_launch)
     value = n * world * K / elapsed
-    counters = env.counters()
+    counters = env.counters(stream=ctypes.c_void_p(env.bench_stream.cuda_stream))
     env.close()
 
-    # ---- roofline: the timed region is K back-to-back k_step launches on
-    # one stream (graph replays), so the HIP-event span / K is the kernel's
-    # average launch duration (rocprofv3 --stats reports the same figure).
+    # ---- roofline: the timed region is ceil(K / ticks_per_launch) back-to-back
+    # k_step_multi launches on one stream, so the HIP-event span / K is the
+    # kernel's average time per tick (rocprofv3 --stats: its average launch
+    # duration / ticks per launch).
     kern_ms = ev_ms / K
     achieved = BYTES_PER_ENV_STEP * n / (kern_ms * 1e-3) / 1e9
     traffic = None
@@ -495,11 +577,45 @@ def main():
         try:
             tj = json.load(open(args.traffic_json))
             if tj.get("envs") == n:
-                traffic = tj.get("hbm_bytes_per_launch")
+                traffic = tj.get("hbm_bytes_per_tick")
         except Exception:
             traffic = None
 
     errors = {}
+    variants = None
+    if not args.no_variants:
+        variants = {"note": "the same step-only contract through the other step kernels, HIP-event timed, "
+                            "reported beside the headline"}
+
+        def _per_tick():
+            k2 = 2000
+            el2, ev2, env2 = timed_ticks(dev, n, args.seed, rank * n, args.tick_limit, k2, 200, ring,
+                                         args.graph_len, 1)
+            env2.close()
+            us = ev2 * 1e3 / k2
+            gbs = BYTES_PER_ENV_STEP * n / (us * 1e-6) / 1e9
+            return dict(kernel="k_step (one graph-replayed launch per tick; the round-2 headline)", ticks=k2,
+                        us_per_tick=us, env_steps_per_s_per_gpu=n / (us * 1e-6), achieved_gbs=gbs,
+                        frac=gbs / HBM_PEAK_GBS)
+
+        def _l2():
+            os.environ["SK_MULTI_POLICY"] = "0"
+            try:
+                k2 = 4000
+                el2, ev2, env2 = timed_multi(dev, n, args.seed, rank * n, args.tick_limit, k2, 200, ring, 1,
+                                             per_launch=args.ticks_per_launch)
+                env2.close()
+            finally:
+                os.environ["SK_MULTI_POLICY"] = "1"
+            us = ev2 * 1e3 / k2
+            gbs = BYTES_PER_ENV_STEP * n / (us * 1e-6) / 1e9
+            return dict(kernel="k_step_multi<0> (plain state port)", ticks=k2, us_per_tick=us,
+                        env_steps_per_s_per_gpu=n / (us * 1e-6), contract_gbs=gbs,
+                        note="state stores and reloads stay in the XCD's L2 (PMC: profiles/"
+                             "traffic_k_step_multi_pol0.json), so this is not an HBM-roofline figure")
+
+        variants["per_tick_launch"] = _guard("step_variants.per_tick_launch", _per_tick, errors)
+        variants["l2_resident"] = _guard("step_variants.l2_resident", _l2, errors)
     rollout = None
     if not args.no_rollout:
         def _rollout():
@@ -579,13 +695,15 @@ def main():
             "data": "synthetic",
             "config": {
                 "workload": f"config-2 step kernel at the metric's size: {total} games in total, {n} per GPU, random "
-                            f"policy (Philox f32 actions pre-generated in HBM), fused k_step per tick (do_actions x2 + "
-                            f"game_tick + done + random auto-reset), tick_limit {args.tick_limit}, graph-replayed",
+                            f"policy (Philox f32 actions pre-generated in a 400-slab HBM ring), every tick do_actions x2 "
+                            f"+ game_tick + done + random auto-reset with each game's state loaded and stored "
+                            f"(write-through), tick_limit {args.tick_limit}; k_step_multi, "
+                            f"{min(K, args.ticks_per_launch)} ticks per launch",
+                "ticks_per_launch": min(K, args.ticks_per_launch),
                 "envs_per_gpu": n,
                 "total_envs": total,
                 "global_batch": total,
                 "parallelism": f"env-shard dp{world}",
-                "graph_len": args.graph_len,
                 "event_ms_per_step": kern_ms,
             },
             "roofline": {
@@ -595,13 +713,15 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "traffic_source": "profiles/traffic_k_step.json (rocprofv3 --pmc pass, not this run)",
-                "kernel": "k_step" if n > 8192 else "k_step_split (auto variant at <= 8,192 games per GPU)",
+                "traffic_source": "profiles/traffic_k_step_multi.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
+                                  "passes, per tick; not this run)",
+                "kernel": "k_step_multi<1> (write-through state port)",
                 "bytes_per_env_step": BYTES_PER_ENV_STEP,
-                "kernel_us": kern_ms * 1e3,
+                "kernel_us_per_tick": kern_ms * 1e3,
             },
             "cpu_baseline": cpu,
             "episodes": counters,
+            "step_variants": variants,
             "full_contract_tick": full,
             "rollout_random": rollout,
             "large_batch": large,

@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define SK_ABI_VERSION 4
+#define SK_ABI_VERSION 5
 
 enum {
   SK_OK = 0,
@@ -118,12 +118,15 @@ int sk_env_attach(sk_env** out, const sk_state_view* view, int64_t env_offset, u
 int sk_env_destroy(sk_env* env);
 int sk_env_get_view(const sk_env* env, sk_state_view* out);
 /* Device counter slots (sk_env_counter_slots x sk_counters, device memory)
- * the step kernels accumulate into. */
+ * the step kernels accumulate into.  A raw-slot reader must sum all
+ * sk_env_counter_slots of them (one line per step-kernel wave), not
+ * SK_COUNTER_SLOTS; sk_env_read_counters does that on device. */
 int sk_env_counters_ptr(const sk_env* env, sk_counters** out);
 /* Number of counter slots at sk_env_counters_ptr (1 for the CPU backend). */
 int sk_env_counter_slots(const sk_env* env, int64_t* out);
-/* Copy the episode counters to host memory (synchronises `stream`), and
- * zero them (stream-ordered). */
+/* Copy the episode counters to host memory (synchronises `stream`; the
+ * slots are summed on device by one workgroup first, so 32 bytes cross
+ * PCIe whatever n_envs is), and zero them (stream-ordered). */
 int sk_env_read_counters(sk_env* env, sk_counters* host_out, void* stream);
 int sk_env_clear_counters(sk_env* env, void* stream);
 /* Host-side RNG step counter: every step / reset call consumes one value
@@ -206,6 +209,21 @@ int sk_env_observe(sk_env* env, float* obs, float* reward, int32_t reward_kind, 
 int sk_env_step(sk_env* env, const float* actions, float* obs, float* reward, int32_t reward_kind,
                 uint8_t* done, uint8_t* winner, int32_t tick_limit, int32_t auto_reset,
                 int32_t random_positions, float* obs_reset, void* stream);
+
+/* n_ticks learner ticks of the step-only contract in ONE launch (ABI 5):
+ * equal, bit for bit, to n_ticks calls of sk_env_step(obs = reward =
+ * obs_reset = NULL) where tick t acts on slab (slab0 + t) % ring_slabs of
+ * `actions` (float[ring_slabs][2][N][2], an HBM ring of per-tick action
+ * slabs) and writes done / winner (uint8[N] each, nullable) at
+ * done + t * out_stride (out_stride 0: every tick overwrites one row;
+ * n_envs: a [n_ticks][N] record).  Every tick loads and stores each game's
+ * state planes (the per-tick loop of SkillshotLearner.py:302-318 with the
+ * random policy, do_actions :206-213 + game_tick SkillshotGame.py:115-122 +
+ * done :302 + random restart :291); only the dispatch boundary is shared.
+ * Advances the step counter by n_ticks; accumulates the episode counters. */
+int sk_env_step_multi(sk_env* env, const float* actions, int64_t ring_slabs, int64_t slab0, int32_t n_ticks,
+                      uint8_t* done, uint8_t* winner, int64_t out_stride, int32_t tick_limit, int32_t auto_reset,
+                      int32_t random_positions, void* stream);
 
 /* Random-policy actions (config 2 synthetic input): float[n_ticks][2][N][2]
  * uniform in [-1,1) from Philox4x32-10 keyed (seed, global env id, step

@@ -47,6 +47,8 @@ struct sk_env {
   // (player per lane), 2 = k_step_fast (fp32 trig + exact fallback); -1 = auto
   // (SK_STEP_VARIANT overrides)
   int step_variant;
+  // k_step_multi state port: 1 write-through (default), 0 plain (SK_MULTI_POLICY)
+  int multi_policy;
   // device = -1: the CPU backend (sk_host.cpp) owns the games; every entry
   // point below forwards to it and takes host pointers
   skh::Host* host;
@@ -671,6 +673,170 @@ __global__ void __launch_bounds__(kStepBlock) k_rollout_random(RolloutArgs a, Cf
   }
 }
 
+// ------------------------------------------------------------------ multi-tick step
+// k_step_multi: n_ticks learner ticks of the step-only contract (sk_env_step
+// with obs/reward NULL, n_ticks times) in ONE launch, one lane per game.  Each
+// wave loops over the ticks; every tick it loads its 64 games' state, reads
+// that tick's action slab from the HBM ring, runs k_step's tick, writes done
+// / winner and stores the state back — so the 193 B per env-step of the
+// contract move every tick, as in one k_step launch per tick,
+// but the dependent-dispatch boundary (~1.7 us, MI355X_MICROARCH.md
+// "boundary") and the end-of-dispatch L2 write-back are paid once per launch
+// instead of once per tick.  Games are independent (SkillshotGame.py:58-94
+// is intra-game), so no wave waits for another: no grid barrier.  The RNG
+// step of tick t is step0 + t, as n_ticks sk_env_step calls would use.
+//
+// State port (SK_MULTI_POLICY / the `POL` template):
+//   0  plain loads / stores, as k_step (a wave's own stores stay in its XCD's
+//      L2, so the next tick's reload is an L2 hit),
+//   1  write-through: stores `sc1` (the line leaves L2 and is dropped,
+//      MI355X_MICROARCH.md "stores of each flavour") and loads `sc1` (bypass
+//      L1), so every tick's 176 state bytes cross the L2/fabric boundary like
+//      k_step's between launches.  Through buffer instructions (the cache
+//      policy is an operand and the compiler tracks the waits) over ONE
+//      resource whose base is the lowest plane (the host checks that every
+//      plane lies within 4 GiB of it): one resource per plane spilled SGPRs.
+typedef int skb4i __attribute__((ext_vector_type(4)));
+typedef int skb2i __attribute__((ext_vector_type(2)));
+typedef double skb2d __attribute__((ext_vector_type(2)));
+
+struct MultiArgs {
+  View v;
+  int64_t n;
+  const float2* actions;  // ring: [ring][2][N] float2
+  int64_t ring;           // slabs in the ring
+  int64_t slab0;          // slab of tick 0 (< ring)
+  int n_ticks;
+  uint8_t* done;          // tick t writes done + t * out_stride (nullable)
+  uint8_t* winner;        // same (nullable)
+  int64_t out_stride;
+  int tick_limit;
+  int auto_reset;
+  int random_positions;
+  uint64_t seed;
+  int64_t env_offset;
+  StepRef step;
+  sk_counters* ctr;
+  const char* base;       // POL 1: the lowest plane; off[k] = plane k - base (pos, rot, qpos, qrot, qcdage, misc)
+  uint32_t off[6];
+};
+
+template <int POL>
+__device__ __forceinline__ void load_env_port(const MultiArgs& a, __amdgpu_buffer_rsrc_t r, int64_t i, Env& e) {
+  if constexpr (POL == 0) {
+    load_env(a.v, i, e);
+  } else {
+    const uint32_t o16 = (uint32_t)i * 16u, o8 = (uint32_t)i * 8u;
+    const skb4i p = __builtin_amdgcn_raw_buffer_load_b128(r, o16 + a.off[0], 0, 16);
+    const skb4i rb = __builtin_amdgcn_raw_buffer_load_b128(r, o16 + a.off[1], 0, 16);
+    const skb4i q = __builtin_amdgcn_raw_buffer_load_b128(r, o16 + a.off[2], 0, 16);
+    const skb4i qb = __builtin_amdgcn_raw_buffer_load_b128(r, o16 + a.off[3], 0, 16);
+    const skb4i ca = __builtin_amdgcn_raw_buffer_load_b128(r, o16 + a.off[4], 0, 16);
+    const skb2i m = __builtin_amdgcn_raw_buffer_load_b64(r, o8 + a.off[5], 0, 16);
+    const skb2d rr = __builtin_bit_cast(skb2d, rb), qr = __builtin_bit_cast(skb2d, qb);
+    decode_env(EnvRaw{make_int4(p.x, p.y, p.z, p.w), make_double2(rr.x, rr.y), make_int4(q.x, q.y, q.z, q.w),
+                      make_double2(qr.x, qr.y), make_int4(ca.x, ca.y, ca.z, ca.w), make_int2(m.x, m.y)},
+               e);
+  }
+}
+
+// store_env_q through the port: the projectile-rotation plane only where it
+// changed (a projectile fired, or the game restarted)
+template <int POL>
+__device__ __forceinline__ void store_env_port(const MultiArgs& a, __amdgpu_buffer_rsrc_t r, int64_t i, const Env& e,
+                                               double q_old0, double q_old1) {
+  if constexpr (POL == 0) {
+    store_env_q(a.v, i, e, q_old0, q_old1);
+  } else {
+    const uint32_t o16 = (uint32_t)i * 16u, o8 = (uint32_t)i * 8u;
+    const unsigned f = (unsigned)(e.qvalid[0] & 0xff) | ((unsigned)(e.qvalid[1] & 0xff) << 8) |
+                       ((unsigned)(e.live & 0xff) << 16) | ((unsigned)(e.winner & 0xff) << 24);
+    const bool qrot_changed = (int)(__double_as_longlong(e.qrot[0]) != __double_as_longlong(q_old0)) |
+                              (int)(__double_as_longlong(e.qrot[1]) != __double_as_longlong(q_old1));
+    __builtin_amdgcn_raw_buffer_store_b128((skb4i){e.px[0], e.py[0], e.px[1], e.py[1]}, r, o16 + a.off[0], 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(skb4i, (skb2d){e.rot[0], e.rot[1]}), r,
+                                           o16 + a.off[1], 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b128((skb4i){e.qx[0], e.qy[0], e.qx[1], e.qy[1]}, r, o16 + a.off[2], 0, 16);
+    if (qrot_changed)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(skb4i, (skb2d){e.qrot[0], e.qrot[1]}), r,
+                                             o16 + a.off[3], 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b128((skb4i){e.qcd[0], e.qage[0], e.qcd[1], e.qage[1]}, r, o16 + a.off[4], 0,
+                                           16);
+    __builtin_amdgcn_raw_buffer_store_b64((skb2i){e.ticks, (int)f}, r, o8 + a.off[5], 0, 16);
+  }
+}
+
+template <int POL>
+__global__ void __launch_bounds__(kStepBlock) k_step_multi(MultiArgs a, Cfg c) {
+  const int64_t i = (int64_t)blockIdx.x * kStepBlock + threadIdx.x;
+  const bool in = i < a.n;
+  WaveCtr wc = ctr_load(a.ctr);
+  const uint64_t step0 = step_read(a.step);
+  step_advance(a.step, step0, (uint64_t)a.n_ticks);
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(a.base), (short)0, -1, 0x00020000);
+  // lanes past the end of a ragged batch load game 0 and store nothing
+  const int64_t ic = in ? i : 0;
+  const bool early = a.random_positions && a.n >= kEarlyDrawMinEnvs;
+  unsigned n_done = 0, n_h1 = 0, n_h2 = 0, t_sum = 0;  // this lane's (t_sum < n_ticks * tick_limit)
+  int64_t slab = a.slab0;
+  for (int t = 0; t < a.n_ticks; ++t) {
+    const uint64_t step = step0 + (uint64_t)t;
+    Env e;
+    // state first, actions last (k_step's order): the players' sincos of the
+    // old rotations run while the action slab arrives from HBM
+    load_env_port<POL>(a, r, ic, e);
+    const double q_old0 = e.qrot[0], q_old1 = e.qrot[1];
+    __builtin_amdgcn_sched_barrier(0);
+    const float2* ap = a.actions + slab * 2 * a.n;
+    const float2 a0 = load_action(ap + ic);
+    const float2 a1 = load_action(ap + a.n + ic);
+    __builtin_amdgcn_sched_barrier(0);
+    U4 ru = {0u, 0u, 0u, 0u};
+    if (early) {  // the restart's draw under the loads (k_step)
+      ru = draw4(a.seed, (uint64_t)(a.env_offset + i), step, 1u);
+      asm volatile("" : "+v"(ru.x), "+v"(ru.y), "+v"(ru.z), "+v"(ru.w));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    bool k0, k1;
+    const sktrig::SinCos m0 = sktrig::sincos_bf(e.rot[0], &k0);
+    const sktrig::SinCos m1 = sktrig::sincos_bf(e.rot[1], &k1);
+    tick_env_m(c, e, m0, m1, k0 & k1, (double)a0.x, (double)a0.y, (double)a1.x, (double)a1.y);
+    // every load consumed (the slot's, issued first, with them): without this
+    // the waitcnt pass, its tracking lost across the loop, drains every store
+    // before the final counter store
+    ctr_settle(wc);
+    const bool d = in && ((!e.live) || (e.ticks >= a.tick_limit));  // SkillshotLearner.py:302
+    if (in) {
+      if (a.done) a.done[(int64_t)t * a.out_stride + i] = (uint8_t)d;
+      if (a.winner) a.winner[(int64_t)t * a.out_stride + i] = (uint8_t)e.winner;
+    }
+    // episode counters: per lane here, one wave reduction after the loop
+    n_done += d;
+    n_h1 += d && e.winner == 1;
+    n_h2 += d && e.winner == 2;
+    t_sum += d ? (unsigned)e.ticks : 0u;
+    if (d && a.auto_reset) {
+      if (a.random_positions) {
+        if (early) reset_random_u(c, e, ru);
+        else reset_random(c, e, a.seed, (uint64_t)(a.env_offset + i), step);
+      } else {
+        reset_fixed(c, e);
+      }
+    }
+    if (in) store_env_port<POL>(a, r, i, e, q_old0, q_old1);
+    slab = slab + 1 == a.ring ? 0 : slab + 1;
+  }
+  if (a.ctr) {
+    uint64_t v[4] = {n_done, n_h1, n_h2, t_sum};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off, 64);
+    ctr_store(a.ctr, wc, v[0], v[1], v[2], v[3]);
+  }
+}
+
 __global__ void __launch_bounds__(kBlock) k_gen_actions(float4* out, int64_t n, int n_ticks, uint64_t seed,
                                                         int64_t env_offset, StepRef sref) {
   const uint64_t step0 = step_read(sref);
@@ -906,6 +1072,8 @@ static int make_env(sk_env** out, const sk_state_view* view, int32_t n, int64_t 
   e->parity = 0;
   e->step_variant = -1;
   if (const char* sv = std::getenv("SK_STEP_VARIANT")) e->step_variant = std::atoi(sv);
+  e->multi_policy = 1;  // write-through (the contract bytes leave L2 every tick)
+  if (const char* mp = std::getenv("SK_MULTI_POLICY")) e->multi_policy = std::atoi(mp);
   if (view) {
     if (view->n_envs != n || !view->pos || !view->rot || !view->qpos || !view->qrot || !view->qcdage ||
         !view->misc) {
@@ -1015,25 +1183,36 @@ int sk_env_counter_slots(const sk_env* e, int64_t* out) {
   return SK_OK;
 }
 
+// one workgroup sums every wave's slot line into a 32-byte result (ADVICE r02:
+// read_counters copied the O(n) slot array to the host)
+__global__ void __launch_bounds__(kBlock) k_sum_counters(const sk_counters* slots, int64_t ns, sk_counters* out) {
+  __shared__ unsigned long long part[4][kBlock];
+  unsigned long long s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+  for (int64_t k = threadIdx.x; k < ns; k += kBlock) {
+    const sk_counters v = slots[k];
+    s0 += v.dones; s1 += v.hits_p1; s2 += v.hits_p2; s3 += v.ticks_sum;
+  }
+  part[0][threadIdx.x] = s0; part[1][threadIdx.x] = s1; part[2][threadIdx.x] = s2; part[3][threadIdx.x] = s3;
+  __syncthreads();
+  for (int w = kBlock / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w)
+      for (int j = 0; j < 4; ++j) part[j][threadIdx.x] += part[j][threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out = sk_counters{part[0][0], part[1][0], part[2][0], part[3][0]};
+}
+
 int sk_env_read_counters(sk_env* e, sk_counters* out, void* stream) {
   if (!e || !out) return fail(SK_EINVAL, "NULL argument");
   if (e->host) {
     *out = e->host->ctr;
     return SK_OK;
   }
-  const int64_t ns = counter_slots(e->n);
-  std::vector<sk_counters> slots((size_t)ns);
-  HIP_TRY(hipMemcpyAsync(slots.data(), e->d_counters, (size_t)ns * sizeof(sk_counters), hipMemcpyDeviceToHost,
-                         (hipStream_t)stream));
+  sk_counters* d_sum = reinterpret_cast<sk_counters*>(e->d_aux + 64);  // step slots use bytes 0-15
+  k_sum_counters<<<1, kBlock, 0, (hipStream_t)stream>>>(e->d_counters, counter_slots(e->n), d_sum);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out, d_sum, sizeof(sk_counters), hipMemcpyDeviceToHost, (hipStream_t)stream));
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
-  sk_counters sum = {0, 0, 0, 0};
-  for (int64_t k = 0; k < ns; ++k) {
-    sum.dones += slots[k].dones;
-    sum.hits_p1 += slots[k].hits_p1;
-    sum.hits_p2 += slots[k].hits_p2;
-    sum.ticks_sum += slots[k].ticks_sum;
-  }
-  *out = sum;
   return SK_OK;
 }
 
@@ -1250,6 +1429,68 @@ int sk_env_step(sk_env* e, const float* actions, float* obs, float* reward, int3
     k_step<true><<<step_grid(e->n), kStepBlock, 0, (hipStream_t)stream>>>(a, e->dcfg);
   else
     k_step<false><<<step_grid(e->n), kStepBlock, 0, (hipStream_t)stream>>>(a, e->dcfg);
+  SK_LAUNCH_CHECK();
+  e->parity ^= 1;
+  return SK_OK;
+}
+
+int sk_env_step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64_t slab0, int32_t n_ticks,
+                      uint8_t* done, uint8_t* winner, int64_t out_stride, int32_t tick_limit, int32_t auto_reset,
+                      int32_t random_positions, void* stream) {
+  SK_CHECK_ENV(e);
+  if (!actions) return fail(SK_EINVAL, "actions is NULL");
+  if (((uintptr_t)actions) & 7) return fail(SK_EINVAL, "actions must be 8-byte aligned");
+  if (n_ticks <= 0 || ring_slabs <= 0 || slab0 < 0 || slab0 >= ring_slabs || out_stride < 0)
+    return fail(SK_EINVAL, "bad n_ticks / ring_slabs / slab0 / out_stride");
+  if (e->host) {
+    const int64_t slab_floats = 4 * (int64_t)e->n;
+    for (int32_t t = 0; t < n_ticks; ++t) {
+      const int64_t s = (slab0 + t) % ring_slabs;
+      skh::step(*e->host, actions + s * slab_floats, nullptr, nullptr, SK_REWARD_LOOKING,
+                done ? done + (int64_t)t * out_stride : nullptr, winner ? winner + (int64_t)t * out_stride : nullptr,
+                tick_limit, auto_reset, random_positions, nullptr);
+    }
+    return SK_OK;
+  }
+  if ((int64_t)e->n > (int64_t)0x7fffffff / 16) return fail(SK_EINVAL, "n_envs too large for k_step_multi");
+  MultiArgs a;
+  a.v = e->view;
+  a.n = e->n;
+  a.actions = reinterpret_cast<const float2*>(actions);
+  a.ring = ring_slabs;
+  a.slab0 = slab0;
+  a.n_ticks = n_ticks;
+  a.done = done;
+  a.winner = winner;
+  a.out_stride = out_stride;
+  a.tick_limit = tick_limit;
+  a.auto_reset = auto_reset;
+  a.random_positions = random_positions;
+  a.seed = e->seed;
+  a.env_offset = e->env_offset;
+  a.step = StepRef{e->d_step, e->parity};
+  a.ctr = e->d_counters;
+  a.base = nullptr;
+  for (int k = 0; k < 6; ++k) a.off[k] = 0;
+  int pol = e->multi_policy;
+  if (pol == 1) {  // one buffer resource over the planes: they must lie within 4 GiB of the lowest
+    const char* p[6] = {(const char*)e->hview.pos, (const char*)e->hview.rot, (const char*)e->hview.qpos,
+                        (const char*)e->hview.qrot, (const char*)e->hview.qcdage, (const char*)e->hview.misc};
+    const char* lo = p[0];
+    for (int k = 1; k < 6; ++k) lo = p[k] < lo ? p[k] : lo;
+    bool ok = true;
+    for (int k = 0; k < 6; ++k) {
+      const uint64_t end = (uint64_t)(p[k] - lo) + (uint64_t)e->n * (k == 5 ? 8u : 16u);
+      ok &= end <= 0xffffffffull;
+      a.off[k] = (uint32_t)(p[k] - lo);
+    }
+    if (!ok) return fail(SK_EINVAL, "SK_MULTI_POLICY=1 needs the state planes within 4 GiB of each other");
+    a.base = lo;
+  }
+  if (pol == 1)
+    k_step_multi<1><<<step_grid(e->n), kStepBlock, 0, (hipStream_t)stream>>>(a, e->dcfg);
+  else
+    k_step_multi<0><<<step_grid(e->n), kStepBlock, 0, (hipStream_t)stream>>>(a, e->dcfg);
   SK_LAUNCH_CHECK();
   e->parity ^= 1;
   return SK_OK;

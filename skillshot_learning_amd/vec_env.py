@@ -171,15 +171,18 @@ class VecSkillshotGame:
         f = self.misc[:, 1]
         return torch.stack([(f & 0xFF), (f >> 8) & 0xFF], -1).to(torch.bool)
 
-    def counters(self):
+    def counters(self, stream=None):
         """Episode counters (dones, hits by id, tick sum) accumulated on device
-        by the step kernels' wavefront ballots."""
+        by the step kernels' wavefront ballots (read on `stream`, default
+        torch's current one: pass the stream the steps ran on)."""
         c = _capi.SkCounters()
-        check(self._L.sk_env_read_counters(self._h, ctypes.byref(c), self._stream()))
+        check(self._L.sk_env_read_counters(self._h, ctypes.byref(c), stream if stream is not None else self._stream()))
         return dict(dones=c.dones, hits_p1=c.hits_p1, hits_p2=c.hits_p2, ticks_sum=c.ticks_sum)
 
-    def clear_counters(self):
-        check(self._L.sk_env_clear_counters(self._h, self._stream()))
+    def clear_counters(self, stream=None):
+        """Zero the episode counters, ordered on `stream` (default torch's
+        current one: pass the stream the steps run on)."""
+        check(self._L.sk_env_clear_counters(self._h, stream if stream is not None else self._stream()))
 
     # ------------------------------------------------------------ reference API
     def reset(self, mask=None, random_positions=None):
@@ -272,6 +275,41 @@ class VecSkillshotGame:
         check(self._L.sk_env_step(self._h, actions_ptr, obs_ptr, reward_ptr, 0, done_ptr, winner_ptr,
                                   self.tick_limit, int(bool(auto_reset)), int(self.random_positions), None,
                                   stream if stream is not None else self._stream()))
+
+    def step_multi(self, actions, n_ticks=None, slab0=0, done=None, winner=None, record=False, auto_reset=True,
+                   stream=None):
+        """n_ticks step-only learner ticks (SkillshotLearner.py:302-318: do_actions x2,
+        game_tick, done, random restart) in ONE launch (sk_env_step_multi).
+
+        actions: float32 [R, 2, N, 2], a ring of R per-tick slabs; tick t acts on
+        slab (slab0 + t) % R.  n_ticks defaults to R.  done / winner: u8 [N]
+        (the last tick's) or, with record=True, [n_ticks, N] (every tick's).
+        Equal bit for bit to n_ticks `step(actions[s], obs=False)` calls."""
+        a = torch.as_tensor(actions, device=self.device)
+        if a.dtype != torch.float32 or not a.is_contiguous() or a.dim() != 4 or tuple(a.shape[1:]) != (2, self.n, 2):
+            raise ValueError(f"actions must be contiguous float32 [R, 2, {self.n}, 2]")
+        R = a.shape[0]
+        T = R if n_ticks is None else int(n_ticks)
+        rows = T if record else 1
+        if done is None:
+            done = torch.empty((rows, self.n), dtype=torch.uint8, device=self.device)
+        if winner is None:
+            winner = torch.empty((rows, self.n), dtype=torch.uint8, device=self.device)
+        for t in (done, winner):
+            if t.numel() < rows * self.n or t.dtype != torch.uint8 or not t.is_contiguous():
+                raise ValueError(f"done / winner must be contiguous uint8 with {rows} x {self.n} elements")
+        check(self._L.sk_env_step_multi(self._h, _ptr(a), R, int(slab0) % R, T, _ptr(done), _ptr(winner),
+                                        self.n if record else 0, self.tick_limit, int(bool(auto_reset)),
+                                        int(self.random_positions), stream if stream is not None else self._stream()))
+        return done.view(rows, self.n) if record else done.view(-1)[: self.n], \
+            winner.view(rows, self.n) if record else winner.view(-1)[: self.n]
+
+    def step_multi_raw(self, actions_ptr, ring, slab0, n_ticks, done_ptr=None, winner_ptr=None, out_stride=0,
+                       auto_reset=True, stream=None):
+        """Pointer-level sk_env_step_multi (bench / graph capture; no allocation)."""
+        check(self._L.sk_env_step_multi(self._h, actions_ptr, int(ring), int(slab0), int(n_ticks), done_ptr,
+                                        winner_ptr, int(out_stride), self.tick_limit, int(bool(auto_reset)),
+                                        int(self.random_positions), stream if stream is not None else self._stream()))
 
     def gen_random_actions(self, n_ticks, out=None):
         """Random-policy actions float32 [n_ticks, 2, N, 2] (config 2 synthetic input)."""

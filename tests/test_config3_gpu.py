@@ -2,6 +2,8 @@
 fused env step with obs/reward/auto-reset, 1 M-row replay ring in HBM,
 minibatch 256, one critic + actor update per tick), replayed as captured
 learner ticks (SkillshotLearner.tick_graph) for 200+ ticks."""
+import ctypes
+
 import pytest
 import torch
 
@@ -29,7 +31,7 @@ def test_config3_tick_graph(learner_mod, exploration):
     calls0 = int(L.ddpg.drop_calls)
     step0 = g.step_counter
     w0 = [p.clone() for p in L.model_actor.parameters()]
-    g.clear_counters()
+    g.clear_counters(stream=ctypes.c_void_p(tg.stream.cuda_stream))  # ordered after the capture's warm-up ticks
     tg.run(100)  # 200 ticks
     torch.cuda.synchronize()
     ticks = 200
@@ -53,6 +55,8 @@ def test_config3_tick_graph(learner_mod, exploration):
     assert any((p - q).abs().max() > 0 for p, q in zip(L.model_actor.parameters(), w0))
     c = g.counters()
     assert c["dones"] > 0 and c["hits_p1"] + c["hits_p2"] <= c["dones"]
+    # only episodes that ended inside the 200 counted ticks: each lasted <= 200 + the warm-up
+    assert c["ticks_sum"] <= c["dones"] * (ticks + 8)
     # the replay rows hold finite observations in the reference's ranges
     rows = L.replay.buf[:min(L.replay.size, 65536)]
     assert bool(torch.isfinite(rows).all())

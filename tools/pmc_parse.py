@@ -39,15 +39,20 @@ def main():
     p.add_argument("--envs", type=int, default=65536)
     p.add_argument("--bytes-per-env", type=int, default=193)
     p.add_argument("--write", default=None)
+    p.add_argument("--ticks-per-launch", type=int, default=1, help="k_step_multi: ticks per dispatch")
     a = p.parse_args()
     mean, count = load(a.dirs, a.kernel)
     out = {"kernel": a.kernel, "envs": a.envs, "counters_mean_per_dispatch": mean, "dispatches": count}
     if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
         fetch = mean["FETCH_SIZE"] * 1024 * 2
         write = mean["WRITE_SIZE"] * 1024
+        T = a.ticks_per_launch
         out.update(fetch_bytes_corrected=fetch, write_bytes=write, hbm_bytes_per_launch=fetch + write,
-                   algorithmic_bytes_per_launch=a.bytes_per_env * a.envs,
-                   traffic_over_algorithmic=(fetch + write) / (a.bytes_per_env * a.envs))
+                   algorithmic_bytes_per_launch=a.bytes_per_env * a.envs * T,
+                   traffic_over_algorithmic=(fetch + write) / (a.bytes_per_env * a.envs * T))
+        if T > 1:
+            out.update(ticks_per_launch=T, hbm_bytes_per_tick=(fetch + write) / T,
+                       algorithmic_bytes_per_tick=a.bytes_per_env * a.envs)
     print(json.dumps(out, indent=1))
     if a.write:
         os.makedirs(os.path.dirname(a.write), exist_ok=True)

@@ -1,4 +1,4 @@
-"""Eager k_step launches for rocprofv3 --pmc passes (graph replay is avoided so
+"""Eager k_step (or, --multi T, k_step_multi) launches for rocprofv3 --pmc passes (graph replay is avoided so
 every dispatch is attributed).  Same workload as bench.py (random policy,
 pre-generated actions ring, done output, random auto-reset).
 
@@ -21,6 +21,7 @@ def main():
     p.add_argument("--launches", type=int, default=300)
     p.add_argument("--ring", type=int, default=300)
     p.add_argument("--obs", action="store_true")
+    p.add_argument("--multi", type=int, default=0, help="k_step_multi launches of this many ticks instead")
     a = p.parse_args()
     from skillshot_learning_amd import VecSkillshotGame
     n = a.envs
@@ -31,6 +32,14 @@ def main():
     o = torch.empty((2, n, 12), dtype=torch.float32, device="cuda") if a.obs else None
     r = torch.empty((2, n), dtype=torch.float32, device="cuda") if a.obs else None
     torch.cuda.synchronize()
+    if a.multi:
+        slab = 0
+        for _ in range(a.launches):
+            env.step_multi_raw(ctypes.c_void_p(acts.data_ptr()), a.ring, slab, a.multi, ctypes.c_void_p(done.data_ptr()))
+            slab = (slab + a.multi) % a.ring
+        torch.cuda.synchronize()
+        print("multi launches", a.launches, "x", a.multi, "ticks, envs", n)
+        return
     for t in range(a.launches):
         env.step_raw(ctypes.c_void_p(acts.data_ptr() + (t % a.ring) * 16 * n), ctypes.c_void_p(done.data_ptr()),
                      obs_ptr=None if o is None else ctypes.c_void_p(o.data_ptr()),
