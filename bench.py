@@ -150,6 +150,11 @@ class TickGraphs:
 _HIP = None
 
 
+def _capi_check(rc):
+    from skillshot_learning_amd import _capi
+    _capi.check(rc)
+
+
 def _hip():
     global _HIP
     if _HIP is None:
@@ -303,35 +308,40 @@ def timed_multi(dev, n, seed, env_offset, tick_limit, k, warmup, ring, world, pe
     sp = ctypes.c_void_p(st.cuda_stream)
     done = torch.empty(n, dtype=torch.uint8, device=dev)
     ap, dp = ctypes.c_void_p(acts.data_ptr()), ctypes.c_void_p(done.data_ptr())
+    # the bound C entry point itself (sk_env_step_multi): no Python wrapper in
+    # the timed region (tools/short_run_multi.py)
+    fn, h, lim, rp = env._L.sk_env_step_multi, env._h, env.tick_limit, int(env.random_positions)
     slab = 0
 
     def run(m):
         nonlocal slab
         while m > 0:
             t = min(m, per_launch)
-            env.step_multi_raw(ap, ring, slab, t, dp, None, 0, stream=sp)
+            rc = fn(h, ap, ring, slab, t, dp, None, 0, lim, 1, rp, sp)
+            if rc:
+                _capi_check(rc)
             if trace is not None:
                 trace.append(("slabs", slab, t))
             slab = (slab + t) % ring
             m -= t
 
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)  # torch creates the HIP events at their first record: not inside the timed region
     run(1)  # the first launch loads the code object
+    e1.record(st)
     st.synchronize()
     env.clear_counters(stream=sp)
     if trace is not None:
         trace.append(("clear",))
     run(warmup)
     st.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    with torch.cuda.stream(st):
-        e0.record()
+    e0.record(st)  # (a `with torch.cuda.stream` block costs ~9 us of host time per record)
     run(k)
-    with torch.cuda.stream(st):
-        e1.record()
+    e1.record(st)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

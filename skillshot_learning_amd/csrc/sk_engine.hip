@@ -49,6 +49,8 @@ struct sk_env {
   int step_variant;
   // k_step_multi state port: 1 write-through (default), 0 plain (SK_MULTI_POLICY)
   int multi_policy;
+  // k_step_multi geometry: -1 auto, 0 lane per game, 1 player per lane (SK_MULTI_SPLIT)
+  int multi_split;
   // device = -1: the CPU backend (sk_host.cpp) owns the games; every entry
   // point below forwards to it and takes host pointers
   skh::Host* host;
@@ -85,7 +87,11 @@ static constexpr int64_t kFastStepMaxEnvs = 786432;
 // 3.58 vs 3.51 (profiles/r02_step_small_ab.jsonl) -- the per-GPU size of the
 // metric's 65,536 games over 8 ranks
 static constexpr int64_t kSplitStepMaxEnvs = 8192;
-static constexpr int64_t kEarlyDrawMinEnvs = 32768;  // k_step: restart draw under the loads
+static constexpr int64_t kEarlyDrawMinEnvs = 32768;
+// k_step_multi: two lanes per game up to this many games.  Write-through
+// port, 400 ticks per launch: 8,192 games 1.59 vs 1.85 us per tick, 32,768
+// 1.80 vs 2.02, but 65,536 2.59 vs 2.36 (profiles/r03c_multi_split_sweep.jsonl)
+static constexpr int64_t kSplitMultiMaxEnvs = 32768;  // k_step: restart draw under the loads
 // Counter slots per wave: 4 x 32 B = one 128-B line, so no two waves (on
 // different XCDs, whose L2s write partial lines back at the end of the
 // dispatch) share a line: 0.27 us less per 65,536-game k_step than packed
@@ -721,6 +727,7 @@ struct MultiArgs {
   uint32_t off[6];
 };
 
+
 template <int POL>
 __device__ __forceinline__ void load_env_port(const MultiArgs& a, __amdgpu_buffer_rsrc_t r, int64_t i, Env& e) {
   if constexpr (POL == 0) {
@@ -766,69 +773,245 @@ __device__ __forceinline__ void store_env_port(const MultiArgs& a, __amdgpu_buff
   }
 }
 
+struct MultiLane {
+  int64_t i, ic;  // game; the game this lane loads (lanes past the end of a ragged batch: game 0, no stores)
+  bool in, early;
+  unsigned n_done, n_h1, n_h2, t_sum;  // this lane's episode counts (t_sum < n_ticks * tick_limit)
+};
+
+// one tick of k_step_multi on slab `slab` of the action ring.  State first,
+// actions last (k_step's order: the players' sincos of the old rotations
+// run while the slab arrives).  Prefetching the slab a tick ahead was slower
+// (65,536 games 2.51 vs 2.36 us per tick, 8,192 split 1.71 vs 1.59;
+// profiles/r03d_multi_prefetch_sweep.jsonl): vector memory returns in issue
+// order, so the next tick's state waited for the prefetched HBM loads anyway.
+template <int POL>
+__device__ __forceinline__ void multi_tick(const MultiArgs& a, const Cfg& c, __amdgpu_buffer_rsrc_t r, MultiLane& L,
+                                           WaveCtr& wc, int t, uint64_t step, int64_t slab) {
+  Env e;
+  load_env_port<POL>(a, r, L.ic, e);
+  const double q_old0 = e.qrot[0], q_old1 = e.qrot[1];
+  __builtin_amdgcn_sched_barrier(0);
+  float2 acts[2];
+  acts[0] = load_action(a.actions + slab * 2 * a.n + L.ic);
+  acts[1] = load_action(a.actions + slab * 2 * a.n + a.n + L.ic);
+  __builtin_amdgcn_sched_barrier(0);
+  U4 ru = {0u, 0u, 0u, 0u};
+  if (L.early) {  // the restart's draw under the loads (k_step)
+    ru = draw4(a.seed, (uint64_t)(a.env_offset + L.i), step, 1u);
+    asm volatile("" : "+v"(ru.x), "+v"(ru.y), "+v"(ru.z), "+v"(ru.w));
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  bool k0, k1;
+  const sktrig::SinCos m0 = sktrig::sincos_bf(e.rot[0], &k0);
+  const sktrig::SinCos m1 = sktrig::sincos_bf(e.rot[1], &k1);
+  tick_env_m(c, e, m0, m1, k0 & k1, (double)acts[0].x, (double)acts[0].y, (double)acts[1].x, (double)acts[1].y);
+  // every load of this tick consumed (the counter slot's, issued first, with
+  // them): without this the waitcnt pass, its tracking lost across the loop,
+  // drains every store before the final counter store
+  ctr_settle(wc);
+  const bool d = L.in && ((!e.live) || (e.ticks >= a.tick_limit));  // SkillshotLearner.py:302
+  if (L.in) {
+    if (a.done) a.done[(int64_t)t * a.out_stride + L.i] = (uint8_t)d;
+    if (a.winner) a.winner[(int64_t)t * a.out_stride + L.i] = (uint8_t)e.winner;
+  }
+  L.n_done += d;
+  L.n_h1 += d && e.winner == 1;
+  L.n_h2 += d && e.winner == 2;
+  L.t_sum += d ? (unsigned)e.ticks : 0u;
+  if (d && a.auto_reset) {
+    if (a.random_positions) {
+      if (L.early) reset_random_u(c, e, ru);
+      else reset_random(c, e, a.seed, (uint64_t)(a.env_offset + L.i), step);
+    } else {
+      reset_fixed(c, e);
+    }
+  }
+  if (L.in) store_env_port<POL>(a, r, L.i, e, q_old0, q_old1);
+}
+
 template <int POL>
 __global__ void __launch_bounds__(kStepBlock) k_step_multi(MultiArgs a, Cfg c) {
-  const int64_t i = (int64_t)blockIdx.x * kStepBlock + threadIdx.x;
-  const bool in = i < a.n;
+  MultiLane L;
+  L.i = (int64_t)blockIdx.x * kStepBlock + threadIdx.x;
+  L.in = L.i < a.n;
+  L.ic = L.in ? L.i : 0;
+  L.early = a.random_positions && a.n >= kEarlyDrawMinEnvs;
+  L.n_done = L.n_h1 = L.n_h2 = L.t_sum = 0;
   WaveCtr wc = ctr_load(a.ctr);
   const uint64_t step0 = step_read(a.step);
   step_advance(a.step, step0, (uint64_t)a.n_ticks);
   const __amdgpu_buffer_rsrc_t r =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(a.base), (short)0, -1, 0x00020000);
-  // lanes past the end of a ragged batch load game 0 and store nothing
-  const int64_t ic = in ? i : 0;
-  const bool early = a.random_positions && a.n >= kEarlyDrawMinEnvs;
-  unsigned n_done = 0, n_h1 = 0, n_h2 = 0, t_sum = 0;  // this lane's (t_sum < n_ticks * tick_limit)
   int64_t slab = a.slab0;
   for (int t = 0; t < a.n_ticks; ++t) {
-    const uint64_t step = step0 + (uint64_t)t;
-    Env e;
-    // state first, actions last (k_step's order): the players' sincos of the
-    // old rotations run while the action slab arrives from HBM
-    load_env_port<POL>(a, r, ic, e);
-    const double q_old0 = e.qrot[0], q_old1 = e.qrot[1];
-    __builtin_amdgcn_sched_barrier(0);
-    const float2* ap = a.actions + slab * 2 * a.n;
-    const float2 a0 = load_action(ap + ic);
-    const float2 a1 = load_action(ap + a.n + ic);
-    __builtin_amdgcn_sched_barrier(0);
-    U4 ru = {0u, 0u, 0u, 0u};
-    if (early) {  // the restart's draw under the loads (k_step)
-      ru = draw4(a.seed, (uint64_t)(a.env_offset + i), step, 1u);
-      asm volatile("" : "+v"(ru.x), "+v"(ru.y), "+v"(ru.z), "+v"(ru.w));
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    bool k0, k1;
-    const sktrig::SinCos m0 = sktrig::sincos_bf(e.rot[0], &k0);
-    const sktrig::SinCos m1 = sktrig::sincos_bf(e.rot[1], &k1);
-    tick_env_m(c, e, m0, m1, k0 & k1, (double)a0.x, (double)a0.y, (double)a1.x, (double)a1.y);
-    // every load consumed (the slot's, issued first, with them): without this
-    // the waitcnt pass, its tracking lost across the loop, drains every store
-    // before the final counter store
-    ctr_settle(wc);
-    const bool d = in && ((!e.live) || (e.ticks >= a.tick_limit));  // SkillshotLearner.py:302
-    if (in) {
-      if (a.done) a.done[(int64_t)t * a.out_stride + i] = (uint8_t)d;
-      if (a.winner) a.winner[(int64_t)t * a.out_stride + i] = (uint8_t)e.winner;
-    }
-    // episode counters: per lane here, one wave reduction after the loop
-    n_done += d;
-    n_h1 += d && e.winner == 1;
-    n_h2 += d && e.winner == 2;
-    t_sum += d ? (unsigned)e.ticks : 0u;
-    if (d && a.auto_reset) {
-      if (a.random_positions) {
-        if (early) reset_random_u(c, e, ru);
-        else reset_random(c, e, a.seed, (uint64_t)(a.env_offset + i), step);
-      } else {
-        reset_fixed(c, e);
-      }
-    }
-    if (in) store_env_port<POL>(a, r, i, e, q_old0, q_old1);
+    multi_tick<POL>(a, c, r, L, wc, t, step0 + (uint64_t)t, slab);
     slab = slab + 1 == a.ring ? 0 : slab + 1;
   }
   if (a.ctr) {
-    uint64_t v[4] = {n_done, n_h1, n_h2, t_sum};
+    uint64_t v[4] = {L.n_done, L.n_h1, L.n_h2, L.t_sum};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off, 64);
+    ctr_store(a.ctr, wc, v[0], v[1], v[2], v[3]);
+  }
+}
+
+// k_step_split_multi: k_step_multi with k_step_split's geometry — lanes (2i,
+// 2i+1) own players 1 and 2 of game i, each loading and storing its player's
+// 8-byte half of every plane (the pair covers the game's 16 bytes; a wave
+// moves 512 contiguous bytes per plane), exchanging positions / projectiles
+// with __shfl_xor(., 1) for the collision test.  Twice the waves of
+// k_step_multi at half the dependent chain per lane: at 65,536 games two
+// waves share each SIMD, so one wave's state round trip through memory
+// overlaps the other's tick.  Same contract, same state ports.
+template <int POL>
+__device__ __forceinline__ double ld_half_d(const MultiArgs& a, __amdgpu_buffer_rsrc_t r, int k, const double* plane,
+                                            int64_t h) {
+  if constexpr (POL == 0) return plane[h];
+  else return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (uint32_t)h * 8u + a.off[k], 0, 16));
+}
+template <int POL>
+__device__ __forceinline__ int2 ld_half_i(const MultiArgs& a, __amdgpu_buffer_rsrc_t r, int k, const int2* plane,
+                                          int64_t h) {
+  if constexpr (POL == 0) {
+    return plane[h];
+  } else {
+    const skb2i v = __builtin_amdgcn_raw_buffer_load_b64(r, (uint32_t)h * 8u + a.off[k], 0, 16);
+    return make_int2(v.x, v.y);
+  }
+}
+template <int POL>
+__device__ __forceinline__ void st_half_d(const MultiArgs& a, __amdgpu_buffer_rsrc_t r, int k, double* plane, int64_t h,
+                                          double v) {
+  if constexpr (POL == 0) plane[h] = v;
+  else __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(skb2i, v), r, (uint32_t)h * 8u + a.off[k], 0, 16);
+}
+template <int POL>
+__device__ __forceinline__ void st_half_i(const MultiArgs& a, __amdgpu_buffer_rsrc_t r, int k, int2* plane, int64_t h,
+                                          int x, int y) {
+  if constexpr (POL == 0) plane[h] = make_int2(x, y);
+  else __builtin_amdgcn_raw_buffer_store_b64((skb2i){x, y}, r, (uint32_t)h * 8u + a.off[k], 0, 16);
+}
+
+struct SplitLane {
+  int64_t i, ic, hc, h;  // game, loaded game, loaded / stored half-plane index
+  int p;                 // player of this lane
+  bool in;
+  unsigned n_done, n_h1, n_h2, t_sum;  // this pair's episode counts (lane p = 0 counts)
+};
+
+template <int POL>
+__device__ __forceinline__ void split_multi_tick(const MultiArgs& a, const Cfg& c, __amdgpu_buffer_rsrc_t r,
+                                                 SplitLane& L, WaveCtr& wc, int t, uint64_t step, int64_t slab) {
+  int2* const pos2 = reinterpret_cast<int2*>(a.v.pos);
+  double* const rot1 = reinterpret_cast<double*>(a.v.rot);
+  int2* const qpos2 = reinterpret_cast<int2*>(a.v.qpos);
+  double* const qrot1 = reinterpret_cast<double*>(a.v.qrot);
+  int2* const ca2 = reinterpret_cast<int2*>(a.v.qcdage);
+  const int p = L.p;
+  // k_step_split's load order: rotation first
+  double rot = ld_half_d<POL>(a, r, 1, rot1, L.hc);
+  double qrot = ld_half_d<POL>(a, r, 3, qrot1, L.hc);
+  const int2 pp = ld_half_i<POL>(a, r, 0, pos2, L.hc);
+  const int2 ca = ld_half_i<POL>(a, r, 4, ca2, L.hc);
+  const int2 qq = ld_half_i<POL>(a, r, 2, qpos2, L.hc);
+  const int2 mi = ld_half_i<POL>(a, r, 5, a.v.misc, L.ic);
+  __builtin_amdgcn_sched_barrier(0);
+  const float2 act = load_action(a.actions + slab * 2 * a.n + (int64_t)p * a.n + L.ic);  // action last
+  __builtin_amdgcn_sched_barrier(0);
+  bool k0, k1;
+  sktrig::SinCos m = sktrig::sincos_bf(rot, &k0);
+  int px = pp.x, py = pp.y, qx = qq.x, qy = qq.y, qcd = ca.x, qage = ca.y, ticks = mi.x;
+  const int flags = mi.y;
+  int qvalid = ((unsigned)flags >> (8 * p)) & 0xff;
+  int live = ((unsigned)flags >> 16) & 0xff;
+  int winner = ((unsigned)flags >> 24) & 0xff;
+  const double q_old = qrot;
+  // do_actions(p+1, ...)  SkillshotLearner.py:206-213 (both sincos up front)
+  const double rn = rot + clamp_action((double)act.y) * c.look;
+  const double qn = (qcd <= 0) ? rn : qrot;
+  sktrig::SinCos tq = sktrig::sincos_bf(qn, &k1);
+  if (!(k0 & k1)) {
+    if (!k0) m = sincos_lib(rot);
+    if (!k1) tq = sincos_lib(qn);
+  }
+  move_direction_sc(c, px, py, m, (double)act.x);
+  rot = rn;
+  shoot_s(c, px, py, rot, qx, qy, qrot, qcd, qage, qvalid);
+  // game_tick  SkillshotGame.py:115-122 (live is identical in both lanes)
+  if (live) {
+    ticks += 1;
+    projectile_tick_sc(c, qx, qy, tq, qcd, qage, qvalid);
+  }
+  const int opx = __shfl_xor(px, 1, 64), opy = __shfl_xor(py, 1, 64);
+  const int oqx = __shfl_xor(qx, 1, 64), oqy = __shfl_xor(qy, 1, 64), oqv = __shfl_xor(qvalid, 1, 64);
+  if (live) {
+    if (p == 0) collide_s(c, px, py, qx, qy, qvalid, opx, opy, oqx, oqy, oqv, live, winner);
+    else collide_s(c, opx, opy, oqx, oqy, oqv, px, py, qx, qy, qvalid, live, winner);
+  }
+  ctr_settle(wc);  // every load of this tick consumed (see multi_tick)
+  const bool d = L.in && ((!live) || (ticks >= a.tick_limit));  // SkillshotLearner.py:302
+  if (L.in && p == 0) {
+    if (a.done) a.done[(int64_t)t * a.out_stride + L.i] = (uint8_t)d;
+    if (a.winner) a.winner[(int64_t)t * a.out_stride + L.i] = (uint8_t)winner;
+  }
+  const bool dc = d && p == 0;
+  L.n_done += dc;
+  L.n_h1 += dc && winner == 1;
+  L.n_h2 += dc && winner == 2;
+  L.t_sum += dc ? (unsigned)ticks : 0u;
+  if (d && a.auto_reset) {  // SkillshotGame.__init__ :10-25 for this lane's player
+    if (a.random_positions) {
+      const U4 u = draw4(a.seed, (uint64_t)(a.env_offset + L.i), step, 1u);
+      px = u32_to_pos(p ? u.z : u.x, c.rlo, c.rhi);
+      py = u32_to_pos(p ? u.w : u.y, c.rlo, c.rhi);
+    } else {
+      px = p ? c.f2x : c.f1x;
+      py = p ? c.f2y : c.f1y;
+    }
+    rot = 0.0; qx = 0; qy = 0; qrot = 0.0; qcd = 0; qage = 0; qvalid = 0;
+    ticks = 0; live = 1; winner = 0;
+  }
+  const int ov = __shfl_xor(qvalid, 1, 64);
+  if (L.in) {
+    st_half_i<POL>(a, r, 0, pos2, L.h, px, py);
+    st_half_d<POL>(a, r, 1, rot1, L.h, rot);
+    st_half_i<POL>(a, r, 2, qpos2, L.h, qx, qy);
+    if (__double_as_longlong(qrot) != __double_as_longlong(q_old)) st_half_d<POL>(a, r, 3, qrot1, L.h, qrot);
+    st_half_i<POL>(a, r, 4, ca2, L.h, qcd, qage);
+    if (p == 0) {
+      const unsigned f = (unsigned)(qvalid & 0xff) | ((unsigned)(ov & 0xff) << 8) |
+                         ((unsigned)(live & 0xff) << 16) | ((unsigned)(winner & 0xff) << 24);
+      st_half_i<POL>(a, r, 5, a.v.misc, L.i, ticks, (int)f);
+    }
+  }
+}
+
+template <int POL>
+__global__ void __launch_bounds__(kStepBlock) k_step_split_multi(MultiArgs a, Cfg c) {
+  SplitLane L;
+  const int64_t gt = (int64_t)blockIdx.x * kStepBlock + threadIdx.x;
+  L.i = gt >> 1;
+  L.p = (int)(gt & 1);
+  L.in = L.i < a.n;
+  L.ic = L.in ? L.i : 0;
+  L.hc = 2 * L.ic + L.p;
+  L.h = 2 * L.i + L.p;
+  L.n_done = L.n_h1 = L.n_h2 = L.t_sum = 0;
+  WaveCtr wc = ctr_load(a.ctr);
+  const uint64_t step0 = step_read(a.step);
+  step_advance(a.step, step0, (uint64_t)a.n_ticks);
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(a.base), (short)0, -1, 0x00020000);
+  int64_t slab = a.slab0;
+  for (int t = 0; t < a.n_ticks; ++t) {
+    split_multi_tick<POL>(a, c, r, L, wc, t, step0 + (uint64_t)t, slab);
+    slab = slab + 1 == a.ring ? 0 : slab + 1;
+  }
+  if (a.ctr) {
+    uint64_t v[4] = {L.n_done, L.n_h1, L.n_h2, L.t_sum};
 #pragma unroll
     for (int k = 0; k < 4; ++k)
 #pragma unroll
@@ -1074,6 +1257,8 @@ static int make_env(sk_env** out, const sk_state_view* view, int32_t n, int64_t 
   if (const char* sv = std::getenv("SK_STEP_VARIANT")) e->step_variant = std::atoi(sv);
   e->multi_policy = 1;  // write-through (the contract bytes leave L2 every tick)
   if (const char* mp = std::getenv("SK_MULTI_POLICY")) e->multi_policy = std::atoi(mp);
+  e->multi_split = -1;
+  if (const char* ms = std::getenv("SK_MULTI_SPLIT")) e->multi_split = std::atoi(ms);
   if (view) {
     if (view->n_envs != n || !view->pos || !view->rot || !view->qpos || !view->qrot || !view->qcdage ||
         !view->misc) {
@@ -1487,10 +1672,17 @@ int sk_env_step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64
     if (!ok) return fail(SK_EINVAL, "SK_MULTI_POLICY=1 needs the state planes within 4 GiB of each other");
     a.base = lo;
   }
-  if (pol == 1)
-    k_step_multi<1><<<step_grid(e->n), kStepBlock, 0, (hipStream_t)stream>>>(a, e->dcfg);
-  else
-    k_step_multi<0><<<step_grid(e->n), kStepBlock, 0, (hipStream_t)stream>>>(a, e->dcfg);
+  // geometry: one lane per game (k_step_multi) or two (k_step_split_multi);
+  // SK_MULTI_SPLIT = 0 / 1 forces one, else auto (kSplitMultiMaxEnvs)
+  const bool split = e->multi_split >= 0 ? e->multi_split != 0 : (int64_t)e->n <= kSplitMultiMaxEnvs;
+  const hipStream_t hs = (hipStream_t)stream;
+  if (split) {
+    if (pol == 1) k_step_split_multi<1><<<step_grid(2 * (int64_t)e->n), kStepBlock, 0, hs>>>(a, e->dcfg);
+    else k_step_split_multi<0><<<step_grid(2 * (int64_t)e->n), kStepBlock, 0, hs>>>(a, e->dcfg);
+  } else {
+    if (pol == 1) k_step_multi<1><<<step_grid(e->n), kStepBlock, 0, hs>>>(a, e->dcfg);
+    else k_step_multi<0><<<step_grid(e->n), kStepBlock, 0, hs>>>(a, e->dcfg);
+  }
   SK_LAUNCH_CHECK();
   e->parity ^= 1;
   return SK_OK;

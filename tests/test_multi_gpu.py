@@ -20,6 +20,13 @@ def ssa():
     return m
 
 
+@pytest.fixture(params=["0", "1"], ids=["lane_per_game", "player_split"])
+def split(request, monkeypatch):
+    """both multi-tick geometries (k_step_multi, k_step_split_multi) meet the same bar"""
+    monkeypatch.setenv("SK_MULTI_SPLIT", request.param)
+    return request.param
+
+
 def _pair(ssa, n, seed, tick_limit, monkeypatch, pol):
     monkeypatch.setenv("SK_MULTI_POLICY", str(pol))
     a = ssa.VecSkillshotGame(n, seed=seed, tick_limit=tick_limit)
@@ -38,7 +45,7 @@ def _same_state(x, y):
 
 @pytest.mark.parametrize("pol", [0, 1], ids=["plain", "write_through"])
 @pytest.mark.parametrize("n", [3000, 40000])
-def test_step_multi_equals_stepwise(ssa, monkeypatch, pol, n):
+def test_step_multi_equals_stepwise(ssa, monkeypatch, pol, n, split):
     T, R, slab0, limit = 300, 7, 3, 120
     a, b = _pair(ssa, n, 21, limit, monkeypatch, pol)
     acts = a.gen_random_actions(R)
@@ -59,7 +66,7 @@ def test_step_multi_equals_stepwise(ssa, monkeypatch, pol, n):
 
 
 @pytest.mark.parametrize("pol", [0, 1], ids=["plain", "write_through"])
-def test_step_multi_chunks_and_last_row(ssa, monkeypatch, pol):
+def test_step_multi_chunks_and_last_row(ssa, monkeypatch, pol, split):
     """Several launches of different lengths (slab0 carried over the ring)
     equal one; out_stride 0 leaves the last tick's done row."""
     n, R = 5000, 11
@@ -76,7 +83,7 @@ def test_step_multi_chunks_and_last_row(ssa, monkeypatch, pol):
     assert a.counters() == b.counters()
 
 
-def test_step_multi_cpu_backend_equals_gpu(ssa, monkeypatch):
+def test_step_multi_cpu_backend_equals_gpu(ssa, monkeypatch, split):
     monkeypatch.setenv("SK_MULTI_POLICY", "1")
     n, T, R = 4096, 260, 5
     g = ssa.VecSkillshotGame(n, seed=9, tick_limit=100)

@@ -18,8 +18,10 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 
-def multi_rate(n, T, pol, K=2000, ring=400, seed=0):
+def multi_rate(n, T, pol, split=-1, stagger=0, K=2000, ring=400, seed=0):
     os.environ["SK_MULTI_POLICY"] = str(pol)
+    os.environ["SK_MULTI_SPLIT"] = str(split)
+    os.environ["SK_MULTI_STAGGER"] = str(stagger)
     from skillshot_learning_amd import VecSkillshotGame
     dev = torch.device("cuda", 0)
     env = VecSkillshotGame(n, device=dev, seed=seed, tick_limit=2000, random_positions=True)
@@ -49,7 +51,7 @@ def multi_rate(n, T, pol, K=2000, ring=400, seed=0):
     st.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / (launches * T)
     env.close()
-    return dict(kind="multi", envs=n, ticks_per_launch=T, policy=pol, us_per_tick=us,
+    return dict(kind="multi", envs=n, ticks_per_launch=T, policy=pol, split=split, stagger=stagger, us_per_tick=us,
                 env_steps_per_s=n / (us * 1e-6), frac=193 * n / (us * 1e-6) / 8e12)
 
 
@@ -67,14 +69,20 @@ def main():
     p.add_argument("--ticks", default="1,5,20,100,400")
     p.add_argument("--pols", default="0,1")
     p.add_argument("--reps", type=int, default=2)
+    p.add_argument("--splits", default="-1")
+    p.add_argument("--staggers", default="0")
+    p.add_argument("--no-graph", action="store_true")
     a = p.parse_args()
     torch.cuda.set_device(0)
     for rep in range(a.reps):
         for n in [int(x) for x in a.envs.split(",")]:
-            print(json.dumps(dict(graph_rate(n), rep=rep)), flush=True)
+            if not a.no_graph:
+                print(json.dumps(dict(graph_rate(n), rep=rep)), flush=True)
             for pol in [int(x) for x in a.pols.split(",")]:
-                for T in [int(x) for x in a.ticks.split(",")]:
-                    print(json.dumps(dict(multi_rate(n, T, pol), rep=rep)), flush=True)
+                for sp in [int(x) for x in a.splits.split(",")]:
+                    for T in [int(x) for x in a.ticks.split(",")]:
+                        for sg in [int(x) for x in a.staggers.split(",")]:
+                            print(json.dumps(dict(multi_rate(n, T, pol, sp, sg), rep=rep)), flush=True)
 
 
 if __name__ == "__main__":
