@@ -51,6 +51,12 @@ struct sk_env {
   int multi_policy;
   // k_step_multi geometry: -1 auto, 0 lane per game, 1 player per lane (SK_MULTI_SPLIT)
   int multi_split;
+  int multi_early;    // k_step_multi: the restart draw under the loads, 0 (default) / 1 (SK_MULTI_EARLY)
+  int multi_block;    // split geometry workgroup: -1 auto, 64 or 512 (SK_MULTI_BLOCK)
+  int multi_stagger;  // waves 4-7 of a 512-lane workgroup start this x 512 cycles late (SK_MULTI_STAGGER)
+  // k_step_multi's packed resident form between ticks (SK_MULTI_PACK=0 keeps the 88-B form)
+  int multi_pack;
+  char* d_pack;  // its scratch (48 B x n), allocated at the first multi-tick launch
   // device = -1: the CPU backend (sk_host.cpp) owns the games; every entry
   // point below forwards to it and takes host pointers
   skh::Host* host;
@@ -121,10 +127,11 @@ static inline unsigned step_grid(int64_t n) { return (unsigned)((n + kStepBlock 
 // the slots.  Round 1 added per-wave device atomics into 256 shared slots and
 // summed the ticks with a 64-bit shuffle tree; counting then cost 0.42 of a
 // 4.62 us 65,536-game k_step, now 0.04 us (profiles/r02_step_ablation.jsonl).
+template <int BLK = kStepBlock>
 __device__ __forceinline__ sk_counters* ctr_slot(sk_counters* base) {
-  // every kernel that counts launches kStepBlock-lane workgroups (a constant,
-  // not blockDim, whose dispatch-packet load would land on the wave's tail)
-  const unsigned wave = blockIdx.x * (kStepBlock >> 6) + (threadIdx.x >> 6);
+  // every kernel that counts launches BLK-lane workgroups (a constant, not
+  // blockDim, whose dispatch-packet load would land on the wave's tail)
+  const unsigned wave = blockIdx.x * (BLK >> 6) + (threadIdx.x >> 6);
   return base + (size_t)wave * SK_CTR_STRIDE;
 }
 
@@ -132,12 +139,13 @@ struct WaveCtr {
   ulonglong4 v;
 };
 
+template <int BLK = kStepBlock>
 __device__ __forceinline__ WaveCtr ctr_load(sk_counters* base) {
   WaveCtr w;
 #ifdef SK_CTR_NOMEM  // timing ablation: counting without its memory traffic
   w.v = make_ulonglong4(0, 0, 0, 0);
 #else
-  w.v = base ? *reinterpret_cast<const ulonglong4*>(ctr_slot(base)) : make_ulonglong4(0, 0, 0, 0);
+  w.v = base ? *reinterpret_cast<const ulonglong4*>(ctr_slot<BLK>(base)) : make_ulonglong4(0, 0, 0, 0);
 #endif
   return w;
 }
@@ -153,6 +161,7 @@ __device__ __forceinline__ void ctr_settle(WaveCtr& w) {
   asm volatile("" : "+v"(w.v.x), "+v"(w.v.y), "+v"(w.v.z), "+v"(w.v.w));
 }
 
+template <int BLK = kStepBlock>
 __device__ __forceinline__ void ctr_store(sk_counters* base, const WaveCtr& w, uint64_t dones, uint64_t h1,
                                           uint64_t h2, uint64_t tsum) {
 #ifdef SK_CTR_NOMEM
@@ -160,7 +169,7 @@ __device__ __forceinline__ void ctr_store(sk_counters* base, const WaveCtr& w, u
   return;
 #endif
   if ((threadIdx.x & 63) == 0)
-    *reinterpret_cast<ulonglong4*>(ctr_slot(base)) =
+    *reinterpret_cast<ulonglong4*>(ctr_slot<BLK>(base)) =
         make_ulonglong4(w.v.x + dones, w.v.y + h1, w.v.z + h2, w.v.w + tsum);
 }
 
@@ -702,6 +711,22 @@ __global__ void __launch_bounds__(kStepBlock) k_rollout_random(RolloutArgs a, Cf
 //      policy is an operand and the compiler tracks the waits) over ONE
 //      resource whose base is the lowest plane (the host checks that every
 //      plane lies within 4 GiB of it): one resource per plane spilled SGPRs.
+//
+// Resident format between ticks.  The 88-B SoA of include/skillshot.h is the
+// exchange format: every launch loads it at its first tick and stores it at
+// its last.  In between, a wave whose games all fit keeps them in a packed
+// 48-B form in a scratch buffer of the handle (`pack`: R double2[n]
+// rotations, Q double2[n] projectile rotations, S int4[n] = per player
+// {px, py, qx, qy as bytes; cooldown int8, age u8, and ticks u16 (player 1)
+// or the flag byte qv1 | qv2 << 1 | live << 2 | winner << 3 (player 2)}).
+// Every tick still loads and stores every game's state through the same
+// port; only the encoding is narrower (48 + ~40 B move
+// per game-tick instead of 88 + ~72, reported against the fixed 193 B
+// contract).  Fits: positions 0..255 (the board is 250), cooldown -128..127,
+// age 0..255, ticks 0..65535, valid / live bytes 0..1, winner 0..3 — always
+// true under the step protocol after the first tick (shoot is attempted
+// every tick, Player.py:78-89, so cooldown and age stay in 0..16); a wave
+// with any lane outside keeps the 88-B form for the rest of the launch.
 typedef int skb4i __attribute__((ext_vector_type(4)));
 typedef int skb2i __attribute__((ext_vector_type(2)));
 typedef double skb2d __attribute__((ext_vector_type(2)));
@@ -725,8 +750,12 @@ struct MultiArgs {
   sk_counters* ctr;
   const char* base;       // POL 1: the lowest plane; off[k] = plane k - base (pos, rot, qpos, qrot, qcdage, misc)
   uint32_t off[6];
+  char* pack;             // the packed resident planes (48 B x n), or NULL: the 88-B form every tick
 };
 
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t raw_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, -1, 0x00020000);
+}
 
 template <int POL>
 __device__ __forceinline__ void load_env_port(const MultiArgs& a, __amdgpu_buffer_rsrc_t r, int64_t i, Env& e) {
@@ -748,18 +777,24 @@ __device__ __forceinline__ void load_env_port(const MultiArgs& a, __amdgpu_buffe
 }
 
 // store_env_q through the port: the projectile-rotation plane only where it
-// changed (a projectile fired, or the game restarted)
+// changed (a projectile fired, or the game restarted) unless force_q (the
+// previous tick's state was packed: this plane is stale)
 template <int POL>
 __device__ __forceinline__ void store_env_port(const MultiArgs& a, __amdgpu_buffer_rsrc_t r, int64_t i, const Env& e,
-                                               double q_old0, double q_old1) {
+                                               double q_old0, double q_old1, bool force_q) {
+  const unsigned f = (unsigned)(e.qvalid[0] & 0xff) | ((unsigned)(e.qvalid[1] & 0xff) << 8) |
+                     ((unsigned)(e.live & 0xff) << 16) | ((unsigned)(e.winner & 0xff) << 24);
+  const bool qrot_changed = force_q | (int)(__double_as_longlong(e.qrot[0]) != __double_as_longlong(q_old0)) |
+                            (int)(__double_as_longlong(e.qrot[1]) != __double_as_longlong(q_old1));
   if constexpr (POL == 0) {
-    store_env_q(a.v, i, e, q_old0, q_old1);
+    a.v.pos[i] = make_int4(e.px[0], e.py[0], e.px[1], e.py[1]);
+    a.v.rot[i] = make_double2(e.rot[0], e.rot[1]);
+    a.v.qpos[i] = make_int4(e.qx[0], e.qy[0], e.qx[1], e.qy[1]);
+    if (qrot_changed) a.v.qrot[i] = make_double2(e.qrot[0], e.qrot[1]);
+    a.v.qcdage[i] = make_int4(e.qcd[0], e.qage[0], e.qcd[1], e.qage[1]);
+    a.v.misc[i] = make_int2(e.ticks, (int)f);
   } else {
     const uint32_t o16 = (uint32_t)i * 16u, o8 = (uint32_t)i * 8u;
-    const unsigned f = (unsigned)(e.qvalid[0] & 0xff) | ((unsigned)(e.qvalid[1] & 0xff) << 8) |
-                       ((unsigned)(e.live & 0xff) << 16) | ((unsigned)(e.winner & 0xff) << 24);
-    const bool qrot_changed = (int)(__double_as_longlong(e.qrot[0]) != __double_as_longlong(q_old0)) |
-                              (int)(__double_as_longlong(e.qrot[1]) != __double_as_longlong(q_old1));
     __builtin_amdgcn_raw_buffer_store_b128((skb4i){e.px[0], e.py[0], e.px[1], e.py[1]}, r, o16 + a.off[0], 0, 16);
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(skb4i, (skb2d){e.rot[0], e.rot[1]}), r,
                                            o16 + a.off[1], 0, 16);
@@ -770,6 +805,72 @@ __device__ __forceinline__ void store_env_port(const MultiArgs& a, __amdgpu_buff
     __builtin_amdgcn_raw_buffer_store_b128((skb4i){e.qcd[0], e.qage[0], e.qcd[1], e.qage[1]}, r, o16 + a.off[4], 0,
                                            16);
     __builtin_amdgcn_raw_buffer_store_b64((skb2i){e.ticks, (int)f}, r, o8 + a.off[5], 0, 16);
+  }
+}
+
+// ---- the packed form
+__device__ __forceinline__ bool pack_fits_player(int px, int py, int qx, int qy, int cd, int age, int qv) {
+  return ((unsigned)px < 256u) & ((unsigned)py < 256u) & ((unsigned)qx < 256u) & ((unsigned)qy < 256u) &
+         (cd >= -128) & (cd <= 127) & ((unsigned)age < 256u) & ((unsigned)qv < 2u);
+}
+__device__ __forceinline__ bool pack_fits_game(int ticks, int live, int winner) {
+  return ((unsigned)ticks < 65536u) & ((unsigned)live < 2u) & ((unsigned)winner < 4u);
+}
+__device__ __forceinline__ unsigned pack_flags(int qv0, int qv1, int live, int winner) {
+  return (unsigned)qv0 | ((unsigned)qv1 << 1) | ((unsigned)live << 2) | ((unsigned)winner << 3);
+}
+__device__ __forceinline__ int pack_pos(int px, int py, int qx, int qy) {
+  return (int)((unsigned)px | ((unsigned)py << 8) | ((unsigned)qx << 16) | ((unsigned)qy << 24));
+}
+__device__ __forceinline__ int pack_cah(int cd, int age, unsigned hi) {
+  return (int)(((unsigned)cd & 0xffu) | ((unsigned)age << 8) | (hi << 16));
+}
+
+template <int POL>
+__device__ __forceinline__ void load_env_pack(const MultiArgs& a, __amdgpu_buffer_rsrc_t rp, int64_t i, Env& e) {
+  skb4i rb, qb, sb;
+  if constexpr (POL == 0) {
+    const skb4i* P = reinterpret_cast<const skb4i*>(a.pack);
+    rb = P[i];
+    qb = P[a.n + i];
+    sb = P[2 * a.n + i];
+  } else {
+    const uint32_t o = (uint32_t)i * 16u, plane = (uint32_t)a.n * 16u;
+    rb = __builtin_amdgcn_raw_buffer_load_b128(rp, o, 0, 16);
+    qb = __builtin_amdgcn_raw_buffer_load_b128(rp, o + plane, 0, 16);
+    sb = __builtin_amdgcn_raw_buffer_load_b128(rp, o + 2u * plane, 0, 16);
+  }
+  const skb2d rr = __builtin_bit_cast(skb2d, rb), qr = __builtin_bit_cast(skb2d, qb);
+  e.rot[0] = rr.x; e.rot[1] = rr.y;
+  e.qrot[0] = qr.x; e.qrot[1] = qr.y;
+  const unsigned s0 = (unsigned)sb.x, c0 = (unsigned)sb.y, s1 = (unsigned)sb.z, c1 = (unsigned)sb.w;
+  e.px[0] = s0 & 0xff; e.py[0] = (s0 >> 8) & 0xff; e.qx[0] = (s0 >> 16) & 0xff; e.qy[0] = s0 >> 24;
+  e.px[1] = s1 & 0xff; e.py[1] = (s1 >> 8) & 0xff; e.qx[1] = (s1 >> 16) & 0xff; e.qy[1] = s1 >> 24;
+  e.qcd[0] = (int)(signed char)(c0 & 0xff); e.qage[0] = (c0 >> 8) & 0xff;
+  e.qcd[1] = (int)(signed char)(c1 & 0xff); e.qage[1] = (c1 >> 8) & 0xff;
+  e.ticks = (int)(c0 >> 16);
+  const unsigned fl = c1 >> 16;
+  e.qvalid[0] = fl & 1; e.qvalid[1] = (fl >> 1) & 1; e.live = (fl >> 2) & 1; e.winner = (fl >> 3) & 3;
+}
+
+template <int POL>
+__device__ __forceinline__ void store_env_pack(const MultiArgs& a, __amdgpu_buffer_rsrc_t rp, int64_t i, const Env& e,
+                                               bool store_q) {
+  const skb4i rb = __builtin_bit_cast(skb4i, (skb2d){e.rot[0], e.rot[1]});
+  const skb4i qb = __builtin_bit_cast(skb4i, (skb2d){e.qrot[0], e.qrot[1]});
+  const skb4i sb = {pack_pos(e.px[0], e.py[0], e.qx[0], e.qy[0]), pack_cah(e.qcd[0], e.qage[0], (unsigned)e.ticks),
+                    pack_pos(e.px[1], e.py[1], e.qx[1], e.qy[1]),
+                    pack_cah(e.qcd[1], e.qage[1], pack_flags(e.qvalid[0], e.qvalid[1], e.live, e.winner))};
+  if constexpr (POL == 0) {
+    skb4i* P = reinterpret_cast<skb4i*>(a.pack);
+    P[i] = rb;
+    if (store_q) P[a.n + i] = qb;
+    P[2 * a.n + i] = sb;
+  } else {
+    const uint32_t o = (uint32_t)i * 16u, plane = (uint32_t)a.n * 16u;
+    __builtin_amdgcn_raw_buffer_store_b128(rb, rp, o, 0, 16);
+    if (store_q) __builtin_amdgcn_raw_buffer_store_b128(qb, rp, o + plane, 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(sb, rp, o + 2u * plane, 0, 16);
   }
 }
 
@@ -785,11 +886,15 @@ struct MultiLane {
 // (65,536 games 2.51 vs 2.36 us per tick, 8,192 split 1.71 vs 1.59;
 // profiles/r03d_multi_prefetch_sweep.jsonl): vector memory returns in issue
 // order, so the next tick's state waited for the prefetched HBM loads anyway.
+// `packed` (wave-uniform): where the state lives now; `last`: the final tick
+// (its state goes to the exchange format).
 template <int POL>
-__device__ __forceinline__ void multi_tick(const MultiArgs& a, const Cfg& c, __amdgpu_buffer_rsrc_t r, MultiLane& L,
-                                           WaveCtr& wc, int t, uint64_t step, int64_t slab) {
+__device__ __forceinline__ void multi_tick(const MultiArgs& a, const Cfg& c, __amdgpu_buffer_rsrc_t r,
+                                           __amdgpu_buffer_rsrc_t rp, MultiLane& L, WaveCtr& wc, int t, uint64_t step,
+                                           int64_t slab, bool& packed, bool last) {
   Env e;
-  load_env_port<POL>(a, r, L.ic, e);
+  if (packed) load_env_pack<POL>(a, rp, L.ic, e);
+  else load_env_port<POL>(a, r, L.ic, e);
   const double q_old0 = e.qrot[0], q_old1 = e.qrot[1];
   __builtin_amdgcn_sched_barrier(0);
   float2 acts[2];
@@ -802,6 +907,10 @@ __device__ __forceinline__ void multi_tick(const MultiArgs& a, const Cfg& c, __a
     asm volatile("" : "+v"(ru.x), "+v"(ru.y), "+v"(ru.z), "+v"(ru.w));
   }
   __builtin_amdgcn_sched_barrier(0);
+  // k_step's fp64 tick.  k_step_fast's (fp32 trig, exact fp64 redo) was no
+  // faster at 400 ticks per launch and 20 % slower at 20 (65,536 games:
+  // 2.50 vs 2.51 and 3.37 vs 2.71 us per tick; profiles/
+  // r03i_multi_fast_early_sweep.jsonl)
   bool k0, k1;
   const sktrig::SinCos m0 = sktrig::sincos_bf(e.rot[0], &k0);
   const sktrig::SinCos m1 = sktrig::sincos_bf(e.rot[1], &k1);
@@ -827,25 +936,38 @@ __device__ __forceinline__ void multi_tick(const MultiArgs& a, const Cfg& c, __a
       reset_fixed(c, e);
     }
   }
-  if (L.in) store_env_port<POL>(a, r, L.i, e, q_old0, q_old1);
+  const bool fit = !L.in || (pack_fits_player(e.px[0], e.py[0], e.qx[0], e.qy[0], e.qcd[0], e.qage[0], e.qvalid[0]) &
+                             pack_fits_player(e.px[1], e.py[1], e.qx[1], e.qy[1], e.qcd[1], e.qage[1], e.qvalid[1]) &
+                             pack_fits_game(e.ticks, e.live, e.winner));
+  const bool to_pack = a.pack != nullptr && !last && __ballot(!fit) == 0;  // wave-uniform
+  if (L.in) {
+    if (to_pack) {
+      const bool qch = !packed || (__double_as_longlong(e.qrot[0]) != __double_as_longlong(q_old0)) ||
+                       (__double_as_longlong(e.qrot[1]) != __double_as_longlong(q_old1));
+      store_env_pack<POL>(a, rp, L.i, e, qch);
+    } else {
+      store_env_port<POL>(a, r, L.i, e, q_old0, q_old1, packed);
+    }
+  }
+  packed = to_pack;
 }
 
 template <int POL>
-__global__ void __launch_bounds__(kStepBlock) k_step_multi(MultiArgs a, Cfg c) {
+__global__ void __launch_bounds__(kStepBlock) k_step_multi(MultiArgs a, Cfg c, int early) {
   MultiLane L;
   L.i = (int64_t)blockIdx.x * kStepBlock + threadIdx.x;
   L.in = L.i < a.n;
   L.ic = L.in ? L.i : 0;
-  L.early = a.random_positions && a.n >= kEarlyDrawMinEnvs;
+  L.early = a.random_positions && early;
   L.n_done = L.n_h1 = L.n_h2 = L.t_sum = 0;
   WaveCtr wc = ctr_load(a.ctr);
   const uint64_t step0 = step_read(a.step);
   step_advance(a.step, step0, (uint64_t)a.n_ticks);
-  const __amdgpu_buffer_rsrc_t r =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(a.base), (short)0, -1, 0x00020000);
+  const __amdgpu_buffer_rsrc_t r = raw_rsrc(a.base), rp = raw_rsrc(a.pack);
   int64_t slab = a.slab0;
+  bool packed = false;  // every launch starts from (and ends in) the exchange format
   for (int t = 0; t < a.n_ticks; ++t) {
-    multi_tick<POL>(a, c, r, L, wc, t, step0 + (uint64_t)t, slab);
+    multi_tick<POL>(a, c, r, rp, L, wc, t, step0 + (uint64_t)t, slab, packed, t + 1 == a.n_ticks);
     slab = slab + 1 == a.ring ? 0 : slab + 1;
   }
   if (a.ctr) {
@@ -865,7 +987,8 @@ __global__ void __launch_bounds__(kStepBlock) k_step_multi(MultiArgs a, Cfg c) {
 // with __shfl_xor(., 1) for the collision test.  Twice the waves of
 // k_step_multi at half the dependent chain per lane: at 65,536 games two
 // waves share each SIMD, so one wave's state round trip through memory
-// overlaps the other's tick.  Same contract, same state ports.
+// overlaps the other's tick.  Same contract, same state ports, same packed
+// form (a lane moves its player's 8-byte half of R, Q and S).
 template <int POL>
 __device__ __forceinline__ double ld_half_d(const MultiArgs& a, __amdgpu_buffer_rsrc_t r, int k, const double* plane,
                                             int64_t h) {
@@ -894,6 +1017,17 @@ __device__ __forceinline__ void st_half_i(const MultiArgs& a, __amdgpu_buffer_rs
   if constexpr (POL == 0) plane[h] = make_int2(x, y);
   else __builtin_amdgcn_raw_buffer_store_b64((skb2i){x, y}, r, (uint32_t)h * 8u + a.off[k], 0, 16);
 }
+// the packed planes by half: k = 0 R, 1 Q, 2 S (8 bytes per player)
+template <int POL>
+__device__ __forceinline__ skb2i ld_pack_half(const MultiArgs& a, __amdgpu_buffer_rsrc_t rp, int k, int64_t h) {
+  if constexpr (POL == 0) return reinterpret_cast<const skb2i*>(a.pack)[(int64_t)k * 2 * a.n + h];
+  else return __builtin_amdgcn_raw_buffer_load_b64(rp, (uint32_t)h * 8u + (uint32_t)k * (uint32_t)a.n * 16u, 0, 16);
+}
+template <int POL>
+__device__ __forceinline__ void st_pack_half(const MultiArgs& a, __amdgpu_buffer_rsrc_t rp, int k, int64_t h, skb2i v) {
+  if constexpr (POL == 0) reinterpret_cast<skb2i*>(a.pack)[(int64_t)k * 2 * a.n + h] = v;
+  else __builtin_amdgcn_raw_buffer_store_b64(v, rp, (uint32_t)h * 8u + (uint32_t)k * (uint32_t)a.n * 16u, 0, 16);
+}
 
 struct SplitLane {
   int64_t i, ic, hc, h;  // game, loaded game, loaded / stored half-plane index
@@ -904,30 +1038,49 @@ struct SplitLane {
 
 template <int POL>
 __device__ __forceinline__ void split_multi_tick(const MultiArgs& a, const Cfg& c, __amdgpu_buffer_rsrc_t r,
-                                                 SplitLane& L, WaveCtr& wc, int t, uint64_t step, int64_t slab) {
+                                                 __amdgpu_buffer_rsrc_t rp, SplitLane& L, WaveCtr& wc, int t,
+                                                 uint64_t step, int64_t slab, bool& packed, bool last) {
   int2* const pos2 = reinterpret_cast<int2*>(a.v.pos);
   double* const rot1 = reinterpret_cast<double*>(a.v.rot);
   int2* const qpos2 = reinterpret_cast<int2*>(a.v.qpos);
   double* const qrot1 = reinterpret_cast<double*>(a.v.qrot);
   int2* const ca2 = reinterpret_cast<int2*>(a.v.qcdage);
   const int p = L.p;
-  // k_step_split's load order: rotation first
-  double rot = ld_half_d<POL>(a, r, 1, rot1, L.hc);
-  double qrot = ld_half_d<POL>(a, r, 3, qrot1, L.hc);
-  const int2 pp = ld_half_i<POL>(a, r, 0, pos2, L.hc);
-  const int2 ca = ld_half_i<POL>(a, r, 4, ca2, L.hc);
-  const int2 qq = ld_half_i<POL>(a, r, 2, qpos2, L.hc);
-  const int2 mi = ld_half_i<POL>(a, r, 5, a.v.misc, L.ic);
+  double rot, qrot;
+  int px, py, qx, qy, qcd, qage, ticks, qvalid, live, winner;
+  if (packed) {
+    rot = __builtin_bit_cast(double, ld_pack_half<POL>(a, rp, 0, L.hc));
+    qrot = __builtin_bit_cast(double, ld_pack_half<POL>(a, rp, 1, L.hc));
+    const skb2i sv = ld_pack_half<POL>(a, rp, 2, L.hc);
+    const unsigned s0 = (unsigned)sv.x, c0 = (unsigned)sv.y;
+    px = s0 & 0xff; py = (s0 >> 8) & 0xff; qx = (s0 >> 16) & 0xff; qy = s0 >> 24;
+    qcd = (int)(signed char)(c0 & 0xff);
+    qage = (c0 >> 8) & 0xff;
+    const unsigned hi = c0 >> 16, other = (unsigned)__shfl_xor((int)hi, 1, 64);
+    ticks = (int)(p == 0 ? hi : other);
+    const unsigned fl = p == 0 ? other : hi;
+    qvalid = (fl >> p) & 1;
+    live = (fl >> 2) & 1;
+    winner = (fl >> 3) & 3;
+  } else {
+    // k_step_split's load order: rotation first
+    rot = ld_half_d<POL>(a, r, 1, rot1, L.hc);
+    qrot = ld_half_d<POL>(a, r, 3, qrot1, L.hc);
+    const int2 pp = ld_half_i<POL>(a, r, 0, pos2, L.hc);
+    const int2 ca = ld_half_i<POL>(a, r, 4, ca2, L.hc);
+    const int2 qq = ld_half_i<POL>(a, r, 2, qpos2, L.hc);
+    const int2 mi = ld_half_i<POL>(a, r, 5, a.v.misc, L.ic);
+    px = pp.x; py = pp.y; qx = qq.x; qy = qq.y; qcd = ca.x; qage = ca.y; ticks = mi.x;
+    const int flags = mi.y;
+    qvalid = ((unsigned)flags >> (8 * p)) & 0xff;
+    live = ((unsigned)flags >> 16) & 0xff;
+    winner = ((unsigned)flags >> 24) & 0xff;
+  }
   __builtin_amdgcn_sched_barrier(0);
   const float2 act = load_action(a.actions + slab * 2 * a.n + (int64_t)p * a.n + L.ic);  // action last
   __builtin_amdgcn_sched_barrier(0);
   bool k0, k1;
   sktrig::SinCos m = sktrig::sincos_bf(rot, &k0);
-  int px = pp.x, py = pp.y, qx = qq.x, qy = qq.y, qcd = ca.x, qage = ca.y, ticks = mi.x;
-  const int flags = mi.y;
-  int qvalid = ((unsigned)flags >> (8 * p)) & 0xff;
-  int live = ((unsigned)flags >> 16) & 0xff;
-  int winner = ((unsigned)flags >> 24) & 0xff;
   const double q_old = qrot;
   // do_actions(p+1, ...)  SkillshotLearner.py:206-213 (both sincos up front)
   const double rn = rot + clamp_action((double)act.y) * c.look;
@@ -975,24 +1128,41 @@ __device__ __forceinline__ void split_multi_tick(const MultiArgs& a, const Cfg& 
     ticks = 0; live = 1; winner = 0;
   }
   const int ov = __shfl_xor(qvalid, 1, 64);
+  const bool fit = !L.in || (pack_fits_player(px, py, qx, qy, qcd, qage, qvalid) & pack_fits_game(ticks, live, winner));
+  const bool to_pack = a.pack != nullptr && !last && __ballot(!fit) == 0;  // wave-uniform
+  const bool qch = __double_as_longlong(qrot) != __double_as_longlong(q_old);
   if (L.in) {
-    st_half_i<POL>(a, r, 0, pos2, L.h, px, py);
-    st_half_d<POL>(a, r, 1, rot1, L.h, rot);
-    st_half_i<POL>(a, r, 2, qpos2, L.h, qx, qy);
-    if (__double_as_longlong(qrot) != __double_as_longlong(q_old)) st_half_d<POL>(a, r, 3, qrot1, L.h, qrot);
-    st_half_i<POL>(a, r, 4, ca2, L.h, qcd, qage);
-    if (p == 0) {
-      const unsigned f = (unsigned)(qvalid & 0xff) | ((unsigned)(ov & 0xff) << 8) |
-                         ((unsigned)(live & 0xff) << 16) | ((unsigned)(winner & 0xff) << 24);
-      st_half_i<POL>(a, r, 5, a.v.misc, L.i, ticks, (int)f);
+    if (to_pack) {
+      st_pack_half<POL>(a, rp, 0, L.h, __builtin_bit_cast(skb2i, rot));
+      if (qch || !packed) st_pack_half<POL>(a, rp, 1, L.h, __builtin_bit_cast(skb2i, qrot));
+      const unsigned hi = p == 0 ? (unsigned)ticks
+                                 : pack_flags(p ? ov : qvalid, p ? qvalid : ov, live, winner);
+      st_pack_half<POL>(a, rp, 2, L.h, (skb2i){pack_pos(px, py, qx, qy), pack_cah(qcd, qage, hi)});
+    } else {
+      st_half_i<POL>(a, r, 0, pos2, L.h, px, py);
+      st_half_d<POL>(a, r, 1, rot1, L.h, rot);
+      st_half_i<POL>(a, r, 2, qpos2, L.h, qx, qy);
+      if (qch || packed) st_half_d<POL>(a, r, 3, qrot1, L.h, qrot);
+      st_half_i<POL>(a, r, 4, ca2, L.h, qcd, qage);
+      if (p == 0) {
+        const unsigned f = (unsigned)(qvalid & 0xff) | ((unsigned)(ov & 0xff) << 8) |
+                           ((unsigned)(live & 0xff) << 16) | ((unsigned)(winner & 0xff) << 24);
+        st_half_i<POL>(a, r, 5, a.v.misc, L.i, ticks, (int)f);
+      }
     }
   }
+  packed = to_pack;
 }
 
-template <int POL>
-__global__ void __launch_bounds__(kStepBlock) k_step_split_multi(MultiArgs a, Cfg c) {
+// BLK 512 (the 65,536-game geometry): one workgroup of 8 waves per CU, so
+// each SIMD hosts waves w and w + 4 of ONE workgroup (MI355X_MICROARCH.md
+// "Two waves per SIMD"); `stagger` > 0 starts waves 4-7 stagger x 512
+// cycles late, so the pair alternates a tick's memory round trip with the
+// partner's arithmetic instead of both waiting at once.
+template <int POL, int BLK>
+__global__ void __launch_bounds__(BLK) k_step_split_multi(MultiArgs a, Cfg c, int stagger) {
   SplitLane L;
-  const int64_t gt = (int64_t)blockIdx.x * kStepBlock + threadIdx.x;
+  const int64_t gt = (int64_t)blockIdx.x * BLK + threadIdx.x;
   L.i = gt >> 1;
   L.p = (int)(gt & 1);
   L.in = L.i < a.n;
@@ -1000,14 +1170,16 @@ __global__ void __launch_bounds__(kStepBlock) k_step_split_multi(MultiArgs a, Cf
   L.hc = 2 * L.ic + L.p;
   L.h = 2 * L.i + L.p;
   L.n_done = L.n_h1 = L.n_h2 = L.t_sum = 0;
-  WaveCtr wc = ctr_load(a.ctr);
+  if (stagger > 0 && (threadIdx.x >> 6) >= (BLK >> 7))
+    for (int k = 0; k < stagger; ++k) __builtin_amdgcn_s_sleep(8);
+  WaveCtr wc = ctr_load<BLK>(a.ctr);
   const uint64_t step0 = step_read(a.step);
   step_advance(a.step, step0, (uint64_t)a.n_ticks);
-  const __amdgpu_buffer_rsrc_t r =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(a.base), (short)0, -1, 0x00020000);
+  const __amdgpu_buffer_rsrc_t r = raw_rsrc(a.base), rp = raw_rsrc(a.pack);
   int64_t slab = a.slab0;
+  bool packed = false;
   for (int t = 0; t < a.n_ticks; ++t) {
-    split_multi_tick<POL>(a, c, r, L, wc, t, step0 + (uint64_t)t, slab);
+    split_multi_tick<POL>(a, c, r, rp, L, wc, t, step0 + (uint64_t)t, slab, packed, t + 1 == a.n_ticks);
     slab = slab + 1 == a.ring ? 0 : slab + 1;
   }
   if (a.ctr) {
@@ -1016,7 +1188,7 @@ __global__ void __launch_bounds__(kStepBlock) k_step_split_multi(MultiArgs a, Cf
     for (int k = 0; k < 4; ++k)
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off, 64);
-    ctr_store(a.ctr, wc, v[0], v[1], v[2], v[3]);
+    ctr_store<BLK>(a.ctr, wc, v[0], v[1], v[2], v[3]);
   }
 }
 
@@ -1259,6 +1431,15 @@ static int make_env(sk_env** out, const sk_state_view* view, int32_t n, int64_t 
   if (const char* mp = std::getenv("SK_MULTI_POLICY")) e->multi_policy = std::atoi(mp);
   e->multi_split = -1;
   if (const char* ms = std::getenv("SK_MULTI_SPLIT")) e->multi_split = std::atoi(ms);
+  e->multi_early = 0;
+  if (const char* me = std::getenv("SK_MULTI_EARLY")) e->multi_early = std::atoi(me);
+  e->multi_block = -1;
+  if (const char* mb = std::getenv("SK_MULTI_BLOCK")) e->multi_block = std::atoi(mb);
+  e->multi_stagger = 0;
+  if (const char* mg = std::getenv("SK_MULTI_STAGGER")) e->multi_stagger = std::atoi(mg);
+  e->multi_pack = 1;
+  if (const char* mk = std::getenv("SK_MULTI_PACK")) e->multi_pack = std::atoi(mk);
+  e->d_pack = nullptr;
   if (view) {
     if (view->n_envs != n || !view->pos || !view->rot || !view->qpos || !view->qrot || !view->qcdage ||
         !view->misc) {
@@ -1342,6 +1523,7 @@ int sk_env_destroy(sk_env* e) {
   (void)hipSetDevice(e->device);
   if (e->owned) (void)hipFree(e->hview.pos);
   (void)hipFree(e->d_aux);
+  if (e->d_pack) (void)hipFree(e->d_pack);
   delete e;
   return SK_OK;
 }
@@ -1657,6 +1839,13 @@ int sk_env_step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64
   a.ctr = e->d_counters;
   a.base = nullptr;
   for (int k = 0; k < 6; ++k) a.off[k] = 0;
+  a.pack = nullptr;
+  if (n_ticks > 1 && e->multi_pack && (uint64_t)e->n * 48u <= 0xffffffffull) {
+    if (!e->d_pack) {
+      if (hipMalloc(&e->d_pack, (size_t)e->n * 48) != hipSuccess) return fail(SK_ENOMEM, "hipMalloc pack");
+    }
+    a.pack = e->d_pack;
+  }
   int pol = e->multi_policy;
   if (pol == 1) {  // one buffer resource over the planes: they must lie within 4 GiB of the lowest
     const char* p[6] = {(const char*)e->hview.pos, (const char*)e->hview.rot, (const char*)e->hview.qpos,
@@ -1669,19 +1858,35 @@ int sk_env_step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64
       ok &= end <= 0xffffffffull;
       a.off[k] = (uint32_t)(p[k] - lo);
     }
-    if (!ok) return fail(SK_EINVAL, "SK_MULTI_POLICY=1 needs the state planes within 4 GiB of each other");
-    a.base = lo;
+    // planes farther apart than one 32-bit buffer offset (a caller's own
+    // allocations; VecSkillshotGame and sk_env_create use one block): the
+    // plain port, same results
+    if (ok) a.base = lo;
+    else pol = 0;
   }
   // geometry: one lane per game (k_step_multi) or two (k_step_split_multi);
   // SK_MULTI_SPLIT = 0 / 1 forces one, else auto (kSplitMultiMaxEnvs)
   const bool split = e->multi_split >= 0 ? e->multi_split != 0 : (int64_t)e->n <= kSplitMultiMaxEnvs;
   const hipStream_t hs = (hipStream_t)stream;
   if (split) {
-    if (pol == 1) k_step_split_multi<1><<<step_grid(2 * (int64_t)e->n), kStepBlock, 0, hs>>>(a, e->dcfg);
-    else k_step_split_multi<0><<<step_grid(2 * (int64_t)e->n), kStepBlock, 0, hs>>>(a, e->dcfg);
+    const int64_t lanes = 2 * (int64_t)e->n;
+    const bool wide = e->multi_block == 512 || (e->multi_block < 0 && lanes >= 512 * 256);
+    const unsigned g512 = (unsigned)((lanes + 511) / 512);
+    if (wide) {
+      if (pol == 1) k_step_split_multi<1, 512><<<g512, 512, 0, hs>>>(a, e->dcfg, e->multi_stagger);
+      else k_step_split_multi<0, 512><<<g512, 512, 0, hs>>>(a, e->dcfg, e->multi_stagger);
+    } else {
+      if (pol == 1) k_step_split_multi<1, kStepBlock><<<step_grid(lanes), kStepBlock, 0, hs>>>(a, e->dcfg, 0);
+      else k_step_split_multi<0, kStepBlock><<<step_grid(lanes), kStepBlock, 0, hs>>>(a, e->dcfg, 0);
+    }
   } else {
-    if (pol == 1) k_step_multi<1><<<step_grid(e->n), kStepBlock, 0, hs>>>(a, e->dcfg);
-    else k_step_multi<0><<<step_grid(e->n), kStepBlock, 0, hs>>>(a, e->dcfg);
+    // the restart draw under the loads (k_step's early draw) is off by
+    // default here: 65,536 games 2.73 vs 2.81 us per tick at 20 ticks per
+    // launch, 131,072 3.69 vs 3.70 / 3.33 vs 3.37 (profiles/r03i_multi_fast_early_sweep.jsonl)
+    const int early = e->multi_early > 0;
+    const unsigned g = step_grid(e->n);
+    if (pol == 1) k_step_multi<1><<<g, kStepBlock, 0, hs>>>(a, e->dcfg, early);
+    else k_step_multi<0><<<g, kStepBlock, 0, hs>>>(a, e->dcfg, early);
   }
   SK_LAUNCH_CHECK();
   e->parity ^= 1;

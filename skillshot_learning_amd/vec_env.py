@@ -69,8 +69,15 @@ class VecSkillshotGame:
         self.tick_limit = int(tick_limit)
         self.random_positions = bool(random_positions)
         self._L = _capi.load()
+        # one allocation, the planes back to back (88 B per game, every plane
+        # 16-byte aligned): the multi-tick kernels address all six through
+        # one buffer resource with 32-bit offsets (sk_env_step_multi)
+        self._state_buf = torch.zeros(88 * self.n, dtype=torch.uint8, device=self.device)
+        off = 0
         for name, dt, w in PLANES:
-            setattr(self, name, torch.zeros((self.n, w), dtype=dt, device=self.device))
+            nbytes = self.n * w * torch.empty((), dtype=dt).element_size()
+            setattr(self, name, self._state_buf[off:off + nbytes].view(dt).view(self.n, w))
+            off += nbytes
         view = _capi.SkStateView(self.n, *[getattr(self, name).data_ptr() for name, _, _ in PLANES])
         cfg = config if config is not None else _capi.default_config()
         self.config = cfg

@@ -20,10 +20,18 @@ def ssa():
     return m
 
 
-@pytest.fixture(params=["0", "1"], ids=["lane_per_game", "player_split"])
+@pytest.fixture(params=["0", "0e", "1", "1w"],
+                ids=["lane_per_game", "lane_per_game_early_draw", "player_split", "player_split_512"])
 def split(request, monkeypatch):
-    """both multi-tick geometries (k_step_multi, k_step_split_multi) meet the same bar"""
-    monkeypatch.setenv("SK_MULTI_SPLIT", request.param)
+    """every multi-tick geometry (k_step_multi, with or without the restart
+    draw under the loads; k_step_split_multi on 64-lane workgroups, and on
+    512-lane ones with waves 4-7 staggered) meets the same bar"""
+    monkeypatch.setenv("SK_MULTI_SPLIT", request.param[0])
+    if request.param == "0e":
+        monkeypatch.setenv("SK_MULTI_EARLY", "1")
+    if request.param == "1w":
+        monkeypatch.setenv("SK_MULTI_BLOCK", "512")
+        monkeypatch.setenv("SK_MULTI_STAGGER", "2")
     return request.param
 
 
@@ -99,3 +107,30 @@ def test_step_multi_cpu_backend_equals_gpu(ssa, monkeypatch, split):
     assert np.array_equal(wg.cpu().numpy(), wc.numpy())
     _same_state(g, c)
     assert g.counters() == c.counters()
+
+
+@pytest.mark.parametrize("pack", ["1", "0"], ids=["packed", "exchange_form"])
+def test_step_multi_states_outside_the_packed_range(ssa, monkeypatch, split, pack):
+    """Games whose fields do not fit the packed resident form (cooldown far
+    below -128, ages past 255, ticks past 65,535, a projectile 'valid' byte of
+    3, positions off the board) keep their wave in the 88-B form; every other
+    wave packs.  Both equal the stepwise kernels bit for bit."""
+    monkeypatch.setenv("SK_MULTI_PACK", pack)
+    n, T, R = 6000, 40, 3
+    a, b = _pair(ssa, n, 33, 10 ** 6, monkeypatch, 1)
+    st = a.state_dict()
+    rng = np.random.default_rng(0)
+    idx = rng.choice(n, 40, replace=False)
+    st["qcdage"][idx[:10], 0] = -900
+    st["qcdage"][idx[10:20], 3] = 100000
+    st["misc"][idx[20:30], 0] = 70000
+    st["misc"][idx[30:35], 1] = (st["misc"][idx[30:35], 1] & ~0xFF) | 3
+    st["pos"][idx[35:40], 0] = 300
+    for g in (a, b):
+        g.load_state_dict(st)
+    acts = a.gen_random_actions(R)
+    done, win = a.step_multi(acts, n_ticks=T, record=True)
+    for t in range(T):
+        o = b.step(acts[t % R], obs=False, auto_reset=True)
+        assert torch.equal(done[t], o["done"]) and torch.equal(win[t], o["winner"]), t
+    _same_state(a, b)

@@ -18,7 +18,10 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 
-def multi_rate(n, T, pol, split=-1, stagger=0, K=2000, ring=400, seed=0):
+def multi_rate(n, T, pol, split=-1, stagger=0, block=-1, fast=0, early=-1, K=2000, ring=400, seed=0):
+    os.environ["SK_MULTI_FAST"] = str(fast)
+    os.environ["SK_MULTI_EARLY"] = str(early)
+    os.environ["SK_MULTI_BLOCK"] = str(block)
     os.environ["SK_MULTI_POLICY"] = str(pol)
     os.environ["SK_MULTI_SPLIT"] = str(split)
     os.environ["SK_MULTI_STAGGER"] = str(stagger)
@@ -51,7 +54,7 @@ def multi_rate(n, T, pol, split=-1, stagger=0, K=2000, ring=400, seed=0):
     st.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / (launches * T)
     env.close()
-    return dict(kind="multi", envs=n, ticks_per_launch=T, policy=pol, split=split, stagger=stagger, us_per_tick=us,
+    return dict(kind="multi", envs=n, ticks_per_launch=T, policy=pol, split=split, stagger=stagger, block=block, fast=fast, early=early, us_per_tick=us,
                 env_steps_per_s=n / (us * 1e-6), frac=193 * n / (us * 1e-6) / 8e12)
 
 
@@ -71,6 +74,9 @@ def main():
     p.add_argument("--reps", type=int, default=2)
     p.add_argument("--splits", default="-1")
     p.add_argument("--staggers", default="0")
+    p.add_argument("--blocks", default="-1")
+    p.add_argument("--fasts", default="0")
+    p.add_argument("--earlys", default="-1")
     p.add_argument("--no-graph", action="store_true")
     a = p.parse_args()
     torch.cuda.set_device(0)
@@ -82,7 +88,11 @@ def main():
                 for sp in [int(x) for x in a.splits.split(",")]:
                     for T in [int(x) for x in a.ticks.split(",")]:
                         for sg in [int(x) for x in a.staggers.split(",")]:
-                            print(json.dumps(dict(multi_rate(n, T, pol, sp, sg), rep=rep)), flush=True)
+                            for bk in [int(x) for x in a.blocks.split(",")]:
+                                for fa in [int(x) for x in a.fasts.split(",")]:
+                                    for ea in [int(x) for x in a.earlys.split(",")]:
+                                        print(json.dumps(dict(multi_rate(n, T, pol, sp, sg, bk, fa, ea), rep=rep)),
+                                              flush=True)
 
 
 if __name__ == "__main__":
