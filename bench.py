@@ -443,13 +443,88 @@ def learner_rate(envs, world, rank, ticks, batch=256, exploration="param_noise",
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
     n_ticks = (ticks // 2) * 2
+    gpu_ms = e0.elapsed_time(e1) / n_ticks
     out = dict(envs_per_gpu=envs, total_envs=envs * world, n_gpus=world, ticks=n_ticks, batch_per_rank=batch,
                exploration=exploration, updates_per_tick=1, dtype=precision, multi_rank=tg.multi_rank_mode,
                env_steps_per_s=envs * world * n_ticks / el, ms_per_tick=el * 1e3 / n_ticks,
-               gpu_ms_per_tick=e0.elapsed_time(e1) / n_ticks, episodes=L.game_environment.counters())
+               gpu_ms_per_tick=gpu_ms,
+               episodes=L.game_environment.counters(stream=ctypes.c_void_p(tg.stream.cuda_stream)))
+    try:
+        out["roofline"] = learner_roofline(L, tg, batch, precision, exploration, gpu_ms)
+    except Exception as e:  # noqa: BLE001 (a measurement beside the leg must not cost it)
+        out["roofline_error"] = f"{type(e).__name__}: {e}"
     del tg, L
     torch.cuda.empty_cache()
     return out
+
+
+ACTOR_FLOP_ROW = 72192   # 2 x (12*256 + 256*128 + 128*2) multiply-adds per row
+CRITIC_FLOP_ROW = 72448  # A16: 2 x (12*256 + 258*128 + 128*1)
+MFMA_PEAK_TF = {"fp32": 157.3, "bf16": 2500.0}  # MI355X_MICROARCH.md: f32 MFMA 157.3 TF; bf16 ~2.5 PF dense
+
+
+def learner_roofline(L, tg, batch, precision, exploration, gpu_ms_per_tick, reps=20):
+    """MFMA roofline of a learner leg: the tick's three
+    GEMM-chain kernels timed one by one on the learner's own nets, with HIP
+    events around `reps` eager launches on the leg's stream, after its timed
+    region — the actor forward for both players of every game (2N rows; with
+    parameter noise the local-reparameterisation variance GEMM doubles its
+    FLOPs), the critic gradient on a replay minibatch (critic forward +
+    backward, bootstrap target nets' forwards: 3 x critic + actor + critic
+    FLOP per row) and the actor gradient (actor forward + backward, critic
+    forward + input backward: 3 x actor + 2 x critic).  `achieved` is the
+    dominant (longest) kernel's FLOPs / its average launch; `tick_tflops` the
+    whole tick's FLOPs / the tick's GPU time."""
+    fu = L.ddpg._fused
+    if fu is None:
+        raise RuntimeError("no fused update path")
+    st = tg.stream
+    rows = tg.obs.view(-1, 12).shape[0]
+    x = tg.obs.view(-1, 12)
+    act = torch.empty((rows, 2), dtype=torch.float32, device=L.device)
+    s, a, r, s2, d = [t.contiguous() for t in L.replay.sample(batch)]
+    part_c = fu._partial(batch, fu.fc.numel())
+    part_a = fu._partial(batch, fu.fa.numel())
+    noise = L.param_noise_sd if exploration == "param_noise" else 0.0
+    ak = L.actor_kernel
+
+    def actor():
+        if exploration == "action_noise" and getattr(ak, "fused_action_noise", False):
+            ak(x, out=act, action_sd=L.action_noise_sd)
+        else:
+            ak(x, noise_sd=noise, out=act)
+
+    def critic():
+        fu._critic_grad(s, a, None, s2, r, d, float(L.ddpg.gamma or 0.0), 0, batch, part_c, None, None, stat=False)
+
+    def actor_g():
+        fu._actor_grad(s, part_a, None, None)
+
+    jobs = {"actor_forward": (actor, rows * ACTOR_FLOP_ROW * (2 if noise else 1)),
+            "critic_grad": (critic, batch * (4 * CRITIC_FLOP_ROW + ACTOR_FLOP_ROW)),
+            "actor_grad": (actor_g, batch * (3 * ACTOR_FLOP_ROW + 2 * CRITIC_FLOP_ROW))}
+    kern = {}
+    with torch.cuda.stream(st):
+        for name, (fn, flop) in jobs.items():
+            fn()
+            fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(reps):
+                fn()
+            e1.record(st)
+            st.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / reps
+            kern[name] = dict(us=us, flop=flop, tflops=flop / (us * 1e-6) / 1e12)
+    dom = max(kern, key=lambda k: kern[k]["us"])
+    peak = MFMA_PEAK_TF[precision]
+    tick_flop = sum(v["flop"] for v in kern.values())
+    return dict(bound="mfma", achieved=kern[dom]["tflops"], peak=peak, unit="TFLOP/s",
+                frac=kern[dom]["tflops"] / peak, traffic=None, kernel=dom, kernel_us=kern[dom]["us"],
+                kernels=kern, tick_flop=tick_flop, tick_tflops=tick_flop / (gpu_ms_per_tick * 1e-3) / 1e12,
+                tick_frac=tick_flop / (gpu_ms_per_tick * 1e-3) / 1e12 / peak,
+                note="kernel times: HIP events over eager launches after the timed region; "
+                     "FLOP per row from SURVEY §8(a)/(d)")
 
 
 def _log(msg):
@@ -673,10 +748,15 @@ def main():
                 learner[f"config5_1gpu_{prec}"] = _guard(f"learner.config5_1gpu_{prec}", lambda: learner_rate(
                     65536, 1, 0, T, batch=256, exploration="param_noise", precision=prec), errors)
         else:
+            # every leg at the reference's fp32 (Keras) precision; config 5 at
+            # bf16 beside it (the bf16 leg alone was narrower
+            # than the reference)
             legs = (("config4", dict(envs=32768 // world, batch=256, exploration="action_noise", precision="fp32",
                                      multi_rank="grad", ticks=T)),
-                    ("config5", dict(envs=65536 // world, batch=256, exploration="param_noise", precision="bf16",
-                                     multi_rank="shared", ticks=T)))
+                    ("config5", dict(envs=65536 // world, batch=256, exploration="param_noise", precision="fp32",
+                                     multi_rank="shared", ticks=T)),
+                    ("config5_bf16", dict(envs=65536 // world, batch=256, exploration="param_noise",
+                                          precision="bf16", multi_rank="shared", ticks=T)))
             for k, (name, cfg) in enumerate(legs):
                 dist.barrier()
                 if verbose:

@@ -389,12 +389,17 @@ class DDPG:
     Per-rank update work is `batch` rows whatever the world size."""
 
     def __init__(self, device="cpu", seed=0, batch_size=16, gamma=0.0, tau=None, replay_capacity=0,
-                 process_group=None, rank_seed_offset=0, fused_update=None, multi_rank="grad", precision="bf16"):
+                 process_group=None, rank_seed_offset=0, fused_update=None, multi_rank="grad", precision="bf16",
+                 force_collectives=False):
         self.device = torch.device(device)
         torch.manual_seed(seed)
         self.model_actor = Actor().to(self.device)
         self.model_critic = Critic().to(self.device)
         self.group = process_group
+        # run the multi-rank update (collectives and all) even on a 1-rank
+        # group: a one-GPU rehearsal of the RCCL path that configs 4 and 5
+        # take (tests/test_rccl_capture_gpu.py)
+        self.force_collectives = bool(force_collectives)
         if multi_rank not in ("grad", "shared"):
             raise ValueError("multi_rank must be 'grad' or 'shared'")
         self.multi_rank = multi_rank
@@ -435,6 +440,11 @@ class DDPG:
     def rank(self):
         return dist.get_rank(self.group) if self.world() > 1 else 0
 
+    def multi(self):
+        """the update goes through the collectives (more than one rank, or a
+        forced 1-rank rehearsal)"""
+        return self.world() > 1 or (self.force_collectives and dist.is_available() and dist.is_initialized())
+
     def _sync_params(self):
         """Start every rank from rank 0's weights (broadcast)."""
         if self.world() > 1:
@@ -461,7 +471,7 @@ class DDPG:
         """Gradient all-reduce (sum: each rank's loss is already normalised
         by the global batch) as ONE flat bucket per update: 36,482 actor /
         36,609 critic fp32 parameters (RCCL over xGMI)."""
-        if self.world() <= 1:
+        if not self.multi():
             return
         grads = [p.grad for p in module.parameters()]
         flat = torch.cat([g.reshape(-1) for g in grads])
@@ -477,7 +487,7 @@ class DDPG:
         one all-gather of a packed buffer; returns the [world*b] batch (rank
         0's rows first)."""
         w = self.world()
-        if w <= 1:
+        if not self.multi():
             return tensors
         flat = torch.cat([t.reshape(t.shape[0], -1) for t in tensors], dim=1).contiguous()
         out = torch.empty((w * flat.shape[0], flat.shape[1]), device=flat.device, dtype=flat.dtype)
@@ -568,7 +578,7 @@ class DDPG:
     def update_batch(self, s, a, r, s2, d):
         """replay_update on this rank's sampled rows s, a, r, s2, d."""
         w, rk, b = self.world(), self.rank(), s.shape[0]
-        if w > 1 and self.multi_rank == "shared":
+        if self.multi() and self.multi_rank == "shared":
             s, a, r, s2, d = [t[rk::w] for t in self._allgather_batch(s, a, r, s2, d)]
         row0, gb = rk * b, w * b
         if w > 1 and b % 4:
@@ -645,7 +655,7 @@ class SkillshotLearner:
     def __init__(self, n_envs=1, device="cuda", seed=0, env_offset=0, exploration="param_noise",
                  tick_limit=2000, use_random_start=True, replay_capacity=1 << 20, batch_size=16,
                  gamma=0.0, tau=None, actor_kernel=True, process_group=None, precision="bf16",
-                 multi_rank="grad"):
+                 multi_rank="grad", force_collectives=False):
         from .vec_env import VecSkillshotGame
         if precision not in ("bf16", "fp32"):
             raise ValueError("precision must be 'bf16' or 'fp32'")
@@ -671,7 +681,7 @@ class SkillshotLearner:
         self.training_progress_dir_name, self.training_boards_dir_name = "training_progress", "training_boards"
         self.ddpg = DDPG(self.device, seed=seed, batch_size=batch_size, gamma=gamma, tau=tau,
                          replay_capacity=replay_capacity, process_group=process_group, rank_seed_offset=env_offset,
-                         multi_rank=multi_rank, precision=precision)
+                         multi_rank=multi_rank, precision=precision, force_collectives=force_collectives)
         self.gen = self.ddpg.gen
         self.actor_kernel = None
         if actor_kernel and self.device.type == "cuda":
@@ -920,9 +930,8 @@ class TickGraph:
 
     def __init__(self, L, batch, updates_per_tick, ticks_per_graph, warmup):
         self.L, self.batch, self.updates, self.ticks = L, batch, updates_per_tick, ticks_per_graph
-        world = L.ddpg.world()
         self.multi_rank_mode = None
-        if world > 1:
+        if L.ddpg.multi():
             mode = os.environ.get("SK_TICKGRAPH_MODE") or (
                 "full" if dist.get_backend(L.ddpg.group) == "nccl" else "segmented")
             if mode not in ("full", "segmented"):

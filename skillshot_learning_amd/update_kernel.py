@@ -219,8 +219,7 @@ class FusedUpdate:
                 packs = PackTargets(packs.param_gpack, None, packs.actor_fwd_pack, packs.ld2, packs.n_out)
         pk = ctypes.byref(packs) if packs is not None else None
         tau = float(self.d.tau) if target is not None else 0.0
-        world = self.d.world()
-        if world > 1:  # sum partials -> flat grad -> RCCL sum (losses are global-batch normalised) -> apply
+        if self.d.multi():  # sum partials -> flat grad -> RCCL sum (losses are global-batch normalised) -> apply
             if self.grad_flat is None or self.grad_flat.numel() < P:
                 self.grad_flat = torch.empty(max(36609, P), dtype=torch.float32, device=self.dev)
             g = self.grad_flat[:P]
