@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Benchmark: env-steps/s of the fused Skillshot step kernel on MI355X.
+"""Benchmark: env-steps/s of the Skillshot step kernels on MI355X.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--envs 65536]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
@@ -10,23 +10,28 @@ envs; 1/2/4/8 GPU scaling", SURVEY.md §8(d) config 2 at the metric's size and
 §8(e)): 65,536 games IN TOTAL, split over the N ranks by contiguous global id
 (65,536 / 32,768 / 16,384 / 8,192 per GPU at N = 1 / 2 / 4 / 8: "scaling":
 "strong", no data-path collective), random policy.  One bench step = one
-k_step launch over all of a GPU's games: both players' do_actions
+tick of every game on a GPU: both players' do_actions
 (SkillshotLearner.py:206-213) + game_tick (SkillshotGame.py:115-122) + done
-+ random auto-reset.  Actions are Philox uniform(-1,1) float32 pre-generated
-into HBM (K4, not timed), a distinct 1 MiB slab per tick, read from a ring
-larger than the 256 MiB Infinity Cache.  Whatever K and W are, the launches
-are replayed from hipGraphs (TickGraphs below: a chunk graph of --graph-len
-launches replayed K // len times plus one remainder graph), so the timed
-region never holds eager ctypes launches.  Weak scaling (65,536 games per GPU)
-is reported beside it for N > 1.
++ random auto-reset, with every game's state loaded from and stored to memory
+(write-through: the bytes leave the L2 every tick).  Actions are Philox
+uniform(-1,1) float32 pre-generated into HBM (K4, not timed), a distinct
+1 MiB slab per tick, read from a ring larger than the 256 MiB Infinity Cache.
+The K ticks run in ceil(K / --ticks-per-launch) k_step_multi launches
+(sk_env_step_multi; the driver's --steps 20 is one launch of 20 ticks).  The
+round-2 headline (one graph-replayed k_step launch per tick) and the
+L2-resident state port are reported beside it (step_variants).  Weak scaling
+(65,536 games per GPU) is reported beside it for N > 1.
 
 Roofline: algorithmic bytes per env-step = 193 B (state 88 B read + 88 B
-written, actions 16 B, done 1 B: SURVEY.md §8(d)); average launch duration =
-HIP-event span of the timed region on the launch stream / K.  `traffic` comes
-from the committed PMC pass (profiles/traffic_k_step.json, rocprofv3 --pmc
-FETCH_SIZE / WRITE_SIZE), not from this run.  cpu_baseline: the
-C oracle (a port of the reference step) on the box's host cores over a
-bounded sample of the same workload.
+written, actions 16 B, done 1 B: SURVEY.md §8(d)); the kernels' time = the
+HIP-event span of the timed region on the launch stream / K.  (Events
+recorded by the launches themselves, hipExtLaunchKernel, read 2-4 % less but
+cost ~14 us of host time per launch: profiles/r03k_bench_k20_kernel_events.json.)  `traffic` comes
+from the committed PMC pass (profiles/traffic_k_step_multi.json, rocprofv3
+--pmc FETCH_SIZE / WRITE_SIZE, per tick), not from this run.
+cpu_baseline: the C oracle (a port of the reference step) on the box's host
+cores over a bounded sample of the same workload.  The learner legs (configs
+3-5) carry an MFMA roofline of their dominant kernel.
 """
 import argparse
 import ctypes
@@ -314,6 +319,7 @@ def timed_multi(dev, n, seed, env_offset, tick_limit, k, warmup, ring, world, pe
     slab = 0
 
     def run(m):
+        """m ticks in launches of at most per_launch"""
         nonlocal slab
         while m > 0:
             t = min(m, per_launch)
@@ -327,8 +333,8 @@ def timed_multi(dev, n, seed, env_offset, tick_limit, k, warmup, ring, world, pe
 
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(st)  # torch creates the HIP events at their first record: not inside the timed region
-    run(1)  # the first launch loads the code object
     e1.record(st)
+    run(1)  # the first launch loads the code object
     st.synchronize()
     env.clear_counters(stream=sp)
     if trace is not None:
@@ -339,7 +345,7 @@ def timed_multi(dev, n, seed, env_offset, tick_limit, k, warmup, ring, world, pe
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    e0.record(st)  # (a `with torch.cuda.stream` block costs ~9 us of host time per record)
+    e0.record(st)
     run(k)
     e1.record(st)
     torch.cuda.synchronize()

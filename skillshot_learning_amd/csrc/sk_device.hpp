@@ -219,6 +219,13 @@ __device__ __forceinline__ void store_env_q(const View& v, int64_t i, const Env&
 #endif
 }
 
+// ---------------------------------------------------------------- lane pairs
+// The partner lane's value (lane ^ 1) for the player-per-lane kernels: DPP
+// quad_perm [1,0,3,2], one VALU instruction, instead of __shfl_xor(v, 1)'s
+// ds_bpermute (an LDS round trip on the tick's dependent chain).  Every lane
+// of the wave must be active (the callers use it at the top level).
+__device__ __forceinline__ int pair_swap(int v) { return __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false); }
+
 // ---------------------------------------------------------------- Philox4x32-10
 struct U4 { uint32_t x, y, z, w; };
 

@@ -12,6 +12,7 @@
 //                     the reference's per-method API, batched
 // Episode counters: wavefront ballots + popcount into one 128-B slot line per
 // wave, read-modify-written without atomics (see "counters" below).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -489,7 +490,7 @@ __global__ void __launch_bounds__(kStepBlock) k_step_fast(StepArgs a, Cfg c) {
 // pair covering the env's 16 bytes: still fully coalesced), runs that
 // player's do_actions and projectile tick (a player's actions never read the
 // other player), then the pair swaps positions/projectiles with one
-// __shfl_xor(.,1) each for the collision test, which both lanes evaluate
+// pair_swap (DPP) each for the collision test, which both lanes evaluate
 // identically.  Twice the waves of k_step, half the dependent chain per lane.
 __global__ void __launch_bounds__(kStepBlock) k_step_split(StepArgs a, Cfg c) {
   const int64_t gt = (int64_t)blockIdx.x * kStepBlock + threadIdx.x;
@@ -545,8 +546,8 @@ __global__ void __launch_bounds__(kStepBlock) k_step_split(StepArgs a, Cfg c) {
     ticks += 1;
     projectile_tick_sc(c, qx, qy, t, qcd, qage, qvalid);
   }
-  const int opx = __shfl_xor(px, 1, 64), opy = __shfl_xor(py, 1, 64);
-  const int oqx = __shfl_xor(qx, 1, 64), oqy = __shfl_xor(qy, 1, 64), oqv = __shfl_xor(qvalid, 1, 64);
+  const int opx = pair_swap(px), opy = pair_swap(py);
+  const int oqx = pair_swap(qx), oqy = pair_swap(qy), oqv = pair_swap(qvalid);
   if (live) {
     if (p == 0) collide_s(c, px, py, qx, qy, qvalid, opx, opy, oqx, oqy, oqv, live, winner);
     else collide_s(c, opx, opy, oqx, oqy, oqv, px, py, qx, qy, qvalid, live, winner);
@@ -603,7 +604,7 @@ __global__ void __launch_bounds__(kStepBlock) k_step_split(StepArgs a, Cfg c) {
     // a game that did not restart acts next on the obs just computed; a
     // restarted one (both lanes of the pair) on its fresh state's, whose
     // rotations are 0 (sin 0, cos 1: no trig) and projectile invalid
-    const int rpx = __shfl_xor(px, 1, 64), rpy = __shfl_xor(py, 1, 64);
+    const int rpx = pair_swap(px), rpy = pair_swap(py);
     if (reset) {  // (its projectile is invalid: the flag is 0, never ambiguous)
       float pd;
       bool amb_r;
@@ -617,7 +618,7 @@ __global__ void __launch_bounds__(kStepBlock) k_step_split(StepArgs a, Cfg c) {
   reinterpret_cast<int2*>(a.v.qpos)[h] = make_int2(qx, qy);
   reinterpret_cast<double*>(a.v.qrot)[h] = qrot;
   reinterpret_cast<int2*>(a.v.qcdage)[h] = make_int2(qcd, qage);
-  const int ov = __shfl_xor(qvalid, 1, 64);
+  const int ov = pair_swap(qvalid);
   if (p == 0) {
     unsigned f = (unsigned)(qvalid & 0xff) | ((unsigned)(ov & 0xff) << 8) | ((unsigned)(live & 0xff) << 16) |
                  ((unsigned)(winner & 0xff) << 24);
@@ -984,7 +985,7 @@ __global__ void __launch_bounds__(kStepBlock) k_step_multi(MultiArgs a, Cfg c, i
 // 2i+1) own players 1 and 2 of game i, each loading and storing its player's
 // 8-byte half of every plane (the pair covers the game's 16 bytes; a wave
 // moves 512 contiguous bytes per plane), exchanging positions / projectiles
-// with __shfl_xor(., 1) for the collision test.  Twice the waves of
+// with pair_swap (DPP) for the collision test.  Twice the waves of
 // k_step_multi at half the dependent chain per lane: at 65,536 games two
 // waves share each SIMD, so one wave's state round trip through memory
 // overlaps the other's tick.  Same contract, same state ports, same packed
@@ -1056,7 +1057,7 @@ __device__ __forceinline__ void split_multi_tick(const MultiArgs& a, const Cfg& 
     px = s0 & 0xff; py = (s0 >> 8) & 0xff; qx = (s0 >> 16) & 0xff; qy = s0 >> 24;
     qcd = (int)(signed char)(c0 & 0xff);
     qage = (c0 >> 8) & 0xff;
-    const unsigned hi = c0 >> 16, other = (unsigned)__shfl_xor((int)hi, 1, 64);
+    const unsigned hi = c0 >> 16, other = (unsigned)pair_swap((int)hi);
     ticks = (int)(p == 0 ? hi : other);
     const unsigned fl = p == 0 ? other : hi;
     qvalid = (fl >> p) & 1;
@@ -1098,8 +1099,8 @@ __device__ __forceinline__ void split_multi_tick(const MultiArgs& a, const Cfg& 
     ticks += 1;
     projectile_tick_sc(c, qx, qy, tq, qcd, qage, qvalid);
   }
-  const int opx = __shfl_xor(px, 1, 64), opy = __shfl_xor(py, 1, 64);
-  const int oqx = __shfl_xor(qx, 1, 64), oqy = __shfl_xor(qy, 1, 64), oqv = __shfl_xor(qvalid, 1, 64);
+  const int opx = pair_swap(px), opy = pair_swap(py);
+  const int oqx = pair_swap(qx), oqy = pair_swap(qy), oqv = pair_swap(qvalid);
   if (live) {
     if (p == 0) collide_s(c, px, py, qx, qy, qvalid, opx, opy, oqx, oqy, oqv, live, winner);
     else collide_s(c, opx, opy, oqx, oqy, oqv, px, py, qx, qy, qvalid, live, winner);
@@ -1127,7 +1128,7 @@ __device__ __forceinline__ void split_multi_tick(const MultiArgs& a, const Cfg& 
     rot = 0.0; qx = 0; qy = 0; qrot = 0.0; qcd = 0; qage = 0; qvalid = 0;
     ticks = 0; live = 1; winner = 0;
   }
-  const int ov = __shfl_xor(qvalid, 1, 64);
+  const int ov = pair_swap(qvalid);
   const bool fit = !L.in || (pack_fits_player(px, py, qx, qy, qcd, qage, qvalid) & pack_fits_game(ticks, live, winner));
   const bool to_pack = a.pack != nullptr && !last && __ballot(!fit) == 0;  // wave-uniform
   const bool qch = __double_as_longlong(qrot) != __double_as_longlong(q_old);
@@ -1332,6 +1333,21 @@ __global__ void __launch_bounds__(kBlock) k_features(View v, int64_t n, double* 
     double* d = feat + (i * 2 + p) * 18;
     for (int k = 0; k < 18; ++k) d[k] = f[k];
   }
+}
+
+// A launch that records `e0` as its first wave starts and `e1` after its
+// last wave ends (hipExtLaunchKernel; either may be NULL): the kernel's own
+// duration on its stream, without the host-side gap between a separate
+// event record and the launch.
+template <typename... P, typename... A>
+static hipError_t launch_timed(void (*k)(P...), dim3 grid, dim3 block, hipStream_t s, hipEvent_t e0, hipEvent_t e1,
+                               A... args) {
+  if (!e0 && !e1) {
+    k<<<grid, block, 0, s>>>(args...);
+    return hipGetLastError();
+  }
+  void* argv[] = {static_cast<void*>(&args)...};
+  return hipExtLaunchKernel(reinterpret_cast<const void*>(k), grid, block, argv, 0, s, e0, e1, 0);
 }
 
 // ------------------------------------------------------------------ host ABI
@@ -1868,27 +1884,28 @@ int sk_env_step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64
   // SK_MULTI_SPLIT = 0 / 1 forces one, else auto (kSplitMultiMaxEnvs)
   const bool split = e->multi_split >= 0 ? e->multi_split != 0 : (int64_t)e->n <= kSplitMultiMaxEnvs;
   const hipStream_t hs = (hipStream_t)stream;
+  hipEvent_t e0 = nullptr, e1 = nullptr;  // launch_timed's events (A/B hook; unused by the ABI)
+  hipError_t err;
   if (split) {
     const int64_t lanes = 2 * (int64_t)e->n;
     const bool wide = e->multi_block == 512 || (e->multi_block < 0 && lanes >= 512 * 256);
-    const unsigned g512 = (unsigned)((lanes + 511) / 512);
-    if (wide) {
-      if (pol == 1) k_step_split_multi<1, 512><<<g512, 512, 0, hs>>>(a, e->dcfg, e->multi_stagger);
-      else k_step_split_multi<0, 512><<<g512, 512, 0, hs>>>(a, e->dcfg, e->multi_stagger);
-    } else {
-      if (pol == 1) k_step_split_multi<1, kStepBlock><<<step_grid(lanes), kStepBlock, 0, hs>>>(a, e->dcfg, 0);
-      else k_step_split_multi<0, kStepBlock><<<step_grid(lanes), kStepBlock, 0, hs>>>(a, e->dcfg, 0);
-    }
+    const dim3 g512((unsigned)((lanes + 511) / 512)), g64(step_grid(lanes));
+    if (wide)
+      err = pol == 1 ? launch_timed(k_step_split_multi<1, 512>, g512, dim3(512), hs, e0, e1, a, e->dcfg, e->multi_stagger)
+                     : launch_timed(k_step_split_multi<0, 512>, g512, dim3(512), hs, e0, e1, a, e->dcfg, e->multi_stagger);
+    else
+      err = pol == 1 ? launch_timed(k_step_split_multi<1, kStepBlock>, g64, dim3(kStepBlock), hs, e0, e1, a, e->dcfg, 0)
+                     : launch_timed(k_step_split_multi<0, kStepBlock>, g64, dim3(kStepBlock), hs, e0, e1, a, e->dcfg, 0);
   } else {
     // the restart draw under the loads (k_step's early draw) is off by
     // default here: 65,536 games 2.73 vs 2.81 us per tick at 20 ticks per
     // launch, 131,072 3.69 vs 3.70 / 3.33 vs 3.37 (profiles/r03i_multi_fast_early_sweep.jsonl)
     const int early = e->multi_early > 0;
-    const unsigned g = step_grid(e->n);
-    if (pol == 1) k_step_multi<1><<<g, kStepBlock, 0, hs>>>(a, e->dcfg, early);
-    else k_step_multi<0><<<g, kStepBlock, 0, hs>>>(a, e->dcfg, early);
+    const dim3 g(step_grid(e->n));
+    err = pol == 1 ? launch_timed(k_step_multi<1>, g, dim3(kStepBlock), hs, e0, e1, a, e->dcfg, early)
+                   : launch_timed(k_step_multi<0>, g, dim3(kStepBlock), hs, e0, e1, a, e->dcfg, early);
   }
-  SK_LAUNCH_CHECK();
+  if (err != hipSuccess) return fail(SK_EHIP, std::string("k_step_multi launch: ") + hipGetErrorString(err));
   e->parity ^= 1;
   return SK_OK;
 }
