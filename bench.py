@@ -472,8 +472,8 @@ MFMA_PEAK_TF = {"fp32": 157.3, "bf16": 2500.0}  # MI355X_MICROARCH.md: f32 MFMA 
 def learner_roofline(L, tg, batch, precision, exploration, gpu_ms_per_tick, reps=20):
     """MFMA roofline of a learner leg: the tick's three
     GEMM-chain kernels timed one by one on the learner's own nets, with HIP
-    events around `reps` eager launches on the leg's stream, after its timed
-    region — the actor forward for both players of every game (2N rows; with
+    events around one graph replay of `reps` launches on the leg's stream,
+    after its timed region — the actor forward for both players of every game (2N rows; with
     parameter noise the local-reparameterisation variance GEMM doubles its
     FLOPs), the critic gradient on a replay minibatch (critic forward +
     backward, bootstrap target nets' forwards: 3 x critic + actor + critic
@@ -514,12 +514,20 @@ def learner_roofline(L, tg, batch, precision, exploration, gpu_ms_per_tick, reps
         for name, (fn, flop) in jobs.items():
             fn()
             fn()
+            st.synchronize()
+            # the reps captured and replayed as one graph: eager Python
+            # launches (10-80 us of host time each) would time the host
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=st):
+                for _ in range(reps):
+                    fn()
+            g.replay()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(st)
-            for _ in range(reps):
-                fn()
+            g.replay()
             e1.record(st)
             st.synchronize()
+            del g
             us = e0.elapsed_time(e1) * 1e3 / reps
             kern[name] = dict(us=us, flop=flop, tflops=flop / (us * 1e-6) / 1e12)
     dom = max(kern, key=lambda k: kern[k]["us"])
@@ -529,7 +537,7 @@ def learner_roofline(L, tg, batch, precision, exploration, gpu_ms_per_tick, reps
                 frac=kern[dom]["tflops"] / peak, traffic=None, kernel=dom, kernel_us=kern[dom]["us"],
                 kernels=kern, tick_flop=tick_flop, tick_tflops=tick_flop / (gpu_ms_per_tick * 1e-3) / 1e12,
                 tick_frac=tick_flop / (gpu_ms_per_tick * 1e-3) / 1e12 / peak,
-                note="kernel times: HIP events over eager launches after the timed region; "
+                note="kernel times: HIP events over a graph of `reps` launches after the timed region; "
                      "FLOP per row from SURVEY §8(a)/(d)")
 
 
