@@ -889,12 +889,12 @@ struct MultiLane {
 // order, so the next tick's state waited for the prefetched HBM loads anyway.
 // `packed` (wave-uniform): where the state lives now; `last`: the final tick
 // (its state goes to the exchange format).
-template <int POL>
+template <int POL, bool PACK>
 __device__ __forceinline__ void multi_tick(const MultiArgs& a, const Cfg& c, __amdgpu_buffer_rsrc_t r,
                                            __amdgpu_buffer_rsrc_t rp, MultiLane& L, WaveCtr& wc, int t, uint64_t step,
                                            int64_t slab, bool& packed, bool last) {
   Env e;
-  if (packed) load_env_pack<POL>(a, rp, L.ic, e);
+  if (PACK && packed) load_env_pack<POL>(a, rp, L.ic, e);
   else load_env_port<POL>(a, r, L.ic, e);
   const double q_old0 = e.qrot[0], q_old1 = e.qrot[1];
   __builtin_amdgcn_sched_barrier(0);
@@ -937,12 +937,16 @@ __device__ __forceinline__ void multi_tick(const MultiArgs& a, const Cfg& c, __a
       reset_fixed(c, e);
     }
   }
-  const bool fit = !L.in || (pack_fits_player(e.px[0], e.py[0], e.qx[0], e.qy[0], e.qcd[0], e.qage[0], e.qvalid[0]) &
-                             pack_fits_player(e.px[1], e.py[1], e.qx[1], e.qy[1], e.qcd[1], e.qage[1], e.qvalid[1]) &
-                             pack_fits_game(e.ticks, e.live, e.winner));
-  const bool to_pack = a.pack != nullptr && !last && __ballot(!fit) == 0;  // wave-uniform
+  bool to_pack = false;
+  if constexpr (PACK) {
+    const bool fit =
+        !L.in || ((int)pack_fits_player(e.px[0], e.py[0], e.qx[0], e.qy[0], e.qcd[0], e.qage[0], e.qvalid[0]) &
+                  (int)pack_fits_player(e.px[1], e.py[1], e.qx[1], e.qy[1], e.qcd[1], e.qage[1], e.qvalid[1]) &
+                  (int)pack_fits_game(e.ticks, e.live, e.winner));
+    to_pack = a.pack != nullptr && !last && __ballot(!fit) == 0;  // wave-uniform
+  }
   if (L.in) {
-    if (to_pack) {
+    if (PACK && to_pack) {
       const bool qch = !packed || (__double_as_longlong(e.qrot[0]) != __double_as_longlong(q_old0)) ||
                        (__double_as_longlong(e.qrot[1]) != __double_as_longlong(q_old1));
       store_env_pack<POL>(a, rp, L.i, e, qch);
@@ -953,7 +957,7 @@ __device__ __forceinline__ void multi_tick(const MultiArgs& a, const Cfg& c, __a
   packed = to_pack;
 }
 
-template <int POL>
+template <int POL, bool PACK>
 __global__ void __launch_bounds__(kStepBlock) k_step_multi(MultiArgs a, Cfg c, int early) {
   MultiLane L;
   L.i = (int64_t)blockIdx.x * kStepBlock + threadIdx.x;
@@ -968,7 +972,7 @@ __global__ void __launch_bounds__(kStepBlock) k_step_multi(MultiArgs a, Cfg c, i
   int64_t slab = a.slab0;
   bool packed = false;  // every launch starts from (and ends in) the exchange format
   for (int t = 0; t < a.n_ticks; ++t) {
-    multi_tick<POL>(a, c, r, rp, L, wc, t, step0 + (uint64_t)t, slab, packed, t + 1 == a.n_ticks);
+    multi_tick<POL, PACK>(a, c, r, rp, L, wc, t, step0 + (uint64_t)t, slab, packed, t + 1 == a.n_ticks);
     slab = slab + 1 == a.ring ? 0 : slab + 1;
   }
   if (a.ctr) {
@@ -988,8 +992,10 @@ __global__ void __launch_bounds__(kStepBlock) k_step_multi(MultiArgs a, Cfg c, i
 // with pair_swap (DPP) for the collision test.  Twice the waves of
 // k_step_multi at half the dependent chain per lane: at 65,536 games two
 // waves share each SIMD, so one wave's state round trip through memory
-// overlaps the other's tick.  Same contract, same state ports, same packed
-// form (a lane moves its player's 8-byte half of R, Q and S).
+// overlaps the other's tick.  Same contract, same state ports; the 88-B form
+// every tick (the packed form compiled in cost the small grids a quarter of
+// their tick: 8,192 games 1.98 vs 1.59 us; profiles/r03f_multi_pack*_sweep.jsonl
+// vs r03c_multi_split_sweep.jsonl).
 template <int POL>
 __device__ __forceinline__ double ld_half_d(const MultiArgs& a, __amdgpu_buffer_rsrc_t r, int k, const double* plane,
                                             int64_t h) {
@@ -1018,18 +1024,6 @@ __device__ __forceinline__ void st_half_i(const MultiArgs& a, __amdgpu_buffer_rs
   if constexpr (POL == 0) plane[h] = make_int2(x, y);
   else __builtin_amdgcn_raw_buffer_store_b64((skb2i){x, y}, r, (uint32_t)h * 8u + a.off[k], 0, 16);
 }
-// the packed planes by half: k = 0 R, 1 Q, 2 S (8 bytes per player)
-template <int POL>
-__device__ __forceinline__ skb2i ld_pack_half(const MultiArgs& a, __amdgpu_buffer_rsrc_t rp, int k, int64_t h) {
-  if constexpr (POL == 0) return reinterpret_cast<const skb2i*>(a.pack)[(int64_t)k * 2 * a.n + h];
-  else return __builtin_amdgcn_raw_buffer_load_b64(rp, (uint32_t)h * 8u + (uint32_t)k * (uint32_t)a.n * 16u, 0, 16);
-}
-template <int POL>
-__device__ __forceinline__ void st_pack_half(const MultiArgs& a, __amdgpu_buffer_rsrc_t rp, int k, int64_t h, skb2i v) {
-  if constexpr (POL == 0) reinterpret_cast<skb2i*>(a.pack)[(int64_t)k * 2 * a.n + h] = v;
-  else __builtin_amdgcn_raw_buffer_store_b64(v, rp, (uint32_t)h * 8u + (uint32_t)k * (uint32_t)a.n * 16u, 0, 16);
-}
-
 struct SplitLane {
   int64_t i, ic, hc, h;  // game, loaded game, loaded / stored half-plane index
   int p;                 // player of this lane
@@ -1039,8 +1033,7 @@ struct SplitLane {
 
 template <int POL>
 __device__ __forceinline__ void split_multi_tick(const MultiArgs& a, const Cfg& c, __amdgpu_buffer_rsrc_t r,
-                                                 __amdgpu_buffer_rsrc_t rp, SplitLane& L, WaveCtr& wc, int t,
-                                                 uint64_t step, int64_t slab, bool& packed, bool last) {
+                                                 SplitLane& L, WaveCtr& wc, int t, uint64_t step, int64_t slab) {
   int2* const pos2 = reinterpret_cast<int2*>(a.v.pos);
   double* const rot1 = reinterpret_cast<double*>(a.v.rot);
   int2* const qpos2 = reinterpret_cast<int2*>(a.v.qpos);
@@ -1049,21 +1042,7 @@ __device__ __forceinline__ void split_multi_tick(const MultiArgs& a, const Cfg& 
   const int p = L.p;
   double rot, qrot;
   int px, py, qx, qy, qcd, qage, ticks, qvalid, live, winner;
-  if (packed) {
-    rot = __builtin_bit_cast(double, ld_pack_half<POL>(a, rp, 0, L.hc));
-    qrot = __builtin_bit_cast(double, ld_pack_half<POL>(a, rp, 1, L.hc));
-    const skb2i sv = ld_pack_half<POL>(a, rp, 2, L.hc);
-    const unsigned s0 = (unsigned)sv.x, c0 = (unsigned)sv.y;
-    px = s0 & 0xff; py = (s0 >> 8) & 0xff; qx = (s0 >> 16) & 0xff; qy = s0 >> 24;
-    qcd = (int)(signed char)(c0 & 0xff);
-    qage = (c0 >> 8) & 0xff;
-    const unsigned hi = c0 >> 16, other = (unsigned)pair_swap((int)hi);
-    ticks = (int)(p == 0 ? hi : other);
-    const unsigned fl = p == 0 ? other : hi;
-    qvalid = (fl >> p) & 1;
-    live = (fl >> 2) & 1;
-    winner = (fl >> 3) & 3;
-  } else {
+  {
     // k_step_split's load order: rotation first
     rot = ld_half_d<POL>(a, r, 1, rot1, L.hc);
     qrot = ld_half_d<POL>(a, r, 3, qrot1, L.hc);
@@ -1129,21 +1108,13 @@ __device__ __forceinline__ void split_multi_tick(const MultiArgs& a, const Cfg& 
     ticks = 0; live = 1; winner = 0;
   }
   const int ov = pair_swap(qvalid);
-  const bool fit = !L.in || (pack_fits_player(px, py, qx, qy, qcd, qage, qvalid) & pack_fits_game(ticks, live, winner));
-  const bool to_pack = a.pack != nullptr && !last && __ballot(!fit) == 0;  // wave-uniform
   const bool qch = __double_as_longlong(qrot) != __double_as_longlong(q_old);
   if (L.in) {
-    if (to_pack) {
-      st_pack_half<POL>(a, rp, 0, L.h, __builtin_bit_cast(skb2i, rot));
-      if (qch || !packed) st_pack_half<POL>(a, rp, 1, L.h, __builtin_bit_cast(skb2i, qrot));
-      const unsigned hi = p == 0 ? (unsigned)ticks
-                                 : pack_flags(p ? ov : qvalid, p ? qvalid : ov, live, winner);
-      st_pack_half<POL>(a, rp, 2, L.h, (skb2i){pack_pos(px, py, qx, qy), pack_cah(qcd, qage, hi)});
-    } else {
+    {
       st_half_i<POL>(a, r, 0, pos2, L.h, px, py);
       st_half_d<POL>(a, r, 1, rot1, L.h, rot);
       st_half_i<POL>(a, r, 2, qpos2, L.h, qx, qy);
-      if (qch || packed) st_half_d<POL>(a, r, 3, qrot1, L.h, qrot);
+      if (qch) st_half_d<POL>(a, r, 3, qrot1, L.h, qrot);
       st_half_i<POL>(a, r, 4, ca2, L.h, qcd, qage);
       if (p == 0) {
         const unsigned f = (unsigned)(qvalid & 0xff) | ((unsigned)(ov & 0xff) << 8) |
@@ -1152,7 +1123,6 @@ __device__ __forceinline__ void split_multi_tick(const MultiArgs& a, const Cfg& 
       }
     }
   }
-  packed = to_pack;
 }
 
 // BLK 512 (the 65,536-game geometry): one workgroup of 8 waves per CU, so
@@ -1176,11 +1146,10 @@ __global__ void __launch_bounds__(BLK) k_step_split_multi(MultiArgs a, Cfg c, in
   WaveCtr wc = ctr_load<BLK>(a.ctr);
   const uint64_t step0 = step_read(a.step);
   step_advance(a.step, step0, (uint64_t)a.n_ticks);
-  const __amdgpu_buffer_rsrc_t r = raw_rsrc(a.base), rp = raw_rsrc(a.pack);
+  const __amdgpu_buffer_rsrc_t r = raw_rsrc(a.base);
   int64_t slab = a.slab0;
-  bool packed = false;
   for (int t = 0; t < a.n_ticks; ++t) {
-    split_multi_tick<POL>(a, c, r, rp, L, wc, t, step0 + (uint64_t)t, slab, packed, t + 1 == a.n_ticks);
+    split_multi_tick<POL>(a, c, r, L, wc, t, step0 + (uint64_t)t, slab);
     slab = slab + 1 == a.ring ? 0 : slab + 1;
   }
   if (a.ctr) {
@@ -1886,24 +1855,35 @@ int sk_env_step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64
   const hipStream_t hs = (hipStream_t)stream;
   hipEvent_t e0 = nullptr, e1 = nullptr;  // launch_timed's events (A/B hook; unused by the ABI)
   hipError_t err;
+  // the packed resident form in the lane-per-game kernel only (see
+  // k_step_split_multi)
+  const bool pk = a.pack != nullptr;
   if (split) {
     const int64_t lanes = 2 * (int64_t)e->n;
     const bool wide = e->multi_block == 512 || (e->multi_block < 0 && lanes >= 512 * 256);
     const dim3 g512((unsigned)((lanes + 511) / 512)), g64(step_grid(lanes));
     if (wide)
-      err = pol == 1 ? launch_timed(k_step_split_multi<1, 512>, g512, dim3(512), hs, e0, e1, a, e->dcfg, e->multi_stagger)
-                     : launch_timed(k_step_split_multi<0, 512>, g512, dim3(512), hs, e0, e1, a, e->dcfg, e->multi_stagger);
+      err = pol == 1 ? launch_timed(k_step_split_multi<1, 512>, g512, dim3(512), hs, e0, e1, a, e->dcfg,
+                                    e->multi_stagger)
+                     : launch_timed(k_step_split_multi<0, 512>, g512, dim3(512), hs, e0, e1, a, e->dcfg,
+                                    e->multi_stagger);
     else
-      err = pol == 1 ? launch_timed(k_step_split_multi<1, kStepBlock>, g64, dim3(kStepBlock), hs, e0, e1, a, e->dcfg, 0)
-                     : launch_timed(k_step_split_multi<0, kStepBlock>, g64, dim3(kStepBlock), hs, e0, e1, a, e->dcfg, 0);
+      err = pol == 1 ? launch_timed(k_step_split_multi<1, kStepBlock>, g64, dim3(kStepBlock), hs, e0, e1, a,
+                                    e->dcfg, 0)
+                     : launch_timed(k_step_split_multi<0, kStepBlock>, g64, dim3(kStepBlock), hs, e0, e1, a,
+                                    e->dcfg, 0);
   } else {
     // the restart draw under the loads (k_step's early draw) is off by
     // default here: 65,536 games 2.73 vs 2.81 us per tick at 20 ticks per
     // launch, 131,072 3.69 vs 3.70 / 3.33 vs 3.37 (profiles/r03i_multi_fast_early_sweep.jsonl)
     const int early = e->multi_early > 0;
     const dim3 g(step_grid(e->n));
-    err = pol == 1 ? launch_timed(k_step_multi<1>, g, dim3(kStepBlock), hs, e0, e1, a, e->dcfg, early)
-                   : launch_timed(k_step_multi<0>, g, dim3(kStepBlock), hs, e0, e1, a, e->dcfg, early);
+    if (pk)
+      err = pol == 1 ? launch_timed(k_step_multi<1, true>, g, dim3(kStepBlock), hs, e0, e1, a, e->dcfg, early)
+                     : launch_timed(k_step_multi<0, true>, g, dim3(kStepBlock), hs, e0, e1, a, e->dcfg, early);
+    else
+      err = pol == 1 ? launch_timed(k_step_multi<1, false>, g, dim3(kStepBlock), hs, e0, e1, a, e->dcfg, early)
+                     : launch_timed(k_step_multi<0, false>, g, dim3(kStepBlock), hs, e0, e1, a, e->dcfg, early);
   }
   if (err != hipSuccess) return fail(SK_EHIP, std::string("k_step_multi launch: ") + hipGetErrorString(err));
   e->parity ^= 1;
