@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define SK_ABI_VERSION 5
+#define SK_ABI_VERSION 6
 
 enum {
   SK_OK = 0,
@@ -434,6 +434,15 @@ int sk_adam_flat_packed(const float* partials, int32_t n_partials, int32_t n_par
                         const float* step_counter, float lr, float beta1, float beta2, float eps, float* target,
                         float tau, float* stat_acc, float stat_scale, float* stat_out, int64_t* counter,
                         const sk_pack_targets* packs, void* stream);
+/* sk_adam_flat_packed for the sliced fp32 gradient kernels (below): the
+ * gradient of W1 and b1 (flat parameters 0 .. 3,327) is the sum of n_w1
+ * contribution rows of 3,328 floats at partials_w1 instead of the partial
+ * rows (partials_w1 NULL: exactly sk_adam_flat_packed). */
+int sk_adam_flat_sliced(const float* partials, int32_t n_partials, const float* partials_w1, int32_t n_w1,
+                        int32_t n_params, const float* grad_in, float* grad_out, int32_t apply, float* param,
+                        float* exp_avg, float* exp_avg_sq, const float* step_counter, float lr, float beta1,
+                        float beta2, float eps, float* target, float tau, float* stat_acc, float stat_scale,
+                        float* stat_out, int64_t* counter, const sk_pack_targets* packs, void* stream);
 
 /* --- the learner at the reference's precision (A13, A16, F1, F2) ----------
  * The same nets and update as above with fp32 operands and fp32 accumulation
@@ -457,8 +466,17 @@ int sk_adam_flat_packed(const float* partials, int32_t n_partials, int32_t n_par
  *   sk_critic_grad_f32    as sk_critic_grad_bootstrap (target_actor_flat NULL:
  *                         y = targets; else y = rewards + gamma (1 - done)
  *                         Q'(next_obs, mu'(next_obs)) from the target nets).
- *   sk_actor_grad_f32     as sk_actor_grad. */
+ *   sk_actor_grad_f32     as sk_actor_grad.
+ * Small minibatches (sk_update_scratch_f32(batch) > 0: up to 512 rows, or
+ * any batch with SK_SLICE32=1; none with SK_SLICE32=0) take the sliced
+ * schedule: two launches per step, layer 2 split over 8 workgroups per
+ * 16-row tile.  The caller then passes scratch = float[sk_update_scratch_f32
+ * (batch, &w1_rows)] (NULL -> SK_EINVAL), the partials leave W1 / b1 unwritten,
+ * and their gradient is the first w1_rows x 3,328 floats of scratch, summed by
+ * sk_adam_flat_sliced(partials, n, scratch, w1_rows, ...).  Otherwise scratch
+ * is ignored (may be NULL) and *w1_rows = 0. */
 int64_t sk_update_partials_f32(int64_t batch);
+int64_t sk_update_scratch_f32(int64_t batch, int64_t* w1_rows);
 int sk_actor_forward_f32(const float* actor_flat, const float* obs, float* actions, int64_t rows, float noise_sd,
                          float action_sd, uint64_t seed, uint64_t* call_counter, void* stream);
 int sk_critic_grad_f32(const float* critic_flat, const float* obs, const float* actions, const float* targets,
@@ -466,10 +484,10 @@ int sk_critic_grad_f32(const float* critic_flat, const float* obs, const float* 
                        const float* target_actor_flat, const float* target_critic_flat, int64_t batch,
                        int64_t row_offset, float grad_scale, uint64_t seed, const int64_t* call_counter,
                        float* partials, float* step_counters, int32_t n_steps, float* loss_sum,
-                       uint8_t* dropout_mask, void* stream);
+                       uint8_t* dropout_mask, float* scratch, void* stream);
 int sk_actor_grad_f32(const float* actor_flat, const float* critic_flat, const float* obs, int64_t batch,
                       float loss_scale, float* partials, float* step_counters, int32_t n_steps, float* q_sum,
-                      void* stream);
+                      float* scratch, void* stream);
 
 #ifdef __cplusplus
 }

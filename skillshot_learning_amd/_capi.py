@@ -16,7 +16,7 @@ from . import build as _build
 
 SK_OK, SK_EINVAL, SK_EHIP, SK_ENOMEM, SK_ENODEV = 0, -1, -2, -3, -4
 SK_REWARD_LOOKING, SK_REWARD_SIMPLE = 0, 1
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 # every symbol include/skillshot.h declares
 EXPORTS = (
@@ -30,7 +30,7 @@ EXPORTS = (
     "sk_actor_forward_advance", "sk_actor_forward_noise",
     "sk_critic_packed_bytes", "sk_critic_pack", "sk_critic_forward", "sk_target_q",
     "sk_grad_packed_bytes", "sk_update_partials", "sk_grad_pack", "sk_critic_grad", "sk_actor_grad", "sk_adam_flat",
-    "sk_adam_flat_packed",
+    "sk_adam_flat_packed", "sk_adam_flat_sliced", "sk_update_scratch_f32",
     "sk_target_y", "sk_replay_insert", "sk_replay_sample", "sk_replay_insert_sample", "sk_grad_pack_flat",
     "sk_critic_grad_bootstrap",
     "sk_update_partials_f32", "sk_actor_forward_f32", "sk_critic_grad_f32", "sk_actor_grad_f32",
@@ -142,9 +142,12 @@ def load(build_if_missing=True):
                                      ctypes.c_int),
         "sk_update_partials_f32": ([i64], ctypes.c_int64),
         "sk_actor_forward_f32": ([P, P, P, i64, f32, f32, u64, P, P], ctypes.c_int),
-        "sk_critic_grad_f32": ([P, P, P, P, P, P, P, f32, P, P, i64, i64, f32, u64, P, P, P, i32, P, P, P],
+        "sk_critic_grad_f32": ([P, P, P, P, P, P, P, f32, P, P, i64, i64, f32, u64, P, P, P, i32, P, P, P, P],
                                ctypes.c_int),
-        "sk_actor_grad_f32": ([P, P, P, i64, f32, P, P, i32, P, P], ctypes.c_int),
+        "sk_actor_grad_f32": ([P, P, P, i64, f32, P, P, i32, P, P, P], ctypes.c_int),
+        "sk_update_scratch_f32": ([i64, P], ctypes.c_int64),
+        "sk_adam_flat_sliced": ([P, i32, P, i32, i32, P, P, i32, P, P, P, P, f32, f32, f32, f32, P, f32, P, f32, P, P,
+                                 P, P], ctypes.c_int),
     }
     for name, (argt, rest) in sig.items():
         fn = getattr(L, name)

@@ -28,6 +28,7 @@
 // different order, which fp32 tolerates: tests hold it to 1e-5 of fp64).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/skillshot.h"
 #include "sk_partial.hpp"
@@ -902,6 +903,433 @@ __global__ void __launch_bounds__(kThreads) k_actor_grad32(const float* __restri
   if (threadIdx.x == 0 && q_out) atomicAdd(q_out, L.RED[2]);
 }
 
+// ================================================================ sliced gradient kernels
+// Small minibatches.  The kernels above give a 256-row
+// minibatch 16 workgroups (one per 16-row tile), each running the whole
+// phase chain on one CU at two waves per SIMD: MFMA-rate bound on 16 of 256
+// CUs.  The sliced schedule splits layer 2 over kSlices workgroups per row
+// tile (16 units each: RT x 8 workgroups, 128 at batch 256), two launches per
+// step:
+//   fwd (rt, s)  layer 1 of every net the step reads (all 256 units; the
+//                critic's Dropout), then the slice's 16 layer-2 units with K
+//                split over the 4 waves -> pre-activations z2 (no b2, no
+//                action columns) [rt][net][row][unit] in the scratch buffer
+//   bwd (rt, s)  per row, from all 128 units of z2 (read back: 8 KB per net
+//                and row tile): q, mu', Q', y, dL/dq (critic) or mu, dQ/da,
+//                dL/dz3 (actor); then the slice's dz2, its dW2 rows and its
+//                b2 / action-column / W3 gradients; and the slice's share of
+//                dz1 = dz2_s W2_s (dz1 is linear in dz2, the relu' and
+//                Dropout masks are elementwise) -> dW1 / db1 contributions
+//                written to a second partial buffer [RT * kSlices][3328]
+//                that k_adam_flat sums for W1 and b1.
+// Every partial entry is written by exactly one workgroup.  Block b is row
+// tile b / 8, slice b % 8: slice s always lands on XCD s, whose L2 then holds
+// that slice's W2 rows for every row tile.
+constexpr int kSlices = 8, kSliceU = kH2 / kSlices;  // 16 units per slice
+constexpr int kSlThreads = 256;                       // 4 waves: one per SIMD
+constexpr int kZPlane = kR * kH2;                     // one net's z2 of a row tile
+constexpr int kLdZ = kH2 + 4;
+constexpr int kW1Part = kPW2;                         // W1 + b1: floats per contribution row
+enum { kSlCriticY = 0, kSlCriticBoot = 1, kSlActor = 2 };
+__host__ __device__ constexpr int sl_planes(int mode) { return mode == kSlCriticBoot ? 3 : (mode == kSlActor ? 2 : 1); }
+// net p of a step: critic modes 0 critic, 1 target actor, 2 target critic;
+// actor mode 0 actor, 1 critic
+__host__ __device__ constexpr int sl_ld(int mode, int p) {
+  return (mode == kSlActor && p == 0) || (mode == kSlCriticBoot && p == 1) ? kALd : kCLd;
+}
+__host__ __device__ constexpr int sl_nout(int mode, int p) { return sl_ld(mode, p) == kALd ? 2 : 1; }
+constexpr size_t sl_fwd_lds(int) { return (size_t)(kR * kLdS16 + kR * kLdH1 + kH1 + 4 * kR * kSliceU) * 4; }
+constexpr size_t sl_bwd_lds(int mode) {
+  return (size_t)(2 * kR * kLdS16 + sl_planes(mode) * (kR * kLdZ + 1024) + kR * kLdH1 + kH1 * kLdT16 +
+                  3 * kSliceU * kLdT16 + 32 + 2 * kR + 2 * kR + kR + 4) *
+         4;
+}
+static_assert(sl_fwd_lds(kSlCriticBoot) <= 160 * 1024 && sl_bwd_lds(kSlCriticBoot) <= 160 * 1024, "LDS budget");
+
+// layer-1 fragment of unit n0 + i (g16_l1 with the weights already loaded:
+// the fragments are issued ahead of the staging barrier)
+__device__ __forceinline__ f4 w1_frag(gfp W1, int n0, int lane) {
+  const int i = lane & 15, g = lane >> 4;
+  f4 w = {0.f, 0.f, 0.f, 0.f};
+  if (g < 3) w = *(gf4u)(W1 + (n0 + i) * kIn + 4 * g);
+  return w;
+}
+__device__ __forceinline__ f32x4 g16_l1w(const float* S, f4 w, int lane) {
+  const int i = lane & 15, g = lane >> 4;
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+  return m16x4(*(const f4*)(S + i * kLdS16 + 4 * g), w, z);
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(kSlThreads) k_grad_slice_fwd(const float* __restrict__ f0, const float* __restrict__ f1,
+                                                              const float* __restrict__ f2, const float* __restrict__ Sg,
+                                                              const float* __restrict__ S2g, int64_t B,
+                                                              int64_t key_row0, uint64_t seed,
+                                                              const int64_t* __restrict__ call_ctr,
+                                                              float* __restrict__ Z, float* step_ctr, int n_steps) {
+  constexpr int NP = sl_planes(MODE);
+  extern __shared__ __attribute__((aligned(16))) float smem_sl[];
+  float* sS = smem_sl;              // [16][20]
+  float* sH = sS + kR * kLdS16;     // [16][260] layer-1 outputs
+  float* sB1 = sH + kR * kLdH1;     // [256]
+  float* sRed = sB1 + kH1;          // [4 waves][16 rows][16 units] K-split partials
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tid = threadIdx.x, lane = tid & 63, i = lane & 15, g = lane >> 4;
+  // block = (row tile, net, slice), slice fastest
+  const int b = blockIdx.x, s = b % kSlices, p = (b / kSlices) % NP, rt = b / (kSlices * NP);
+  const int64_t row0 = (int64_t)rt * kR;
+  if (b == 0 && tid < n_steps) step_ctr[tid] += 1.0f;  // Adam's step (read by k_adam_flat)
+  const float* F = p == 0 ? f0 : (p == 1 ? f1 : f2);
+  const int ld = (MODE == kSlActor && p == 0) || (MODE == kSlCriticBoot && p == 1) ? kALd : kCLd;
+  const float* Ssrc = MODE == kSlCriticBoot && p > 0 ? S2g : Sg;
+  const bool drop = MODE != kSlActor && p == 0;
+  // the slice's W2 fragments, rows 16 s + i, k = 64 w + 16 t + 4 g, and the
+  // layer-1 fragments of n-tiles w + 4q: in flight under the staging
+  f4 wv[4], w1v[4];
+  {
+    const gfp wr = (gfp)F + kPW2 + (size_t)(kSliceU * s + i) * ld + 64 * w + 4 * g;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) wv[t] = *(gf4u)(wr + 16 * t);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) w1v[q] = w1_frag((gfp)F + kPW1, 16 * (w + 4 * q), lane);
+  const int si = tid >> 4, sk = tid & 15;
+  const float sv = sk < kIn && row0 + si < B ? Ssrc[(row0 + si) * kIn + sk] : 0.f;
+  const float bv = F[kPB1 + tid];
+  uint32_t keep0 = 0, keep1 = 0;
+  if (drop) {
+    const uint64_t call = (uint64_t)*call_ctr;
+    keep0 = dropout_bits16(seed, call, key_row0 + row0, w, lane);      // n-tiles w, w + 8
+    keep1 = dropout_bits16(seed, call, key_row0 + row0, w + 4, lane);  // n-tiles w + 4, w + 12
+  }
+  sS[si * kLdS16 + sk] = sv;
+  sB1[tid] = bv;
+  lds_sync32();
+  // ---- layer 1, n-tiles w, w + 4, w + 8, w + 12
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t bits = ((q & 1) ? keep1 : keep0) >> (4 * (q >> 1));
+    l1_out(g16_l1w(sS, w1v[q], lane), sB1, w + 4 * q, lane, sH, nullptr, drop, bits);
+  }
+  lds_sync32();
+  // ---- layer 2 of the slice: wave w contracts inputs 64 w .. 64 w + 63
+  {
+    const float* xr = sH + i * kLdH1 + 64 * w + 4 * g;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc = m16x4(*(const f4*)(xr + 16 * t), wv[t], acc);
+    float* red = sRed + w * kR * kSliceU;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[(4 * g + r) * kSliceU + i] = acc[r];
+  }
+  lds_sync32();
+  // ---- z2[row][16 s + j] = the 4 waves' partials (thread = (row, j))
+  {
+    const int row = tid >> 4, j = tid & 15;
+    const float* red = sRed + row * kSliceU + j;
+    const float z = (red[0] + red[kR * kSliceU]) + (red[2 * kR * kSliceU] + red[3 * kR * kSliceU]);
+    Z[((int64_t)rt * NP + p) * kZPlane + row * kH2 + kSliceU * s + j] = z;
+  }
+}
+
+// sum over the 16 lanes of a DPP row, in every lane of the row (xor 1, xor 2,
+// half-row mirror, row mirror: each step adds a lane-symmetric pair, so every
+// lane ends with the same bits)
+template <int CTRL>
+__device__ __forceinline__ float dpp_all(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float rowall16(float v) {
+  v += dpp_all<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_all<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_all<0x141>(v);  // row_half_mirror
+  v += dpp_all<0x140>(v);  // row_mirror
+  return v;
+}
+
+
+template <int MODE>
+__global__ void __launch_bounds__(kSlThreads) k_grad_slice_bwd(
+    const float* __restrict__ f0, const float* __restrict__ f1, const float* __restrict__ f2,
+    const float* __restrict__ Sg, const float* __restrict__ Ag, const float* __restrict__ Yg,
+    const float* __restrict__ Rg, const float* __restrict__ Dg, float gamma, int64_t B, int64_t key_row0,
+    float scale, uint64_t seed, const int64_t* __restrict__ call_ctr, const float* __restrict__ Z,
+    float* __restrict__ partial, float* __restrict__ partial_w1, float* __restrict__ stat_out,
+    uint8_t* __restrict__ mask_out) {
+  constexpr int NP = sl_planes(MODE);
+  constexpr bool CRIT = MODE != kSlActor;
+  constexpr int LD0 = sl_ld(MODE, 0), NPAR = CRIT ? kCP : kAP;
+  extern __shared__ __attribute__((aligned(16))) float smem_sl[];
+  float* sS = smem_sl;                  // [16][20]
+  float* sST = sS + kR * kLdS16;        // [16 features][16 rows (+4)]
+  float* sZ = sST + kR * kLdS16;        // [NP][16][132]
+  float* sTL = sZ + NP * kR * kLdZ;     // [NP][1024] the nets' fp32 tails
+  float* sH1 = sTL + NP * 1024;         // [16][260] layer 1 of the trained net (after Dropout)
+  float* sH1T = sH1 + kR * kLdH1;       // [256][20]
+  float* sDZ2 = sH1T + kH1 * kLdT16;    // [16 rows][16 slice units (+4)]
+  float* sDZ2T = sDZ2 + kSliceU * kLdT16;  // [16 units][16 rows (+4)]
+  float* sH2T = sDZ2T + kSliceU * kLdT16;  // [4 waves][16 units][4] per-unit gradient sums
+  float* sA = sH2T + kSliceU * kLdT16;  // [16][2] actions (critic)
+  float* sRD = sA + 32;                 // [16] r or y, [16] done
+  float* sDQ = sRD + 2 * kR;            // [16][2] dL/dq (critic) or dL/dz3 (actor)
+  float* sST8 = sDQ + 2 * kR;           // [16] per-row e^2 (critic) or Q (actor)
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tid = threadIdx.x, lane = tid & 63, i = lane & 15, g = lane >> 4;
+  const int rt = blockIdx.x / kSlices, s = blockIdx.x - rt * kSlices;
+  const int64_t row0 = (int64_t)rt * kR;
+  const float* fl[3] = {f0, f1, f2};
+  const gfp W2 = (gfp)f0 + kPW2;
+  // ---- phase 0: every global load
+  // the slice's W2 rows down the columns of n-tiles w + 4q (the dz1 GEMM of phase 3)
+  float wd[4][4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) wd[q][c] = W2[(size_t)(kSliceU * s + 4 * g + c) * LD0 + 16 * (w + 4 * q) + i];
+  f4 w1v[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) w1v[q] = w1_frag((gfp)f0 + kPW1, 16 * (w + 4 * q), lane);
+  f4 zv[NP][2];
+#pragma unroll
+  for (int p = 0; p < NP; ++p)
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+      zv[p][m] = *(const f4*)(Z + ((int64_t)rt * NP + p) * kZPlane + 4 * (tid + kSlThreads * m));
+  const int si = tid >> 4, sk = tid & 15;
+  const float sv = sk < kIn && row0 + si < B ? Sg[(row0 + si) * kIn + sk] : 0.f;
+  const bool rok = tid < kR && row0 + tid < B;
+  const float av = CRIT && tid < 32 && row0 + (tid >> 1) < B ? Ag[row0 * 2 + tid] : 0.f;
+  const float rv = CRIT && rok ? (MODE == kSlCriticBoot ? Rg[row0 + tid] : Yg[row0 + tid]) : 0.f;
+  const float dv = MODE == kSlCriticBoot && rok ? Dg[row0 + tid] : 0.f;
+  float tv[NP][4];
+#pragma unroll
+  for (int p = 0; p < NP; ++p)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) tv[p][k] = tail_src((gfp)fl[p], sl_ld(MODE, p), sl_nout(MODE, p), tid + kSlThreads * k);
+  uint32_t keep0 = 0, keep1 = 0;
+  if (CRIT) {
+    const uint64_t call = (uint64_t)*call_ctr;
+    keep0 = dropout_bits16(seed, call, key_row0 + row0, w, lane);
+    keep1 = dropout_bits16(seed, call, key_row0 + row0, w + 4, lane);
+  }
+  sS[si * kLdS16 + sk] = sv;
+  sST[sk * kLdT16 + si] = sv;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int q = tid + kSlThreads * m;
+      *(f4*)(sZ + p * kR * kLdZ + (q >> 5) * kLdZ + 4 * (q & 31)) = zv[p][m];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sTL[p * 1024 + tid + kSlThreads * k] = tv[p][k];
+  }
+  if (CRIT && tid < 32) sA[tid] = av;
+  if (CRIT && tid < kR) {
+    sRD[tid] = rv;
+    sRD[kR + tid] = dv;
+  }
+  if (CRIT && mask_out && s == 0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t bits = ((q & 1) ? keep1 : keep0) >> (4 * (q >> 1));
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (row0 + 4 * g + r < B) mask_out[(row0 + 4 * g + r) * kH1 + 16 * (w + 4 * q) + i] = (bits >> r) & 1u;
+    }
+  }
+  lds_sync32();
+  // ---- phase 1: layer 1 of the trained net (MFMA) and the per-row reductions (VALU)
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int nt = w + 4 * q;
+    const uint32_t bits = ((q & 1) ? keep1 : keep0) >> (4 * (q >> 1));
+    l1_out(g16_l1w(sS, w1v[q], lane), sTL, nt, lane, sH1, sH1T, CRIT, bits);
+  }
+  {
+    const int row = tid >> 4, c = tid & 15;
+    const bool valid = row0 + row < B;
+    const float* T0 = sTL;
+    const float* T1 = sTL + 1024;
+    const float* z0 = sZ + row * kLdZ;
+    if (CRIT) {
+      const float a0 = sA[2 * row], a1 = sA[2 * row + 1];
+      float y;
+      if (MODE == kSlCriticBoot) {
+        const float* za = sZ + kR * kLdZ + row * kLdZ;
+        const float* zt = sZ + 2 * kR * kLdZ + row * kLdZ;
+        const float* T2 = sTL + 2048;
+        float m0 = 0.f, m1 = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int u = c + 16 * k;
+          const float h = fmaxf(za[u] + T1[kT2 + u], 0.f);
+          m0 += h * T1[kT3 + u];
+          m1 += h * T1[kT3 + kH2 + u];
+        }
+        const float mu0 = tanhf(rowall16((m0)) + T1[kTB]);
+        const float mu1 = tanhf(rowall16((m1)) + T1[kTB + 1]);
+        float qt = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int u = c + 16 * k;
+          qt += fmaxf(zt[u] + T2[kT2 + u] + T2[kTA + 2 * u] * mu0 + T2[kTA + 2 * u + 1] * mu1, 0.f) * T2[kT3 + u];
+        }
+        y = sRD[row] + gamma * (1.f - sRD[kR + row]) * (T2[kTB] + rowall16((qt)));
+      } else {
+        y = sRD[row];
+      }
+      float qc = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int u = c + 16 * k;
+        qc += fmaxf(z0[u] + T0[kT2 + u] + T0[kTA + 2 * u] * a0 + T0[kTA + 2 * u + 1] * a1, 0.f) * T0[kT3 + u];
+      }
+      qc = rowsum16(qc);
+      if (c == 15) {
+        const float e = valid ? qc + T0[kTB] - y : 0.f;
+        sDQ[2 * row] = scale * e;
+        sST8[row] = e * e;
+      }
+    } else {
+      const float* zc = sZ + kR * kLdZ + row * kLdZ;
+      float m0 = 0.f, m1 = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int u = c + 16 * k;
+        const float h = fmaxf(z0[u] + T0[kT2 + u], 0.f);
+        m0 += h * T0[kT3 + u];
+        m1 += h * T0[kT3 + kH2 + u];
+      }
+      const float mu0 = tanhf(rowall16((m0)) + T0[kTB]);
+      const float mu1 = tanhf(rowall16((m1)) + T0[kTB + 1]);
+      float d0 = 0.f, d1 = 0.f, qs = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int u = c + 16 * k;
+        const float wa0 = T1[kTA + 2 * u], wa1 = T1[kTA + 2 * u + 1], w3 = T1[kT3 + u];
+        const float z = zc[u] + T1[kT2 + u] + wa0 * mu0 + wa1 * mu1;
+        const float dq = z > 0.f ? w3 : 0.f;
+        d0 += dq * wa0;
+        d1 += dq * wa1;
+        qs += fmaxf(z, 0.f) * w3;
+      }
+      d0 = rowsum16(d0);
+      d1 = rowsum16(d1);
+      qs = rowsum16(qs);
+      if (c == 15) {
+        sDQ[2 * row] = valid ? -scale * d0 * (1.f - mu0 * mu0) : 0.f;
+        sDQ[2 * row + 1] = valid ? -scale * d1 * (1.f - mu1 * mu1) : 0.f;
+        sST8[row] = valid ? qs + T1[kTB] : 0.f;
+      }
+    }
+  }
+  lds_sync32();
+  // ---- phase 2: dz2 of the slice's units (thread = (row, j))
+  {
+    const int row = tid >> 4, j = tid & 15, u = kSliceU * s + j;
+    const float* T0 = sTL;
+    float dz, h2x;
+    if (CRIT) {
+      const float z = sZ[row * kLdZ + u] + T0[kT2 + u] + T0[kTA + 2 * u] * sA[2 * row] + T0[kTA + 2 * u + 1] * sA[2 * row + 1];
+      const float h2 = fmaxf(z, 0.f), dq = sDQ[2 * row];
+      dz = h2 > 0.f ? dq * T0[kT3 + u] : 0.f;
+      h2x = dq * h2;
+    } else {
+      const float h2 = fmaxf(sZ[row * kLdZ + u] + T0[kT2 + u], 0.f);
+      dz = h2 > 0.f ? sDQ[2 * row] * T0[kT3 + u] + sDQ[2 * row + 1] * T0[kT3 + kH2 + u] : 0.f;
+      h2x = h2;
+    }
+    sDZ2[row * kLdT16 + j] = dz;
+    sDZ2T[j * kLdT16 + row] = dz;
+    // the unit's b2 and W3 (and, critic, action-column) gradients over the
+    // wave's 4 rows (lanes j, j + 16, j + 32, j + 48), then across waves in phase 3
+    float v[4];
+    if (CRIT) {
+      v[0] = dz;
+      v[1] = dz * sA[2 * row];
+      v[2] = dz * sA[2 * row + 1];
+      v[3] = h2x;
+    } else {
+      v[0] = dz;
+      v[1] = sDQ[2 * row] * h2x;
+      v[2] = sDQ[2 * row + 1] * h2x;
+      v[3] = 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[k] += __shfl_xor(v[k], 16, 64);
+      v[k] += __shfl_xor(v[k], 32, 64);
+    }
+    if (lane < kSliceU) *(f4*)(sH2T + (w * kSliceU + j) * 4) = f4{v[0], v[1], v[2], v[3]};
+  }
+  lds_sync32();
+  // ---- phase 3: the slice's per-unit gradients; dW2 rows; dz1 share -> dW1, db1
+  float* P = partial + (int64_t)rt * NPAR;
+  float* PW = partial_w1 + (int64_t)blockIdx.x * kW1Part;
+  if (tid < kSliceU) {
+    const int j = tid, u = kSliceU * s + j;
+    const f4 v = (*(const f4*)(sH2T + j * 4) + *(const f4*)(sH2T + (kSliceU + j) * 4)) +
+                 (*(const f4*)(sH2T + (2 * kSliceU + j) * 4) + *(const f4*)(sH2T + (3 * kSliceU + j) * 4));
+    const float b2 = v.x, x0 = v.y, x1 = v.z, x3 = v.w;
+    if (CRIT) {
+      P[pB2(kCLd) + u] = b2;
+      P[skpart::critic_w2_action(u, 0)] = x0;
+      P[skpart::critic_w2_action(u, 1)] = x1;
+      P[pW3(kCLd) + u] = x3;
+    } else {
+      P[pB2(kALd) + u] = b2;
+      P[pW3(kALd) + u] = x0;
+      P[pW3(kALd) + kH2 + u] = x1;
+    }
+  } else if (s == 0 && tid == 64) {  // a lane of wave 1: b3 and the step's loss / Q sum
+    float b30 = 0.f, b31 = 0.f, st = 0.f;
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      b30 += sDQ[2 * r];
+      b31 += sDQ[2 * r + 1];
+      st += sST8[r];
+    }
+    if (CRIT) {
+      P[pB3(kCLd, 1)] = b30;
+    } else {
+      P[pB3(kALd, 2)] = b30;
+      P[pB3(kALd, 2) + 1] = b31;
+    }
+    if (stat_out) atomicAdd(stat_out, st);
+  }
+  const float dscale = CRIT ? 1.25f : 1.f;  // Dropout(0.2): kept activations x 1.25
+  const f4 dzr = *(const f4*)(sDZ2 + i * kLdT16 + 4 * g);
+  const f4 sT = *(const f4*)(sST + i * kLdT16 + 4 * g);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int nt = w + 4 * q, n = 16 * nt + i;
+    const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+    const f32x4 gw2 = g16_wgrad(z4, sDZ2T, 0, sH1T, 16 * nt, lane);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int o = kSliceU * s + 4 * g + r;
+      P[CRIT ? skpart::critic_w2_main(o, n) : kPW2 + o * kALd + n] = gw2[r];
+    }
+    const f32x4 acc = m16x4(dzr, f4{wd[q][0], wd[q][1], wd[q][2], wd[q][3]}, z4);
+    f4 d;
+    float b = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      d[r] = sH1[(4 * g + r) * kLdH1 + n] > 0.f ? acc[r] * dscale : 0.f;
+      b += d[r];
+    }
+    b += __shfl_xor(b, 16, 64);
+    b += __shfl_xor(b, 32, 64);
+    if (g == 0) PW[kPB1 + n] = b;
+    const f32x4 gw1 = m16x4(d, sT, z4);
+    if (i < kIn) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) PW[kPW1 + (16 * nt + 4 * g + r) * kIn + i] = gw1[r];
+    }
+  }
+}
+
 // ---------------------------------------------------------------- actor forward
 // 4 normals for the rows r .. r+3 of unit `unit` of `layer` (Box-Muller on
 // the 4 Philox words: two pairs)
@@ -1061,12 +1489,57 @@ void set_lds32(K kernel, size_t bytes) {
   (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
+// the sliced schedule: automatic up to kSliceMaxTiles row tiles (batch 512);
+// SK_SLICE32=0 never, =1 at every batch (A/B and tests)
+constexpr int64_t kSliceMaxTiles = 32;
+int slice_env() {  // read at every call: tests switch it per case
+  const char* e = getenv("SK_SLICE32");
+  return e && *e ? atoi(e) : -1;
+}
+
+template <int MODE>
+int launch_sliced(const float* f0, const float* f1, const float* f2, const float* S, const float* S2,
+                  const float* A, const float* Y, const float* R, const float* D, float gamma, int64_t B,
+                  int64_t key_row0, float scale, uint64_t seed, const int64_t* call_ctr, float* partials,
+                  float* scratch, int64_t w1_rows, float* step_ctr, int n_steps, float* stat_out, uint8_t* mask_out,
+                  hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    set_lds32(k_grad_slice_fwd<MODE>, sl_fwd_lds(MODE));
+    set_lds32(k_grad_slice_bwd<MODE>, sl_bwd_lds(MODE));
+    attr = true;
+  }
+  float* Z = scratch + w1_rows * kW1Part;
+  const unsigned G = (unsigned)w1_rows;  // row tiles x slices
+  k_grad_slice_fwd<MODE><<<G * sl_planes(MODE), kSlThreads, sl_fwd_lds(MODE), st>>>(f0, f1, f2, S, S2, B, key_row0, seed, call_ctr, Z,
+                                                                  step_ctr, n_steps);
+  k_grad_slice_bwd<MODE><<<G, kSlThreads, sl_bwd_lds(MODE), st>>>(f0, f1, f2, S, A, Y, R, D, gamma, B, key_row0,
+                                                                  scale, seed, call_ctr, Z, partials, scratch,
+                                                                  stat_out, mask_out);
+  return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
+}
+
 }  // namespace
 
 extern "C" {
 
+int64_t sk_update_scratch_f32(int64_t batch, int64_t* w1_rows) {
+  int64_t rows = 0, floats = 0;
+  if (batch > 0 && batch <= ((int64_t)1 << 30)) {
+    const int64_t RT = (batch + kR - 1) / kR;
+    const int m = slice_env();
+    if (m == 1 || (m != 0 && RT <= kSliceMaxTiles)) {
+      rows = RT * kSlices;
+      floats = rows * kW1Part + RT * 3 * kZPlane;
+    }
+  }
+  if (w1_rows) *w1_rows = rows;
+  return floats;
+}
+
 int64_t sk_update_partials_f32(int64_t batch) {
   if (batch <= 0) return 0;
+  if (sk_update_scratch_f32(batch, nullptr) > 0) return (batch + kR - 1) / kR;  // sliced: one row per row tile
   const int64_t spw = subtiles_per_wg32(batch);
   return ((batch + kR - 1) / kR + spw - 1) / spw;
 }
@@ -1076,13 +1549,25 @@ int sk_critic_grad_f32(const float* critic_flat, const float* obs, const float* 
                        const float* target_actor_flat, const float* target_critic_flat, int64_t batch,
                        int64_t row_offset, float grad_scale, uint64_t seed, const int64_t* call_counter,
                        float* partials, float* step_counters, int32_t n_steps, float* loss_sum,
-                       uint8_t* dropout_mask, void* stream) {
+                       uint8_t* dropout_mask, float* scratch, void* stream) {
   const bool boot = target_actor_flat != nullptr;
   if (boot && (!target_critic_flat || !next_obs || !rewards || !done)) return SK_EINVAL;
   if (!boot && !targets) return SK_EINVAL;
   if (!critic_flat || !obs || !actions || !call_counter || !partials || batch <= 0) return SK_EINVAL;
   if (row_offset < 0 || (row_offset & 3)) return SK_EINVAL;
   if ((n_steps > 0 && !step_counters) || n_steps < 0 || n_steps > 64) return SK_EINVAL;
+  int64_t w1_rows = 0;
+  if (sk_update_scratch_f32(batch, &w1_rows) > 0) {
+    if (!scratch) return SK_EINVAL;
+    if (boot)
+      return launch_sliced<kSlCriticBoot>(critic_flat, target_actor_flat, target_critic_flat, obs, next_obs, actions,
+                                          nullptr, rewards, done, gamma, batch, row_offset, grad_scale, seed,
+                                          call_counter, partials, scratch, w1_rows, step_counters, n_steps, loss_sum,
+                                          dropout_mask, (hipStream_t)stream);
+    return launch_sliced<kSlCriticY>(critic_flat, nullptr, nullptr, obs, nullptr, actions, targets, nullptr, nullptr,
+                                     0.f, batch, row_offset, grad_scale, seed, call_counter, partials, scratch,
+                                     w1_rows, step_counters, n_steps, loss_sum, dropout_mask, (hipStream_t)stream);
+  }
   static bool attr = false;
   if (!attr) {
     set_lds32(k_critic_grad32<true>, kLdsGrad32);
@@ -1101,9 +1586,16 @@ int sk_critic_grad_f32(const float* critic_flat, const float* obs, const float* 
 
 int sk_actor_grad_f32(const float* actor_flat, const float* critic_flat, const float* obs, int64_t batch,
                       float loss_scale, float* partials, float* step_counters, int32_t n_steps, float* q_sum,
-                      void* stream) {
+                      float* scratch, void* stream) {
   if (!actor_flat || !critic_flat || !obs || !partials || batch <= 0) return SK_EINVAL;
   if ((n_steps > 0 && !step_counters) || n_steps < 0 || n_steps > 64) return SK_EINVAL;
+  int64_t w1_rows = 0;
+  if (sk_update_scratch_f32(batch, &w1_rows) > 0) {
+    if (!scratch) return SK_EINVAL;
+    return launch_sliced<kSlActor>(actor_flat, critic_flat, nullptr, obs, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                   0.f, batch, 0, loss_scale, 0, nullptr, partials, scratch, w1_rows, step_counters,
+                                   n_steps, q_sum, nullptr, (hipStream_t)stream);
+  }
   static bool attr = false;
   if (!attr) {
     set_lds32(k_actor_grad32, kLdsGrad32);

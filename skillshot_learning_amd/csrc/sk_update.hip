@@ -975,7 +975,8 @@ __global__ void __launch_bounds__(kAdamParams * kAdamSlices) k_adam_flat(const f
                             float* __restrict__ grad_out, int apply, float* __restrict__ param, float* __restrict__ m,
                             float* __restrict__ v, const float* __restrict__ step_ctr, float lr, float beta1,
                             float beta2, float eps, float* __restrict__ target, float tau, float* stat_acc,
-                            float stat_scale, float* stat_out, int64_t* counter, PackOut po) {
+                            float stat_scale, float* stat_out, int64_t* counter, PackOut po,
+                            const float* __restrict__ partial_w1, int G1) {
   // a workgroup owns kAdamParams consecutive parameters; its kAdamSlices
   // waves each sum every kAdamSlices-th partial of them (64-lane coalesced
   // rows, 8 loads in flight per lane), then fold through LDS: 4x the waves
@@ -991,15 +992,21 @@ __global__ void __launch_bounds__(kAdamParams * kAdamSlices) k_adam_flat(const f
     if (counter) *counter += 1;
   }
   const bool in = p < P;
-  const int pp = skpart::index(p, P);  // the partial layout (sk_partial.hpp)
+  int pp = skpart::index(p, P);  // the partial layout (sk_partial.hpp)
+  // W1 / b1 of the sliced fp32 kernels (sk_learn32.hip): G1 contribution
+  // rows of kPW2 floats (workgroup-uniform: kPW2 is a multiple of kAdamParams)
+  const bool w1 = partial_w1 && p < skpart::kPW2;
+  const float* src = w1 ? partial_w1 : partial;
+  const int64_t ld = w1 ? skpart::kPW2 : P;
+  const int GG = w1 ? G1 : G;
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // 8 independent loads in flight
   if (in) {
     int k = slice;
-    for (; k + 7 * kAdamSlices < G; k += 8 * kAdamSlices) {
+    for (; k + 7 * kAdamSlices < GG; k += 8 * kAdamSlices) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += partial[(int64_t)(k + j * kAdamSlices) * P + pp];
+      for (int j = 0; j < 8; ++j) acc[j] += src[(int64_t)(k + j * kAdamSlices) * ld + pp];
     }
-    for (; k < G; k += kAdamSlices) acc[0] += partial[(int64_t)k * P + pp];
+    for (; k < GG; k += kAdamSlices) acc[0] += src[(int64_t)k * ld + pp];
   }
   const float part = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   if (slice > 0) red[slice - 1][lane] = part;
@@ -1132,12 +1139,13 @@ int sk_actor_grad(const void* apack, const void* cpack, const float* obs, int64_
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
 }
 
-int sk_adam_flat_packed(const float* partial, int32_t n_partials, int32_t n_params, const float* grad_in,
-                        float* grad_out, int32_t apply, float* param, float* exp_avg, float* exp_avg_sq,
-                        const float* step_counter, float lr, float beta1, float beta2, float eps, float* target,
-                        float tau, float* stat_acc, float stat_scale, float* stat_out, int64_t* counter,
-                        const sk_pack_targets* packs, void* stream) {
+int sk_adam_flat_sliced(const float* partial, int32_t n_partials, const float* partials_w1, int32_t n_w1,
+                        int32_t n_params, const float* grad_in, float* grad_out, int32_t apply, float* param,
+                        float* exp_avg, float* exp_avg_sq, const float* step_counter, float lr, float beta1,
+                        float beta2, float eps, float* target, float tau, float* stat_acc, float stat_scale,
+                        float* stat_out, int64_t* counter, const sk_pack_targets* packs, void* stream) {
   if (n_params <= 0 || n_partials < 0 || (n_partials > 0 && !partial)) return SK_EINVAL;
+  if (n_w1 < 0 || (n_w1 > 0 && !partials_w1) || (partials_w1 && n_params < skpart::kPW2)) return SK_EINVAL;
   if (apply && (!param || !exp_avg || !exp_avg_sq || !step_counter)) return SK_EINVAL;
   PackOut po = {nullptr, nullptr, nullptr, kH1, 1};
   if (packs && apply) {
@@ -1152,8 +1160,18 @@ int sk_adam_flat_packed(const float* partial, int32_t n_partials, int32_t n_para
   }
   k_adam_flat<<<(n_params + kAdamParams - 1) / kAdamParams, kAdamParams * kAdamSlices, 0, (hipStream_t)stream>>>(
       partial, n_partials, n_params, grad_in, grad_out, apply, param, exp_avg, exp_avg_sq, step_counter, lr, beta1,
-      beta2, eps, target, tau, stat_acc, stat_scale, stat_out, counter, po);
+      beta2, eps, target, tau, stat_acc, stat_scale, stat_out, counter, po, partials_w1, n_w1);
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
+}
+
+int sk_adam_flat_packed(const float* partial, int32_t n_partials, int32_t n_params, const float* grad_in,
+                        float* grad_out, int32_t apply, float* param, float* exp_avg, float* exp_avg_sq,
+                        const float* step_counter, float lr, float beta1, float beta2, float eps, float* target,
+                        float tau, float* stat_acc, float stat_scale, float* stat_out, int64_t* counter,
+                        const sk_pack_targets* packs, void* stream) {
+  return sk_adam_flat_sliced(partial, n_partials, nullptr, 0, n_params, grad_in, grad_out, apply, param, exp_avg,
+                             exp_avg_sq, step_counter, lr, beta1, beta2, eps, target, tau, stat_acc, stat_scale,
+                             stat_out, counter, packs, stream);
 }
 
 int sk_adam_flat(const float* partial, int32_t n_partials, int32_t n_params, const float* grad_in, float* grad_out,

@@ -110,6 +110,19 @@ class _AdamState:
             st["step"] = self.steps[i]
 
 
+class _Partials:
+    """Gradient partials of one (batch, net): rows [G][n_params] and, for the
+    sliced fp32 kernels (sk_update_scratch_f32 > 0), their scratch, whose first
+    w1_rows x 3,328 floats are the W1 / b1 contribution rows"""
+
+    def __init__(self, main, scratch=None, w1_rows=0):
+        self.main, self.scratch, self.w1_rows = main, scratch, int(w1_rows)
+
+    @property
+    def rows(self):
+        return self.main.shape[0]
+
+
 class FusedUpdate:
     """Kernel path of DDPG.critic_step / model_actor_fit_step (+ soft update)."""
 
@@ -172,7 +185,14 @@ class FusedUpdate:
         t = self._partials.get(key)
         if t is None:
             g = int(self.L.sk_update_partials_f32(batch) if self.f32 else self.L.sk_update_partials(batch))
-            t = self._partials[key] = torch.empty((g, n_params), dtype=torch.float32, device=self.dev)
+            main = torch.empty((g, n_params), dtype=torch.float32, device=self.dev)
+            scratch, rows = None, 0
+            if self.f32:
+                r = ctypes.c_int64(0)
+                n = int(self.L.sk_update_scratch_f32(batch, ctypes.byref(r)))
+                if n > 0:
+                    scratch, rows = torch.empty(n, dtype=torch.float32, device=self.dev), r.value
+            t = self._partials[key] = _Partials(main, scratch, rows)
         return t
 
     def _pack_flat(self, jobs):
@@ -223,17 +243,22 @@ class FusedUpdate:
             if self.grad_flat is None or self.grad_flat.numel() < P:
                 self.grad_flat = torch.empty(max(36609, P), dtype=torch.float32, device=self.dev)
             g = self.grad_flat[:P]
-            _capi.check(self.L.sk_adam_flat(_p(part), part.shape[0], P, None, _p(g), 0, None, None, None, None,
-                                            0.0, 0.0, 0.0, 0.0, None, 0.0, None, 0.0, None, None, self._stream()))
+            self._sum_partials(part, P, g)
             self.d.allreduce_sum(g)
             _capi.check(self.L.sk_adam_flat_packed(None, 0, P, _p(g), None, 1, _p(flat), _p(st.m), _p(st.v),
                                                    _p(st.steps), st.lr, st.b1, st.b2, st.eps, _p(target), tau,
                                                    _p(stat), float(scale), _p(out), _p(counter), pk, self._stream()))
         else:
-            _capi.check(self.L.sk_adam_flat_packed(_p(part), part.shape[0], P, None, None, 1, _p(flat), _p(st.m),
-                                                   _p(st.v), _p(st.steps), st.lr, st.b1, st.b2, st.eps, _p(target),
-                                                   tau, _p(stat), float(scale), _p(out), _p(counter), pk,
-                                                   self._stream()))
+            _capi.check(self.L.sk_adam_flat_sliced(_p(part.main), part.rows, _p(part.scratch), part.w1_rows, P, None,
+                                                   None, 1, _p(flat), _p(st.m), _p(st.v), _p(st.steps), st.lr, st.b1,
+                                                   st.b2, st.eps, _p(target), tau, _p(stat), float(scale), _p(out),
+                                                   _p(counter), pk, self._stream()))
+
+    def _sum_partials(self, part, P, g):
+        """the flat gradient (no step) from a step's partials"""
+        _capi.check(self.L.sk_adam_flat_sliced(_p(part.main), part.rows, _p(part.scratch), part.w1_rows, P, None,
+                                               _p(g), 0, None, None, None, None, 0.0, 0.0, 0.0, 0.0, None, 0.0, None,
+                                               0.0, None, None, None, self._stream()))
 
     @torch.no_grad()
     def critic_step(self, s, a, target=None, mask_out=None, s2=None, r=None, d=None, gamma=0.0, row_offset=0,
@@ -269,17 +294,17 @@ class FusedUpdate:
             y = None if boot else target.float().contiguous()
             return self.L.sk_critic_grad_f32(
                 _p(self.fc), _p(s), _p(a), _p(y), _p(s2c), _p(rc_), _p(dc), float(gamma), _p(ta), _p(tc), s.shape[0],
-                int(row_offset), 2.0 / gb, self.seed, _p(self.calls), _p(part), _p(steps), n_steps, statp,
-                _p(mask_out), self._stream())
+                int(row_offset), 2.0 / gb, self.seed, _p(self.calls), _p(part.main), _p(steps), n_steps, statp,
+                _p(mask_out), _p(part.scratch), self._stream())
         if s2 is not None:
             s2c, rc_, dc = s2.float().contiguous(), r.float().contiguous(), d.float().contiguous()
             return self.L.sk_critic_grad_bootstrap(
                 _p(self.gpc), _p(s), _p(a), None, _p(s2c), _p(rc_), _p(dc), float(gamma), _p(self.gpta),
-                _p(self.gptc), s.shape[0], int(row_offset), 2.0 / gb, self.seed, _p(self.calls), _p(part), _p(steps),
+                _p(self.gptc), s.shape[0], int(row_offset), 2.0 / gb, self.seed, _p(self.calls), _p(part.main), _p(steps),
                 n_steps, statp, _p(mask_out), self._stream())
         y = target.float().contiguous()
         return self.L.sk_critic_grad(_p(self.gpc), _p(s), _p(a), _p(y), s.shape[0], int(row_offset), 2.0 / gb,
-                                     self.seed, _p(self.calls), _p(part), _p(steps), n_steps, statp, _p(mask_out),
+                                     self.seed, _p(self.calls), _p(part.main), _p(steps), n_steps, statp, _p(mask_out),
                                      self._stream())
 
     @torch.no_grad()
@@ -300,9 +325,9 @@ class FusedUpdate:
     def _actor_grad(self, s, part, steps, stat):
         n = steps.numel() if steps is not None else 0
         if self.f32:
-            return self.L.sk_actor_grad_f32(_p(self.fa), _p(self.fc), _p(s), s.shape[0], 1.0, _p(part), _p(steps), n,
-                                            _p(stat), self._stream())
-        return self.L.sk_actor_grad(_p(self.gpa), _p(self.gpc), _p(s), s.shape[0], 1.0, _p(part), _p(steps), n,
+            return self.L.sk_actor_grad_f32(_p(self.fa), _p(self.fc), _p(s), s.shape[0], 1.0, _p(part.main), _p(steps),
+                                            n, _p(stat), _p(part.scratch), self._stream())
+        return self.L.sk_actor_grad(_p(self.gpa), _p(self.gpc), _p(s), s.shape[0], 1.0, _p(part.main), _p(steps), n,
                                     _p(stat), self._stream())
 
     @torch.no_grad()
@@ -325,6 +350,5 @@ class FusedUpdate:
             part = self._partial(B, flat.numel())
             _capi.check(self._actor_grad(s.float().contiguous(), part, None, None))
         g = torch.empty_like(flat)
-        _capi.check(self.L.sk_adam_flat(_p(part), part.shape[0], flat.numel(), None, _p(g), 0, None, None, None, None,
-                                        0.0, 0.0, 0.0, 0.0, None, 0.0, None, 0.0, None, None, self._stream()))
+        self._sum_partials(part, flat.numel(), g)
         return g

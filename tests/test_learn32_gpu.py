@@ -30,6 +30,15 @@ def mods():
     return learner, keras_ref
 
 
+@pytest.fixture(params=["0", "1"], ids=["one_launch", "sliced"])
+def sched(request, monkeypatch):
+    """both gradient schedules: one launch per step (16-row tiles per
+    workgroup) and the sliced two-launch one (layer 2 over 8 workgroups per
+    tile; automatic up to 512 rows) at every batch size"""
+    monkeypatch.setenv("SK_SLICE32", request.param)
+    return request.param
+
+
 def _ddpg(learner, seed=0, scale=2.0, tau=None, gamma=0.0):
     d = learner.DDPG("cuda", seed=seed, tau=tau, gamma=gamma, fused_update=True, precision="fp32")
     with torch.no_grad():
@@ -65,7 +74,7 @@ def _check_flat(flat, module, want, rel=GRAD_REL):
 
 
 @pytest.mark.parametrize("rows", [1, 37, 256, 4096 + 17])
-def test_critic_grad_f32_matches_keras(mods, rows):
+def test_critic_grad_f32_matches_keras(mods, sched, rows):
     learner, kr = mods
     d = _ddpg(learner, seed=1)
     s, a = _obs(rows, 1), torch.rand(rows, 2, device="cuda") * 2 - 1
@@ -79,8 +88,8 @@ def test_critic_grad_f32_matches_keras(mods, rows):
     _check_flat(g, d.model_critic, want)
 
 
-@pytest.mark.parametrize("rows", [37, 4096 + 17])
-def test_critic_grad_f32_bootstrap_matches_keras(mods, rows):
+@pytest.mark.parametrize("rows", [37, 256, 4096 + 17])
+def test_critic_grad_f32_bootstrap_matches_keras(mods, sched, rows):
     learner, kr = mods
     d = _ddpg(learner, seed=4, tau=0.05, gamma=0.9)
     s, a = _obs(rows, 2), torch.rand(rows, 2, device="cuda") * 2 - 1
@@ -95,7 +104,7 @@ def test_critic_grad_f32_bootstrap_matches_keras(mods, rows):
 
 
 @pytest.mark.parametrize("rows", [1, 37, 256, 4096 + 17])
-def test_actor_grad_f32_matches_keras(mods, rows):
+def test_actor_grad_f32_matches_keras(mods, sched, rows):
     learner, kr = mods
     d = _ddpg(learner, seed=2)
     s = _obs(rows, 4)
@@ -104,7 +113,7 @@ def test_actor_grad_f32_matches_keras(mods, rows):
     _check_flat(g, d.model_actor, want)
 
 
-def test_critic_grad_f32_split_rows_equal_whole(mods):
+def test_critic_grad_f32_split_rows_equal_whole(mods, sched):
     learner, _ = mods
     d = _ddpg(learner, seed=6)
     s, a, y = _obs(512, 5), torch.rand(512, 2, device="cuda") * 2 - 1, torch.randn(512, device="cuda")
@@ -175,7 +184,7 @@ def test_actor_forward_f32_param_noise_distribution(mods):
         assert float((fa - fb).abs().max()) < 1.95 * math.sqrt(2 / n) * 1.3
 
 
-def test_f32_replay_updates_match_keras(mods):
+def test_f32_replay_updates_match_keras(mods, sched):
     """three fused fp32 replay updates (bootstrap target, critic step, actor
     step, Keras Adam, soft update) against the restatement step by step"""
     learner, kr = mods

@@ -4,7 +4,10 @@ a hipGraph, HIP events around the replay, microseconds per launch.  Pieces:
 replay sample, critic grad (bootstrap target in launch), critic Adam, actor
 grad, actor Adam, and the whole update.  One JSON line per (precision, batch).
 
-    python tools/bench_update_parts.py [--batches 256,4096] [--k 20]"""
+    python tools/bench_update_parts.py [--batches 256,4096] [--k 20] [--slices -1,0,1]
+
+--slices sets SK_SLICE32 per pass (fp32: -1 automatic, 0 one-launch
+gradient kernels, 1 the sliced two-launch schedule at every batch)."""
 import argparse
 import json
 import os
@@ -44,9 +47,12 @@ def main():
     p.add_argument("--batches", default="256,4096")
     p.add_argument("--k", type=int, default=20)
     p.add_argument("--precisions", default="fp32,bf16")
+    p.add_argument("--slices", default="-1")
     a = p.parse_args()
-    for prec in a.precisions.split(","):
-        for B in [int(x) for x in a.batches.split(",")]:
+    for prec, sl, B in [(p_, s_, int(b)) for p_ in a.precisions.split(",") for s_ in a.slices.split(",")
+                        for b in a.batches.split(",")]:
+        if True:
+            os.environ["SK_SLICE32"] = sl
             d = DDPG("cuda", seed=0, gamma=0.99, tau=0.005, replay_capacity=1 << 16, fused_update=True,
                      precision=prec)
             g = torch.Generator(device="cuda").manual_seed(0)
@@ -63,7 +69,7 @@ def main():
             st.synchronize()
             pc = fu._partial(B, fu.fc.numel())
             pa = fu._partial(B, fu.fa.numel())
-            out = dict(precision=prec, batch=B, k=a.k)
+            out = dict(precision=prec, batch=B, k=a.k, slice=int(sl), sliced=pc.scratch is not None)
             out["sample"] = timed(lambda: d.sample_local(B, device_sampling=True), st, a.k)
             out["critic_grad"] = timed(lambda: fu._critic_grad(bs, ba, None, bs2, br, bd, 0.99, 0, B, pc,
                                                                 fu.sc.steps, None), st, a.k)
