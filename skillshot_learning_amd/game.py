@@ -20,6 +20,7 @@ import math
 import numpy as np
 import torch
 
+from . import _capi
 from .vec_env import FEATURE_KEYS, VecSkillshotGame
 
 # get_state value types (SkillshotGame.py:145-163): Python ints, bools and floats
@@ -279,12 +280,13 @@ class SkillshotGame(object):
             views["rot_p"] = views["rot"][0]
             views["rot_q"] = views["qrot"][0]
             self._cache = views
-            self._move_direction = lambda pid, v: L.sk_player_move_direction(h, pid, None, v, None)
-            self._move_look = lambda pid, v: L.sk_player_move_look(h, pid, None, v, None)
-            self._move_discrete = lambda pid, k: L.sk_player_move_discrete(h, pid, k, None, None)
-            self._shoot = lambda pid: L.sk_player_shoot(h, pid, None, None)
-            self._projectile_move = lambda pid, t: L.sk_projectile_move(h, pid, t, None, None)
-            self._game_tick_c = lambda: L.sk_game_tick(h, None)
+            ck = _capi.check  # SK_EINVAL etc. raise here as on the GPU path
+            self._move_direction = lambda pid, v: ck(L.sk_player_move_direction(h, pid, None, v, None))
+            self._move_look = lambda pid, v: ck(L.sk_player_move_look(h, pid, None, v, None))
+            self._move_discrete = lambda pid, k: ck(L.sk_player_move_discrete(h, pid, k, None, None))
+            self._shoot = lambda pid: ck(L.sk_player_shoot(h, pid, None, None))
+            self._projectile_move = lambda pid, t: ck(L.sk_projectile_move(h, pid, t, None, None))
+            self._game_tick_c = lambda: ck(L.sk_game_tick(h, None))
         else:
             def mut(f):
                 def g(*a):
