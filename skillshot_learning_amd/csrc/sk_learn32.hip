@@ -1331,6 +1331,54 @@ __global__ void __launch_bounds__(kSlThreads) k_grad_slice_bwd(
 }
 
 // ---------------------------------------------------------------- actor forward
+// the last workgroup to arrive stores the call number the launch drew with.
+// Grouped arrival (as the bf16 actor's advance_call, csrc/sk_actor.hip):
+// workgroup b on group line call_ctr[2 + 16 (b % 8)], the last of each group
+// on call_ctr[1] (SK_ACTOR_COUNTER_WORDS)
+__device__ __forceinline__ void advance_call32(uint64_t* call_ctr, uint64_t call) {
+  if (threadIdx.x == 0) {
+    const unsigned g = blockIdx.x & 7u;
+    const unsigned long long members = (gridDim.x - g + 7u) / 8u;
+    unsigned long long* gc = (unsigned long long*)&call_ctr[2 + 16 * g];
+    if (atomicAdd(gc, 1ull) == members - 1) {
+      *gc = 0;
+      const unsigned long long groups = gridDim.x < 8u ? gridDim.x : 8u;
+      if (atomicAdd((unsigned long long*)&call_ctr[1], 1ull) == groups - 1) {
+        call_ctr[0] = call;
+        call_ctr[1] = 0;
+      }
+    }
+  }
+}
+// mean and variance GEMMs of parameter noise on 16-row tiles (g16_xwT256 with
+// x^2 w^2 beside: every operand load feeds both chains)
+__device__ __forceinline__ void g16_xwT256_mv(f32x4& m, f32x4& v, const float* X, gfp W, int n0, int lane) {
+  const int i = lane & 15, g = lane >> 4;
+  const float* xr = X + i * kLdH1 + 4 * g;
+  const gfp wr = W + (size_t)(n0 + i) * kALd + 4 * g;
+  m = f32x4{0.f, 0.f, 0.f, 0.f};
+  v = f32x4{0.f, 0.f, 0.f, 0.f};
+  f4 wn[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) wn[t] = *(gf4u)(wr + 16 * t);
+#pragma unroll
+  for (int k = 0; k < 256; k += 64) {
+    f4 wc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) wc[t] = wn[t];
+    if (k + 64 < 256) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) wn[t] = *(gf4u)(wr + k + 64 + 16 * t);
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const f4 x = *(const f4*)(xr + k + 16 * t);
+      m = m16x4(x, wc[t], m);
+      v = m16x4(x * x, wc[t] * wc[t], v);
+    }
+  }
+}
+
 // 4 normals for the rows r .. r+3 of unit `unit` of `layer` (Box-Muller on
 // the 4 Philox words: two pairs)
 __device__ __forceinline__ void normals4(uint64_t seed, uint64_t call, uint32_t r, uint32_t layer_unit, float z[4]) {
@@ -1460,22 +1508,136 @@ __global__ void __launch_bounds__(kFwdThreads) k_actor_fwd32(const float* __rest
   }
   if (draws) {  // the last workgroup to finish stores the call number it drew with
     __syncthreads();
-    // grouped arrival (as the bf16 actor's advance_call, csrc/sk_actor.hip):
-    // workgroup b on group line call_ctr[2 + 16 (b % 8)], the last of each
-    // group on call_ctr[1] (SK_ACTOR_COUNTER_WORDS)
-    if (threadIdx.x == 0) {
-      const unsigned g = blockIdx.x & 7u;
-      const unsigned long long members = (gridDim.x - g + 7u) / 8u;
-      unsigned long long* gc = (unsigned long long*)&call_ctr[2 + 16 * g];
-      if (atomicAdd(gc, 1ull) == members - 1) {
-        *gc = 0;
-        const unsigned long long groups = gridDim.x < 8u ? gridDim.x : 8u;
-        if (atomicAdd((unsigned long long*)&call_ctr[1], 1ull) == groups - 1) {
-          call_ctr[0] = call;
-          call_ctr[1] = 0;
-        }
+    advance_call32(call_ctr, call);
+  }
+}
+
+// ---------------------------------------------------------------- actor forward, 16-row tiles
+// The same forward for small row counts: a 32-row tile is a serial chain of
+// load latencies around 3.4 us of MFMA per workgroup (9.4 us at 256 rows);
+// 16-row tiles on v_mfma_f32_16x16x4_f32 halve the per-workgroup MFMA chain
+// (6.5 us at 256 rows).  Above ~4,096 rows the 32-row tiles win: the chip's
+// fp32 MFMA time dominates and two 16-row workgroups per CU contend.  Every weight
+// fragment a wave needs before layer 2 is issued ahead of the staging
+// barrier.  Wave w: layer-1 n-tiles w + 4q (16 units each), layer-2 n-tiles w
+// and w + 4; layer 3 from DPP row sums of the layer-2 tiles.  The noise draws
+// are keyed exactly as k_actor_fwd32's: normals4 per (first row of a 4-row
+// group, unit), z[r] for row + r.
+template <bool NOISE>
+__global__ void __launch_bounds__(kFwdThreads) k_actor_fwd16(const float* __restrict__ aflat,
+                                                             const float* __restrict__ X, float* __restrict__ out,
+                                                             int64_t rows, float sd, float action_sd, uint64_t seed,
+                                                             uint64_t* __restrict__ call_ctr) {
+  __shared__ __attribute__((aligned(16))) float S[kR * kLdS16];
+  __shared__ __attribute__((aligned(16))) float H1[kR * kLdH1];
+  __shared__ __attribute__((aligned(16))) f4 MP[4][kR];  // per wave and row: {m0, m1, v0, v1} of layer 3
+  const int tid = threadIdx.x, lane = tid & 63, i = lane & 15, g = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const Net A = net_of(aflat, kALd, 2);
+  const int64_t row0 = (int64_t)blockIdx.x * kR;
+  const bool draws = (NOISE || action_sd != 0.f) && call_ctr;
+  const uint64_t call = draws ? call_ctr[0] + 1 : 0;
+  // ---- every load ahead of the barrier: states, layer-1 fragments and biases, the
+  // first layer-2 fragments (g16_xwT256's prefetch), W3 / b2 of the wave's units
+  const int si = tid >> 4, sk = tid & 15;
+  const float sv = sk < kIn && row0 + si < rows ? X[(row0 + si) * kIn + sk] : 0.f;
+  f4 w1v[4];
+  float b1v[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    w1v[q] = w1_frag(A.W1, 16 * (w + 4 * q), lane);
+    b1v[q] = A.b1[16 * (w + 4 * q) + i];
+  }
+  float b2v[2], w30[2], w31[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int u = 16 * (w + 4 * t) + i;
+    b2v[t] = A.b2[u];
+    w30[t] = A.W3[u];
+    w31[t] = A.W3[kH2 + u];
+  }
+  S[si * kLdS16 + sk] = sv;
+  lds_sync32();
+  // ---- layer 1
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int u = 16 * (w + 4 * q) + i;
+    const f4 x = *(const f4*)(S + i * kLdS16 + 4 * g);
+    const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+    const f32x4 m = m16x4(x, w1v[q], z4);
+    const float b = b1v[q];
+    if (NOISE) {
+      const f32x4 var = m16x4(x * x, w1v[q] * w1v[q], z4);
+      float z[4];
+      normals4(seed, call, (uint32_t)(row0 + 4 * g), (uint32_t)u, z);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float y = __builtin_fmaf(sd * __builtin_amdgcn_sqrtf(__builtin_fmaf(b, b, var[r])), z[r], m[r] + b);
+        H1[(4 * g + r) * kLdH1 + u] = fmaxf(y, 0.f);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) H1[(4 * g + r) * kLdH1 + u] = fmaxf(m[r] + b, 0.f);
+    }
+  }
+  lds_sync32();
+  // ---- layer 2 (n-tiles w, w + 4) and the layer-3 partials of the wave's units
+  // per row 4g + r: the layer-3 dot products (and their variances) over this lane's two units
+  float pm0[4] = {0.f, 0.f, 0.f, 0.f}, pm1[4] = {0.f, 0.f, 0.f, 0.f}, pv0[4] = {0.f, 0.f, 0.f, 0.f},
+        pv1[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int nt = w + 4 * t, u = 16 * nt + i;
+    f32x4 m, var;
+    if (NOISE) {
+      g16_xwT256_mv(m, var, H1, A.W2, 16 * nt, lane);
+    } else {
+      m = g16_xwT256(H1, kLdH1, A.W2, kALd, 16 * nt, lane);
+    }
+    float z[4];
+    if (NOISE) normals4(seed, call, (uint32_t)(row0 + 4 * g), (uint32_t)(kH1 + u), z);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float y = m[r] + b2v[t];
+      if (NOISE) y = __builtin_fmaf(sd * __builtin_amdgcn_sqrtf(__builtin_fmaf(b2v[t], b2v[t], var[r])), z[r], y);
+      const float h = fmaxf(y, 0.f);
+      pm0[r] += h * w30[t];
+      pm1[r] += h * w31[t];
+      if (NOISE) {
+        pv0[r] += h * h * w30[t] * w30[t];
+        pv1[r] += h * h * w31[t] * w31[t];
       }
     }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const f4 v = {rowsum16(pm0[r]), rowsum16(pm1[r]), NOISE ? rowsum16(pv0[r]) : 0.f, NOISE ? rowsum16(pv1[r]) : 0.f};
+    if (i == 15) MP[w][4 * g + r] = v;
+  }
+  lds_sync32();
+  // ---- layer 3, tanh, action noise: one thread per row
+  if (tid < kR && row0 + tid < rows) {
+    const f4 v = (MP[0][tid] + MP[1][tid]) + (MP[2][tid] + MP[3][tid]);
+    const float b30 = A.b3[0], b31 = A.b3[1];
+    float y0 = v.x + b30, y1 = v.y + b31;
+    if (NOISE) {
+      float z[4];
+      normals4(seed, call, (uint32_t)(row0 + tid), (uint32_t)(kH1 + kH2), z);
+      y0 += sd * __builtin_amdgcn_sqrtf(v.z + b30 * b30) * z[0];
+      y1 += sd * __builtin_amdgcn_sqrtf(v.w + b31 * b31) * z[1];
+    }
+    float o0 = tanhf(y0), o1 = tanhf(y1);
+    if (action_sd != 0.f) {
+      float z[4];
+      normals4(seed, call, (uint32_t)(row0 + tid), (uint32_t)(kH1 + kH2 + 1), z);
+      o0 += action_sd * z[0];
+      o1 += action_sd * z[1];
+    }
+    *(float2*)(out + (row0 + tid) * 2) = make_float2(o0, o1);
+  }
+  if (draws) {
+    __syncthreads();
+    advance_call32(call_ctr, call);
   }
 }
 
@@ -1487,6 +1649,15 @@ int64_t subtiles_per_wg32(int64_t B) {  // 16-row sub-tiles; <= 256 workgroups, 
 template <typename K>
 void set_lds32(K kernel, size_t bytes) {
   (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+// 16-row actor forward up to 4,096 rows (at most half the CUs busy with 32-row
+// tiles; profiles/r03u_actor_fwd.jsonl: 2,048 rows 9.6 -> 6.6 us, but 8,192
+// rows 10.4 -> 10.9 us); SK_FWD16=0 / 1 forces the 32- / 16-row kernel
+bool fwd16_rows(int64_t rows) {
+  const char* e = getenv("SK_FWD16");
+  const int v = e && *e ? atoi(e) : -1;
+  return v == 1 || (v != 0 && rows <= 4096);
 }
 
 // the sliced schedule: automatic up to kSliceMaxTiles row tiles (batch 512);
@@ -1613,6 +1784,16 @@ int sk_actor_forward_f32(const float* actor_flat, const float* obs, float* actio
                          float action_sd, uint64_t seed, uint64_t* call_counter, void* stream) {
   if (!actor_flat || !obs || !actions || rows <= 0) return SK_EINVAL;
   if ((((uintptr_t)actions) & 7)) return SK_EINVAL;
+  if (fwd16_rows(rows)) {
+    const unsigned G16 = (unsigned)((rows + kR - 1) / kR);
+    if (noise_sd != 0.f)
+      k_actor_fwd16<true><<<G16, kFwdThreads, 0, (hipStream_t)stream>>>(actor_flat, obs, actions, rows, noise_sd,
+                                                                          action_sd, seed, call_counter);
+    else
+      k_actor_fwd16<false><<<G16, kFwdThreads, 0, (hipStream_t)stream>>>(actor_flat, obs, actions, rows, 0.f,
+                                                                           action_sd, seed, call_counter);
+    return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
+  }
   const unsigned G = (unsigned)((rows + 31) / 32);
   if (noise_sd != 0.f)
     k_actor_fwd32<true><<<G, kFwdThreads, 0, (hipStream_t)stream>>>(actor_flat, obs, actions, rows, noise_sd,

@@ -999,6 +999,18 @@ __global__ void __launch_bounds__(kAdamParams * kAdamSlices) k_adam_flat(const f
   const float* src = w1 ? partial_w1 : partial;
   const int64_t ld = w1 ? skpart::kPW2 : P;
   const int GG = w1 ? G1 : G;
+  // the step's own operands are loaded up front, under the partial reads
+  float g0 = 0.f, mm = 0.f, vv = 0.f, w0 = 0.f, tw0 = 0.f, t = 0.f;
+  if (in && slice == 0) {
+    if (grad_in) g0 = grad_in[p];
+    if (apply) {
+      t = step_ctr[0];
+      mm = m[p];
+      vv = v[p];
+      w0 = param[p];
+      if (target) tw0 = target[p];
+    }
+  }
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // 8 independent loads in flight
   if (in) {
     int k = slice;
@@ -1012,25 +1024,23 @@ __global__ void __launch_bounds__(kAdamParams * kAdamSlices) k_adam_flat(const f
   if (slice > 0) red[slice - 1][lane] = part;
   __syncthreads();
   if (slice > 0 || !in) return;
-  float g = grad_in ? grad_in[p] : 0.f;
+  float g = g0;
   g += part;
 #pragma unroll
   for (int j = 0; j < kAdamSlices - 1; ++j) g += red[j][lane];
   if (grad_out) grad_out[p] = g;
   if (!apply) return;
-  const float t = step_ctr[0];
   const float alpha = lr * sqrtf(1.f - powf(beta2, t)) / (1.f - powf(beta1, t));
-  float mm = m[p], vv = v[p];
   mm = mm + (g - mm) * (1.f - beta1);
   vv = vv + (g * g - vv) * (1.f - beta2);
   m[p] = mm;
   v[p] = vv;
-  const float w = param[p] - (mm * alpha) / (sqrtf(vv) + eps);
+  const float w = w0 - (mm * alpha) / (sqrtf(vv) + eps);
   param[p] = w;
   if (po.gp) scatter_grad_pack(po.gp, p, w, po.ld2, po.n_out);
   if (po.fp) scatter_fwd_pack(po.fp, p, w);
   if (target) {
-    const float tw = target[p] + tau * (w - target[p]);
+    const float tw = tw0 + tau * (w - tw0);
     target[p] = tw;
     if (po.tp) scatter_grad_pack(po.tp, p, tw, po.ld2, po.n_out);
   }

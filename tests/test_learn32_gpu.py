@@ -39,6 +39,14 @@ def sched(request, monkeypatch):
     return request.param
 
 
+@pytest.fixture(params=["0", "1"], ids=["rows32", "rows16"])
+def fwd(request, monkeypatch):
+    """both actor forward kernels: 32-row tiles (large row counts) and
+    16-row tiles (automatic below 32,768 rows)"""
+    monkeypatch.setenv("SK_FWD16", request.param)
+    return request.param
+
+
 def _ddpg(learner, seed=0, scale=2.0, tau=None, gamma=0.0):
     d = learner.DDPG("cuda", seed=seed, tau=tau, gamma=gamma, fused_update=True, precision="fp32")
     with torch.no_grad():
@@ -127,7 +135,7 @@ def test_critic_grad_f32_split_rows_equal_whole(mods, sched):
 
 
 @pytest.mark.parametrize("rows", [1, 33, 8192])
-def test_actor_forward_f32_matches_keras(mods, rows):
+def test_actor_forward_f32_matches_keras(mods, fwd, rows):
     learner, kr = mods
     from skillshot_learning_amd.actor_kernel import ActorKernel32
     d = _ddpg(learner, seed=7)
@@ -138,7 +146,7 @@ def test_actor_forward_f32_matches_keras(mods, rows):
     assert np.abs(_np(out) - want).max() <= 1e-5
 
 
-def test_actor_forward_f32_param_noise_distribution(mods):
+def test_actor_forward_f32_param_noise_distribution(mods, fwd):
     """model_act_param_noise (:245-281) per row: the kernel's outputs for one
     state repeated over 32,768 rows against explicit weight noise w (1 +
     0.5 N(0,1)) drawn per sample in fp64 (two-sample KS, moments); the device
@@ -231,7 +239,7 @@ def test_f32_learner_tick_graph(mods):
     assert bool(torch.isfinite(tg.act).all()) and float(tg.act.abs().max()) <= 1.0
 
 
-def test_actor_forward_f32_action_noise(mods):
+def test_actor_forward_f32_action_noise(mods, fwd):
     """model_act_action_noise (:229-243): the tanh outputs + N(0, 0.15) drawn
     in the kernel; the call counter advances per launch (fresh draws on every
     replay of a captured tick)"""
