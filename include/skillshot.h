@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define SK_ABI_VERSION 6
+#define SK_ABI_VERSION 7
 
 enum {
   SK_OK = 0,
@@ -209,6 +209,22 @@ int sk_env_observe(sk_env* env, float* obs, float* reward, int32_t reward_kind, 
 int sk_env_step(sk_env* env, const float* actions, float* obs, float* reward, int32_t reward_kind,
                 uint8_t* done, uint8_t* winner, int32_t tick_limit, int32_t auto_reset,
                 int32_t random_positions, float* obs_reset, void* stream);
+
+/* sk_env_step followed by sk_replay_insert of the tick's 2N transitions, in
+ * ONE launch (ABI 7; the learner tick's env step + ring insert,
+ * SkillshotLearner.py:302-324 + the replay ring of SURVEY 8(d) config 3):
+ * row r = p N + i of the actor's [2N] order holds (acting_obs[r], actions[r],
+ * reward[r], obs[r], done[i]) and goes to ring row (*total + r) % capacity;
+ * *total advances by 2N, exactly as sk_replay_insert(ring, capacity, total,
+ * arrivals, acting_obs, actions, reward, obs, done, N, 2N) after the step.
+ * obs and reward must be given (the ring holds them); acting_obs float[2N][12]
+ * and ring float[capacity][28] 16-byte aligned, capacity >= 2N, arrivals
+ * uint32[SK_REPLAY_ARRIVAL_WORDS] zeroed once (every launch leaves it zero).
+ * The CPU backend (device -1) takes host pointers for all of them. */
+int sk_env_step_insert(sk_env* env, const float* actions, float* obs, float* reward, int32_t reward_kind,
+                       uint8_t* done, uint8_t* winner, int32_t tick_limit, int32_t auto_reset,
+                       int32_t random_positions, float* obs_reset, const float* acting_obs, float* ring,
+                       int64_t capacity, int64_t* total, uint32_t* arrivals, void* stream);
 
 /* n_ticks learner ticks of the step-only contract in ONE launch (ABI 5):
  * equal, bit for bit, to n_ticks calls of sk_env_step(obs = reward =
@@ -485,6 +501,31 @@ int sk_critic_grad_f32(const float* critic_flat, const float* obs, const float* 
                        int64_t row_offset, float grad_scale, uint64_t seed, const int64_t* call_counter,
                        float* partials, float* step_counters, int32_t n_steps, float* loss_sum,
                        uint8_t* dropout_mask, float* scratch, void* stream);
+/* The replay-rule critic step on a minibatch drawn from the ring (ABI 7):
+ * equal, bit for bit, to sk_replay_sample(q->ring, q->capacity, q->total,
+ * q->seed, q->draw, batch, q->s, q->a, q->r, q->s2, q->d) followed by
+ * sk_critic_grad_f32 on those rows (bootstrap target when target_actor_flat
+ * is given, else y = q->r).  Sliced batches gather inside the step's first
+ * launch (one launch fewer per learner tick); larger batches run the gather
+ * as its own launch.  The sample buffers are written either way (the actor
+ * step reads q->s). */
+typedef struct sk_ring_sample {
+  const float* ring;      /* float[capacity][28], 16-byte aligned */
+  int64_t capacity;
+  const int64_t* total;   /* rows ever inserted (device) */
+  uint64_t seed;
+  int32_t draw;
+  float* s;               /* [batch][12] */
+  float* a;               /* [batch][2] */
+  float* r;               /* [batch] */
+  float* s2;              /* [batch][12] */
+  float* d;               /* [batch] */
+} sk_ring_sample;
+int sk_critic_grad_f32_sampled(const float* critic_flat, const sk_ring_sample* sample, float gamma,
+                               const float* target_actor_flat, const float* target_critic_flat, int64_t batch,
+                               int64_t row_offset, float grad_scale, uint64_t seed, const int64_t* call_counter,
+                               float* partials, float* step_counters, int32_t n_steps, float* loss_sum,
+                               uint8_t* dropout_mask, float* scratch, void* stream);
 int sk_actor_grad_f32(const float* actor_flat, const float* critic_flat, const float* obs, int64_t batch,
                       float loss_scale, float* partials, float* step_counters, int32_t n_steps, float* q_sum,
                       float* scratch, void* stream);

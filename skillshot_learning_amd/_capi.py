@@ -16,7 +16,7 @@ from . import build as _build
 
 SK_OK, SK_EINVAL, SK_EHIP, SK_ENOMEM, SK_ENODEV = 0, -1, -2, -3, -4
 SK_REWARD_LOOKING, SK_REWARD_SIMPLE = 0, 1
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 # every symbol include/skillshot.h declares
 EXPORTS = (
@@ -25,7 +25,7 @@ EXPORTS = (
     "sk_env_clear_counters", "sk_env_get_step_counter",
     "sk_env_set_step_counter", "sk_env_sync_step_counter", "sk_env_reset", "sk_player_move_direction", "sk_player_move_look",
     "sk_player_move_discrete", "sk_player_shoot", "sk_projectile_move", "sk_game_check_collision", "sk_game_tick", "sk_env_features", "sk_env_observe",
-    "sk_env_step", "sk_env_step_multi", "sk_gen_random_actions", "sk_env_rollout_random",
+    "sk_env_step", "sk_env_step_insert", "sk_env_step_multi", "sk_gen_random_actions", "sk_env_rollout_random",
     "sk_actor_packed_bytes", "sk_actor_pack", "sk_actor_forward", "sk_actor_forward_dev",
     "sk_actor_forward_advance", "sk_actor_forward_noise",
     "sk_critic_packed_bytes", "sk_critic_pack", "sk_critic_forward", "sk_target_q",
@@ -33,7 +33,8 @@ EXPORTS = (
     "sk_adam_flat_packed", "sk_adam_flat_sliced", "sk_update_scratch_f32",
     "sk_target_y", "sk_replay_insert", "sk_replay_sample", "sk_replay_insert_sample", "sk_grad_pack_flat",
     "sk_critic_grad_bootstrap",
-    "sk_update_partials_f32", "sk_actor_forward_f32", "sk_critic_grad_f32", "sk_actor_grad_f32",
+    "sk_update_partials_f32", "sk_actor_forward_f32", "sk_critic_grad_f32", "sk_critic_grad_f32_sampled",
+    "sk_actor_grad_f32",
 )
 
 
@@ -110,6 +111,7 @@ def load(build_if_missing=True):
         "sk_env_features": ([P, P, P], ctypes.c_int),
         "sk_env_observe": ([P, P, P, i32, P], ctypes.c_int),
         "sk_env_step": ([P, P, P, P, i32, P, P, i32, i32, i32, P, P], ctypes.c_int),
+        "sk_env_step_insert": ([P, P, P, P, i32, P, P, i32, i32, i32, P, P, P, i64, P, P, P], ctypes.c_int),
         "sk_env_step_multi": ([P, P, i64, i64, i32, P, P, i64, i32, i32, i32, P], ctypes.c_int),
         "sk_gen_random_actions": ([P, P, i32, P], ctypes.c_int),
         "sk_env_rollout_random": ([P, i32, i32, P], ctypes.c_int),
@@ -144,6 +146,8 @@ def load(build_if_missing=True):
         "sk_actor_forward_f32": ([P, P, P, i64, f32, f32, u64, P, P], ctypes.c_int),
         "sk_critic_grad_f32": ([P, P, P, P, P, P, P, f32, P, P, i64, i64, f32, u64, P, P, P, i32, P, P, P, P],
                                ctypes.c_int),
+        "sk_critic_grad_f32_sampled": ([P, P, f32, P, P, i64, i64, f32, u64, P, P, P, i32, P, P, P, P],
+                                       ctypes.c_int),
         "sk_actor_grad_f32": ([P, P, P, i64, f32, P, P, i32, P, P, P], ctypes.c_int),
         "sk_update_scratch_f32": ([i64, P], ctypes.c_int64),
         "sk_adam_flat_sliced": ([P, i32, P, i32, i32, P, P, i32, P, P, P, P, f32, f32, f32, f32, P, f32, P, f32, P, P,

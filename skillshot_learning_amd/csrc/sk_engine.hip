@@ -273,7 +273,35 @@ struct StepArgs {
   int64_t env_offset;
   StepRef step;
   sk_counters* ctr;
+  // the replay ring insert of the tick's 2N transitions (sk_env_step_insert;
+  // k_step_split only, with obs and reward): row r = p N + i of the [2N]
+  // actor order -> ring row (total + r) % cap, as sk_replay_insert
+  const float* acting_obs;  // [2N][12] the observations the actions were taken on
+  float* ring;              // [cap][28] (NULL: no insert)
+  int64_t ring_cap;
+  int64_t* ring_total;
+  uint32_t* ring_arrivals;  // SK_REPLAY_ARRIVAL_WORDS
 };
+
+// The ring insert's end of launch (sk_replay.hip's grouped arrival): lane 0
+// of workgroup b arrives on group line arrivals[32 (1 + b % 8)], the last of
+// each group on arrivals[0]; the last workgroup (every other one has read
+// total) stores the new total.  Called by every lane 0 (lane 0 of a launched
+// workgroup always steps a game).
+__device__ __forceinline__ void ring_arrive(uint32_t* arrivals, int64_t* total, int64_t new_total) {
+  if (threadIdx.x != 0) return;
+  const unsigned g = blockIdx.x & 7u;
+  const unsigned members = (gridDim.x - g + 7u) / 8u;
+  uint32_t* gc = arrivals + 32u * (1u + g);
+  if (atomicAdd(gc, 1u) == members - 1u) {
+    *gc = 0u;
+    const unsigned groups = gridDim.x < 8u ? gridDim.x : 8u;
+    if (atomicAdd(arrivals, 1u) == groups - 1u) {
+      *total = new_total;
+      *arrivals = 0u;
+    }
+  }
+}
 
 // OBS: the launch writes obs / reward / obs_reset (instantiated apart so the
 // step-only tick keeps no obs state live: holding the projectiles' sincos for
@@ -516,6 +544,18 @@ __global__ void __launch_bounds__(kStepBlock) k_step_split(StepArgs a, Cfg c) {
   __builtin_amdgcn_sched_barrier(0);
   const float2 act = load_action(a.actions + (int64_t)p * a.n + ic);
   __builtin_amdgcn_sched_barrier(0);
+  // the ring insert's sources and base (wave-uniform scalar load; read before
+  // this workgroup signals its arrival below)
+  const bool ins = a.ring != nullptr;  // launch-uniform
+  int64_t rbase = 0;
+  float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0, s2 = s0;
+  if (ins) {
+    rbase = *a.ring_total;
+    const float4* so = reinterpret_cast<const float4*>(a.acting_obs + ((int64_t)p * a.n + ic) * 12);
+    s0 = so[0];
+    s1 = so[1];
+    s2 = so[2];
+  }
   bool k0, k1, k2;
   sktrig::SinCos m = sktrig::sincos_bf(rot, &k0);
   int px = pp.x, py = pp.y, qx = qq.x, qy = qq.y, qcd = ca.x, qage = ca.y, ticks = mi.x;
@@ -577,8 +617,19 @@ __global__ void __launch_bounds__(kStepBlock) k_step_split(StepArgs a, Cfg c) {
         r = (float)(-(double)pd / (double)c.W);
       }
       a.reward[(int64_t)p * a.n + i] = r;
+      if (ins) {  // s, a, r, s', done: the row sk_replay_insert would write
+        float4* dst = reinterpret_cast<float4*>(a.ring + ((rbase + (int64_t)p * a.n + i) % a.ring_cap) * 28);
+        dst[0] = s0;
+        dst[1] = s1;
+        dst[2] = s2;
+        dst[3] = make_float4(act.x, act.y, r, o[0]);
+        dst[4] = make_float4(o[1], o[2], o[3], o[4]);
+        dst[5] = make_float4(o[5], o[6], o[7], o[8]);
+        dst[6] = make_float4(o[9], o[10], o[11], d ? 1.f : 0.f);
+      }
     }
   }
+  if (ins) ring_arrive(a.ring_arrivals, a.ring_total, rbase + 2 * a.n);
   if (in && p == 0) {
     if (a.done) a.done[i] = (uint8_t)d;
     if (a.winner) a.winner[i] = (uint8_t)winner;
@@ -635,6 +686,7 @@ __global__ void __launch_bounds__(kStepBlock) k_step_split(StepArgs a, Cfg c) {
     const float f = fi >= 0 ? (float)fi : future_flag_cr(c, aqx, aqy, aqrot, opx, opy);
     if (a.obs) a.obs[((int64_t)p * a.n + i) * 12 + 11] = f;
     if (a.obs_reset && !reset) a.obs_reset[((int64_t)p * a.n + i) * 12 + 11] = f;
+    if (ins) a.ring[((rbase + (int64_t)p * a.n + i) % a.ring_cap) * 28 + 26] = f;  // s'[11]
   }
 }
 
@@ -1731,9 +1783,10 @@ int sk_env_observe(sk_env* e, float* obs, float* reward, int32_t kind, void* str
   return SK_OK;
 }
 
-int sk_env_step(sk_env* e, const float* actions, float* obs, float* reward, int32_t reward_kind, uint8_t* done,
-                uint8_t* winner, int32_t tick_limit, int32_t auto_reset, int32_t random_positions,
-                float* obs_reset, void* stream) {
+static int step_launch(sk_env* e, const float* actions, float* obs, float* reward, int32_t reward_kind,
+                       uint8_t* done, uint8_t* winner, int32_t tick_limit, int32_t auto_reset,
+                       int32_t random_positions, float* obs_reset, const float* acting_obs, float* ring,
+                       int64_t capacity, int64_t* total, uint32_t* arrivals, void* stream) {
   SK_CHECK_ENV(e);
   if (!actions) return fail(SK_EINVAL, "actions is NULL");
   if (((uintptr_t)actions) & 7) return fail(SK_EINVAL, "actions must be 8-byte aligned");
@@ -1741,9 +1794,29 @@ int sk_env_step(sk_env* e, const float* actions, float* obs, float* reward, int3
     return fail(SK_EINVAL, "obs buffers must be 16-byte aligned");
   if (reward_kind != SK_REWARD_LOOKING && reward_kind != SK_REWARD_SIMPLE)
     return fail(SK_EINVAL, "bad reward_kind");
+  if (ring) {
+    if (!obs || !reward || !acting_obs || !total || !arrivals)
+      return fail(SK_EINVAL, "ring insert needs obs, reward, acting_obs, total and arrivals");
+    if (capacity <= 0 || 2 * (int64_t)e->n > capacity) return fail(SK_EINVAL, "ring capacity below 2 N rows");
+    if ((((uintptr_t)ring) & 15) || (((uintptr_t)acting_obs) & 15) || (((uintptr_t)total) & 7))
+      return fail(SK_EINVAL, "ring / acting_obs must be 16-byte aligned, total 8-byte");
+  }
   if (e->host) {
     skh::step(*e->host, actions, obs, reward, reward_kind, done, winner, tick_limit, auto_reset, random_positions,
               obs_reset);
+    if (ring) {  // sk_replay_insert's rows on the host ring (player-major [2N] order)
+      const int64_t n = e->n, base = *total;
+      for (int64_t r = 0; r < 2 * n; ++r) {
+        float* dst = ring + ((base + r) % capacity) * 28;
+        std::memcpy(dst, acting_obs + r * 12, 12 * sizeof(float));
+        dst[12] = actions[2 * r];
+        dst[13] = actions[2 * r + 1];
+        dst[14] = reward[r];
+        std::memcpy(dst + 15, obs + r * 12, 12 * sizeof(float));
+        dst[27] = done ? (float)done[r % n] : 0.f;
+      }
+      *total = base + 2 * n;
+    }
     return SK_OK;
   }
   StepArgs a;
@@ -1763,13 +1836,20 @@ int sk_env_step(sk_env* e, const float* actions, float* obs, float* reward, int3
   a.env_offset = e->env_offset;
   a.step = StepRef{e->d_step, e->parity};
   a.ctr = e->d_counters;
+  a.acting_obs = acting_obs;
+  a.ring = ring;
+  a.ring_cap = capacity;
+  a.ring_total = total;
+  a.ring_arrivals = arrivals;
   // auto: k_step_fast once several waves share a SIMD (>= 2 per SIMD on 256
   // CUs) up to ~3 per SIMD (262,144 games: 8.3 vs 9.1 us); k_step from
   // 1 M games, where the step is HBM-bound (1 M: 30.1 vs 31.6 us, 4 M: 137
   // vs 151 us; profiles/r01x_sweep_qskip.jsonl); below 196,608 k_step, or
   // k_step_split when observations are written (65,536 games with obs: 9.8
-  // vs 10.5 us; profiles/r01g_step_variants.jsonl, r01v_step_block_ab.jsonl)
-  const int variant = e->step_variant >= 0 ? e->step_variant
+  // vs 10.5 us; profiles/r01g_step_variants.jsonl, r01v_step_block_ab.jsonl).
+  // The ring insert is k_step_split's.
+  const int variant = ring ? 1
+                      : e->step_variant >= 0 ? e->step_variant
                       : (e->n >= kFastStepMinEnvs && e->n < kFastStepMaxEnvs) ? 2
                       : e->n >= kFastStepMaxEnvs ? 0
                       : (obs || reward || obs_reset || e->n <= kSplitStepMaxEnvs) ? 1 : 0;
@@ -1784,6 +1864,22 @@ int sk_env_step(sk_env* e, const float* actions, float* obs, float* reward, int3
   SK_LAUNCH_CHECK();
   e->parity ^= 1;
   return SK_OK;
+}
+
+int sk_env_step(sk_env* e, const float* actions, float* obs, float* reward, int32_t reward_kind, uint8_t* done,
+                uint8_t* winner, int32_t tick_limit, int32_t auto_reset, int32_t random_positions,
+                float* obs_reset, void* stream) {
+  return step_launch(e, actions, obs, reward, reward_kind, done, winner, tick_limit, auto_reset, random_positions,
+                     obs_reset, nullptr, nullptr, 0, nullptr, nullptr, stream);
+}
+
+int sk_env_step_insert(sk_env* e, const float* actions, float* obs, float* reward, int32_t reward_kind,
+                       uint8_t* done, uint8_t* winner, int32_t tick_limit, int32_t auto_reset,
+                       int32_t random_positions, float* obs_reset, const float* acting_obs, float* ring,
+                       int64_t capacity, int64_t* total, uint32_t* arrivals, void* stream) {
+  if (!ring) return fail(SK_EINVAL, "ring is NULL");
+  return step_launch(e, actions, obs, reward, reward_kind, done, winner, tick_limit, auto_reset, random_positions,
+                     obs_reset, acting_obs, ring, capacity, total, arrivals, stream);
 }
 
 int sk_env_step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64_t slab0, int32_t n_ticks,

@@ -960,13 +960,37 @@ __device__ __forceinline__ f32x4 g16_l1w(const float* S, f4 w, int lane) {
   return m16x4(*(const f4*)(S + i * kLdS16 + 4 * g), w, z);
 }
 
+// The replay minibatch gathered inside the critic's first launch
+// (sk_critic_grad_f32_sampled): batch row b is ring row floor(u_b size), u_b
+// from Philox4x32-10 keyed (seed; b, draw, total), exactly sk_replay_sample's
+// row, so the step equals sk_replay_sample + sk_critic_grad_f32.  Each
+// workgroup reads its own rows' states from the ring; the (slice 0, net 0)
+// workgroup of every row tile also writes its 16 rows into the sample
+// buffers, which the second launch and the actor step read.
+struct RingSample {
+  const float* ring;  // NULL: states from Sg / S2g
+  int64_t cap;
+  const int64_t* total;
+  uint64_t seed;
+  int draw;
+  float *s, *a, *r, *s2, *d;
+};
+__device__ __forceinline__ int64_t ring_row(const RingSample& q, int64_t b, int64_t t) {
+  const uint64_t size = (uint64_t)(t < q.cap ? t : q.cap);
+  const uint4 u = philox(make_uint4((uint32_t)b, (uint32_t)q.draw, (uint32_t)t, (uint32_t)(t >> 32)), (uint32_t)q.seed,
+                         (uint32_t)(q.seed >> 32));
+  const uint64_t u53 = (((uint64_t)u.x << 32) | u.y) >> 11;
+  return (int64_t)(((unsigned __int128)u53 * size) >> 53);
+}
+
 template <int MODE>
 __global__ void __launch_bounds__(kSlThreads) k_grad_slice_fwd(const float* __restrict__ f0, const float* __restrict__ f1,
                                                               const float* __restrict__ f2, const float* __restrict__ Sg,
                                                               const float* __restrict__ S2g, int64_t B,
                                                               int64_t key_row0, uint64_t seed,
                                                               const int64_t* __restrict__ call_ctr,
-                                                              float* __restrict__ Z, float* step_ctr, int n_steps) {
+                                                              float* __restrict__ Z, float* step_ctr, int n_steps,
+                                                              RingSample rs) {
   constexpr int NP = sl_planes(MODE);
   extern __shared__ __attribute__((aligned(16))) float smem_sl[];
   float* sS = smem_sl;              // [16][20]
@@ -994,7 +1018,28 @@ __global__ void __launch_bounds__(kSlThreads) k_grad_slice_fwd(const float* __re
 #pragma unroll
   for (int q = 0; q < 4; ++q) w1v[q] = w1_frag((gfp)F + kPW1, 16 * (w + 4 * q), lane);
   const int si = tid >> 4, sk = tid & 15;
-  const float sv = sk < kIn && row0 + si < B ? Ssrc[(row0 + si) * kIn + sk] : 0.f;
+  float sv;
+  if (rs.ring) {
+    const int64_t b = row0 + si, t = *rs.total;
+    const bool ok = b < B && t > 0;
+    const int64_t idx = ok ? ring_row(rs, b, t) : 0;
+    const float* src = rs.ring + idx * 28;
+    sv = ok && sk < kIn ? src[(MODE == kSlCriticBoot && p > 0 ? 15 : 0) + sk] : 0.f;
+    if (ok && s == 0 && p == 0 && sk < 7) {  // the row into the sample buffers
+      const f4 v = *(const f4*)(src + 4 * sk);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int f = 4 * sk + c;
+        if (f < 12) rs.s[b * 12 + f] = v[c];
+        else if (f < 14) rs.a[b * 2 + f - 12] = v[c];
+        else if (f == 14) rs.r[b] = v[c];
+        else if (f < 27) rs.s2[b * 12 + f - 15] = v[c];
+        else rs.d[b] = v[c];
+      }
+    }
+  } else {
+    sv = sk < kIn && row0 + si < B ? Ssrc[(row0 + si) * kIn + sk] : 0.f;
+  }
   const float bv = F[kPB1 + tid];
   uint32_t keep0 = 0, keep1 = 0;
   if (drop) {
@@ -1673,7 +1718,7 @@ int launch_sliced(const float* f0, const float* f1, const float* f2, const float
                   const float* A, const float* Y, const float* R, const float* D, float gamma, int64_t B,
                   int64_t key_row0, float scale, uint64_t seed, const int64_t* call_ctr, float* partials,
                   float* scratch, int64_t w1_rows, float* step_ctr, int n_steps, float* stat_out, uint8_t* mask_out,
-                  hipStream_t st) {
+                  hipStream_t st, RingSample rs = RingSample{}) {
   static bool attr = false;
   if (!attr) {
     set_lds32(k_grad_slice_fwd<MODE>, sl_fwd_lds(MODE));
@@ -1683,7 +1728,7 @@ int launch_sliced(const float* f0, const float* f1, const float* f2, const float
   float* Z = scratch + w1_rows * kW1Part;
   const unsigned G = (unsigned)w1_rows;  // row tiles x slices
   k_grad_slice_fwd<MODE><<<G * sl_planes(MODE), kSlThreads, sl_fwd_lds(MODE), st>>>(f0, f1, f2, S, S2, B, key_row0, seed, call_ctr, Z,
-                                                                  step_ctr, n_steps);
+                                                                  step_ctr, n_steps, rs);
   k_grad_slice_bwd<MODE><<<G, kSlThreads, sl_bwd_lds(MODE), st>>>(f0, f1, f2, S, A, Y, R, D, gamma, B, key_row0,
                                                                   scale, seed, call_ctr, Z, partials, scratch,
                                                                   stat_out, mask_out);
@@ -1753,6 +1798,42 @@ int sk_critic_grad_f32(const float* critic_flat, const float* obs, const float* 
       step_counters, n_steps, loss_sum, dropout_mask, next_obs, rewards, done, gamma, target_actor_flat,
       target_critic_flat);
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
+}
+
+int sk_critic_grad_f32_sampled(const float* critic_flat, const sk_ring_sample* q, float gamma,
+                               const float* target_actor_flat, const float* target_critic_flat, int64_t batch,
+                               int64_t row_offset, float grad_scale, uint64_t seed, const int64_t* call_counter,
+                               float* partials, float* step_counters, int32_t n_steps, float* loss_sum,
+                               uint8_t* dropout_mask, float* scratch, void* stream) {
+  if (!q || !q->ring || !q->total || !q->s || !q->a || !q->r || !q->s2 || !q->d || q->capacity <= 0) return SK_EINVAL;
+  if ((((uintptr_t)q->ring) & 15) || (((uintptr_t)q->s) & 15) || (((uintptr_t)q->s2) & 15) || (((uintptr_t)q->a) & 7))
+    return SK_EINVAL;
+  const bool boot = target_actor_flat != nullptr;
+  if (boot && !target_critic_flat) return SK_EINVAL;
+  if (!critic_flat || !call_counter || !partials || batch <= 0) return SK_EINVAL;
+  if (row_offset < 0 || (row_offset & 3)) return SK_EINVAL;
+  if ((n_steps > 0 && !step_counters) || n_steps < 0 || n_steps > 64) return SK_EINVAL;
+  int64_t w1_rows = 0;
+  if (sk_update_scratch_f32(batch, &w1_rows) > 0) {
+    if (!scratch) return SK_EINVAL;
+    const RingSample rs{q->ring, q->capacity, q->total, q->seed, q->draw, q->s, q->a, q->r, q->s2, q->d};
+    if (boot)
+      return launch_sliced<kSlCriticBoot>(critic_flat, target_actor_flat, target_critic_flat, q->s, q->s2, q->a,
+                                          nullptr, q->r, q->d, gamma, batch, row_offset, grad_scale, seed,
+                                          call_counter, partials, scratch, w1_rows, step_counters, n_steps, loss_sum,
+                                          dropout_mask, (hipStream_t)stream, rs);
+    return launch_sliced<kSlCriticY>(critic_flat, nullptr, nullptr, q->s, nullptr, q->a, q->r, nullptr, nullptr, 0.f,
+                                     batch, row_offset, grad_scale, seed, call_counter, partials, scratch, w1_rows,
+                                     step_counters, n_steps, loss_sum, dropout_mask, (hipStream_t)stream, rs);
+  }
+  // unsliced batches: the gather as its own launch
+  const int rc = sk_replay_sample(q->ring, q->capacity, q->total, q->seed, q->draw, batch, q->s, q->a, q->r, q->s2,
+                                  q->d, stream);
+  if (rc != SK_OK) return rc;
+  return sk_critic_grad_f32(critic_flat, q->s, q->a, boot ? nullptr : q->r, boot ? q->s2 : nullptr,
+                            boot ? q->r : nullptr, boot ? q->d : nullptr, gamma, target_actor_flat,
+                            target_critic_flat, batch, row_offset, grad_scale, seed, call_counter, partials,
+                            step_counters, n_steps, loss_sum, dropout_mask, scratch, stream);
 }
 
 int sk_actor_grad_f32(const float* actor_flat, const float* critic_flat, const float* obs, int64_t batch,

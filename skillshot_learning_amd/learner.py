@@ -243,12 +243,20 @@ class ReplayRing:
         self._ar = {}
         self.seed = int(seed) & ((1 << 64) - 1)
         self._k = None
+        self._arrivals = None
+        self._draws = 0
+        self._batches = {}
         if self.buf.is_cuda:
             from . import _capi
             self._k = _capi.load()
             self._arrivals = torch.zeros(288, dtype=torch.int32, device=device)  # SK_REPLAY_ARRIVAL_WORDS
-            self._draws = 0
-            self._batches = {}
+
+    def arrivals(self):
+        """the insert launches' arrival counters (SK_REPLAY_ARRIVAL_WORDS,
+        left zeroed by every launch)"""
+        if self._arrivals is None:
+            self._arrivals = torch.zeros(288, dtype=torch.int32, device=self.buf.device)
+        return self._arrivals
 
     head = property(lambda self: self.total % self.cap)
     size = property(lambda self: min(self.total, self.cap))
@@ -343,6 +351,13 @@ class ReplayRing:
                                       torch.empty(b, device=dev), torch.empty(b, STATE_DIM, device=dev),
                                       torch.empty(b, device=dev))
         return out
+
+    def next_draw(self, b):
+        """(the batch buffers, the draw number) of the next device-side sample
+        of b rows (sample_dev's, for a launch that gathers by itself)"""
+        draw = self._draws
+        self._draws = (self._draws + 1) & 0x7FFFFFFF
+        return self._batch_bufs(b), draw
 
     def sample_dev(self, b, generator=None):
         """Capturable uniform sample over the device-side size."""
@@ -574,6 +589,21 @@ class DDPG:
         device_sampling draws the minibatch over the ring's device-side size
         (hipGraph capture)."""
         return self.update_batch(*self.sample_local(batch, device_sampling))
+
+    def update_sampled(self, batch):
+        """replay_update(batch, device_sampling=True) with the minibatch drawn
+        inside the critic step's first launch where the kernels do that (the
+        fp32 fused path, one rank or multi_rank "grad"): one launch fewer per
+        update, bit-identical (the same Philox rows as sample_dev)."""
+        fu = self._fused
+        if fu is None or not fu.f32 or (self.multi() and self.multi_rank == "shared"):
+            return self.replay_update(batch, device_sampling=True)
+        w, rk, b = self.world(), self.rank(), int(batch)
+        if w > 1 and b % 4:
+            raise ValueError("multi-rank batches must be a multiple of 4 rows (Dropout key groups)")
+        lc, (s, _, _, _, _) = fu.critic_step_sampled(self.replay, b, gamma=self.gamma, row_offset=rk * b,
+                                                     global_batch=w * b)
+        return lc, fu.actor_step(s)
 
     def update_batch(self, s, a, r, s2, d):
         """replay_update on this rank's sampled rows s, a, r, s2, d."""
@@ -1035,12 +1065,26 @@ class TickGraph:
                 a.add_(L.action_noise_sd * torch.randn(a.shape, device=a.device, generator=L.gen))
         else:
             a.copy_(L.model_act(obs).view(-1, ACTION_DIM))
+        # SK_FUSED_REPLAY (A/B): 2 (default) the ring insert inside the step
+        # launch and the minibatch drawn inside the critic step's (fp32); 1 the
+        # insert and the first minibatch in one launch after the step; 0 the
+        # insert and the sample as their own launches
+        fused = os.environ.get("SK_FUSED_REPLAY", "2")
+        if fused == "2":
+            L.game_environment.step_insert(self.act, obs, L.replay, reward="looking", auto_reset=True,
+                                           reset_obs=True, out=self.out)
+            self._cur ^= 1
+            if update:
+                for _ in range(self.updates):
+                    L.ddpg.update_sampled(self.batch)
+                L._refresh_actor_pack()
+            return
         o = L.game_environment.step(self.act, obs=True, reward="looking", auto_reset=True, reset_obs=True,
                                     out=self.out)
         # per game: row r of the [2N] rows takes game r % N
         rows = (x, a, o["reward"].view(-1), o["obs"].view(-1, STATE_DIM), o["done"])
         self._cur ^= 1
-        if update and self.updates > 0 and os.environ.get("SK_FUSED_REPLAY", "1") != "0":
+        if update and self.updates > 0 and fused != "0":
             # the insert and the first update's minibatch in one launch
             # (SK_FUSED_REPLAY=0: the two launches, for A/B)
             L.ddpg.update_batch(*L.replay.add_sample_dev(*rows, self.batch))

@@ -29,6 +29,14 @@ def _p(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
+class RingSample(ctypes.Structure):
+    """sk_ring_sample (include/skillshot.h): a minibatch drawn from the replay
+    ring inside the critic step (sk_critic_grad_f32_sampled)."""
+    _fields_ = [("ring", ctypes.c_void_p), ("capacity", ctypes.c_int64), ("total", ctypes.c_void_p),
+                ("seed", ctypes.c_uint64), ("draw", ctypes.c_int32), ("s", ctypes.c_void_p),
+                ("a", ctypes.c_void_p), ("r", ctypes.c_void_p), ("s2", ctypes.c_void_p), ("d", ctypes.c_void_p)]
+
+
 class PackTargets(ctypes.Structure):
     """sk_pack_targets (include/skillshot.h): the packed copies an Adam launch writes."""
     _fields_ = [("param_gpack", ctypes.c_void_p), ("target_gpack", ctypes.c_void_p),
@@ -280,6 +288,33 @@ class FusedUpdate:
         self._adam(part, self.fc, st, self.tc, stat=self.stats[0:1], scale=1.0 / gb, out=loss, counter=self.calls,
                    packs=self._packs(critic=True))
         return loss
+
+    @torch.no_grad()
+    def critic_step_sampled(self, ring, batch, gamma=0.0, row_offset=0, global_batch=None):
+        """critic_step on a minibatch the launch draws from the replay ring
+        (fp32 only): equal to ring.sample_dev(batch) followed by critic_step
+        with the bootstrap target (gamma > 0) or y = r.  Returns (loss, (s, a,
+        r, s2, d)), the sample buffers."""
+        if not self.f32:
+            raise SkillshotError("critic_step_sampled is the fp32 path's")
+        B = int(batch)
+        gb = B if global_batch is None else int(global_batch)
+        out, draw = ring.next_draw(B)
+        q = RingSample(ring.buf.data_ptr(), ring.cap, ring.total_t.data_ptr(), ring.seed, draw,
+                       *[t.data_ptr() for t in out])
+        part = self._partial(B, self.fc.numel())
+        st = self.sc
+        boot = gamma > 0.0
+        ta = (self.ta if self.ta is not None else self.fa) if boot else None
+        tc = (self.tc if self.tc is not None else self.fc) if boot else None
+        _capi.check(self.L.sk_critic_grad_f32_sampled(
+            _p(self.fc), ctypes.byref(q), float(gamma), _p(ta), _p(tc), B, int(row_offset), 2.0 / gb, self.seed,
+            _p(self.calls), _p(part.main), _p(st.steps), st.steps.numel(), _p(self.stats[0:1]), None,
+            _p(part.scratch), self._stream()))
+        loss = self._loss_slot(0)
+        self._adam(part, self.fc, st, self.tc, stat=self.stats[0:1], scale=1.0 / gb, out=loss, counter=self.calls,
+                   packs=self._packs(critic=True))
+        return loss, out
 
     def _critic_grad(self, s, a, target, s2, r, d, gamma, row_offset, gb, part, steps, mask_out, stat=True):
         n_steps = steps.numel() if steps is not None else 0

@@ -276,6 +276,32 @@ class VecSkillshotGame:
                                   _ptr(obs_r), self._stream()))
         return dict(obs=obs_t, reward=rew_t, done=done, winner=win, obs_reset=obs_r)
 
+    def step_insert(self, actions, acting_obs, ring, reward="looking", auto_reset=True, reset_obs=True, out=None):
+        """`step` (obs and reward on) and the replay ring's insert of the tick's
+        2N transitions (acting_obs[r], actions[r], reward[r], obs[r],
+        done[r % N]) in ONE launch (sk_env_step_insert): equal, bit for bit,
+        to step(...) followed by ring.add_dev(acting_obs, actions, reward,
+        obs, done).  ring: learner.ReplayRing on this env's device."""
+        a = self._actions(actions)
+        o = out or {}
+        obs_t = o.get("obs") if o.get("obs") is not None else self.new_obs()
+        rew_t = o.get("reward") if o.get("reward") is not None else torch.empty((2, self.n), dtype=torch.float32,
+                                                                                device=self.device)
+        done = o.get("done") if o.get("done") is not None else torch.empty(self.n, dtype=torch.uint8,
+                                                                            device=self.device)
+        win = o.get("winner") if o.get("winner") is not None else torch.empty(self.n, dtype=torch.uint8,
+                                                                               device=self.device)
+        obs_r = (o.get("obs_reset") if o.get("obs_reset") is not None else self.new_obs()) if reset_obs else None
+        s = acting_obs.float().contiguous()
+        if s.numel() != 2 * self.n * 12:
+            raise ValueError("acting_obs must hold [2, N, 12] floats")
+        check(self._L.sk_env_step_insert(self._h, _ptr(a), _ptr(obs_t), _ptr(rew_t), REWARD_KINDS[reward],
+                                         _ptr(done), _ptr(win), self.tick_limit, int(bool(auto_reset)),
+                                         int(self.random_positions), _ptr(obs_r), _ptr(s), _ptr(ring.buf), ring.cap,
+                                         _ptr(ring.total_t), _ptr(ring.arrivals()), self._stream()))
+        ring.total += 2 * self.n  # host mirror (exact while the row count is fixed)
+        return dict(obs=obs_t, reward=rew_t, done=done, winner=win, obs_reset=obs_r)
+
     def step_raw(self, actions_ptr, done_ptr=None, obs_ptr=None, reward_ptr=None, winner_ptr=None,
                  auto_reset=True, stream=None):
         """Pointer-level fused step (bench / graph capture; no allocation)."""

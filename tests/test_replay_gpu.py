@@ -119,3 +119,91 @@ def test_tick_graph_fused_replay_equals_two_launches(learner, monkeypatch):
     (a1, c1, b1, t1), (a2, c2, b2, t2) = out
     assert t1 == t2 and torch.equal(b1, b2)
     assert torch.equal(a1, a2) and torch.equal(c1, c2)
+
+
+@pytest.mark.parametrize("n,cap", [(5, 64), (300, 1000), (4096, 1 << 14)])
+def test_step_insert_equals_step_then_insert(learner, n, cap):
+    """sk_env_step_insert (the env step with the ring insert in its launch)
+    against sk_env_step followed by sk_replay_insert: the same step outputs,
+    ring and counters bit for bit, every tick, through wrap-around and
+    episode restarts (tick limit 40)"""
+    from skillshot_learning_amd.vec_env import VecSkillshotGame
+    envs = [VecSkillshotGame(n, device="cuda", seed=11, tick_limit=40) for _ in range(2)]
+    rings = [learner.ReplayRing(cap, "cuda", seed=3) for _ in range(2)]
+    obs = [e.reset(random_positions=True) or e.observe()[0].clone() for e in envs]
+    gen = torch.Generator(device="cuda").manual_seed(4)
+    for t in range(2 * cap // (2 * n) + 60):
+        act = torch.rand((2, n, 2), device="cuda", generator=gen) * 2.4 - 1.2
+        o1 = envs[0].step_insert(act, obs[0], rings[0], reset_obs=True)
+        o2 = envs[1].step(act, obs=True, reward="looking", auto_reset=True, reset_obs=True)
+        rings[1].add_dev(obs[1].view(-1, 12), act.view(-1, 2), o2["reward"].view(-1), o2["obs"].view(-1, 12),
+                         o2["done"])
+        torch.cuda.synchronize()
+        for k in ("obs", "reward", "done", "winner", "obs_reset"):
+            assert torch.equal(o1[k], o2[k]), (t, k)
+        assert int(rings[0].total_t) == int(rings[1].total_t) == rings[0].total == rings[1].total
+        assert torch.equal(rings[0].buf, rings[1].buf), t
+        assert not rings[0].arrivals().any()
+        obs = [o1["obs_reset"], o2["obs_reset"]]
+    assert envs[0].counters() == envs[1].counters()
+    assert envs[0].counters()["dones"] > 0
+
+
+@pytest.mark.parametrize("B,gamma", [(256, 0.9), (256, 0.0), (100, 0.9), (1000, 0.9)])
+def test_critic_step_sampled_equals_sample_then_step(learner, B, gamma):
+    """the fp32 critic step drawing its minibatch from the ring inside its
+    first launch (sk_critic_grad_f32_sampled) against sample_dev + the critic
+    step on those rows: identical sample buffers, losses and nets, bit for bit,
+    over several steps (1000 rows: the unsliced path, gather as its own launch)"""
+    out = []
+    for sampled in (True, False):
+        torch.manual_seed(0)
+        d = learner.DDPG("cuda", seed=2, gamma=gamma, tau=0.05, replay_capacity=3000, precision="fp32")
+        g = torch.Generator(device="cuda").manual_seed(9)
+        for t in range(3):
+            d.replay.add_dev(torch.rand(1000, 12, device="cuda", generator=g),
+                             torch.rand(1000, 2, device="cuda", generator=g),
+                             torch.randn(1000, device="cuda", generator=g),
+                             torch.rand(1000, 12, device="cuda", generator=g),
+                             (torch.rand(1000, device="cuda", generator=g) < 0.2).float())
+        losses, batches = [], []
+        for _ in range(4):
+            if sampled:
+                lc, la = d.update_sampled(B)
+            else:
+                lc, la = d.replay_update(B, device_sampling=True)
+            losses.append((lc.clone(), la.clone()))
+            batches.append([x.clone() for x in d.replay._batch_bufs(B)])
+        torch.cuda.synchronize()
+        out.append((losses, batches, torch.cat([p.detach().flatten() for p in d.model_actor.parameters()]),
+                    torch.cat([p.detach().flatten() for p in d.model_critic.parameters()])))
+    (l1, b1, a1, c1), (l2, b2, a2, c2) = out
+    for x, y in zip(b1, b2):
+        for u, v in zip(x, y):
+            assert torch.equal(u, v)
+    for (x1, y1), (x2, y2) in zip(l1, l2):
+        assert torch.equal(x1, x2) and torch.equal(y1, y2)
+    assert torch.equal(a1, a2) and torch.equal(c1, c2)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_tick_graph_replay_modes_equal(learner, monkeypatch, precision):
+    """the captured learner tick with the ring insert in the step launch and
+    the minibatch drawn in the critic's (SK_FUSED_REPLAY=2, default), with the
+    insert + minibatch as one launch (1), and as two (0): identical nets, ring
+    and counters after the same ticks, bit for bit"""
+    out = []
+    for fused in ("2", "1", "0"):
+        monkeypatch.setenv("SK_FUSED_REPLAY", fused)
+        L = learner.SkillshotLearner(n_envs=256, device="cuda", seed=5, exploration="action_noise", gamma=0.9,
+                                     tau=0.05, replay_capacity=4096, precision=precision)
+        tg = L.tick_graph(batch=128, ticks_per_graph=2, warmup=2)
+        tg.run(10)
+        torch.cuda.synchronize()
+        out.append((torch.cat([p.detach().flatten() for p in L.model_actor.parameters()]),
+                    torch.cat([p.detach().flatten() for p in L.model_critic.parameters()]),
+                    L.replay.buf.clone(), int(L.replay.total_t), L.game_environment.counters()))
+    for a, c, b, t, k in out[1:]:
+        assert t == out[0][3] and torch.equal(b, out[0][2])
+        assert torch.equal(a, out[0][0]) and torch.equal(c, out[0][1])
+        assert k == out[0][4]
