@@ -226,6 +226,20 @@ int sk_env_step_insert(sk_env* env, const float* actions, float* obs, float* rew
                        int32_t random_positions, float* obs_reset, const float* acting_obs, float* ring,
                        int64_t capacity, int64_t* total, uint32_t* arrivals, void* stream);
 
+/* The self-play tick's act + step in ONE launch (ABI 7; SkillshotLearner.py
+ * :304-314 act -> do_actions -> game_tick -> get_state): equal, bit for bit,
+ * to sk_actor_forward_f32(actor_flat, acting_obs, actions, 2N, noise_sd,
+ * action_sd, noise_seed, call_counter) with 32-row tiles (SK_FWD16=0)
+ * followed by sk_env_step_insert(env, actions, obs, ..., acting_obs, ring,
+ * ...), or by sk_env_step when ring is NULL.  The observations never
+ * leave the CU between the actor and the step; actions float[2N][2] is
+ * still written.  N % 4 != 0 runs the two launches.  GPU backend only. */
+int sk_env_act_step(sk_env* env, const float* actor_flat, const float* acting_obs, float* actions, float noise_sd,
+                    float action_sd, uint64_t noise_seed, uint64_t* call_counter, float* obs, float* reward,
+                    int32_t reward_kind, uint8_t* done, uint8_t* winner, int32_t tick_limit, int32_t auto_reset,
+                    int32_t random_positions, float* obs_reset, float* ring, int64_t capacity, int64_t* total,
+                    uint32_t* arrivals, void* stream);
+
 /* n_ticks learner ticks of the step-only contract in ONE launch (ABI 5):
  * equal, bit for bit, to n_ticks calls of sk_env_step(obs = reward =
  * obs_reset = NULL) where tick t acts on slab (slab0 + t) % ring_slabs of

@@ -95,6 +95,7 @@ class ActorKernel32:
         self.flat = flatten_module(self.actor)  # idempotent: the parameters stay views of it
 
     fused_action_noise = True  # model_act_action_noise's N(0, sd) is drawn in the kernel
+    fused_act_step = True  # the self-play tick runs it inside the step launch (VecSkillshotGame.act_step)
 
     @torch.no_grad()
     def __call__(self, obs, noise_sd=0.0, generator=None, out=None, action_sd=0.0):

@@ -24,6 +24,7 @@
 
 #include "sk_device.hpp"
 #include "sk_host.hpp"
+#include "sk_step.hpp"
 
 using namespace sk;
 
@@ -78,14 +79,6 @@ static int fail(int code, const std::string& msg) {
   } while (0)
 
 static constexpr int kBlock = 256;
-// Step kernels (k_step*, k_rollout_random) launch one-wave workgroups: 64 vs
-// 256 lanes measured 4.66 vs 4.74 us (65,536 games) and 9.17 vs 9.48 us
-// (262,144) per k_step launch, never slower beyond noise
-// (profiles/r01v_step_block_ab.jsonl; -DSK_STEP_BLOCK=… rebuilds for A/B).
-#ifndef SK_STEP_BLOCK
-#define SK_STEP_BLOCK 64
-#endif
-static constexpr int kStepBlock = SK_STEP_BLOCK;
 static constexpr int64_t kFastStepMinEnvs = 196608;
 static constexpr int64_t kFastStepMaxEnvs = 786432;
 // at or below this many games the step-only tick is latency-bound on a
@@ -99,109 +92,17 @@ static constexpr int64_t kEarlyDrawMinEnvs = 32768;
 // port, 400 ticks per launch: 8,192 games 1.59 vs 1.85 us per tick, 32,768
 // 1.80 vs 2.02, but 65,536 2.59 vs 2.36 (profiles/r03c_multi_split_sweep.jsonl)
 static constexpr int64_t kSplitMultiMaxEnvs = 32768;  // k_step: restart draw under the loads
-// Counter slots per wave: 4 x 32 B = one 128-B line, so no two waves (on
-// different XCDs, whose L2s write partial lines back at the end of the
-// dispatch) share a line: 0.27 us less per 65,536-game k_step than packed
-// 32-B slots (profiles/r02_step_ablation.jsonl).  Only the first slot of a
-// wave's line is written; the host sums them all.
-#ifndef SK_CTR_STRIDE
-#define SK_CTR_STRIDE 4
-#endif
 // SK_CTR_STRIDE slots per wave of the widest step grid (k_step_split: two
 // lanes per game), at least SK_COUNTER_SLOTS
 static inline int64_t counter_slots(int64_t n) {
-  const int64_t waves = (2 * n + 63) / 64;
+  // k_act_step32 counts one line per 16-game workgroup
+  const int64_t w2 = (2 * n + 63) / 64, w16 = (n + 15) / 16, waves = w2 > w16 ? w2 : w16;
   return waves * SK_CTR_STRIDE > SK_COUNTER_SLOTS ? waves * SK_CTR_STRIDE : SK_COUNTER_SLOTS;
 }
 static inline size_t aux_bytes(int64_t n) { return 256 + (size_t)counter_slots(n) * sizeof(sk_counters); }
 
 static inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 static inline unsigned step_grid(int64_t n) { return (unsigned)((n + kStepBlock - 1) / kStepBlock); }
-
-// ------------------------------------------------------------------ counters
-// Episode counters: one slot line per wave of the launch (global wave index),
-// so no two waves of a launch share a slot and no atomics are needed.  A wave
-// loads its slot at entry (ctr_load, under the state loads' latency), ballots
-// its done / hit-by-id lanes, sums their final ticks, and lane 0 stores
-// slot + counts with one vector store after the state stores.  Launches on a
-// stream are ordered, so the read-modify-write is race-free; the host sums
-// the slots.  Round 1 added per-wave device atomics into 256 shared slots and
-// summed the ticks with a 64-bit shuffle tree; counting then cost 0.42 of a
-// 4.62 us 65,536-game k_step, now 0.04 us (profiles/r02_step_ablation.jsonl).
-template <int BLK = kStepBlock>
-__device__ __forceinline__ sk_counters* ctr_slot(sk_counters* base) {
-  // every kernel that counts launches BLK-lane workgroups (a constant, not
-  // blockDim, whose dispatch-packet load would land on the wave's tail)
-  const unsigned wave = blockIdx.x * (BLK >> 6) + (threadIdx.x >> 6);
-  return base + (size_t)wave * SK_CTR_STRIDE;
-}
-
-struct WaveCtr {
-  ulonglong4 v;
-};
-
-template <int BLK = kStepBlock>
-__device__ __forceinline__ WaveCtr ctr_load(sk_counters* base) {
-  WaveCtr w;
-#ifdef SK_CTR_NOMEM  // timing ablation: counting without its memory traffic
-  w.v = make_ulonglong4(0, 0, 0, 0);
-#else
-  w.v = base ? *reinterpret_cast<const ulonglong4*>(ctr_slot<BLK>(base)) : make_ulonglong4(0, 0, 0, 0);
-#endif
-  return w;
-}
-
-// Called once the wave's loads have all been consumed (the tick is done): an
-// empty asm that redefines the slot values, so the final counter store does
-// not depend on a load the waitcnt pass still sees pending.  Without it the
-// pass (its tracking lost across the tick's branches) put an s_waitcnt
-// vmcnt(0) before that store, i.e. made every wave wait for its own state
-// stores to be acknowledged before issuing one more: +0.5 us per 65,536-game
-// k_step (profiles/r02_step_ablation.jsonl).
-__device__ __forceinline__ void ctr_settle(WaveCtr& w) {
-  asm volatile("" : "+v"(w.v.x), "+v"(w.v.y), "+v"(w.v.z), "+v"(w.v.w));
-}
-
-template <int BLK = kStepBlock>
-__device__ __forceinline__ void ctr_store(sk_counters* base, const WaveCtr& w, uint64_t dones, uint64_t h1,
-                                          uint64_t h2, uint64_t tsum) {
-#ifdef SK_CTR_NOMEM
-  asm volatile("" ::"s"(dones + h1 + h2 + tsum));
-  return;
-#endif
-  if ((threadIdx.x & 63) == 0)
-    *reinterpret_cast<ulonglong4*>(ctr_slot<BLK>(base)) =
-        make_ulonglong4(w.v.x + dones, w.v.y + h1, w.v.z + h2, w.v.w + tsum);
-}
-
-// The store is unconditional (32 B per wave per launch), so the slot's load
-// has a use on every path and stays at kernel entry instead of being sunk
-// into the rare done branch.  The finished games' ticks are summed by a
-// wave-uniform scalar loop of readlanes over the done lanes (almost always
-// one), not a 6-step 64-bit shuffle tree: a wave with a finished game is the
-// tick's slowest (it also draws the random restart), and the kernel ends with
-// it.  Callers count after their state stores, so this overlaps the stores'
-// drain.
-__device__ __forceinline__ void wave_count(sk_counters* ctr, const WaveCtr& w, bool done, int winner, int ticks) {
-  const uint64_t m_done = __ballot(done);
-  const uint64_t m_w1 = __ballot(done && winner == 1);
-  const uint64_t m_w2 = __ballot(done && winner == 2);
-  uint64_t t = 0;
-  for (uint64_t m = m_done; m; m &= m - 1)  // wave-uniform
-    t += (uint32_t)__builtin_amdgcn_readlane(ticks, (int)__builtin_ctzll(m));
-  ctr_store(ctr, w, __popcll(m_done), __popcll(m_w1), __popcll(m_w2), t);
-}
-
-__device__ __forceinline__ void store_obs(float* obs, int64_t n, int p, int64_t i, const float o[12]) {
-  // the row is 48 B into a 16-B aligned buffer: say so, or the backend may
-  // re-split the three vector stores at 4-byte alignment (dwordx3 + x4 + x4
-  // + x1 at offsets 0/12/28/44 in k_step_split)
-  typedef float f4 __attribute__((ext_vector_type(4)));
-  f4* d = reinterpret_cast<f4*>(__builtin_assume_aligned(obs + ((int64_t)p * n + i) * 12, 16));
-  d[0] = f4{o[0], o[1], o[2], o[3]};
-  d[1] = f4{o[4], o[5], o[6], o[7]};
-  d[2] = f4{o[8], o[9], o[10], o[11]};
-}
 
 __device__ __forceinline__ float reward_of(const Cfg& c, const Env& e, int p, int kind, double path_dist) {
   if (kind == SK_REWARD_SIMPLE) {  // SkillshotLearner.py:600
@@ -211,23 +112,6 @@ __device__ __forceinline__ float reward_of(const Cfg& c, const Env& e, int p, in
     return (float)(mine - theirs);
   }
   return (float)(-path_dist / (double)c.W);  // SkillshotLearner.py:584
-}
-
-// ------------------------------------------------------------------ step slots
-struct StepRef {
-  uint64_t* slots;
-  int parity;
-};
-
-// Wave-uniform plain load (one s_load per wave through the scalar cache; the
-// dispatch boundary's cache invalidation makes the previous launch's write
-// visible).  Per-lane agent-scope loads of this one line throttled big grids.
-__device__ __forceinline__ uint64_t step_read(const StepRef& s) {
-  return s.slots[s.parity];
-}
-
-__device__ __forceinline__ void step_advance(const StepRef& s, uint64_t base, uint64_t inc) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) s.slots[1 - s.parity] = base + inc;
 }
 
 // ------------------------------------------------------------------ step trace
@@ -242,66 +126,6 @@ __device__ unsigned long long* sk_step_trace;
 #else
 #define SK_TS(var)
 #endif
-
-// ------------------------------------------------------------------ actions
-// The action slab is read once per tick (the actor's output or a pre-generated
-// random-policy slab): nontemporal (streaming) loads.  At 65,536 games with
-// the slab streamed from HBM the tick takes 4.74 instead of 4.93 us
-// (profiles/r01x_act_nt_ab.jsonl, three alternating passes).
-__device__ __forceinline__ float2 load_action(const float2* p) {
-  float2 v;
-  v.x = __builtin_nontemporal_load(&p->x);
-  v.y = __builtin_nontemporal_load(&p->y);
-  return v;
-}
-
-// ------------------------------------------------------------------ kernels
-struct StepArgs {
-  View v;
-  int64_t n;
-  const float2* actions;  // [2][N] float2
-  float* obs;
-  float* reward;
-  int reward_kind;
-  uint8_t* done;
-  uint8_t* winner;
-  int tick_limit;
-  int auto_reset;
-  int random_positions;
-  float* obs_reset;
-  uint64_t seed;
-  int64_t env_offset;
-  StepRef step;
-  sk_counters* ctr;
-  // the replay ring insert of the tick's 2N transitions (sk_env_step_insert;
-  // k_step_split only, with obs and reward): row r = p N + i of the [2N]
-  // actor order -> ring row (total + r) % cap, as sk_replay_insert
-  const float* acting_obs;  // [2N][12] the observations the actions were taken on
-  float* ring;              // [cap][28] (NULL: no insert)
-  int64_t ring_cap;
-  int64_t* ring_total;
-  uint32_t* ring_arrivals;  // SK_REPLAY_ARRIVAL_WORDS
-};
-
-// The ring insert's end of launch (sk_replay.hip's grouped arrival): lane 0
-// of workgroup b arrives on group line arrivals[32 (1 + b % 8)], the last of
-// each group on arrivals[0]; the last workgroup (every other one has read
-// total) stores the new total.  Called by every lane 0 (lane 0 of a launched
-// workgroup always steps a game).
-__device__ __forceinline__ void ring_arrive(uint32_t* arrivals, int64_t* total, int64_t new_total) {
-  if (threadIdx.x != 0) return;
-  const unsigned g = blockIdx.x & 7u;
-  const unsigned members = (gridDim.x - g + 7u) / 8u;
-  uint32_t* gc = arrivals + 32u * (1u + g);
-  if (atomicAdd(gc, 1u) == members - 1u) {
-    *gc = 0u;
-    const unsigned groups = gridDim.x < 8u ? gridDim.x : 8u;
-    if (atomicAdd(arrivals, 1u) == groups - 1u) {
-      *total = new_total;
-      *arrivals = 0u;
-    }
-  }
-}
 
 // OBS: the launch writes obs / reward / obs_reset (instantiated apart so the
 // step-only tick keeps no obs state live: holding the projectiles' sincos for
@@ -522,172 +346,15 @@ __global__ void __launch_bounds__(kStepBlock) k_step_fast(StepArgs a, Cfg c) {
 // identically.  Twice the waves of k_step, half the dependent chain per lane.
 __global__ void __launch_bounds__(kStepBlock) k_step_split(StepArgs a, Cfg c) {
   const int64_t gt = (int64_t)blockIdx.x * kStepBlock + threadIdx.x;
-  const int64_t i = gt >> 1;
-  const int p = (int)(gt & 1);
-  const uint64_t step = step_read(a.step);
-  step_advance(a.step, step, 1);
-  const bool in = i < a.n;
-  const int64_t h = 2 * i + p;  // this lane's half-plane index
-  WaveCtr wc = ctr_load(a.ctr);
-  // Loads are unconditional (a lane past the end reads game 0 and stores
-  // nothing), so no exec-mask branch surrounds them and each value is waited
-  // for on its own: issued rotation first, action last, the player's sincos
-  // of its old rotation then runs while the rest arrives.  (Loads inside
-  // `if (in)` made the join wait for all of them, action included.)
-  const int64_t ic = in ? i : 0, hc = 2 * ic + p;
-  double rot = reinterpret_cast<const double*>(a.v.rot)[hc];
-  double qrot = reinterpret_cast<const double*>(a.v.qrot)[hc];
-  const int2 pp = reinterpret_cast<const int2*>(a.v.pos)[hc];
-  const int2 ca = reinterpret_cast<const int2*>(a.v.qcdage)[hc];
-  const int2 qq = reinterpret_cast<const int2*>(a.v.qpos)[hc];
-  const int2 mi = a.v.misc[ic];
+  sk_counters* slot = a.ctr ? ctr_slot(a.ctr) : nullptr;
+  const StepLane L = split_load(a, gt, slot);
+  // Loads are unconditional (split_load): issued rotation first, action
+  // last, the player's sincos of its old rotation then runs while the rest
+  // arrives
   __builtin_amdgcn_sched_barrier(0);
-  const float2 act = load_action(a.actions + (int64_t)p * a.n + ic);
+  const float2 act = load_action(a.actions + (int64_t)L.p * a.n + L.ic);
   __builtin_amdgcn_sched_barrier(0);
-  // the ring insert's sources and base (wave-uniform scalar load; read before
-  // this workgroup signals its arrival below)
-  const bool ins = a.ring != nullptr;  // launch-uniform
-  int64_t rbase = 0;
-  float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0, s2 = s0;
-  if (ins) {
-    rbase = *a.ring_total;
-    const float4* so = reinterpret_cast<const float4*>(a.acting_obs + ((int64_t)p * a.n + ic) * 12);
-    s0 = so[0];
-    s1 = so[1];
-    s2 = so[2];
-  }
-  bool k0, k1, k2;
-  sktrig::SinCos m = sktrig::sincos_bf(rot, &k0);
-  int px = pp.x, py = pp.y, qx = qq.x, qy = qq.y, qcd = ca.x, qage = ca.y, ticks = mi.x;
-  const int flags = mi.y;
-  int qvalid = ((unsigned)flags >> (8 * p)) & 0xff;
-  int live = ((unsigned)flags >> 16) & 0xff;
-  int winner = ((unsigned)flags >> 24) & 0xff;
-  // do_actions(p+1, ...)  SkillshotLearner.py:206-213, both sincos up front (tick_env)
-  const double rn = rot + clamp_action((double)act.y) * c.look;
-  const double qn = (qcd <= 0) ? rn : qrot;
-  sktrig::SinCos t = sktrig::sincos_bf(qn, &k1);
-  // the post-look rotation's sin/cos for the obs epilogue (fp32: obs12_sc)
-  sktrig::SinCosF pr = sktrig::sincos_fast(rn, &k2);
-  if (!(k0 & k1 & k2)) {
-    if (!k0) m = sincos_lib(rot);
-    if (!k1) t = sincos_lib(qn);
-    if (!k2) {
-      const sktrig::SinCos r = sincos_lib(rn);
-      pr.s = (float)r.s;
-      pr.c = (float)r.c;
-    }
-  }
-  move_direction_sc(c, px, py, m, (double)act.x);
-  rot = rn;
-  shoot_s(c, px, py, rot, qx, qy, qrot, qcd, qage, qvalid);
-  // game_tick  SkillshotGame.py:115-122 (live is identical in both lanes)
-  if (live) {
-    ticks += 1;
-    projectile_tick_sc(c, qx, qy, t, qcd, qage, qvalid);
-  }
-  const int opx = pair_swap(px), opy = pair_swap(py);
-  const int oqx = pair_swap(qx), oqy = pair_swap(qy), oqv = pair_swap(qvalid);
-  if (live) {
-    if (p == 0) collide_s(c, px, py, qx, qy, qvalid, opx, opy, oqx, oqy, oqv, live, winner);
-    else collide_s(c, opx, opy, oqx, oqy, oqv, px, py, qx, qy, qvalid, live, winner);
-  }
-  ctr_settle(wc);  // every load consumed, no state store issued yet
-  const bool d = in && ((!live) || (ticks >= a.tick_limit));  // SkillshotLearner.py:302
-  const bool want_obs = a.obs || a.reward || a.obs_reset;     // launch-uniform
-  float o[12];
-  bool amb = false;
-  double gq = 0.0;  // the fast projectile gradient (the ambiguous flag's interval check)
-  if (in && want_obs) {
-    float pd;
-#ifdef SK_ABL_NOOBS  // timing ablation only: obs values without their arithmetic
-    for (int k = 0; k < 12; ++k) o[k] = (float)(px + k * qx) + pr.s * (float)t.c;
-    pd = o[3];
-#else
-    obs12_sc(c, px, py, rot, pr, qx, qy, qrot, t, qcd, qvalid, opx, opy, o, &pd, &amb, &gq);
-#endif
-    if (a.obs) store_obs(a.obs, a.n, p, i, o);
-    if (a.reward) {
-      float r;
-      if (a.reward_kind == SK_REWARD_SIMPLE) {  // a difference of distances: fp64 roots
-        double mine = dist_point_point(qx, qy, opx, opy);
-        double theirs = dist_point_point(oqx, oqy, px, py);
-        r = (float)(mine - theirs);
-      } else {
-        r = (float)(-(double)pd / (double)c.W);
-      }
-      a.reward[(int64_t)p * a.n + i] = r;
-      if (ins) {  // s, a, r, s', done: the row sk_replay_insert would write
-        float4* dst = reinterpret_cast<float4*>(a.ring + ((rbase + (int64_t)p * a.n + i) % a.ring_cap) * 28);
-        dst[0] = s0;
-        dst[1] = s1;
-        dst[2] = s2;
-        dst[3] = make_float4(act.x, act.y, r, o[0]);
-        dst[4] = make_float4(o[1], o[2], o[3], o[4]);
-        dst[5] = make_float4(o[5], o[6], o[7], o[8]);
-        dst[6] = make_float4(o[9], o[10], o[11], d ? 1.f : 0.f);
-      }
-    }
-  }
-  if (ins) ring_arrive(a.ring_arrivals, a.ring_total, rbase + 2 * a.n);
-  if (in && p == 0) {
-    if (a.done) a.done[i] = (uint8_t)d;
-    if (a.winner) a.winner[i] = (uint8_t)winner;
-  }
-  if (!in) return;
-  const int fin_winner = winner, fin_ticks = ticks;  // before the restart
-  const int aqx = qx, aqy = qy;  // the post-tick projectile, for the flag's redo
-  const double aqrot = qrot;
-  const bool reset = d && a.auto_reset;
-  if (reset) {  // SkillshotGame.__init__ :10-25 for this lane's player
-    if (a.random_positions) {
-      U4 u = draw4(a.seed, (uint64_t)(a.env_offset + i), step, 1u);
-      px = u32_to_pos(p ? u.z : u.x, c.rlo, c.rhi);
-      py = u32_to_pos(p ? u.w : u.y, c.rlo, c.rhi);
-    } else {
-      px = p ? c.f2x : c.f1x;
-      py = p ? c.f2y : c.f1y;
-    }
-    rot = 0.0; qx = 0; qy = 0; qrot = 0.0; qcd = 0; qage = 0; qvalid = 0;
-    ticks = 0; live = 1; winner = 0;
-  }
-  if (a.obs_reset) {
-    // a game that did not restart acts next on the obs just computed; a
-    // restarted one (both lanes of the pair) on its fresh state's, whose
-    // rotations are 0 (sin 0, cos 1: no trig) and projectile invalid
-    const int rpx = pair_swap(px), rpy = pair_swap(py);
-    if (reset) {  // (its projectile is invalid: the flag is 0, never ambiguous)
-      float pd;
-      bool amb_r;
-      obs12_sc(c, px, py, rot, sktrig::SinCosF{0.0f, 1.0f}, qx, qy, qrot, sktrig::SinCos{0.0, 1.0}, qcd, qvalid,
-               rpx, rpy, o, &pd, &amb_r);
-    }
-    store_obs(a.obs_reset, a.n, p, i, o);
-  }
-  reinterpret_cast<int2*>(a.v.pos)[h] = make_int2(px, py);
-  reinterpret_cast<double*>(a.v.rot)[h] = rot;
-  reinterpret_cast<int2*>(a.v.qpos)[h] = make_int2(qx, qy);
-  reinterpret_cast<double*>(a.v.qrot)[h] = qrot;
-  reinterpret_cast<int2*>(a.v.qcdage)[h] = make_int2(qcd, qage);
-  const int ov = pair_swap(qvalid);
-  if (p == 0) {
-    unsigned f = (unsigned)(qvalid & 0xff) | ((unsigned)(ov & 0xff) << 8) | ((unsigned)(live & 0xff) << 16) |
-                 ((unsigned)(winner & 0xff) << 24);
-    a.v.misc[i] = make_int2(ticks, (int)f);
-  }
-  if (a.ctr) wave_count(a.ctr, wc, d && p == 0, fin_winner, fin_ticks);  // after the stores (see wave_count)
-  // The future-collision flag within its margin of an edge is settled here,
-  // after every other store: ~3 lanes per 65,536-game tick, mostly hits
-  // (terminal states); by the interval check unless it depends on g's last
-  // bits (then the correctly rounded tan).  tan_cr on those lanes made their
-  // waves the tick's tail: 8.5 vs 6.9 us (profiles/r02_split_flag_ab.jsonl).
-  if (amb) {
-    const int fi = future_flag_interval(c, aqx, aqy, opx, opy, gq);
-    const float f = fi >= 0 ? (float)fi : future_flag_cr(c, aqx, aqy, aqrot, opx, opy);
-    if (a.obs) a.obs[((int64_t)p * a.n + i) * 12 + 11] = f;
-    if (a.obs_reset && !reset) a.obs_reset[((int64_t)p * a.n + i) * 12 + 11] = f;
-    if (ins) a.ring[((rbase + (int64_t)p * a.n + i) % a.ring_cap) * 28 + 26] = f;  // s'[11]
-  }
+  split_finish(a, c, L, act, slot);
 }
 
 struct RolloutArgs {
@@ -1880,6 +1547,62 @@ int sk_env_step_insert(sk_env* e, const float* actions, float* obs, float* rewar
   if (!ring) return fail(SK_EINVAL, "ring is NULL");
   return step_launch(e, actions, obs, reward, reward_kind, done, winner, tick_limit, auto_reset, random_positions,
                      obs_reset, acting_obs, ring, capacity, total, arrivals, stream);
+}
+
+int sk_env_act_step(sk_env* e, const float* actor_flat, const float* acting_obs, float* actions, float noise_sd,
+                    float action_sd, uint64_t noise_seed, uint64_t* call_counter, float* obs, float* reward,
+                    int32_t reward_kind, uint8_t* done, uint8_t* winner, int32_t tick_limit, int32_t auto_reset,
+                    int32_t random_positions, float* obs_reset, float* ring, int64_t capacity, int64_t* total,
+                    uint32_t* arrivals, void* stream) {
+  SK_CHECK_ENV(e);
+  if (e->host) return fail(SK_EINVAL, "sk_env_act_step runs on the GPU backend");
+  if (!actor_flat || !acting_obs || !actions) return fail(SK_EINVAL, "actor_flat / acting_obs / actions is NULL");
+  if ((((uintptr_t)actions) & 7) || (((uintptr_t)acting_obs) & 15))
+    return fail(SK_EINVAL, "actions must be 8-byte aligned, acting_obs 16-byte");
+  if (e->n % 4) {  // the fused tile keys its noise by aligned 4-row groups: two launches
+    const int rc = sk_actor_forward_f32(actor_flat, acting_obs, actions, 2 * (int64_t)e->n, noise_sd, action_sd,
+                                        noise_seed, call_counter, stream);
+    if (rc != SK_OK) return fail(rc, "sk_actor_forward_f32 failed");
+    return step_launch(e, actions, obs, reward, reward_kind, done, winner, tick_limit, auto_reset,
+                       random_positions, obs_reset, acting_obs, ring, capacity, total, arrivals, stream);
+  }
+  if ((((uintptr_t)obs) & 15) || (((uintptr_t)obs_reset) & 15))
+    return fail(SK_EINVAL, "obs buffers must be 16-byte aligned");
+  if (reward_kind != SK_REWARD_LOOKING && reward_kind != SK_REWARD_SIMPLE) return fail(SK_EINVAL, "bad reward_kind");
+  if (ring) {
+    if (!obs || !reward || !total || !arrivals)
+      return fail(SK_EINVAL, "ring insert needs obs, reward, total and arrivals");
+    if (capacity <= 0 || 2 * (int64_t)e->n > capacity) return fail(SK_EINVAL, "ring capacity below 2 N rows");
+    if ((((uintptr_t)ring) & 15) || (((uintptr_t)total) & 7))
+      return fail(SK_EINVAL, "ring must be 16-byte aligned, total 8-byte");
+  }
+  StepArgs a;
+  a.v = e->view;
+  a.n = e->n;
+  a.actions = reinterpret_cast<const float2*>(actions);
+  a.obs = obs;
+  a.reward = reward;
+  a.reward_kind = reward_kind;
+  a.done = done;
+  a.winner = winner;
+  a.tick_limit = tick_limit;
+  a.auto_reset = auto_reset;
+  a.random_positions = random_positions;
+  a.obs_reset = obs_reset;
+  a.seed = e->seed;
+  a.env_offset = e->env_offset;
+  a.step = StepRef{e->d_step, e->parity};
+  a.ctr = e->d_counters;
+  a.acting_obs = acting_obs;
+  a.ring = ring;
+  a.ring_cap = capacity;
+  a.ring_total = total;
+  a.ring_arrivals = arrivals;
+  const int rc = sk_launch_act_step32(actor_flat, actions, noise_sd, action_sd, noise_seed, call_counter, a, e->dcfg,
+                                      (hipStream_t)stream);
+  if (rc != SK_OK) return fail(rc, "k_act_step32 launch failed");
+  e->parity ^= 1;
+  return SK_OK;
 }
 
 int sk_env_step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64_t slab0, int32_t n_ticks,

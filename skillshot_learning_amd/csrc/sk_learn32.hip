@@ -32,6 +32,7 @@
 
 #include "../../include/skillshot.h"
 #include "sk_partial.hpp"
+#include "sk_step.hpp"
 
 namespace {
 
@@ -1440,27 +1441,39 @@ __device__ __forceinline__ void normals4(uint64_t seed, uint64_t call, uint32_t 
   }
 }
 
+// Row maps of a 32-row actor tile: local row i -> global row of the [rows]
+// batch, and whether it exists.  Contiguous: rows row0 .. row0 + 31.
+// Players (the self-play tick, k_act_step32): games g0 .. g0 + 15, rows
+// g0 + i (player 1) and N + g0 + i - 16 (player 2) of the actor's
+// player-major [2N] order.  Parameter / action noise is keyed by the global
+// row (the first row of an aligned 4-row group), so with N % 4 == 0 both maps
+// draw the same noise for the same row.
+struct RowsContig {
+  int64_t row0, rows;
+  __device__ int64_t operator()(int i) const { return row0 + i; }
+  __device__ bool valid(int i) const { return row0 + i < rows; }
+};
+struct RowsPlayers {
+  int64_t g0, n;
+  __device__ int64_t operator()(int i) const { return i < 16 ? g0 + i : n + g0 + (i - 16); }
+  __device__ bool valid(int i) const { return g0 + (i & 15) < n; }
+};
+
 // one 32-row tile per workgroup of 4 waves: layer 1 n-tiles 2w, 2w+1,
 // layer 2 n-tile w, layer 3 by all threads.  NOISE: per layer y = xW + b +
 // sd sqrt(x^2 W^2 + b^2) xi, xi ~ N(0,1) per (row, unit) (exact in
 // distribution for w' = w (1 + sd N(0,1)) drawn per row, each noisy weight
-// being used once per row).
-template <bool NOISE>
-__global__ void __launch_bounds__(kFwdThreads) k_actor_fwd32(const float* __restrict__ aflat,
-                                                             const float* __restrict__ X, float* __restrict__ out,
-                                                             int64_t rows, float sd, float action_sd, uint64_t seed,
-                                                             uint64_t* __restrict__ call_ctr) {
-  __shared__ __attribute__((aligned(16))) float S[32 * kLdS];
-  __shared__ __attribute__((aligned(16))) float H1[32 * kLdH1];
-  __shared__ __attribute__((aligned(16))) float H2[32 * kLdH2];
+// being used once per row).  The actions go to out[R(i)] and, if act_lds,
+// to act_lds[i].  S, H1, H2: the tile's LDS.
+template <bool NOISE, typename MAP>
+__device__ __forceinline__ void actor_tile32(const Net& A, const float* __restrict__ X, float* __restrict__ out,
+                                             const MAP& R, float sd, float action_sd, uint64_t seed, uint64_t call,
+                                             float* S, float* H1, float* H2, float2* act_lds) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const Net A = net_of(aflat, kALd, 2);
-  const int64_t row0 = (int64_t)blockIdx.x * 32;
-  // a launch that draws noise (parameter or action) uses call number
-  // counter + 1 and its last workgroup stores that number back
-  const bool draws = (NOISE || action_sd != 0.f) && call_ctr;
-  const uint64_t call = draws ? call_ctr[0] + 1 : 0;
-  stage_states(S, X, row0, rows);
+  for (int t = threadIdx.x; t < 32 * kLdS; t += kFwdThreads) {  // S[i][k] = obs (k < 12, valid rows), else 0
+    const int i = t / kLdS, k = t - i * kLdS;
+    S[t] = (k < kIn && R.valid(i)) ? X[R(i) * kIn + k] : 0.f;
+  }
   __syncthreads();
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -1472,7 +1485,7 @@ __global__ void __launch_bounds__(kFwdThreads) k_actor_fwd32(const float* __rest
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         float z[4];
-        normals4(seed, call, (uint32_t)(row0 + drow(4 * g, lane)), (uint32_t)u, z);
+        normals4(seed, call, (uint32_t)R(drow(4 * g, lane)), (uint32_t)u, z);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int v = 4 * g + q;
@@ -1496,7 +1509,7 @@ __global__ void __launch_bounds__(kFwdThreads) k_actor_fwd32(const float* __rest
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         float z[4];
-        normals4(seed, call, (uint32_t)(row0 + drow(4 * g, lane)), (uint32_t)(kH1 + u), z);
+        normals4(seed, call, (uint32_t)R(drow(4 * g, lane)), (uint32_t)(kH1 + u), z);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int v = 4 * g + q;
@@ -1533,25 +1546,84 @@ __global__ void __launch_bounds__(kFwdThreads) k_actor_fwd32(const float* __rest
         v1 += __shfl_xor(v1, off, 64);
       }
     }
-    if (c == 0 && row0 + i < rows) {
+    if (c == 0 && R.valid(i)) {
+      const int64_t row = R(i);
       float y0 = m0 + A.b3[0], y1 = m1 + A.b3[1];
       if (NOISE) {
         float z[4];
-        normals4(seed, call, (uint32_t)(row0 + i), (uint32_t)(kH1 + kH2), z);
+        normals4(seed, call, (uint32_t)row, (uint32_t)(kH1 + kH2), z);
         y0 += sd * __builtin_amdgcn_sqrtf(v0 + A.b3[0] * A.b3[0]) * z[0];
         y1 += sd * __builtin_amdgcn_sqrtf(v1 + A.b3[1] * A.b3[1]) * z[1];
       }
       float o0 = tanhf(y0), o1 = tanhf(y1);
       if (action_sd != 0.f) {  // model_act_action_noise (:229-243): tanh output + N(0, sd), unclipped
         float z[4];
-        normals4(seed, call, (uint32_t)(row0 + i), (uint32_t)(kH1 + kH2 + 1), z);
+        normals4(seed, call, (uint32_t)row, (uint32_t)(kH1 + kH2 + 1), z);
         o0 += action_sd * z[0];
         o1 += action_sd * z[1];
       }
-      *(float2*)(out + (row0 + i) * 2) = make_float2(o0, o1);
+      *(float2*)(out + row * 2) = make_float2(o0, o1);
+      if (act_lds) act_lds[i] = make_float2(o0, o1);
     }
   }
+}
+
+template <bool NOISE>
+__global__ void __launch_bounds__(kFwdThreads) k_actor_fwd32(const float* __restrict__ aflat,
+                                                             const float* __restrict__ X, float* __restrict__ out,
+                                                             int64_t rows, float sd, float action_sd, uint64_t seed,
+                                                             uint64_t* __restrict__ call_ctr) {
+  __shared__ __attribute__((aligned(16))) float S[32 * kLdS];
+  __shared__ __attribute__((aligned(16))) float H1[32 * kLdH1];
+  __shared__ __attribute__((aligned(16))) float H2[32 * kLdH2];
+  const Net A = net_of(aflat, kALd, 2);
+  // a launch that draws noise (parameter or action) uses call number
+  // counter + 1 and its last workgroup stores that number back
+  const bool draws = (NOISE || action_sd != 0.f) && call_ctr;
+  const uint64_t call = draws ? call_ctr[0] + 1 : 0;
+  actor_tile32<NOISE>(A, X, out, RowsContig{(int64_t)blockIdx.x * 32, rows}, sd, action_sd, seed, call, S, H1, H2,
+                      nullptr);
   if (draws) {  // the last workgroup to finish stores the call number it drew with
+    __syncthreads();
+    advance_call32(call_ctr, call);
+  }
+}
+
+// The self-play tick's act + step in ONE launch (VERDICT r02 item 3;
+// SkillshotLearner.py:304-314 act -> do_actions -> game_tick -> get_state,
+// with the replay ring insert of sk_env_step_insert): workgroup b owns games
+// 16b .. 16b + 15.  Wave 0's lanes 0-31 issue k_step_split's state loads
+// (both players of the 16 games) first, so they land under the actor's
+// MFMA chain; the 4 waves run the fp32 actor tile on the games' 32
+// observation rows (RowsPlayers); the actions meet in LDS; wave 0 then
+// finishes k_step_split's tick for its lanes.  Equal, bit for bit, to
+// sk_actor_forward_f32 (32-row tiles) followed by sk_env_step(_insert).
+// Wave 0 counts its games into counter slot line b.
+template <bool NOISE>
+__global__ void __launch_bounds__(kFwdThreads) k_act_step32(const float* __restrict__ aflat, float* __restrict__ act_out,
+                                                            float sd, float action_sd, uint64_t seed,
+                                                            uint64_t* __restrict__ call_ctr, sk::StepArgs a,
+                                                            sk::Cfg c) {
+  __shared__ __attribute__((aligned(16))) float S[32 * kLdS];
+  __shared__ __attribute__((aligned(16))) float H1[32 * kLdH1];
+  __shared__ __attribute__((aligned(16))) float H2[32 * kLdH2];
+  __shared__ float2 sAct[32];
+  const int lane = threadIdx.x & 63;
+  const bool w0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0;
+  const int64_t g0 = (int64_t)blockIdx.x * 16;
+  sk_counters* slot = a.ctr ? a.ctr + (size_t)blockIdx.x * SK_CTR_STRIDE : nullptr;
+  sk::StepLane L;
+  if (w0) L = sk::split_load(a, lane < 32 ? 2 * g0 + lane : 2 * a.n, slot);
+  const Net A = net_of(aflat, kALd, 2);
+  const bool draws = (NOISE || action_sd != 0.f) && call_ctr;
+  const uint64_t call = draws ? call_ctr[0] + 1 : 0;
+  actor_tile32<NOISE>(A, a.acting_obs, act_out, RowsPlayers{g0, a.n}, sd, action_sd, seed, call, S, H1, H2, sAct);
+  __syncthreads();
+  if (w0) {
+    const float2 act = lane < 32 ? sAct[(lane & 1) * 16 + (lane >> 1)] : make_float2(0.f, 0.f);
+    sk::split_finish(a, c, L, act, slot);
+  }
+  if (draws) {
     __syncthreads();
     advance_call32(call_ctr, call);
   }
@@ -1736,6 +1808,17 @@ int launch_sliced(const float* f0, const float* f1, const float* f2, const float
 }
 
 }  // namespace
+
+// the self-play tick launch (sk_env_act_step, csrc/sk_engine.hip): a.n % 4 == 0
+int sk_launch_act_step32(const float* aflat, float* act_out, float sd, float action_sd, uint64_t seed,
+                         uint64_t* call_ctr, const sk::StepArgs& a, const sk::Cfg& c, hipStream_t st) {
+  const unsigned G = (unsigned)((a.n + 15) / 16);
+  if (sd != 0.f)
+    k_act_step32<true><<<G, kFwdThreads, 0, st>>>(aflat, act_out, sd, action_sd, seed, call_ctr, a, c);
+  else
+    k_act_step32<false><<<G, kFwdThreads, 0, st>>>(aflat, act_out, 0.f, action_sd, seed, call_ctr, a, c);
+  return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
+}
 
 extern "C" {
 

@@ -1056,6 +1056,21 @@ class TickGraph:
         x = obs.view(-1, STATE_DIM)
         a = self.act.view(-1, ACTION_DIM)
         mode = L.exploration
+        fused = os.environ.get("SK_FUSED_REPLAY", "2")
+        if (fused == "2" and getattr(L.actor_kernel, "fused_act_step", False)
+                and os.environ.get("SK_FUSED_ACT", "1") != "0"):
+            # the actor forward inside the step launch (sk_env_act_step): the
+            # observations stay on the CU between act and step
+            L.game_environment.act_step(L.actor_kernel, obs,
+                                        noise_sd=L.param_noise_sd if mode == "param_noise" else 0.0,
+                                        action_sd=L.action_noise_sd if mode == "action_noise" else 0.0,
+                                        ring=L.replay, out=self.out, actions=self.act)
+            self._cur ^= 1
+            if update:
+                for _ in range(self.updates):
+                    L.ddpg.update_sampled(self.batch)
+                L._refresh_actor_pack()
+            return
         if L.actor_kernel is not None and mode == "action_noise" and getattr(L.actor_kernel, "fused_action_noise",
                                                                                False):
             L.actor_kernel(x, out=a, action_sd=L.action_noise_sd)
@@ -1068,8 +1083,8 @@ class TickGraph:
         # SK_FUSED_REPLAY (A/B): 2 (default) the ring insert inside the step
         # launch and the minibatch drawn inside the critic step's (fp32); 1 the
         # insert and the first minibatch in one launch after the step; 0 the
-        # insert and the sample as their own launches
-        fused = os.environ.get("SK_FUSED_REPLAY", "2")
+        # insert and the sample as their own launches.  SK_FUSED_ACT=0 keeps
+        # the actor forward as its own launch (fp32 actor, mode 2)
         if fused == "2":
             L.game_environment.step_insert(self.act, obs, L.replay, reward="looking", auto_reset=True,
                                            reset_obs=True, out=self.out)

@@ -302,6 +302,40 @@ class VecSkillshotGame:
         ring.total += 2 * self.n  # host mirror (exact while the row count is fixed)
         return dict(obs=obs_t, reward=rew_t, done=done, winner=win, obs_reset=obs_r)
 
+    def act_step(self, actor, acting_obs, noise_sd=0.0, action_sd=0.0, ring=None, reward="looking", auto_reset=True,
+                 reset_obs=True, out=None, actions=None):
+        """The self-play tick's act + step (+ ring insert) in ONE launch
+        (sk_env_act_step): `actor` (actor_kernel.ActorKernel32, the fp32
+        actor) acts on acting_obs [2, N, 12] for both players of every game
+        with parameter noise noise_sd and/or action noise action_sd, and the
+        step runs on those actions; equal, bit for bit, to actor(...) with
+        32-row tiles followed by step_insert (ring given) or step.  Returns
+        step's dict plus `actions` [2, N, 2]."""
+        o = out or {}
+        obs_t = o.get("obs") if o.get("obs") is not None else self.new_obs()
+        rew_t = o.get("reward") if o.get("reward") is not None else torch.empty((2, self.n), dtype=torch.float32,
+                                                                                device=self.device)
+        done = o.get("done") if o.get("done") is not None else torch.empty(self.n, dtype=torch.uint8,
+                                                                            device=self.device)
+        win = o.get("winner") if o.get("winner") is not None else torch.empty(self.n, dtype=torch.uint8,
+                                                                               device=self.device)
+        obs_r = (o.get("obs_reset") if o.get("obs_reset") is not None else self.new_obs()) if reset_obs else None
+        act = actions if actions is not None else torch.empty((2, self.n, 2), dtype=torch.float32, device=self.device)
+        s = acting_obs.float().contiguous()
+        if s.numel() != 2 * self.n * 12 or act.numel() != 4 * self.n or not act.is_contiguous():
+            raise ValueError("acting_obs must hold [2, N, 12] floats, actions [2, N, 2] (contiguous)")
+        ring_args = ((_ptr(ring.buf), ring.cap, _ptr(ring.total_t), _ptr(ring.arrivals())) if ring is not None
+                     else (None, 0, None, None))
+        actor.calls += 1
+        check(self._L.sk_env_act_step(self._h, _ptr(actor.flat), _ptr(s), _ptr(act), float(noise_sd),
+                                      float(action_sd), actor.seed, _ptr(actor._ctr), _ptr(obs_t), _ptr(rew_t),
+                                      REWARD_KINDS[reward], _ptr(done), _ptr(win), self.tick_limit,
+                                      int(bool(auto_reset)), int(self.random_positions), _ptr(obs_r), *ring_args,
+                                      self._stream()))
+        if ring is not None:
+            ring.total += 2 * self.n  # host mirror
+        return dict(obs=obs_t, reward=rew_t, done=done, winner=win, obs_reset=obs_r, actions=act)
+
     def step_raw(self, actions_ptr, done_ptr=None, obs_ptr=None, reward_ptr=None, winner_ptr=None,
                  auto_reset=True, stream=None):
         """Pointer-level fused step (bench / graph capture; no allocation)."""

@@ -186,24 +186,64 @@ def test_critic_step_sampled_equals_sample_then_step(learner, B, gamma):
     assert torch.equal(a1, a2) and torch.equal(c1, c2)
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
-def test_tick_graph_replay_modes_equal(learner, monkeypatch, precision):
-    """the captured learner tick with the ring insert in the step launch and
-    the minibatch drawn in the critic's (SK_FUSED_REPLAY=2, default), with the
-    insert + minibatch as one launch (1), and as two (0): identical nets, ring
-    and counters after the same ticks, bit for bit"""
+@pytest.mark.parametrize("precision,exploration", [("fp32", "action_noise"), ("fp32", "param_noise"),
+                                                   ("bf16", "action_noise")])
+def test_tick_graph_replay_modes_equal(learner, monkeypatch, precision, exploration):
+    """the captured learner tick with the actor forward, the env step and the
+    ring insert in one launch and the minibatch drawn in the critic's
+    (SK_FUSED_REPLAY=2, default; fp32), with the actor as its own launch
+    (SK_FUSED_ACT=0), with the insert + minibatch as one launch (1), and as two
+    (0): identical nets, ring and counters after the same ticks, bit for bit
+    (32-row actor tiles everywhere: SK_FWD16=0)"""
+    monkeypatch.setenv("SK_FWD16", "0")
     out = []
-    for fused in ("2", "1", "0"):
+    for fused, act in (("2", "1"), ("2", "0"), ("1", "1"), ("0", "1")):
         monkeypatch.setenv("SK_FUSED_REPLAY", fused)
-        L = learner.SkillshotLearner(n_envs=256, device="cuda", seed=5, exploration="action_noise", gamma=0.9,
-                                     tau=0.05, replay_capacity=4096, precision=precision)
+        monkeypatch.setenv("SK_FUSED_ACT", act)
+        L = learner.SkillshotLearner(n_envs=256, device="cuda", seed=5, exploration=exploration, gamma=0.9,
+                                     tau=0.05, replay_capacity=4096, precision=precision, tick_limit=50)
         tg = L.tick_graph(batch=128, ticks_per_graph=2, warmup=2)
-        tg.run(10)
+        tg.run(30)
         torch.cuda.synchronize()
         out.append((torch.cat([p.detach().flatten() for p in L.model_actor.parameters()]),
                     torch.cat([p.detach().flatten() for p in L.model_critic.parameters()]),
                     L.replay.buf.clone(), int(L.replay.total_t), L.game_environment.counters()))
+    assert out[0][4]["dones"] > 0
     for a, c, b, t, k in out[1:]:
         assert t == out[0][3] and torch.equal(b, out[0][2])
         assert torch.equal(a, out[0][0]) and torch.equal(c, out[0][1])
         assert k == out[0][4]
+
+
+@pytest.mark.parametrize("n", [256, 4096, 300, 302])
+@pytest.mark.parametrize("noise", ["none", "param", "action"])
+def test_act_step_equals_actor_then_step_insert(learner, monkeypatch, n, noise):
+    """sk_env_act_step (the fp32 actor forward, the env step and the ring
+    insert in one launch) against sk_actor_forward_f32 (32-row tiles) then
+    sk_env_step_insert: the same actions, step outputs, ring, counters and
+    noise call number bit for bit, every tick, through restarts (300 games: a
+    partial last 16-game tile; 302: N % 4 != 0, the two-launch fallback)"""
+    from skillshot_learning_amd.actor_kernel import ActorKernel32
+    from skillshot_learning_amd.vec_env import VecSkillshotGame
+    monkeypatch.setenv("SK_FWD16", "0")
+    torch.manual_seed(1)
+    actor = learner.Actor().cuda()
+    sd, asd = {"none": (0.0, 0.0), "param": (0.5, 0.0), "action": (0.0, 0.15)}[noise]
+    ks = [ActorKernel32(actor, seed=9) for _ in range(2)]
+    envs = [VecSkillshotGame(n, device="cuda", seed=11, tick_limit=30) for _ in range(2)]
+    rings = [learner.ReplayRing(1 << 13, "cuda", seed=3) for _ in range(2)]
+    obs = [e.observe()[0].clone() for e in envs]
+    for t in range(45):
+        o1 = envs[0].act_step(ks[0], obs[0], noise_sd=sd, action_sd=asd, ring=rings[0])
+        act = ks[1](obs[1].view(-1, 12), noise_sd=sd, action_sd=asd).view(2, n, 2)
+        o2 = envs[1].step_insert(act, obs[1], rings[1], reset_obs=True)
+        torch.cuda.synchronize()
+        assert torch.equal(o1["actions"], act), t
+        for k in ("obs", "reward", "done", "winner", "obs_reset"):
+            assert torch.equal(o1[k], o2[k]), (t, k)
+        assert torch.equal(rings[0].buf, rings[1].buf), t
+        assert int(rings[0].total_t) == int(rings[1].total_t)
+        assert torch.equal(ks[0]._ctr, ks[1]._ctr)
+        obs = [o1["obs_reset"], o2["obs_reset"]]
+    assert envs[0].counters() == envs[1].counters()
+    assert envs[0].counters()["dones"] > 0

@@ -1,7 +1,8 @@
 #!/bin/bash
 # full GPU suite; config-3 learner tick A/B of the replay fusion modes
-# (SK_FUSED_REPLAY 2 = insert in the step, gather in the critic; 1 = one
-# insert+sample launch), 3 alternating passes; rocprof stats of mode 2
+# (SK_FUSED_REPLAY 2 = insert in the step, gather in the critic, with the fp32
+# actor in the step launch (SK_FUSED_ACT=1) or not; 1 = one insert+sample
+# launch), 3 alternating passes; rocprof stats of the default
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && export TMPDIR=/tmp
 O=gpurun_out/r03x; mkdir -p $O
@@ -12,11 +13,14 @@ import json, os, sys
 sys.path.insert(0, ".")
 import bench
 for rep in range(3):
-    for mode in ("1", "2"):
+    for mode, act in (("1", "1"), ("2", "0"), ("2", "1")):
         for pr in ("fp32", "bf16"):
+            if pr == "bf16" and act == "0":
+                continue
             os.environ["SK_FUSED_REPLAY"] = mode
+            os.environ["SK_FUSED_ACT"] = act
             r = bench.learner_rate(4096, 1, 0, 400, batch=256, exploration="action_noise", precision=pr)
-            print(json.dumps(dict(rep=rep, mode=mode, precision=pr, us_per_tick=round(r["ms_per_tick"] * 1e3, 2),
+            print(json.dumps(dict(rep=rep, mode=mode, act=act, precision=pr, us_per_tick=round(r["ms_per_tick"] * 1e3, 2),
                                   gpu_us=round(r["gpu_ms_per_tick"] * 1e3, 2))), flush=True)
 PY
 cat $O/replay_modes_ab.jsonl
