@@ -223,18 +223,32 @@ __global__ void __launch_bounds__(threads_for<NOISE>()) k_actor_fwd(const float*
     // each lane accumulates fp32 partial dot products of W3 (and W3^2 for the
     // noise variance) over the 64 layer-2 units it holds; the two lane halves
     // are combined with one cross-half shuffle.
+    // k-step outer, output chunk inner: the 4 chunks' accumulator chains (8
+    // with the variance GEMM) are independent, so no MFMA waits on its
+    // predecessor's result, and each k-step's h1^2 fragment is squared once
+    // (not once per chunk).  Every accumulator sums its k-steps in the same
+    // order as a chunk-outer loop: the results are bit-identical.
+    f32x16 accs[4], vars[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      accs[t] = f32x16{0};
+      vars[t] = f32x16{0};
+    }
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      const bf16x8 hs = NOISE ? sq_bf16(h1[kk]) : h1[kk];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        accs[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sW2[(t * 16 + kk) * 64 + lane], h1[kk], accs[t], 0, 0, 0);
+        if (NOISE)
+          vars[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sW2s[(t * 16 + kk) * 64 + lane], hs, vars[t], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // cap hoisted LDS fragments
+    }
     float m0 = 0.f, m1 = 0.f, q0 = 0.f, q1 = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      f32x16 acc = {0}, var = {0};
-#pragma unroll
-      for (int kk = 0; kk < 16; ++kk) {
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sW2[(t * 16 + kk) * 64 + lane], h1[kk], acc, 0, 0, 0);
-        if (NOISE)
-          var = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sW2s[(t * 16 + kk) * 64 + lane], sq_bf16(h1[kk]), var, 0, 0,
-                                                        0);
-        if (NOISE && (kk & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // cap hoisted LDS fragments
-      }
+      const f32x16 acc = accs[t], var = vars[t];
       float z[16];
       if (NOISE) normals16(seed, call, (uint32_t)row, (uint32_t)(8 + t), h, k2, z);
 #pragma unroll

@@ -154,7 +154,8 @@ def test_critic_step_sampled_equals_sample_then_step(learner, B, gamma):
     """the fp32 critic step drawing its minibatch from the ring inside its
     first launch (sk_critic_grad_f32_sampled) against sample_dev + the critic
     step on those rows: identical sample buffers, losses and nets, bit for bit,
-    over several steps (1000 rows: the unsliced path, gather as its own launch)"""
+    over several steps (1000 rows: the unsliced path, gather as its own launch);
+    the reported losses to 1e-5 (their per-workgroup sums arrive by atomics)"""
     out = []
     for sampled in (True, False):
         torch.manual_seed(0)
@@ -181,8 +182,8 @@ def test_critic_step_sampled_equals_sample_then_step(learner, B, gamma):
     for x, y in zip(b1, b2):
         for u, v in zip(x, y):
             assert torch.equal(u, v)
-    for (x1, y1), (x2, y2) in zip(l1, l2):
-        assert torch.equal(x1, x2) and torch.equal(y1, y2)
+    for (x1, y1), (x2, y2) in zip(l1, l2):  # the loss sums arrive by float atomics: order-dependent rounding
+        assert torch.allclose(x1, x2, rtol=1e-5, atol=0) and torch.allclose(y1, y2, rtol=1e-5, atol=0)
     assert torch.equal(a1, a2) and torch.equal(c1, c2)
 
 

@@ -170,7 +170,7 @@ def test_critic_bootstrap_grad_matches_explicit_target(mods, rows):
 
 
 def test_adam_and_soft_update_match_torch(mods):
-    from skillshot_learning_amd.update_kernel import partial_index
+    from skillshot_learning_amd.update_kernel import _Partials, partial_index
     learner = mods
     torch.manual_seed(0)
     d = _ddpg(learner, seed=3, tau=0.05)
@@ -186,7 +186,7 @@ def test_adam_and_soft_update_match_torch(mods):
         st.steps += 1
         part = torch.empty_like(g)
         part[partial_index(P, g.device)] = g
-        d._fused._adam(part.view(1, -1), d._fused.fc, st, d._fused.tc)
+        d._fused._adam(_Partials(part.view(1, -1)), d._fused.fc, st, d._fused.tc)
         # torch: the same gradient through torch.optim.Adam + lerp
         off = 0
         for p in ref.model_critic.parameters():

@@ -6,8 +6,9 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && export TMPDIR=/tmp
 O=gpurun_out/r03x; mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 240 --timeout-method thread > $O/pytest_gpu.txt 2>&1 || { tail -30 $O/pytest_gpu.txt; exit 1; }
-tail -3 $O/pytest_gpu.txt
+timeout -k 10 600 python -u -m pytest tests -m gpu --maxfail=10 -q -p no:cacheprovider --timeout 240 --timeout-method thread > $O/pytest_gpu.txt 2>&1
+rc=$?; grep -E "^(FAILED|ERROR)" $O/pytest_gpu.txt; tail -3 $O/pytest_gpu.txt
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc  # a fault / abort / timeout ends the call
 timeout -k 10 300 python -u - > $O/replay_modes_ab.jsonl 2> $O/replay_modes_ab.err <<'PY' || { tail -20 $O/replay_modes_ab.err; exit 1; }
 import json, os, sys
 sys.path.insert(0, ".")
