@@ -1464,7 +1464,13 @@ struct RowsPlayers {
 // sd sqrt(x^2 W^2 + b^2) xi, xi ~ N(0,1) per (row, unit) (exact in
 // distribution for w' = w (1 + sd N(0,1)) drawn per row, each noisy weight
 // being used once per row).  The actions go to out[R(i)] and, if act_lds,
-// to act_lds[i].  S, H1, H2: the tile's LDS.
+// to act_lds[i].  S, H1, H2: the tile's LDS.  Phase trace of the 4,096-game
+// act + step launch (tools/trace_act_step.py, profiles/r03t_*): staging 1.1,
+// layer 1 1.3, layer 2 5.2 (128 dependent 32x32x2 f32 MFMAs per wave, ~0.77
+// of the CU's f32 MFMA rate), layer 3 1.2, the step 2.8 us.  Preloading every
+// weight operand before (or after) the staging loads was slower at every
+// size (profiles/r03u2_*, r03u3_*: layer 2 stays ~4.4 us, the staging waits
+// behind the weight traffic, occupancy halves).
 template <bool NOISE, typename MAP>
 __device__ __forceinline__ void actor_tile32(const Net& A, const float* __restrict__ X, float* __restrict__ out,
                                              const MAP& R, float sd, float action_sd, uint64_t seed, uint64_t call,
@@ -1475,6 +1481,7 @@ __device__ __forceinline__ void actor_tile32(const Net& A, const float* __restri
     S[t] = (k < kIn && R.valid(i)) ? X[R(i) * kIn + k] : 0.f;
   }
   __syncthreads();
+  TP32(2);
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const int nt = 2 * w + t, u = 32 * nt + (lane & 31);
@@ -1499,6 +1506,7 @@ __device__ __forceinline__ void actor_tile32(const Net& A, const float* __restri
     }
   }
   __syncthreads();
+  TP32(3);
   {
     const int u = 32 * w + (lane & 31);
     f32x16 m = {0}, var = {0};
@@ -1523,6 +1531,7 @@ __device__ __forceinline__ void actor_tile32(const Net& A, const float* __restri
     }
   }
   __syncthreads();
+  TP32(4);
   {  // layer 3: thread t -> row t / 8, units 16 (t % 8) .. (both outputs)
     const int i = threadIdx.x >> 3, c = threadIdx.x & 7;
     float m0 = 0.f, m1 = 0.f, v0 = 0.f, v1 = 0.f;
@@ -1612,17 +1621,22 @@ __global__ void __launch_bounds__(kFwdThreads) k_act_step32(const float* __restr
   const bool w0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0;
   const int64_t g0 = (int64_t)blockIdx.x * 16;
   sk_counters* slot = a.ctr ? a.ctr + (size_t)blockIdx.x * SK_CTR_STRIDE : nullptr;
+  TP32(0);
   sk::StepLane L;
   if (w0) L = sk::split_load(a, lane < 32 ? 2 * g0 + lane : 2 * a.n, slot);
+  TP32(1);
   const Net A = net_of(aflat, kALd, 2);
   const bool draws = (NOISE || action_sd != 0.f) && call_ctr;
   const uint64_t call = draws ? call_ctr[0] + 1 : 0;
   actor_tile32<NOISE>(A, a.acting_obs, act_out, RowsPlayers{g0, a.n}, sd, action_sd, seed, call, S, H1, H2, sAct);
+  TP32(5);
   __syncthreads();
+  TP32(6);
   if (w0) {
     const float2 act = lane < 32 ? sAct[(lane & 1) * 16 + (lane >> 1)] : make_float2(0.f, 0.f);
     sk::split_finish(a, c, L, act, slot);
   }
+  TP32(7);
   if (draws) {
     __syncthreads();
     advance_call32(call_ctr, call);
