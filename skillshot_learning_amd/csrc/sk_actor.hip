@@ -198,13 +198,13 @@ __global__ void __launch_bounds__(threads_for<NOISE>()) k_actor_fwd(const float*
       f32x16 acc = {0}, var = {0};
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gW1[c * 64 + lane], xb, acc, 0, 0, 0);
       if (NOISE) var = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gW1s[c * 64 + lane], xs, var, 0, 0, 0);
-      float z[16];
-      if (NOISE) normals16(seed, call, (uint32_t)row, (uint32_t)c, h, k2, z);
+      Pairs8 z;
+      if (NOISE) pairs8(seed, call, (uint32_t)row, (uint32_t)c, h, k2, z);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int hid = 32 * c + (i & 3) + 8 * (i >> 2) + 4 * h;
         const float b = sB[hid];
-        float y = NOISE ? noisy_pre(acc[i], b, var[i], z[i]) : acc[i] + b;
+        float y = NOISE ? noisy_pre_pair(acc[i], b, var[i], z, i) : acc[i] + b;
         y = fmaxf(y, 0.f);
         acc[i] = y;
         if (DBG && valid) dbg[row * kDbgCols + hid] = y;
@@ -249,19 +249,19 @@ __global__ void __launch_bounds__(threads_for<NOISE>()) k_actor_fwd(const float*
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const f32x16 acc = accs[t], var = vars[t];
-      float z[16];
-      if (NOISE) normals16(seed, call, (uint32_t)row, (uint32_t)(8 + t), h, k2, z);
+      Pairs8 z;
+      if (NOISE) pairs8(seed, call, (uint32_t)row, (uint32_t)(8 + t), h, k2, z);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int hid = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
         const float b = sB[kH1 + hid];
-        float y = NOISE ? noisy_pre(acc[i], b, var[i], z[i]) : acc[i] + b;
+        float y = NOISE ? noisy_pre_pair(acc[i], b, var[i], z, i) : acc[i] + b;
         y = fmaxf(y, 0.f);
         if (DBG && valid) {
           dbg[row * kDbgCols + kH1 + hid] = y;
           dbg[row * kDbgCols + 386 + hid] = acc[i];
           dbg[row * kDbgCols + 386 + kH2 + hid] = NOISE ? var[i] : 0.f;
-          dbg[row * kDbgCols + 386 + 2 * kH2 + hid] = NOISE ? z[i] / sd : 0.f;
+          dbg[row * kDbgCols + 386 + 2 * kH2 + hid] = NOISE ? pair_normal(z, i) / sd : 0.f;
         }
         m0 = __builtin_fmaf(sW3[hid], y, m0);
         m1 = __builtin_fmaf(sW3[kH2 + hid], y, m1);
@@ -377,13 +377,13 @@ __global__ void __launch_bounds__(kWgThreads) k_actor_fwd_wg(const float* __rest
       f32x16 acc = {0}, var = {0};
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gW1[c * 64 + lane], xb, acc, 0, 0, 0);
       if (NOISE) var = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gW1s[c * 64 + lane], xs, var, 0, 0, 0);
-      float z[16];
-      if (NOISE) normals16(seed, call, (uint32_t)row, (uint32_t)c, h, k2, z);
+      Pairs8 z;
+      if (NOISE) pairs8(seed, call, (uint32_t)row, (uint32_t)c, h, k2, z);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int hid = 32 * c + (i & 3) + 8 * (i >> 2) + 4 * h;
         const float b = sB[hid];
-        float y = NOISE ? noisy_pre(acc[i], b, var[i], z[i]) : acc[i] + b;
+        float y = NOISE ? noisy_pre_pair(acc[i], b, var[i], z, i) : acc[i] + b;
         acc[i] = fmaxf(y, 0.f);
       }
 #pragma unroll
@@ -407,13 +407,13 @@ __global__ void __launch_bounds__(kWgThreads) k_actor_fwd_wg(const float* __rest
         if (NOISE)
           var = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sW2s[(t * 16 + kk) * 64 + lane], sq_bf16(hb), var, 0, 0, 0);
       }
-      float z[16];
-      if (NOISE) normals16(seed, call, (uint32_t)row, (uint32_t)(8 + t), h, k2, z);
+      Pairs8 z;
+      if (NOISE) pairs8(seed, call, (uint32_t)row, (uint32_t)(8 + t), h, k2, z);
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int hid = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
         const float b = sB[kH1 + hid];
-        float y = NOISE ? noisy_pre(acc[i], b, var[i], z[i]) : acc[i] + b;
+        float y = NOISE ? noisy_pre_pair(acc[i], b, var[i], z, i) : acc[i] + b;
         y = fmaxf(y, 0.f);
         m0 = __builtin_fmaf(sW3[hid], y, m0);
         m1 = __builtin_fmaf(sW3[kH2 + hid], y, m1);

@@ -58,8 +58,17 @@ __host__ __device__ __forceinline__ int w2_k(int kk, int h, int j) {
 }
 
 // ---------------------------------------------------------------- noise
-#ifndef SK_NOISE_ROUNDS  // Philox rounds of the actors' exploration noise (A/B builds)
-#define SK_NOISE_ROUNDS 10
+// Philox rounds of the bf16 actor's parameter-noise draws (normals16 /
+// pairs8; A/B builds override).  Philox4x32-7 is the fewest rounds of the
+// family that pass TestU01 BigCrush (Salmon et al., SC'11; 10 is the library
+// default, kept as a safety margin everywhere else: the fp32 path's noise,
+// the Dropout masks, the replay sampling, action noise).  The noisy bf16
+// forward is VALU-issue-bound (~29 % of its cycles were Philox's 64-bit
+// multiplies): 7 rounds take the 131,072-row launch 60.4 -> 55.8 us
+// (profiles/r03y3_bf16_noise_pair_philox_ab.jsonl); the noise is pinned
+// statistically (the two-sample KS test against explicit weight noise).
+#ifndef SK_NOISE_ROUNDS
+#define SK_NOISE_ROUNDS 7
 #endif
 template <int ROUNDS = 10>
 __device__ __forceinline__ uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
@@ -105,6 +114,42 @@ __device__ __forceinline__ void normals16(uint64_t seed, uint64_t call, uint32_t
       z[8 * q + 2 * p + 1] = rad * __builtin_amdgcn_sinf(rev);
     }
   }
+}
+
+// The same 16 draws as normals16 in Box-Muller pair form, for the noisy
+// pre-activations: pair p holds L = k2 log2 u1 (the squared radius) and the
+// angle's cos / sin, so y_i = m + b + sqrt((b^2 + v) L) * {cos, sin} takes one
+// square root per element (noisy_pre_pair) instead of the radius's plus the
+// element's: 5 transcendentals per pair instead of 6 (the noisy bf16 forward is
+// VALU-issue-bound; profiles/r03y3_bf16_noise_pair_philox_ab.jsonl)
+struct Pairs8 {
+  float L[8], c[8], s[8];
+};
+__device__ __forceinline__ void pairs8(uint64_t seed, uint64_t call, uint32_t row, uint32_t stream, int h, float k2,
+                                       Pairs8& n) {
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    uint4 u = philox<SK_NOISE_ROUNDS>(make_uint4(row, (stream * 2 + (uint32_t)h) * 2 + q, (uint32_t)call,
+                                                 (uint32_t)(call >> 32)),
+                     (uint32_t)seed, (uint32_t)(seed >> 32));
+    uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const float u1 = ((float)(w[p] & 0xFFFFu) + 0.5f) * 0x1p-16f;  // (0, 1)
+      const float rev = (float)(w[p] >> 16) * 0x1p-16f;               // [0, 1) revolutions
+      n.L[4 * q + p] = k2 * __builtin_amdgcn_logf(u1);
+      n.c[4 * q + p] = __builtin_amdgcn_cosf(rev);
+      n.s[4 * q + p] = __builtin_amdgcn_sinf(rev);
+    }
+  }
+}
+// element i of the pair form (normal i of normals16, for diagnostics)
+__device__ __forceinline__ float pair_normal(const Pairs8& n, int i) {
+  return __builtin_amdgcn_sqrtf(n.L[i >> 1]) * ((i & 1) ? n.s[i >> 1] : n.c[i >> 1]);
+}
+__device__ __forceinline__ float noisy_pre_pair(float m, float b, float v, const Pairs8& n, int i) {
+  return __builtin_fmaf(__builtin_amdgcn_sqrtf(__builtin_fmaf(b, b, v) * n.L[i >> 1]),
+                        (i & 1) ? n.s[i >> 1] : n.c[i >> 1], m + b);
 }
 
 // 2 normals of standard deviation sd (model_act_action_noise's N(0, sd) on

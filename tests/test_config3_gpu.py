@@ -70,12 +70,12 @@ def test_config3_fused_update_equals_autograd(learner_mod, precision):
     on the same batch and Dropout masks.  fp32 (the reference's precision):
     1e-4 relative Frobenius per parameter (measured ~1e-6: fp32 sums in
     another order; tests/test_learn32_gpu.py holds the kernels to 1e-5 of the
-    fp64 Keras restatement).  bf16: 12 % (measured 0.2-2 % over seeds 22-24
+    fp64 Keras restatement).  bf16: 5 % (measured 0.2-2 % over seeds 22-24
     on the replay's real observations, tools/diag_config3.py; the rotation
     features reach ~9.9, so layer-1 operand rounding weighs more than on
     test_update_gpu's data)."""
     from test_update_gpu import _check_grads
-    REL = 1e-4 if precision == "fp32" else 0.12
+    REL = 1e-4 if precision == "fp32" else 0.05
     L = learner_mod.SkillshotLearner(n_envs=N, device="cuda", seed=22, exploration="action_noise", gamma=0.99,
                                      tau=0.005, replay_capacity=CAP, precision=precision)
     L.train_ticks(4, batch=BATCH)
