@@ -427,7 +427,7 @@ def learner_rate(envs, world, rank, ticks, batch=256, exploration="param_noise",
     verbose = os.environ.get("SK_BENCH_VERBOSE") == "1"
     if verbose:
         _log(f"learner {envs} games: capturing")
-    tg = L.tick_graph(batch=batch, updates_per_tick=1, ticks_per_graph=2)
+    tg = L.tick_graph(batch=batch, updates_per_tick=1, ticks_per_graph=int(os.environ.get("SK_TICKS_PER_GRAPH", "2")))
     if verbose:
         _log(f"learner {envs} games: captured ({tg.multi_rank_mode})")
     tg.run(10)
@@ -438,7 +438,7 @@ def learner_rate(envs, world, rank, ticks, batch=256, exploration="param_noise",
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     e0.record(tg.stream)
-    tg.run(ticks // 2)
+    tg.run(max(1, ticks // tg.ticks))
     e1.record(tg.stream)
     torch.cuda.synchronize()
     if world > 1:
@@ -448,7 +448,7 @@ def learner_rate(envs, world, rank, ticks, batch=256, exploration="param_noise",
         tt = torch.tensor([el], dtype=torch.float64, device=L.device)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
-    n_ticks = (ticks // 2) * 2
+    n_ticks = max(1, ticks // tg.ticks) * tg.ticks
     gpu_ms = e0.elapsed_time(e1) / n_ticks
     out = dict(envs_per_gpu=envs, total_envs=envs * world, n_gpus=world, ticks=n_ticks, batch_per_rank=batch,
                exploration=exploration, updates_per_tick=1, dtype=precision, multi_rank=tg.multi_rank_mode,

@@ -1004,7 +1004,11 @@ class TickGraph:
         else:
             self.graph = torch.cuda.CUDAGraph()
             self.graph.register_generator_state(L.gen)
-            with torch.cuda.graph(self.graph, stream=self.stream):
+            # thread-local capture: only this thread's HIP calls are checked
+            # against the capture, so RCCL's watchdog thread may keep
+            # querying the events of eager collectives from the warm-up
+            # (global mode aborted the process when it did, intermittently)
+            with torch.cuda.graph(self.graph, stream=self.stream, capture_error_mode="thread_local"):
                 for _ in range(self.ticks):
                     self._tick(update=True)
         self.stream.synchronize()
@@ -1023,7 +1027,7 @@ class TickGraph:
         def begin():
             g = torch.cuda.CUDAGraph()
             g.register_generator_state(L.gen)
-            g.capture_begin(pool=pool)
+            g.capture_begin(pool=pool, capture_error_mode="thread_local")
             cur[:] = [g]
 
         def cut(fn):
