@@ -540,6 +540,16 @@ int sk_critic_grad_f32_sampled(const float* critic_flat, const sk_ring_sample* s
                                int64_t row_offset, float grad_scale, uint64_t seed, const int64_t* call_counter,
                                float* partials, float* step_counters, int32_t n_steps, float* loss_sum,
                                uint8_t* dropout_mask, float* scratch, void* stream);
+/* The bf16 critic step (sk_critic_grad_bootstrap; target_actor_gpack NULL:
+ * y = q->r) on a minibatch its launch draws from the ring (ABI 7): equal,
+ * bit for bit, to sk_replay_sample into q's buffers followed by
+ * sk_critic_grad_bootstrap on them; the sample buffers are written (the
+ * actor step reads q->s). */
+int sk_critic_grad_bootstrap_sampled(const void* critic_gpack, const sk_ring_sample* sample, float gamma,
+                                     const void* target_actor_gpack, const void* target_critic_gpack, int64_t batch,
+                                     int64_t row_offset, float grad_scale, uint64_t seed,
+                                     const int64_t* call_counter, float* partials, float* step_counters,
+                                     int32_t n_steps, float* loss_sum, uint8_t* dropout_mask, void* stream);
 int sk_actor_grad_f32(const float* actor_flat, const float* critic_flat, const float* obs, int64_t batch,
                       float loss_scale, float* partials, float* step_counters, int32_t n_steps, float* q_sum,
                       float* scratch, void* stream);

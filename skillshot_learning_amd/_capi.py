@@ -34,7 +34,7 @@ EXPORTS = (
     "sk_target_y", "sk_replay_insert", "sk_replay_sample", "sk_replay_insert_sample", "sk_grad_pack_flat",
     "sk_critic_grad_bootstrap",
     "sk_update_partials_f32", "sk_actor_forward_f32", "sk_critic_grad_f32", "sk_critic_grad_f32_sampled",
-    "sk_actor_grad_f32",
+    "sk_critic_grad_bootstrap_sampled", "sk_actor_grad_f32",
 )
 
 
@@ -150,6 +150,8 @@ def load(build_if_missing=True):
                                ctypes.c_int),
         "sk_critic_grad_f32_sampled": ([P, P, f32, P, P, i64, i64, f32, u64, P, P, P, i32, P, P, P, P],
                                        ctypes.c_int),
+        "sk_critic_grad_bootstrap_sampled": ([P, P, f32, P, P, i64, i64, f32, u64, P, P, P, i32, P, P, P],
+                                             ctypes.c_int),
         "sk_actor_grad_f32": ([P, P, P, i64, f32, P, P, i32, P, P, P], ctypes.c_int),
         "sk_update_scratch_f32": ([i64, P], ctypes.c_int64),
         "sk_adam_flat_sliced": ([P, i32, P, i32, i32, P, P, i32, P, P, P, P, f32, f32, f32, f32, P, f32, P, f32, P, P,

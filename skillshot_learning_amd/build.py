@@ -14,8 +14,10 @@ ROOT = os.path.dirname(HERE)
 LIB_DIR = os.path.join(HERE, "lib")
 # SK_LIB_PATH: load a prebuilt variant instead (A/B experiments, tools/gpu_lib_ab.sh)
 LIB_PATH = os.environ.get("SK_LIB_PATH") or os.path.join(LIB_DIR, "libskillshot.so")
-SOURCES = [os.path.join(HERE, "csrc", "sk_engine.hip"), os.path.join(HERE, "csrc", "sk_diag.hip"),
-           os.path.join(HERE, "csrc", "sk_actor.hip"),
+# csrc/sk_diag.hip (measurement-only kernels: the copy floor) is not part of
+# the product library: tools/build_variant.sh builds it into diagnostic
+# variants (tools/sweep.py --diag loads one through SK_LIB_PATH)
+SOURCES = [os.path.join(HERE, "csrc", "sk_engine.hip"), os.path.join(HERE, "csrc", "sk_actor.hip"),
            os.path.join(HERE, "csrc", "sk_critic.hip"), os.path.join(HERE, "csrc", "sk_update.hip"),
            os.path.join(HERE, "csrc", "sk_replay.hip"), os.path.join(HERE, "csrc", "sk_learn32.hip"),
            os.path.join(HERE, "csrc", "sk_host.cpp")]

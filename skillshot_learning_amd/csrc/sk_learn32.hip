@@ -31,6 +31,7 @@
 #include <stdlib.h>
 
 #include "../../include/skillshot.h"
+#include "sk_mlp.hpp"
 #include "sk_partial.hpp"
 #include "sk_step.hpp"
 
@@ -962,27 +963,12 @@ __device__ __forceinline__ f32x4 g16_l1w(const float* S, f4 w, int lane) {
 }
 
 // The replay minibatch gathered inside the critic's first launch
-// (sk_critic_grad_f32_sampled): batch row b is ring row floor(u_b size), u_b
-// from Philox4x32-10 keyed (seed; b, draw, total), exactly sk_replay_sample's
-// row, so the step equals sk_replay_sample + sk_critic_grad_f32.  Each
-// workgroup reads its own rows' states from the ring; the (slice 0, net 0)
-// workgroup of every row tile also writes its 16 rows into the sample
+// (sk_critic_grad_f32_sampled): skmlp::RingSample / ring_row (sk_mlp.hpp).
+// Each workgroup reads its own rows' states from the ring; the (slice 0, net
+// 0) workgroup of every row tile also writes its 16 rows into the sample
 // buffers, which the second launch and the actor step read.
-struct RingSample {
-  const float* ring;  // NULL: states from Sg / S2g
-  int64_t cap;
-  const int64_t* total;
-  uint64_t seed;
-  int draw;
-  float *s, *a, *r, *s2, *d;
-};
-__device__ __forceinline__ int64_t ring_row(const RingSample& q, int64_t b, int64_t t) {
-  const uint64_t size = (uint64_t)(t < q.cap ? t : q.cap);
-  const uint4 u = philox(make_uint4((uint32_t)b, (uint32_t)q.draw, (uint32_t)t, (uint32_t)(t >> 32)), (uint32_t)q.seed,
-                         (uint32_t)(q.seed >> 32));
-  const uint64_t u53 = (((uint64_t)u.x << 32) | u.y) >> 11;
-  return (int64_t)(((unsigned __int128)u53 * size) >> 53);
-}
+using skmlp::RingSample;
+using skmlp::ring_row;
 
 template <int MODE>
 __global__ void __launch_bounds__(kSlThreads) k_grad_slice_fwd(const float* __restrict__ f0, const float* __restrict__ f1,
@@ -1029,14 +1015,7 @@ __global__ void __launch_bounds__(kSlThreads) k_grad_slice_fwd(const float* __re
     if (ok && s == 0 && p == 0 && sk < 7) {  // the row into the sample buffers
       const f4 v = *(const f4*)(src + 4 * sk);
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int f = 4 * sk + c;
-        if (f < 12) rs.s[b * 12 + f] = v[c];
-        else if (f < 14) rs.a[b * 2 + f - 12] = v[c];
-        else if (f == 14) rs.r[b] = v[c];
-        else if (f < 27) rs.s2[b * 12 + f - 15] = v[c];
-        else rs.d[b] = v[c];
-      }
+      for (int c = 0; c < 4; ++c) skmlp::ring_scatter(rs, b, 4 * sk + c, v[c]);
     }
   } else {
     sv = sk < kIn && row0 + si < B ? Ssrc[(row0 + si) * kIn + sk] : 0.f;

@@ -171,4 +171,34 @@ __device__ __forceinline__ float noisy_pre(float m, float b, float v, float zs) 
   return __builtin_fmaf(__builtin_amdgcn_sqrtf(__builtin_fmaf(b, b, v)), zs, m + b);
 }
 
+// ---------------------------------------------------------------- replay minibatch
+// A minibatch drawn from the HBM replay ring inside a gradient launch
+// (sk_critic_grad_f32_sampled, sk_critic_grad_bootstrap_sampled): batch row b
+// is ring row floor(u_b size), u_b from Philox4x32-10 keyed (seed; b, draw,
+// total), exactly k_replay_sample's row (csrc/sk_replay.hip), so the step
+// equals sk_replay_sample + the step on the sampled rows, bit for bit.
+struct RingSample {
+  const float* ring;  // [cap][28]; NULL: no gather
+  int64_t cap;
+  const int64_t* total;
+  uint64_t seed;
+  int draw;
+  float *s, *a, *r, *s2, *d;  // the sample buffers
+};
+__device__ __forceinline__ int64_t ring_row(const RingSample& q, int64_t b, int64_t t) {
+  const uint64_t size = (uint64_t)(t < q.cap ? t : q.cap);
+  const uint4 u = philox<10>(make_uint4((uint32_t)b, (uint32_t)q.draw, (uint32_t)t, (uint32_t)(t >> 32)),
+                             (uint32_t)q.seed, (uint32_t)(q.seed >> 32));
+  const uint64_t u53 = (((uint64_t)u.x << 32) | u.y) >> 11;
+  return (int64_t)(((unsigned __int128)u53 * size) >> 53);
+}
+// float f (0..27) of a gathered ring row into the sample buffers
+__device__ __forceinline__ void ring_scatter(const RingSample& q, int64_t b, int f, float v) {
+  if (f < 12) q.s[b * 12 + f] = v;
+  else if (f < 14) q.a[b * 2 + f - 12] = v;
+  else if (f == 14) q.r[b] = v;
+  else if (f < 27) q.s2[b * 12 + f - 15] = v;
+  else q.d[b] = v;
+}
+
 }  // namespace skmlp

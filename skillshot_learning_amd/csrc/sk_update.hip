@@ -441,6 +441,10 @@ __device__ __forceinline__ void store_b1(float* P, int w, int lane, float gb1) {
   if (lane < 32) P[kPB1 + 32 * w + lane] = b;
 }
 
+__device__ __forceinline__ int64_t ring_row_of(const skmlp::RingSample& q, int64_t b, int64_t t) {
+  return skmlp::ring_row(q, b, t);
+}
+
 // ---------------------------------------------------------------- critic step
 // Critic.forward in train mode + F.mse_loss(q, y) backward
 // (DDPG.critic_step; critic.fit, SkillshotLearner.py:434): dL/dq =
@@ -466,7 +470,8 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad(const float* __restric
                                                           uint8_t* __restrict__ mask_out, const float* __restrict__ S2,
                                                           const float* __restrict__ R, const float* __restrict__ D,
                                                           float gamma, const char* __restrict__ tapack,
-                                                          const char* __restrict__ tcpack) {
+                                                          const char* __restrict__ tcpack,
+                                                          skmlp::RingSample rs = skmlp::RingSample{}) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const Lds L = carve(smem);
   SK_TP(0);
@@ -500,12 +505,37 @@ __global__ void __launch_bounds__(kThreads) k_critic_grad(const float* __restric
       f1t = load_l1(tp, w, lane);
     }
     // ---- phase 0: every global load of the sub-tile, the Dropout bits while they fly, then LDS
-    const float sv = load_state(S, row0, B, tid);
-    const float s2v = BOOT ? load_state(S2, row0, B, tid) : 0.f;
-    const float av = tid < 64 && row0 + (tid >> 1) < B ? A[row0 * 2 + tid] : 0.f;
+    float sv, s2v, av, rv, dv;
     const bool rok = tid < 32 && row0 + tid < B;
-    const float rv = rok ? (BOOT ? R[row0 + tid] : Y[row0 + tid]) : 0.f;
-    const float dv = BOOT && rok ? D[row0 + tid] : 0.f;
+    if (rs.ring) {  // the minibatch drawn from the replay ring here (sk_critic_grad_bootstrap_sampled)
+      const int64_t t = *rs.total;
+      const int64_t bs = row0 + (tid >> 4), ba = row0 + (tid >> 1), br = row0 + tid;
+      const int ks = tid & 15;
+      const bool oks = bs < B && t > 0 && ks < kIn, oka = tid < 64 && ba < B && t > 0, okr = rok && t > 0;
+      const float* rows = rs.ring;
+      const float* srow = rows + (oks ? ring_row_of(rs, bs, t) : 0) * 28;
+      sv = oks ? srow[ks] : 0.f;
+      s2v = BOOT && oks ? srow[15 + ks] : 0.f;
+      av = oka ? rows[ring_row_of(rs, ba, t) * 28 + 12 + (tid & 1)] : 0.f;
+      const float* rrow = rows + (okr ? ring_row_of(rs, br, t) : 0) * 28;
+      rv = okr ? rrow[14] : 0.f;
+      dv = BOOT && okr ? rrow[27] : 0.f;
+      if (tid < 32 * 7 && row0 + tid / 7 < B && t > 0) {  // the sub-tile's rows into the sample buffers
+        const int64_t b = row0 + tid / 7;
+        const int k = tid - (tid / 7) * 7;
+        const float4 v = *(const float4*)(rows + ring_row_of(rs, b, t) * 28 + 4 * k);
+        skmlp::ring_scatter(rs, b, 4 * k, v.x);
+        skmlp::ring_scatter(rs, b, 4 * k + 1, v.y);
+        skmlp::ring_scatter(rs, b, 4 * k + 2, v.z);
+        skmlp::ring_scatter(rs, b, 4 * k + 3, v.w);
+      }
+    } else {
+      sv = load_state(S, row0, B, tid);
+      s2v = BOOT ? load_state(S2, row0, B, tid) : 0.f;
+      av = tid < 64 && row0 + (tid >> 1) < B ? A[row0 * 2 + tid] : 0.f;
+      rv = rok ? (BOOT ? R[row0 + tid] : Y[row0 + tid]) : 0.f;
+      dv = BOOT && rok ? D[row0 + tid] : 0.f;
+    }
     f4v tla = {}, tlb = {};
     if (sub == 0) load_tails(tla, tlb, cp, ap, tp, BOOT ? 3 : 1, w, tid);
     uint32_t keep = dropout_bits(seed, call, key_row0 + row0, w, lane);
@@ -1127,7 +1157,39 @@ int sk_critic_grad_bootstrap(const void* cpack, const float* obs, const float* a
   kern<<<G, kThreads, kLdsGrad, (hipStream_t)stream>>>(
       obs, actions, targets, batch, row_offset, (int)spw, grad_scale, seed, call_counter, (const char*)cpack, partial,
       step_counters, n_steps, loss_sum, dropout_mask, next_obs, rewards, done, gamma,
-      (const char*)target_actor_gpack, (const char*)target_critic_gpack);
+      (const char*)target_actor_gpack, (const char*)target_critic_gpack, skmlp::RingSample{});
+  return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
+}
+
+int sk_critic_grad_bootstrap_sampled(const void* cpack, const sk_ring_sample* q, float gamma,
+                                     const void* target_actor_gpack, const void* target_critic_gpack, int64_t batch,
+                                     int64_t row_offset, float grad_scale, uint64_t seed,
+                                     const int64_t* call_counter, float* partial, float* step_counters,
+                                     int32_t n_steps, float* loss_sum, uint8_t* dropout_mask, void* stream) {
+  if (!q || !q->ring || !q->total || !q->s || !q->a || !q->r || !q->s2 || !q->d || q->capacity <= 0) return SK_EINVAL;
+  if ((((uintptr_t)q->ring) & 15) || (((uintptr_t)q->s) & 15) || (((uintptr_t)q->s2) & 15) || (((uintptr_t)q->a) & 7))
+    return SK_EINVAL;
+  const bool boot = target_actor_gpack != nullptr;
+  if (row_offset < 0 || (row_offset & 3)) return SK_EINVAL;
+  if (boot && !target_critic_gpack) return SK_EINVAL;
+  if (boot && ((((uintptr_t)target_actor_gpack) & 15) || (((uintptr_t)target_critic_gpack) & 15))) return SK_EINVAL;
+  if (!cpack || !call_counter || !partial || batch <= 0) return SK_EINVAL;
+  if ((n_steps > 0 && !step_counters) || n_steps < 0 || n_steps > 64) return SK_EINVAL;
+  if (((uintptr_t)cpack) & 15) return SK_EINVAL;
+  static bool attr = false;
+  if (!attr) {
+    set_lds(k_critic_grad<true>, kLdsGrad);
+    set_lds(k_critic_grad<false>, kLdsGrad);
+    attr = true;
+  }
+  const int64_t spw = subtiles_per_wg(batch);
+  const unsigned G = (unsigned)sk_update_partials(batch);
+  const skmlp::RingSample rs{q->ring, q->capacity, q->total, q->seed, q->draw, q->s, q->a, q->r, q->s2, q->d};
+  auto kern = boot ? k_critic_grad<true> : k_critic_grad<false>;
+  kern<<<G, kThreads, kLdsGrad, (hipStream_t)stream>>>(
+      q->s, q->a, q->r, batch, row_offset, (int)spw, grad_scale, seed, call_counter, (const char*)cpack, partial,
+      step_counters, n_steps, loss_sum, dropout_mask, q->s2, q->r, q->d, gamma, (const char*)target_actor_gpack,
+      (const char*)target_critic_gpack, rs);
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
 }
 

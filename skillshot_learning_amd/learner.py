@@ -592,11 +592,12 @@ class DDPG:
 
     def update_sampled(self, batch):
         """replay_update(batch, device_sampling=True) with the minibatch drawn
-        inside the critic step's first launch where the kernels do that (the
-        fp32 fused path, one rank or multi_rank "grad"): one launch fewer per
-        update, bit-identical (the same Philox rows as sample_dev)."""
+        inside the critic step's (first) launch where the kernels do that (the
+        fused path at either precision, one rank or multi_rank "grad"): one
+        launch fewer per update, bit-identical (the same Philox rows as
+        sample_dev)."""
         fu = self._fused
-        if fu is None or not fu.f32 or (self.multi() and self.multi_rank == "shared"):
+        if fu is None or (self.multi() and self.multi_rank == "shared"):
             return self.replay_update(batch, device_sampling=True)
         w, rk, b = self.world(), self.rank(), int(batch)
         if w > 1 and b % 4:
@@ -1085,7 +1086,7 @@ class TickGraph:
         else:
             a.copy_(L.model_act(obs).view(-1, ACTION_DIM))
         # SK_FUSED_REPLAY (A/B): 2 (default) the ring insert inside the step
-        # launch and the minibatch drawn inside the critic step's (fp32); 1 the
+        # launch and the minibatch drawn inside the critic step's; 1 the
         # insert and the first minibatch in one launch after the step; 0 the
         # insert and the sample as their own launches.  SK_FUSED_ACT=0 keeps
         # the actor forward as its own launch (fp32 actor, mode 2)

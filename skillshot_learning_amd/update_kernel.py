@@ -291,12 +291,10 @@ class FusedUpdate:
 
     @torch.no_grad()
     def critic_step_sampled(self, ring, batch, gamma=0.0, row_offset=0, global_batch=None):
-        """critic_step on a minibatch the launch draws from the replay ring
-        (fp32 only): equal to ring.sample_dev(batch) followed by critic_step
-        with the bootstrap target (gamma > 0) or y = r.  Returns (loss, (s, a,
-        r, s2, d)), the sample buffers."""
-        if not self.f32:
-            raise SkillshotError("critic_step_sampled is the fp32 path's")
+        """critic_step on a minibatch the launch draws from the replay ring:
+        equal to ring.sample_dev(batch) followed by critic_step with the
+        bootstrap target (gamma > 0) or y = r.  Returns (loss, (s, a, r, s2,
+        d)), the sample buffers."""
         B = int(batch)
         gb = B if global_batch is None else int(global_batch)
         out, draw = ring.next_draw(B)
@@ -305,12 +303,18 @@ class FusedUpdate:
         part = self._partial(B, self.fc.numel())
         st = self.sc
         boot = gamma > 0.0
-        ta = (self.ta if self.ta is not None else self.fa) if boot else None
-        tc = (self.tc if self.tc is not None else self.fc) if boot else None
-        _capi.check(self.L.sk_critic_grad_f32_sampled(
-            _p(self.fc), ctypes.byref(q), float(gamma), _p(ta), _p(tc), B, int(row_offset), 2.0 / gb, self.seed,
-            _p(self.calls), _p(part.main), _p(st.steps), st.steps.numel(), _p(self.stats[0:1]), None,
-            _p(part.scratch), self._stream()))
+        if self.f32:
+            ta = (self.ta if self.ta is not None else self.fa) if boot else None
+            tc = (self.tc if self.tc is not None else self.fc) if boot else None
+            _capi.check(self.L.sk_critic_grad_f32_sampled(
+                _p(self.fc), ctypes.byref(q), float(gamma), _p(ta), _p(tc), B, int(row_offset), 2.0 / gb, self.seed,
+                _p(self.calls), _p(part.main), _p(st.steps), st.steps.numel(), _p(self.stats[0:1]), None,
+                _p(part.scratch), self._stream()))
+        else:
+            _capi.check(self.L.sk_critic_grad_bootstrap_sampled(
+                _p(self.gpc), ctypes.byref(q), float(gamma), _p(self.gpta) if boot else None,
+                _p(self.gptc) if boot else None, B, int(row_offset), 2.0 / gb, self.seed, _p(self.calls),
+                _p(part.main), _p(st.steps), st.steps.numel(), _p(self.stats[0:1]), None, self._stream()))
         loss = self._loss_slot(0)
         self._adam(part, self.fc, st, self.tc, stat=self.stats[0:1], scale=1.0 / gb, out=loss, counter=self.calls,
                    packs=self._packs(critic=True))

@@ -149,17 +149,20 @@ def test_step_insert_equals_step_then_insert(learner, n, cap):
     assert envs[0].counters()["dones"] > 0
 
 
-@pytest.mark.parametrize("B,gamma", [(256, 0.9), (256, 0.0), (100, 0.9), (1000, 0.9)])
-def test_critic_step_sampled_equals_sample_then_step(learner, B, gamma):
-    """the fp32 critic step drawing its minibatch from the ring inside its
-    first launch (sk_critic_grad_f32_sampled) against sample_dev + the critic
-    step on those rows: identical sample buffers, losses and nets, bit for bit,
-    over several steps (1000 rows: the unsliced path, gather as its own launch);
-    the reported losses to 1e-5 (their per-workgroup sums arrive by atomics)"""
+@pytest.mark.parametrize("precision,B,gamma", [("fp32", 256, 0.9), ("fp32", 256, 0.0), ("fp32", 100, 0.9),
+                                                ("fp32", 1000, 0.9), ("bf16", 256, 0.9), ("bf16", 100, 0.0),
+                                                ("bf16", 1000, 0.9)])
+def test_critic_step_sampled_equals_sample_then_step(learner, precision, B, gamma):
+    """the critic step drawing its minibatch from the ring inside its (first)
+    launch (sk_critic_grad_f32_sampled, sk_critic_grad_bootstrap_sampled)
+    against sample_dev + the critic step on those rows: identical sample
+    buffers, losses and nets, bit for bit, over several steps (fp32 at 1000
+    rows: the unsliced path, gather as its own launch); the reported losses to
+    1e-5 (their per-workgroup sums arrive by atomics)"""
     out = []
     for sampled in (True, False):
         torch.manual_seed(0)
-        d = learner.DDPG("cuda", seed=2, gamma=gamma, tau=0.05, replay_capacity=3000, precision="fp32")
+        d = learner.DDPG("cuda", seed=2, gamma=gamma, tau=0.05, replay_capacity=3000, precision=precision)
         g = torch.Generator(device="cuda").manual_seed(9)
         for t in range(3):
             d.replay.add_dev(torch.rand(1000, 12, device="cuda", generator=g),

@@ -2,6 +2,8 @@
 
     python tools/sweep.py [--variants 0,1] [--envs 65536,262144,1048576] [--steps 2000]
 Prints one JSON line per (variant, N): us/step, env-steps/s, GB/s at 193 B/env-step.
+The 'empty' / 'copy' floor variants need a diagnostic build with csrc/sk_diag.hip:
+    tools/build_variant.sh ab/diag.so && SK_LIB_PATH=$PWD/ab/diag.so python tools/sweep.py ...
 """
 import argparse
 import ctypes
