@@ -315,31 +315,25 @@ def timed_multi(dev, n, seed, env_offset, tick_limit, k, warmup, ring, world, pe
     ap, dp = ctypes.c_void_p(acts.data_ptr()), ctypes.c_void_p(done.data_ptr())
     # the bound C entry point itself (sk_env_step_multi): no Python wrapper in
     # the timed region (tools/short_run_multi.py)
-    fn, h, lim, rp = env._L.sk_env_step_multi_timed, env._h, env.tick_limit, int(env.random_positions)
+    fn, h, lim, rp = env._L.sk_env_step_multi, env._h, env.tick_limit, int(env.random_positions)
     slab = 0
 
-    def run(m, ev0=None, ev1=None):
-        """m ticks in launches of at most per_launch; ev0 / ev1 (raw HIP
-        events) are recorded by the C call itself right before the first
-        launch and after the last (sk_env_step_multi_timed)"""
+    def run(m):
+        """m ticks in launches of at most per_launch"""
         nonlocal slab
-        first = True
         while m > 0:
             t = min(m, per_launch)
-            rc = fn(h, ap, ring, slab, t, dp, None, 0, lim, 1, rp, ev0 if first else None, ev1 if m == t else None,
-                    sp)
+            rc = fn(h, ap, ring, slab, t, dp, None, 0, lim, 1, rp, sp)
             if rc:
                 _capi_check(rc)
             if trace is not None:
                 trace.append(("slabs", slab, t))
             slab = (slab + t) % ring
             m -= t
-            first = False
 
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(st)  # torch creates the HIP events at their first record: not inside the timed region
     e1.record(st)
-    ev0, ev1 = ctypes.c_void_p(e0.cuda_event), ctypes.c_void_p(e1.cuda_event)
     run(1)  # the first launch loads the code object
     st.synchronize()
     env.clear_counters(stream=sp)
@@ -351,7 +345,9 @@ def timed_multi(dev, n, seed, env_offset, tick_limit, k, warmup, ring, world, pe
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    run(k, ev0, ev1)  # the events ride in the launch call: one host call in the region
+    e0.record(st)
+    run(k)
+    e1.record(st)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

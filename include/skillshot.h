@@ -255,16 +255,6 @@ int sk_env_step_multi(sk_env* env, const float* actions, int64_t ring_slabs, int
                       uint8_t* done, uint8_t* winner, int64_t out_stride, int32_t tick_limit, int32_t auto_reset,
                       int32_t random_positions, void* stream);
 
-/* sk_env_step_multi with HIP events (hipEvent_t, nullable) recorded on the
- * stream immediately before and after the launch, in the same call (ABI 7):
- * the bench's timed region then holds one host call, not three (the event
- * records from Python cost ~1-2 us of host time each).  GPU backend only
- * when an event is given. */
-int sk_env_step_multi_timed(sk_env* env, const float* actions, int64_t ring_slabs, int64_t slab0, int32_t n_ticks,
-                            uint8_t* done, uint8_t* winner, int64_t out_stride, int32_t tick_limit,
-                            int32_t auto_reset, int32_t random_positions, void* start_event, void* stop_event,
-                            void* stream);
-
 /* Random-policy actions (config 2 synthetic input): float[n_ticks][2][N][2]
  * uniform in [-1,1) from Philox4x32-10 keyed (seed, global env id, step
  * counter + t).  Does not advance the step counter. */

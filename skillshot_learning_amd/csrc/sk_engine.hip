@@ -1605,9 +1605,9 @@ int sk_env_act_step(sk_env* e, const float* actor_flat, const float* acting_obs,
   return SK_OK;
 }
 
-static int step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64_t slab0, int32_t n_ticks,
+int sk_env_step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64_t slab0, int32_t n_ticks,
                       uint8_t* done, uint8_t* winner, int64_t out_stride, int32_t tick_limit, int32_t auto_reset,
-                      int32_t random_positions, hipEvent_t ev_start, hipEvent_t ev_stop, void* stream) {
+                      int32_t random_positions, void* stream) {
   SK_CHECK_ENV(e);
   if (!actions) return fail(SK_EINVAL, "actions is NULL");
   if (((uintptr_t)actions) & 7) return fail(SK_EINVAL, "actions must be 8-byte aligned");
@@ -1674,7 +1674,6 @@ static int step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64
   const hipStream_t hs = (hipStream_t)stream;
   hipEvent_t e0 = nullptr, e1 = nullptr;  // launch_timed's events (A/B hook; unused by the ABI)
   hipError_t err;
-  if (ev_start && hipEventRecord(ev_start, hs) != hipSuccess) return fail(SK_EHIP, "hipEventRecord(start)");
   // the packed resident form in the lane-per-game kernel only (see
   // k_step_split_multi)
   const bool pk = a.pack != nullptr;
@@ -1706,25 +1705,8 @@ static int step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64
                      : launch_timed(k_step_multi<0, false>, g, dim3(kStepBlock), hs, e0, e1, a, e->dcfg, early);
   }
   if (err != hipSuccess) return fail(SK_EHIP, std::string("k_step_multi launch: ") + hipGetErrorString(err));
-  if (ev_stop && hipEventRecord(ev_stop, hs) != hipSuccess) return fail(SK_EHIP, "hipEventRecord(stop)");
   e->parity ^= 1;
   return SK_OK;
-}
-
-int sk_env_step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64_t slab0, int32_t n_ticks,
-                      uint8_t* done, uint8_t* winner, int64_t out_stride, int32_t tick_limit, int32_t auto_reset,
-                      int32_t random_positions, void* stream) {
-  return step_multi(e, actions, ring_slabs, slab0, n_ticks, done, winner, out_stride, tick_limit, auto_reset,
-                    random_positions, nullptr, nullptr, stream);
-}
-
-int sk_env_step_multi_timed(sk_env* e, const float* actions, int64_t ring_slabs, int64_t slab0, int32_t n_ticks,
-                            uint8_t* done, uint8_t* winner, int64_t out_stride, int32_t tick_limit,
-                            int32_t auto_reset, int32_t random_positions, void* start_event, void* stop_event,
-                            void* stream) {
-  if (e && e->host && (start_event || stop_event)) return fail(SK_EINVAL, "events need the GPU backend");
-  return step_multi(e, actions, ring_slabs, slab0, n_ticks, done, winner, out_stride, tick_limit, auto_reset,
-                    random_positions, (hipEvent_t)start_event, (hipEvent_t)stop_event, stream);
 }
 
 int sk_gen_random_actions(sk_env* e, float* actions, int32_t n_ticks, void* stream) {
