@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define SK_ABI_VERSION 7
+#define SK_ABI_VERSION 8
 
 enum {
   SK_OK = 0,
@@ -220,11 +220,14 @@ int sk_env_step(sk_env* env, const float* actions, float* obs, float* reward, in
  * obs and reward must be given (the ring holds them); acting_obs float[2N][12]
  * and ring float[capacity][28] 16-byte aligned, capacity >= 2N, arrivals
  * uint32[SK_REPLAY_ARRIVAL_WORDS] zeroed once (every launch leaves it zero).
+ * total_copy (ABI 8; NULL for none) receives the new *total as well, from
+ * the same launch: the count a concurrent update keys its minibatch on (the
+ * overlapped learner tick) without a copy launch.
  * The CPU backend (device -1) takes host pointers for all of them. */
 int sk_env_step_insert(sk_env* env, const float* actions, float* obs, float* reward, int32_t reward_kind,
                        uint8_t* done, uint8_t* winner, int32_t tick_limit, int32_t auto_reset,
                        int32_t random_positions, float* obs_reset, const float* acting_obs, float* ring,
-                       int64_t capacity, int64_t* total, uint32_t* arrivals, void* stream);
+                       int64_t capacity, int64_t* total, uint32_t* arrivals, int64_t* total_copy, void* stream);
 
 /* The self-play tick's act + step in ONE launch (ABI 7; SkillshotLearner.py
  * :304-314 act -> do_actions -> game_tick -> get_state): equal, bit for bit,
@@ -233,12 +236,13 @@ int sk_env_step_insert(sk_env* env, const float* actions, float* obs, float* rew
  * followed by sk_env_step_insert(env, actions, obs, ..., acting_obs, ring,
  * ...), or by sk_env_step when ring is NULL.  The observations never
  * leave the CU between the actor and the step; actions float[2N][2] is
- * still written.  N % 4 != 0 runs the two launches.  GPU backend only. */
+ * still written.  N % 4 != 0 runs the two launches.  total_copy as
+ * sk_env_step_insert's (ABI 8).  GPU backend only. */
 int sk_env_act_step(sk_env* env, const float* actor_flat, const float* acting_obs, float* actions, float noise_sd,
                     float action_sd, uint64_t noise_seed, uint64_t* call_counter, float* obs, float* reward,
                     int32_t reward_kind, uint8_t* done, uint8_t* winner, int32_t tick_limit, int32_t auto_reset,
                     int32_t random_positions, float* obs_reset, float* ring, int64_t capacity, int64_t* total,
-                    uint32_t* arrivals, void* stream);
+                    uint32_t* arrivals, int64_t* total_copy, void* stream);
 
 /* n_ticks learner ticks of the step-only contract in ONE launch (ABI 5):
  * equal, bit for bit, to n_ticks calls of sk_env_step(obs = reward =
@@ -534,6 +538,10 @@ typedef struct sk_ring_sample {
   float* r;               /* [batch] */
   float* s2;              /* [batch][12] */
   float* d;               /* [batch] */
+  int64_t exclude;        /* 0: rows floor(u min(*total, capacity)), sk_replay_sample's draw.
+                           * E > 0 (ABI 8; the learner tick whose update runs beside the next
+                           * insert): the min(*total, capacity - E) most recent rows as of
+                           * *total, none of the E rows that insert writes */
 } sk_ring_sample;
 int sk_critic_grad_f32_sampled(const float* critic_flat, const sk_ring_sample* sample, float gamma,
                                const float* target_actor_flat, const float* target_critic_flat, int64_t batch,

@@ -16,7 +16,7 @@ from . import build as _build
 
 SK_OK, SK_EINVAL, SK_EHIP, SK_ENOMEM, SK_ENODEV = 0, -1, -2, -3, -4
 SK_REWARD_LOOKING, SK_REWARD_SIMPLE = 0, 1
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 # every symbol include/skillshot.h declares
 EXPORTS = (
@@ -111,8 +111,8 @@ def load(build_if_missing=True):
         "sk_env_features": ([P, P, P], ctypes.c_int),
         "sk_env_observe": ([P, P, P, i32, P], ctypes.c_int),
         "sk_env_step": ([P, P, P, P, i32, P, P, i32, i32, i32, P, P], ctypes.c_int),
-        "sk_env_step_insert": ([P, P, P, P, i32, P, P, i32, i32, i32, P, P, P, i64, P, P, P], ctypes.c_int),
-        "sk_env_act_step": ([P, P, P, P, f32, f32, u64, P, P, P, i32, P, P, i32, i32, i32, P, P, i64, P, P, P],
+        "sk_env_step_insert": ([P, P, P, P, i32, P, P, i32, i32, i32, P, P, P, i64, P, P, P, P], ctypes.c_int),
+        "sk_env_act_step": ([P, P, P, P, f32, f32, u64, P, P, P, i32, P, P, i32, i32, i32, P, P, i64, P, P, P, P],
                             ctypes.c_int),
         "sk_env_step_multi": ([P, P, i64, i64, i32, P, P, i64, i32, i32, i32, P], ctypes.c_int),
         "sk_gen_random_actions": ([P, P, i32, P], ctypes.c_int),

@@ -1453,7 +1453,8 @@ int sk_env_observe(sk_env* e, float* obs, float* reward, int32_t kind, void* str
 static int step_launch(sk_env* e, const float* actions, float* obs, float* reward, int32_t reward_kind,
                        uint8_t* done, uint8_t* winner, int32_t tick_limit, int32_t auto_reset,
                        int32_t random_positions, float* obs_reset, const float* acting_obs, float* ring,
-                       int64_t capacity, int64_t* total, uint32_t* arrivals, void* stream) {
+                       int64_t capacity, int64_t* total, uint32_t* arrivals, int64_t* total_copy,
+                       void* stream) {
   SK_CHECK_ENV(e);
   if (!actions) return fail(SK_EINVAL, "actions is NULL");
   if (((uintptr_t)actions) & 7) return fail(SK_EINVAL, "actions must be 8-byte aligned");
@@ -1465,8 +1466,9 @@ static int step_launch(sk_env* e, const float* actions, float* obs, float* rewar
     if (!obs || !reward || !acting_obs || !total || !arrivals)
       return fail(SK_EINVAL, "ring insert needs obs, reward, acting_obs, total and arrivals");
     if (capacity <= 0 || 2 * (int64_t)e->n > capacity) return fail(SK_EINVAL, "ring capacity below 2 N rows");
-    if ((((uintptr_t)ring) & 15) || (((uintptr_t)acting_obs) & 15) || (((uintptr_t)total) & 7))
-      return fail(SK_EINVAL, "ring / acting_obs must be 16-byte aligned, total 8-byte");
+    if ((((uintptr_t)ring) & 15) || (((uintptr_t)acting_obs) & 15) || (((uintptr_t)total) & 7) ||
+        (((uintptr_t)total_copy) & 7))
+      return fail(SK_EINVAL, "ring / acting_obs must be 16-byte aligned, total / total_copy 8-byte");
   }
   if (e->host) {
     skh::step(*e->host, actions, obs, reward, reward_kind, done, winner, tick_limit, auto_reset, random_positions,
@@ -1483,6 +1485,7 @@ static int step_launch(sk_env* e, const float* actions, float* obs, float* rewar
         dst[27] = done ? (float)done[r % n] : 0.f;
       }
       *total = base + 2 * n;
+      if (total_copy) *total_copy = base + 2 * n;
     }
     return SK_OK;
   }
@@ -1508,6 +1511,7 @@ static int step_launch(sk_env* e, const float* actions, float* obs, float* rewar
   a.ring_cap = capacity;
   a.ring_total = total;
   a.ring_arrivals = arrivals;
+  a.ring_total_copy = ring ? total_copy : nullptr;
   // auto: k_step_fast once several waves share a SIMD (>= 2 per SIMD on 256
   // CUs) up to ~3 per SIMD (262,144 games: 8.3 vs 9.1 us); k_step from
   // 1 M games, where the step is HBM-bound (1 M: 30.1 vs 31.6 us, 4 M: 137
@@ -1537,23 +1541,24 @@ int sk_env_step(sk_env* e, const float* actions, float* obs, float* reward, int3
                 uint8_t* winner, int32_t tick_limit, int32_t auto_reset, int32_t random_positions,
                 float* obs_reset, void* stream) {
   return step_launch(e, actions, obs, reward, reward_kind, done, winner, tick_limit, auto_reset, random_positions,
-                     obs_reset, nullptr, nullptr, 0, nullptr, nullptr, stream);
+                     obs_reset, nullptr, nullptr, 0, nullptr, nullptr, nullptr, stream);
 }
 
 int sk_env_step_insert(sk_env* e, const float* actions, float* obs, float* reward, int32_t reward_kind,
                        uint8_t* done, uint8_t* winner, int32_t tick_limit, int32_t auto_reset,
                        int32_t random_positions, float* obs_reset, const float* acting_obs, float* ring,
-                       int64_t capacity, int64_t* total, uint32_t* arrivals, void* stream) {
+                       int64_t capacity, int64_t* total, uint32_t* arrivals, int64_t* total_copy,
+                       void* stream) {
   if (!ring) return fail(SK_EINVAL, "ring is NULL");
   return step_launch(e, actions, obs, reward, reward_kind, done, winner, tick_limit, auto_reset, random_positions,
-                     obs_reset, acting_obs, ring, capacity, total, arrivals, stream);
+                     obs_reset, acting_obs, ring, capacity, total, arrivals, total_copy, stream);
 }
 
 int sk_env_act_step(sk_env* e, const float* actor_flat, const float* acting_obs, float* actions, float noise_sd,
                     float action_sd, uint64_t noise_seed, uint64_t* call_counter, float* obs, float* reward,
                     int32_t reward_kind, uint8_t* done, uint8_t* winner, int32_t tick_limit, int32_t auto_reset,
                     int32_t random_positions, float* obs_reset, float* ring, int64_t capacity, int64_t* total,
-                    uint32_t* arrivals, void* stream) {
+                    uint32_t* arrivals, int64_t* total_copy, void* stream) {
   SK_CHECK_ENV(e);
   if (e->host) return fail(SK_EINVAL, "sk_env_act_step runs on the GPU backend");
   if (!actor_flat || !acting_obs || !actions) return fail(SK_EINVAL, "actor_flat / acting_obs / actions is NULL");
@@ -1564,7 +1569,7 @@ int sk_env_act_step(sk_env* e, const float* actor_flat, const float* acting_obs,
                                         noise_seed, call_counter, stream);
     if (rc != SK_OK) return fail(rc, "sk_actor_forward_f32 failed");
     return step_launch(e, actions, obs, reward, reward_kind, done, winner, tick_limit, auto_reset,
-                       random_positions, obs_reset, acting_obs, ring, capacity, total, arrivals, stream);
+                       random_positions, obs_reset, acting_obs, ring, capacity, total, arrivals, total_copy, stream);
   }
   if ((((uintptr_t)obs) & 15) || (((uintptr_t)obs_reset) & 15))
     return fail(SK_EINVAL, "obs buffers must be 16-byte aligned");
@@ -1573,8 +1578,8 @@ int sk_env_act_step(sk_env* e, const float* actor_flat, const float* acting_obs,
     if (!obs || !reward || !total || !arrivals)
       return fail(SK_EINVAL, "ring insert needs obs, reward, total and arrivals");
     if (capacity <= 0 || 2 * (int64_t)e->n > capacity) return fail(SK_EINVAL, "ring capacity below 2 N rows");
-    if ((((uintptr_t)ring) & 15) || (((uintptr_t)total) & 7))
-      return fail(SK_EINVAL, "ring must be 16-byte aligned, total 8-byte");
+    if ((((uintptr_t)ring) & 15) || (((uintptr_t)total) & 7) || (((uintptr_t)total_copy) & 7))
+      return fail(SK_EINVAL, "ring must be 16-byte aligned, total / total_copy 8-byte");
   }
   StepArgs a;
   a.v = e->view;
@@ -1598,6 +1603,7 @@ int sk_env_act_step(sk_env* e, const float* actor_flat, const float* acting_obs,
   a.ring_cap = capacity;
   a.ring_total = total;
   a.ring_arrivals = arrivals;
+  a.ring_total_copy = ring ? total_copy : nullptr;
   const int rc = sk_launch_act_step32(actor_flat, actions, noise_sd, action_sd, noise_seed, call_counter, a, e->dcfg,
                                       (hipStream_t)stream);
   if (rc != SK_OK) return fail(rc, "k_act_step32 launch failed");

@@ -1802,6 +1802,11 @@ int launch_sliced(const float* f0, const float* f1, const float* f2, const float
 
 }  // namespace
 
+// csrc/sk_replay.hip
+int replay_sample_excl(const float* ring, int64_t capacity, const int64_t* total, uint64_t seed, int32_t draw,
+                       int64_t batch, float* s, float* a, float* r, float* s2, float* d, int64_t excl,
+                       hipStream_t stream);
+
 // the self-play tick launch (sk_env_act_step, csrc/sk_engine.hip): a.n % 4 == 0
 int sk_launch_act_step32(const float* aflat, float* act_out, float sd, float action_sd, uint64_t seed,
                          uint64_t* call_ctr, const sk::StepArgs& a, const sk::Cfg& c, hipStream_t st) {
@@ -1892,7 +1897,7 @@ int sk_critic_grad_f32_sampled(const float* critic_flat, const sk_ring_sample* q
   int64_t w1_rows = 0;
   if (sk_update_scratch_f32(batch, &w1_rows) > 0) {
     if (!scratch) return SK_EINVAL;
-    const RingSample rs{q->ring, q->capacity, q->total, q->seed, q->draw, q->s, q->a, q->r, q->s2, q->d};
+    const RingSample rs{q->ring, q->capacity, q->total, q->seed, q->draw, q->s, q->a, q->r, q->s2, q->d, q->exclude};
     if (boot)
       return launch_sliced<kSlCriticBoot>(critic_flat, target_actor_flat, target_critic_flat, q->s, q->s2, q->a,
                                           nullptr, q->r, q->d, gamma, batch, row_offset, grad_scale, seed,
@@ -1903,8 +1908,8 @@ int sk_critic_grad_f32_sampled(const float* critic_flat, const sk_ring_sample* q
                                      step_counters, n_steps, loss_sum, dropout_mask, (hipStream_t)stream, rs);
   }
   // unsliced batches: the gather as its own launch
-  const int rc = sk_replay_sample(q->ring, q->capacity, q->total, q->seed, q->draw, batch, q->s, q->a, q->r, q->s2,
-                                  q->d, stream);
+  const int rc = replay_sample_excl(q->ring, q->capacity, q->total, q->seed, q->draw, batch, q->s, q->a, q->r, q->s2,
+                                    q->d, q->exclude, (hipStream_t)stream);
   if (rc != SK_OK) return rc;
   return sk_critic_grad_f32(critic_flat, q->s, q->a, boot ? nullptr : q->r, boot ? q->s2 : nullptr,
                             boot ? q->r : nullptr, boot ? q->d : nullptr, gamma, target_actor_flat,

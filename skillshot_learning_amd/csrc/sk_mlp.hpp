@@ -184,13 +184,23 @@ struct RingSample {
   uint64_t seed;
   int draw;
   float *s, *a, *r, *s2, *d;  // the sample buffers
+  int64_t excl;  // rows a concurrent insert writes (0: every min(total, cap) row)
 };
+// excl == 0: floor(u min(t, cap)), k_replay_sample's row.  excl = E > 0 (the
+// learner tick with the update beside the insert): the min(t, cap - E) most
+// recent rows as of count t, i.e. none of the E rows the insert running
+// beside it overwrites or adds, drawn with the same key.
 __device__ __forceinline__ int64_t ring_row(const RingSample& q, int64_t b, int64_t t) {
-  const uint64_t size = (uint64_t)(t < q.cap ? t : q.cap);
   const uint4 u = philox<10>(make_uint4((uint32_t)b, (uint32_t)q.draw, (uint32_t)t, (uint32_t)(t >> 32)),
                              (uint32_t)q.seed, (uint32_t)(q.seed >> 32));
   const uint64_t u53 = (((uint64_t)u.x << 32) | u.y) >> 11;
-  return (int64_t)(((unsigned __int128)u53 * size) >> 53);
+  if (q.excl <= 0) {
+    const uint64_t size = (uint64_t)(t < q.cap ? t : q.cap);
+    return (int64_t)(((unsigned __int128)u53 * size) >> 53);
+  }
+  const int64_t lim = q.cap - q.excl, el = t < lim ? t : lim;
+  const int64_t k = (int64_t)(((unsigned __int128)u53 * (uint64_t)el) >> 53);
+  return (t - el + k) % q.cap;
 }
 // float f (0..27) of a gathered ring row into the sample buffers
 __device__ __forceinline__ void ring_scatter(const RingSample& q, int64_t b, int f, float v) {

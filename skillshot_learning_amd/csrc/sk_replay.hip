@@ -70,16 +70,16 @@ __global__ void __launch_bounds__(kThreads) k_replay_sample(const float* __restr
                                                             const int64_t* __restrict__ total, uint64_t seed,
                                                             int draw, int64_t batch, float* __restrict__ s,
                                                             float* __restrict__ a, float* __restrict__ r,
-                                                            float* __restrict__ s2, float* __restrict__ d) {
+                                                            float* __restrict__ s2, float* __restrict__ d,
+                                                            int64_t excl) {
   const int64_t t = *total;
   const uint64_t size = (uint64_t)(t < cap ? t : cap);
   const int64_t b = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (b >= batch || size == 0) return;
-  const uint4 u = skmlp::philox(make_uint4((uint32_t)b, (uint32_t)draw, (uint32_t)t, (uint32_t)(t >> 32)),
-                                (uint32_t)seed, (uint32_t)(seed >> 32));
-  const uint64_t u53 = (((uint64_t)u.x << 32) | u.y) >> 11;     // uniform in [0, 2^53)
-  const uint64_t idx = (uint64_t)(((unsigned __int128)u53 * size) >> 53);  // floor(u * size)
-  const float4* src = (const float4*)(ring + (int64_t)idx * kW);
+  // floor(u * size), or with excl the rows skmlp::ring_row draws (sk_mlp.hpp)
+  const skmlp::RingSample q{ring, cap, total, seed, draw, s, a, r, s2, d, excl};
+  const int64_t idx = skmlp::ring_row(q, b, t);
+  const float4* src = (const float4*)(ring + idx * kW);
   float4 v[7];
 #pragma unroll
   for (int k = 0; k < 7; ++k) v[k] = src[k];
@@ -218,7 +218,7 @@ int sk_replay_sample(const float* ring, int64_t capacity, const int64_t* total, 
     return SK_EINVAL;
   const unsigned grid = (unsigned)((batch + kThreads - 1) / kThreads);
   k_replay_sample<<<grid, kThreads, 0, (hipStream_t)stream>>>(ring, capacity, total, seed, draw, batch, s, a, r, s2,
-                                                              d);
+                                                              d, 0);
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
 }
 
@@ -242,3 +242,15 @@ int sk_replay_insert_sample(float* ring, int64_t capacity, int64_t* total, uint3
 }
 
 }  // extern "C"
+
+// sk_replay_sample with the ring_row exclusion (sk_critic_grad_f32_sampled's
+// unsliced batches)
+int replay_sample_excl(const float* ring, int64_t capacity, const int64_t* total, uint64_t seed, int32_t draw,
+                       int64_t batch, float* s, float* a, float* r, float* s2, float* d, int64_t excl,
+                       hipStream_t stream) {
+  if (!ring || !total || !s || !a || !r || !s2 || !d || capacity <= 0 || batch <= 0 || excl < 0 || excl >= capacity)
+    return SK_EINVAL;
+  const unsigned grid = (unsigned)((batch + kThreads - 1) / kThreads);
+  k_replay_sample<<<grid, kThreads, 0, stream>>>(ring, capacity, total, seed, draw, batch, s, a, r, s2, d, excl);
+  return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
+}

@@ -178,14 +178,17 @@ struct StepArgs {
   int64_t ring_cap;
   int64_t* ring_total;
   uint32_t* ring_arrivals;  // SK_REPLAY_ARRIVAL_WORDS
+  int64_t* ring_total_copy; // NULL, or a second store of the new total
 };
 
 // The ring insert's end of launch (sk_replay.hip's grouped arrival): lane 0
 // of workgroup b arrives on group line arrivals[32 (1 + b % 8)], the last of
 // each group on arrivals[0]; the last workgroup (every other one has read
-// total) stores the new total.  Called by every lane 0 (lane 0 of a launched
+// total) stores the new total (and into total_copy when given: the
+// overlapped learner tick's count for the next update, no copy launch).  Called by every lane 0 (lane 0 of a launched
 // workgroup always steps a game).
-__device__ __forceinline__ void ring_arrive(uint32_t* arrivals, int64_t* total, int64_t new_total) {
+__device__ __forceinline__ void ring_arrive(uint32_t* arrivals, int64_t* total, int64_t new_total,
+                                            int64_t* total_copy = nullptr) {
   if (threadIdx.x != 0) return;
   const unsigned g = blockIdx.x & 7u;
   const unsigned members = (gridDim.x - g + 7u) / 8u;
@@ -195,6 +198,7 @@ __device__ __forceinline__ void ring_arrive(uint32_t* arrivals, int64_t* total, 
     const unsigned groups = gridDim.x < 8u ? gridDim.x : 8u;
     if (atomicAdd(arrivals, 1u) == groups - 1u) {
       *total = new_total;
+      if (total_copy) *total_copy = new_total;
       *arrivals = 0u;
     }
   }
@@ -345,7 +349,7 @@ __device__ __forceinline__ void split_finish(const StepArgs& a, const Cfg& c, co
       }
     }
   }
-  if (ins) ring_arrive(a.ring_arrivals, a.ring_total, rbase + 2 * a.n);
+  if (ins) ring_arrive(a.ring_arrivals, a.ring_total, rbase + 2 * a.n, a.ring_total_copy);
   if (in && p == 0) {
     if (a.done) a.done[i] = (uint8_t)d;
     if (a.winner) a.winner[i] = (uint8_t)winner;

@@ -1184,7 +1184,7 @@ int sk_critic_grad_bootstrap_sampled(const void* cpack, const sk_ring_sample* q,
   }
   const int64_t spw = subtiles_per_wg(batch);
   const unsigned G = (unsigned)sk_update_partials(batch);
-  const skmlp::RingSample rs{q->ring, q->capacity, q->total, q->seed, q->draw, q->s, q->a, q->r, q->s2, q->d};
+  const skmlp::RingSample rs{q->ring, q->capacity, q->total, q->seed, q->draw, q->s, q->a, q->r, q->s2, q->d, q->exclude};
   auto kern = boot ? k_critic_grad<true> : k_critic_grad<false>;
   kern<<<G, kThreads, kLdsGrad, (hipStream_t)stream>>>(
       q->s, q->a, q->r, batch, row_offset, (int)spw, grad_scale, seed, call_counter, (const char*)cpack, partial,

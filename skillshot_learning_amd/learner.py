@@ -246,6 +246,9 @@ class ReplayRing:
         self._arrivals = None
         self._draws = 0
         self._batches = {}
+        # the overlapped learner tick's sample counts: slot p holds the row
+        # count before the insert of a tick of parity p (TickGraph)
+        self.horizon = torch.zeros(2, dtype=torch.int64, device=device)
         if self.buf.is_cuda:
             from . import _capi
             self._k = _capi.load()
@@ -590,6 +593,18 @@ class DDPG:
         (hipGraph capture)."""
         return self.update_batch(*self.sample_local(batch, device_sampling))
 
+    def update_overlapped(self, batch, total, exclude, before_actor_adam):
+        """The overlapped tick's update (TickGraph, SK_TICK_OVERLAP): the
+        critic step and the actor gradient on a minibatch keyed on `total`
+        (the count before this tick's insert) that leaves out the `exclude`
+        rows the insert running beside it writes, then before_actor_adam()
+        (the join with the acting stream), then the actor's Adam launch."""
+        fu = self._fused
+        b = int(batch)
+        lc, (s, _, _, _, _) = fu.critic_step_sampled(self.replay, b, gamma=self.gamma, row_offset=0, global_batch=b,
+                                                     total=total, exclude=exclude)
+        return lc, fu.actor_step(s, before_adam=before_actor_adam)
+
     def update_sampled(self, batch):
         """replay_update(batch, device_sampling=True) with the minibatch drawn
         inside the critic step's (first) launch where the kernels do that (the
@@ -916,6 +931,10 @@ class SkillshotLearner:
         collective and replays graph segments with the collectives issued
         between them (any backend, e.g. gloo).  Default: "full" for nccl,
         "segmented" otherwise; SK_TICKGRAPH_MODE overrides.
+
+        One rank from TICK_OVERLAP_MIN_ENVS games (SK_TICK_OVERLAP): the acting
+        launches run beside the update on a second stream, and the update draws
+        from the rows inserted before the tick (TickGraph.overlap).
         """
         if self.device.type != "cuda":
             raise RuntimeError("tick_graph needs the GPU engine")
@@ -956,6 +975,9 @@ class SkillshotLearner:
             self.ddpg._tq.refresh()
 
 
+TICK_OVERLAP_MIN_ENVS = 16384  # TickGraph's auto overlap threshold (games per rank)
+
+
 class TickGraph:
     """Captured replay-rule ticks (see SkillshotLearner.tick_graph)."""
 
@@ -983,16 +1005,42 @@ class TickGraph:
                         winner=torch.empty(n, dtype=torch.uint8, device=dev), obs_reset=self._obs[1])
         self.stream = torch.cuda.Stream(device=dev)
         self.stream.wait_stream(torch.cuda.current_stream(dev))
+        # The overlapped tick (one rank): the acting launches (act + step +
+        # ring insert) run on a second stream beside the update, whose
+        # minibatch comes from the rows inserted before this tick
+        # (ReplayRing.horizon, the insert's rows excluded: the reference's
+        # replay draws after the tick's remember, SkillshotLearner.py:316-324,
+        # so this sees the ring one tick late); the two streams join before
+        # the actor's Adam launch, which rewrites the weights the acting
+        # launch reads (_tick_overlap).  SK_TICK_OVERLAP: auto (default) from
+        # TICK_OVERLAP_MIN_ENVS games, where the acting launches are long
+        # enough to hide the update (config 5 on one GPU: fp32 280 -> 259 us,
+        # bf16 130.6 -> 118 us; config 3 neutral, the graph's cross-queue
+        # edges cost what the overlap saves: profiles/r03ov_*); 1 / 0 force.
+        # (the ring must hold a batch beside the rows one insert overwrites)
+        ov = os.environ.get("SK_TICK_OVERLAP", "auto")
+        self.overlap = (not L.ddpg.multi() and L.ddpg._fused is not None and updates_per_tick == 1
+                        and L.replay.cap >= batch + 4 * n
+                        and os.environ.get("SK_FUSED_REPLAY", "2") == "2"
+                        and ov != "0" and (ov != "auto" or n >= TICK_OVERLAP_MIN_ENVS))
+        # (SK_TICK_OVERLAP=serial: the same tick on one stream, the check
+        # that the two streams share nothing they race on)
+        self.side = (torch.cuda.Stream(device=dev) if self.overlap and os.environ.get("SK_TICK_OVERLAP") != "serial"
+                     else None)
+        self._hp = 0  # host parity of the horizon slots
+        self._capturing = False
         with torch.cuda.stream(self.stream):
-            # fill the ring past one batch without updates, then warm the
-            # update path eagerly (allocator pools, autograd, Adam state)
-            while L.replay.size < batch:
+            # fill the ring past one batch plus one tick without updates (the
+            # overlapped update samples the rows before the tick's insert),
+            # then warm the update path eagerly (allocator pools, Adam state)
+            while L.replay.size < batch + (2 * n if self.overlap else 0):
                 self._tick(update=False)
             for _ in range(max(warmup, 1)):
                 self._tick(update=True)
             if self._cur:  # start the captured ticks from buffer 0
                 self._obs[0].copy_(self._obs[1])
                 self._cur = 0
+            self._hp = 0
         self.stream.synchronize()
         # capture at a synced step counter (both device slots current, host
         # parity 0): run() syncs before replaying, so eager steps between
@@ -1009,9 +1057,13 @@ class TickGraph:
             # against the capture, so RCCL's watchdog thread may keep
             # querying the events of eager collectives from the warm-up
             # (global mode aborted the process when it did, intermittently)
-            with torch.cuda.graph(self.graph, stream=self.stream, capture_error_mode="thread_local"):
-                for _ in range(self.ticks):
-                    self._tick(update=True)
+            self._capturing = True
+            try:
+                with torch.cuda.graph(self.graph, stream=self.stream, capture_error_mode="thread_local"):
+                    for _ in range(self.ticks):
+                        self._tick(update=True)
+            finally:
+                self._capturing = False
         self.stream.synchronize()
         L.replay.total = mirror
         self.replays = 0
@@ -1054,8 +1106,62 @@ class TickGraph:
         """the observation the next tick acts on"""
         return self._obs[self._cur]
 
+    def _act_insert(self, obs, total_copy=None):
+        """act -> do_actions -> game_tick -> get_state (SkillshotLearner.py
+        :304-314) and the ring insert: the fp32 actor inside the step launch
+        (sk_env_act_step: the observations stay on the CU), else the actor
+        launch then sk_env_step_insert"""
+        L = self.L
+        mode = L.exploration
+        if getattr(L.actor_kernel, "fused_act_step", False) and os.environ.get("SK_FUSED_ACT", "1") != "0":
+            L.game_environment.act_step(L.actor_kernel, obs,
+                                        noise_sd=L.param_noise_sd if mode == "param_noise" else 0.0,
+                                        action_sd=L.action_noise_sd if mode == "action_noise" else 0.0,
+                                        ring=L.replay, out=self.out, actions=self.act, total_copy=total_copy)
+            return
+        x, a = obs.view(-1, STATE_DIM), self.act.view(-1, ACTION_DIM)
+        if L.actor_kernel is not None and mode == "action_noise" and getattr(L.actor_kernel, "fused_action_noise",
+                                                                               False):
+            L.actor_kernel(x, out=a, action_sd=L.action_noise_sd)
+        elif L.actor_kernel is not None:
+            L.actor_kernel(x, noise_sd=L.param_noise_sd if mode == "param_noise" else 0.0, out=a)
+            if mode == "action_noise":
+                a.add_(L.action_noise_sd * torch.randn(a.shape, device=a.device, generator=L.gen))
+        else:
+            a.copy_(L.model_act(obs).view(-1, ACTION_DIM))
+        L.game_environment.step_insert(self.act, obs, L.replay, reward="looking", auto_reset=True, reset_obs=True,
+                                       out=self.out, total_copy=total_copy)
+
+    def _tick_overlap(self):
+        """one overlapped tick: the acting launches on the side stream, the
+        update on this one (see __init__).  The update of a tick of parity p
+        keys its minibatch on horizon[p], the row count before the tick's
+        insert; the insert's launch writes horizon[1 - p] (its total_copy).  Eager ticks
+        set horizon[p] first; a captured replay starts at parity 0 with
+        horizon[0] set by run().  Deterministic: the update reads no row and
+        no count that the acting launches write."""
+        L = self.L
+        ring = L.replay
+        main = torch.cuda.current_stream(L.device)
+        p = self._hp
+        if not self._capturing:
+            ring.horizon[p].copy_(ring.total_t)
+        obs = self._obs[self._cur]
+        self.out["obs_reset"] = self._obs[1 - self._cur]
+        side = self.side if self.side is not None else main
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            self._act_insert(obs, total_copy=ring.horizon[1 - p])
+        self._cur ^= 1
+        self._hp ^= 1
+        L.ddpg.update_overlapped(self.batch, ring.horizon[p], 2 * L.n_envs,
+                                 before_actor_adam=lambda: main.wait_stream(side))
+        L._refresh_actor_pack()
+
     def _tick(self, update):
         L = self.L
+        if update and self.overlap:
+            return self._tick_overlap()
         obs = self._obs[self._cur]
         self.out["obs_reset"] = self._obs[1 - self._cur]
         x = obs.view(-1, STATE_DIM)
@@ -1064,12 +1170,7 @@ class TickGraph:
         fused = os.environ.get("SK_FUSED_REPLAY", "2")
         if (fused == "2" and getattr(L.actor_kernel, "fused_act_step", False)
                 and os.environ.get("SK_FUSED_ACT", "1") != "0"):
-            # the actor forward inside the step launch (sk_env_act_step): the
-            # observations stay on the CU between act and step
-            L.game_environment.act_step(L.actor_kernel, obs,
-                                        noise_sd=L.param_noise_sd if mode == "param_noise" else 0.0,
-                                        action_sd=L.action_noise_sd if mode == "action_noise" else 0.0,
-                                        ring=L.replay, out=self.out, actions=self.act)
+            self._act_insert(obs)
             self._cur ^= 1
             if update:
                 for _ in range(self.updates):
@@ -1124,6 +1225,8 @@ class TickGraph:
         self.stream.wait_stream(cur)
         with torch.cuda.stream(self.stream):  # replay() launches on the current stream
             self.L.game_environment.sync_step_counter(ctypes.c_void_p(self.stream.cuda_stream))
+            if self.overlap:  # a replay starts at parity 0: its first update samples the current count
+                self.L.replay.horizon[0].copy_(self.L.replay.total_t)
             for _ in range(n):
                 if self._segments is None:
                     self.graph.replay()

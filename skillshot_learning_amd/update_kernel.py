@@ -34,7 +34,8 @@ class RingSample(ctypes.Structure):
     ring inside the critic step (sk_critic_grad_f32_sampled)."""
     _fields_ = [("ring", ctypes.c_void_p), ("capacity", ctypes.c_int64), ("total", ctypes.c_void_p),
                 ("seed", ctypes.c_uint64), ("draw", ctypes.c_int32), ("s", ctypes.c_void_p),
-                ("a", ctypes.c_void_p), ("r", ctypes.c_void_p), ("s2", ctypes.c_void_p), ("d", ctypes.c_void_p)]
+                ("a", ctypes.c_void_p), ("r", ctypes.c_void_p), ("s2", ctypes.c_void_p), ("d", ctypes.c_void_p),
+                ("exclude", ctypes.c_int64)]
 
 
 class PackTargets(ctypes.Structure):
@@ -290,16 +291,19 @@ class FusedUpdate:
         return loss
 
     @torch.no_grad()
-    def critic_step_sampled(self, ring, batch, gamma=0.0, row_offset=0, global_batch=None):
+    def critic_step_sampled(self, ring, batch, gamma=0.0, row_offset=0, global_batch=None, total=None, exclude=0):
         """critic_step on a minibatch the launch draws from the replay ring:
         equal to ring.sample_dev(batch) followed by critic_step with the
-        bootstrap target (gamma > 0) or y = r.  Returns (loss, (s, a, r, s2,
-        d)), the sample buffers."""
+        bootstrap target (gamma > 0) or y = r.  total: the device count the
+        draw is keyed on (default the ring's); exclude > 0 leaves out the
+        rows an insert running beside the step writes (sk_ring_sample).
+        Returns (loss, (s, a, r, s2, d)), the sample buffers."""
         B = int(batch)
         gb = B if global_batch is None else int(global_batch)
         out, draw = ring.next_draw(B)
-        q = RingSample(ring.buf.data_ptr(), ring.cap, ring.total_t.data_ptr(), ring.seed, draw,
-                       *[t.data_ptr() for t in out])
+        tp = (total if total is not None else ring.total_t).data_ptr()
+        q = RingSample(ring.buf.data_ptr(), ring.cap, tp, ring.seed, draw, *[t.data_ptr() for t in out],
+                       int(exclude))
         part = self._partial(B, self.fc.numel())
         st = self.sc
         boot = gamma > 0.0
@@ -347,15 +351,19 @@ class FusedUpdate:
                                      self._stream())
 
     @torch.no_grad()
-    def actor_step(self, s):
+    def actor_step(self, s, before_adam=None):
         """One actor Adam step on -sum_b Q(s_b, mu(s_b)) (critic at inference);
-        returns that loss (device scalar)."""
+        returns that loss (device scalar).  before_adam() runs between the
+        gradient and the Adam launch (the overlapped tick joins the acting
+        stream there: the Adam launch rewrites the weights the actor reads)."""
         s = s.float().contiguous()
         B = s.shape[0]
         part = self._partial(B, self.fa.numel())
         st = self.sa
         rc = self._actor_grad(s, part, st.steps, self.stats[1:])
         _capi.check(rc)
+        if before_adam is not None:
+            before_adam()
         loss = self._loss_slot(1)
         self._adam(part, self.fa, st, self.ta, stat=self.stats[1:], scale=-1.0, out=loss,
                    packs=self._packs(critic=False))

@@ -276,12 +276,14 @@ class VecSkillshotGame:
                                   _ptr(obs_r), self._stream()))
         return dict(obs=obs_t, reward=rew_t, done=done, winner=win, obs_reset=obs_r)
 
-    def step_insert(self, actions, acting_obs, ring, reward="looking", auto_reset=True, reset_obs=True, out=None):
+    def step_insert(self, actions, acting_obs, ring, reward="looking", auto_reset=True, reset_obs=True, out=None,
+                    total_copy=None):
         """`step` (obs and reward on) and the replay ring's insert of the tick's
         2N transitions (acting_obs[r], actions[r], reward[r], obs[r],
         done[r % N]) in ONE launch (sk_env_step_insert): equal, bit for bit,
         to step(...) followed by ring.add_dev(acting_obs, actions, reward,
-        obs, done).  ring: learner.ReplayRing on this env's device."""
+        obs, done).  ring: learner.ReplayRing on this env's device;
+        total_copy: an int64 element that receives the new row count too."""
         a = self._actions(actions)
         o = out or {}
         obs_t = o.get("obs") if o.get("obs") is not None else self.new_obs()
@@ -298,18 +300,20 @@ class VecSkillshotGame:
         check(self._L.sk_env_step_insert(self._h, _ptr(a), _ptr(obs_t), _ptr(rew_t), REWARD_KINDS[reward],
                                          _ptr(done), _ptr(win), self.tick_limit, int(bool(auto_reset)),
                                          int(self.random_positions), _ptr(obs_r), _ptr(s), _ptr(ring.buf), ring.cap,
-                                         _ptr(ring.total_t), _ptr(ring.arrivals()), self._stream()))
+                                         _ptr(ring.total_t), _ptr(ring.arrivals()), _ptr(total_copy),
+                                         self._stream()))
         ring.total += 2 * self.n  # host mirror (exact while the row count is fixed)
         return dict(obs=obs_t, reward=rew_t, done=done, winner=win, obs_reset=obs_r)
 
     def act_step(self, actor, acting_obs, noise_sd=0.0, action_sd=0.0, ring=None, reward="looking", auto_reset=True,
-                 reset_obs=True, out=None, actions=None):
+                 reset_obs=True, out=None, actions=None, total_copy=None):
         """The self-play tick's act + step (+ ring insert) in ONE launch
         (sk_env_act_step): `actor` (actor_kernel.ActorKernel32, the fp32
         actor) acts on acting_obs [2, N, 12] for both players of every game
         with parameter noise noise_sd and/or action noise action_sd, and the
         step runs on those actions; equal, bit for bit, to actor(...) with
-        32-row tiles followed by step_insert (ring given) or step.  Returns
+        32-row tiles followed by step_insert (ring given; total_copy as
+        step_insert's) or step.  Returns
         step's dict plus `actions` [2, N, 2]."""
         o = out or {}
         obs_t = o.get("obs") if o.get("obs") is not None else self.new_obs()
@@ -324,8 +328,8 @@ class VecSkillshotGame:
         s = acting_obs.float().contiguous()
         if s.numel() != 2 * self.n * 12 or act.numel() != 4 * self.n or not act.is_contiguous():
             raise ValueError("acting_obs must hold [2, N, 12] floats, actions [2, N, 2] (contiguous)")
-        ring_args = ((_ptr(ring.buf), ring.cap, _ptr(ring.total_t), _ptr(ring.arrivals())) if ring is not None
-                     else (None, 0, None, None))
+        ring_args = ((_ptr(ring.buf), ring.cap, _ptr(ring.total_t), _ptr(ring.arrivals()), _ptr(total_copy))
+                     if ring is not None else (None, 0, None, None, None))
         actor.calls += 1
         check(self._L.sk_env_act_step(self._h, _ptr(actor.flat), _ptr(s), _ptr(act), float(noise_sd),
                                       float(action_sd), actor.seed, _ptr(actor._ctr), _ptr(obs_t), _ptr(rew_t),

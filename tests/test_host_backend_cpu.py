@@ -174,7 +174,8 @@ def test_cuda_request_without_gpu_raises(ssa):
 def test_cpu_backend_step_insert_equals_step_then_add(ssa):
     """sk_env_step_insert on the CPU backend: the step's outputs and the ring
     rows of ReplayRing.add (torch path) after the same step, bit for bit,
-    through wrap-around and restarts"""
+    through wrap-around and restarts; total_copy (ABI 8) receives the new
+    row count"""
     from skillshot_learning_amd.learner import ReplayRing
     n, cap = 37, 200
     a = ssa.VecSkillshotGame(n, device="cpu", seed=5, tick_limit=30)
@@ -184,12 +185,14 @@ def test_cpu_backend_step_insert_equals_step_then_add(ssa):
     g = torch.Generator().manual_seed(2)
     for t in range(70):
         act = torch.rand((2, n, 2), generator=g) * 2.4 - 1.2
-        x = a.step_insert(act, oa, ra, reset_obs=True)
+        copy = torch.full((1,), -1, dtype=torch.int64)
+        x = a.step_insert(act, oa, ra, reset_obs=True, total_copy=copy if t % 2 else None)
         y = b.step(act, obs=True, reward="looking", auto_reset=True, reset_obs=True)
         rb.add(ob.reshape(-1, 12), act.reshape(-1, 2), y["reward"].reshape(-1), y["obs"].reshape(-1, 12), y["done"])
         for k in ("obs", "reward", "done", "winner", "obs_reset"):
             assert torch.equal(x[k], y[k]), (t, k)
         assert torch.equal(ra.buf, rb.buf), t
         assert int(ra.total_t) == int(rb.total_t) == ra.total == rb.total
+        assert int(copy) == (ra.total if t % 2 else -1)
         oa, ob = x["obs_reset"], y["obs_reset"]
     assert a.counters()["dones"] > 0

@@ -37,6 +37,9 @@ def nccl_group():
 
 def _run(mode, multi_rank, force, precision):
     from skillshot_learning_amd.learner import SkillshotLearner
+    # the plain 1-rank tick would otherwise overlap its acting launches with
+    # the update (a different minibatch schedule from the multi-rank ticks)
+    os.environ["SK_TICK_OVERLAP"] = "0"
     if mode:
         os.environ["SK_TICKGRAPH_MODE"] = mode
     else:
@@ -60,6 +63,7 @@ def _run(mode, multi_rank, force, precision):
         out[f"env.{k}"] = torch.as_tensor(v).clone()
     del tg, L
     os.environ.pop("SK_TICKGRAPH_MODE", None)
+    os.environ.pop("SK_TICK_OVERLAP", None)
     return got_mode, out
 
 

@@ -1,6 +1,8 @@
 """F1 on the GPU: the replay ring kernels (csrc/sk_replay.hip) and the fused
 bootstrap target (sk_target_y) against the torch path of learner.ReplayRing /
 DDPG.replay_update (exact: these are copies, gathers and one fp32 FMA)."""
+import ctypes
+
 import pytest
 import torch
 
@@ -200,6 +202,7 @@ def test_tick_graph_replay_modes_equal(learner, monkeypatch, precision, explorat
     (0): identical nets, ring and counters after the same ticks, bit for bit
     (32-row actor tiles everywhere: SK_FWD16=0)"""
     monkeypatch.setenv("SK_FWD16", "0")
+    monkeypatch.setenv("SK_TICK_OVERLAP", "0")  # the sequential tick (the overlapped one: test_tick_overlap_*)
     out = []
     for fused, act in (("2", "1"), ("2", "0"), ("1", "1"), ("0", "1")):
         monkeypatch.setenv("SK_FUSED_REPLAY", fused)
@@ -251,3 +254,55 @@ def test_act_step_equals_actor_then_step_insert(learner, monkeypatch, n, noise):
         obs = [o1["obs_reset"], o2["obs_reset"]]
     assert envs[0].counters() == envs[1].counters()
     assert envs[0].counters()["dones"] > 0
+
+
+@pytest.mark.parametrize("precision,exploration", [("fp32", "action_noise"), ("fp32", "param_noise"),
+                                                   ("bf16", "action_noise")])
+def test_tick_overlap_equals_serial(learner, monkeypatch, precision, exploration):
+    """the overlapped learner tick (acting launches on a second stream beside
+    the update, minibatch keyed on the count before the tick's insert, the
+    insert's rows excluded; joined before the actor's Adam launch): 20
+    graph-replayed ticks equal the same ticks captured on one stream
+    (SK_TICK_OVERLAP=serial) bit for bit -- nets, target nets, ring,
+    counters -- i.e. the two streams share no data they race on"""
+    out = []
+    for mode in ("1", "serial"):
+        monkeypatch.setenv("SK_TICK_OVERLAP", mode)
+        L = learner.SkillshotLearner(n_envs=256, device="cuda", seed=7, exploration=exploration, gamma=0.9,
+                                     tau=0.05, replay_capacity=4096, precision=precision, tick_limit=50)
+        tg = L.tick_graph(batch=128, ticks_per_graph=2, warmup=2)
+        assert tg.overlap and (tg.side is None) == (mode == "serial")
+        tg.run(10)
+        torch.cuda.synchronize()
+        out.append((torch.cat([p.detach().flatten() for p in L.model_actor.parameters()]),
+                    torch.cat([p.detach().flatten() for p in L.model_critic.parameters()]),
+                    torch.cat([p.detach().flatten() for p in L.ddpg.target_actor.parameters()]),
+                    L.replay.buf.clone(), int(L.replay.total_t), L.game_environment.counters(
+                        stream=ctypes.c_void_p(tg.stream.cuda_stream))))
+    (a1, c1, t1, b1, n1, k1), (a2, c2, t2, b2, n2, k2) = out
+    assert n1 == n2 and torch.equal(b1, b2)
+    assert torch.equal(a1, a2) and torch.equal(c1, c2) and torch.equal(t1, t2)
+    assert k1 == k2 and k1["dones"] > 0
+
+
+def test_overlap_sample_excludes_rows_being_written(learner):
+    """ring_row with exclude = E keys on the count before an insert and draws
+    only the min(count, capacity - E) most recent rows: never a row the E-row
+    insert after that count overwrites (a full ring wraps here)"""
+    from skillshot_learning_amd.update_kernel import RingSample  # noqa: F401 (the ABI struct)
+    cap, E, B = 1000, 300, 4096
+    d = learner.DDPG("cuda", seed=1, gamma=0.0, replay_capacity=cap, precision="fp32")
+    ring = d.replay
+    for t in range(9):  # 2,700 rows: wrapped twice
+        ids = torch.arange(E, device="cuda", dtype=torch.float32) + E * t
+        ring.add_dev(ids[:, None].expand(E, 12).contiguous(), torch.zeros(E, 2, device="cuda"),
+                     torch.zeros(E, device="cuda"), torch.zeros(E, 12, device="cuda"), torch.zeros(E, device="cuda"))
+    count = torch.tensor(int(ring.total_t), dtype=torch.int64, device="cuda")
+    d._fused.critic_step_sampled(ring, B, total=count, exclude=E)
+    s = ring._batch_bufs(B)[0]
+    torch.cuda.synchronize()
+    got = s[:, 0].long()
+    total = int(count)
+    lo = total - min(total, cap - E)  # the oldest row id still eligible
+    assert int(got.min()) >= lo and int(got.max()) < total
+    assert got.unique().numel() > 0.9 * (cap - E)  # uniform over the eligible rows
