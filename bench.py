@@ -452,7 +452,7 @@ def learner_rate(envs, world, rank, ticks, batch=256, exploration="param_noise",
     gpu_ms = e0.elapsed_time(e1) / n_ticks
     out = dict(envs_per_gpu=envs, total_envs=envs * world, n_gpus=world, ticks=n_ticks, batch_per_rank=batch,
                exploration=exploration, updates_per_tick=1, dtype=precision, multi_rank=tg.multi_rank_mode,
-               tick_overlap=bool(tg.overlap), env_steps_per_s=envs * world * n_ticks / el, ms_per_tick=el * 1e3 / n_ticks,
+               tick_mode=tg.mode, env_steps_per_s=envs * world * n_ticks / el, ms_per_tick=el * 1e3 / n_ticks,
                gpu_ms_per_tick=gpu_ms,
                episodes=L.game_environment.counters(stream=ctypes.c_void_p(tg.stream.cuda_stream)))
     try:

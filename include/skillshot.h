@@ -244,6 +244,24 @@ int sk_env_act_step(sk_env* env, const float* actor_flat, const float* acting_ob
                     int32_t random_positions, float* obs_reset, float* ring, int64_t capacity, int64_t* total,
                     uint32_t* arrivals, int64_t* total_copy, void* stream);
 
+/* sk_env_act_step prepared, not launched (ABI 8): the same arguments
+ * (N % 4 == 0, ring given or not) into *job, and the env advances its step
+ * slot as if the launch had been issued.  The job is then run, exactly once
+ * and before the env's next step, by sk_actor_grad_f32_step, whose actor
+ * backward launch carries it (the fused overlapped learner tick: the acting
+ * tick beside the actor step; the minibatch must already be drawn, excluding
+ * the rows this insert writes).  Opaque: copy it, do not edit it. */
+#define SK_STEP_JOB_WORDS 128
+typedef struct sk_step_job {
+  uint64_t opaque[SK_STEP_JOB_WORDS];
+} sk_step_job;
+int sk_env_act_step_job(sk_env* env, const float* actor_flat, const float* acting_obs, float* actions,
+                        float noise_sd, float action_sd, uint64_t noise_seed, uint64_t* call_counter, float* obs,
+                        float* reward, int32_t reward_kind, uint8_t* done, uint8_t* winner, int32_t tick_limit,
+                        int32_t auto_reset, int32_t random_positions, float* obs_reset, float* ring,
+                        int64_t capacity, int64_t* total, uint32_t* arrivals, int64_t* total_copy,
+                        sk_step_job* job);
+
 /* n_ticks learner ticks of the step-only contract in ONE launch (ABI 5):
  * equal, bit for bit, to n_ticks calls of sk_env_step(obs = reward =
  * obs_reset = NULL) where tick t acts on slab (slab0 + t) % ring_slabs of
@@ -561,6 +579,14 @@ int sk_critic_grad_bootstrap_sampled(const void* critic_gpack, const sk_ring_sam
 int sk_actor_grad_f32(const float* actor_flat, const float* critic_flat, const float* obs, int64_t batch,
                       float loss_scale, float* partials, float* step_counters, int32_t n_steps, float* q_sum,
                       float* scratch, void* stream);
+/* sk_actor_grad_f32 with a prepared acting tick (sk_env_act_step_job) run in
+ * its backward launch's spare workgroups (ABI 8; the sliced schedule; else the
+ * gradient launch then the acting launch).  Results equal, bit for bit,
+ * sk_actor_grad_f32 followed by the sk_env_act_step the job was prepared
+ * from. */
+int sk_actor_grad_f32_step(const float* actor_flat, const float* critic_flat, const float* obs, int64_t batch,
+                           float loss_scale, float* partials, float* step_counters, int32_t n_steps, float* q_sum,
+                           float* scratch, const sk_step_job* job, void* stream);
 
 #ifdef __cplusplus
 }

@@ -25,7 +25,7 @@ EXPORTS = (
     "sk_env_clear_counters", "sk_env_get_step_counter",
     "sk_env_set_step_counter", "sk_env_sync_step_counter", "sk_env_reset", "sk_player_move_direction", "sk_player_move_look",
     "sk_player_move_discrete", "sk_player_shoot", "sk_projectile_move", "sk_game_check_collision", "sk_game_tick", "sk_env_features", "sk_env_observe",
-    "sk_env_step", "sk_env_step_insert", "sk_env_act_step", "sk_env_step_multi", "sk_gen_random_actions", "sk_env_rollout_random",
+    "sk_env_step", "sk_env_step_insert", "sk_env_act_step", "sk_env_act_step_job", "sk_env_step_multi", "sk_gen_random_actions", "sk_env_rollout_random",
     "sk_actor_packed_bytes", "sk_actor_pack", "sk_actor_forward", "sk_actor_forward_dev",
     "sk_actor_forward_advance", "sk_actor_forward_noise",
     "sk_critic_packed_bytes", "sk_critic_pack", "sk_critic_forward", "sk_target_q",
@@ -34,7 +34,7 @@ EXPORTS = (
     "sk_target_y", "sk_replay_insert", "sk_replay_sample", "sk_replay_insert_sample", "sk_grad_pack_flat",
     "sk_critic_grad_bootstrap",
     "sk_update_partials_f32", "sk_actor_forward_f32", "sk_critic_grad_f32", "sk_critic_grad_f32_sampled",
-    "sk_critic_grad_bootstrap_sampled", "sk_actor_grad_f32",
+    "sk_critic_grad_bootstrap_sampled", "sk_actor_grad_f32", "sk_actor_grad_f32_step",
 )
 
 
@@ -56,6 +56,11 @@ class SkStateView(ctypes.Structure):
     _fields_ = [("n_envs", ctypes.c_int32), ("pos", ctypes.c_void_p), ("rot", ctypes.c_void_p),
                 ("qpos", ctypes.c_void_p), ("qrot", ctypes.c_void_p), ("qcdage", ctypes.c_void_p),
                 ("misc", ctypes.c_void_p)]
+
+
+class SkStepJob(ctypes.Structure):
+    """sk_step_job: one prepared acting launch (opaque)"""
+    _fields_ = [("opaque", ctypes.c_uint64 * 128)]
 
 
 class SkCounters(ctypes.Structure):
@@ -114,6 +119,8 @@ def load(build_if_missing=True):
         "sk_env_step_insert": ([P, P, P, P, i32, P, P, i32, i32, i32, P, P, P, i64, P, P, P, P], ctypes.c_int),
         "sk_env_act_step": ([P, P, P, P, f32, f32, u64, P, P, P, i32, P, P, i32, i32, i32, P, P, i64, P, P, P, P],
                             ctypes.c_int),
+        "sk_env_act_step_job": ([P, P, P, P, f32, f32, u64, P, P, P, i32, P, P, i32, i32, i32, P, P, i64, P, P, P,
+                                 ctypes.POINTER(SkStepJob)], ctypes.c_int),
         "sk_env_step_multi": ([P, P, i64, i64, i32, P, P, i64, i32, i32, i32, P], ctypes.c_int),
         "sk_gen_random_actions": ([P, P, i32, P], ctypes.c_int),
         "sk_env_rollout_random": ([P, i32, i32, P], ctypes.c_int),
@@ -153,6 +160,7 @@ def load(build_if_missing=True):
         "sk_critic_grad_bootstrap_sampled": ([P, P, f32, P, P, i64, i64, f32, u64, P, P, P, i32, P, P, P],
                                              ctypes.c_int),
         "sk_actor_grad_f32": ([P, P, P, i64, f32, P, P, i32, P, P, P], ctypes.c_int),
+        "sk_actor_grad_f32_step": ([P, P, P, i64, f32, P, P, i32, P, P, ctypes.POINTER(SkStepJob), P], ctypes.c_int),
         "sk_update_scratch_f32": ([i64, P], ctypes.c_int64),
         "sk_adam_flat_sliced": ([P, i32, P, i32, i32, P, P, i32, P, P, P, P, f32, f32, f32, f32, P, f32, P, f32, P, P,
                                  P, P], ctypes.c_int),

@@ -1512,6 +1512,7 @@ static int step_launch(sk_env* e, const float* actions, float* obs, float* rewar
   a.ring_total = total;
   a.ring_arrivals = arrivals;
   a.ring_total_copy = ring ? total_copy : nullptr;
+  a.grid_blocks = 0;
   // auto: k_step_fast once several waves share a SIMD (>= 2 per SIMD on 256
   // CUs) up to ~3 per SIMD (262,144 games: 8.3 vs 9.1 us); k_step from
   // 1 M games, where the step is HBM-bound (1 M: 30.1 vs 31.6 us, 4 M: 137
@@ -1554,23 +1555,11 @@ int sk_env_step_insert(sk_env* e, const float* actions, float* obs, float* rewar
                      obs_reset, acting_obs, ring, capacity, total, arrivals, total_copy, stream);
 }
 
-int sk_env_act_step(sk_env* e, const float* actor_flat, const float* acting_obs, float* actions, float noise_sd,
-                    float action_sd, uint64_t noise_seed, uint64_t* call_counter, float* obs, float* reward,
-                    int32_t reward_kind, uint8_t* done, uint8_t* winner, int32_t tick_limit, int32_t auto_reset,
-                    int32_t random_positions, float* obs_reset, float* ring, int64_t capacity, int64_t* total,
-                    uint32_t* arrivals, int64_t* total_copy, void* stream) {
-  SK_CHECK_ENV(e);
-  if (e->host) return fail(SK_EINVAL, "sk_env_act_step runs on the GPU backend");
-  if (!actor_flat || !acting_obs || !actions) return fail(SK_EINVAL, "actor_flat / acting_obs / actions is NULL");
-  if ((((uintptr_t)actions) & 7) || (((uintptr_t)acting_obs) & 15))
-    return fail(SK_EINVAL, "actions must be 8-byte aligned, acting_obs 16-byte");
-  if (e->n % 4) {  // the fused tile keys its noise by aligned 4-row groups: two launches
-    const int rc = sk_actor_forward_f32(actor_flat, acting_obs, actions, 2 * (int64_t)e->n, noise_sd, action_sd,
-                                        noise_seed, call_counter, stream);
-    if (rc != SK_OK) return fail(rc, "sk_actor_forward_f32 failed");
-    return step_launch(e, actions, obs, reward, reward_kind, done, winner, tick_limit, auto_reset,
-                       random_positions, obs_reset, acting_obs, ring, capacity, total, arrivals, total_copy, stream);
-  }
+// sk_env_act_step's checks and StepArgs (N % 4 == 0)
+static int act_step_args(sk_env* e, const float* acting_obs, const float* actions, float* obs, float* reward,
+                         int32_t reward_kind, uint8_t* done, uint8_t* winner, int32_t tick_limit, int32_t auto_reset,
+                         int32_t random_positions, float* obs_reset, float* ring, int64_t capacity, int64_t* total,
+                         uint32_t* arrivals, int64_t* total_copy, StepArgs& a) {
   if ((((uintptr_t)obs) & 15) || (((uintptr_t)obs_reset) & 15))
     return fail(SK_EINVAL, "obs buffers must be 16-byte aligned");
   if (reward_kind != SK_REWARD_LOOKING && reward_kind != SK_REWARD_SIMPLE) return fail(SK_EINVAL, "bad reward_kind");
@@ -1581,7 +1570,6 @@ int sk_env_act_step(sk_env* e, const float* actor_flat, const float* acting_obs,
     if ((((uintptr_t)ring) & 15) || (((uintptr_t)total) & 7) || (((uintptr_t)total_copy) & 7))
       return fail(SK_EINVAL, "ring must be 16-byte aligned, total / total_copy 8-byte");
   }
-  StepArgs a;
   a.v = e->view;
   a.n = e->n;
   a.actions = reinterpret_cast<const float2*>(actions);
@@ -1604,9 +1592,70 @@ int sk_env_act_step(sk_env* e, const float* actor_flat, const float* acting_obs,
   a.ring_total = total;
   a.ring_arrivals = arrivals;
   a.ring_total_copy = ring ? total_copy : nullptr;
-  const int rc = sk_launch_act_step32(actor_flat, actions, noise_sd, action_sd, noise_seed, call_counter, a, e->dcfg,
-                                      (hipStream_t)stream);
+  a.grid_blocks = 0;
+  return SK_OK;
+}
+
+static int act_step_common(sk_env* e, const float* actor_flat, const float* acting_obs, const float* actions) {
+  SK_CHECK_ENV(e);
+  if (e->host) return fail(SK_EINVAL, "sk_env_act_step runs on the GPU backend");
+  if (!actor_flat || !acting_obs || !actions) return fail(SK_EINVAL, "actor_flat / acting_obs / actions is NULL");
+  if ((((uintptr_t)actions) & 7) || (((uintptr_t)acting_obs) & 15))
+    return fail(SK_EINVAL, "actions must be 8-byte aligned, acting_obs 16-byte");
+  return SK_OK;
+}
+
+int sk_env_act_step(sk_env* e, const float* actor_flat, const float* acting_obs, float* actions, float noise_sd,
+                    float action_sd, uint64_t noise_seed, uint64_t* call_counter, float* obs, float* reward,
+                    int32_t reward_kind, uint8_t* done, uint8_t* winner, int32_t tick_limit, int32_t auto_reset,
+                    int32_t random_positions, float* obs_reset, float* ring, int64_t capacity, int64_t* total,
+                    uint32_t* arrivals, int64_t* total_copy, void* stream) {
+  int rc = act_step_common(e, actor_flat, acting_obs, actions);
+  if (rc != SK_OK) return rc;
+  if (e->n % 4) {  // the fused tile keys its noise by aligned 4-row groups: two launches
+    rc = sk_actor_forward_f32(actor_flat, acting_obs, actions, 2 * (int64_t)e->n, noise_sd, action_sd, noise_seed,
+                              call_counter, stream);
+    if (rc != SK_OK) return fail(rc, "sk_actor_forward_f32 failed");
+    return step_launch(e, actions, obs, reward, reward_kind, done, winner, tick_limit, auto_reset,
+                       random_positions, obs_reset, acting_obs, ring, capacity, total, arrivals, total_copy, stream);
+  }
+  StepArgs a;
+  rc = act_step_args(e, acting_obs, actions, obs, reward, reward_kind, done, winner, tick_limit, auto_reset,
+                     random_positions, obs_reset, ring, capacity, total, arrivals, total_copy, a);
+  if (rc != SK_OK) return rc;
+  rc = sk_launch_act_step32(actor_flat, actions, noise_sd, action_sd, noise_seed, call_counter, a, e->dcfg,
+                            (hipStream_t)stream);
   if (rc != SK_OK) return fail(rc, "k_act_step32 launch failed");
+  e->parity ^= 1;
+  return SK_OK;
+}
+
+static_assert(sizeof(ActStepJob) <= sizeof(sk_step_job), "sk_step_job too small for ActStepJob");
+
+int sk_env_act_step_job(sk_env* e, const float* actor_flat, const float* acting_obs, float* actions, float noise_sd,
+                        float action_sd, uint64_t noise_seed, uint64_t* call_counter, float* obs, float* reward,
+                        int32_t reward_kind, uint8_t* done, uint8_t* winner, int32_t tick_limit, int32_t auto_reset,
+                        int32_t random_positions, float* obs_reset, float* ring, int64_t capacity, int64_t* total,
+                        uint32_t* arrivals, int64_t* total_copy, sk_step_job* job) {
+  int rc = act_step_common(e, actor_flat, acting_obs, actions);
+  if (rc != SK_OK) return rc;
+  if (!job) return fail(SK_EINVAL, "job is NULL");
+  if (e->n % 4) return fail(SK_EINVAL, "a prepared act_step needs N % 4 == 0 (use sk_env_act_step)");
+  ActStepJob j;
+  std::memset(&j, 0, sizeof(j));
+  rc = act_step_args(e, acting_obs, actions, obs, reward, reward_kind, done, winner, tick_limit, auto_reset,
+                     random_positions, obs_reset, ring, capacity, total, arrivals, total_copy, j.a);
+  if (rc != SK_OK) return rc;
+  j.magic = kActStepJobMagic;
+  j.c = e->dcfg;
+  j.aflat = actor_flat;
+  j.act_out = actions;
+  j.sd = noise_sd;
+  j.action_sd = action_sd;
+  j.seed = noise_seed;
+  j.call_ctr = call_counter;
+  std::memset(job, 0, sizeof(*job));
+  std::memcpy(job, &j, sizeof(j));
   e->parity ^= 1;
   return SK_OK;
 }

@@ -30,6 +30,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <cstring>
+
 #include "../../include/skillshot.h"
 #include "sk_mlp.hpp"
 #include "sk_partial.hpp"
@@ -1073,18 +1075,24 @@ __device__ __forceinline__ float rowall16(float v) {
 }
 
 
+// The backward launch's workgroup `bid` (row tile bid / kSlices, slice
+// bid % kSlices) on the LDS at smem_sl (sl_bwd_lds(MODE) bytes): the body of
+// k_grad_slice_bwd, and of k_actor_bwd_act_step32's backward workgroups.
+#define SK_SLICE_BWD_PARAMS                                                                                      \
+  const float *__restrict__ f0, const float *__restrict__ f1, const float *__restrict__ f2,                       \
+      const float *__restrict__ Sg, const float *__restrict__ Ag, const float *__restrict__ Yg,                  \
+      const float *__restrict__ Rg, const float *__restrict__ Dg, float gamma, int64_t B, int64_t key_row0,      \
+      float scale, uint64_t seed, const int64_t *__restrict__ call_ctr, const float *__restrict__ Z,             \
+      float *__restrict__ partial, float *__restrict__ partial_w1, float *__restrict__ stat_out,                 \
+      uint8_t *__restrict__ mask_out
+#define SK_SLICE_BWD_ARGS \
+  f0, f1, f2, Sg, Ag, Yg, Rg, Dg, gamma, B, key_row0, scale, seed, call_ctr, Z, partial, partial_w1, stat_out, mask_out
+
 template <int MODE>
-__global__ void __launch_bounds__(kSlThreads) k_grad_slice_bwd(
-    const float* __restrict__ f0, const float* __restrict__ f1, const float* __restrict__ f2,
-    const float* __restrict__ Sg, const float* __restrict__ Ag, const float* __restrict__ Yg,
-    const float* __restrict__ Rg, const float* __restrict__ Dg, float gamma, int64_t B, int64_t key_row0,
-    float scale, uint64_t seed, const int64_t* __restrict__ call_ctr, const float* __restrict__ Z,
-    float* __restrict__ partial, float* __restrict__ partial_w1, float* __restrict__ stat_out,
-    uint8_t* __restrict__ mask_out) {
+__device__ __forceinline__ void grad_slice_bwd(int bid, float* smem_sl, SK_SLICE_BWD_PARAMS) {
   constexpr int NP = sl_planes(MODE);
   constexpr bool CRIT = MODE != kSlActor;
   constexpr int LD0 = sl_ld(MODE, 0), NPAR = CRIT ? kCP : kAP;
-  extern __shared__ __attribute__((aligned(16))) float smem_sl[];
   float* sS = smem_sl;                  // [16][20]
   float* sST = sS + kR * kLdS16;        // [16 features][16 rows (+4)]
   float* sZ = sST + kR * kLdS16;        // [NP][16][132]
@@ -1100,7 +1108,7 @@ __global__ void __launch_bounds__(kSlThreads) k_grad_slice_bwd(
   float* sST8 = sDQ + 2 * kR;           // [16] per-row e^2 (critic) or Q (actor)
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int tid = threadIdx.x, lane = tid & 63, i = lane & 15, g = lane >> 4;
-  const int rt = blockIdx.x / kSlices, s = blockIdx.x - rt * kSlices;
+  const int rt = bid / kSlices, s = bid - rt * kSlices;
   const int64_t row0 = (int64_t)rt * kR;
   const float* fl[3] = {f0, f1, f2};
   const gfp W2 = (gfp)f0 + kPW2;
@@ -1291,7 +1299,7 @@ __global__ void __launch_bounds__(kSlThreads) k_grad_slice_bwd(
   lds_sync32();
   // ---- phase 3: the slice's per-unit gradients; dW2 rows; dz1 share -> dW1, db1
   float* P = partial + (int64_t)rt * NPAR;
-  float* PW = partial_w1 + (int64_t)blockIdx.x * kW1Part;
+  float* PW = partial_w1 + (int64_t)bid * kW1Part;
   if (tid < kSliceU) {
     const int j = tid, u = kSliceU * s + j;
     const f4 v = (*(const f4*)(sH2T + j * 4) + *(const f4*)(sH2T + (kSliceU + j) * 4)) +
@@ -1355,19 +1363,26 @@ __global__ void __launch_bounds__(kSlThreads) k_grad_slice_bwd(
   }
 }
 
+template <int MODE>
+__global__ void __launch_bounds__(kSlThreads) k_grad_slice_bwd(SK_SLICE_BWD_PARAMS) {
+  extern __shared__ __attribute__((aligned(16))) float smem_sl[];
+  grad_slice_bwd<MODE>(blockIdx.x, smem_sl, SK_SLICE_BWD_ARGS);
+}
+
 // ---------------------------------------------------------------- actor forward
 // the last workgroup to arrive stores the call number the launch drew with.
 // Grouped arrival (as the bf16 actor's advance_call, csrc/sk_actor.hip):
 // workgroup b on group line call_ctr[2 + 16 (b % 8)], the last of each group
-// on call_ctr[1] (SK_ACTOR_COUNTER_WORDS)
-__device__ __forceinline__ void advance_call32(uint64_t* call_ctr, uint64_t call) {
+// on call_ctr[1] (SK_ACTOR_COUNTER_WORDS); nb = the launch's workgroups that
+// arrive (the first nb of the grid)
+__device__ __forceinline__ void advance_call32(uint64_t* call_ctr, uint64_t call, unsigned nb) {
   if (threadIdx.x == 0) {
     const unsigned g = blockIdx.x & 7u;
-    const unsigned long long members = (gridDim.x - g + 7u) / 8u;
+    const unsigned long long members = (nb - g + 7u) / 8u;
     unsigned long long* gc = (unsigned long long*)&call_ctr[2 + 16 * g];
     if (atomicAdd(gc, 1ull) == members - 1) {
       *gc = 0;
-      const unsigned long long groups = gridDim.x < 8u ? gridDim.x : 8u;
+      const unsigned long long groups = nb < 8u ? nb : 8u;
       if (atomicAdd((unsigned long long*)&call_ctr[1], 1ull) == groups - 1) {
         call_ctr[0] = call;
         call_ctr[1] = 0;
@@ -1573,7 +1588,7 @@ __global__ void __launch_bounds__(kFwdThreads) k_actor_fwd32(const float* __rest
                       nullptr);
   if (draws) {  // the last workgroup to finish stores the call number it drew with
     __syncthreads();
-    advance_call32(call_ctr, call);
+    advance_call32(call_ctr, call, gridDim.x);
   }
 }
 
@@ -1587,15 +1602,15 @@ __global__ void __launch_bounds__(kFwdThreads) k_actor_fwd32(const float* __rest
 // finishes k_step_split's tick for its lanes.  Equal, bit for bit, to
 // sk_actor_forward_f32 (32-row tiles) followed by sk_env_step(_insert).
 // Wave 0 counts its games into counter slot line b.
+// act_step32: the body on LDS S / H1 / H2 / sAct for the first nb workgroups
+// of the grid (k_act_step32: all of them; k_actor_bwd_act_step32: the
+// workgroups before the backward's)
+constexpr size_t kActStepLds = (size_t)32 * (kLdS + kLdH1 + kLdH2) * 4 + 32 * sizeof(float2);
 template <bool NOISE>
-__global__ void __launch_bounds__(kFwdThreads) k_act_step32(const float* __restrict__ aflat, float* __restrict__ act_out,
-                                                            float sd, float action_sd, uint64_t seed,
-                                                            uint64_t* __restrict__ call_ctr, sk::StepArgs a,
-                                                            sk::Cfg c) {
-  __shared__ __attribute__((aligned(16))) float S[32 * kLdS];
-  __shared__ __attribute__((aligned(16))) float H1[32 * kLdH1];
-  __shared__ __attribute__((aligned(16))) float H2[32 * kLdH2];
-  __shared__ float2 sAct[32];
+__device__ __forceinline__ void act_step32(const float* __restrict__ aflat, float* __restrict__ act_out, float sd,
+                                           float action_sd, uint64_t seed, uint64_t* __restrict__ call_ctr,
+                                           sk::StepArgs a, sk::Cfg c, float* S, float* H1, float* H2,
+                                           float2* sAct, unsigned nb) {
   const int lane = threadIdx.x & 63;
   const bool w0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0;
   const int64_t g0 = (int64_t)blockIdx.x * 16;
@@ -1618,7 +1633,51 @@ __global__ void __launch_bounds__(kFwdThreads) k_act_step32(const float* __restr
   TP32(7);
   if (draws) {
     __syncthreads();
-    advance_call32(call_ctr, call);
+    advance_call32(call_ctr, call, nb);
+  }
+}
+
+template <bool NOISE>
+__global__ void __launch_bounds__(kFwdThreads) k_act_step32(const float* __restrict__ aflat, float* __restrict__ act_out,
+                                                            float sd, float action_sd, uint64_t seed,
+                                                            uint64_t* __restrict__ call_ctr, sk::StepArgs a,
+                                                            sk::Cfg c) {
+  extern __shared__ __attribute__((aligned(16))) float smem_sl[];
+  float* S = smem_sl;
+  float* H1 = S + 32 * kLdS;
+  float* H2 = H1 + 32 * kLdH1;
+  act_step32<NOISE>(aflat, act_out, sd, action_sd, seed, call_ctr, a, c, S, H1, H2, (float2*)(H2 + 32 * kLdH2),
+                    gridDim.x);
+}
+
+// The actor step's backward launch with the next acting tick beside it (the
+// fused overlapped learner tick, sk_actor_grad_f32_step): workgroups
+// [0, GA) run act_step32 (k_act_step32's 16 games each), the rest
+// grad_slice_bwd<kSlActor> (k_grad_slice_bwd's workgroup blockIdx - GA).  The
+// two share no data: the backward reads the minibatch, the nets and the
+// forward's z2; the acting half reads the actor and the observations and
+// writes the env, the actions and the ring (the minibatch was gathered
+// before, excluding the rows this insert writes).  LDS is the larger of the
+// two layouts (two workgroups per CU).
+constexpr size_t kBwdActLds =
+    kActStepLds > sl_bwd_lds(kSlActor) ? kActStepLds : sl_bwd_lds(kSlActor);
+static_assert(kSlThreads == kFwdThreads, "one workgroup size for both halves");
+template <bool NOISE>
+__global__ void __launch_bounds__(kFwdThreads) k_actor_bwd_act_step32(SK_SLICE_BWD_PARAMS, unsigned GA,
+                                                                      const float* __restrict__ aflat,
+                                                                      float* __restrict__ act_out, float sd,
+                                                                      float action_sd, uint64_t aseed,
+                                                                      uint64_t* __restrict__ acall_ctr,
+                                                                      sk::StepArgs a, sk::Cfg c) {
+  extern __shared__ __attribute__((aligned(16))) float smem_sl[];
+  if (blockIdx.x < GA) {
+    float* S = smem_sl;
+    float* H1 = S + 32 * kLdS;
+    float* H2 = H1 + 32 * kLdH1;
+    act_step32<NOISE>(aflat, act_out, sd, action_sd, aseed, acall_ctr, a, c, S, H1, H2, (float2*)(H2 + 32 * kLdH2),
+                      GA);
+  } else {
+    grad_slice_bwd<kSlActor>((int)(blockIdx.x - GA), smem_sl, SK_SLICE_BWD_ARGS);
   }
 }
 
@@ -1747,7 +1806,7 @@ __global__ void __launch_bounds__(kFwdThreads) k_actor_fwd16(const float* __rest
   }
   if (draws) {
     __syncthreads();
-    advance_call32(call_ctr, call);
+    advance_call32(call_ctr, call, gridDim.x);
   }
 }
 
@@ -1783,17 +1842,37 @@ int launch_sliced(const float* f0, const float* f1, const float* f2, const float
                   const float* A, const float* Y, const float* R, const float* D, float gamma, int64_t B,
                   int64_t key_row0, float scale, uint64_t seed, const int64_t* call_ctr, float* partials,
                   float* scratch, int64_t w1_rows, float* step_ctr, int n_steps, float* stat_out, uint8_t* mask_out,
-                  hipStream_t st, RingSample rs = RingSample{}) {
+                  hipStream_t st, RingSample rs = RingSample{}, const sk::ActStepJob* job = nullptr) {
   static bool attr = false;
   if (!attr) {
     set_lds32(k_grad_slice_fwd<MODE>, sl_fwd_lds(MODE));
     set_lds32(k_grad_slice_bwd<MODE>, sl_bwd_lds(MODE));
+    if constexpr (MODE == kSlActor) {
+      set_lds32(k_actor_bwd_act_step32<true>, kBwdActLds);
+      set_lds32(k_actor_bwd_act_step32<false>, kBwdActLds);
+    }
     attr = true;
   }
   float* Z = scratch + w1_rows * kW1Part;
   const unsigned G = (unsigned)w1_rows;  // row tiles x slices
   k_grad_slice_fwd<MODE><<<G * sl_planes(MODE), kSlThreads, sl_fwd_lds(MODE), st>>>(f0, f1, f2, S, S2, B, key_row0, seed, call_ctr, Z,
                                                                   step_ctr, n_steps, rs);
+  if constexpr (MODE == kSlActor) {
+    if (job) {  // the acting tick's workgroups first, then the backward's
+      sk::StepArgs a = job->a;
+      const unsigned GA = (unsigned)((a.n + 15) / 16);
+      a.grid_blocks = GA;
+      if (job->sd != 0.f)
+        k_actor_bwd_act_step32<true><<<GA + G, kFwdThreads, kBwdActLds, st>>>(
+            f0, f1, f2, S, A, Y, R, D, gamma, B, key_row0, scale, seed, call_ctr, Z, partials, scratch, stat_out,
+            mask_out, GA, job->aflat, job->act_out, job->sd, job->action_sd, job->seed, job->call_ctr, a, job->c);
+      else
+        k_actor_bwd_act_step32<false><<<GA + G, kFwdThreads, kBwdActLds, st>>>(
+            f0, f1, f2, S, A, Y, R, D, gamma, B, key_row0, scale, seed, call_ctr, Z, partials, scratch, stat_out,
+            mask_out, GA, job->aflat, job->act_out, 0.f, job->action_sd, job->seed, job->call_ctr, a, job->c);
+      return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
+    }
+  }
   k_grad_slice_bwd<MODE><<<G, kSlThreads, sl_bwd_lds(MODE), st>>>(f0, f1, f2, S, A, Y, R, D, gamma, B, key_row0,
                                                                   scale, seed, call_ctr, Z, partials, scratch,
                                                                   stat_out, mask_out);
@@ -1810,11 +1889,17 @@ int replay_sample_excl(const float* ring, int64_t capacity, const int64_t* total
 // the self-play tick launch (sk_env_act_step, csrc/sk_engine.hip): a.n % 4 == 0
 int sk_launch_act_step32(const float* aflat, float* act_out, float sd, float action_sd, uint64_t seed,
                          uint64_t* call_ctr, const sk::StepArgs& a, const sk::Cfg& c, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    set_lds32(k_act_step32<true>, kActStepLds);
+    set_lds32(k_act_step32<false>, kActStepLds);
+    attr = true;
+  }
   const unsigned G = (unsigned)((a.n + 15) / 16);
   if (sd != 0.f)
-    k_act_step32<true><<<G, kFwdThreads, 0, st>>>(aflat, act_out, sd, action_sd, seed, call_ctr, a, c);
+    k_act_step32<true><<<G, kFwdThreads, kActStepLds, st>>>(aflat, act_out, sd, action_sd, seed, call_ctr, a, c);
   else
-    k_act_step32<false><<<G, kFwdThreads, 0, st>>>(aflat, act_out, 0.f, action_sd, seed, call_ctr, a, c);
+    k_act_step32<false><<<G, kFwdThreads, kActStepLds, st>>>(aflat, act_out, 0.f, action_sd, seed, call_ctr, a, c);
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
 }
 
@@ -1940,6 +2025,29 @@ int sk_actor_grad_f32(const float* actor_flat, const float* critic_flat, const f
                                                                   loss_scale, partials, step_counters, n_steps,
                                                                   q_sum);
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
+}
+
+int sk_actor_grad_f32_step(const float* actor_flat, const float* critic_flat, const float* obs, int64_t batch,
+                           float loss_scale, float* partials, float* step_counters, int32_t n_steps, float* q_sum,
+                           float* scratch, const sk_step_job* job, void* stream) {
+  if (!job) return SK_EINVAL;
+  sk::ActStepJob j;
+  std::memcpy(&j, job, sizeof(j));
+  if (j.magic != sk::kActStepJobMagic) return SK_EINVAL;
+  if (!actor_flat || !critic_flat || !obs || !partials || batch <= 0) return SK_EINVAL;
+  if ((n_steps > 0 && !step_counters) || n_steps < 0 || n_steps > 64) return SK_EINVAL;
+  int64_t w1_rows = 0;
+  if (sk_update_scratch_f32(batch, &w1_rows) > 0) {
+    if (!scratch) return SK_EINVAL;
+    return launch_sliced<kSlActor>(actor_flat, critic_flat, nullptr, obs, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                   0.f, batch, 0, loss_scale, 0, nullptr, partials, scratch, w1_rows, step_counters,
+                                   n_steps, q_sum, nullptr, (hipStream_t)stream, RingSample{}, &j);
+  }
+  const int rc = sk_actor_grad_f32(actor_flat, critic_flat, obs, batch, loss_scale, partials, step_counters, n_steps,
+                                   q_sum, scratch, stream);
+  if (rc != SK_OK) return rc;
+  return sk_launch_act_step32(j.aflat, j.act_out, j.sd, j.action_sd, j.seed, j.call_ctr, j.a, j.c,
+                              (hipStream_t)stream);
 }
 
 int sk_actor_forward_f32(const float* actor_flat, const float* obs, float* actions, int64_t rows, float noise_sd,

@@ -179,6 +179,25 @@ struct StepArgs {
   int64_t* ring_total;
   uint32_t* ring_arrivals;  // SK_REPLAY_ARRIVAL_WORDS
   int64_t* ring_total_copy; // NULL, or a second store of the new total
+  // the step's workgroups when they are the first grid_blocks of a larger
+  // launch (k_actor_bwd_act_step32: the actor step's backward beside them),
+  // 0 = the whole grid
+  uint32_t grid_blocks;
+};
+
+// sk_step_job's payload (include/skillshot.h): one prepared act_step32
+// launch (sk_env_act_step_job), run inside the actor step's backward launch
+// (sk_actor_grad_f32_step)
+constexpr uint32_t kActStepJobMagic = 0x534B4A31u;  // "SKJ1"
+struct ActStepJob {
+  uint32_t magic;
+  StepArgs a;
+  Cfg c;
+  const float* aflat;
+  float* act_out;
+  float sd, action_sd;
+  uint64_t seed;
+  uint64_t* call_ctr;
 };
 
 // The ring insert's end of launch (sk_replay.hip's grouped arrival): lane 0
@@ -188,14 +207,14 @@ struct StepArgs {
 // overlapped learner tick's count for the next update, no copy launch).  Called by every lane 0 (lane 0 of a launched
 // workgroup always steps a game).
 __device__ __forceinline__ void ring_arrive(uint32_t* arrivals, int64_t* total, int64_t new_total,
-                                            int64_t* total_copy = nullptr) {
+                                            int64_t* total_copy, unsigned nb) {
   if (threadIdx.x != 0) return;
   const unsigned g = blockIdx.x & 7u;
-  const unsigned members = (gridDim.x - g + 7u) / 8u;
+  const unsigned members = (nb - g + 7u) / 8u;
   uint32_t* gc = arrivals + 32u * (1u + g);
   if (atomicAdd(gc, 1u) == members - 1u) {
     *gc = 0u;
-    const unsigned groups = gridDim.x < 8u ? gridDim.x : 8u;
+    const unsigned groups = nb < 8u ? nb : 8u;
     if (atomicAdd(arrivals, 1u) == groups - 1u) {
       *total = new_total;
       if (total_copy) *total_copy = new_total;
@@ -349,7 +368,8 @@ __device__ __forceinline__ void split_finish(const StepArgs& a, const Cfg& c, co
       }
     }
   }
-  if (ins) ring_arrive(a.ring_arrivals, a.ring_total, rbase + 2 * a.n, a.ring_total_copy);
+  if (ins) ring_arrive(a.ring_arrivals, a.ring_total, rbase + 2 * a.n, a.ring_total_copy,
+                       a.grid_blocks ? a.grid_blocks : gridDim.x);
   if (in && p == 0) {
     if (a.done) a.done[i] = (uint8_t)d;
     if (a.winner) a.winner[i] = (uint8_t)winner;

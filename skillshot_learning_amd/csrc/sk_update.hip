@@ -999,7 +999,10 @@ __device__ __forceinline__ void scatter_fwd_pack(char* out, int p, float v) {  /
   }
 }
 
-constexpr int kAdamParams = 64, kAdamSlices = 4;
+#ifndef SK_ADAM_SLICES
+#define SK_ADAM_SLICES 4
+#endif
+constexpr int kAdamParams = 64, kAdamSlices = SK_ADAM_SLICES;
 
 __global__ void __launch_bounds__(kAdamParams * kAdamSlices) k_adam_flat(const float* __restrict__ partial, int G, int P, const float* __restrict__ grad_in,
                             float* __restrict__ grad_out, int apply, float* __restrict__ param, float* __restrict__ m,

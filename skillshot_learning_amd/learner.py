@@ -593,17 +593,19 @@ class DDPG:
         (hipGraph capture)."""
         return self.update_batch(*self.sample_local(batch, device_sampling))
 
-    def update_overlapped(self, batch, total, exclude, before_actor_adam):
+    def update_overlapped(self, batch, total, exclude, before_actor_adam=None, step_job=None):
         """The overlapped tick's update (TickGraph, SK_TICK_OVERLAP): the
         critic step and the actor gradient on a minibatch keyed on `total`
         (the count before this tick's insert) that leaves out the `exclude`
         rows the insert running beside it writes, then before_actor_adam()
-        (the join with the acting stream), then the actor's Adam launch."""
+        (the join with the acting stream), then the actor's Adam launch.
+        step_job: the tick's prepared acting launch, run in the actor
+        gradient's backward launch (the fused overlapped tick)."""
         fu = self._fused
         b = int(batch)
         lc, (s, _, _, _, _) = fu.critic_step_sampled(self.replay, b, gamma=self.gamma, row_offset=0, global_batch=b,
                                                      total=total, exclude=exclude)
-        return lc, fu.actor_step(s, before_adam=before_actor_adam)
+        return lc, fu.actor_step(s, before_adam=before_actor_adam, step_job=step_job)
 
     def update_sampled(self, batch):
         """replay_update(batch, device_sampling=True) with the minibatch drawn
@@ -1018,15 +1020,31 @@ class TickGraph:
         # bf16 130.6 -> 118 us; config 3 neutral, the graph's cross-queue
         # edges cost what the overlap saves: profiles/r03ov_*); 1 / 0 force.
         # (the ring must hold a batch beside the rows one insert overwrites)
+        # Below that, with the fp32 kernels (SK_TICK_OVERLAP=fused, auto): the
+        # same tick on one stream, the acting launch run by the actor
+        # gradient's backward launch in its spare workgroups
+        # (sk_actor_grad_f32_step; _tick_fused); SK_TICK_OVERLAP=serial: the
+        # same tick with plain launches on one stream (the check that neither
+        # form races).
         ov = os.environ.get("SK_TICK_OVERLAP", "auto")
-        self.overlap = (not L.ddpg.multi() and L.ddpg._fused is not None and updates_per_tick == 1
-                        and L.replay.cap >= batch + 4 * n
-                        and os.environ.get("SK_FUSED_REPLAY", "2") == "2"
-                        and ov != "0" and (ov != "auto" or n >= TICK_OVERLAP_MIN_ENVS))
-        # (SK_TICK_OVERLAP=serial: the same tick on one stream, the check
-        # that the two streams share nothing they race on)
-        self.side = (torch.cuda.Stream(device=dev) if self.overlap and os.environ.get("SK_TICK_OVERLAP") != "serial"
-                     else None)
+        fu = L.ddpg._fused
+        can = (not L.ddpg.multi() and fu is not None and updates_per_tick == 1 and L.replay.cap >= batch + 4 * n
+               and os.environ.get("SK_FUSED_REPLAY", "2") == "2")
+        can_fuse = (can and fu.f32 and getattr(L.actor_kernel, "fused_act_step", False) and n % 4 == 0
+                    and os.environ.get("SK_FUSED_ACT", "1") != "0"
+                    and fu.sliced(batch))
+        if ov == "auto":
+            ov = "1" if n >= TICK_OVERLAP_MIN_ENVS else ("fused" if can_fuse else "0")
+        self.overlap = can and ov != "0" and (ov != "fused" or can_fuse)
+        self.fuse_act = self.overlap and ov == "fused"
+        self.side = (torch.cuda.Stream(device=dev) if self.overlap and ov not in ("serial", "fused") else None)
+        self.mode = ("sequential" if not self.overlap else "fused" if self.fuse_act else
+                     "serial" if self.side is None else "streams")
+        if self.fuse_act:
+            from . import _capi
+            self._job = _capi.SkStepJob()
+        else:
+            self._job = None
         self._hp = 0  # host parity of the horizon slots
         self._capturing = False
         with torch.cuda.stream(self.stream):
@@ -1158,8 +1176,29 @@ class TickGraph:
                                  before_actor_adam=lambda: main.wait_stream(side))
         L._refresh_actor_pack()
 
+    def _tick_fused(self):
+        """one fused overlapped tick: the acting launch is prepared (not
+        issued), the update draws its minibatch from the count before the
+        tick's insert (the insert's rows excluded, as _tick_overlap's), and
+        the actor gradient's backward launch runs the acting tick beside it,
+        before the actor's Adam launch.  Equal, bit for bit, to
+        _tick_overlap's tick (tests/test_replay_gpu.py)."""
+        L = self.L
+        ring = L.replay
+        obs = self._obs[self._cur]
+        self.out["obs_reset"] = self._obs[1 - self._cur]
+        mode = L.exploration
+        L.game_environment.act_step(L.actor_kernel, obs, noise_sd=L.param_noise_sd if mode == "param_noise" else 0.0,
+                                    action_sd=L.action_noise_sd if mode == "action_noise" else 0.0, ring=ring,
+                                    out=self.out, actions=self.act, job=self._job)
+        self._cur ^= 1
+        L.ddpg.update_overlapped(self.batch, ring.total_t, 2 * L.n_envs, step_job=self._job)
+        L._refresh_actor_pack()
+
     def _tick(self, update):
         L = self.L
+        if update and self.fuse_act:
+            return self._tick_fused()
         if update and self.overlap:
             return self._tick_overlap()
         obs = self._obs[self._cur]

@@ -189,6 +189,12 @@ class FusedUpdate:
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
 
+    def sliced(self, batch):
+        """whether the fp32 steps of a `batch`-row minibatch take the sliced
+        schedule (sk_update_scratch_f32 > 0; what sk_actor_grad_f32_step's
+        shared launch needs)"""
+        return bool(self.f32) and int(self.L.sk_update_scratch_f32(int(batch), None)) > 0
+
     def _partial(self, batch, n_params):
         key = (batch, n_params)
         t = self._partials.get(key)
@@ -351,16 +357,26 @@ class FusedUpdate:
                                      self._stream())
 
     @torch.no_grad()
-    def actor_step(self, s, before_adam=None):
+    def actor_step(self, s, before_adam=None, step_job=None):
         """One actor Adam step on -sum_b Q(s_b, mu(s_b)) (critic at inference);
         returns that loss (device scalar).  before_adam() runs between the
         gradient and the Adam launch (the overlapped tick joins the acting
-        stream there: the Adam launch rewrites the weights the actor reads)."""
+        stream there: the Adam launch rewrites the weights the actor reads).
+        step_job (fp32): a prepared acting launch (VecSkillshotGame.act_step
+        (job=...)) run in the gradient's backward launch
+        (sk_actor_grad_f32_step), before the Adam launch."""
         s = s.float().contiguous()
         B = s.shape[0]
         part = self._partial(B, self.fa.numel())
         st = self.sa
-        rc = self._actor_grad(s, part, st.steps, self.stats[1:])
+        if step_job is not None:
+            if not self.f32:
+                raise ValueError("step_job needs the fp32 kernels")
+            rc = self.L.sk_actor_grad_f32_step(_p(self.fa), _p(self.fc), _p(s), B, 1.0, _p(part.main), _p(st.steps),
+                                               st.steps.numel(), _p(self.stats[1:]), _p(part.scratch),
+                                               ctypes.byref(step_job), self._stream())
+        else:
+            rc = self._actor_grad(s, part, st.steps, self.stats[1:])
         _capi.check(rc)
         if before_adam is not None:
             before_adam()

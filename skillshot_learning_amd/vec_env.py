@@ -306,14 +306,16 @@ class VecSkillshotGame:
         return dict(obs=obs_t, reward=rew_t, done=done, winner=win, obs_reset=obs_r)
 
     def act_step(self, actor, acting_obs, noise_sd=0.0, action_sd=0.0, ring=None, reward="looking", auto_reset=True,
-                 reset_obs=True, out=None, actions=None, total_copy=None):
+                 reset_obs=True, out=None, actions=None, total_copy=None, job=None):
         """The self-play tick's act + step (+ ring insert) in ONE launch
         (sk_env_act_step): `actor` (actor_kernel.ActorKernel32, the fp32
         actor) acts on acting_obs [2, N, 12] for both players of every game
         with parameter noise noise_sd and/or action noise action_sd, and the
         step runs on those actions; equal, bit for bit, to actor(...) with
         32-row tiles followed by step_insert (ring given; total_copy as
-        step_insert's) or step.  Returns
+        step_insert's) or step.  job (_capi.SkStepJob): prepare the launch
+        into it instead (sk_env_act_step_job; run by the actor step's
+        backward launch, update_kernel.actor_step(step_job=job)).  Returns
         step's dict plus `actions` [2, N, 2]."""
         o = out or {}
         obs_t = o.get("obs") if o.get("obs") is not None else self.new_obs()
@@ -331,11 +333,13 @@ class VecSkillshotGame:
         ring_args = ((_ptr(ring.buf), ring.cap, _ptr(ring.total_t), _ptr(ring.arrivals()), _ptr(total_copy))
                      if ring is not None else (None, 0, None, None, None))
         actor.calls += 1
-        check(self._L.sk_env_act_step(self._h, _ptr(actor.flat), _ptr(s), _ptr(act), float(noise_sd),
-                                      float(action_sd), actor.seed, _ptr(actor._ctr), _ptr(obs_t), _ptr(rew_t),
-                                      REWARD_KINDS[reward], _ptr(done), _ptr(win), self.tick_limit,
-                                      int(bool(auto_reset)), int(self.random_positions), _ptr(obs_r), *ring_args,
-                                      self._stream()))
+        args = (self._h, _ptr(actor.flat), _ptr(s), _ptr(act), float(noise_sd), float(action_sd), actor.seed,
+                _ptr(actor._ctr), _ptr(obs_t), _ptr(rew_t), REWARD_KINDS[reward], _ptr(done), _ptr(win),
+                self.tick_limit, int(bool(auto_reset)), int(self.random_positions), _ptr(obs_r), *ring_args)
+        if job is not None:
+            check(self._L.sk_env_act_step_job(*args, ctypes.byref(job)))
+        else:
+            check(self._L.sk_env_act_step(*args, self._stream()))
         if ring is not None:
             ring.total += 2 * self.n  # host mirror
         return dict(obs=obs_t, reward=rew_t, done=done, winner=win, obs_reset=obs_r, actions=act)

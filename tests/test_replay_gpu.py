@@ -264,14 +264,16 @@ def test_tick_overlap_equals_serial(learner, monkeypatch, precision, exploration
     insert's rows excluded; joined before the actor's Adam launch): 20
     graph-replayed ticks equal the same ticks captured on one stream
     (SK_TICK_OVERLAP=serial) bit for bit -- nets, target nets, ring,
-    counters -- i.e. the two streams share no data they race on"""
+    counters -- i.e. the two streams share no data they race on; and (fp32)
+    the fused form, the acting launch run by the actor gradient's backward
+    launch (SK_TICK_OVERLAP=fused, sk_actor_grad_f32_step), equals them too"""
     out = []
-    for mode in ("1", "serial"):
+    for mode in ("1", "serial") + (("fused",) if precision == "fp32" else ()):
         monkeypatch.setenv("SK_TICK_OVERLAP", mode)
         L = learner.SkillshotLearner(n_envs=256, device="cuda", seed=7, exploration=exploration, gamma=0.9,
                                      tau=0.05, replay_capacity=4096, precision=precision, tick_limit=50)
         tg = L.tick_graph(batch=128, ticks_per_graph=2, warmup=2)
-        assert tg.overlap and (tg.side is None) == (mode == "serial")
+        assert tg.overlap and (tg.side is None) == (mode != "1") and tg.fuse_act == (mode == "fused")
         tg.run(10)
         torch.cuda.synchronize()
         out.append((torch.cat([p.detach().flatten() for p in L.model_actor.parameters()]),
@@ -279,10 +281,12 @@ def test_tick_overlap_equals_serial(learner, monkeypatch, precision, exploration
                     torch.cat([p.detach().flatten() for p in L.ddpg.target_actor.parameters()]),
                     L.replay.buf.clone(), int(L.replay.total_t), L.game_environment.counters(
                         stream=ctypes.c_void_p(tg.stream.cuda_stream))))
-    (a1, c1, t1, b1, n1, k1), (a2, c2, t2, b2, n2, k2) = out
-    assert n1 == n2 and torch.equal(b1, b2)
-    assert torch.equal(a1, a2) and torch.equal(c1, c2) and torch.equal(t1, t2)
-    assert k1 == k2 and k1["dones"] > 0
+    (a1, c1, t1, b1, n1, k1) = out[0]
+    assert k1["dones"] > 0
+    for a2, c2, t2, b2, n2, k2 in out[1:]:
+        assert n1 == n2 and torch.equal(b1, b2)
+        assert torch.equal(a1, a2) and torch.equal(c1, c2) and torch.equal(t1, t2)
+        assert k1 == k2
 
 
 def test_overlap_sample_excludes_rows_being_written(learner):
@@ -306,3 +310,48 @@ def test_overlap_sample_excludes_rows_being_written(learner):
     lo = total - min(total, cap - E)  # the oldest row id still eligible
     assert int(got.min()) >= lo and int(got.max()) < total
     assert got.unique().numel() > 0.9 * (cap - E)  # uniform over the eligible rows
+
+
+@pytest.mark.parametrize("batch", [128, 1024])  # sliced schedule (one shared launch) / not (two launches)
+@pytest.mark.parametrize("noise", ["param", "action"])
+def test_actor_grad_step_job_equals_separate_launches(learner, monkeypatch, batch, noise):
+    """sk_env_act_step_job + sk_actor_grad_f32_step (the acting tick run in the
+    actor gradient's backward launch) against sk_env_act_step then
+    sk_actor_grad_f32: the actor after each Adam step, the actions, the env
+    outputs, the ring and the noise call number, bit for bit, every tick"""
+    from skillshot_learning_amd import _capi
+    from skillshot_learning_amd.actor_kernel import ActorKernel32
+    from skillshot_learning_amd.vec_env import VecSkillshotGame
+    monkeypatch.setenv("SK_FWD16", "0")
+    n = 256
+    sd, asd = {"param": (0.5, 0.0), "action": (0.0, 0.15)}[noise]
+    out = []
+    for fused in (True, False):
+        d = learner.DDPG("cuda", seed=1, gamma=0.9, tau=0.05, replay_capacity=4096, precision="fp32")
+        fu = d._fused
+        assert fu.sliced(batch) == (batch <= 512)
+        k = ActorKernel32(d.model_actor, seed=9)
+        env = VecSkillshotGame(n, device="cuda", seed=11, tick_limit=30)
+        ring = learner.ReplayRing(1 << 13, "cuda", seed=3)
+        obs = env.observe()[0].clone()
+        g = torch.Generator(device="cuda").manual_seed(5)
+        job = _capi.SkStepJob()
+        rec = []
+        for t in range(6):
+            s = torch.rand((batch, 12), device="cuda", generator=g) * 2 - 1
+            if fused:
+                o = env.act_step(k, obs, noise_sd=sd, action_sd=asd, ring=ring, job=job)
+                fu.actor_step(s, step_job=job)
+            else:
+                o = env.act_step(k, obs, noise_sd=sd, action_sd=asd, ring=ring)
+                fu.actor_step(s)
+            torch.cuda.synchronize()
+            rec.append((fu.fa.clone(), o["actions"].clone(), o["obs"].clone(), o["reward"].clone(),
+                        o["done"].clone(), ring.buf.clone(), k._ctr.clone()))
+            obs = o["obs_reset"]
+        out.append((rec, env.counters()))
+    (r1, c1), (r2, c2) = out
+    for t, (x, y) in enumerate(zip(r1, r2)):
+        for i, (u, v) in enumerate(zip(x, y)):
+            assert torch.equal(u, v), (t, i)
+    assert c1 == c2
