@@ -475,7 +475,8 @@ def learner_roofline(L, tg, batch, precision, exploration, gpu_ms_per_tick, reps
     events around one graph replay of `reps` launches on the leg's stream,
     after its timed region — the actor forward for both players of every game (2N rows; with
     parameter noise the local-reparameterisation variance GEMM doubles its
-    FLOPs), the critic gradient on a replay minibatch (critic forward +
+    FLOPs at bf16; at fp32 that GEMM runs on bf16 MFMA, DESIGN §7, so only the
+    fp32 mean GEMM counts against the fp32 peak), the critic gradient on a replay minibatch (critic forward +
     backward, bootstrap target nets' forwards: 3 x critic + actor + critic
     FLOP per row) and the actor gradient (actor forward + backward, critic
     forward + input backward: 3 x actor + 2 x critic).  `achieved` is the
@@ -506,7 +507,7 @@ def learner_roofline(L, tg, batch, precision, exploration, gpu_ms_per_tick, reps
     def actor_g():
         fu._actor_grad(s, part_a, None, None)
 
-    jobs = {"actor_forward": (actor, rows * ACTOR_FLOP_ROW * (2 if noise else 1)),
+    jobs = {"actor_forward": (actor, rows * ACTOR_FLOP_ROW * (2 if noise and precision == "bf16" else 1)),
             "critic_grad": (critic, batch * (4 * CRITIC_FLOP_ROW + ACTOR_FLOP_ROW)),
             "actor_grad": (actor_g, batch * (3 * ACTOR_FLOP_ROW + 2 * CRITIC_FLOP_ROW))}
     kern = {}

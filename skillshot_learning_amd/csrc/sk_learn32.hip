@@ -170,11 +170,35 @@ __device__ __forceinline__ f32x16 gemm_xwT(f32x16 acc, const float* X, int ldx, 
 }
 // mean and variance GEMMs of parameter noise in one pass: every operand load
 // feeds both (x w and x^2 w^2: two independent accumulator chains per wave)
+// The variance GEMM of parameter noise (x^2 W^2: it only scales the noise)
+// on bf16 operands, fp32 accumulation: one v_mfma_f32_32x32x16_bf16 per 16 k
+// instead of eight 32x32x2 f32 MFMAs; the mean stays fp32.  Lane half h
+// carries k = k0 + 4h + {0..3} and k0 + 8 + 4h + {0..3} in slots 0..7 of
+// both operands (the same k in the same slot: the dot product is unchanged).
+// The noise scale sqrt(b^2 + var) is then within ~2^-9 relative of the fp32
+// form's (SK_VAR_BF16=0 builds that one).
+#ifndef SK_VAR_BF16
+#define SK_VAR_BF16 1
+#endif
 __device__ __forceinline__ void gemm_xwT_mv(f32x16& m, f32x16& v, const float* X, int ldx, gfp W, int ldw,
                                             int n0, int k0, int kc, int lane) {
   const int i = lane & 31, h = lane >> 5;
   const float* xr = X + i * ldx + k0 + 4 * h;
   const gfp wr = W + (size_t)(n0 + i) * ldw + k0 + 4 * h;
+#if SK_VAR_BF16
+#pragma unroll 2
+  for (int k = 0; k < kc; k += 16) {
+    const f4 x0 = *(const f4*)(xr + k), x1 = *(const f4*)(xr + k + 8);
+    const f4 w0 = *(gf4u)(wr + k), w1 = *(gf4u)(wr + k + 8);
+    m = mf4(x0, w0, m);
+    m = mf4(x1, w1, m);
+    const skmlp::bf16x8 xs = {skmlp::f2bf(x0.x * x0.x), skmlp::f2bf(x0.y * x0.y), skmlp::f2bf(x0.z * x0.z), skmlp::f2bf(x0.w * x0.w),
+                       skmlp::f2bf(x1.x * x1.x), skmlp::f2bf(x1.y * x1.y), skmlp::f2bf(x1.z * x1.z), skmlp::f2bf(x1.w * x1.w)};
+    const skmlp::bf16x8 ws = {skmlp::f2bf(w0.x * w0.x), skmlp::f2bf(w0.y * w0.y), skmlp::f2bf(w0.z * w0.z), skmlp::f2bf(w0.w * w0.w),
+                       skmlp::f2bf(w1.x * w1.x), skmlp::f2bf(w1.y * w1.y), skmlp::f2bf(w1.z * w1.z), skmlp::f2bf(w1.w * w1.w)};
+    v = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xs, ws, v, 0, 0, 0);
+  }
+#else
 #pragma unroll 4
   for (int k = 0; k < kc; k += 8) {
     const f4 x = *(const f4*)(xr + k);
@@ -182,6 +206,7 @@ __device__ __forceinline__ void gemm_xwT_mv(f32x16& m, f32x16& v, const float* X
     m = mf4(x, w, m);
     v = mf4(x * x, w * w, v);
   }
+#endif
 }
 // layer 1 (K = 12): k 0..7 by both halves, k 8..11 by half 0 (half 1's
 // 12..15 are zero operands, never loaded)
