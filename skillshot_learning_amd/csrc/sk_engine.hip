@@ -54,7 +54,7 @@ struct sk_env {
   // k_step_multi geometry: -1 auto, 0 lane per game, 1 player per lane (SK_MULTI_SPLIT)
   int multi_split;
   int multi_early;    // k_step_multi: the restart draw under the loads, 0 (default) / 1 (SK_MULTI_EARLY)
-  int multi_block;    // split geometry workgroup: -1 auto, 64 or 512 (SK_MULTI_BLOCK)
+  int multi_block;    // workgroup lanes (SK_MULTI_BLOCK): split geometry -1 auto, 64 or 512; lane per game 256 or 64
   int multi_stagger;  // waves 4-7 of a 512-lane workgroup start this x 512 cycles late (SK_MULTI_STAGGER)
   // k_step_multi's packed resident form between ticks (SK_MULTI_PACK=0 keeps the 88-B form)
   int multi_pack;
@@ -676,15 +676,37 @@ __device__ __forceinline__ void multi_tick(const MultiArgs& a, const Cfg& c, __a
   packed = to_pack;
 }
 
-template <int POL, bool PACK>
-__global__ void __launch_bounds__(kStepBlock) k_step_multi(MultiArgs a, Cfg c, int early) {
+// Measurement build only (-DSK_TRACE_MULTI; tools/trace_multi.py): lane 0 of
+// every k_step_multi wave records s_memrealtime (100 MHz) at entry, after
+// each of the first 30 ticks and at exit into sk_multi_trace[wave][32]
+// (vector stores).
+#ifdef SK_TRACE_MULTI
+__device__ unsigned long long* sk_multi_trace;
+extern "C" int skdiag_set_multi_trace(void* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(sk_multi_trace), &buf, sizeof(buf)) == hipSuccess ? 0 : -1;
+}
+#define SK_MTS(k)                                                                                   \
+  do {                                                                                              \
+    if ((threadIdx.x & 63) == 0)                                                                    \
+      sk_multi_trace[((size_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * 32 + (k)] =    \
+          __builtin_amdgcn_s_memrealtime();                                                         \
+  } while (0)
+#else
+#define SK_MTS(k) \
+  do {            \
+  } while (0)
+#endif
+
+template <int POL, bool PACK, int BLK>
+__global__ void __launch_bounds__(BLK) k_step_multi(MultiArgs a, Cfg c, int early) {
+  SK_MTS(0);
   MultiLane L;
-  L.i = (int64_t)blockIdx.x * kStepBlock + threadIdx.x;
+  L.i = (int64_t)blockIdx.x * BLK + threadIdx.x;
   L.in = L.i < a.n;
   L.ic = L.in ? L.i : 0;
   L.early = a.random_positions && early;
   L.n_done = L.n_h1 = L.n_h2 = L.t_sum = 0;
-  WaveCtr wc = ctr_load(a.ctr);
+  WaveCtr wc = ctr_load<BLK>(a.ctr);
   const uint64_t step0 = step_read(a.step);
   step_advance(a.step, step0, (uint64_t)a.n_ticks);
   const __amdgpu_buffer_rsrc_t r = raw_rsrc(a.base), rp = raw_rsrc(a.pack);
@@ -693,15 +715,17 @@ __global__ void __launch_bounds__(kStepBlock) k_step_multi(MultiArgs a, Cfg c, i
   for (int t = 0; t < a.n_ticks; ++t) {
     multi_tick<POL, PACK>(a, c, r, rp, L, wc, t, step0 + (uint64_t)t, slab, packed, t + 1 == a.n_ticks);
     slab = slab + 1 == a.ring ? 0 : slab + 1;
+#ifdef SK_TRACE_MULTI
+    if (t < 30) SK_MTS(1 + t);
+#endif
   }
   if (a.ctr) {
-    uint64_t v[4] = {L.n_done, L.n_h1, L.n_h2, L.t_sum};
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off, 64);
-    ctr_store(a.ctr, wc, v[0], v[1], v[2], v[3]);
+    const unsigned c4[4] = {L.n_done, L.n_h1, L.n_h2, L.t_sum};
+    uint64_t v[4];
+    wave_sum4_u32(c4, v);
+    ctr_store<BLK>(a.ctr, wc, v[0], v[1], v[2], v[3]);
   }
+  SK_MTS(31);
 }
 
 // k_step_split_multi: k_step_multi with k_step_split's geometry — lanes (2i,
@@ -872,11 +896,9 @@ __global__ void __launch_bounds__(BLK) k_step_split_multi(MultiArgs a, Cfg c, in
     slab = slab + 1 == a.ring ? 0 : slab + 1;
   }
   if (a.ctr) {
-    uint64_t v[4] = {L.n_done, L.n_h1, L.n_h2, L.t_sum};
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off, 64);
+    const unsigned c4[4] = {L.n_done, L.n_h1, L.n_h2, L.t_sum};
+    uint64_t v[4];
+    wave_sum4_u32(c4, v);
     ctr_store<BLK>(a.ctr, wc, v[0], v[1], v[2], v[3]);
   }
 }
@@ -1751,13 +1773,31 @@ int sk_env_step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64
     // default here: 65,536 games 2.73 vs 2.81 us per tick at 20 ticks per
     // launch, 131,072 3.69 vs 3.70 / 3.33 vs 3.37 (profiles/r03i_multi_fast_early_sweep.jsonl)
     const int early = e->multi_early > 0;
-    const dim3 g(step_grid(e->n));
-    if (pk)
-      err = pol == 1 ? launch_timed(k_step_multi<1, true>, g, dim3(kStepBlock), hs, e0, e1, a, e->dcfg, early)
-                     : launch_timed(k_step_multi<0, true>, g, dim3(kStepBlock), hs, e0, e1, a, e->dcfg, early);
-    else
-      err = pol == 1 ? launch_timed(k_step_multi<1, false>, g, dim3(kStepBlock), hs, e0, e1, a, e->dcfg, early)
-                     : launch_timed(k_step_multi<0, false>, g, dim3(kStepBlock), hs, e0, e1, a, e->dcfg, early);
+    // workgroup: four waves (default; a quarter of the workgroups to
+    // dispatch, one wave per SIMD either way: 65,536 games 2.522 vs 2.537 us
+    // per tick at K = 4,000, 2.88 vs 2.92 at K = 20, profiles/r03mb_*) or one
+    // (SK_MULTI_BLOCK=64)
+    if (e->multi_block != 64) {
+      const dim3 g((unsigned)((e->n + 255) / 256));
+      if (pk)
+        err = pol == 1 ? launch_timed(k_step_multi<1, true, 256>, g, dim3(256), hs, e0, e1, a, e->dcfg, early)
+                       : launch_timed(k_step_multi<0, true, 256>, g, dim3(256), hs, e0, e1, a, e->dcfg, early);
+      else
+        err = pol == 1 ? launch_timed(k_step_multi<1, false, 256>, g, dim3(256), hs, e0, e1, a, e->dcfg, early)
+                       : launch_timed(k_step_multi<0, false, 256>, g, dim3(256), hs, e0, e1, a, e->dcfg, early);
+    } else {
+      const dim3 g(step_grid(e->n));
+      if (pk)
+        err = pol == 1
+                  ? launch_timed(k_step_multi<1, true, kStepBlock>, g, dim3(kStepBlock), hs, e0, e1, a, e->dcfg, early)
+                  : launch_timed(k_step_multi<0, true, kStepBlock>, g, dim3(kStepBlock), hs, e0, e1, a, e->dcfg, early);
+      else
+        err = pol == 1
+                  ? launch_timed(k_step_multi<1, false, kStepBlock>, g, dim3(kStepBlock), hs, e0, e1, a, e->dcfg,
+                                 early)
+                  : launch_timed(k_step_multi<0, false, kStepBlock>, g, dim3(kStepBlock), hs, e0, e1, a, e->dcfg,
+                                 early);
+    }
   }
   if (err != hipSuccess) return fail(SK_EHIP, std::string("k_step_multi launch: ") + hipGetErrorString(err));
   e->parity ^= 1;

@@ -49,6 +49,34 @@ struct WaveCtr {
   ulonglong4 v;
 };
 
+// The wave's sum of four per-lane counts (the multi-tick kernels' episode
+// counts, each < 2^32 per lane and per wave), in every lane: DPP butterflies
+// within each 16-lane row (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror,
+// row_mirror: every lane ends with its row's sum), then the four rows'
+// sums by readlane.  The 64-bit __shfl_xor tree it replaces was a chain of 48
+// dependent ds_bpermute round trips, ~1.3 us at the end of a launch
+// (profiles/r03tm_multi_trace.jsonl).
+template <int CTRL>
+__device__ __forceinline__ unsigned dpp_u32(unsigned v) {
+  return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
+}
+__device__ __forceinline__ void wave_sum4_u32(const unsigned in[4], uint64_t out[4]) {
+  unsigned v[4] = {in[0], in[1], in[2], in[3]};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v[k] += dpp_u32<0xB1>(v[k]);   // quad_perm [1,0,3,2]
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v[k] += dpp_u32<0x4E>(v[k]);   // quad_perm [2,3,0,1]
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v[k] += dpp_u32<0x141>(v[k]);  // row_half_mirror
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v[k] += dpp_u32<0x140>(v[k]);  // row_mirror
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    out[k] = (uint64_t)(unsigned)__builtin_amdgcn_readlane((int)v[k], 0) +
+             (unsigned)__builtin_amdgcn_readlane((int)v[k], 16) + (unsigned)__builtin_amdgcn_readlane((int)v[k], 32) +
+             (unsigned)__builtin_amdgcn_readlane((int)v[k], 48);
+}
+
 // the slot line at `slot` (NULL: no counting)
 __device__ __forceinline__ WaveCtr ctr_load_at(const sk_counters* slot) {
   WaveCtr w;
