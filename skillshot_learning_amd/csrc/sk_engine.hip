@@ -56,7 +56,8 @@ struct sk_env {
   int multi_early;    // k_step_multi: the restart draw under the loads, 0 (default) / 1 (SK_MULTI_EARLY)
   int multi_block;    // workgroup lanes (SK_MULTI_BLOCK): split geometry -1 auto, 64 or 512; lane per game 256 or 64
   int multi_stagger;  // waves 4-7 of a 512-lane workgroup start this x 512 cycles late (SK_MULTI_STAGGER)
-  // k_step_multi's packed resident form between ticks (SK_MULTI_PACK=0 keeps the 88-B form)
+  // k_step_multi's packed resident form between ticks: -1 auto (above one
+  // wave per SIMD), 1 / 0 force (SK_MULTI_PACK)
   int multi_pack;
   char* d_pack;  // its scratch (48 B x n), allocated at the first multi-tick launch
   // device = -1: the CPU backend (sk_host.cpp) owns the games; every entry
@@ -88,6 +89,9 @@ static constexpr int64_t kFastStepMaxEnvs = 786432;
 // metric's 65,536 games over 8 ranks
 static constexpr int64_t kSplitStepMaxEnvs = 8192;
 static constexpr int64_t kEarlyDrawMinEnvs = 32768;
+// k_step_multi's packed resident form above this many games (one wave per
+// SIMD on 1,024 SIMDs)
+constexpr int64_t kPackMinEnvs = 65536;
 // k_step_multi: two lanes per game up to this many games.  Write-through
 // port, 400 ticks per launch: 8,192 games 1.59 vs 1.85 us per tick, 32,768
 // 1.80 vs 2.02, but 65,536 2.59 vs 2.36 (profiles/r03c_multi_split_sweep.jsonl)
@@ -1163,7 +1167,7 @@ static int make_env(sk_env** out, const sk_state_view* view, int32_t n, int64_t 
   if (const char* mb = std::getenv("SK_MULTI_BLOCK")) e->multi_block = std::atoi(mb);
   e->multi_stagger = 0;
   if (const char* mg = std::getenv("SK_MULTI_STAGGER")) e->multi_stagger = std::atoi(mg);
-  e->multi_pack = 1;
+  e->multi_pack = -1;
   if (const char* mk = std::getenv("SK_MULTI_PACK")) e->multi_pack = std::atoi(mk);
   e->d_pack = nullptr;
   if (view) {
@@ -1721,7 +1725,13 @@ int sk_env_step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64
   a.base = nullptr;
   for (int k = 0; k < 6; ++k) a.off[k] = 0;
   a.pack = nullptr;
-  if (n_ticks > 1 && e->multi_pack && (uint64_t)e->n * 48u <= 0xffffffffull) {
+  // the packed resident form pays where the tick is bandwidth-bound (two or
+  // more waves per SIMD: 131,072 games 3.33 vs 4.03 us per tick, 262,144 6.4
+  // vs 7.7); at one wave per SIMD the tick is a latency chain and the
+  // pack / unpack work lengthens it (65,536: 2.51 vs 2.38; 32,768: 2.43 vs
+  // 2.04; profiles/r03pk2_multi_pack_sweep.jsonl)
+  const bool want_pack = e->multi_pack > 0 || (e->multi_pack < 0 && e->n > kPackMinEnvs);
+  if (n_ticks > 1 && want_pack && (uint64_t)e->n * 48u <= 0xffffffffull) {
     if (!e->d_pack) {
       if (hipMalloc(&e->d_pack, (size_t)e->n * 48) != hipSuccess) return fail(SK_ENOMEM, "hipMalloc pack");
     }
