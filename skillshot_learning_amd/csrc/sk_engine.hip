@@ -54,7 +54,7 @@ struct sk_env {
   // k_step_multi geometry: -1 auto, 0 lane per game, 1 player per lane (SK_MULTI_SPLIT)
   int multi_split;
   int multi_early;    // k_step_multi: the restart draw under the loads, 0 (default) / 1 (SK_MULTI_EARLY)
-  int multi_block;    // workgroup lanes (SK_MULTI_BLOCK): split geometry -1 auto, 64 or 512; lane per game 256 or 64
+  int multi_block;    // workgroup lanes (SK_MULTI_BLOCK): split geometry -1 auto, 64 or 512; lane per game 64 or 256
   int multi_stagger;  // waves 4-7 of a 512-lane workgroup start this x 512 cycles late (SK_MULTI_STAGGER)
   // k_step_multi's packed resident form between ticks: -1 auto (above one
   // wave per SIMD), 1 / 0 force (SK_MULTI_PACK)
@@ -1783,11 +1783,12 @@ int sk_env_step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64
     // default here: 65,536 games 2.73 vs 2.81 us per tick at 20 ticks per
     // launch, 131,072 3.69 vs 3.70 / 3.33 vs 3.37 (profiles/r03i_multi_fast_early_sweep.jsonl)
     const int early = e->multi_early > 0;
-    // workgroup: four waves (default; a quarter of the workgroups to
-    // dispatch, one wave per SIMD either way: 65,536 games 2.522 vs 2.537 us
-    // per tick at K = 4,000, 2.88 vs 2.92 at K = 20, profiles/r03mb_*) or one
-    // (SK_MULTI_BLOCK=64)
-    if (e->multi_block != 64) {
+    // workgroup: one wave (default) or four (SK_MULTI_BLOCK=256: a quarter of
+    // the workgroups to dispatch, one wave per SIMD either way).  With the
+    // packed form 256 lanes won by ~0.6 %, with the 88-B form 64 lanes win by
+    // about as much (65,536 games, K = 4,000: 2.40 vs 2.415 us per tick;
+    // profiles/r03mb_multi_block_ab.jsonl, r03mb2_multi_block_early_ab.jsonl)
+    if (e->multi_block == 256) {
       const dim3 g((unsigned)((e->n + 255) / 256));
       if (pk)
         err = pol == 1 ? launch_timed(k_step_multi<1, true, 256>, g, dim3(256), hs, e0, e1, a, e->dcfg, early)
