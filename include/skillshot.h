@@ -587,6 +587,17 @@ int sk_actor_grad_f32(const float* actor_flat, const float* critic_flat, const f
 int sk_actor_grad_f32_step(const float* actor_flat, const float* critic_flat, const float* obs, int64_t batch,
                            float loss_scale, float* partials, float* step_counters, int32_t n_steps, float* q_sum,
                            float* scratch, const sk_step_job* job, void* stream);
+/* sk_critic_grad_f32_sampled with a prepared acting tick run in its backward
+ * launch (ABI 8; the minibatch is gathered by the first launch, before the
+ * acting tick's insert: give q->exclude = the insert's rows).  Results equal,
+ * bit for bit, sk_critic_grad_f32_sampled followed by the job's
+ * sk_env_act_step. */
+int sk_critic_grad_f32_sampled_step(const float* critic_flat, const sk_ring_sample* q, float gamma,
+                                    const float* target_actor_flat, const float* target_critic_flat, int64_t batch,
+                                    int64_t row_offset, float grad_scale, uint64_t seed,
+                                    const int64_t* call_counter, float* partials, float* step_counters,
+                                    int32_t n_steps, float* loss_sum, uint8_t* dropout_mask, float* scratch,
+                                    const sk_step_job* job, void* stream);
 
 #ifdef __cplusplus
 }

@@ -35,6 +35,7 @@ EXPORTS = (
     "sk_critic_grad_bootstrap",
     "sk_update_partials_f32", "sk_actor_forward_f32", "sk_critic_grad_f32", "sk_critic_grad_f32_sampled",
     "sk_critic_grad_bootstrap_sampled", "sk_actor_grad_f32", "sk_actor_grad_f32_step",
+    "sk_critic_grad_f32_sampled_step",
 )
 
 
@@ -157,6 +158,8 @@ def load(build_if_missing=True):
                                ctypes.c_int),
         "sk_critic_grad_f32_sampled": ([P, P, f32, P, P, i64, i64, f32, u64, P, P, P, i32, P, P, P, P],
                                        ctypes.c_int),
+        "sk_critic_grad_f32_sampled_step": ([P, P, f32, P, P, i64, i64, f32, u64, P, P, P, i32, P, P, P,
+                                             ctypes.POINTER(SkStepJob), P], ctypes.c_int),
         "sk_critic_grad_bootstrap_sampled": ([P, P, f32, P, P, i64, i64, f32, u64, P, P, P, i32, P, P, P],
                                              ctypes.c_int),
         "sk_actor_grad_f32": ([P, P, P, i64, f32, P, P, i32, P, P, P], ctypes.c_int),

@@ -230,13 +230,6 @@ __device__ __forceinline__ f32x16 gemm_l1(const float* S, gfp W1, int n0, int la
   acc = mf4(x0, w0, acc);
   return mf4(x1, w1, acc);
 }
-// stage a sub-tile's states: S[i][k] = obs (k < 12, row < B), else 0
-__device__ __forceinline__ void stage_states(float* S, const float* X, int64_t row0, int64_t B) {
-  for (int t = threadIdx.x; t < 32 * kLdS; t += blockDim.x) {
-    const int i = t / kLdS, k = t - i * kLdS;
-    S[t] = (k < kIn && row0 + i < B) ? X[(row0 + i) * kIn + k] : 0.f;
-  }
-}
 
 // ================================================================ gradient kernels
 // 16-row sub-tiles on v_mfma_f32_16x16x4_f32 (the fp32 MFMA rate is the
@@ -1675,25 +1668,29 @@ __global__ void __launch_bounds__(kFwdThreads) k_act_step32(const float* __restr
                     gridDim.x);
 }
 
-// The actor step's backward launch with the next acting tick beside it (the
-// fused overlapped learner tick, sk_actor_grad_f32_step): workgroups
-// [0, GA) run act_step32 (k_act_step32's 16 games each), the rest
-// grad_slice_bwd<kSlActor> (k_grad_slice_bwd's workgroup blockIdx - GA).  The
+// A gradient step's backward launch with the next acting tick beside it
+// (the fused overlapped learner tick: sk_critic_grad_f32_sampled_step carries
+// it in the critic's backward, sk_actor_grad_f32_step in the actor's):
+// workgroups [0, GA) run act_step32 (k_act_step32's 16 games each), the rest
+// grad_slice_bwd<MODE> (k_grad_slice_bwd's workgroup blockIdx - GA).  The
 // two share no data: the backward reads the minibatch, the nets and the
 // forward's z2; the acting half reads the actor and the observations and
 // writes the env, the actions and the ring (the minibatch was gathered
 // before, excluding the rows this insert writes).  LDS is the larger of the
-// two layouts (two workgroups per CU).
-constexpr size_t kBwdActLds =
-    kActStepLds > sl_bwd_lds(kSlActor) ? kActStepLds : sl_bwd_lds(kSlActor);
+// two layouts: two workgroups per CU (the critic's 81,616 B twice fill the
+// CU's 160 KiB).
+constexpr size_t bwd_act_lds(int mode) {
+  return kActStepLds > sl_bwd_lds(mode) ? kActStepLds : sl_bwd_lds(mode);
+}
+static_assert(2 * bwd_act_lds(kSlCriticBoot) <= 160 * 1024 && 2 * bwd_act_lds(kSlActor) <= 160 * 1024,
+              "two fused workgroups per CU");
 static_assert(kSlThreads == kFwdThreads, "one workgroup size for both halves");
-template <bool NOISE>
-__global__ void __launch_bounds__(kFwdThreads) k_actor_bwd_act_step32(SK_SLICE_BWD_PARAMS, unsigned GA,
-                                                                      const float* __restrict__ aflat,
-                                                                      float* __restrict__ act_out, float sd,
-                                                                      float action_sd, uint64_t aseed,
-                                                                      uint64_t* __restrict__ acall_ctr,
-                                                                      sk::StepArgs a, sk::Cfg c) {
+template <int MODE, bool NOISE>
+__global__ void __launch_bounds__(kFwdThreads) k_bwd_act_step32(SK_SLICE_BWD_PARAMS, unsigned GA,
+                                                                const float* __restrict__ aflat,
+                                                                float* __restrict__ act_out, float sd, float action_sd,
+                                                                uint64_t aseed, uint64_t* __restrict__ acall_ctr,
+                                                                sk::StepArgs a, sk::Cfg c) {
   extern __shared__ __attribute__((aligned(16))) float smem_sl[];
   if (blockIdx.x < GA) {
     float* S = smem_sl;
@@ -1702,7 +1699,7 @@ __global__ void __launch_bounds__(kFwdThreads) k_actor_bwd_act_step32(SK_SLICE_B
     act_step32<NOISE>(aflat, act_out, sd, action_sd, aseed, acall_ctr, a, c, S, H1, H2, (float2*)(H2 + 32 * kLdH2),
                       GA);
   } else {
-    grad_slice_bwd<kSlActor>((int)(blockIdx.x - GA), smem_sl, SK_SLICE_BWD_ARGS);
+    grad_slice_bwd<MODE>((int)(blockIdx.x - GA), smem_sl, SK_SLICE_BWD_ARGS);
   }
 }
 
@@ -1872,31 +1869,27 @@ int launch_sliced(const float* f0, const float* f1, const float* f2, const float
   if (!attr) {
     set_lds32(k_grad_slice_fwd<MODE>, sl_fwd_lds(MODE));
     set_lds32(k_grad_slice_bwd<MODE>, sl_bwd_lds(MODE));
-    if constexpr (MODE == kSlActor) {
-      set_lds32(k_actor_bwd_act_step32<true>, kBwdActLds);
-      set_lds32(k_actor_bwd_act_step32<false>, kBwdActLds);
-    }
+    set_lds32(k_bwd_act_step32<MODE, true>, bwd_act_lds(MODE));
+    set_lds32(k_bwd_act_step32<MODE, false>, bwd_act_lds(MODE));
     attr = true;
   }
   float* Z = scratch + w1_rows * kW1Part;
   const unsigned G = (unsigned)w1_rows;  // row tiles x slices
   k_grad_slice_fwd<MODE><<<G * sl_planes(MODE), kSlThreads, sl_fwd_lds(MODE), st>>>(f0, f1, f2, S, S2, B, key_row0, seed, call_ctr, Z,
                                                                   step_ctr, n_steps, rs);
-  if constexpr (MODE == kSlActor) {
-    if (job) {  // the acting tick's workgroups first, then the backward's
-      sk::StepArgs a = job->a;
-      const unsigned GA = (unsigned)((a.n + 15) / 16);
-      a.grid_blocks = GA;
-      if (job->sd != 0.f)
-        k_actor_bwd_act_step32<true><<<GA + G, kFwdThreads, kBwdActLds, st>>>(
-            f0, f1, f2, S, A, Y, R, D, gamma, B, key_row0, scale, seed, call_ctr, Z, partials, scratch, stat_out,
-            mask_out, GA, job->aflat, job->act_out, job->sd, job->action_sd, job->seed, job->call_ctr, a, job->c);
-      else
-        k_actor_bwd_act_step32<false><<<GA + G, kFwdThreads, kBwdActLds, st>>>(
-            f0, f1, f2, S, A, Y, R, D, gamma, B, key_row0, scale, seed, call_ctr, Z, partials, scratch, stat_out,
-            mask_out, GA, job->aflat, job->act_out, 0.f, job->action_sd, job->seed, job->call_ctr, a, job->c);
-      return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
-    }
+  if (job) {  // the acting tick's workgroups first, then the backward's
+    sk::StepArgs a = job->a;
+    const unsigned GA = (unsigned)((a.n + 15) / 16);
+    a.grid_blocks = GA;
+    if (job->sd != 0.f)
+      k_bwd_act_step32<MODE, true><<<GA + G, kFwdThreads, bwd_act_lds(MODE), st>>>(
+          f0, f1, f2, S, A, Y, R, D, gamma, B, key_row0, scale, seed, call_ctr, Z, partials, scratch, stat_out,
+          mask_out, GA, job->aflat, job->act_out, job->sd, job->action_sd, job->seed, job->call_ctr, a, job->c);
+    else
+      k_bwd_act_step32<MODE, false><<<GA + G, kFwdThreads, bwd_act_lds(MODE), st>>>(
+          f0, f1, f2, S, A, Y, R, D, gamma, B, key_row0, scale, seed, call_ctr, Z, partials, scratch, stat_out,
+          mask_out, GA, job->aflat, job->act_out, 0.f, job->action_sd, job->seed, job->call_ctr, a, job->c);
+    return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
   }
   k_grad_slice_bwd<MODE><<<G, kSlThreads, sl_bwd_lds(MODE), st>>>(f0, f1, f2, S, A, Y, R, D, gamma, B, key_row0,
                                                                   scale, seed, call_ctr, Z, partials, scratch,
@@ -1991,11 +1984,11 @@ int sk_critic_grad_f32(const float* critic_flat, const float* obs, const float* 
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
 }
 
-int sk_critic_grad_f32_sampled(const float* critic_flat, const sk_ring_sample* q, float gamma,
-                               const float* target_actor_flat, const float* target_critic_flat, int64_t batch,
-                               int64_t row_offset, float grad_scale, uint64_t seed, const int64_t* call_counter,
-                               float* partials, float* step_counters, int32_t n_steps, float* loss_sum,
-                               uint8_t* dropout_mask, float* scratch, void* stream) {
+static int critic_sampled(const float* critic_flat, const sk_ring_sample* q, float gamma,
+                          const float* target_actor_flat, const float* target_critic_flat, int64_t batch,
+                          int64_t row_offset, float grad_scale, uint64_t seed, const int64_t* call_counter,
+                          float* partials, float* step_counters, int32_t n_steps, float* loss_sum,
+                          uint8_t* dropout_mask, float* scratch, const sk::ActStepJob* job, void* stream) {
   if (!q || !q->ring || !q->total || !q->s || !q->a || !q->r || !q->s2 || !q->d || q->capacity <= 0) return SK_EINVAL;
   if ((((uintptr_t)q->ring) & 15) || (((uintptr_t)q->s) & 15) || (((uintptr_t)q->s2) & 15) || (((uintptr_t)q->a) & 7))
     return SK_EINVAL;
@@ -2012,19 +2005,47 @@ int sk_critic_grad_f32_sampled(const float* critic_flat, const sk_ring_sample* q
       return launch_sliced<kSlCriticBoot>(critic_flat, target_actor_flat, target_critic_flat, q->s, q->s2, q->a,
                                           nullptr, q->r, q->d, gamma, batch, row_offset, grad_scale, seed,
                                           call_counter, partials, scratch, w1_rows, step_counters, n_steps, loss_sum,
-                                          dropout_mask, (hipStream_t)stream, rs);
+                                          dropout_mask, (hipStream_t)stream, rs, job);
     return launch_sliced<kSlCriticY>(critic_flat, nullptr, nullptr, q->s, nullptr, q->a, q->r, nullptr, nullptr, 0.f,
                                      batch, row_offset, grad_scale, seed, call_counter, partials, scratch, w1_rows,
-                                     step_counters, n_steps, loss_sum, dropout_mask, (hipStream_t)stream, rs);
+                                     step_counters, n_steps, loss_sum, dropout_mask, (hipStream_t)stream, rs, job);
   }
   // unsliced batches: the gather as its own launch
   const int rc = replay_sample_excl(q->ring, q->capacity, q->total, q->seed, q->draw, batch, q->s, q->a, q->r, q->s2,
                                     q->d, q->exclude, (hipStream_t)stream);
   if (rc != SK_OK) return rc;
-  return sk_critic_grad_f32(critic_flat, q->s, q->a, boot ? nullptr : q->r, boot ? q->s2 : nullptr,
-                            boot ? q->r : nullptr, boot ? q->d : nullptr, gamma, target_actor_flat,
-                            target_critic_flat, batch, row_offset, grad_scale, seed, call_counter, partials,
-                            step_counters, n_steps, loss_sum, dropout_mask, scratch, stream);
+  const int rc2 = sk_critic_grad_f32(critic_flat, q->s, q->a, boot ? nullptr : q->r, boot ? q->s2 : nullptr,
+                                     boot ? q->r : nullptr, boot ? q->d : nullptr, gamma, target_actor_flat,
+                                     target_critic_flat, batch, row_offset, grad_scale, seed, call_counter, partials,
+                                     step_counters, n_steps, loss_sum, dropout_mask, scratch, stream);
+  if (rc2 != SK_OK || !job) return rc2;
+  return sk_launch_act_step32(job->aflat, job->act_out, job->sd, job->action_sd, job->seed, job->call_ctr, job->a,
+                              job->c, (hipStream_t)stream);
+}
+
+int sk_critic_grad_f32_sampled(const float* critic_flat, const sk_ring_sample* q, float gamma,
+                               const float* target_actor_flat, const float* target_critic_flat, int64_t batch,
+                               int64_t row_offset, float grad_scale, uint64_t seed, const int64_t* call_counter,
+                               float* partials, float* step_counters, int32_t n_steps, float* loss_sum,
+                               uint8_t* dropout_mask, float* scratch, void* stream) {
+  return critic_sampled(critic_flat, q, gamma, target_actor_flat, target_critic_flat, batch, row_offset, grad_scale,
+                        seed, call_counter, partials, step_counters, n_steps, loss_sum, dropout_mask, scratch, nullptr,
+                        stream);
+}
+
+int sk_critic_grad_f32_sampled_step(const float* critic_flat, const sk_ring_sample* q, float gamma,
+                                    const float* target_actor_flat, const float* target_critic_flat, int64_t batch,
+                                    int64_t row_offset, float grad_scale, uint64_t seed,
+                                    const int64_t* call_counter, float* partials, float* step_counters,
+                                    int32_t n_steps, float* loss_sum, uint8_t* dropout_mask, float* scratch,
+                                    const sk_step_job* job, void* stream) {
+  if (!job) return SK_EINVAL;
+  sk::ActStepJob j;
+  std::memcpy(&j, job, sizeof(j));
+  if (j.magic != sk::kActStepJobMagic) return SK_EINVAL;
+  return critic_sampled(critic_flat, q, gamma, target_actor_flat, target_critic_flat, batch, row_offset, grad_scale,
+                        seed, call_counter, partials, step_counters, n_steps, loss_sum, dropout_mask, scratch, &j,
+                        stream);
 }
 
 int sk_actor_grad_f32(const float* actor_flat, const float* critic_flat, const float* obs, int64_t batch,

@@ -593,19 +593,21 @@ class DDPG:
         (hipGraph capture)."""
         return self.update_batch(*self.sample_local(batch, device_sampling))
 
-    def update_overlapped(self, batch, total, exclude, before_actor_adam=None, step_job=None):
+    def update_overlapped(self, batch, total, exclude, before_actor_adam=None, step_job=None, job_in="critic"):
         """The overlapped tick's update (TickGraph, SK_TICK_OVERLAP): the
         critic step and the actor gradient on a minibatch keyed on `total`
         (the count before this tick's insert) that leaves out the `exclude`
         rows the insert running beside it writes, then before_actor_adam()
         (the join with the acting stream), then the actor's Adam launch.
-        step_job: the tick's prepared acting launch, run in the actor
-        gradient's backward launch (the fused overlapped tick)."""
+        step_job: the tick's prepared acting launch, run in the critic's
+        (job_in "critic") or the actor's ("actor") gradient backward launch
+        (the fused overlapped tick)."""
         fu = self._fused
         b = int(batch)
+        cj = step_job if job_in == "critic" else None
         lc, (s, _, _, _, _) = fu.critic_step_sampled(self.replay, b, gamma=self.gamma, row_offset=0, global_batch=b,
-                                                     total=total, exclude=exclude)
-        return lc, fu.actor_step(s, before_adam=before_actor_adam, step_job=step_job)
+                                                     total=total, exclude=exclude, step_job=cj)
+        return lc, fu.actor_step(s, before_adam=before_actor_adam, step_job=None if cj is not None else step_job)
 
     def update_sampled(self, batch):
         """replay_update(batch, device_sampling=True) with the minibatch drawn
@@ -1040,6 +1042,9 @@ class TickGraph:
         self.side = (torch.cuda.Stream(device=dev) if self.overlap and ov not in ("serial", "fused") else None)
         self.mode = ("sequential" if not self.overlap else "fused" if self.fuse_act else
                      "serial" if self.side is None else "streams")
+        # which backward launch carries the acting tick (SK_FUSE_ACT_IN): the
+        # critic's (default, the longer of the two) or the actor's
+        self.job_in = os.environ.get("SK_FUSE_ACT_IN", "critic")
         if self.fuse_act:
             from . import _capi
             self._job = _capi.SkStepJob()
@@ -1192,7 +1197,7 @@ class TickGraph:
                                     action_sd=L.action_noise_sd if mode == "action_noise" else 0.0, ring=ring,
                                     out=self.out, actions=self.act, job=self._job)
         self._cur ^= 1
-        L.ddpg.update_overlapped(self.batch, ring.total_t, 2 * L.n_envs, step_job=self._job)
+        L.ddpg.update_overlapped(self.batch, ring.total_t, 2 * L.n_envs, step_job=self._job, job_in=self.job_in)
         L._refresh_actor_pack()
 
     def _tick(self, update):

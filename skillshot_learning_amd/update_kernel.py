@@ -297,13 +297,16 @@ class FusedUpdate:
         return loss
 
     @torch.no_grad()
-    def critic_step_sampled(self, ring, batch, gamma=0.0, row_offset=0, global_batch=None, total=None, exclude=0):
+    def critic_step_sampled(self, ring, batch, gamma=0.0, row_offset=0, global_batch=None, total=None, exclude=0,
+                            step_job=None):
         """critic_step on a minibatch the launch draws from the replay ring:
         equal to ring.sample_dev(batch) followed by critic_step with the
         bootstrap target (gamma > 0) or y = r.  total: the device count the
         draw is keyed on (default the ring's); exclude > 0 leaves out the
         rows an insert running beside the step writes (sk_ring_sample).
-        Returns (loss, (s, a, r, s2, d)), the sample buffers."""
+        step_job (fp32): a prepared acting launch run in the gradient's
+        backward launch (sk_critic_grad_f32_sampled_step), before the Adam
+        launch.  Returns (loss, (s, a, r, s2, d)), the sample buffers."""
         B = int(batch)
         gb = B if global_batch is None else int(global_batch)
         out, draw = ring.next_draw(B)
@@ -313,13 +316,18 @@ class FusedUpdate:
         part = self._partial(B, self.fc.numel())
         st = self.sc
         boot = gamma > 0.0
+        if step_job is not None and not self.f32:
+            raise ValueError("step_job needs the fp32 kernels")
         if self.f32:
             ta = (self.ta if self.ta is not None else self.fa) if boot else None
             tc = (self.tc if self.tc is not None else self.fc) if boot else None
-            _capi.check(self.L.sk_critic_grad_f32_sampled(
-                _p(self.fc), ctypes.byref(q), float(gamma), _p(ta), _p(tc), B, int(row_offset), 2.0 / gb, self.seed,
-                _p(self.calls), _p(part.main), _p(st.steps), st.steps.numel(), _p(self.stats[0:1]), None,
-                _p(part.scratch), self._stream()))
+            args = (_p(self.fc), ctypes.byref(q), float(gamma), _p(ta), _p(tc), B, int(row_offset), 2.0 / gb,
+                    self.seed, _p(self.calls), _p(part.main), _p(st.steps), st.steps.numel(), _p(self.stats[0:1]),
+                    None, _p(part.scratch))
+            if step_job is not None:
+                _capi.check(self.L.sk_critic_grad_f32_sampled_step(*args, ctypes.byref(step_job), self._stream()))
+            else:
+                _capi.check(self.L.sk_critic_grad_f32_sampled(*args, self._stream()))
         else:
             _capi.check(self.L.sk_critic_grad_bootstrap_sampled(
                 _p(self.gpc), ctypes.byref(q), float(gamma), _p(self.gpta) if boot else None,

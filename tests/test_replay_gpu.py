@@ -268,7 +268,9 @@ def test_tick_overlap_equals_serial(learner, monkeypatch, precision, exploration
     the fused form, the acting launch run by the actor gradient's backward
     launch (SK_TICK_OVERLAP=fused, sk_actor_grad_f32_step), equals them too"""
     out = []
-    for mode in ("1", "serial") + (("fused",) if precision == "fp32" else ()):
+    for mode in ("1", "serial") + (("fused", "fused-actor") if precision == "fp32" else ()):
+        monkeypatch.setenv("SK_FUSE_ACT_IN", "actor" if mode == "fused-actor" else "critic")
+        mode = mode.split("-")[0]
         monkeypatch.setenv("SK_TICK_OVERLAP", mode)
         L = learner.SkillshotLearner(n_envs=256, device="cuda", seed=7, exploration=exploration, gamma=0.9,
                                      tau=0.05, replay_capacity=4096, precision=precision, tick_limit=50)
@@ -314,11 +316,13 @@ def test_overlap_sample_excludes_rows_being_written(learner):
 
 @pytest.mark.parametrize("batch", [128, 1024])  # sliced schedule (one shared launch) / not (two launches)
 @pytest.mark.parametrize("noise", ["param", "action"])
-def test_actor_grad_step_job_equals_separate_launches(learner, monkeypatch, batch, noise):
-    """sk_env_act_step_job + sk_actor_grad_f32_step (the acting tick run in the
-    actor gradient's backward launch) against sk_env_act_step then
-    sk_actor_grad_f32: the actor after each Adam step, the actions, the env
-    outputs, the ring and the noise call number, bit for bit, every tick"""
+@pytest.mark.parametrize("carrier", ["actor", "critic"])
+def test_grad_step_job_equals_separate_launches(learner, monkeypatch, batch, noise, carrier):
+    """sk_env_act_step_job + sk_actor_grad_f32_step / sk_critic_grad_f32_sampled_step
+    (the acting tick run in a gradient step's backward launch) against the
+    gradient step and sk_env_act_step as separate launches: the net after
+    each Adam step, the actions, the env outputs, the ring and the noise call
+    number, bit for bit, every tick"""
     from skillshot_learning_amd import _capi
     from skillshot_learning_amd.actor_kernel import ActorKernel32
     from skillshot_learning_amd.vec_env import VecSkillshotGame
@@ -339,14 +343,23 @@ def test_actor_grad_step_job_equals_separate_launches(learner, monkeypatch, batc
         rec = []
         for t in range(6):
             s = torch.rand((batch, 12), device="cuda", generator=g) * 2 - 1
-            if fused:
-                o = env.act_step(k, obs, noise_sd=sd, action_sd=asd, ring=ring, job=job)
-                fu.actor_step(s, step_job=job)
-            else:
+            if carrier == "actor":
+                if fused:
+                    o = env.act_step(k, obs, noise_sd=sd, action_sd=asd, ring=ring, job=job)
+                    fu.actor_step(s, step_job=job)
+                else:
+                    o = env.act_step(k, obs, noise_sd=sd, action_sd=asd, ring=ring)
+                    fu.actor_step(s)
+            elif t == 0:  # the critic draws from the ring: fill it first
                 o = env.act_step(k, obs, noise_sd=sd, action_sd=asd, ring=ring)
-                fu.actor_step(s)
+            elif fused:
+                o = env.act_step(k, obs, noise_sd=sd, action_sd=asd, ring=ring, job=job)
+                fu.critic_step_sampled(ring, batch, gamma=0.9, exclude=2 * n, step_job=job)
+            else:
+                fu.critic_step_sampled(ring, batch, gamma=0.9, exclude=2 * n)
+                o = env.act_step(k, obs, noise_sd=sd, action_sd=asd, ring=ring)
             torch.cuda.synchronize()
-            rec.append((fu.fa.clone(), o["actions"].clone(), o["obs"].clone(), o["reward"].clone(),
+            rec.append((fu.fa.clone(), fu.fc.clone(), o["actions"].clone(), o["obs"].clone(), o["reward"].clone(),
                         o["done"].clone(), ring.buf.clone(), k._ctr.clone()))
             obs = o["obs_reset"]
         out.append((rec, env.counters()))
