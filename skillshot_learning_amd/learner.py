@@ -603,10 +603,12 @@ class DDPG:
         (job_in "critic") or the actor's ("actor") gradient backward launch
         (the fused overlapped tick)."""
         fu = self._fused
-        b = int(batch)
+        w, rk, b = self.world(), self.rank(), int(batch)
+        if w > 1 and b % 4:
+            raise ValueError("multi-rank batches must be a multiple of 4 rows (Dropout key groups)")
         cj = step_job if job_in == "critic" else None
-        lc, (s, _, _, _, _) = fu.critic_step_sampled(self.replay, b, gamma=self.gamma, row_offset=0, global_batch=b,
-                                                     total=total, exclude=exclude, step_job=cj)
+        lc, (s, _, _, _, _) = fu.critic_step_sampled(self.replay, b, gamma=self.gamma, row_offset=rk * b,
+                                                     global_batch=w * b, total=total, exclude=exclude, step_job=cj)
         return lc, fu.actor_step(s, before_adam=before_actor_adam, step_job=None if cj is not None else step_job)
 
     def update_sampled(self, batch):
@@ -937,8 +939,10 @@ class SkillshotLearner:
         "segmented" otherwise; SK_TICKGRAPH_MODE overrides.
 
         One rank from TICK_OVERLAP_MIN_ENVS games (SK_TICK_OVERLAP): the acting
-        launches run beside the update on a second stream, and the update draws
-        from the rows inserted before the tick (TickGraph.overlap).
+        launches run beside the update on a second stream; below that (and
+        with multi_rank "grad") with the fp32 kernels, inside the critic's
+        backward launch.  Either way the update draws from the rows inserted
+        before the tick (TickGraph.overlap).
         """
         if self.device.type != "cuda":
             raise RuntimeError("tick_graph needs the GPU engine")
@@ -1028,15 +1032,21 @@ class TickGraph:
         # (sk_actor_grad_f32_step; _tick_fused); SK_TICK_OVERLAP=serial: the
         # same tick with plain launches on one stream (the check that neither
         # form races).
+        # Several ranks: the fused form with multi_rank "grad" (config 4: each
+        # rank draws from its own ring; the acting tick rides the critic's
+        # backward launch, before the gradient all-reduce); else sequential.
         ov = os.environ.get("SK_TICK_OVERLAP", "auto")
         fu = L.ddpg._fused
-        can = (not L.ddpg.multi() and fu is not None and updates_per_tick == 1 and L.replay.cap >= batch + 4 * n
-               and os.environ.get("SK_FUSED_REPLAY", "2") == "2")
+        multi = L.ddpg.multi()
+        can = (fu is not None and updates_per_tick == 1 and L.replay.cap >= batch + 4 * n
+               and os.environ.get("SK_FUSED_REPLAY", "2") == "2" and (not multi or L.ddpg.multi_rank == "grad"))
         can_fuse = (can and fu.f32 and getattr(L.actor_kernel, "fused_act_step", False) and n % 4 == 0
                     and os.environ.get("SK_FUSED_ACT", "1") != "0"
                     and fu.sliced(batch))
         if ov == "auto":
-            ov = "1" if n >= TICK_OVERLAP_MIN_ENVS else ("fused" if can_fuse else "0")
+            ov = "1" if n >= TICK_OVERLAP_MIN_ENVS and not multi else ("fused" if can_fuse else "0")
+        if multi and ov != "fused":
+            ov = "0"
         self.overlap = can and ov != "0" and (ov != "fused" or can_fuse)
         self.fuse_act = self.overlap and ov == "fused"
         self.side = (torch.cuda.Stream(device=dev) if self.overlap and ov not in ("serial", "fused") else None)

@@ -35,11 +35,11 @@ def nccl_group():
     dist.destroy_process_group()
 
 
-def _run(mode, multi_rank, force, precision):
+def _run(mode, multi_rank, force, precision, tick="0"):
     from skillshot_learning_amd.learner import SkillshotLearner
-    # the plain 1-rank tick would otherwise overlap its acting launches with
-    # the update (a different minibatch schedule from the multi-rank ticks)
-    os.environ["SK_TICK_OVERLAP"] = "0"
+    # one tick form for every run: the sequential one, or (multi_rank
+    # "grad", fp32) the fused overlapped one, which several ranks run too
+    os.environ["SK_TICK_OVERLAP"] = tick
     if mode:
         os.environ["SK_TICKGRAPH_MODE"] = mode
     else:
@@ -48,6 +48,7 @@ def _run(mode, multi_rank, force, precision):
                          replay_capacity=1 << 16, precision=precision, multi_rank=multi_rank,
                          force_collectives=force)
     tg = L.tick_graph(batch=256, ticks_per_graph=2, warmup=2)
+    assert tg.mode == ("fused" if tick == "fused" else "sequential")
     got_mode = tg.multi_rank_mode
     tg.run(4)
     torch.cuda.synchronize()
@@ -67,12 +68,13 @@ def _run(mode, multi_rank, force, precision):
     return got_mode, out
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
-@pytest.mark.parametrize("multi_rank", ["grad", "shared"])
-def test_full_capture_equals_segmented_and_plain(nccl_group, multi_rank, precision):
-    mode_f, full = _run("full", multi_rank, True, precision)
-    mode_s, seg = _run("segmented", multi_rank, True, precision)
-    mode_p, plain = _run(None, multi_rank, False, precision)
+@pytest.mark.parametrize("multi_rank,precision,tick", [("grad", "fp32", "0"), ("grad", "bf16", "0"),
+                                                       ("shared", "fp32", "0"), ("shared", "bf16", "0"),
+                                                       ("grad", "fp32", "fused")])
+def test_full_capture_equals_segmented_and_plain(nccl_group, multi_rank, precision, tick):
+    mode_f, full = _run("full", multi_rank, True, precision, tick)
+    mode_s, seg = _run("segmented", multi_rank, True, precision, tick)
+    mode_p, plain = _run(None, multi_rank, False, precision, tick)
     assert mode_f == f"{multi_rank}/full" and mode_s == f"{multi_rank}/segmented" and mode_p is None
     for k in full:
         assert torch.equal(full[k], seg[k]), f"full vs segmented: {k}"

@@ -10,5 +10,5 @@ python3 -c "
 import json; d = json.loads(open('gpurun_out/bench_2rank_gloo.json').read().strip().splitlines()[-1])
 print(d['value'] / 1e9, d['n_gpus'], d.get('errors'))
 for k, v in (d.get('learner') or {}).items():
-    if isinstance(v, dict): print(k, v.get('ms_per_tick'), v.get('capture_attempts'), v.get('multi_rank'))
+    if isinstance(v, dict): print(k, v.get('ms_per_tick'), v.get('capture_attempts'), v.get('multi_rank'), v.get('tick_mode'))
 "
