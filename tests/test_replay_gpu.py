@@ -368,3 +368,38 @@ def test_grad_step_job_equals_separate_launches(learner, monkeypatch, batch, noi
         for i, (u, v) in enumerate(zip(x, y)):
             assert torch.equal(u, v), (t, i)
     assert c1 == c2
+
+
+@pytest.mark.parametrize("exclude", [0, 300])
+def test_sampled_rows_equal_restated_ring_row(learner, exclude):
+    """the rows the critic launch gathers (ring_row, csrc/sk_mlp.hpp) against
+    a restatement on the host: Philox4x32-10 of (b, draw, count lo, count hi)
+    under the ring's seed (rng.philox4x32_10), u53 = (x << 32 | y) >> 11,
+    index = (u53 * size) >> 53, or with an exclusion E: the
+    min(count, cap - E) newest rows, (count - el + k) mod cap.  Row ids, bit
+    for bit, on a ring that wrapped twice"""
+    from skillshot_learning_amd.rng import philox4x32_10
+    cap, E, B = 1000, 300, 512
+    d = learner.DDPG("cuda", seed=1, gamma=0.0, replay_capacity=cap, precision="fp32")
+    ring = d.replay
+    for t in range(9):
+        ids = torch.arange(E, device="cuda", dtype=torch.float32) + E * t
+        ring.add_dev(ids[:, None].expand(E, 12).contiguous(), torch.zeros(E, 2, device="cuda"),
+                     torch.zeros(E, device="cuda"), torch.zeros(E, 12, device="cuda"), torch.zeros(E, device="cuda"))
+    count = int(ring.total_t)
+    draw = ring._draws
+    d._fused.critic_step_sampled(ring, B, total=torch.tensor(count, dtype=torch.int64, device="cuda"),
+                                 exclude=exclude)
+    got = ring._batch_bufs(B)[0][:, 0].long().cpu()
+    b = torch.arange(B, dtype=torch.int64)
+    x, y, _, _ = philox4x32_10(b, draw, count & 0xFFFFFFFF, count >> 32, ring.seed & 0xFFFFFFFF, ring.seed >> 32)
+    want = []
+    for xi, yi in zip(x.tolist(), y.tolist()):
+        u53 = ((xi << 32) | yi) >> 11
+        if exclude <= 0:
+            idx = (u53 * min(count, cap)) >> 53
+        else:
+            el = min(count, cap - exclude)
+            idx = (count - el + ((u53 * el) >> 53)) % cap
+        want.append(idx + cap * ((count - 1 - idx) // cap))  # the id the ring row holds (latest write)
+    assert got.tolist() == want
