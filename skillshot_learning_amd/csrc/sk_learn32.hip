@@ -1453,6 +1453,34 @@ __device__ __forceinline__ void normals4(uint64_t seed, uint64_t call, uint32_t 
   }
 }
 
+// 4 noisy pre-activations of rows r .. r+3 of unit `layer_unit`:
+// y = m + b + sd sqrt(b^2 + v) xi, the xi keyed as normals4's (the same
+// Philox counter, 24-bit uniforms, Box-Muller in revolutions) but in pair
+// form: sqrt((b^2 + v) L) with L = -2 ln(u1) sd^2 carries the radius, one
+// square root per element instead of the radius's plus the element's, and
+// Philox4x32 with SK_F32_NOISE_ROUNDS rounds (7: the fewest BigCrush-passing
+// rounds, as the bf16 path's noise; sk_mlp.hpp).  k2 = noise_k2(sd).
+#ifndef SK_F32_NOISE_ROUNDS
+#define SK_F32_NOISE_ROUNDS 7
+#endif
+template <typename V>
+__device__ __forceinline__ void noisy4(uint64_t seed, uint64_t call, uint32_t r, uint32_t layer_unit, float k2,
+                                       float b, const V& m, const V& v, int o, float y[4]) {
+  const uint4 u = skmlp::philox<SK_F32_NOISE_ROUNDS>(
+      make_uint4(r, layer_unit, (uint32_t)call, (uint32_t)(call >> 32)), (uint32_t)seed, (uint32_t)(seed >> 32));
+  const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const float u1 = ((float)(wd[2 * q] >> 8) + 0.5f) * 0x1p-24f;  // (0, 1)
+    const float u2 = (float)(wd[2 * q + 1] >> 8) * 0x1p-24f;       // [0, 1) revolutions
+    const float L = k2 * __builtin_amdgcn_logf(u1);                 // -2 ln(u1) sd^2
+    const float c = __builtin_amdgcn_cosf(u2), s = __builtin_amdgcn_sinf(u2);
+    y[2 * q] = __builtin_fmaf(__builtin_amdgcn_sqrtf(__builtin_fmaf(b, b, v[o + 2 * q]) * L), c, m[o + 2 * q] + b);
+    y[2 * q + 1] =
+        __builtin_fmaf(__builtin_amdgcn_sqrtf(__builtin_fmaf(b, b, v[o + 2 * q + 1]) * L), s, m[o + 2 * q + 1] + b);
+  }
+}
+
 // Row maps of a 32-row actor tile: local row i -> global row of the [rows]
 // batch, and whether it exists.  Contiguous: rows row0 .. row0 + 31.
 // Players (the self-play tick, k_act_step32): games g0 .. g0 + 15, rows
@@ -1501,16 +1529,13 @@ __device__ __forceinline__ void actor_tile32(const Net& A, const float* __restri
     const float b = A.b1[u];
     if (NOISE) {
       const f32x16 var = gemm_l1<true>(S, A.W1, 32 * nt, lane);
+      const float k2 = skmlp::noise_k2(sd);
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        float z[4];
-        normals4(seed, call, (uint32_t)R(drow(4 * g, lane)), (uint32_t)u, z);
+        float y[4];
+        noisy4(seed, call, (uint32_t)R(drow(4 * g, lane)), (uint32_t)u, k2, b, m, var, 4 * g, y);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int v = 4 * g + q;
-          const float y = __builtin_fmaf(sd * __builtin_amdgcn_sqrtf(__builtin_fmaf(b, b, var[v])), z[q], m[v] + b);
-          H1[drow(v, lane) * kLdH1 + u] = fmaxf(y, 0.f);
-        }
+        for (int q = 0; q < 4; ++q) H1[drow(4 * g + q, lane) * kLdH1 + u] = fmaxf(y[q], 0.f);
       }
     } else {
 #pragma unroll
@@ -1526,16 +1551,13 @@ __device__ __forceinline__ void actor_tile32(const Net& A, const float* __restri
     else m = gemm_xwT(m, H1, kLdH1, A.W2, kALd, 32 * w, 0, kH1, lane);
     const float b = A.b2[u];
     if (NOISE) {
+      const float k2 = skmlp::noise_k2(sd);
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        float z[4];
-        normals4(seed, call, (uint32_t)R(drow(4 * g, lane)), (uint32_t)(kH1 + u), z);
+        float y[4];
+        noisy4(seed, call, (uint32_t)R(drow(4 * g, lane)), (uint32_t)(kH1 + u), k2, b, m, var, 4 * g, y);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int v = 4 * g + q;
-          const float y = __builtin_fmaf(sd * __builtin_amdgcn_sqrtf(__builtin_fmaf(b, b, var[v])), z[q], m[v] + b);
-          H2[drow(v, lane) * kLdH2 + u] = fmaxf(y, 0.f);
-        }
+        for (int q = 0; q < 4; ++q) H2[drow(4 * g + q, lane) * kLdH2 + u] = fmaxf(y[q], 0.f);
       }
     } else {
 #pragma unroll
@@ -1759,13 +1781,10 @@ __global__ void __launch_bounds__(kFwdThreads) k_actor_fwd16(const float* __rest
     const float b = b1v[q];
     if (NOISE) {
       const f32x4 var = m16x4(x * x, w1v[q] * w1v[q], z4);
-      float z[4];
-      normals4(seed, call, (uint32_t)(row0 + 4 * g), (uint32_t)u, z);
+      float y[4];
+      noisy4(seed, call, (uint32_t)(row0 + 4 * g), (uint32_t)u, skmlp::noise_k2(sd), b, m, var, 0, y);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float y = __builtin_fmaf(sd * __builtin_amdgcn_sqrtf(__builtin_fmaf(b, b, var[r])), z[r], m[r] + b);
-        H1[(4 * g + r) * kLdH1 + u] = fmaxf(y, 0.f);
-      }
+      for (int r = 0; r < 4; ++r) H1[(4 * g + r) * kLdH1 + u] = fmaxf(y[r], 0.f);
     } else {
 #pragma unroll
       for (int r = 0; r < 4; ++r) H1[(4 * g + r) * kLdH1 + u] = fmaxf(m[r] + b, 0.f);
@@ -1785,12 +1804,11 @@ __global__ void __launch_bounds__(kFwdThreads) k_actor_fwd16(const float* __rest
     } else {
       m = g16_xwT256(H1, kLdH1, A.W2, kALd, 16 * nt, lane);
     }
-    float z[4];
-    if (NOISE) normals4(seed, call, (uint32_t)(row0 + 4 * g), (uint32_t)(kH1 + u), z);
+    float yn[4];
+    if (NOISE) noisy4(seed, call, (uint32_t)(row0 + 4 * g), (uint32_t)(kH1 + u), skmlp::noise_k2(sd), b2v[t], m, var, 0, yn);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      float y = m[r] + b2v[t];
-      if (NOISE) y = __builtin_fmaf(sd * __builtin_amdgcn_sqrtf(__builtin_fmaf(b2v[t], b2v[t], var[r])), z[r], y);
+      const float y = NOISE ? yn[r] : m[r] + b2v[t];
       const float h = fmaxf(y, 0.f);
       pm0[r] += h * w30[t];
       pm1[r] += h * w31[t];
