@@ -383,6 +383,12 @@ int sk_replay_insert(float* ring, int64_t capacity, int64_t* total, uint32_t* ar
                      int64_t n_games, int64_t rows, void* stream);
 int sk_replay_sample(const float* ring, int64_t capacity, const int64_t* total, uint64_t seed, int32_t draw,
                      int64_t batch, float* s, float* a, float* r, float* s2, float* d, void* stream);
+/* sk_replay_sample drawing only from the min(*total, capacity - exclude)
+ * newest rows (ABI 8; 0 <= exclude < capacity): never a row an insert of
+ * `exclude` rows after *total writes (sk_ring_sample.exclude's rule). */
+int sk_replay_sample_excl(const float* ring, int64_t capacity, const int64_t* total, uint64_t seed, int32_t draw,
+                          int64_t batch, float* s, float* a, float* r, float* s2, float* d, int64_t exclude,
+                          void* stream);
 /* sk_replay_insert followed by sk_replay_sample in ONE launch, bit for bit
  * (same draw, key and range as a sample after the insert): a sampled row the
  * launch is inserting is read from the insert's sources.  The learner tick's
@@ -592,6 +598,16 @@ int sk_actor_grad_f32_step(const float* actor_flat, const float* critic_flat, co
  * acting tick's insert: give q->exclude = the insert's rows).  Results equal,
  * bit for bit, sk_critic_grad_f32_sampled followed by the job's
  * sk_env_act_step. */
+/* sk_critic_grad_f32 with a prepared acting tick run in its backward
+ * launch (ABI 8; the multi-rank shared-replay tick, whose minibatch is drawn
+ * and all-gathered before): equal, bit for bit, to sk_critic_grad_f32 then the
+ * job's sk_env_act_step. */
+int sk_critic_grad_f32_step(const float* critic_flat, const float* obs, const float* actions, const float* targets,
+                            const float* next_obs, const float* rewards, const float* done, float gamma,
+                            const float* target_actor_flat, const float* target_critic_flat, int64_t batch,
+                            int64_t row_offset, float grad_scale, uint64_t seed, const int64_t* call_counter,
+                            float* partials, float* step_counters, int32_t n_steps, float* loss_sum,
+                            uint8_t* dropout_mask, float* scratch, const sk_step_job* job, void* stream);
 int sk_critic_grad_f32_sampled_step(const float* critic_flat, const sk_ring_sample* q, float gamma,
                                     const float* target_actor_flat, const float* target_critic_flat, int64_t batch,
                                     int64_t row_offset, float grad_scale, uint64_t seed,

@@ -35,7 +35,7 @@ EXPORTS = (
     "sk_critic_grad_bootstrap",
     "sk_update_partials_f32", "sk_actor_forward_f32", "sk_critic_grad_f32", "sk_critic_grad_f32_sampled",
     "sk_critic_grad_bootstrap_sampled", "sk_actor_grad_f32", "sk_actor_grad_f32_step",
-    "sk_critic_grad_f32_sampled_step",
+    "sk_critic_grad_f32_sampled_step", "sk_critic_grad_f32_step", "sk_replay_sample_excl",
 )
 
 
@@ -147,6 +147,7 @@ def load(build_if_missing=True):
         "sk_target_y": ([P, P, P, P, P, f32, P, i64, P], ctypes.c_int),
         "sk_replay_insert": ([P, i64, P, P, P, P, P, P, P, i64, i64, P], ctypes.c_int),
         "sk_replay_sample": ([P, i64, P, u64, i32, i64, P, P, P, P, P, P], ctypes.c_int),
+        "sk_replay_sample_excl": ([P, i64, P, u64, i32, i64, P, P, P, P, P, i64, P], ctypes.c_int),
         "sk_replay_insert_sample": ([P, i64, P, P, P, P, P, P, P, i64, i64, u64, i32, i64, P, P, P, P, P, P],
                                     ctypes.c_int),
         "sk_grad_pack_flat": ([P, P, P, P, i32, P], ctypes.c_int),
@@ -158,6 +159,8 @@ def load(build_if_missing=True):
                                ctypes.c_int),
         "sk_critic_grad_f32_sampled": ([P, P, f32, P, P, i64, i64, f32, u64, P, P, P, i32, P, P, P, P],
                                        ctypes.c_int),
+        "sk_critic_grad_f32_step": ([P, P, P, P, P, P, P, f32, P, P, i64, i64, f32, u64, P, P, P, i32, P, P, P,
+                                     ctypes.POINTER(SkStepJob), P], ctypes.c_int),
         "sk_critic_grad_f32_sampled_step": ([P, P, f32, P, P, i64, i64, f32, u64, P, P, P, i32, P, P, P,
                                              ctypes.POINTER(SkStepJob), P], ctypes.c_int),
         "sk_critic_grad_bootstrap_sampled": ([P, P, f32, P, P, i64, i64, f32, u64, P, P, P, i32, P, P, P],

@@ -1962,12 +1962,12 @@ int64_t sk_update_partials_f32(int64_t batch) {
   return ((batch + kR - 1) / kR + spw - 1) / spw;
 }
 
-int sk_critic_grad_f32(const float* critic_flat, const float* obs, const float* actions, const float* targets,
-                       const float* next_obs, const float* rewards, const float* done, float gamma,
-                       const float* target_actor_flat, const float* target_critic_flat, int64_t batch,
-                       int64_t row_offset, float grad_scale, uint64_t seed, const int64_t* call_counter,
-                       float* partials, float* step_counters, int32_t n_steps, float* loss_sum,
-                       uint8_t* dropout_mask, float* scratch, void* stream) {
+static int critic_f32(const float* critic_flat, const float* obs, const float* actions, const float* targets,
+                      const float* next_obs, const float* rewards, const float* done, float gamma,
+                      const float* target_actor_flat, const float* target_critic_flat, int64_t batch,
+                      int64_t row_offset, float grad_scale, uint64_t seed, const int64_t* call_counter,
+                      float* partials, float* step_counters, int32_t n_steps, float* loss_sum,
+                      uint8_t* dropout_mask, float* scratch, const sk::ActStepJob* job, void* stream) {
   const bool boot = target_actor_flat != nullptr;
   if (boot && (!target_critic_flat || !next_obs || !rewards || !done)) return SK_EINVAL;
   if (!boot && !targets) return SK_EINVAL;
@@ -1981,10 +1981,11 @@ int sk_critic_grad_f32(const float* critic_flat, const float* obs, const float* 
       return launch_sliced<kSlCriticBoot>(critic_flat, target_actor_flat, target_critic_flat, obs, next_obs, actions,
                                           nullptr, rewards, done, gamma, batch, row_offset, grad_scale, seed,
                                           call_counter, partials, scratch, w1_rows, step_counters, n_steps, loss_sum,
-                                          dropout_mask, (hipStream_t)stream);
+                                          dropout_mask, (hipStream_t)stream, RingSample{}, job);
     return launch_sliced<kSlCriticY>(critic_flat, nullptr, nullptr, obs, nullptr, actions, targets, nullptr, nullptr,
                                      0.f, batch, row_offset, grad_scale, seed, call_counter, partials, scratch,
-                                     w1_rows, step_counters, n_steps, loss_sum, dropout_mask, (hipStream_t)stream);
+                                     w1_rows, step_counters, n_steps, loss_sum, dropout_mask, (hipStream_t)stream,
+                                     RingSample{}, job);
   }
   static bool attr = false;
   if (!attr) {
@@ -1999,7 +2000,36 @@ int sk_critic_grad_f32(const float* critic_flat, const float* obs, const float* 
       critic_flat, obs, actions, targets, batch, row_offset, (int)spw, grad_scale, seed, call_counter, partials,
       step_counters, n_steps, loss_sum, dropout_mask, next_obs, rewards, done, gamma, target_actor_flat,
       target_critic_flat);
-  return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
+  if (hipGetLastError() != hipSuccess) return SK_EHIP;
+  if (!job) return SK_OK;
+  return sk_launch_act_step32(job->aflat, job->act_out, job->sd, job->action_sd, job->seed, job->call_ctr, job->a,
+                              job->c, (hipStream_t)stream);
+}
+
+int sk_critic_grad_f32(const float* critic_flat, const float* obs, const float* actions, const float* targets,
+                       const float* next_obs, const float* rewards, const float* done, float gamma,
+                       const float* target_actor_flat, const float* target_critic_flat, int64_t batch,
+                       int64_t row_offset, float grad_scale, uint64_t seed, const int64_t* call_counter,
+                       float* partials, float* step_counters, int32_t n_steps, float* loss_sum,
+                       uint8_t* dropout_mask, float* scratch, void* stream) {
+  return critic_f32(critic_flat, obs, actions, targets, next_obs, rewards, done, gamma, target_actor_flat,
+                    target_critic_flat, batch, row_offset, grad_scale, seed, call_counter, partials, step_counters,
+                    n_steps, loss_sum, dropout_mask, scratch, nullptr, stream);
+}
+
+int sk_critic_grad_f32_step(const float* critic_flat, const float* obs, const float* actions, const float* targets,
+                            const float* next_obs, const float* rewards, const float* done, float gamma,
+                            const float* target_actor_flat, const float* target_critic_flat, int64_t batch,
+                            int64_t row_offset, float grad_scale, uint64_t seed, const int64_t* call_counter,
+                            float* partials, float* step_counters, int32_t n_steps, float* loss_sum,
+                            uint8_t* dropout_mask, float* scratch, const sk_step_job* job, void* stream) {
+  if (!job) return SK_EINVAL;
+  sk::ActStepJob j;
+  std::memcpy(&j, job, sizeof(j));
+  if (j.magic != sk::kActStepJobMagic) return SK_EINVAL;
+  return critic_f32(critic_flat, obs, actions, targets, next_obs, rewards, done, gamma, target_actor_flat,
+                    target_critic_flat, batch, row_offset, grad_scale, seed, call_counter, partials, step_counters,
+                    n_steps, loss_sum, dropout_mask, scratch, &j, stream);
 }
 
 static int critic_sampled(const float* critic_flat, const sk_ring_sample* q, float gamma,

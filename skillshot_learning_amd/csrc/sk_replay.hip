@@ -213,12 +213,19 @@ int sk_replay_insert(float* ring, int64_t capacity, int64_t* total, uint32_t* ar
 
 int sk_replay_sample(const float* ring, int64_t capacity, const int64_t* total, uint64_t seed, int32_t draw,
                      int64_t batch, float* s, float* a, float* r, float* s2, float* d, void* stream) {
+  return sk_replay_sample_excl(ring, capacity, total, seed, draw, batch, s, a, r, s2, d, 0, stream);
+}
+
+int sk_replay_sample_excl(const float* ring, int64_t capacity, const int64_t* total, uint64_t seed, int32_t draw,
+                          int64_t batch, float* s, float* a, float* r, float* s2, float* d, int64_t exclude,
+                          void* stream) {
   if (!ring || !total || !s || !a || !r || !s2 || !d || capacity <= 0 || batch <= 0) return SK_EINVAL;
+  if (exclude < 0 || exclude >= capacity) return SK_EINVAL;
   if ((((uintptr_t)ring) & 15) || (((uintptr_t)s) & 15) || (((uintptr_t)s2) & 15) || (((uintptr_t)a) & 7))
     return SK_EINVAL;
   const unsigned grid = (unsigned)((batch + kThreads - 1) / kThreads);
   k_replay_sample<<<grid, kThreads, 0, (hipStream_t)stream>>>(ring, capacity, total, seed, draw, batch, s, a, r, s2,
-                                                              d, 0);
+                                                              d, exclude);
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
 }
 

@@ -362,18 +362,21 @@ class ReplayRing:
         self._draws = (self._draws + 1) & 0x7FFFFFFF
         return self._batch_bufs(b), draw
 
-    def sample_dev(self, b, generator=None):
-        """Capturable uniform sample over the device-side size."""
+    def sample_dev(self, b, generator=None, exclude=0):
+        """Capturable uniform sample over the device-side size (exclude > 0:
+        over the min(count, cap - exclude) newest rows, sk_replay_sample_excl)."""
         if self._k is not None:
             from . import _capi
             out = self._batch_bufs(b)
             p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
             draw = self._draws
             self._draws = (self._draws + 1) & 0x7FFFFFFF
-            _capi.check(self._k.sk_replay_sample(
-                p(self.buf), self.cap, p(self.total_t), self.seed, draw, b, *[p(t) for t in out],
+            _capi.check(self._k.sk_replay_sample_excl(
+                p(self.buf), self.cap, p(self.total_t), self.seed, draw, b, *[p(t) for t in out], int(exclude),
                 ctypes.c_void_p(torch.cuda.current_stream(self.buf.device).cuda_stream)))
             return out
+        if exclude:
+            raise ValueError("exclude needs the device ring")
         u = torch.rand(b, dtype=torch.float64, device=self.buf.device, generator=generator)
         size_t = self.size_t
         idx = torch.minimum((u * size_t).long(), size_t - 1)
@@ -606,6 +609,19 @@ class DDPG:
         w, rk, b = self.world(), self.rank(), int(batch)
         if w > 1 and b % 4:
             raise ValueError("multi-rank batches must be a multiple of 4 rows (Dropout key groups)")
+        if self.multi() and self.multi_rank == "shared":
+            # the shared replay: this rank's rows drawn as at `total` (the
+            # stream-ordered count: the acting launch runs after this), the
+            # ranks' rows all-gathered, the strided slice rk::w stepped
+            s, a, r, s2, d = self.replay.sample_dev(b, exclude=exclude)
+            s, a, r, s2, d = [t[rk::w] for t in self._allgather_batch(s, a, r, s2, d)]
+            cj = step_job if job_in == "critic" else None
+            if self.gamma > 0.0:
+                lc = fu.critic_step(s, a, s2=s2, r=r, d=d, gamma=self.gamma, row_offset=rk * b, global_batch=w * b,
+                                    step_job=cj)
+            else:
+                lc = fu.critic_step(s, a, r, row_offset=rk * b, global_batch=w * b, step_job=cj)
+            return lc, fu.actor_step(s, before_adam=before_actor_adam, step_job=None if cj is not None else step_job)
         cj = step_job if job_in == "critic" else None
         lc, (s, _, _, _, _) = fu.critic_step_sampled(self.replay, b, gamma=self.gamma, row_offset=rk * b,
                                                      global_batch=w * b, total=total, exclude=exclude, step_job=cj)
@@ -1032,14 +1048,15 @@ class TickGraph:
         # (sk_actor_grad_f32_step; _tick_fused); SK_TICK_OVERLAP=serial: the
         # same tick with plain launches on one stream (the check that neither
         # form races).
-        # Several ranks: the fused form with multi_rank "grad" (config 4: each
-        # rank draws from its own ring; the acting tick rides the critic's
-        # backward launch, before the gradient all-reduce); else sequential.
+        # Several ranks: the fused form (config 4, multi_rank "grad": each
+        # rank draws from its own ring; config 5, "shared": the drawn rows are
+        # all-gathered first; the acting tick rides the critic's backward
+        # launch, before the gradient all-reduce); else sequential.
         ov = os.environ.get("SK_TICK_OVERLAP", "auto")
         fu = L.ddpg._fused
         multi = L.ddpg.multi()
         can = (fu is not None and updates_per_tick == 1 and L.replay.cap >= batch + 4 * n
-               and os.environ.get("SK_FUSED_REPLAY", "2") == "2" and (not multi or L.ddpg.multi_rank == "grad"))
+               and os.environ.get("SK_FUSED_REPLAY", "2") == "2")
         can_fuse = (can and fu.f32 and getattr(L.actor_kernel, "fused_act_step", False) and n % 4 == 0
                     and os.environ.get("SK_FUSED_ACT", "1") != "0"
                     and fu.sliced(batch))

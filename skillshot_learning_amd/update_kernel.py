@@ -277,19 +277,24 @@ class FusedUpdate:
 
     @torch.no_grad()
     def critic_step(self, s, a, target=None, mask_out=None, s2=None, r=None, d=None, gamma=0.0, row_offset=0,
-                    global_batch=None):
+                    global_batch=None, step_job=None):
         """One critic Adam step on MSE(Q(s, a), y), Dropout active; y = target,
         or, given s2 / r / d, the bootstrap y = r + gamma (1 - d) Q'(s2,
         mu'(s2)) computed inside the same launch from the target nets.  The
         rows are global batch rows row_offset .. (their Dropout keys) of a
         global batch of global_batch rows (the loss normaliser; default this
-        batch).  Returns the loss (device scalar; this rank's share)."""
+        batch).  step_job (fp32): a prepared acting launch run in the
+        gradient's backward launch (sk_critic_grad_f32_step).  Returns the
+        loss (device scalar; this rank's share)."""
         s, a = s.float().contiguous(), a.float().contiguous()
         B = s.shape[0]
         gb = B if global_batch is None else int(global_batch)
         part = self._partial(B, self.fc.numel())
         st = self.sc
-        rc = self._critic_grad(s, a, target, s2, r, d, gamma, row_offset, gb, part, st.steps, mask_out)
+        if step_job is not None and not self.f32:
+            raise ValueError("step_job needs the fp32 kernels")
+        rc = self._critic_grad(s, a, target, s2, r, d, gamma, row_offset, gb, part, st.steps, mask_out,
+                               step_job=step_job)
         _capi.check(rc)
         loss = self._loss_slot(0)
         self._adam(part, self.fc, st, self.tc, stat=self.stats[0:1], scale=1.0 / gb, out=loss, counter=self.calls,
@@ -338,7 +343,8 @@ class FusedUpdate:
                    packs=self._packs(critic=True))
         return loss, out
 
-    def _critic_grad(self, s, a, target, s2, r, d, gamma, row_offset, gb, part, steps, mask_out, stat=True):
+    def _critic_grad(self, s, a, target, s2, r, d, gamma, row_offset, gb, part, steps, mask_out, stat=True,
+                     step_job=None):
         n_steps = steps.numel() if steps is not None else 0
         statp = _p(self.stats[0:1]) if stat else None
         if self.f32:
@@ -349,10 +355,12 @@ class FusedUpdate:
             rc_ = r.float().contiguous() if boot else None
             dc = d.float().contiguous() if boot else None
             y = None if boot else target.float().contiguous()
-            return self.L.sk_critic_grad_f32(
-                _p(self.fc), _p(s), _p(a), _p(y), _p(s2c), _p(rc_), _p(dc), float(gamma), _p(ta), _p(tc), s.shape[0],
-                int(row_offset), 2.0 / gb, self.seed, _p(self.calls), _p(part.main), _p(steps), n_steps, statp,
-                _p(mask_out), _p(part.scratch), self._stream())
+            args = (_p(self.fc), _p(s), _p(a), _p(y), _p(s2c), _p(rc_), _p(dc), float(gamma), _p(ta), _p(tc),
+                    s.shape[0], int(row_offset), 2.0 / gb, self.seed, _p(self.calls), _p(part.main), _p(steps),
+                    n_steps, statp, _p(mask_out), _p(part.scratch))
+            if step_job is not None:
+                return self.L.sk_critic_grad_f32_step(*args, ctypes.byref(step_job), self._stream())
+            return self.L.sk_critic_grad_f32(*args, self._stream())
         if s2 is not None:
             s2c, rc_, dc = s2.float().contiguous(), r.float().contiguous(), d.float().contiguous()
             return self.L.sk_critic_grad_bootstrap(

@@ -33,8 +33,8 @@ def _worker(rank, world, port, mode, precision, q):
                              gamma=0.9, tau=0.05, replay_capacity=1 << 14, multi_rank=mode, precision=precision)
         tg = L.tick_graph(batch=64, ticks_per_graph=2, warmup=2)
         assert tg.multi_rank_mode == f"{mode}/segmented"
-        # "grad" at fp32 runs the fused overlapped tick on every rank
-        assert tg.mode == ("fused" if mode == "grad" and precision == "fp32" else "sequential")
+        # fp32 runs the fused overlapped tick on every rank
+        assert tg.mode == ("fused" if precision == "fp32" else "sequential")
         tg.run(4)
         torch.cuda.synchronize()
         flat = torch.cat([p.detach().reshape(-1) for m in (L.model_actor, L.model_critic, L.ddpg.target_actor,
@@ -49,7 +49,7 @@ def _worker(rank, world, port, mode, precision, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode,precision", [("grad", "fp32"), ("shared", "bf16")])
+@pytest.mark.parametrize("mode,precision", [("grad", "fp32"), ("shared", "bf16"), ("shared", "fp32")])
 def test_two_rank_tick_graph_gloo(mode, precision):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")

@@ -37,8 +37,8 @@ def nccl_group():
 
 def _run(mode, multi_rank, force, precision, tick="0"):
     from skillshot_learning_amd.learner import SkillshotLearner
-    # one tick form for every run: the sequential one, or (multi_rank
-    # "grad", fp32) the fused overlapped one, which several ranks run too
+    # one tick form for every run: the sequential one, or (fp32) the fused
+    # overlapped one, which several ranks run too
     os.environ["SK_TICK_OVERLAP"] = tick
     if mode:
         os.environ["SK_TICKGRAPH_MODE"] = mode
@@ -70,7 +70,7 @@ def _run(mode, multi_rank, force, precision, tick="0"):
 
 @pytest.mark.parametrize("multi_rank,precision,tick", [("grad", "fp32", "0"), ("grad", "bf16", "0"),
                                                        ("shared", "fp32", "0"), ("shared", "bf16", "0"),
-                                                       ("grad", "fp32", "fused")])
+                                                       ("grad", "fp32", "fused"), ("shared", "fp32", "fused")])
 def test_full_capture_equals_segmented_and_plain(nccl_group, multi_rank, precision, tick):
     mode_f, full = _run("full", multi_rank, True, precision, tick)
     mode_s, seg = _run("segmented", multi_rank, True, precision, tick)
