@@ -99,8 +99,8 @@ static constexpr int64_t kSplitMultiMaxEnvs = 32768;  // k_step: restart draw un
 // SK_CTR_STRIDE slots per wave of the widest step grid (k_step_split: two
 // lanes per game), at least SK_COUNTER_SLOTS
 static inline int64_t counter_slots(int64_t n) {
-  // k_act_step32 counts one line per 16-game workgroup
-  const int64_t w2 = (2 * n + 63) / 64, w16 = (n + 15) / 16, waves = w2 > w16 ? w2 : w16;
+  // k_act_step32 / k_act_step16 count one line per 16- / 8-game workgroup
+  const int64_t w2 = (2 * n + 63) / 64, w8 = (n + 7) / 8, waves = w2 > w8 ? w2 : w8;
   return waves * SK_CTR_STRIDE > SK_COUNTER_SLOTS ? waves * SK_CTR_STRIDE : SK_COUNTER_SLOTS;
 }
 static inline size_t aux_bytes(int64_t n) { return 256 + (size_t)counter_slots(n) * sizeof(sk_counters); }

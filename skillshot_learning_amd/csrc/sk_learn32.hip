@@ -1690,40 +1690,6 @@ __global__ void __launch_bounds__(kFwdThreads) k_act_step32(const float* __restr
                     gridDim.x);
 }
 
-// A gradient step's backward launch with the next acting tick beside it
-// (the fused overlapped learner tick: sk_critic_grad_f32_sampled_step carries
-// it in the critic's backward, sk_actor_grad_f32_step in the actor's):
-// workgroups [0, GA) run act_step32 (k_act_step32's 16 games each), the rest
-// grad_slice_bwd<MODE> (k_grad_slice_bwd's workgroup blockIdx - GA).  The
-// two share no data: the backward reads the minibatch, the nets and the
-// forward's z2; the acting half reads the actor and the observations and
-// writes the env, the actions and the ring (the minibatch was gathered
-// before, excluding the rows this insert writes).  LDS is the larger of the
-// two layouts: two workgroups per CU (the critic's 81,616 B twice fill the
-// CU's 160 KiB).
-constexpr size_t bwd_act_lds(int mode) {
-  return kActStepLds > sl_bwd_lds(mode) ? kActStepLds : sl_bwd_lds(mode);
-}
-static_assert(2 * bwd_act_lds(kSlCriticBoot) <= 160 * 1024 && 2 * bwd_act_lds(kSlActor) <= 160 * 1024,
-              "two fused workgroups per CU");
-static_assert(kSlThreads == kFwdThreads, "one workgroup size for both halves");
-template <int MODE, bool NOISE>
-__global__ void __launch_bounds__(kFwdThreads) k_bwd_act_step32(SK_SLICE_BWD_PARAMS, unsigned GA,
-                                                                const float* __restrict__ aflat,
-                                                                float* __restrict__ act_out, float sd, float action_sd,
-                                                                uint64_t aseed, uint64_t* __restrict__ acall_ctr,
-                                                                sk::StepArgs a, sk::Cfg c) {
-  extern __shared__ __attribute__((aligned(16))) float smem_sl[];
-  if (blockIdx.x < GA) {
-    float* S = smem_sl;
-    float* H1 = S + 32 * kLdS;
-    float* H2 = H1 + 32 * kLdH1;
-    act_step32<NOISE>(aflat, act_out, sd, action_sd, aseed, acall_ctr, a, c, S, H1, H2, (float2*)(H2 + 32 * kLdH2),
-                      GA);
-  } else {
-    grad_slice_bwd<MODE>((int)(blockIdx.x - GA), smem_sl, SK_SLICE_BWD_ARGS);
-  }
-}
 
 // ---------------------------------------------------------------- actor forward, 16-row tiles
 // The same forward for small row counts: a 32-row tile is a serial chain of
@@ -1736,24 +1702,23 @@ __global__ void __launch_bounds__(kFwdThreads) k_bwd_act_step32(SK_SLICE_BWD_PAR
 // and w + 4; layer 3 from DPP row sums of the layer-2 tiles.  The noise draws
 // are keyed exactly as k_actor_fwd32's: normals4 per (first row of a 4-row
 // group, unit), z[r] for row + r.
-template <bool NOISE>
-__global__ void __launch_bounds__(kFwdThreads) k_actor_fwd16(const float* __restrict__ aflat,
-                                                             const float* __restrict__ X, float* __restrict__ out,
-                                                             int64_t rows, float sd, float action_sd, uint64_t seed,
-                                                             uint64_t* __restrict__ call_ctr) {
-  __shared__ __attribute__((aligned(16))) float S[kR * kLdS16];
-  __shared__ __attribute__((aligned(16))) float H1[kR * kLdH1];
-  __shared__ __attribute__((aligned(16))) f4 MP[4][kR];  // per wave and row: {m0, m1, v0, v1} of layer 3
+// The 16-row tile on the LDS at S / H1 / MP (kActorTile16Lds bytes) for the
+// row map R (local row i -> global row; noise keyed by the global first row of
+// each aligned 4-row group, so with N % 4 == 0 the players' map draws what
+// the contiguous map draws).  k_actor_fwd16 (contiguous rows) and
+// k_act_step16 (8 games: rows g0 .. g0 + 7 and N + g0 .. N + g0 + 7, the
+// actions also into act_lds) run it.
+constexpr size_t kActorTile16Lds = (size_t)(kR * kLdS16 + kR * kLdH1) * 4 + 4 * kR * sizeof(f4);
+template <bool NOISE, typename MAP>
+__device__ __forceinline__ void actor_tile16(const Net& A, const float* __restrict__ X, float* __restrict__ out,
+                                             const MAP& R, float sd, float action_sd, uint64_t seed, uint64_t call,
+                                             float* S, float* H1, f4 (*MP)[kR], float2* act_lds) {
   const int tid = threadIdx.x, lane = tid & 63, i = lane & 15, g = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const Net A = net_of(aflat, kALd, 2);
-  const int64_t row0 = (int64_t)blockIdx.x * kR;
-  const bool draws = (NOISE || action_sd != 0.f) && call_ctr;
-  const uint64_t call = draws ? call_ctr[0] + 1 : 0;
   // ---- every load ahead of the barrier: states, layer-1 fragments and biases, the
   // first layer-2 fragments (g16_xwT256's prefetch), W3 / b2 of the wave's units
   const int si = tid >> 4, sk = tid & 15;
-  const float sv = sk < kIn && row0 + si < rows ? X[(row0 + si) * kIn + sk] : 0.f;
+  const float sv = sk < kIn && R.valid(si) ? X[R(si) * kIn + sk] : 0.f;
   f4 w1v[4];
   float b1v[4];
 #pragma unroll
@@ -1782,7 +1747,7 @@ __global__ void __launch_bounds__(kFwdThreads) k_actor_fwd16(const float* __rest
     if (NOISE) {
       const f32x4 var = m16x4(x * x, w1v[q] * w1v[q], z4);
       float y[4];
-      noisy4(seed, call, (uint32_t)(row0 + 4 * g), (uint32_t)u, skmlp::noise_k2(sd), b, m, var, 0, y);
+      noisy4(seed, call, (uint32_t)R(4 * g), (uint32_t)u, skmlp::noise_k2(sd), b, m, var, 0, y);
 #pragma unroll
       for (int r = 0; r < 4; ++r) H1[(4 * g + r) * kLdH1 + u] = fmaxf(y[r], 0.f);
     } else {
@@ -1805,7 +1770,7 @@ __global__ void __launch_bounds__(kFwdThreads) k_actor_fwd16(const float* __rest
       m = g16_xwT256(H1, kLdH1, A.W2, kALd, 16 * nt, lane);
     }
     float yn[4];
-    if (NOISE) noisy4(seed, call, (uint32_t)(row0 + 4 * g), (uint32_t)(kH1 + u), skmlp::noise_k2(sd), b2v[t], m, var, 0, yn);
+    if (NOISE) noisy4(seed, call, (uint32_t)R(4 * g), (uint32_t)(kH1 + u), skmlp::noise_k2(sd), b2v[t], m, var, 0, yn);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float y = NOISE ? yn[r] : m[r] + b2v[t];
@@ -1825,28 +1790,132 @@ __global__ void __launch_bounds__(kFwdThreads) k_actor_fwd16(const float* __rest
   }
   lds_sync32();
   // ---- layer 3, tanh, action noise: one thread per row
-  if (tid < kR && row0 + tid < rows) {
+  if (tid < kR && R.valid(tid)) {
+    const int64_t row = R(tid);
     const f4 v = (MP[0][tid] + MP[1][tid]) + (MP[2][tid] + MP[3][tid]);
     const float b30 = A.b3[0], b31 = A.b3[1];
     float y0 = v.x + b30, y1 = v.y + b31;
     if (NOISE) {
       float z[4];
-      normals4(seed, call, (uint32_t)(row0 + tid), (uint32_t)(kH1 + kH2), z);
+      normals4(seed, call, (uint32_t)row, (uint32_t)(kH1 + kH2), z);
       y0 += sd * __builtin_amdgcn_sqrtf(v.z + b30 * b30) * z[0];
       y1 += sd * __builtin_amdgcn_sqrtf(v.w + b31 * b31) * z[1];
     }
     float o0 = tanhf(y0), o1 = tanhf(y1);
     if (action_sd != 0.f) {
       float z[4];
-      normals4(seed, call, (uint32_t)(row0 + tid), (uint32_t)(kH1 + kH2 + 1), z);
+      normals4(seed, call, (uint32_t)row, (uint32_t)(kH1 + kH2 + 1), z);
       o0 += action_sd * z[0];
       o1 += action_sd * z[1];
     }
-    *(float2*)(out + (row0 + tid) * 2) = make_float2(o0, o1);
+    *(float2*)(out + row * 2) = make_float2(o0, o1);
+    if (act_lds) act_lds[tid] = make_float2(o0, o1);
   }
+}
+
+template <bool NOISE>
+__global__ void __launch_bounds__(kFwdThreads) k_actor_fwd16(const float* __restrict__ aflat,
+                                                             const float* __restrict__ X, float* __restrict__ out,
+                                                             int64_t rows, float sd, float action_sd, uint64_t seed,
+                                                             uint64_t* __restrict__ call_ctr) {
+  __shared__ __attribute__((aligned(16))) float S[kR * kLdS16];
+  __shared__ __attribute__((aligned(16))) float H1[kR * kLdH1];
+  __shared__ __attribute__((aligned(16))) f4 MP[4][kR];  // per wave and row: {m0, m1, v0, v1} of layer 3
+  const Net A = net_of(aflat, kALd, 2);
+  const bool draws = (NOISE || action_sd != 0.f) && call_ctr;
+  const uint64_t call = draws ? call_ctr[0] + 1 : 0;
+  actor_tile16<NOISE>(A, X, out, RowsContig{(int64_t)blockIdx.x * kR, rows}, sd, action_sd, seed, call, S, H1, MP,
+                      nullptr);
   if (draws) {
     __syncthreads();
     advance_call32(call_ctr, call, gridDim.x);
+  }
+}
+
+// The self-play tick's act + step on 16-row tiles (SK_ACT16, the acting
+// launch below kAct16MaxEnvs games): a workgroup owns 8 games, their 16
+// player rows (RowsPlayers8) through actor_tile16, then wave 0's first 16
+// lanes finish k_step_split's tick (split_load / split_finish) as
+// act_step32's wave 0 does for 16 games.  Equal, bit for bit, to
+// sk_actor_forward_f32 with 16-row tiles (SK_FWD16=1) + sk_env_step_insert.
+struct RowsPlayers8 {
+  int64_t g0, n;
+  __device__ int64_t operator()(int i) const { return i < 8 ? g0 + i : n + g0 + (i - 8); }
+  __device__ bool valid(int i) const { return g0 + (i & 7) < n; }
+};
+template <bool NOISE>
+__device__ __forceinline__ void act_step16(const float* __restrict__ aflat, float* __restrict__ act_out, float sd,
+                                           float action_sd, uint64_t seed, uint64_t* __restrict__ call_ctr,
+                                           sk::StepArgs a, sk::Cfg c, float* lds, unsigned nb) {
+  float* S = lds;
+  float* H1 = S + kR * kLdS16;
+  f4(*MP)[kR] = (f4(*)[kR])(H1 + kR * kLdH1);
+  float2* sAct = (float2*)(MP[4]);
+  const int lane = threadIdx.x & 63;
+  const bool w0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0;
+  const int64_t g0 = (int64_t)blockIdx.x * 8;
+  sk_counters* slot = a.ctr ? a.ctr + (size_t)blockIdx.x * SK_CTR_STRIDE : nullptr;
+  sk::StepLane L;
+  if (w0) L = sk::split_load(a, lane < 16 ? 2 * g0 + lane : 2 * a.n, slot);
+  const Net A = net_of(aflat, kALd, 2);
+  const bool draws = (NOISE || action_sd != 0.f) && call_ctr;
+  const uint64_t call = draws ? call_ctr[0] + 1 : 0;
+  actor_tile16<NOISE>(A, a.acting_obs, act_out, RowsPlayers8{g0, a.n}, sd, action_sd, seed, call, S, H1, MP, sAct);
+  __syncthreads();
+  if (w0) {
+    const float2 act = lane < 16 ? sAct[(lane & 1) * 8 + (lane >> 1)] : make_float2(0.f, 0.f);
+    sk::split_finish(a, c, L, act, slot);
+  }
+  if (draws) {
+    __syncthreads();
+    advance_call32(call_ctr, call, nb);
+  }
+}
+constexpr size_t kActStep16Lds = kActorTile16Lds + 16 * sizeof(float2);
+template <bool NOISE>
+__global__ void __launch_bounds__(kFwdThreads) k_act_step16(const float* __restrict__ aflat, float* __restrict__ act_out,
+                                                            float sd, float action_sd, uint64_t seed,
+                                                            uint64_t* __restrict__ call_ctr, sk::StepArgs a,
+                                                            sk::Cfg c) {
+  extern __shared__ __attribute__((aligned(16))) float smem_sl[];
+  act_step16<NOISE>(aflat, act_out, sd, action_sd, seed, call_ctr, a, c, smem_sl, gridDim.x);
+}
+
+// A gradient step's backward launch with the next acting tick beside it
+// (the fused overlapped learner tick: sk_critic_grad_f32_sampled_step carries
+// it in the critic's backward, sk_actor_grad_f32_step in the actor's):
+// workgroups [0, GA) run act_step32 (k_act_step32's 16 games each), the rest
+// grad_slice_bwd<MODE> (k_grad_slice_bwd's workgroup blockIdx - GA).  The
+// two share no data: the backward reads the minibatch, the nets and the
+// forward's z2; the acting half reads the actor and the observations and
+// writes the env, the actions and the ring (the minibatch was gathered
+// before, excluding the rows this insert writes).  LDS is the larger of the
+// two layouts: two workgroups per CU (the critic's 81,616 B twice fill the
+// CU's 160 KiB).
+constexpr size_t bwd_act_lds(int mode, bool a16 = false) {
+  return (a16 ? kActStep16Lds : kActStepLds) > sl_bwd_lds(mode) ? (a16 ? kActStep16Lds : kActStepLds)
+                                                                  : sl_bwd_lds(mode);
+}
+static_assert(2 * bwd_act_lds(kSlCriticBoot) <= 160 * 1024 && 2 * bwd_act_lds(kSlActor) <= 160 * 1024,
+              "two fused workgroups per CU");
+static_assert(kSlThreads == kFwdThreads, "one workgroup size for both halves");
+template <int MODE, bool NOISE, bool A16>
+__global__ void __launch_bounds__(kFwdThreads) k_bwd_act_step32(SK_SLICE_BWD_PARAMS, unsigned GA,
+                                                                const float* __restrict__ aflat,
+                                                                float* __restrict__ act_out, float sd, float action_sd,
+                                                                uint64_t aseed, uint64_t* __restrict__ acall_ctr,
+                                                                sk::StepArgs a, sk::Cfg c) {
+  extern __shared__ __attribute__((aligned(16))) float smem_sl[];
+  if (A16 && blockIdx.x < GA) {
+    act_step16<NOISE>(aflat, act_out, sd, action_sd, aseed, acall_ctr, a, c, smem_sl, GA);
+  } else if (blockIdx.x < GA) {
+    float* S = smem_sl;
+    float* H1 = S + 32 * kLdS;
+    float* H2 = H1 + 32 * kLdH1;
+    act_step32<NOISE>(aflat, act_out, sd, action_sd, aseed, acall_ctr, a, c, S, H1, H2, (float2*)(H2 + 32 * kLdH2),
+                      GA);
+  } else {
+    grad_slice_bwd<MODE>((int)(blockIdx.x - GA), smem_sl, SK_SLICE_BWD_ARGS);
   }
 }
 
@@ -1863,6 +1932,15 @@ void set_lds32(K kernel, size_t bytes) {
 // 16-row actor forward up to 4,096 rows (at most half the CUs busy with 32-row
 // tiles; profiles/r03u_actor_fwd.jsonl: 2,048 rows 9.6 -> 6.6 us, but 8,192
 // rows 10.4 -> 10.9 us); SK_FWD16=0 / 1 forces the 32- / 16-row kernel
+// the acting launch on 16-row tiles (8 games per workgroup): SK_ACT16=1 / 0
+// forces, else up to kAct16MaxEnvs games
+constexpr int64_t kAct16MaxEnvs = 0;
+bool act16_games(int64_t n) {
+  const char* e = getenv("SK_ACT16");
+  const int v = e && *e ? atoi(e) : -1;
+  return v == 1 || (v != 0 && n <= kAct16MaxEnvs);
+}
+
 bool fwd16_rows(int64_t rows) {
   const char* e = getenv("SK_FWD16");
   const int v = e && *e ? atoi(e) : -1;
@@ -1887,8 +1965,10 @@ int launch_sliced(const float* f0, const float* f1, const float* f2, const float
   if (!attr) {
     set_lds32(k_grad_slice_fwd<MODE>, sl_fwd_lds(MODE));
     set_lds32(k_grad_slice_bwd<MODE>, sl_bwd_lds(MODE));
-    set_lds32(k_bwd_act_step32<MODE, true>, bwd_act_lds(MODE));
-    set_lds32(k_bwd_act_step32<MODE, false>, bwd_act_lds(MODE));
+    set_lds32(k_bwd_act_step32<MODE, true, false>, bwd_act_lds(MODE));
+    set_lds32(k_bwd_act_step32<MODE, false, false>, bwd_act_lds(MODE));
+    set_lds32(k_bwd_act_step32<MODE, true, true>, bwd_act_lds(MODE, true));
+    set_lds32(k_bwd_act_step32<MODE, false, true>, bwd_act_lds(MODE, true));
     attr = true;
   }
   float* Z = scratch + w1_rows * kW1Part;
@@ -1897,16 +1977,22 @@ int launch_sliced(const float* f0, const float* f1, const float* f2, const float
                                                                   step_ctr, n_steps, rs);
   if (job) {  // the acting tick's workgroups first, then the backward's
     sk::StepArgs a = job->a;
-    const unsigned GA = (unsigned)((a.n + 15) / 16);
+    const bool a16 = act16_games(a.n);
+    const unsigned GA = (unsigned)(a16 ? (a.n + 7) / 8 : (a.n + 15) / 16);
     a.grid_blocks = GA;
-    if (job->sd != 0.f)
-      k_bwd_act_step32<MODE, true><<<GA + G, kFwdThreads, bwd_act_lds(MODE), st>>>(
-          f0, f1, f2, S, A, Y, R, D, gamma, B, key_row0, scale, seed, call_ctr, Z, partials, scratch, stat_out,
-          mask_out, GA, job->aflat, job->act_out, job->sd, job->action_sd, job->seed, job->call_ctr, a, job->c);
-    else
-      k_bwd_act_step32<MODE, false><<<GA + G, kFwdThreads, bwd_act_lds(MODE), st>>>(
-          f0, f1, f2, S, A, Y, R, D, gamma, B, key_row0, scale, seed, call_ctr, Z, partials, scratch, stat_out,
-          mask_out, GA, job->aflat, job->act_out, 0.f, job->action_sd, job->seed, job->call_ctr, a, job->c);
+    const size_t lds = bwd_act_lds(MODE, a16);
+#define SK_BWD_ACT(NZ, A6)                                                                                          \
+  k_bwd_act_step32<MODE, NZ, A6><<<GA + G, kFwdThreads, lds, st>>>(                                                 \
+      f0, f1, f2, S, A, Y, R, D, gamma, B, key_row0, scale, seed, call_ctr, Z, partials, scratch, stat_out, mask_out, \
+      GA, job->aflat, job->act_out, NZ ? job->sd : 0.f, job->action_sd, job->seed, job->call_ctr, a, job->c)
+    if (job->sd != 0.f) {
+      if (a16) SK_BWD_ACT(true, true);
+      else SK_BWD_ACT(true, false);
+    } else {
+      if (a16) SK_BWD_ACT(false, true);
+      else SK_BWD_ACT(false, false);
+    }
+#undef SK_BWD_ACT
     return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
   }
   k_grad_slice_bwd<MODE><<<G, kSlThreads, sl_bwd_lds(MODE), st>>>(f0, f1, f2, S, A, Y, R, D, gamma, B, key_row0,
@@ -1930,6 +2016,15 @@ int sk_launch_act_step32(const float* aflat, float* act_out, float sd, float act
     set_lds32(k_act_step32<true>, kActStepLds);
     set_lds32(k_act_step32<false>, kActStepLds);
     attr = true;
+  }
+  if (act16_games(a.n)) {
+    const unsigned G8 = (unsigned)((a.n + 7) / 8);
+    if (sd != 0.f)
+      k_act_step16<true><<<G8, kFwdThreads, kActStep16Lds, st>>>(aflat, act_out, sd, action_sd, seed, call_ctr, a, c);
+    else
+      k_act_step16<false><<<G8, kFwdThreads, kActStep16Lds, st>>>(aflat, act_out, 0.f, action_sd, seed, call_ctr, a,
+                                                                  c);
+    return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
   }
   const unsigned G = (unsigned)((a.n + 15) / 16);
   if (sd != 0.f)

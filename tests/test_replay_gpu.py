@@ -222,17 +222,21 @@ def test_tick_graph_replay_modes_equal(learner, monkeypatch, precision, explorat
         assert k == out[0][4]
 
 
+@pytest.mark.parametrize("tile", ["32", "16"])
 @pytest.mark.parametrize("n", [256, 4096, 300, 302])
 @pytest.mark.parametrize("noise", ["none", "param", "action"])
-def test_act_step_equals_actor_then_step_insert(learner, monkeypatch, n, noise):
+def test_act_step_equals_actor_then_step_insert(learner, monkeypatch, n, noise, tile):
     """sk_env_act_step (the fp32 actor forward, the env step and the ring
     insert in one launch) against sk_actor_forward_f32 (32-row tiles) then
     sk_env_step_insert: the same actions, step outputs, ring, counters and
     noise call number bit for bit, every tick, through restarts (300 games: a
-    partial last 16-game tile; 302: N % 4 != 0, the two-launch fallback)"""
+    partial last 16-game tile; 302: N % 4 != 0, the two-launch fallback).
+    tile 16: k_act_step16 (8 games per workgroup, SK_ACT16=1) against the
+    16-row forward (SK_FWD16=1)"""
     from skillshot_learning_amd.actor_kernel import ActorKernel32
     from skillshot_learning_amd.vec_env import VecSkillshotGame
-    monkeypatch.setenv("SK_FWD16", "0")
+    monkeypatch.setenv("SK_FWD16", "1" if tile == "16" else "0")
+    monkeypatch.setenv("SK_ACT16", "1" if tile == "16" else "0")
     torch.manual_seed(1)
     actor = learner.Actor().cuda()
     sd, asd = {"none": (0.0, 0.0), "param": (0.5, 0.0), "action": (0.0, 0.15)}[noise]
@@ -256,9 +260,10 @@ def test_act_step_equals_actor_then_step_insert(learner, monkeypatch, n, noise):
     assert envs[0].counters()["dones"] > 0
 
 
-@pytest.mark.parametrize("precision,exploration", [("fp32", "action_noise"), ("fp32", "param_noise"),
-                                                   ("bf16", "action_noise")])
-def test_tick_overlap_equals_serial(learner, monkeypatch, precision, exploration):
+@pytest.mark.parametrize("precision,exploration,tile", [("fp32", "action_noise", "32"), ("fp32", "param_noise", "32"),
+                                                        ("bf16", "action_noise", "32"), ("fp32", "action_noise", "16"),
+                                                        ("fp32", "param_noise", "16")])
+def test_tick_overlap_equals_serial(learner, monkeypatch, precision, exploration, tile):
     """the overlapped learner tick (acting launches on a second stream beside
     the update, minibatch keyed on the count before the tick's insert, the
     insert's rows excluded; joined before the actor's Adam launch): 20
@@ -267,6 +272,7 @@ def test_tick_overlap_equals_serial(learner, monkeypatch, precision, exploration
     counters -- i.e. the two streams share no data they race on; and (fp32)
     the fused form, the acting launch run by the actor gradient's backward
     launch (SK_TICK_OVERLAP=fused, sk_actor_grad_f32_step), equals them too"""
+    monkeypatch.setenv("SK_ACT16", "1" if tile == "16" else "0")
     out = []
     for mode in ("1", "serial") + (("fused", "fused-actor") if precision == "fp32" else ()):
         monkeypatch.setenv("SK_FUSE_ACT_IN", "actor" if mode == "fused-actor" else "critic")
@@ -316,8 +322,8 @@ def test_overlap_sample_excludes_rows_being_written(learner):
 
 @pytest.mark.parametrize("batch", [128, 1024])  # sliced schedule (one shared launch) / not (two launches)
 @pytest.mark.parametrize("noise", ["param", "action"])
-@pytest.mark.parametrize("carrier", ["actor", "critic"])
-def test_grad_step_job_equals_separate_launches(learner, monkeypatch, batch, noise, carrier):
+@pytest.mark.parametrize("carrier,tile", [("actor", "32"), ("critic", "32"), ("critic", "16")])
+def test_grad_step_job_equals_separate_launches(learner, monkeypatch, batch, noise, carrier, tile):
     """sk_env_act_step_job + sk_actor_grad_f32_step / sk_critic_grad_f32_sampled_step
     (the acting tick run in a gradient step's backward launch) against the
     gradient step and sk_env_act_step as separate launches: the net after
@@ -327,6 +333,7 @@ def test_grad_step_job_equals_separate_launches(learner, monkeypatch, batch, noi
     from skillshot_learning_amd.actor_kernel import ActorKernel32
     from skillshot_learning_amd.vec_env import VecSkillshotGame
     monkeypatch.setenv("SK_FWD16", "0")
+    monkeypatch.setenv("SK_ACT16", "1" if tile == "16" else "0")
     n = 256
     sd, asd = {"param": (0.5, 0.0), "action": (0.0, 0.15)}[noise]
     out = []
