@@ -418,7 +418,9 @@ def learner_rate(envs, world, rank, ticks, batch=256, exploration="param_noise",
     obs/reward/auto-reset, 2N transitions into the HBM replay ring, one critic
     + actor update (fused MFMA kernels, in-kernel bootstrap target) on a
     `batch` sample, soft target update and actor repack — replayed as one
-    captured hipGraph per 2 ticks (SkillshotLearner.tick_graph).  envs = games
+    captured hipGraph per 10 ticks (SkillshotLearner.tick_graph;
+    SK_TICKS_PER_GRAPH: 10 vs 2 takes ~1.3 us off every leg's tick,
+    profiles/r03tpg_ticks_per_graph_ab.jsonl).  envs = games
     on this rank (global ids rank * envs ..)."""
     from skillshot_learning_amd.learner import SkillshotLearner
     L = SkillshotLearner(n_envs=envs, seed=0, env_offset=rank * envs, exploration=exploration, tick_limit=2000,
@@ -427,7 +429,7 @@ def learner_rate(envs, world, rank, ticks, batch=256, exploration="param_noise",
     verbose = os.environ.get("SK_BENCH_VERBOSE") == "1"
     if verbose:
         _log(f"learner {envs} games: capturing")
-    tg = L.tick_graph(batch=batch, updates_per_tick=1, ticks_per_graph=int(os.environ.get("SK_TICKS_PER_GRAPH", "2")))
+    tg = L.tick_graph(batch=batch, updates_per_tick=1, ticks_per_graph=int(os.environ.get("SK_TICKS_PER_GRAPH", "10")))
     if verbose:
         _log(f"learner {envs} games: captured ({tg.multi_rank_mode})")
     tg.run(10)
