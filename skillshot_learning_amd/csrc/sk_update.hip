@@ -1002,7 +1002,11 @@ __device__ __forceinline__ void scatter_fwd_pack(char* out, int p, float v) {  /
 #ifndef SK_ADAM_SLICES
 #define SK_ADAM_SLICES 4
 #endif
-constexpr int kAdamParams = 64, kAdamSlices = SK_ADAM_SLICES;
+#ifndef SK_ADAM_PARAMS
+#define SK_ADAM_PARAMS 64
+#endif
+constexpr int kAdamParams = SK_ADAM_PARAMS, kAdamSlices = SK_ADAM_SLICES;
+static_assert(skpart::kPW2 % kAdamParams == 0, "the W1 rows stay workgroup-uniform");
 
 __global__ void __launch_bounds__(kAdamParams * kAdamSlices) k_adam_flat(const float* __restrict__ partial, int G, int P, const float* __restrict__ grad_in,
                             float* __restrict__ grad_out, int apply, float* __restrict__ param, float* __restrict__ m,
