@@ -1002,6 +1002,31 @@ class SkillshotLearner:
 TICK_OVERLAP_MIN_ENVS = 16384  # TickGraph's auto overlap threshold (games per rank)
 
 
+def tick_form(n, batch, capacity, updates_per_tick, multi, fused, f32, fused_act, sliced, env=None):
+    """TickGraph's tick form: "sequential" (the reference's order), "streams"
+    (the acting launches on a second stream beside the update), "fused" (the
+    acting launch inside the critic gradient's backward launch) or "serial"
+    (the streams form on one stream, a test reference); see TickGraph.
+    SK_TICK_OVERLAP = auto (default) / 0 / 1 / fused / serial; the overlapped
+    forms need the fused update path, one update per tick, the default
+    replay mode (SK_FUSED_REPLAY=2) and a ring holding a batch beside the rows
+    one insert writes; "fused" the fp32 kernels with the fused act + step
+    launch (SK_FUSED_ACT), N % 4 == 0 and the sliced update schedule; several
+    ranks run "fused" or "sequential"."""
+    env = os.environ if env is None else env
+    ov = env.get("SK_TICK_OVERLAP", "auto")
+    can = (fused and updates_per_tick == 1 and capacity >= batch + 4 * n
+           and env.get("SK_FUSED_REPLAY", "2") == "2")
+    can_fuse = can and f32 and fused_act and n % 4 == 0 and env.get("SK_FUSED_ACT", "1") != "0" and sliced
+    if ov == "auto":
+        ov = "1" if n >= TICK_OVERLAP_MIN_ENVS and not multi else ("fused" if can_fuse else "0")
+    if multi and ov != "fused":
+        ov = "0"
+    if not can or ov == "0" or (ov == "fused" and not can_fuse):
+        return "sequential"
+    return {"fused": "fused", "serial": "serial"}.get(ov, "streams")
+
+
 class TickGraph:
     """Captured replay-rule ticks (see SkillshotLearner.tick_graph)."""
 
@@ -1052,23 +1077,13 @@ class TickGraph:
         # rank draws from its own ring; config 5, "shared": the drawn rows are
         # all-gathered first; the acting tick rides the critic's backward
         # launch, before the gradient all-reduce); else sequential.
-        ov = os.environ.get("SK_TICK_OVERLAP", "auto")
         fu = L.ddpg._fused
-        multi = L.ddpg.multi()
-        can = (fu is not None and updates_per_tick == 1 and L.replay.cap >= batch + 4 * n
-               and os.environ.get("SK_FUSED_REPLAY", "2") == "2")
-        can_fuse = (can and fu.f32 and getattr(L.actor_kernel, "fused_act_step", False) and n % 4 == 0
-                    and os.environ.get("SK_FUSED_ACT", "1") != "0"
-                    and fu.sliced(batch))
-        if ov == "auto":
-            ov = "1" if n >= TICK_OVERLAP_MIN_ENVS and not multi else ("fused" if can_fuse else "0")
-        if multi and ov != "fused":
-            ov = "0"
-        self.overlap = can and ov != "0" and (ov != "fused" or can_fuse)
-        self.fuse_act = self.overlap and ov == "fused"
-        self.side = (torch.cuda.Stream(device=dev) if self.overlap and ov not in ("serial", "fused") else None)
-        self.mode = ("sequential" if not self.overlap else "fused" if self.fuse_act else
-                     "serial" if self.side is None else "streams")
+        self.mode = tick_form(n, batch, L.replay.cap, updates_per_tick, L.ddpg.multi(), fu is not None,
+                              fu is not None and fu.f32, getattr(L.actor_kernel, "fused_act_step", False),
+                              fu is not None and fu.sliced(batch))
+        self.overlap = self.mode != "sequential"
+        self.fuse_act = self.mode == "fused"
+        self.side = torch.cuda.Stream(device=dev) if self.mode == "streams" else None
         # which backward launch carries the acting tick (SK_FUSE_ACT_IN): the
         # critic's (default, the longer of the two) or the actor's
         self.job_in = os.environ.get("SK_FUSE_ACT_IN", "critic")

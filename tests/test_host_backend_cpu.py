@@ -196,3 +196,32 @@ def test_cpu_backend_step_insert_equals_step_then_add(ssa):
         assert int(copy) == (ra.total if t % 2 else -1)
         oa, ob = x["obs_reset"], y["obs_reset"]
     assert a.counters()["dones"] > 0
+
+
+def test_tick_form_selection():
+    """TickGraph's tick form (learner.tick_form): the auto policy (streams
+    from 16,384 games on one rank, fused below with the fp32 kernels, fused or
+    sequential on several ranks) and the SK_TICK_OVERLAP overrides"""
+    from skillshot_learning_amd.learner import tick_form
+
+    def f(n, env=None, multi=False, f32=True, batch=256, cap=1 << 20, **kw):
+        args = dict(updates_per_tick=1, fused=True, fused_act=True, sliced=True)
+        args.update(kw)
+        return tick_form(n, batch, cap, args["updates_per_tick"], multi, args["fused"], f32, args["fused_act"],
+                         args["sliced"], env=env or {})
+    assert f(4096) == "fused" and f(65536) == "streams" and f(16384) == "streams"
+    assert f(4096, f32=False) == "sequential" and f(65536, f32=False) == "streams"
+    assert f(4096, multi=True) == "fused" and f(65536, multi=True) == "fused"
+    assert f(4096, multi=True, f32=False) == "sequential"
+    assert f(4098) == "sequential"                                  # N % 4 != 0: no fused launch
+    assert f(4096, sliced=False) == "sequential"                    # batch past the sliced schedule
+    assert f(4096, cap=4096) == "sequential"                        # ring too small beside an insert
+    assert f(4096, updates_per_tick=2) == "sequential" and f(4096, fused=False) == "sequential"
+    assert f(65536, env={"SK_TICK_OVERLAP": "0"}) == "sequential"
+    assert f(4096, env={"SK_TICK_OVERLAP": "1"}) == "streams"
+    assert f(4096, env={"SK_TICK_OVERLAP": "serial"}) == "serial"
+    assert f(65536, env={"SK_TICK_OVERLAP": "fused"}) == "fused"
+    assert f(4096, env={"SK_TICK_OVERLAP": "fused"}, f32=False) == "sequential"
+    assert f(4096, env={"SK_FUSED_ACT": "0"}) == "sequential"
+    assert f(65536, multi=True, env={"SK_TICK_OVERLAP": "1"}) == "sequential"
+    assert f(4096, env={"SK_FUSED_REPLAY": "1"}) == "sequential"
