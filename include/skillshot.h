@@ -126,7 +126,8 @@ int sk_env_counters_ptr(const sk_env* env, sk_counters** out);
 int sk_env_counter_slots(const sk_env* env, int64_t* out);
 /* Copy the episode counters to host memory (synchronises `stream`; the
  * slots are summed on device by one workgroup first, so 32 bytes cross
- * PCIe whatever n_envs is), and zero them (stream-ordered). */
+ * PCIe whatever n_envs is).  The counters are NOT zeroed: call
+ * sk_env_clear_counters (stream-ordered) for that. */
 int sk_env_read_counters(sk_env* env, sk_counters* host_out, void* stream);
 int sk_env_clear_counters(sk_env* env, void* stream);
 /* Host-side RNG step counter: every step / reset call consumes one value
@@ -247,10 +248,16 @@ int sk_env_act_step(sk_env* env, const float* actor_flat, const float* acting_ob
 /* sk_env_act_step prepared, not launched (ABI 8): the same arguments
  * (N % 4 == 0, ring given or not) into *job, and the env advances its step
  * slot as if the launch had been issued.  The job is then run, exactly once
- * and before the env's next step, by sk_actor_grad_f32_step, whose actor
- * backward launch carries it (the fused overlapped learner tick: the acting
- * tick beside the actor step; the minibatch must already be drawn, excluding
- * the rows this insert writes).  Opaque: copy it, do not edit it. */
+ * and before the env's next step, by one of the three carriers, whose
+ * gradient backward launch runs it: sk_critic_grad_f32_sampled_step (the
+ * default one-rank carrier), sk_critic_grad_f32_step (the multi-rank
+ * shared-replay tick) or sk_actor_grad_f32_step (the fused overlapped learner
+ * tick: the acting tick beside the gradient step; the minibatch must already
+ * be drawn, excluding the rows this insert writes).  A carrier call that
+ * fails (SK_EINVAL, SK_EHIP) leaves the env's step slot advanced without the
+ * acting launch: the env is then unusable until sk_env_sync_step_counter
+ * (and the caller's own host mirrors are rewound).  Opaque: copy it, do not
+ * edit it. */
 #define SK_STEP_JOB_WORDS 128
 typedef struct sk_step_job {
   uint64_t opaque[SK_STEP_JOB_WORDS];
@@ -593,11 +600,6 @@ int sk_actor_grad_f32(const float* actor_flat, const float* critic_flat, const f
 int sk_actor_grad_f32_step(const float* actor_flat, const float* critic_flat, const float* obs, int64_t batch,
                            float loss_scale, float* partials, float* step_counters, int32_t n_steps, float* q_sum,
                            float* scratch, const sk_step_job* job, void* stream);
-/* sk_critic_grad_f32_sampled with a prepared acting tick run in its backward
- * launch (ABI 8; the minibatch is gathered by the first launch, before the
- * acting tick's insert: give q->exclude = the insert's rows).  Results equal,
- * bit for bit, sk_critic_grad_f32_sampled followed by the job's
- * sk_env_act_step. */
 /* sk_critic_grad_f32 with a prepared acting tick run in its backward
  * launch (ABI 8; the multi-rank shared-replay tick, whose minibatch is drawn
  * and all-gathered before): equal, bit for bit, to sk_critic_grad_f32 then the
@@ -608,6 +610,11 @@ int sk_critic_grad_f32_step(const float* critic_flat, const float* obs, const fl
                             int64_t row_offset, float grad_scale, uint64_t seed, const int64_t* call_counter,
                             float* partials, float* step_counters, int32_t n_steps, float* loss_sum,
                             uint8_t* dropout_mask, float* scratch, const sk_step_job* job, void* stream);
+/* sk_critic_grad_f32_sampled with a prepared acting tick run in its backward
+ * launch (ABI 8; the minibatch is gathered by the first launch, before the
+ * acting tick's insert: give q->exclude = the insert's rows).  Results equal,
+ * bit for bit, sk_critic_grad_f32_sampled followed by the job's
+ * sk_env_act_step. */
 int sk_critic_grad_f32_sampled_step(const float* critic_flat, const sk_ring_sample* q, float gamma,
                                     const float* target_actor_flat, const float* target_critic_flat, int64_t batch,
                                     int64_t row_offset, float grad_scale, uint64_t seed,

@@ -1095,7 +1095,7 @@ __device__ __forceinline__ float rowall16(float v) {
 
 // The backward launch's workgroup `bid` (row tile bid / kSlices, slice
 // bid % kSlices) on the LDS at smem_sl (sl_bwd_lds(MODE) bytes): the body of
-// k_grad_slice_bwd, and of k_actor_bwd_act_step32's backward workgroups.
+// k_grad_slice_bwd, and of k_bwd_act_step32's backward workgroups.
 #define SK_SLICE_BWD_PARAMS                                                                                      \
   const float *__restrict__ f0, const float *__restrict__ f1, const float *__restrict__ f2,                       \
       const float *__restrict__ Sg, const float *__restrict__ Ag, const float *__restrict__ Yg,                  \
@@ -1643,7 +1643,7 @@ __global__ void __launch_bounds__(kFwdThreads) k_actor_fwd32(const float* __rest
 // sk_actor_forward_f32 (32-row tiles) followed by sk_env_step(_insert).
 // Wave 0 counts its games into counter slot line b.
 // act_step32: the body on LDS S / H1 / H2 / sAct for the first nb workgroups
-// of the grid (k_act_step32: all of them; k_actor_bwd_act_step32: the
+// of the grid (k_act_step32: all of them; k_bwd_act_step32: the
 // workgroups before the backward's)
 constexpr size_t kActStepLds = (size_t)32 * (kLdS + kLdH1 + kLdH2) * 4 + 32 * sizeof(float2);
 template <bool NOISE>
@@ -2133,6 +2133,7 @@ static int critic_sampled(const float* critic_flat, const sk_ring_sample* q, flo
                           float* partials, float* step_counters, int32_t n_steps, float* loss_sum,
                           uint8_t* dropout_mask, float* scratch, const sk::ActStepJob* job, void* stream) {
   if (!q || !q->ring || !q->total || !q->s || !q->a || !q->r || !q->s2 || !q->d || q->capacity <= 0) return SK_EINVAL;
+  if (q->exclude < 0 || q->exclude >= q->capacity) return SK_EINVAL;  // as sk_replay_sample_excl
   if ((((uintptr_t)q->ring) & 15) || (((uintptr_t)q->s) & 15) || (((uintptr_t)q->s2) & 15) || (((uintptr_t)q->a) & 7))
     return SK_EINVAL;
   const bool boot = target_actor_flat != nullptr;

@@ -198,7 +198,9 @@ __device__ __forceinline__ int64_t ring_row(const RingSample& q, int64_t b, int6
     const uint64_t size = (uint64_t)(t < q.cap ? t : q.cap);
     return (int64_t)(((unsigned __int128)u53 * size) >> 53);
   }
-  const int64_t lim = q.cap - q.excl, el = t < lim ? t : lim;
+  // the entry points reject excl outside [0, cap); the clamp keeps a bad
+  // value from indexing outside the ring regardless
+  const int64_t lim = q.cap - q.excl, el0 = t < lim ? t : lim, el = el0 > 0 ? el0 : 0;
   const int64_t k = (int64_t)(((unsigned __int128)u53 * (uint64_t)el) >> 53);
   return (t - el + k) % q.cap;
 }

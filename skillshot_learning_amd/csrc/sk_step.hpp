@@ -208,7 +208,7 @@ struct StepArgs {
   uint32_t* ring_arrivals;  // SK_REPLAY_ARRIVAL_WORDS
   int64_t* ring_total_copy; // NULL, or a second store of the new total
   // the step's workgroups when they are the first grid_blocks of a larger
-  // launch (k_actor_bwd_act_step32: the actor step's backward beside them),
+  // launch (k_bwd_act_step32: the actor step's backward beside them),
   // 0 = the whole grid
   uint32_t grid_blocks;
 };

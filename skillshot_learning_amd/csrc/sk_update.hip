@@ -1174,6 +1174,7 @@ int sk_critic_grad_bootstrap_sampled(const void* cpack, const sk_ring_sample* q,
                                      const int64_t* call_counter, float* partial, float* step_counters,
                                      int32_t n_steps, float* loss_sum, uint8_t* dropout_mask, void* stream) {
   if (!q || !q->ring || !q->total || !q->s || !q->a || !q->r || !q->s2 || !q->d || q->capacity <= 0) return SK_EINVAL;
+  if (q->exclude < 0 || q->exclude >= q->capacity) return SK_EINVAL;  // as sk_replay_sample_excl
   if ((((uintptr_t)q->ring) & 15) || (((uintptr_t)q->s) & 15) || (((uintptr_t)q->s2) & 15) || (((uintptr_t)q->a) & 7))
     return SK_EINVAL;
   const bool boot = target_actor_gpack != nullptr;

@@ -314,6 +314,8 @@ class FusedUpdate:
         launch.  Returns (loss, (s, a, r, s2, d)), the sample buffers."""
         B = int(batch)
         gb = B if global_batch is None else int(global_batch)
+        if not 0 <= int(exclude) < ring.cap:
+            raise ValueError(f"exclude {exclude} outside [0, capacity {ring.cap})")
         out, draw = ring.next_draw(B)
         tp = (total if total is not None else ring.total_t).data_ptr()
         q = RingSample(ring.buf.data_ptr(), ring.cap, tp, ring.seed, draw, *[t.data_ptr() for t in out],

@@ -112,3 +112,24 @@ def test_partial_layout_index_is_a_permutation():
     assert int(c[w2 + 258 + 257]) == w2 + 128 * 256 + 3  # W2[1][257] (action column 1)
     assert torch.equal(c[:w2], torch.arange(w2)) and torch.equal(c[w2 + 128 * 258:], torch.arange(w2 + 128 * 258, 36609))
     assert torch.equal(partial_index(36482), torch.arange(36482))
+
+
+@pytest.mark.parametrize("exclude", [-1, 64, 65, 1 << 40])
+def test_sampled_critic_rejects_exclude_outside_ring(exclude):
+    """sk_ring_sample.exclude outside [0, capacity) is SK_EINVAL in every
+    in-launch gather (sk_critic_grad_f32_sampled, sk_critic_grad_bootstrap_
+    sampled), as in sk_replay_sample_excl: a negative draw window would index
+    outside the ring.  The checks run before any launch, so the
+    dummy (aligned, never dereferenced) pointers are safe without a GPU."""
+    from skillshot_learning_amd.update_kernel import RingSample
+    L = ssa.load_library()
+    fake = ctypes.c_void_p(0x1000)
+    q = RingSample(0x1000, 64, 0x1000, 0, 0, 0x1000, 0x1000, 0x1000, 0x1000, 0x1000, exclude)
+    rc = L.sk_critic_grad_f32_sampled(fake, ctypes.byref(q), 0.0, None, None, 16, 0, 1.0, 0, fake, fake, None, 0,
+                                      None, None, fake, None)
+    assert rc == _capi.SK_EINVAL
+    rc = L.sk_critic_grad_bootstrap_sampled(fake, ctypes.byref(q), 0.0, None, None, 16, 0, 1.0, 0, fake, fake, None,
+                                            0, None, None, None)
+    assert rc == _capi.SK_EINVAL
+    assert L.sk_replay_sample_excl(fake, 64, fake, 0, 0, 16, fake, fake, fake, fake, fake, exclude,
+                                   None) == _capi.SK_EINVAL
