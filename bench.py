@@ -72,9 +72,16 @@ def parse():
     p.add_argument("--no-full", action="store_true", help="skip the full-contract (obs + reward) tick leg")
     p.add_argument("--no-learner", action="store_true", help="skip the DDPG-in-the-loop legs")
     p.add_argument("--learner-ticks", type=int, default=200)
-    p.add_argument("--learner-timeout", type=float, default=240.0,
-                   help="seconds per multi-rank learner leg (run in child processes)")
+    p.add_argument("--learner-timeout", type=float, default=150.0,
+                   help="seconds per learner leg (each runs in child processes)")
+    p.add_argument("--leg-timeout", type=float, default=120.0, help="seconds per one-GPU step leg (child process)")
+    p.add_argument("--leg-budget", type=float, default=480.0,
+                   help="wall seconds for all legs beside the headline: a leg that would start past it is skipped "
+                        "(reported in errors), so the headline line always prints")
+    p.add_argument("--no-overlapped", action="store_true",
+                   help="skip the opt-in overlapped learner tick reported beside each leg's reference-order tick")
     p.add_argument("--learner-child", default=None, help=argparse.SUPPRESS)
+    p.add_argument("--leg-child", default=None, help=argparse.SUPPRESS)
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_k_step_multi.json"))
     p.add_argument("--ticks-per-launch", type=int, default=400,
                    help="k_step_multi: ticks per launch (the headline runs K ticks in ceil(K / this) launches)")
@@ -204,8 +211,17 @@ def cpu_baseline(n_envs, seconds, tick_limit, seed, cores):
                                str(c * per), "--seconds", str(seconds), "--seed", str(seed), "--tick-limit",
                                str(tick_limit)], cwd=ROOT, stdout=subprocess.PIPE, text=True)
              for c in range(cores)]
-    outs = [json.loads(p.communicate()[0].strip().splitlines()[-1]) for p in procs]
+    outs = []
+    for p in procs:  # each bounded to ~`seconds` of work: a stuck one is killed, not waited for
+        try:
+            outs.append(json.loads(p.communicate(timeout=3 * seconds + 60)[0].strip().splitlines()[-1]))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.communicate()
+    if not outs:
+        raise RuntimeError("no CPU baseline process finished")
     rate = sum(o["env_steps_per_s"] for o in outs)
+    cores = len(outs)  # the processes that finished (each one core)
     # the pure-Python restatement on config 1 (one game, one core), and the
     # reference-equivalent rate through the ratio measured where the
     # reference is importable (tools/ref_ratio.py -> profiles/ref_vs_pyoracle.json)
@@ -411,8 +427,8 @@ def weak_rate(dev, args, rank, world, n=65536, ticks=4000):
                 kernel="k_step_multi<1>")
 
 
-def learner_rate(envs, world, rank, ticks, batch=256, exploration="param_noise", precision="bf16", group=None,
-                 multi_rank="grad"):
+def learner_rate(envs, world, rank, ticks, batch=256, exploration="param_noise", precision="fp32", group=None,
+                 multi_rank="grad", overlap=None, roofline=True):
     """per tick the actor forward (exploration
     noise) for both players of every game, the fused env step with
     obs/reward/auto-reset, 2N transitions into the HBM replay ring, one critic
@@ -420,8 +436,10 @@ def learner_rate(envs, world, rank, ticks, batch=256, exploration="param_noise",
     `batch` sample, soft target update and actor repack — replayed as one
     captured hipGraph per 10 ticks (SkillshotLearner.tick_graph;
     SK_TICKS_PER_GRAPH: 10 vs 2 takes ~1.3 us off every leg's tick,
-    profiles/r03tpg_ticks_per_graph_ab.jsonl).  envs = games
-    on this rank (global ids rank * envs ..)."""
+    profiles/r03tpg_ticks_per_graph_ab.jsonl).  envs = games on this rank
+    (global ids rank * envs ..).  overlap: tick_graph's tick form (None: the
+    reference's draw order, the update sampling after the tick's insert;
+    "auto": the opt-in overlapped tick, one tick late)."""
     from skillshot_learning_amd.learner import SkillshotLearner
     L = SkillshotLearner(n_envs=envs, seed=0, env_offset=rank * envs, exploration=exploration, tick_limit=2000,
                          replay_capacity=1 << 20, gamma=0.99, tau=0.005, precision=precision, process_group=group,
@@ -429,9 +447,10 @@ def learner_rate(envs, world, rank, ticks, batch=256, exploration="param_noise",
     verbose = os.environ.get("SK_BENCH_VERBOSE") == "1"
     if verbose:
         _log(f"learner {envs} games: capturing")
-    tg = L.tick_graph(batch=batch, updates_per_tick=1, ticks_per_graph=int(os.environ.get("SK_TICKS_PER_GRAPH", "10")))
+    tg = L.tick_graph(batch=batch, updates_per_tick=1, ticks_per_graph=int(os.environ.get("SK_TICKS_PER_GRAPH", "10")),
+                      overlap=overlap)
     if verbose:
-        _log(f"learner {envs} games: captured ({tg.multi_rank_mode})")
+        _log(f"learner {envs} games: captured ({tg.multi_rank_mode}, {tg.mode})")
     tg.run(10)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -452,15 +471,22 @@ def learner_rate(envs, world, rank, ticks, batch=256, exploration="param_noise",
         el = float(tt.item())
     n_ticks = max(1, ticks // tg.ticks) * tg.ticks
     gpu_ms = e0.elapsed_time(e1) / n_ticks
+    # the fp32 parameter noise's variance GEMM runs on bf16 MFMA (DESIGN §7;
+    # the mean GEMM, i.e. the actions' own arithmetic, is fp32)
+    dtype = precision
+    if precision == "fp32" and exploration == "param_noise":
+        dtype = "fp32 (noise-variance GEMM on bf16 MFMA)"
     out = dict(envs_per_gpu=envs, total_envs=envs * world, n_gpus=world, ticks=n_ticks, batch_per_rank=batch,
-               exploration=exploration, updates_per_tick=1, dtype=precision, multi_rank=tg.multi_rank_mode,
-               tick_mode=tg.mode, env_steps_per_s=envs * world * n_ticks / el, ms_per_tick=el * 1e3 / n_ticks,
-               gpu_ms_per_tick=gpu_ms,
+               exploration=exploration, updates_per_tick=1, dtype=dtype, multi_rank=tg.multi_rank_mode,
+               tick_mode=tg.mode, draw_order="reference (after the tick's insert)" if tg.mode == "sequential"
+               else "one tick late (before the tick's insert)",
+               env_steps_per_s=envs * world * n_ticks / el, ms_per_tick=el * 1e3 / n_ticks, gpu_ms_per_tick=gpu_ms,
                episodes=L.game_environment.counters(stream=ctypes.c_void_p(tg.stream.cuda_stream)))
-    try:
-        out["roofline"] = learner_roofline(L, tg, batch, precision, exploration, gpu_ms)
-    except Exception as e:  # noqa: BLE001 (a measurement beside the leg must not cost it)
-        out["roofline_error"] = f"{type(e).__name__}: {e}"
+    if roofline and world == 1 and tg.mode == "sequential":
+        try:
+            out["roofline"] = learner_roofline(L, tg, batch, precision, exploration, gpu_ms)
+        except Exception as e:  # noqa: BLE001 (a measurement beside the leg must not cost it)
+            out["roofline_error"] = f"{type(e).__name__}: {e}"
     del tg, L
     torch.cuda.empty_cache()
     return out
@@ -471,47 +497,65 @@ CRITIC_FLOP_ROW = 72448  # A16: 2 x (12*256 + 258*128 + 128*1)
 MFMA_PEAK_TF = {"fp32": 157.3, "bf16": 2500.0}  # MI355X_MICROARCH.md: f32 MFMA 157.3 TF; bf16 ~2.5 PF dense
 
 
+def _launch_sets(precision, exploration):
+    """the kernels each of the reference-order tick's launch sets issues
+    (the names rocprofv3 --kernel-trace reports)"""
+    nz = "true" if exploration == "param_noise" else "false"
+    if precision == "fp32":
+        return {"acting": f"k_act_step32<{nz}> (sk_env_act_step: actor forward + env step + obs/reward + ring insert, "
+                          "one launch)",
+                "critic_step": "k_grad_slice_fwd<1> (minibatch drawn in-launch) + k_grad_slice_bwd<1> + k_adam_flat",
+                "actor_step": "k_grad_slice_fwd<2> + k_grad_slice_bwd<2> + k_adam_flat"}
+    return {"acting": f"k_actor_fwd_wg<{nz}> + k_step_split (sk_actor_forward_noise + sk_env_step_insert)",
+            "critic_step": "k_critic_grad<true> (minibatch drawn in-launch) + k_adam_flat",
+            "actor_step": "k_actor_grad + k_adam_flat"}
+
+
 def learner_roofline(L, tg, batch, precision, exploration, gpu_ms_per_tick, reps=20):
-    """MFMA roofline of a learner leg: the tick's three
-    GEMM-chain kernels timed one by one on the learner's own nets, with HIP
-    events around one graph replay of `reps` launches on the leg's stream,
-    after its timed region — the actor forward for both players of every game (2N rows; with
-    parameter noise the local-reparameterisation variance GEMM doubles its
-    FLOPs at bf16; at fp32 that GEMM runs on bf16 MFMA, DESIGN §7, so only the
-    fp32 mean GEMM counts against the fp32 peak), the critic gradient on a replay minibatch (critic forward +
-    backward, bootstrap target nets' forwards: 3 x critic + actor + critic
-    FLOP per row) and the actor gradient (actor forward + backward, critic
-    forward + input backward: 3 x actor + 2 x critic).  `achieved` is the
-    dominant (longest) kernel's FLOPs / its average launch; `tick_tflops` the
-    whole tick's FLOPs / the tick's GPU time."""
+    """MFMA roofline of a learner leg, on the launches its tick issues
+    (VERDICT r03 item 2): the reference-order tick is three launch sets,
+    each timed on the learner's own nets and buffers with HIP events around
+    one graph replay of `reps` of it on the leg's stream, after the timed
+    region —
+      acting       the tick's own acting launch(es) (TickGraph._tick without
+                   the update: fp32 k_act_step32, actor forward + env step +
+                   ring insert in one launch), 2N actor rows;
+      critic_step  the sampled critic step (bootstrap target nets' forwards,
+                   critic forward + backward) and its Adam launch;
+      actor_step   the actor step (actor forward + backward through the
+                   critic) and its Adam launch.
+    FLOPs per row from SURVEY §8(a)/(d): actor forward 72,192 (x 2 with
+    parameter noise at bf16, whose variance GEMM runs beside the mean; at fp32
+    that GEMM runs on bf16 MFMA, DESIGN §7, so only the fp32 mean GEMM counts
+    against the fp32 peak); critic step 4 x 72,448 + 72,192; actor step
+    3 x 72,192 + 2 x 72,448.  `achieved` = the dominant (longest) set's FLOPs
+    / its time; `kernel` names that set's kernels; `tick_tflops` = the tick's
+    FLOPs / the tick's GPU time."""
     fu = L.ddpg._fused
     if fu is None:
         raise RuntimeError("no fused update path")
     st = tg.stream
-    rows = tg.obs.view(-1, 12).shape[0]
-    x = tg.obs.view(-1, 12)
-    act = torch.empty((rows, 2), dtype=torch.float32, device=L.device)
-    s, a, r, s2, d = [t.contiguous() for t in L.replay.sample(batch)]
-    part_c = fu._partial(batch, fu.fc.numel())
-    part_a = fu._partial(batch, fu.fa.numel())
-    noise = L.param_noise_sd if exploration == "param_noise" else 0.0
-    ak = L.actor_kernel
+    rows = 2 * L.n_envs
+    noise = exploration == "param_noise"
+    gamma = float(L.ddpg.gamma or 0.0)
+    with torch.cuda.stream(st):
+        _, (s_buf, _, _, _, _) = fu.critic_step_sampled(L.replay, batch, gamma=gamma)
+    st.synchronize()
 
-    def actor():
-        if exploration == "action_noise" and getattr(ak, "fused_action_noise", False):
-            ak(x, out=act, action_sd=L.action_noise_sd)
-        else:
-            ak(x, noise_sd=noise, out=act)
+    def acting():
+        tg._tick(update=False)
 
     def critic():
-        fu._critic_grad(s, a, None, s2, r, d, float(L.ddpg.gamma or 0.0), 0, batch, part_c, None, None, stat=False)
+        fu.critic_step_sampled(L.replay, batch, gamma=gamma)
 
-    def actor_g():
-        fu._actor_grad(s, part_a, None, None)
+    def actor():
+        fu.actor_step(s_buf)
+        L._refresh_actor_pack()
 
-    jobs = {"actor_forward": (actor, rows * ACTOR_FLOP_ROW * (2 if noise and precision == "bf16" else 1)),
-            "critic_grad": (critic, batch * (4 * CRITIC_FLOP_ROW + ACTOR_FLOP_ROW)),
-            "actor_grad": (actor_g, batch * (3 * ACTOR_FLOP_ROW + 2 * CRITIC_FLOP_ROW))}
+    names = _launch_sets(precision, exploration)
+    jobs = {"acting": (acting, rows * ACTOR_FLOP_ROW * (2 if noise and precision == "bf16" else 1)),
+            "critic_step": (critic, batch * (4 * CRITIC_FLOP_ROW + ACTOR_FLOP_ROW)),
+            "actor_step": (actor, batch * (3 * ACTOR_FLOP_ROW + 2 * CRITIC_FLOP_ROW))}
     kern = {}
     with torch.cuda.stream(st):
         for name, (fn, flop) in jobs.items():
@@ -521,7 +565,7 @@ def learner_roofline(L, tg, batch, precision, exploration, gpu_ms_per_tick, reps
             # the reps captured and replayed as one graph: eager Python
             # launches (10-80 us of host time each) would time the host
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=st):
+            with torch.cuda.graph(g, stream=st, capture_error_mode="thread_local"):
                 for _ in range(reps):
                     fn()
             g.replay()
@@ -532,16 +576,17 @@ def learner_roofline(L, tg, batch, precision, exploration, gpu_ms_per_tick, reps
             st.synchronize()
             del g
             us = e0.elapsed_time(e1) * 1e3 / reps
-            kern[name] = dict(us=us, flop=flop, tflops=flop / (us * 1e-6) / 1e12)
+            kern[name] = dict(us=us, flop=flop, tflops=flop / (us * 1e-6) / 1e12, kernels=names[name])
     dom = max(kern, key=lambda k: kern[k]["us"])
     peak = MFMA_PEAK_TF[precision]
     tick_flop = sum(v["flop"] for v in kern.values())
     return dict(bound="mfma", achieved=kern[dom]["tflops"], peak=peak, unit="TFLOP/s",
-                frac=kern[dom]["tflops"] / peak, traffic=None, kernel=dom, kernel_us=kern[dom]["us"],
-                kernels=kern, tick_flop=tick_flop, tick_tflops=tick_flop / (gpu_ms_per_tick * 1e-3) / 1e12,
+                frac=kern[dom]["tflops"] / peak, traffic=None, kernel=names[dom], launch_set=dom,
+                kernel_us=kern[dom]["us"], kernels=kern, tick_flop=tick_flop,
+                tick_tflops=tick_flop / (gpu_ms_per_tick * 1e-3) / 1e12,
                 tick_frac=tick_flop / (gpu_ms_per_tick * 1e-3) / 1e12 / peak,
-                note="kernel times: HIP events over a graph of `reps` launches after the timed region; "
-                     "FLOP per row from SURVEY §8(a)/(d)")
+                note="the reference-order tick's three launch sets, each timed with HIP events over a graph of "
+                     f"{reps}; FLOP per row from SURVEY §8(a)/(d)")
 
 
 def _log(msg):
@@ -569,54 +614,81 @@ def learner_child_main(cfg):
         os.environ["SK_TICKGRAPH_MODE"] = cfg["mode"]
     if os.environ.get("SK_BENCH_VERBOSE") == "1":
         _log(f"learner child up: {cfg}")
-    out = learner_rate(cfg["envs"], world, rank, cfg["ticks"], batch=cfg["batch"], exploration=cfg["exploration"],
-                       precision=cfg["precision"], multi_rank=cfg["multi_rank"])
-    if rank == 0:
-        print(json.dumps(out), flush=True)
+    for ov in cfg.get("overlaps", [None]):
+        out = learner_rate(cfg["envs"], world, rank, cfg["ticks"], batch=cfg["batch"], exploration=cfg["exploration"],
+                           precision=cfg["precision"], multi_rank=cfg["multi_rank"], overlap=ov)
+        if rank == 0:
+            print(json.dumps(dict(out, overlap=ov)), flush=True)
     dist.barrier()
     dist.destroy_process_group()
 
 
+def _child(cmd, env, timeout, label):
+    """run a child process with a heartbeat on stderr, killing it after
+    `timeout` s; returns (ok, stdout lines that parse as JSON objects, stderr)"""
+    import subprocess
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, start_new_session=True,
+                         stderr=None if os.environ.get("SK_BENCH_VERBOSE") == "1" else subprocess.PIPE)
+    t0, ok = time.time(), False
+    while True:
+        try:
+            out, err = p.communicate(timeout=min(20.0, max(1.0, timeout - (time.time() - t0))))
+            ok = p.returncode == 0
+            break
+        except subprocess.TimeoutExpired:
+            if time.time() - t0 > timeout:
+                try:
+                    os.killpg(p.pid, 9)  # the child's own session: its whole group, nothing else
+                except OSError:
+                    p.kill()
+                out, err = p.communicate()
+                err = (err or "") + f"\n[killed after {timeout:.0f} s]"
+                break
+            _log(f"{label} running {time.time() - t0:.0f} s")
+    res = []
+    for ln in (out or "").splitlines():
+        ln = ln.strip()
+        if ln.startswith("{"):
+            try:
+                res.append(json.loads(ln))
+            except ValueError:
+                pass
+    return ok, res, err or ""
+
+
 def learner_leg_ranks(cfg, world, timeout, leg):
     """run a multi-rank learner leg as one child process per rank; returns
-    rank 0's result (None elsewhere) or raises.  "full" capture (RCCL inside
-    the graph) first; if any rank's child fails, every rank retries with the
-    segmented capture (collectives between graph segments)."""
-    import subprocess
+    rank 0's results (a list, one per tick form; None elsewhere) or raises.
+    "full" capture (RCCL inside the graph) first; if any rank's child fails,
+    every rank retries with the segmented capture (collectives between graph
+    segments) while the leg's timeout lasts."""
     base = int(os.environ.get("MASTER_PORT", "29500"))
     tried = []
+    t_start = time.time()
     for attempt, mode in enumerate(("", "segmented")):
+        left = timeout - (time.time() - t_start)
+        flag = torch.tensor([left], device=torch.device("cuda", torch.cuda.current_device()))
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)  # every rank takes the same decision
+        if float(flag.item()) < 20.0:
+            break
         env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC")}
         env["TORCHELASTIC_USE_AGENT_STORE"] = "False"  # the children's rank 0 hosts their own TCPStore
         env["MASTER_PORT"] = str(base + 11 + 2 * leg + attempt)
-        c = dict(cfg, mode=mode, timeout=timeout)
-        p = subprocess.Popen([sys.executable, os.path.abspath(__file__), "--learner-child", json.dumps(c)],
-                             env=env, stdout=subprocess.PIPE, text=True,
-                             stderr=None if os.environ.get("SK_BENCH_VERBOSE") == "1" else subprocess.PIPE)
-        t0, ok = time.time(), False
-        while True:  # a heartbeat on stderr while the child runs
-            try:
-                out, err = p.communicate(timeout=20)
-                ok = p.returncode == 0
-                break
-            except subprocess.TimeoutExpired:
-                if time.time() - t0 > timeout:
-                    p.kill()
-                    out, err = p.communicate()
-                    break
-                _log(f"learner leg {leg} ({mode or 'auto'}) running {time.time() - t0:.0f} s")
+        c = dict(cfg, mode=mode, timeout=float(flag.item()))
+        ok, res, err = _child([sys.executable, os.path.abspath(__file__), "--learner-child", json.dumps(c)], env,
+                              float(flag.item()), f"learner leg {leg} ({mode or 'auto'})")
         flag = torch.tensor([1.0 if ok else 0.0], device=torch.device("cuda", torch.cuda.current_device()))
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         tried.append(mode or "auto")
         if float(flag.item()) == 1.0:
             if int(os.environ.get("RANK", "0")) == 0:
-                res = json.loads(out.strip().splitlines()[-1])
-                res["capture_attempts"] = tried
+                for r in res:
+                    r["capture_attempts"] = list(tried)
                 return res
             return None
-        if ok is False:
-            sys.stderr.write(f"learner leg {cfg} ({mode or 'auto'}) failed rc={p.returncode}:\n{(err or '')[-3000:]}\n")
-    raise RuntimeError(f"learner leg failed in modes {tried}")
+        if not ok:
+            sys.stderr.write(f"learner leg {cfg} ({mode or 'auto'}) failed:\n{err[-3000:]}\n")
+    raise RuntimeError(f"learner leg failed in modes {tried} (timeout {timeout:.0f} s)")
 
 
 def _guard(name, fn, errors):
@@ -629,10 +701,98 @@ def _guard(name, fn, errors):
         return None
 
 
+def leg_child_main(args, spec):
+    """one one-GPU secondary leg in a child process of the bench (VERDICT r03
+    item 1: a hung or failing leg is killed and reported, the headline line
+    still prints); prints one JSON line per result"""
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    name, n = spec["leg"], spec["n"]
+    if name == "learner":
+        for ov in spec.get("overlaps", [None]):
+            r = learner_rate(spec["envs"], 1, 0, args.learner_ticks, batch=spec["batch"],
+                             exploration=spec["exploration"], precision=spec["precision"], overlap=ov)
+            print(json.dumps(dict(r, overlap=ov)), flush=True)
+        return
+    fn = {"per_tick_launch": lambda: per_tick_rate(dev, args, n), "l2_resident": lambda: l2_rate(dev, args, n),
+          "rollout_random": lambda: rollout_rate(dev, args, n), "full_contract_tick":
+          lambda: full_contract_rate(dev, args, 0, n), "large_batch": lambda: large_batch_rate(dev, args, 0)}[name]
+    print(json.dumps(fn()), flush=True)
+
+
+def run_leg(args, spec, timeout, label):
+    """a one-GPU secondary leg in a child process under `timeout`: its JSON
+    results (list), or raises with the child's stderr tail"""
+    cmd = [sys.executable, os.path.abspath(__file__)] + [a for a in sys.argv[1:]] + ["--leg-child", json.dumps(spec)]
+    env = dict(os.environ)
+    ok, res, err = _child(cmd, env, timeout, label)
+    if not res:
+        raise RuntimeError(f"{label}: no result ({'ok' if ok else 'failed'}): {err[-1500:]}")
+    if not ok:
+        sys.stderr.write(f"{label} ended with an error after {len(res)} result(s):\n{err[-1500:]}\n")
+    return res
+
+
+def per_tick_rate(dev, args, n):
+    """the round-2 headline: one graph-replayed k_step launch per tick"""
+    k2 = 2000
+    ring = max(args.graph_len, args.action_ring)
+    el2, ev2, env2 = timed_ticks(dev, n, args.seed, 0, args.tick_limit, k2, 200, ring, args.graph_len, 1)
+    env2.close()
+    us = ev2 * 1e3 / k2
+    gbs = BYTES_PER_ENV_STEP * n / (us * 1e-6) / 1e9
+    return dict(kernel="k_step (one graph-replayed launch per tick; the round-2 headline)", ticks=k2,
+                us_per_tick=us, env_steps_per_s_per_gpu=n / (us * 1e-6), achieved_gbs=gbs,
+                frac=gbs / HBM_PEAK_GBS)
+
+
+def l2_rate(dev, args, n):
+    """k_step_multi with the plain (L2-resident) state port"""
+    os.environ["SK_MULTI_POLICY"] = "0"
+    ring = max(args.graph_len, args.action_ring)
+    try:
+        k2 = 4000
+        el2, ev2, env2 = timed_multi(dev, n, args.seed, 0, args.tick_limit, k2, 200, ring, 1,
+                                     per_launch=args.ticks_per_launch)
+        env2.close()
+    finally:
+        os.environ["SK_MULTI_POLICY"] = "1"
+    us = ev2 * 1e3 / k2
+    gbs = BYTES_PER_ENV_STEP * n / (us * 1e-6) / 1e9
+    return dict(kernel="k_step_multi<0> (plain state port)", ticks=k2, us_per_tick=us,
+                env_steps_per_s_per_gpu=n / (us * 1e-6), contract_gbs=gbs,
+                note="state stores and reloads stay in the XCD's L2 (PMC: profiles/"
+                     "traffic_k_step_multi_pol0.json), so this is not an HBM-roofline figure")
+
+
+def rollout_rate(dev, args, n):
+    """k_rollout_random: the register-resident random-policy rollout"""
+    from skillshot_learning_amd import VecSkillshotGame
+    g = VecSkillshotGame(n, device=dev, seed=args.seed, env_offset=0, tick_limit=args.tick_limit,
+                         random_positions=True)
+    g.reset(random_positions=True)
+    ticks, reps = 200, 10
+    g.rollout_random(ticks)
+    torch.cuda.synchronize()
+    r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    r0.record()
+    for _ in range(reps):
+        g.rollout_random(ticks)
+    r1.record()
+    torch.cuda.synchronize()
+    g.close()
+    return dict(kernel="k_rollout_random", ticks_per_launch=ticks, envs_per_gpu=n,
+                env_steps_per_s_per_gpu=n * ticks * reps / (r0.elapsed_time(r1) * 1e-3),
+                note="state held in registers across ticks; reported beside, not as, the headline")
+
+
 def main():
     args = parse()
     if args.learner_child:
         learner_child_main(json.loads(args.learner_child))
+        return
+    if args.leg_child:
+        leg_child_main(args, json.loads(args.leg_child))
         return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -684,102 +844,107 @@ def main():
             traffic = None
 
     errors = {}
+    t_legs = time.time()
+
+    def budget_left():
+        """seconds left of --leg-budget (the same figure on every rank)"""
+        left = args.leg_budget - (time.time() - t_legs)
+        if world > 1:
+            tt = torch.tensor([left], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MIN)
+            left = float(tt.item())
+        return left
+
+    def leg(name, spec, timeout):
+        """one secondary leg under min(timeout, the budget left): in a child
+        process at N = 1, in-process per rank at N > 1"""
+        left = budget_left()
+        if left < 15.0:
+            errors[name] = f"skipped: leg budget ({args.leg_budget:.0f} s) spent"
+            return None
+        if verbose:
+            _log(f"leg {name} (timeout {min(timeout, left):.0f} s)")
+        if world == 1:
+            return _guard(name, lambda: run_leg(args, spec, min(timeout, left), name), errors)
+        fn = {"per_tick_launch": lambda: per_tick_rate(dev, args, n), "l2_resident": lambda: l2_rate(dev, args, n),
+              "rollout_random": lambda: rollout_rate(dev, args, n),
+              "full_contract_tick": lambda: full_contract_rate(dev, args, rank, n),
+              "large_batch": lambda: large_batch_rate(dev, args, rank)}[spec["leg"]]
+        r = _guard(name, fn, errors)
+        return None if r is None else [r]
+
+    def one(name, timeout):
+        r = leg(name, {"leg": name, "n": n}, timeout)
+        return r[0] if r else None
+
     variants = None
     if not args.no_variants:
         variants = {"note": "the same step-only contract through the other step kernels, HIP-event timed, "
-                            "reported beside the headline"}
-
-        def _per_tick():
-            k2 = 2000
-            el2, ev2, env2 = timed_ticks(dev, n, args.seed, rank * n, args.tick_limit, k2, 200, ring,
-                                         args.graph_len, 1)
-            env2.close()
-            us = ev2 * 1e3 / k2
-            gbs = BYTES_PER_ENV_STEP * n / (us * 1e-6) / 1e9
-            return dict(kernel="k_step (one graph-replayed launch per tick; the round-2 headline)", ticks=k2,
-                        us_per_tick=us, env_steps_per_s_per_gpu=n / (us * 1e-6), achieved_gbs=gbs,
-                        frac=gbs / HBM_PEAK_GBS)
-
-        def _l2():
-            os.environ["SK_MULTI_POLICY"] = "0"
-            try:
-                k2 = 4000
-                el2, ev2, env2 = timed_multi(dev, n, args.seed, rank * n, args.tick_limit, k2, 200, ring, 1,
-                                             per_launch=args.ticks_per_launch)
-                env2.close()
-            finally:
-                os.environ["SK_MULTI_POLICY"] = "1"
-            us = ev2 * 1e3 / k2
-            gbs = BYTES_PER_ENV_STEP * n / (us * 1e-6) / 1e9
-            return dict(kernel="k_step_multi<0> (plain state port)", ticks=k2, us_per_tick=us,
-                        env_steps_per_s_per_gpu=n / (us * 1e-6), contract_gbs=gbs,
-                        note="state stores and reloads stay in the XCD's L2 (PMC: profiles/"
-                             "traffic_k_step_multi_pol0.json), so this is not an HBM-roofline figure")
-
-        variants["per_tick_launch"] = _guard("step_variants.per_tick_launch", _per_tick, errors)
-        variants["l2_resident"] = _guard("step_variants.l2_resident", _l2, errors)
-    rollout = None
-    if not args.no_rollout:
-        def _rollout():
-            from skillshot_learning_amd import VecSkillshotGame
-            g = VecSkillshotGame(n, device=dev, seed=args.seed, env_offset=rank * n, tick_limit=args.tick_limit,
-                                 random_positions=True)
-            g.reset(random_positions=True)
-            ticks, reps = 200, 10
-            g.rollout_random(ticks)
-            torch.cuda.synchronize()
-            r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            r0.record()
-            for _ in range(reps):
-                g.rollout_random(ticks)
-            r1.record()
-            torch.cuda.synchronize()
-            g.close()
-            return dict(kernel="k_rollout_random", ticks_per_launch=ticks, envs_per_gpu=n,
-                        env_steps_per_s_per_gpu=n * ticks * reps / (r0.elapsed_time(r1) * 1e-3),
-                        note="state held in registers across ticks; reported beside, not as, the headline")
-        rollout = _guard("rollout_random", _rollout, errors)
-
-    if verbose:
-        _log("secondary legs")
-    full = None if args.no_full else _guard("full_contract_tick", lambda: full_contract_rate(dev, args, rank, n),
-                                            errors)
-    large = None if args.no_large else _guard("large_batch", lambda: large_batch_rate(dev, args, rank), errors)
+                            "reported beside the headline",
+                    "per_tick_launch": one("per_tick_launch", args.leg_timeout),
+                    "l2_resident": one("l2_resident", args.leg_timeout)}
+    rollout = None if args.no_rollout else one("rollout_random", args.leg_timeout)
+    full = None if args.no_full else one("full_contract_tick", args.leg_timeout)
+    large = None if args.no_large else one("large_batch", args.leg_timeout)
     weak = None
-    if world > 1 and not args.no_weak:
+    if world > 1 and not args.no_weak and budget_left() >= 15.0:
         weak = _guard("weak_scaling", lambda: weak_rate(dev, args, rank, world), errors)
 
     # ---- the DDPG learner in the loop: configs 3 / 5 on one GPU; configs 4
     # (32,768 games over the ranks, gradient all-reduce) and 5 (65,536, param
-    # noise, shared-replay all-gather) at N > 1
+    # noise, shared-replay all-gather) at N > 1.  Every leg reports the
+    # reference-order tick (the update draws after the tick's insert); the
+    # opt-in overlapped tick (one tick late) is reported beside it.
     learner = None
+    overlaps = [None] if args.no_overlapped else [None, "auto"]
+
+    def forms(res):
+        """a leg's results: the reference-order tick, the overlapped beside"""
+        if not res:
+            return None
+        main_r = next((r for r in res if r.get("overlap") is None), None)
+        ovl = next((r for r in res if r.get("overlap") == "auto"), None)
+        if main_r is None:
+            return dict(ovl, note="the reference-order run did not report") if ovl else None
+        if ovl is not None:
+            main_r["overlapped"] = {k: ovl.get(k) for k in ("tick_mode", "draw_order", "gpu_ms_per_tick",
+                                                           "ms_per_tick", "env_steps_per_s", "capture_attempts")}
+        return main_r
+
     if not args.no_learner:
         T = args.learner_ticks
         learner = {"note": "actor + env step + replay insert/sample + critic/actor update per tick, graph-replayed; "
-                           "reported beside, not as, the headline"}
+                           "reported beside, not as, the headline.  The leg's figures are the reference-order "
+                           "tick (tick_mode sequential: the update samples after the tick's insert); "
+                           "`overlapped` is the opt-in overlapped tick (one tick late).  bf16 is an opt-in "
+                           "precision, reported where it is faster (config 5)"}
         if world == 1:
-            for prec in ("fp32", "bf16"):
-                learner[f"config3_{prec}"] = _guard(f"learner.config3_{prec}", lambda: learner_rate(
-                    4096, 1, 0, T, batch=256, exploration="action_noise", precision=prec), errors)
-            for prec in ("fp32", "bf16"):
-                learner[f"config5_1gpu_{prec}"] = _guard(f"learner.config5_1gpu_{prec}", lambda: learner_rate(
-                    65536, 1, 0, T, batch=256, exploration="param_noise", precision=prec), errors)
+            legs = (("config3_fp32", dict(envs=4096, exploration="action_noise", precision="fp32")),
+                    ("config5_1gpu_fp32", dict(envs=65536, exploration="param_noise", precision="fp32")),
+                    ("config5_1gpu_bf16", dict(envs=65536, exploration="param_noise", precision="bf16")))
+            for name, cfg in legs:
+                spec = dict(cfg, leg="learner", n=n, batch=256, overlaps=overlaps)
+                learner[name] = forms(leg(f"learner.{name}", spec, args.learner_timeout))
         else:
             # every leg at the reference's fp32 (Keras) precision; config 5 at
-            # bf16 beside it (the bf16 leg alone was narrower
-            # than the reference)
+            # bf16 beside it
+            T = args.learner_ticks
             legs = (("config4", dict(envs=32768 // world, batch=256, exploration="action_noise", precision="fp32",
-                                     multi_rank="grad", ticks=T)),
+                                     multi_rank="grad", ticks=T, overlaps=overlaps)),
                     ("config5", dict(envs=65536 // world, batch=256, exploration="param_noise", precision="fp32",
-                                     multi_rank="shared", ticks=T)),
+                                     multi_rank="shared", ticks=T, overlaps=overlaps)),
                     ("config5_bf16", dict(envs=65536 // world, batch=256, exploration="param_noise",
-                                          precision="bf16", multi_rank="shared", ticks=T)))
+                                          precision="bf16", multi_rank="shared", ticks=T, overlaps=[None])))
             for k, (name, cfg) in enumerate(legs):
                 dist.barrier()
+                left = budget_left()
+                if left < 30.0:
+                    errors[f"learner.{name}"] = f"skipped: leg budget ({args.leg_budget:.0f} s) spent"
+                    continue
                 if verbose:
                     _log(f"learner {name}")
-                learner[name] = _guard(f"learner.{name}", lambda: learner_leg_ranks(cfg, world, args.learner_timeout,
-                                                                                    k), errors)
+                learner[name] = forms(_guard(f"learner.{name}", lambda: learner_leg_ranks(
+                    cfg, world, min(args.learner_timeout, left), k), errors))
 
     cpu = None
     if world == 1 and not args.no_cpu_baseline:  # N=1 only (the CPU baseline is a per-box figure)

@@ -410,7 +410,7 @@ class DDPG:
     Per-rank update work is `batch` rows whatever the world size."""
 
     def __init__(self, device="cpu", seed=0, batch_size=16, gamma=0.0, tau=None, replay_capacity=0,
-                 process_group=None, rank_seed_offset=0, fused_update=None, multi_rank="grad", precision="bf16",
+                 process_group=None, rank_seed_offset=0, fused_update=None, multi_rank="grad", precision="fp32",
                  force_collectives=False):
         self.device = torch.device(device)
         torch.manual_seed(seed)
@@ -722,7 +722,7 @@ class SkillshotLearner:
 
     def __init__(self, n_envs=1, device="cuda", seed=0, env_offset=0, exploration="param_noise",
                  tick_limit=2000, use_random_start=True, replay_capacity=1 << 20, batch_size=16,
-                 gamma=0.0, tau=None, actor_kernel=True, process_group=None, precision="bf16",
+                 gamma=0.0, tau=None, actor_kernel=True, process_group=None, precision="fp32",
                  multi_rank="grad", force_collectives=False):
         from .vec_env import VecSkillshotGame
         if precision not in ("bf16", "fp32"):
@@ -933,7 +933,7 @@ class SkillshotLearner:
             self._refresh_actor_pack()
         return stats
 
-    def tick_graph(self, batch=256, updates_per_tick=1, ticks_per_graph=2, warmup=3):
+    def tick_graph(self, batch=256, updates_per_tick=1, ticks_per_graph=2, warmup=3, overlap=None):
         """The replay-rule tick of `train_ticks` captured as ONE hipGraph.
 
         One replay runs `ticks_per_graph` ticks (even: the engine's device step
@@ -954,17 +954,20 @@ class SkillshotLearner:
         between them (any backend, e.g. gloo).  Default: "full" for nccl,
         "segmented" otherwise; SK_TICKGRAPH_MODE overrides.
 
-        One rank from TICK_OVERLAP_MIN_ENVS games (SK_TICK_OVERLAP): the acting
-        launches run beside the update on a second stream; below that (and
-        with multi_rank "grad") with the fp32 kernels, inside the critic's
-        backward launch.  Either way the update draws from the rows inserted
-        before the tick (TickGraph.overlap).
+        The tick form (tick_form; overlap= or SK_TICK_OVERLAP): by default the
+        sequential tick in the reference's order (the update draws after the
+        tick's insert).  overlap="auto" opts into the overlapped ticks: from
+        TICK_OVERLAP_MIN_ENVS games on one rank the acting launches run beside
+        the update on a second stream; below that (and with multi_rank "grad")
+        with the fp32 kernels, inside the critic's backward launch.  Either way
+        the overlapped update draws from the rows inserted before the tick
+        (TickGraph.overlap), one tick later than the reference.
         """
         if self.device.type != "cuda":
             raise RuntimeError("tick_graph needs the GPU engine")
         if ticks_per_graph % 2:
             raise ValueError("ticks_per_graph must be even (step-counter ping-pong slots)")
-        return TickGraph(self, batch, updates_per_tick, ticks_per_graph, warmup)
+        return TickGraph(self, batch, updates_per_tick, ticks_per_graph, warmup, overlap)
 
     # ------------------------------------------------------------ persistence
     def state_dict(self):
@@ -1007,14 +1010,19 @@ def tick_form(n, batch, capacity, updates_per_tick, multi, fused, f32, fused_act
     (the acting launches on a second stream beside the update), "fused" (the
     acting launch inside the critic gradient's backward launch) or "serial"
     (the streams form on one stream, a test reference); see TickGraph.
-    SK_TICK_OVERLAP = auto (default) / 0 / 1 / fused / serial; the overlapped
-    forms need the fused update path, one update per tick, the default
+    SK_TICK_OVERLAP (or tick_graph's overlap=) = 0 (default: the reference's
+    draw order, the update sampling the ring after the tick's insert,
+    SkillshotLearner.py:316-324) / auto (the overlapped form this function
+    picks: streams from TICK_OVERLAP_MIN_ENVS games, else fused where it can)
+    / 1 / fused / serial.  The overlapped forms draw the minibatch from the
+    ring as it stood before the tick's insert (one tick later than the
+    reference; ADVICE r03: opt-in only).  They need the fused update path, one update per tick, the default
     replay mode (SK_FUSED_REPLAY=2) and a ring holding a batch beside the rows
     one insert writes; "fused" the fp32 kernels with the fused act + step
     launch (SK_FUSED_ACT), N % 4 == 0 and the sliced update schedule; several
     ranks run "fused" or "sequential"."""
     env = os.environ if env is None else env
-    ov = env.get("SK_TICK_OVERLAP", "auto")
+    ov = str(env.get("SK_TICK_OVERLAP", "0"))
     can = (fused and updates_per_tick == 1 and capacity >= batch + 4 * n
            and env.get("SK_FUSED_REPLAY", "2") == "2")
     can_fuse = can and f32 and fused_act and n % 4 == 0 and env.get("SK_FUSED_ACT", "1") != "0" and sliced
@@ -1030,7 +1038,7 @@ def tick_form(n, batch, capacity, updates_per_tick, multi, fused, f32, fused_act
 class TickGraph:
     """Captured replay-rule ticks (see SkillshotLearner.tick_graph)."""
 
-    def __init__(self, L, batch, updates_per_tick, ticks_per_graph, warmup):
+    def __init__(self, L, batch, updates_per_tick, ticks_per_graph, warmup, overlap=None):
         self.L, self.batch, self.updates, self.ticks = L, batch, updates_per_tick, ticks_per_graph
         self.multi_rank_mode = None
         if L.ddpg.multi():
@@ -1080,7 +1088,8 @@ class TickGraph:
         fu = L.ddpg._fused
         self.mode = tick_form(n, batch, L.replay.cap, updates_per_tick, L.ddpg.multi(), fu is not None,
                               fu is not None and fu.f32, getattr(L.actor_kernel, "fused_act_step", False),
-                              fu is not None and fu.sliced(batch))
+                              fu is not None and fu.sliced(batch),
+                              env=dict(os.environ, **({} if overlap is None else {"SK_TICK_OVERLAP": str(overlap)})))
         self.overlap = self.mode != "sequential"
         self.fuse_act = self.mode == "fused"
         self.side = torch.cuda.Stream(device=dev) if self.mode == "streams" else None

@@ -159,7 +159,7 @@ def test_action_noise_in_kernel(mods, rows):
 
 def test_learner_replay_training_runs(mods):
     learner, _ = mods
-    L = learner.SkillshotLearner(n_envs=2048, seed=1, tick_limit=300, replay_capacity=1 << 16, gamma=0.9, tau=0.005)
+    L = learner.SkillshotLearner(n_envs=2048, seed=1, tick_limit=300, replay_capacity=1 << 16, gamma=0.9, tau=0.005, precision="bf16")
     # games start their first episode in the learner's start mode (random)
     pos = L.game_environment.state_dict()["pos"]
     assert torch.unique(torch.as_tensor(pos), dim=0).shape[0] > 1900
@@ -175,7 +175,7 @@ def test_learner_reference_epochs(mods):
     """model_train with the reference update rule (batch 16, one pass) on a few
     games with a short tick limit (SkillshotLearner.main uses 200, :688)."""
     learner, _ = mods
-    L = learner.SkillshotLearner(n_envs=4, seed=2, tick_limit=60, exploration="param_noise")
+    L = learner.SkillshotLearner(n_envs=4, seed=2, tick_limit=60, exploration="param_noise", precision="bf16")
     before = [p.detach().clone() for p in L.model_actor.parameters()]
     prog = L.model_train(epochs=2)
     assert len(prog["epoch_ticks"]) == 2
@@ -195,7 +195,7 @@ def test_model_train_saves_progress_boards_models(mods, tmp_path):
     import numpy as np
     from skillshot_learning_amd.game import rasterize_board
     learner, _ = mods
-    L = learner.SkillshotLearner(n_envs=1, seed=4, tick_limit=40)  # one game, as the reference plays
+    L = learner.SkillshotLearner(n_envs=1, seed=4, tick_limit=40, precision="bf16")  # one game, as the reference plays
     L.save_location = str(tmp_path / "training_models")
     prog = L.model_train(epochs=2, save_progress=True, save_boards=True)
     df = L.load_training_progress()
@@ -223,7 +223,7 @@ def test_learner_reference_epochs_full_reward(mods):
     """model_train with the alternative reward functions (:324-326)."""
     learner, _ = mods
     for reward in ("full", "simple"):
-        L = learner.SkillshotLearner(n_envs=8, seed=4, tick_limit=80, exploration="param_noise")
+        L = learner.SkillshotLearner(n_envs=8, seed=4, tick_limit=80, exploration="param_noise", precision="bf16")
         before = [p.detach().clone() for p in L.model_critic.parameters()]
         prog = L.model_train(epochs=1, reward=reward)
         assert len(prog["epoch_ticks"]) == 1
@@ -235,7 +235,7 @@ def test_tick_graph_replays_train(mods):
     """The replay-rule tick captured as one hipGraph: replays keep inserting
     at the device-side head, draw fresh parameter noise and keep training."""
     learner, _ = mods
-    L = learner.SkillshotLearner(n_envs=1024, seed=6, tick_limit=300, replay_capacity=1 << 14, gamma=0.9, tau=0.01)
+    L = learner.SkillshotLearner(n_envs=1024, seed=6, tick_limit=300, replay_capacity=1 << 14, gamma=0.9, tau=0.01, precision="bf16")
     tg = L.tick_graph(batch=256, updates_per_tick=1, ticks_per_graph=2)
     size0 = int(L.replay.size_t)
     head0 = int(L.replay.head_t)

@@ -20,10 +20,13 @@ def learner_mod():
     return learner
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
 @pytest.mark.parametrize("exploration", ["action_noise", "param_noise"])
-def test_config3_tick_graph(learner_mod, exploration):
+def test_config3_tick_graph(learner_mod, exploration, precision):
+    """fp32 (the reference's precision, the learner's default) and the bf16
+    opt-in, each in the tick form the learner picks by default"""
     L = learner_mod.SkillshotLearner(n_envs=N, device="cuda", seed=21, exploration=exploration, gamma=0.99,
-                                     tau=0.005, replay_capacity=CAP)
+                                     tau=0.005, replay_capacity=CAP, precision=precision)
     tg = L.tick_graph(batch=BATCH, ticks_per_graph=2, warmup=2)
     g = L.game_environment
     total0 = int(L.replay.total_t)

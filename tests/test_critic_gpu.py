@@ -116,7 +116,7 @@ def test_ddpg_target_uses_fused_kernel(mods, fused_update):
     moved the targets inside their Adam launches) against the torch target
     nets."""
     learner, _, _ = mods
-    d = learner.DDPG("cuda", seed=4, gamma=0.9, tau=0.05, replay_capacity=4096, fused_update=fused_update)
+    d = learner.DDPG("cuda", seed=4, gamma=0.9, tau=0.05, replay_capacity=4096, fused_update=fused_update, precision="bf16")
     g = torch.Generator(device="cuda").manual_seed(0)
     for _ in range(4):
         d.replay.add(torch.rand(512, 12, device="cuda", generator=g), torch.rand(512, 2, device="cuda") * 2 - 1,

@@ -199,16 +199,23 @@ def test_cpu_backend_step_insert_equals_step_then_add(ssa):
 
 
 def test_tick_form_selection():
-    """TickGraph's tick form (learner.tick_form): the auto policy (streams
+    """TickGraph's tick form (learner.tick_form): sequential by default; the
+    opt-in auto policy (streams
     from 16,384 games on one rank, fused below with the fp32 kernels, fused or
     sequential on several ranks) and the SK_TICK_OVERLAP overrides"""
     from skillshot_learning_amd.learner import tick_form
+
+    # the default is the reference's order (ADVICE r03): the overlapped forms
+    # are opt-in
+    assert tick_form(4096, 256, 1 << 20, 1, False, True, True, True, True, env={}) == "sequential"
+    assert tick_form(65536, 256, 1 << 20, 1, False, True, True, True, True, env={}) == "sequential"
+    assert tick_form(4096, 256, 1 << 20, 1, True, True, True, True, True, env={}) == "sequential"
 
     def f(n, env=None, multi=False, f32=True, batch=256, cap=1 << 20, **kw):
         args = dict(updates_per_tick=1, fused=True, fused_act=True, sliced=True)
         args.update(kw)
         return tick_form(n, batch, cap, args["updates_per_tick"], multi, args["fused"], f32, args["fused_act"],
-                         args["sliced"], env=env or {})
+                         args["sliced"], env=dict({"SK_TICK_OVERLAP": "auto"}, **(env or {})))
     assert f(4096) == "fused" and f(65536) == "streams" and f(16384) == "streams"
     assert f(4096, f32=False) == "sequential" and f(65536, f32=False) == "streams"
     assert f(4096, multi=True) == "fused" and f(65536, multi=True) == "fused"

@@ -220,15 +220,18 @@ def test_f32_replay_updates_match_keras(mods, sched):
                 assert err <= PARAM_ABS, (it, name, err)
 
 
-def test_f32_learner_tick_graph(mods):
+@pytest.mark.parametrize("overlap", ["0", "auto"])
+def test_f32_learner_tick_graph(mods, overlap):
     """config 3 at the reference's precision: the captured learner tick with
     the fp32 kernels (actor forward with parameter noise, fused step, replay,
-    fp32 critic / actor steps) runs, trains and stays finite"""
+    fp32 critic / actor steps) runs, trains and stays finite, in the
+    reference-order tick (default) and the opt-in overlapped (fused) one"""
     learner, _ = mods
     L = learner.SkillshotLearner(n_envs=4096, device="cuda", seed=23, exploration="param_noise", gamma=0.99,
                                  tau=0.005, replay_capacity=1 << 20, precision="fp32")
     assert L.ddpg._fused.f32
-    tg = L.tick_graph(batch=256, ticks_per_graph=2, warmup=2)
+    tg = L.tick_graph(batch=256, ticks_per_graph=2, warmup=2, overlap=overlap)
+    assert tg.mode == ("sequential" if overlap == "0" else "fused")
     w0 = [p.clone() for p in L.model_actor.parameters()]
     c0 = int(L.actor_kernel._ctr[0])
     tg.run(50)

@@ -21,7 +21,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, mode, precision, q):
+def _worker(rank, world, port, mode, precision, overlap, q):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -31,10 +31,11 @@ def _worker(rank, world, port, mode, precision, q):
         n = 512
         L = SkillshotLearner(n_envs=n, device="cuda", seed=31, env_offset=rank * n, exploration="param_noise",
                              gamma=0.9, tau=0.05, replay_capacity=1 << 14, multi_rank=mode, precision=precision)
-        tg = L.tick_graph(batch=64, ticks_per_graph=2, warmup=2)
+        tg = L.tick_graph(batch=64, ticks_per_graph=2, warmup=2, overlap=overlap)
         assert tg.multi_rank_mode == f"{mode}/segmented"
-        # fp32 runs the fused overlapped tick on every rank
-        assert tg.mode == ("fused" if precision == "fp32" else "sequential")
+        # the reference-order tick by default; opted in, fp32 runs the fused
+        # overlapped tick on every rank
+        assert tg.mode == ("fused" if precision == "fp32" and overlap == "auto" else "sequential")
         tg.run(4)
         torch.cuda.synchronize()
         flat = torch.cat([p.detach().reshape(-1) for m in (L.model_actor, L.model_critic, L.ddpg.target_actor,
@@ -49,15 +50,16 @@ def _worker(rank, world, port, mode, precision, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode,precision", [("grad", "fp32"), ("shared", "bf16"), ("shared", "fp32")])
-def test_two_rank_tick_graph_gloo(mode, precision):
+@pytest.mark.parametrize("mode,precision,overlap", [("grad", "fp32", "0"), ("grad", "fp32", "auto"),
+                                                    ("shared", "bf16", "0"), ("shared", "fp32", "auto")])
+def test_two_rank_tick_graph_gloo(mode, precision, overlap):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import multiprocessing as mp
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, precision, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, precision, overlap, q)) for r in range(world)]
     for p in procs:
         p.start()
     out = {}

@@ -73,7 +73,7 @@ def test_sample_gathers_consistent_rows(learner):
 
 def test_fused_target_matches_unfused(learner):
     torch.manual_seed(3)
-    d = learner.DDPG("cuda", seed=3, gamma=0.9, tau=0.01)
+    d = learner.DDPG("cuda", seed=3, gamma=0.9, tau=0.01, precision="bf16")
     s2 = torch.rand(777, 12, device="cuda")
     r = torch.randn(777, device="cuda")
     done = (torch.rand(777, device="cuda") < 0.3).float()
@@ -111,7 +111,7 @@ def test_tick_graph_fused_replay_equals_two_launches(learner, monkeypatch):
     for fused in ("1", "0"):
         monkeypatch.setenv("SK_FUSED_REPLAY", fused)
         L = learner.SkillshotLearner(n_envs=256, device="cuda", seed=5, exploration="action_noise", gamma=0.9,
-                                     tau=0.05, replay_capacity=4096)
+                                     tau=0.05, replay_capacity=4096, precision="bf16")
         tg = L.tick_graph(batch=128, ticks_per_graph=2, warmup=2)
         tg.run(10)
         torch.cuda.synchronize()
@@ -318,6 +318,23 @@ def test_overlap_sample_excludes_rows_being_written(learner):
     lo = total - min(total, cap - E)  # the oldest row id still eligible
     assert int(got.min()) >= lo and int(got.max()) < total
     assert got.unique().numel() > 0.9 * (cap - E)  # uniform over the eligible rows
+    # the overlapped draw's window is exactly the sequential
+    # (reference-order) tick's window minus the E rows that tick inserts.
+    # The sequential tick draws after its insert, keyed on count + E with no
+    # exclusion: rows [count + E - min(count + E, cap), count + E)
+    ids = torch.arange(E, device="cuda", dtype=torch.float32) + total
+    ring.add_dev(ids[:, None].expand(E, 12).contiguous(), torch.zeros(E, 2, device="cuda"),
+                 torch.zeros(E, device="cuda"), torch.zeros(E, 12, device="cuda"), torch.zeros(E, device="cuda"))
+    d._fused.critic_step_sampled(ring, B, exclude=0)
+    seq = ring._batch_bufs(B)[0][:, 0].long()
+    torch.cuda.synchronize()
+    after = int(ring.total_t)
+    assert after == total + E
+    seq_window = set(range(after - min(after, cap), after))
+    assert set(seq.tolist()) <= seq_window
+    over_window = set(range(lo, total))
+    assert over_window == seq_window - set(range(total, total + E))
+    assert set(got.tolist()) <= over_window
 
 
 @pytest.mark.parametrize("batch", [128, 1024])  # sliced schedule (one shared launch) / not (two launches)

@@ -29,7 +29,7 @@ def mods():
 
 
 def _ddpg(learner, seed=0, scale=2.0, tau=None):
-    d = learner.DDPG("cuda", seed=seed, tau=tau, fused_update=True)
+    d = learner.DDPG("cuda", seed=seed, tau=tau, fused_update=True, precision="bf16")
     with torch.no_grad():  # non-trivial weights and biases
         for m in (d.model_actor, d.model_critic):
             for l in (m.l1, m.l2, m.l3):
@@ -174,7 +174,7 @@ def test_adam_and_soft_update_match_torch(mods):
     learner = mods
     torch.manual_seed(0)
     d = _ddpg(learner, seed=3, tau=0.05)
-    ref = learner.DDPG("cuda", seed=3, tau=0.05, fused_update=False)
+    ref = learner.DDPG("cuda", seed=3, tau=0.05, fused_update=False, precision="bf16")
     ref.model_critic.load_state_dict(d.model_critic.state_dict())
     ref.target_critic.load_state_dict(d.target_critic.state_dict())
     st = d._fused.sc
@@ -213,7 +213,7 @@ def test_fused_replay_update_trains(mods):
     losses = {}
     for fused in (True, False):
         torch.manual_seed(5)
-        d = learner.DDPG("cuda", seed=5, tau=0.01, gamma=0.0, replay_capacity=4096, fused_update=fused)
+        d = learner.DDPG("cuda", seed=5, tau=0.01, gamma=0.0, replay_capacity=4096, fused_update=fused, precision="bf16")
         s = _obs(4096)
         a = torch.rand(4096, 2, device="cuda") * 2 - 1
         r = -(s[:, 0] - 0.5).abs() - 0.3 * a[:, 0]  # a learnable immediate reward
@@ -234,7 +234,7 @@ def test_fused_tick_graph(mods):
     """The learner tick (act, step, insert, fused update) still captures and
     replays as one hipGraph."""
     learner = mods
-    L = learner.SkillshotLearner(n_envs=256, device="cuda", seed=9, gamma=0.9, tau=0.01, replay_capacity=1 << 14)
+    L = learner.SkillshotLearner(n_envs=256, device="cuda", seed=9, gamma=0.9, tau=0.01, replay_capacity=1 << 14, precision="bf16")
     assert L.ddpg._fused is not None
     g = L.tick_graph(batch=256, ticks_per_graph=2, warmup=2)
     w0 = [p.clone() for p in L.model_actor.parameters()]
@@ -250,7 +250,7 @@ def test_adam_launches_keep_every_pack_current(mods):
     target grad packs and the actor forward pack equal, byte for byte, full
     packs made from the parameters."""
     learner = mods
-    L = learner.SkillshotLearner(n_envs=256, device="cuda", seed=4, gamma=0.9, tau=0.05, replay_capacity=1 << 14)
+    L = learner.SkillshotLearner(n_envs=256, device="cuda", seed=4, gamma=0.9, tau=0.05, replay_capacity=1 << 14, precision="bf16")
     fu = L.ddpg._fused
     assert fu.fwd_pack is L.actor_kernel.buf
     w0 = [p.clone() for p in L.model_actor.parameters()]
@@ -284,7 +284,7 @@ def _rank_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from skillshot_learning_amd import learner
-        d = learner.DDPG("cuda", seed=200 + rank, tau=0.05, rank_seed_offset=rank, fused_update=True)
+        d = learner.DDPG("cuda", seed=200 + rank, tau=0.05, rank_seed_offset=rank, fused_update=True, precision="bf16")
         w0 = torch.cat([p.detach().reshape(-1) for p in d.model_critic.parameters()]).cpu()
         g = torch.Generator(device="cuda").manual_seed(rank)  # different data per rank
         for _ in range(3):
@@ -349,7 +349,7 @@ def test_load_state_dict_rebinds_fused_adam(mods):
     the LOADED moments and step counts (the optimiser's state tensors are
     views of the flat buffers the kernels read)."""
     learner = mods
-    L = learner.SkillshotLearner(n_envs=256, device="cuda", seed=12, gamma=0.9, tau=0.05, replay_capacity=1 << 14)
+    L = learner.SkillshotLearner(n_envs=256, device="cuda", seed=12, gamma=0.9, tau=0.05, replay_capacity=1 << 14, precision="bf16")
     L.train_ticks(6, batch=256)
     sd = {k: ({kk: (vv.cpu().clone() if torch.is_tensor(vv) else vv) for kk, vv in v.items()}
               if isinstance(v, dict) and k not in ("actor_opt", "critic_opt") else v)

@@ -44,7 +44,7 @@ def main():
     torch.manual_seed(0)
     actor, critic = learner.Actor().cuda(), learner.Critic().cuda().eval()
     ak, ck, tk = ActorKernel(actor, seed=1), CriticKernel(critic), TargetQKernel(actor, critic)
-    ddpg = learner.DDPG("cuda", seed=0, fused_update=True)
+    ddpg = learner.DDPG("cuda", seed=0, fused_update=True, precision="bf16")
     fu = ddpg._fused
     st = torch.cuda.Stream()
     for rows in [int(r) for r in a.rows.split(",")]:

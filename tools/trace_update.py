@@ -52,7 +52,7 @@ def main():
     p.add_argument("--rows", default="256,4096")
     a = p.parse_args()
     from skillshot_learning_amd import learner, _capi
-    ddpg = learner.DDPG("cuda", seed=0, fused_update=True)
+    ddpg = learner.DDPG("cuda", seed=0, fused_update=True, precision="bf16")
     fu = ddpg._fused
     L = fu.L
     L.sk_debug_update_trace.argtypes = [ctypes.c_void_p]
