@@ -390,31 +390,93 @@ def large_batch_rate(dev, args, rank, n=1 << 22, launches=60, ring=8):
                 note="state 369 MB > Infinity Cache: the HBM-bound regime; reported beside, not as, the headline")
 
 
-def full_contract_rate(dev, args, rank, n, launches=2000):
+def timed_multi_obs(dev, n, seed, env_offset, tick_limit, k, warmup, ring, out_slabs, per_launch=400):
+    """k ticks of the FULL contract (obs + reward + done of the post-tick
+    state, random auto-reset; 297 B per env-step) through
+    sk_env_step_multi_obs: launches of at most `per_launch` ticks, actions
+    from the HBM ring, outputs into a ring of `out_slabs` slabs (larger than
+    the Infinity Cache at the metric's size, so the written bytes go to
+    HBM).  Returns (wall s, HIP-event ms on the launch stream, env)."""
+    env, st, acts = _env_and_actions(dev, n, seed, env_offset, tick_limit, ring)
+    sp = ctypes.c_void_p(st.cuda_stream)
+    obs = torch.empty((out_slabs, 2, n, 12), dtype=torch.float32, device=dev)
+    rew = torch.empty((out_slabs, 2, n), dtype=torch.float32, device=dev)
+    done = torch.empty((out_slabs, n), dtype=torch.uint8, device=dev)
+    ap = ctypes.c_void_p(acts.data_ptr())
+    op, rp_, dp = (ctypes.c_void_p(t.data_ptr()) for t in (obs, rew, done))
+    fn, h, lim, rpos = env._L.sk_env_step_multi_obs, env._h, env.tick_limit, int(env.random_positions)
+    slab, so = 0, 0
+
+    def run(m):
+        nonlocal slab, so
+        while m > 0:
+            t = min(m, per_launch)
+            rc = fn(h, ap, ring, slab, t, op, rp_, 0, dp, None, out_slabs, so, lim, 1, rpos, sp)
+            if rc:
+                _capi_check(rc)
+            slab = (slab + t) % ring
+            so = (so + t) % out_slabs
+            m -= t
+
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    e1.record(st)
+    run(1)
+    st.synchronize()
+    env.clear_counters(stream=sp)
+    run(warmup)
+    st.synchronize()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record(st)
+    run(k)
+    e1.record(st)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    env.bench_stream = st
+    return el, e0.elapsed_time(e1), env
+
+
+def full_contract_rate(dev, args, rank, n, ticks=2000):
     """The learner's env tick (SkillshotLearner.py:302-324): actions in, state
     stepped, obs + reward of the post-tick state and done out, random
-    auto-reset — 297 B per env-step (SURVEY §8(d) full contract); the auto
-    variant picks k_step_split when observations are written."""
-    el, ev, env = timed_ticks(dev, n, args.seed + 3, rank * n, args.tick_limit, launches, 200, args.action_ring,
-                              args.graph_len, 1, obs=True)
+    auto-reset — 297 B per env-step (SURVEY §8(d) full contract).  The
+    multi-tick kernel (sk_env_step_multi_obs, k_step_split_multi<1, *, true>:
+    400 ticks per launch, every tick's state loaded and stored write-through,
+    obs / reward into a 64-slab output ring) is the leg's figure; one
+    graph-replayed k_step_split launch per tick (the round-3 figure) beside it."""
+    out_slabs = 64
+    el, ev, env = timed_multi_obs(dev, n, args.seed + 3, rank * n, args.tick_limit, ticks, 200, args.action_ring,
+                                  out_slabs, per_launch=args.ticks_per_launch)
+    counters = env.counters(stream=ctypes.c_void_p(env.bench_stream.cuda_stream))
     env.close()
-    us = ev * 1e3 / launches
+    torch.cuda.empty_cache()
+    us = ev * 1e3 / ticks
     gbs = BYTES_FULL_CONTRACT * n / (us * 1e-6) / 1e9
-    traffic = None
-    tj = os.path.join(ROOT, "profiles", "traffic_k_step_split.json")
+    traffic, traffic_src = None, None
+    tj = os.path.join(ROOT, "profiles", "traffic_k_step_split_multi_obs.json")
     if os.path.exists(tj):
         try:
             t = json.load(open(tj))
-            traffic = t.get("hbm_bytes_per_launch") if t.get("envs") == n else None
+            if t.get("envs") == n:
+                traffic, traffic_src = t.get("hbm_bytes_per_tick"), os.path.relpath(tj, ROOT)
         except Exception:
             traffic = None
-    return dict(envs_per_gpu=n, kernel="k_step_split (auto variant with obs)", launches=launches,
-                us_per_launch=us, env_steps_per_s_per_gpu=n / (us * 1e-6),
+    # beside it: one launch per tick (k_step_split through the graph path)
+    el1, ev1, env1 = timed_ticks(dev, n, args.seed + 3, rank * n, args.tick_limit, ticks, 200, args.action_ring,
+                                 args.graph_len, 1, obs=True)
+    env1.close()
+    us1 = ev1 * 1e3 / ticks
+    gbs1 = BYTES_FULL_CONTRACT * n / (us1 * 1e-6) / 1e9
+    return dict(envs_per_gpu=n, kernel="k_step_split_multi<1, *, true> (sk_env_step_multi_obs)", ticks=ticks,
+                ticks_per_launch=min(ticks, args.ticks_per_launch), us_per_launch=us, us_per_tick=us,
+                env_steps_per_s_per_gpu=n / (us * 1e-6), wall_env_steps_per_s=n * ticks / el, episodes=counters,
                 roofline=dict(bound="hbm", achieved=gbs, peak=HBM_PEAK_GBS, unit="GB/s", frac=gbs / HBM_PEAK_GBS,
-                              traffic=traffic,
-                              traffic_source="profiles/traffic_k_step_split.json (rocprofv3 --pmc pass, not this run)",
+                              traffic=traffic, traffic_source=traffic_src or "not measured for this kernel yet",
                               bytes_per_env_step=BYTES_FULL_CONTRACT,
-                              bytes="state 88 read + 88 written, actions 16, obs 96, reward 8, done 1"))
+                              bytes="state 88 read + 88 written, actions 16, obs 96, reward 8, done 1"),
+                per_tick_launch=dict(kernel="k_step_split (one graph-replayed launch per tick)", us_per_tick=us1,
+                                     env_steps_per_s_per_gpu=n / (us1 * 1e-6), frac=gbs1 / HBM_PEAK_GBS))
 
 
 def weak_rate(dev, args, rank, world, n=65536, ticks=4000):

@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define SK_ABI_VERSION 8
+#define SK_ABI_VERSION 9
 
 enum {
   SK_OK = 0,
@@ -283,6 +283,24 @@ int sk_env_act_step_job(sk_env* env, const float* actor_flat, const float* actin
 int sk_env_step_multi(sk_env* env, const float* actions, int64_t ring_slabs, int64_t slab0, int32_t n_ticks,
                       uint8_t* done, uint8_t* winner, int64_t out_stride, int32_t tick_limit, int32_t auto_reset,
                       int32_t random_positions, void* stream);
+
+/* n_ticks ticks of the FULL contract in ONE launch (ABI 9; the learner's
+ * per-tick protocol SkillshotLearner.py:302-324 with the actions given:
+ * do_actions :206-213, game_tick SkillshotGame.py:115-122, prepare_states
+ * :512-543 of the post-tick state, the reward (reward_kind SK_REWARD_LOOKING,
+ * calculate_rewards_looking :575-588, or SK_REWARD_SIMPLE, :590-603), done
+ * :302 and the auto-reset :291): equal, bit for bit, to n_ticks calls of
+ * sk_env_step(obs, reward, obs_reset = NULL, done, winner) where tick t acts
+ * on action slab (slab0 + t) % ring_slabs and writes output slab
+ * so = (out0 + t) % out_slabs: obs float[out_slabs][2][N][12] (16-B
+ * aligned), reward float[out_slabs][2][N], done / winner uint8[out_slabs][N]
+ * (each nullable).  Every tick loads and stores each game's state planes
+ * (297 B per env-step with the outputs); two lanes per game.
+ * Advances the step counter by n_ticks; accumulates the episode counters. */
+int sk_env_step_multi_obs(sk_env* env, const float* actions, int64_t ring_slabs, int64_t slab0, int32_t n_ticks,
+                          float* obs, float* reward, int32_t reward_kind, uint8_t* done, uint8_t* winner,
+                          int64_t out_slabs, int64_t out0, int32_t tick_limit, int32_t auto_reset,
+                          int32_t random_positions, void* stream);
 
 /* Random-policy actions (config 2 synthetic input): float[n_ticks][2][N][2]
  * uniform in [-1,1) from Philox4x32-10 keyed (seed, global env id, step

@@ -475,6 +475,14 @@ struct MultiArgs {
   const char* base;       // POL 1: the lowest plane; off[k] = plane k - base (pos, rot, qpos, qrot, qcdage, misc)
   uint32_t off[6];
   char* pack;             // the packed resident planes (48 B x n), or NULL: the 88-B form every tick
+  // the full contract (sk_env_step_multi_obs; k_step_split_multi<POL, true>):
+  // tick t writes output slab so = (out0 + t) % out_slabs of obs
+  // [slab][2][N][12], reward [slab][2][N] and (stride out_stride) done /
+  // winner.  The step-only entry point: out0 0, out_slabs n_ticks (so = t).
+  float* obs;
+  float* reward;
+  int reward_kind;
+  int64_t out0, out_slabs;
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t raw_rsrc(const void* base) {
@@ -614,8 +622,8 @@ struct MultiLane {
 // (its state goes to the exchange format).
 template <int POL, bool PACK>
 __device__ __forceinline__ void multi_tick(const MultiArgs& a, const Cfg& c, __amdgpu_buffer_rsrc_t r,
-                                           __amdgpu_buffer_rsrc_t rp, MultiLane& L, WaveCtr& wc, int t, uint64_t step,
-                                           int64_t slab, bool& packed, bool last) {
+                                           __amdgpu_buffer_rsrc_t rp, MultiLane& L, WaveCtr& wc, int64_t t,
+                                           uint64_t step, int64_t slab, bool& packed, bool last) {
   Env e;
   if (PACK && packed) load_env_pack<POL>(a, rp, L.ic, e);
   else load_env_port<POL>(a, r, L.ic, e);
@@ -714,11 +722,12 @@ __global__ void __launch_bounds__(BLK) k_step_multi(MultiArgs a, Cfg c, int earl
   const uint64_t step0 = step_read(a.step);
   step_advance(a.step, step0, (uint64_t)a.n_ticks);
   const __amdgpu_buffer_rsrc_t r = raw_rsrc(a.base), rp = raw_rsrc(a.pack);
-  int64_t slab = a.slab0;
+  int64_t slab = a.slab0, so = a.out0;
   bool packed = false;  // every launch starts from (and ends in) the exchange format
   for (int t = 0; t < a.n_ticks; ++t) {
-    multi_tick<POL, PACK>(a, c, r, rp, L, wc, t, step0 + (uint64_t)t, slab, packed, t + 1 == a.n_ticks);
+    multi_tick<POL, PACK>(a, c, r, rp, L, wc, so, step0 + (uint64_t)t, slab, packed, t + 1 == a.n_ticks);
     slab = slab + 1 == a.ring ? 0 : slab + 1;
+    so = so + 1 == a.out_slabs ? 0 : so + 1;
 #ifdef SK_TRACE_MULTI
     if (t < 30) SK_MTS(1 + t);
 #endif
@@ -778,9 +787,14 @@ struct SplitLane {
   unsigned n_done, n_h1, n_h2, t_sum;  // this pair's episode counts (lane p = 0 counts)
 };
 
-template <int POL>
+// OBS (sk_env_step_multi_obs, the full contract of configs 3-5): the tick
+// also writes the post-tick observation and reward of its player
+// (k_step_split's obs12_sc epilogue from the tick's sin/cos, the looking or
+// simple reward) into output slab `so`, and settles an ambiguous
+// future-collision flag after its state stores, as k_step_split does.
+template <int POL, bool OBS>
 __device__ __forceinline__ void split_multi_tick(const MultiArgs& a, const Cfg& c, __amdgpu_buffer_rsrc_t r,
-                                                 SplitLane& L, WaveCtr& wc, int t, uint64_t step, int64_t slab) {
+                                                 SplitLane& L, WaveCtr& wc, int64_t so, uint64_t step, int64_t slab) {
   int2* const pos2 = reinterpret_cast<int2*>(a.v.pos);
   double* const rot1 = reinterpret_cast<double*>(a.v.rot);
   int2* const qpos2 = reinterpret_cast<int2*>(a.v.qpos);
@@ -806,16 +820,24 @@ __device__ __forceinline__ void split_multi_tick(const MultiArgs& a, const Cfg& 
   __builtin_amdgcn_sched_barrier(0);
   const float2 act = load_action(a.actions + slab * 2 * a.n + (int64_t)p * a.n + L.ic);  // action last
   __builtin_amdgcn_sched_barrier(0);
-  bool k0, k1;
+  bool k0, k1, k2 = true;
   sktrig::SinCos m = sktrig::sincos_bf(rot, &k0);
   const double q_old = qrot;
   // do_actions(p+1, ...)  SkillshotLearner.py:206-213 (both sincos up front)
   const double rn = rot + clamp_action((double)act.y) * c.look;
   const double qn = (qcd <= 0) ? rn : qrot;
   sktrig::SinCos tq = sktrig::sincos_bf(qn, &k1);
-  if (!(k0 & k1)) {
+  // the post-look rotation's sin/cos for the obs epilogue (fp32: obs12_sc)
+  sktrig::SinCosF pr{0.0f, 1.0f};
+  if constexpr (OBS) pr = sktrig::sincos_fast(rn, &k2);
+  if (!(k0 & k1 & k2)) {
     if (!k0) m = sincos_lib(rot);
     if (!k1) tq = sincos_lib(qn);
+    if (!k2) {
+      const sktrig::SinCos rr = sincos_lib(rn);
+      pr.s = (float)rr.s;
+      pr.c = (float)rr.c;
+    }
   }
   move_direction_sc(c, px, py, m, (double)act.x);
   rot = rn;
@@ -833,9 +855,31 @@ __device__ __forceinline__ void split_multi_tick(const MultiArgs& a, const Cfg& 
   }
   ctr_settle(wc);  // every load of this tick consumed (see multi_tick)
   const bool d = L.in && ((!live) || (ticks >= a.tick_limit));  // SkillshotLearner.py:302
+  bool amb = false;
+  double gq = 0.0;  // the fast projectile gradient (the ambiguous flag's interval check)
+  const int aqx = qx, aqy = qy;  // the post-tick projectile, for the flag's redo
+  const double aqrot = qrot;
+  if constexpr (OBS) {
+    if (L.in) {  // prepare_states / calculate_rewards_* (SkillshotLearner.py:512-603) of the post-tick state
+      float o[12], pd;
+      obs12_sc(c, px, py, rot, pr, qx, qy, qrot, tq, qcd, qvalid, opx, opy, o, &pd, &amb, &gq);
+      if (a.obs) store_obs(a.obs + so * 24 * a.n, a.n, p, L.i, o);
+      if (a.reward) {
+        float rw;
+        if (a.reward_kind == SK_REWARD_SIMPLE) {  // a difference of distances: fp64 roots
+          const double mine = dist_point_point(qx, qy, opx, opy);
+          const double theirs = dist_point_point(oqx, oqy, px, py);
+          rw = (float)(mine - theirs);
+        } else {
+          rw = (float)(-(double)pd / (double)c.W);
+        }
+        a.reward[so * 2 * a.n + (int64_t)p * a.n + L.i] = rw;
+      }
+    }
+  }
   if (L.in && p == 0) {
-    if (a.done) a.done[(int64_t)t * a.out_stride + L.i] = (uint8_t)d;
-    if (a.winner) a.winner[(int64_t)t * a.out_stride + L.i] = (uint8_t)winner;
+    if (a.done) a.done[so * a.out_stride + L.i] = (uint8_t)d;
+    if (a.winner) a.winner[so * a.out_stride + L.i] = (uint8_t)winner;
   }
   const bool dc = d && p == 0;
   L.n_done += dc;
@@ -870,6 +914,16 @@ __device__ __forceinline__ void split_multi_tick(const MultiArgs& a, const Cfg& 
       }
     }
   }
+  if constexpr (OBS) {
+    // the future-collision flag within its margin of an edge, settled after
+    // this tick's state stores (k_step_split's tail rule): by the interval
+    // check unless it depends on g's last bits (then the correctly rounded tan)
+    if (amb && a.obs) {
+      const int fi = future_flag_interval(c, aqx, aqy, opx, opy, gq);
+      const float f = fi >= 0 ? (float)fi : future_flag_cr(c, aqx, aqy, aqrot, opx, opy);
+      a.obs[so * 24 * a.n + ((int64_t)p * a.n + L.i) * 12 + 11] = f;
+    }
+  }
 }
 
 // BLK 512 (the 65,536-game geometry): one workgroup of 8 waves per CU, so
@@ -877,7 +931,7 @@ __device__ __forceinline__ void split_multi_tick(const MultiArgs& a, const Cfg& 
 // "Two waves per SIMD"); `stagger` > 0 starts waves 4-7 stagger x 512
 // cycles late, so the pair alternates a tick's memory round trip with the
 // partner's arithmetic instead of both waiting at once.
-template <int POL, int BLK>
+template <int POL, int BLK, bool OBS = false>
 __global__ void __launch_bounds__(BLK) k_step_split_multi(MultiArgs a, Cfg c, int stagger) {
   SplitLane L;
   const int64_t gt = (int64_t)blockIdx.x * BLK + threadIdx.x;
@@ -894,10 +948,11 @@ __global__ void __launch_bounds__(BLK) k_step_split_multi(MultiArgs a, Cfg c, in
   const uint64_t step0 = step_read(a.step);
   step_advance(a.step, step0, (uint64_t)a.n_ticks);
   const __amdgpu_buffer_rsrc_t r = raw_rsrc(a.base);
-  int64_t slab = a.slab0;
+  int64_t slab = a.slab0, so = a.out0;
   for (int t = 0; t < a.n_ticks; ++t) {
-    split_multi_tick<POL>(a, c, r, L, wc, t, step0 + (uint64_t)t, slab);
+    split_multi_tick<POL, OBS>(a, c, r, L, wc, so, step0 + (uint64_t)t, slab);
     slab = slab + 1 == a.ring ? 0 : slab + 1;
+    so = so + 1 == a.out_slabs ? 0 : so + 1;
   }
   if (a.ctr) {
     const unsigned c4[4] = {L.n_done, L.n_h1, L.n_h2, L.t_sum};
@@ -1686,26 +1741,39 @@ int sk_env_act_step_job(sk_env* e, const float* actor_flat, const float* acting_
   return SK_OK;
 }
 
-int sk_env_step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64_t slab0, int32_t n_ticks,
-                      uint8_t* done, uint8_t* winner, int64_t out_stride, int32_t tick_limit, int32_t auto_reset,
-                      int32_t random_positions, void* stream) {
+// sk_env_step_multi (obs == reward == NULL, full == false) and
+// sk_env_step_multi_obs (full == true: the split geometry with the obs /
+// reward epilogue, k_step_split_multi<POL, BLK, true>)
+static int step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64_t slab0, int32_t n_ticks,
+                      float* obs, float* reward, int32_t reward_kind, uint8_t* done, uint8_t* winner,
+                      int64_t out_stride, int64_t out0, int64_t out_slabs, int32_t tick_limit, int32_t auto_reset,
+                      int32_t random_positions, void* stream, bool full) {
   SK_CHECK_ENV(e);
   if (!actions) return fail(SK_EINVAL, "actions is NULL");
   if (((uintptr_t)actions) & 7) return fail(SK_EINVAL, "actions must be 8-byte aligned");
   if (n_ticks <= 0 || ring_slabs <= 0 || slab0 < 0 || slab0 >= ring_slabs || out_stride < 0)
     return fail(SK_EINVAL, "bad n_ticks / ring_slabs / slab0 / out_stride");
+  if (out_slabs <= 0 || out0 < 0 || out0 >= out_slabs) return fail(SK_EINVAL, "bad out_slabs / out0");
+  if (obs && (((uintptr_t)obs) & 15)) return fail(SK_EINVAL, "obs must be 16-byte aligned");
+  if (full && reward_kind != SK_REWARD_LOOKING && reward_kind != SK_REWARD_SIMPLE)
+    return fail(SK_EINVAL, "bad reward_kind");
   if (e->host) {
-    const int64_t slab_floats = 4 * (int64_t)e->n;
+    const int64_t slab_floats = 4 * (int64_t)e->n, n = e->n;
     for (int32_t t = 0; t < n_ticks; ++t) {
-      const int64_t s = (slab0 + t) % ring_slabs;
-      skh::step(*e->host, actions + s * slab_floats, nullptr, nullptr, SK_REWARD_LOOKING,
-                done ? done + (int64_t)t * out_stride : nullptr, winner ? winner + (int64_t)t * out_stride : nullptr,
-                tick_limit, auto_reset, random_positions, nullptr);
+      const int64_t s = (slab0 + t) % ring_slabs, so = (out0 + t) % out_slabs;
+      skh::step(*e->host, actions + s * slab_floats, obs ? obs + so * 24 * n : nullptr,
+                reward ? reward + so * 2 * n : nullptr, reward_kind, done ? done + so * out_stride : nullptr,
+                winner ? winner + so * out_stride : nullptr, tick_limit, auto_reset, random_positions, nullptr);
     }
     return SK_OK;
   }
   if ((int64_t)e->n > (int64_t)0x7fffffff / 16) return fail(SK_EINVAL, "n_envs too large for k_step_multi");
   MultiArgs a;
+  a.obs = full ? obs : nullptr;
+  a.reward = full ? reward : nullptr;
+  a.reward_kind = reward_kind;
+  a.out0 = out0;
+  a.out_slabs = out_slabs;
   a.v = e->view;
   a.n = e->n;
   a.actions = reinterpret_cast<const float2*>(actions);
@@ -1730,7 +1798,7 @@ int sk_env_step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64
   // vs 7.7); at one wave per SIMD the tick is a latency chain and the
   // pack / unpack work lengthens it (65,536: 2.51 vs 2.38; 32,768: 2.43 vs
   // 2.04; profiles/r03pk2_multi_pack_sweep.jsonl)
-  const bool want_pack = e->multi_pack > 0 || (e->multi_pack < 0 && e->n > kPackMinEnvs);
+  const bool want_pack = !full && (e->multi_pack > 0 || (e->multi_pack < 0 && e->n > kPackMinEnvs));
   if (n_ticks > 1 && want_pack && (uint64_t)e->n * 48u <= 0xffffffffull) {
     if (!e->d_pack) {
       if (hipMalloc(&e->d_pack, (size_t)e->n * 48) != hipSuccess) return fail(SK_ENOMEM, "hipMalloc pack");
@@ -1757,7 +1825,9 @@ int sk_env_step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64
   }
   // geometry: one lane per game (k_step_multi) or two (k_step_split_multi);
   // SK_MULTI_SPLIT = 0 / 1 forces one, else auto (kSplitMultiMaxEnvs)
-  const bool split = e->multi_split >= 0 ? e->multi_split != 0 : (int64_t)e->n <= kSplitMultiMaxEnvs;
+  // (the full contract always runs the split geometry: a lane per player
+  // computes that player's observation, as k_step_split does)
+  const bool split = full || (e->multi_split >= 0 ? e->multi_split != 0 : (int64_t)e->n <= kSplitMultiMaxEnvs);
   const hipStream_t hs = (hipStream_t)stream;
   hipEvent_t e0 = nullptr, e1 = nullptr;  // launch_timed's events (A/B hook; unused by the ABI)
   hipError_t err;
@@ -1768,7 +1838,16 @@ int sk_env_step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64
     const int64_t lanes = 2 * (int64_t)e->n;
     const bool wide = e->multi_block == 512 || (e->multi_block < 0 && lanes >= 512 * 256);
     const dim3 g512((unsigned)((lanes + 511) / 512)), g64(step_grid(lanes));
-    if (wide)
+    if (full) {
+      if (wide)
+        err = pol == 1 ? launch_timed(k_step_split_multi<1, 512, true>, g512, dim3(512), hs, e0, e1, a, e->dcfg, 0)
+                       : launch_timed(k_step_split_multi<0, 512, true>, g512, dim3(512), hs, e0, e1, a, e->dcfg, 0);
+      else
+        err = pol == 1 ? launch_timed(k_step_split_multi<1, kStepBlock, true>, g64, dim3(kStepBlock), hs, e0, e1, a,
+                                      e->dcfg, 0)
+                       : launch_timed(k_step_split_multi<0, kStepBlock, true>, g64, dim3(kStepBlock), hs, e0, e1, a,
+                                      e->dcfg, 0);
+    } else if (wide)
       err = pol == 1 ? launch_timed(k_step_split_multi<1, 512>, g512, dim3(512), hs, e0, e1, a, e->dcfg,
                                     e->multi_stagger)
                      : launch_timed(k_step_split_multi<0, 512>, g512, dim3(512), hs, e0, e1, a, e->dcfg,
@@ -1813,6 +1892,22 @@ int sk_env_step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64
   if (err != hipSuccess) return fail(SK_EHIP, std::string("k_step_multi launch: ") + hipGetErrorString(err));
   e->parity ^= 1;
   return SK_OK;
+}
+
+int sk_env_step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64_t slab0, int32_t n_ticks,
+                      uint8_t* done, uint8_t* winner, int64_t out_stride, int32_t tick_limit, int32_t auto_reset,
+                      int32_t random_positions, void* stream) {
+  return step_multi(e, actions, ring_slabs, slab0, n_ticks, nullptr, nullptr, SK_REWARD_LOOKING, done, winner,
+                    out_stride, 0, n_ticks > 0 ? n_ticks : 1, tick_limit, auto_reset, random_positions, stream, false);
+}
+
+int sk_env_step_multi_obs(sk_env* e, const float* actions, int64_t ring_slabs, int64_t slab0, int32_t n_ticks,
+                          float* obs, float* reward, int32_t reward_kind, uint8_t* done, uint8_t* winner,
+                          int64_t out_slabs, int64_t out0, int32_t tick_limit, int32_t auto_reset,
+                          int32_t random_positions, void* stream) {
+  SK_CHECK_ENV(e);
+  return step_multi(e, actions, ring_slabs, slab0, n_ticks, obs, reward, reward_kind, done, winner, e->n, out0,
+                    out_slabs, tick_limit, auto_reset, random_positions, stream, true);
 }
 
 int sk_gen_random_actions(sk_env* e, float* actions, int32_t n_ticks, void* stream) {

@@ -379,6 +379,41 @@ class VecSkillshotGame:
         return done.view(rows, self.n) if record else done.view(-1)[: self.n], \
             winner.view(rows, self.n) if record else winner.view(-1)[: self.n]
 
+    def step_multi_obs(self, actions, n_ticks=None, slab0=0, out_slabs=None, out0=0, reward="looking",
+                       auto_reset=True, out=None, stream=None):
+        """n_ticks ticks of the FULL contract (SkillshotLearner.py:302-324 with
+        the actions given: do_actions x2, game_tick, prepare_states and the
+        reward of the post-tick state, done, random restart) in ONE launch
+        (sk_env_step_multi_obs).
+
+        actions: float32 [R, 2, N, 2], tick t acting on slab (slab0 + t) % R;
+        tick t writes output slab (out0 + t) % out_slabs (out_slabs defaults to
+        n_ticks: one slab per tick) of obs [S, 2, N, 12], reward [S, 2, N],
+        done / winner [S, N].  Equal bit for bit to n_ticks
+        `step(actions[s], obs=True, reward=reward)` calls."""
+        a = torch.as_tensor(actions, device=self.device)
+        if a.dtype != torch.float32 or not a.is_contiguous() or a.dim() != 4 or tuple(a.shape[1:]) != (2, self.n, 2):
+            raise ValueError(f"actions must be contiguous float32 [R, 2, {self.n}, 2]")
+        R = a.shape[0]
+        T = R if n_ticks is None else int(n_ticks)
+        S = T if out_slabs is None else int(out_slabs)
+        if out is None:
+            out = dict(obs=torch.empty((S, 2, self.n, 12), dtype=torch.float32, device=self.device),
+                       reward=torch.empty((S, 2, self.n), dtype=torch.float32, device=self.device),
+                       done=torch.empty((S, self.n), dtype=torch.uint8, device=self.device),
+                       winner=torch.empty((S, self.n), dtype=torch.uint8, device=self.device))
+        for k, shape in (("obs", (S, 2, self.n, 12)), ("reward", (S, 2, self.n)), ("done", (S, self.n)),
+                         ("winner", (S, self.n))):
+            t = out.get(k)
+            if t is not None and (tuple(t.shape) != shape or not t.is_contiguous()):
+                raise ValueError(f"{k} must be contiguous {shape}")
+        check(self._L.sk_env_step_multi_obs(self._h, _ptr(a), R, int(slab0) % R, T, _ptr(out.get("obs")),
+                                            _ptr(out.get("reward")), REWARD_KINDS[reward], _ptr(out.get("done")),
+                                            _ptr(out.get("winner")), S, int(out0) % S, self.tick_limit,
+                                            int(bool(auto_reset)), int(self.random_positions),
+                                            stream if stream is not None else self._stream()))
+        return out
+
     def step_multi_raw(self, actions_ptr, ring, slab0, n_ticks, done_ptr=None, winner_ptr=None, out_stride=0,
                        auto_reset=True, stream=None):
         """Pointer-level sk_env_step_multi (bench / graph capture; no allocation)."""

@@ -437,3 +437,38 @@ def test_cpu_backend_equals_gpu_engine(ssa):
                         {k: v for k, v in sc.items() if k != "step_counter"}, "end")
     assert sg["step_counter"] == sc["step_counter"]
     assert g.counters() == c.counters()
+
+
+@pytest.mark.parametrize("pol", [1, 0], ids=["write_through", "plain"])
+@pytest.mark.parametrize("name", gr.fixture_names())
+def test_golden_fixture_multi_obs(ssa, monkeypatch, name, pol):
+    """The full-contract multi-tick kernel (sk_env_step_multi_obs, ABI 9): a
+    learner-protocol fixture's whole trajectory in ONE launch (the action
+    ring = the fixture's per-tick actions, one output slab per tick), every
+    tick's obs / reward / done / winner and the final state against the
+    reference's golden values, at the same bar as the one-tick kernels."""
+    d = gr.load(name)
+    if str(d["protocol"]) != "learner":
+        pytest.skip("per-method protocol (no fused step)")
+    monkeypatch.setenv("SK_MULTI_POLICY", str(pol))
+    E = d["pos"].shape[0]
+    n_steps = d["n_steps"]
+    T = int(n_steps.max())
+    g = ssa.VecSkillshotGame(E, tick_limit=int(d["tick_limit"]))
+    g.load_state_dict(gr.state_at(d, 0))
+    acts = np.ascontiguousarray(np.transpose(d["actions"][:, :T], (1, 2, 0, 3)))  # [T, 2, E, 2]
+    out = g.step_multi_obs(torch.as_tensor(acts, dtype=torch.float32).cuda(), auto_reset=False)
+    torch.cuda.synchronize()
+    o = {k: v.cpu().numpy() for k, v in out.items()}
+    for t in range(T):
+        active = n_steps >= t + 1
+        where = f"{d['scenario']} multi t={t + 1}"
+        gr.compare_obs(o["obs"][t], d["obs"][:, t + 1], active, where, OBS_TOL)
+        gr.compare_reward(o["reward"][t], d["reward"][:, t + 1], active, where, OBS_TOL)
+        live = d["live"][:, t + 1].astype(bool)
+        want_done = (~live) | (d["ticks"][:, t + 1] >= int(d["tick_limit"]))
+        assert (o["done"][t][active].astype(bool) == want_done[active]).all(), where
+        assert (o["winner"][t][active] == d["winner"][:, t + 1][active]).all(), where
+    st = g.state_dict()
+    st.pop("step_counter")
+    gr.compare_state(st, gr.state_at(d, T), n_steps >= T, f"{d['scenario']} multi final")

@@ -232,3 +232,29 @@ def test_tick_form_selection():
     assert f(4096, env={"SK_FUSED_ACT": "0"}) == "sequential"
     assert f(65536, multi=True, env={"SK_TICK_OVERLAP": "1"}) == "sequential"
     assert f(4096, env={"SK_FUSED_REPLAY": "1"}) == "sequential"
+
+
+def test_cpu_backend_step_multi_obs_equals_steps():
+    """sk_env_step_multi_obs on the CPU backend (ABI 9): n_ticks sk_env_step
+    calls with obs and reward, output slab (out0 + t) % out_slabs, bit for bit"""
+    import skillshot_learning_amd as ssa
+    n, T, R, S = 257, 90, 4, 6
+    a = ssa.VecSkillshotGame(n, device="cpu", seed=3, tick_limit=40)
+    a.reset(random_positions=True)
+    b = ssa.VecSkillshotGame(n, device="cpu", seed=3, tick_limit=40)
+    b.load_state_dict(a.state_dict())
+    b.step_counter = a.step_counter
+    acts = a.gen_random_actions(R)
+    for reward in ("looking", "simple"):
+        out = a.step_multi_obs(acts, n_ticks=T, slab0=3, out_slabs=S, out0=5, reward=reward)
+        want = {}
+        for t in range(T):
+            o = b.step(acts[(3 + t) % R], obs=True, reward=reward, auto_reset=True)
+            want[(5 + t) % S] = {k: o[k].clone() for k in ("obs", "reward", "done", "winner")}
+        for s, w in want.items():
+            for k, v in w.items():
+                assert torch.equal(out[k][s], v.view(out[k][s].shape)), (reward, s, k)
+        sa, sb = a.state_dict(), b.state_dict()
+        for k in sa:
+            assert np.array_equal(np.asarray(sa[k]), np.asarray(sb[k])), k
+    assert a.counters() == b.counters() and a.counters()["dones"] > n
