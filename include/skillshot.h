@@ -232,14 +232,15 @@ int sk_env_step_insert(sk_env* env, const float* actions, float* obs, float* rew
 
 /* The self-play tick's act + step in ONE launch (ABI 7; SkillshotLearner.py
  * :304-314 act -> do_actions -> game_tick -> get_state): equal, bit for bit,
- * to sk_actor_forward_f32(actor_flat, acting_obs, actions, 2N, noise_sd,
+ * to sk_actor_forward_f32(actor_flat, actor_pack, acting_obs, actions, 2N, noise_sd,
  * action_sd, noise_seed, call_counter) with 32-row tiles (SK_FWD16=0)
  * followed by sk_env_step_insert(env, actions, obs, ..., acting_obs, ring,
  * ...), or by sk_env_step when ring is NULL.  The observations never
  * leave the CU between the actor and the step; actions float[2N][2] is
  * still written.  N % 4 != 0 runs the two launches.  total_copy as
  * sk_env_step_insert's (ABI 8).  GPU backend only. */
-int sk_env_act_step(sk_env* env, const float* actor_flat, const float* acting_obs, float* actions, float noise_sd,
+int sk_env_act_step(sk_env* env, const float* actor_flat, const void* actor_pack, const float* acting_obs,
+                    float* actions, float noise_sd,
                     float action_sd, uint64_t noise_seed, uint64_t* call_counter, float* obs, float* reward,
                     int32_t reward_kind, uint8_t* done, uint8_t* winner, int32_t tick_limit, int32_t auto_reset,
                     int32_t random_positions, float* obs_reset, float* ring, int64_t capacity, int64_t* total,
@@ -262,7 +263,8 @@ int sk_env_act_step(sk_env* env, const float* actor_flat, const float* acting_ob
 typedef struct sk_step_job {
   uint64_t opaque[SK_STEP_JOB_WORDS];
 } sk_step_job;
-int sk_env_act_step_job(sk_env* env, const float* actor_flat, const float* acting_obs, float* actions,
+int sk_env_act_step_job(sk_env* env, const float* actor_flat, const void* actor_pack, const float* acting_obs,
+                        float* actions,
                         float noise_sd, float action_sd, uint64_t noise_seed, uint64_t* call_counter, float* obs,
                         float* reward, int32_t reward_kind, uint8_t* done, uint8_t* winner, int32_t tick_limit,
                         int32_t auto_reset, int32_t random_positions, float* obs_reset, float* ring,
@@ -511,6 +513,7 @@ typedef struct sk_pack_targets {
   void* actor_fwd_pack;
   int32_t ld2;   /* 256 (actor) or 258 (critic: W2 carries the 2 action columns) */
   int32_t n_out; /* 2 (actor) or 1 (critic) */
+  void* actor_split_pack; /* the fp32 actor's split pack (ABI 9; nullable, actor only) */
 } sk_pack_targets;
 int sk_adam_flat_packed(const float* partials, int32_t n_partials, int32_t n_params, const float* grad_in,
                         float* grad_out, int32_t apply, float* param, float* exp_avg, float* exp_avg_sq,
@@ -560,8 +563,23 @@ int sk_adam_flat_sliced(const float* partials, int32_t n_partials, const float* 
  * is ignored (may be NULL) and *w1_rows = 0. */
 int64_t sk_update_partials_f32(int64_t batch);
 int64_t sk_update_scratch_f32(int64_t batch, int64_t* w1_rows);
-int sk_actor_forward_f32(const float* actor_flat, const float* obs, float* actions, int64_t rows, float noise_sd,
-                         float action_sd, uint64_t seed, uint64_t* call_counter, void* stream);
+int sk_actor_forward_f32(const float* actor_flat, const void* actor_pack, const float* obs, float* actions,
+                         int64_t rows, float noise_sd, float action_sd, uint64_t seed, uint64_t* call_counter,
+                         void* stream);
+/* The fp32 actor's split pack (ABI 9): W1 and W2 as three bf16 pieces each
+ * (hi + mid + lo = the fp32 weight to 2^-26) and their bf16 squares, in
+ * v_mfma_f32_32x32x16_bf16 fragment order.  The 32-row acting tile
+ * (sk_actor_forward_f32 above 4,096 rows or with SK_FWD16=0, sk_env_act_step,
+ * sk_env_act_step_job) computes its GEMMs as six bf16 MFMAs per 16 k from
+ * these pieces: every product within ~2^-25 of the fp32 product, the fp32
+ * accumulation unchanged, at the bf16 MFMA rate.  actor_pack =
+ * sk_actor_split_pack_bytes() bytes, 16-byte aligned; it must hold the pack
+ * of the actor_flat it is passed with: sk_actor_split_pack_f32 writes it
+ * from the flat parameters, and sk_adam_flat_* keeps it current when given
+ * as sk_pack_targets.actor_split_pack.  Biases and W3 are read from
+ * actor_flat. */
+size_t sk_actor_split_pack_bytes(void);
+int sk_actor_split_pack_f32(const float* actor_flat, void* actor_pack, void* stream);
 int sk_critic_grad_f32(const float* critic_flat, const float* obs, const float* actions, const float* targets,
                        const float* next_obs, const float* rewards, const float* done, float gamma,
                        const float* target_actor_flat, const float* target_critic_flat, int64_t batch,

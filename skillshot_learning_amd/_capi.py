@@ -33,7 +33,7 @@ EXPORTS = (
     "sk_adam_flat_packed", "sk_adam_flat_sliced", "sk_update_scratch_f32",
     "sk_target_y", "sk_replay_insert", "sk_replay_sample", "sk_replay_insert_sample", "sk_grad_pack_flat",
     "sk_critic_grad_bootstrap",
-    "sk_update_partials_f32", "sk_actor_forward_f32", "sk_critic_grad_f32", "sk_critic_grad_f32_sampled",
+    "sk_update_partials_f32", "sk_actor_forward_f32", "sk_actor_split_pack_bytes", "sk_actor_split_pack_f32", "sk_critic_grad_f32", "sk_critic_grad_f32_sampled",
     "sk_critic_grad_bootstrap_sampled", "sk_actor_grad_f32", "sk_actor_grad_f32_step",
     "sk_critic_grad_f32_sampled_step", "sk_critic_grad_f32_step", "sk_replay_sample_excl",
 )
@@ -118,9 +118,9 @@ def load(build_if_missing=True):
         "sk_env_observe": ([P, P, P, i32, P], ctypes.c_int),
         "sk_env_step": ([P, P, P, P, i32, P, P, i32, i32, i32, P, P], ctypes.c_int),
         "sk_env_step_insert": ([P, P, P, P, i32, P, P, i32, i32, i32, P, P, P, i64, P, P, P, P], ctypes.c_int),
-        "sk_env_act_step": ([P, P, P, P, f32, f32, u64, P, P, P, i32, P, P, i32, i32, i32, P, P, i64, P, P, P, P],
+        "sk_env_act_step": ([P, P, P, P, P, f32, f32, u64, P, P, P, i32, P, P, i32, i32, i32, P, P, i64, P, P, P, P],
                             ctypes.c_int),
-        "sk_env_act_step_job": ([P, P, P, P, f32, f32, u64, P, P, P, i32, P, P, i32, i32, i32, P, P, i64, P, P, P,
+        "sk_env_act_step_job": ([P, P, P, P, P, f32, f32, u64, P, P, P, i32, P, P, i32, i32, i32, P, P, i64, P, P, P,
                                  ctypes.POINTER(SkStepJob)], ctypes.c_int),
         "sk_env_step_multi": ([P, P, i64, i64, i32, P, P, i64, i32, i32, i32, P], ctypes.c_int),
         "sk_env_step_multi_obs": ([P, P, i64, i64, i32, P, P, i32, P, P, i64, i64, i32, i32, i32, P], ctypes.c_int),
@@ -155,7 +155,9 @@ def load(build_if_missing=True):
         "sk_critic_grad_bootstrap": ([P, P, P, P, P, P, P, f32, P, P, i64, i64, f32, u64, P, P, P, i32, P, P, P],
                                      ctypes.c_int),
         "sk_update_partials_f32": ([i64], ctypes.c_int64),
-        "sk_actor_forward_f32": ([P, P, P, i64, f32, f32, u64, P, P], ctypes.c_int),
+        "sk_actor_forward_f32": ([P, P, P, P, i64, f32, f32, u64, P, P], ctypes.c_int),
+        "sk_actor_split_pack_bytes": ([], ctypes.c_size_t),
+        "sk_actor_split_pack_f32": ([P, P, P], ctypes.c_int),
         "sk_critic_grad_f32": ([P, P, P, P, P, P, P, f32, P, P, i64, i64, f32, u64, P, P, P, i32, P, P, P, P],
                                ctypes.c_int),
         "sk_critic_grad_f32_sampled": ([P, P, f32, P, P, i64, i64, f32, u64, P, P, P, i32, P, P, P, P],

@@ -70,6 +70,74 @@ class ActorKernel:
 
 class ActorKernel32:
     """The actor forward at the reference's precision (csrc/sk_learn32.hip
+    k_actor_fwd32 / k_actor_fwd16), reading biases and W3 from the actor's
+    flat fp32 parameter vector and W1 / W2 from its split pack (`pack`,
+    sk_split.hpp: three bf16 pieces per weight, so the 32-row tile computes
+    fp32 products at the bf16 MFMA rate).  The pack follows the parameters:
+    the fused update's Adam launch rewrites it (DDPG._fused.split_pack), and
+    a change made through torch (optimizer steps, load_state_dict, copy_)
+    bumps the flat buffer's version counter, on which every call repacks
+    (ensure_pack).  Same call interface as ActorKernel."""
+
+    buf = None  # no bf16 forward pack
+
+    def __init__(self, actor, seed=0):
+        from .update_kernel import flatten_module
+        self.actor = actor
+        self.L = _capi.load()
+        p = next(actor.parameters())
+        if p.device.type != "cuda":
+            raise SkillshotError("ActorKernel32 needs the actor on a gfx950 GPU")
+        self.device = p.device
+        self.flat = flatten_module(actor)
+        self.seed = int(seed) & ((1 << 64) - 1)
+        self.calls = 0
+        self._ctr = torch.zeros(130, dtype=torch.int64, device=self.device)  # SK_ACTOR_COUNTER_WORDS
+        self.counter = self._ctr[:1]
+        self.pack = torch.zeros(int(self.L.sk_actor_split_pack_bytes()), dtype=torch.uint8, device=self.device)
+        self._packed = None  # (flat buffer, its version) the pack was last written from
+        self.ensure_pack()
+
+    def refresh(self):
+        """repack from the current flat parameters"""
+        from .update_kernel import flatten_module
+        self.flat = flatten_module(self.actor)  # idempotent: the parameters stay views of it
+        rc = self.L.sk_actor_split_pack_f32(ctypes.c_void_p(self.flat.data_ptr()),
+                                            ctypes.c_void_p(self.pack.data_ptr()), self._stream())
+        if rc != 0:
+            raise SkillshotError(f"sk_actor_split_pack_f32 failed ({rc})")
+        self._packed = (self.flat.data_ptr(), self.flat._version)
+
+    def ensure_pack(self):
+        """the split pack, repacked first if the parameters were changed
+        through torch since it was written (returns it)"""
+        if self._packed != (self.flat.data_ptr(), self.flat._version):
+            self.refresh()
+        return self.pack
+
+    fused_action_noise = True  # model_act_action_noise's N(0, sd) is drawn in the kernel (sk_actor_forward_noise)
+
+    @torch.no_grad()
+    def __call__(self, obs, noise_sd=0.0, generator=None, out=None, action_sd=0.0):
+        """obs float32 [M, 12] -> actions float32 [M, 2]; noise_sd: parameter
+        noise, action_sd: action noise on the tanh outputs."""
+        x = obs if obs.dtype == torch.float32 else obs.float()
+        x = x.contiguous()
+        if x.dim() != 2 or x.shape[1] != 12:
+            raise ValueError("obs must be [M, 12]")
+        m = x.shape[0]
+        y = out if out is not None else torch.empty((m, 2), dtype=torch.float32, device=self.device)
+        self.calls += 1
+        rc = self.L.sk_actor_forward_noise(ctypes.c_void_p(self.buf.data_ptr()), ctypes.c_void_p(x.data_ptr()),
+                                           ctypes.c_void_p(y.data_ptr()), m, float(noise_sd), float(action_sd),
+                                           self.seed, ctypes.c_void_p(self._ctr.data_ptr()), self._stream())
+        if rc != 0:
+            raise SkillshotError(f"sk_actor_forward failed ({rc})")
+        return y
+
+
+class ActorKernel32:
+    """The actor forward at the reference's precision (csrc/sk_learn32.hip
     k_actor_fwd32: fp32 operands on v_mfma_f32_32x32x2_f32), reading the
     actor's flat fp32 parameter vector directly: no pack, nothing to refresh
     after an update.  Same call interface as ActorKernel."""
@@ -108,7 +176,9 @@ class ActorKernel32:
         m = x.shape[0]
         y = out if out is not None else torch.empty((m, 2), dtype=torch.float32, device=self.device)
         self.calls += 1
-        rc = self.L.sk_actor_forward_f32(ctypes.c_void_p(self.flat.data_ptr()), ctypes.c_void_p(x.data_ptr()),
+        pack = self.ensure_pack()
+        rc = self.L.sk_actor_forward_f32(ctypes.c_void_p(self.flat.data_ptr()), ctypes.c_void_p(pack.data_ptr()),
+                                         ctypes.c_void_p(x.data_ptr()),
                                          ctypes.c_void_p(y.data_ptr()), m, float(noise_sd), float(action_sd),
                                          self.seed, ctypes.c_void_p(self._ctr.data_ptr()), self._stream())
         if rc != 0:

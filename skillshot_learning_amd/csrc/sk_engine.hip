@@ -1686,7 +1686,8 @@ static int act_step_common(sk_env* e, const float* actor_flat, const float* acti
   return SK_OK;
 }
 
-int sk_env_act_step(sk_env* e, const float* actor_flat, const float* acting_obs, float* actions, float noise_sd,
+int sk_env_act_step(sk_env* e, const float* actor_flat, const void* actor_pack, const float* acting_obs,
+                    float* actions, float noise_sd,
                     float action_sd, uint64_t noise_seed, uint64_t* call_counter, float* obs, float* reward,
                     int32_t reward_kind, uint8_t* done, uint8_t* winner, int32_t tick_limit, int32_t auto_reset,
                     int32_t random_positions, float* obs_reset, float* ring, int64_t capacity, int64_t* total,
@@ -1694,8 +1695,8 @@ int sk_env_act_step(sk_env* e, const float* actor_flat, const float* acting_obs,
   int rc = act_step_common(e, actor_flat, acting_obs, actions);
   if (rc != SK_OK) return rc;
   if (e->n % 4) {  // the fused tile keys its noise by aligned 4-row groups: two launches
-    rc = sk_actor_forward_f32(actor_flat, acting_obs, actions, 2 * (int64_t)e->n, noise_sd, action_sd, noise_seed,
-                              call_counter, stream);
+    rc = sk_actor_forward_f32(actor_flat, actor_pack, acting_obs, actions, 2 * (int64_t)e->n, noise_sd, action_sd,
+                              noise_seed, call_counter, stream);
     if (rc != SK_OK) return fail(rc, "sk_actor_forward_f32 failed");
     return step_launch(e, actions, obs, reward, reward_kind, done, winner, tick_limit, auto_reset,
                        random_positions, obs_reset, acting_obs, ring, capacity, total, arrivals, total_copy, stream);
@@ -1704,8 +1705,8 @@ int sk_env_act_step(sk_env* e, const float* actor_flat, const float* acting_obs,
   rc = act_step_args(e, acting_obs, actions, obs, reward, reward_kind, done, winner, tick_limit, auto_reset,
                      random_positions, obs_reset, ring, capacity, total, arrivals, total_copy, a);
   if (rc != SK_OK) return rc;
-  rc = sk_launch_act_step32(actor_flat, actions, noise_sd, action_sd, noise_seed, call_counter, a, e->dcfg,
-                            (hipStream_t)stream);
+  rc = sk_launch_act_step32(actor_flat, actor_pack, actions, noise_sd, action_sd, noise_seed, call_counter, a,
+                            e->dcfg, (hipStream_t)stream);
   if (rc != SK_OK) return fail(rc, "k_act_step32 launch failed");
   e->parity ^= 1;
   return SK_OK;
@@ -1713,7 +1714,8 @@ int sk_env_act_step(sk_env* e, const float* actor_flat, const float* acting_obs,
 
 static_assert(sizeof(ActStepJob) <= sizeof(sk_step_job), "sk_step_job too small for ActStepJob");
 
-int sk_env_act_step_job(sk_env* e, const float* actor_flat, const float* acting_obs, float* actions, float noise_sd,
+int sk_env_act_step_job(sk_env* e, const float* actor_flat, const void* actor_pack, const float* acting_obs,
+                        float* actions, float noise_sd,
                         float action_sd, uint64_t noise_seed, uint64_t* call_counter, float* obs, float* reward,
                         int32_t reward_kind, uint8_t* done, uint8_t* winner, int32_t tick_limit, int32_t auto_reset,
                         int32_t random_positions, float* obs_reset, float* ring, int64_t capacity, int64_t* total,
@@ -1722,6 +1724,7 @@ int sk_env_act_step_job(sk_env* e, const float* actor_flat, const float* acting_
   if (rc != SK_OK) return rc;
   if (!job) return fail(SK_EINVAL, "job is NULL");
   if (e->n % 4) return fail(SK_EINVAL, "a prepared act_step needs N % 4 == 0 (use sk_env_act_step)");
+  if (!actor_pack || (((uintptr_t)actor_pack) & 15)) return fail(SK_EINVAL, "actor_pack is NULL or misaligned");
   ActStepJob j;
   std::memset(&j, 0, sizeof(j));
   rc = act_step_args(e, acting_obs, actions, obs, reward, reward_kind, done, winner, tick_limit, auto_reset,
@@ -1730,6 +1733,7 @@ int sk_env_act_step_job(sk_env* e, const float* actor_flat, const float* acting_
   j.magic = kActStepJobMagic;
   j.c = e->dcfg;
   j.aflat = actor_flat;
+  j.apack = (const char*)actor_pack;
   j.act_out = actions;
   j.sd = noise_sd;
   j.action_sd = action_sd;
@@ -1840,8 +1844,10 @@ static int step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64
     const dim3 g512((unsigned)((lanes + 511) / 512)), g64(step_grid(lanes));
     if (full) {
       if (wide)
-        err = pol == 1 ? launch_timed(k_step_split_multi<1, 512, true>, g512, dim3(512), hs, e0, e1, a, e->dcfg, 0)
-                       : launch_timed(k_step_split_multi<0, 512, true>, g512, dim3(512), hs, e0, e1, a, e->dcfg, 0);
+        err = pol == 1 ? launch_timed(k_step_split_multi<1, 512, true>, g512, dim3(512), hs, e0, e1, a, e->dcfg,
+                                      e->multi_stagger)
+                       : launch_timed(k_step_split_multi<0, 512, true>, g512, dim3(512), hs, e0, e1, a, e->dcfg,
+                                      e->multi_stagger);
       else
         err = pol == 1 ? launch_timed(k_step_split_multi<1, kStepBlock, true>, g64, dim3(kStepBlock), hs, e0, e1, a,
                                       e->dcfg, 0)

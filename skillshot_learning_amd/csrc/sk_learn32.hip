@@ -35,6 +35,7 @@
 #include "../../include/skillshot.h"
 #include "sk_mlp.hpp"
 #include "sk_partial.hpp"
+#include "sk_split.hpp"
 #include "sk_step.hpp"
 
 namespace {
@@ -43,9 +44,6 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));  // W2 rows of the critic are 8-B aligned
 
-#ifndef UNROLL_XW
-#define UNROLL_XW 4
-#endif
 constexpr int kIn = 12, kH1 = 256, kH2 = 128;
 constexpr int kLdS = 36, kLdH1 = 260, kLdH2 = 132;  // LDS row strides (floats): 16-B aligned, banks rotated
 constexpr int kThreads = 512;                        // grad kernels: 8 waves per 32-row sub-tile
@@ -127,108 +125,59 @@ __device__ unsigned long long g_sk_trace32[2][32][2];
   } while (0)
 #endif
 
-// ------------------------------------------------------------------ GEMM tiles
-// acc[i][j] += sum_{k0 <= k < k0+kc} X[i][k] W[n0 + j][k]: X in LDS row-major,
-// W global row-major (ldw); kc a multiple of 8
-// Software-pipelined: the weight loads of the next 4 steps (32 k) are in
-// flight while the MFMAs of the current 4 run (the weights come from L2 and
-// would otherwise stall both waves of a SIMD at every batch).
-template <int KC>
-__device__ __forceinline__ f32x16 gemm_xwT_p(f32x16 acc, const float* X, int ldx, gfp W, int ldw, int n0,
-                                             int k0, int lane) {
-  static_assert(KC % 32 == 0, "KC: multiple of 32");
+// ------------------------------------------------------------------ the acting tile's GEMMs
+// fp32 products from bf16 pieces (sk_split.hpp): D[i][n] += sum_k X[i][k]
+// W[n][k] as six v_mfma_f32_32x32x16_bf16 per 16 k — the small piece
+// products first, the hi x hi last — into one fp32 accumulator; the
+// variance GEMM of parameter noise (x^2 W^2, which only scales the noise) is
+// one more on bf16 squares.  A = the activations, row-major bf16 planes in
+// LDS (hi, mid, lo, square: `xp` elements apart), lane (r, h) reading row r,
+// k = 16 kk + 8 h + 0..7 (16 bytes); B = the weights' split pack in global
+// memory (fragment order, planes `wp` elements apart), one 16-byte load per
+// lane and k-step.  D register v of lane l is D[8(v/4) + 4(l/32) + v%4][l%32],
+// the layout of the f32 MFMA these replace: every epilogue is unchanged.
+typedef const __attribute__((address_space(1))) skmlp::bf16x8* gbf8;
+using skmlp::bf16x8;
+__device__ __forceinline__ f32x16 mfb(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x16 mf6(const bf16x8 x[3], const bf16x8 w[3], f32x16 m) {
+  m = mfb(x[2], w[0], m);
+  m = mfb(x[0], w[2], m);
+  m = mfb(x[1], w[1], m);
+  m = mfb(x[1], w[0], m);
+  m = mfb(x[0], w[1], m);
+  return mfb(x[0], w[0], m);
+}
+// kk k-steps of the tile: X rows at X (row stride ldx elements), W fragments
+// of n-tile `frag0` (kk-th at frag0 + 64 kk lanes); VAR adds the variance GEMM
+template <int KK, bool VAR>
+__device__ __forceinline__ void gemm6(f32x16& m, f32x16& v, const short* X, int ldx, int xp, gbf8 W, int wp,
+                                      int lane) {
   const int i = lane & 31, h = lane >> 5;
-  const float* xr = X + i * ldx + k0 + 4 * h;
-  const gfp wr = W + (size_t)(n0 + i) * ldw + k0 + 4 * h;
-  f4 wn[4];
+  const short* xr = X + i * ldx + 8 * h;
+  gbf8 wr = W + lane;
+  constexpr int NP = VAR ? 4 : 3;
+  bf16x8 wn[2][NP];  // two k-steps of weight fragments in flight
 #pragma unroll
-  for (int t = 0; t < 4; ++t) wn[t] = *(gf4u)(wr + 8 * t);
+  for (int d = 0; d < 2 && d < KK; ++d)
 #pragma unroll
-  for (int k = 0; k < KC; k += 32) {
-    f4 wc[4];
+    for (int q = 0; q < NP; ++q) wn[d][q] = wr[(size_t)q * (wp / 8) + 64 * d];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) wc[t] = wn[t];
-    if (k + 32 < KC) {
+  for (int kk = 0; kk < KK; ++kk) {
+    bf16x8 wc[NP];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) wn[t] = *(gf4u)(wr + k + 32 + 8 * t);
+    for (int q = 0; q < NP; ++q) wc[q] = wn[kk & 1][q];
+    if (kk + 2 < KK) {
+#pragma unroll
+      for (int q = 0; q < NP; ++q) wn[kk & 1][q] = wr[(size_t)q * (wp / 8) + 64 * (kk + 2)];
     }
+    bf16x8 x[NP];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc = mf4(*(const f4*)(xr + k + 8 * t), wc[t], acc);
+    for (int q = 0; q < NP; ++q) x[q] = *(const bf16x8*)(xr + q * xp + 16 * kk);
+    m = mf6(x, wc, m);
+    if (VAR) v = mfb(x[3], wc[3], v);
   }
-  return acc;
-}
-__device__ __forceinline__ f32x16 gemm_xwT(f32x16 acc, const float* X, int ldx, gfp W, int ldw, int n0,
-                                           int k0, int kc, int lane) {
-  if (kc == 128) return gemm_xwT_p<128>(acc, X, ldx, W, ldw, n0, k0, lane);
-  if (kc == 256) return gemm_xwT_p<256>(acc, X, ldx, W, ldw, n0, k0, lane);
-  const int i = lane & 31, h = lane >> 5;
-  const float* xr = X + i * ldx + k0 + 4 * h;
-  const gfp wr = W + (size_t)(n0 + i) * ldw + k0 + 4 * h;
-#pragma unroll UNROLL_XW
-  for (int k = 0; k < kc; k += 8) acc = mf4(*(const f4*)(xr + k), *(gf4u)(wr + k), acc);
-  return acc;
-}
-// mean and variance GEMMs of parameter noise in one pass: every operand load
-// feeds both (x w and x^2 w^2: two independent accumulator chains per wave)
-// The variance GEMM of parameter noise (x^2 W^2: it only scales the noise)
-// on bf16 operands, fp32 accumulation: one v_mfma_f32_32x32x16_bf16 per 16 k
-// instead of eight 32x32x2 f32 MFMAs; the mean stays fp32.  Lane half h
-// carries k = k0 + 4h + {0..3} and k0 + 8 + 4h + {0..3} in slots 0..7 of
-// both operands (the same k in the same slot: the dot product is unchanged).
-// The noise scale sqrt(b^2 + var) is then within ~2^-9 relative of the fp32
-// form's (SK_VAR_BF16=0 builds that one).
-#ifndef SK_VAR_BF16
-#define SK_VAR_BF16 1
-#endif
-__device__ __forceinline__ void gemm_xwT_mv(f32x16& m, f32x16& v, const float* X, int ldx, gfp W, int ldw,
-                                            int n0, int k0, int kc, int lane) {
-  const int i = lane & 31, h = lane >> 5;
-  const float* xr = X + i * ldx + k0 + 4 * h;
-  const gfp wr = W + (size_t)(n0 + i) * ldw + k0 + 4 * h;
-#if SK_VAR_BF16
-#pragma unroll 2
-  for (int k = 0; k < kc; k += 16) {
-    const f4 x0 = *(const f4*)(xr + k), x1 = *(const f4*)(xr + k + 8);
-    const f4 w0 = *(gf4u)(wr + k), w1 = *(gf4u)(wr + k + 8);
-    m = mf4(x0, w0, m);
-    m = mf4(x1, w1, m);
-    const skmlp::bf16x8 xs = {skmlp::f2bf(x0.x * x0.x), skmlp::f2bf(x0.y * x0.y), skmlp::f2bf(x0.z * x0.z), skmlp::f2bf(x0.w * x0.w),
-                       skmlp::f2bf(x1.x * x1.x), skmlp::f2bf(x1.y * x1.y), skmlp::f2bf(x1.z * x1.z), skmlp::f2bf(x1.w * x1.w)};
-    const skmlp::bf16x8 ws = {skmlp::f2bf(w0.x * w0.x), skmlp::f2bf(w0.y * w0.y), skmlp::f2bf(w0.z * w0.z), skmlp::f2bf(w0.w * w0.w),
-                       skmlp::f2bf(w1.x * w1.x), skmlp::f2bf(w1.y * w1.y), skmlp::f2bf(w1.z * w1.z), skmlp::f2bf(w1.w * w1.w)};
-    v = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xs, ws, v, 0, 0, 0);
-  }
-#else
-#pragma unroll 4
-  for (int k = 0; k < kc; k += 8) {
-    const f4 x = *(const f4*)(xr + k);
-    const f4 w = *(gf4u)(wr + k);
-    m = mf4(x, w, m);
-    v = mf4(x * x, w * w, v);
-  }
-#endif
-}
-// layer 1 (K = 12): k 0..7 by both halves, k 8..11 by half 0 (half 1's
-// 12..15 are zero operands, never loaded)
-template <bool SQ>
-__device__ __forceinline__ f32x16 gemm_l1(const float* S, gfp W1, int n0, int lane) {
-  const int i = lane & 31, h = lane >> 5;
-  f4 x0 = *(const f4*)(S + i * kLdS + 4 * h);
-  f4 w0 = *(gf4u)(W1 + (n0 + i) * kIn + 4 * h);
-  f4 x1 = {0.f, 0.f, 0.f, 0.f}, w1 = {0.f, 0.f, 0.f, 0.f};
-  if (h == 0) {
-    x1 = *(const f4*)(S + i * kLdS + 8);
-    w1 = *(gf4u)(W1 + (n0 + i) * kIn + 8);
-  }
-  if (SQ) {
-    x0 *= x0;
-    w0 *= w0;
-    x1 *= x1;
-    w1 *= w1;
-  }
-  f32x16 acc = {0};
-  acc = mf4(x0, w0, acc);
-  return mf4(x1, w1, acc);
 }
 
 // ================================================================ gradient kernels
@@ -1504,42 +1453,72 @@ struct RowsPlayers {
 // sd sqrt(x^2 W^2 + b^2) xi, xi ~ N(0,1) per (row, unit) (exact in
 // distribution for w' = w (1 + sd N(0,1)) drawn per row, each noisy weight
 // being used once per row).  The actions go to out[R(i)] and, if act_lds,
-// to act_lds[i].  S, H1, H2: the tile's LDS.  Phase trace of the 4,096-game
-// act + step launch (tools/trace_act_step.py, profiles/r03t_*): staging 1.1,
-// layer 1 1.3, layer 2 5.2 (128 dependent 32x32x2 f32 MFMAs per wave, ~0.77
-// of the CU's f32 MFMA rate), layer 3 1.2, the step 2.8 us.  Preloading every
-// weight operand before (or after) the staging loads was slower at every
-// size (profiles/r03u2_*, r03u3_*: layer 2 stays ~4.4 us, the staging waits
-// behind the weight traffic, occupancy halves).
+// to act_lds[i].  GEMMs on split bf16 pieces (gemm6, sk_split.hpp): fp32
+// products at the bf16 MFMA rate, W1 / W2 read from the actor's split pack
+// `pk`, biases and W3 from the flat vector.  LDS (ActorLds, kActorTileLds
+// bytes): the observations and the layer-1 outputs as four bf16 planes each
+// (hi, mid, lo, square; written once by the producing lane, read by every
+// wave's A fragments), layer 2's fp32 outputs over the layer-1 planes once
+// every wave has read them.  Round 3's f32-MFMA tile (128 dependent 32x32x2
+// f32 MFMAs per wave in layer 2: 5.2 us of the 4,096-game acting launch,
+// profiles/r03t_*) and its variance GEMM's bf16 operands are replaced.
+constexpr int kLdX1 = 24, kLdX2 = 264;              // bf16 row strides (48 / 528 B: conflict-free 16-B reads)
+constexpr int kX1Plane = 32 * kLdX1, kX2Plane = 32 * kLdX2;
+constexpr size_t kActorTileLds = (size_t)(4 * kX1Plane + 4 * kX2Plane) * 2;
+static_assert((size_t)32 * kLdH2 * 4 <= (size_t)4 * kX2Plane * 2, "layer 2's outputs fit over the layer-1 planes");
+struct ActorLds {
+  short* S;   // [4 planes][32][kLdX1]
+  short* H1;  // [4 planes][32][kLdX2]
+  float* H2;  // [32][kLdH2], aliasing H1
+};
+__device__ __forceinline__ ActorLds actor_lds(char* base) {
+  ActorLds L;
+  L.S = (short*)base;
+  L.H1 = L.S + 4 * kX1Plane;
+  L.H2 = (float*)L.H1;
+  return L;
+}
+// the four planes of element (row, col) of a bf16-plane block
+__device__ __forceinline__ void put4(short* P, int plane, int at, float v) {
+  short hi, mid, lo, sq;
+  sksplit::split4(v, hi, mid, lo, sq);
+  P[at] = hi;
+  P[plane + at] = mid;
+  P[2 * plane + at] = lo;
+  P[3 * plane + at] = sq;
+}
+
 template <bool NOISE, typename MAP>
-__device__ __forceinline__ void actor_tile32(const Net& A, const float* __restrict__ X, float* __restrict__ out,
-                                             const MAP& R, float sd, float action_sd, uint64_t seed, uint64_t call,
-                                             float* S, float* H1, float* H2, float2* act_lds) {
+__device__ __forceinline__ void actor_tile32(const Net& A, const char* __restrict__ pk,
+                                             const float* __restrict__ X, float* __restrict__ out, const MAP& R,
+                                             float sd, float action_sd, uint64_t seed, uint64_t call, ActorLds T,
+                                             float2* act_lds) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int t = threadIdx.x; t < 32 * kLdS; t += kFwdThreads) {  // S[i][k] = obs (k < 12, valid rows), else 0
-    const int i = t / kLdS, k = t - i * kLdS;
-    S[t] = (k < kIn && R.valid(i)) ? X[R(i) * kIn + k] : 0.f;
+  for (int t = threadIdx.x; t < 32 * 16; t += kFwdThreads) {  // S[i][k] = obs (k < 12, valid rows), else 0
+    const int i = t >> 4, k = t & 15;
+    put4(T.S, kX1Plane, i * kLdX1 + k, (k < kIn && R.valid(i)) ? X[R(i) * kIn + k] : 0.f);
   }
   __syncthreads();
   TP32(2);
+  const gbf8 W1 = (gbf8)(pk + sksplit::kOffW1), W2 = (gbf8)(pk + sksplit::kOffW2);
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const int nt = 2 * w + t, u = 32 * nt + (lane & 31);
-    const f32x16 m = gemm_l1<false>(S, A.W1, 32 * nt, lane);
+    f32x16 m = {0}, var = {0};
+    gemm6<1, NOISE>(m, var, T.S, kLdX1, kX1Plane, W1 + 64 * nt, sksplit::kW1Plane, lane);
     const float b = A.b1[u];
     if (NOISE) {
-      const f32x16 var = gemm_l1<true>(S, A.W1, 32 * nt, lane);
       const float k2 = skmlp::noise_k2(sd);
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         float y[4];
         noisy4(seed, call, (uint32_t)R(drow(4 * g, lane)), (uint32_t)u, k2, b, m, var, 4 * g, y);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) H1[drow(4 * g + q, lane) * kLdH1 + u] = fmaxf(y[q], 0.f);
+        for (int q = 0; q < 4; ++q) put4(T.H1, kX2Plane, drow(4 * g + q, lane) * kLdX2 + u, fmaxf(y[q], 0.f));
       }
     } else {
 #pragma unroll
-      for (int v = 0; v < 16; ++v) H1[drow(v, lane) * kLdH1 + u] = fmaxf(m[v] + b, 0.f);
+      for (int v = 0; v < 16; ++v) put4(T.H1, kX2Plane, drow(v, lane) * kLdX2 + u, fmaxf(m[v] + b, 0.f));
     }
   }
   __syncthreads();
@@ -1547,9 +1526,9 @@ __device__ __forceinline__ void actor_tile32(const Net& A, const float* __restri
   {
     const int u = 32 * w + (lane & 31);
     f32x16 m = {0}, var = {0};
-    if (NOISE) gemm_xwT_mv(m, var, H1, kLdH1, A.W2, kALd, 32 * w, 0, kH1, lane);
-    else m = gemm_xwT(m, H1, kLdH1, A.W2, kALd, 32 * w, 0, kH1, lane);
+    gemm6<16, NOISE>(m, var, T.H1, kLdX2, kX2Plane, W2 + 16 * 64 * w, sksplit::kW2Plane, lane);
     const float b = A.b2[u];
+    __syncthreads();  // every wave has read the layer-1 planes: layer 2's outputs go over them
     if (NOISE) {
       const float k2 = skmlp::noise_k2(sd);
 #pragma unroll
@@ -1557,16 +1536,17 @@ __device__ __forceinline__ void actor_tile32(const Net& A, const float* __restri
         float y[4];
         noisy4(seed, call, (uint32_t)R(drow(4 * g, lane)), (uint32_t)(kH1 + u), k2, b, m, var, 4 * g, y);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) H2[drow(4 * g + q, lane) * kLdH2 + u] = fmaxf(y[q], 0.f);
+        for (int q = 0; q < 4; ++q) T.H2[drow(4 * g + q, lane) * kLdH2 + u] = fmaxf(y[q], 0.f);
       }
     } else {
 #pragma unroll
-      for (int v = 0; v < 16; ++v) H2[drow(v, lane) * kLdH2 + u] = fmaxf(m[v] + b, 0.f);
+      for (int v = 0; v < 16; ++v) T.H2[drow(v, lane) * kLdH2 + u] = fmaxf(m[v] + b, 0.f);
     }
   }
   __syncthreads();
   TP32(4);
   {  // layer 3: thread t -> row t / 8, units 16 (t % 8) .. (both outputs)
+    const float* H2 = T.H2;
     const int i = threadIdx.x >> 3, c = threadIdx.x & 7;
     float m0 = 0.f, m1 = 0.f, v0 = 0.f, v1 = 0.f;
 #pragma unroll
@@ -1613,19 +1593,18 @@ __device__ __forceinline__ void actor_tile32(const Net& A, const float* __restri
 
 template <bool NOISE>
 __global__ void __launch_bounds__(kFwdThreads) k_actor_fwd32(const float* __restrict__ aflat,
+                                                             const char* __restrict__ apack,
                                                              const float* __restrict__ X, float* __restrict__ out,
                                                              int64_t rows, float sd, float action_sd, uint64_t seed,
                                                              uint64_t* __restrict__ call_ctr) {
-  __shared__ __attribute__((aligned(16))) float S[32 * kLdS];
-  __shared__ __attribute__((aligned(16))) float H1[32 * kLdH1];
-  __shared__ __attribute__((aligned(16))) float H2[32 * kLdH2];
+  extern __shared__ __attribute__((aligned(16))) float smem_sl[];
   const Net A = net_of(aflat, kALd, 2);
   // a launch that draws noise (parameter or action) uses call number
   // counter + 1 and its last workgroup stores that number back
   const bool draws = (NOISE || action_sd != 0.f) && call_ctr;
   const uint64_t call = draws ? call_ctr[0] + 1 : 0;
-  actor_tile32<NOISE>(A, X, out, RowsContig{(int64_t)blockIdx.x * 32, rows}, sd, action_sd, seed, call, S, H1, H2,
-                      nullptr);
+  actor_tile32<NOISE>(A, apack, X, out, RowsContig{(int64_t)blockIdx.x * 32, rows}, sd, action_sd, seed, call,
+                      actor_lds((char*)smem_sl), nullptr);
   if (draws) {  // the last workgroup to finish stores the call number it drew with
     __syncthreads();
     advance_call32(call_ctr, call, gridDim.x);
@@ -1642,15 +1621,16 @@ __global__ void __launch_bounds__(kFwdThreads) k_actor_fwd32(const float* __rest
 // finishes k_step_split's tick for its lanes.  Equal, bit for bit, to
 // sk_actor_forward_f32 (32-row tiles) followed by sk_env_step(_insert).
 // Wave 0 counts its games into counter slot line b.
-// act_step32: the body on LDS S / H1 / H2 / sAct for the first nb workgroups
-// of the grid (k_act_step32: all of them; k_bwd_act_step32: the
-// workgroups before the backward's)
-constexpr size_t kActStepLds = (size_t)32 * (kLdS + kLdH1 + kLdH2) * 4 + 32 * sizeof(float2);
+// act_step32: the body on the LDS at `smem` (the actor tile's, then sAct)
+// for the first nb workgroups of the grid (k_act_step32: all of them;
+// k_bwd_act_step32: the workgroups before the backward's)
+constexpr size_t kActStepLds = kActorTileLds + 32 * sizeof(float2);
 template <bool NOISE>
-__device__ __forceinline__ void act_step32(const float* __restrict__ aflat, float* __restrict__ act_out, float sd,
-                                           float action_sd, uint64_t seed, uint64_t* __restrict__ call_ctr,
-                                           sk::StepArgs a, sk::Cfg c, float* S, float* H1, float* H2,
-                                           float2* sAct, unsigned nb) {
+__device__ __forceinline__ void act_step32(const float* __restrict__ aflat, const char* __restrict__ apack,
+                                           float* __restrict__ act_out, float sd, float action_sd, uint64_t seed,
+                                           uint64_t* __restrict__ call_ctr, sk::StepArgs a, sk::Cfg c, char* smem,
+                                           unsigned nb) {
+  float2* sAct = (float2*)(smem + kActorTileLds);
   const int lane = threadIdx.x & 63;
   const bool w0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0;
   const int64_t g0 = (int64_t)blockIdx.x * 16;
@@ -1662,7 +1642,8 @@ __device__ __forceinline__ void act_step32(const float* __restrict__ aflat, floa
   const Net A = net_of(aflat, kALd, 2);
   const bool draws = (NOISE || action_sd != 0.f) && call_ctr;
   const uint64_t call = draws ? call_ctr[0] + 1 : 0;
-  actor_tile32<NOISE>(A, a.acting_obs, act_out, RowsPlayers{g0, a.n}, sd, action_sd, seed, call, S, H1, H2, sAct);
+  actor_tile32<NOISE>(A, apack, a.acting_obs, act_out, RowsPlayers{g0, a.n}, sd, action_sd, seed, call,
+                      actor_lds(smem), sAct);
   TP32(5);
   __syncthreads();
   TP32(6);
@@ -1678,16 +1659,13 @@ __device__ __forceinline__ void act_step32(const float* __restrict__ aflat, floa
 }
 
 template <bool NOISE>
-__global__ void __launch_bounds__(kFwdThreads) k_act_step32(const float* __restrict__ aflat, float* __restrict__ act_out,
-                                                            float sd, float action_sd, uint64_t seed,
-                                                            uint64_t* __restrict__ call_ctr, sk::StepArgs a,
-                                                            sk::Cfg c) {
+__global__ void __launch_bounds__(kFwdThreads) k_act_step32(const float* __restrict__ aflat,
+                                                            const char* __restrict__ apack,
+                                                            float* __restrict__ act_out, float sd, float action_sd,
+                                                            uint64_t seed, uint64_t* __restrict__ call_ctr,
+                                                            sk::StepArgs a, sk::Cfg c) {
   extern __shared__ __attribute__((aligned(16))) float smem_sl[];
-  float* S = smem_sl;
-  float* H1 = S + 32 * kLdS;
-  float* H2 = H1 + 32 * kLdH1;
-  act_step32<NOISE>(aflat, act_out, sd, action_sd, seed, call_ctr, a, c, S, H1, H2, (float2*)(H2 + 32 * kLdH2),
-                    gridDim.x);
+  act_step32<NOISE>(aflat, apack, act_out, sd, action_sd, seed, call_ctr, a, c, (char*)smem_sl, gridDim.x);
 }
 
 
@@ -1902,6 +1880,7 @@ static_assert(kSlThreads == kFwdThreads, "one workgroup size for both halves");
 template <int MODE, bool NOISE, bool A16>
 __global__ void __launch_bounds__(kFwdThreads) k_bwd_act_step32(SK_SLICE_BWD_PARAMS, unsigned GA,
                                                                 const float* __restrict__ aflat,
+                                                                const char* __restrict__ apack,
                                                                 float* __restrict__ act_out, float sd, float action_sd,
                                                                 uint64_t aseed, uint64_t* __restrict__ acall_ctr,
                                                                 sk::StepArgs a, sk::Cfg c) {
@@ -1909,11 +1888,7 @@ __global__ void __launch_bounds__(kFwdThreads) k_bwd_act_step32(SK_SLICE_BWD_PAR
   if (A16 && blockIdx.x < GA) {
     act_step16<NOISE>(aflat, act_out, sd, action_sd, aseed, acall_ctr, a, c, smem_sl, GA);
   } else if (blockIdx.x < GA) {
-    float* S = smem_sl;
-    float* H1 = S + 32 * kLdS;
-    float* H2 = H1 + 32 * kLdH1;
-    act_step32<NOISE>(aflat, act_out, sd, action_sd, aseed, acall_ctr, a, c, S, H1, H2, (float2*)(H2 + 32 * kLdH2),
-                      GA);
+    act_step32<NOISE>(aflat, apack, act_out, sd, action_sd, aseed, acall_ctr, a, c, (char*)smem_sl, GA);
   } else {
     grad_slice_bwd<MODE>((int)(blockIdx.x - GA), smem_sl, SK_SLICE_BWD_ARGS);
   }
@@ -1984,7 +1959,8 @@ int launch_sliced(const float* f0, const float* f1, const float* f2, const float
 #define SK_BWD_ACT(NZ, A6)                                                                                          \
   k_bwd_act_step32<MODE, NZ, A6><<<GA + G, kFwdThreads, lds, st>>>(                                                 \
       f0, f1, f2, S, A, Y, R, D, gamma, B, key_row0, scale, seed, call_ctr, Z, partials, scratch, stat_out, mask_out, \
-      GA, job->aflat, job->act_out, NZ ? job->sd : 0.f, job->action_sd, job->seed, job->call_ctr, a, job->c)
+      GA, job->aflat, job->apack, job->act_out, NZ ? job->sd : 0.f, job->action_sd, job->seed, job->call_ctr, a, \
+      job->c)
     if (job->sd != 0.f) {
       if (a16) SK_BWD_ACT(true, true);
       else SK_BWD_ACT(true, false);
@@ -2001,6 +1977,38 @@ int launch_sliced(const float* f0, const float* f1, const float* f2, const float
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
 }
 
+// the split pack (sk_split.hpp) from the actor's flat fp32 parameters: one
+// thread per plane element (the W1 padding k = 12..15 written as zero)
+__global__ void k_split_pack32(const float* __restrict__ aflat, char* __restrict__ out) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  short* b;
+  int idx, plane;
+  float v;
+  if (t < sksplit::kW1Plane) {
+    idx = t;
+    const int j = t & 7, lane = (t >> 3) & 63, nt = t >> 9;
+    const int n = 32 * nt + (lane & 31), k = 8 * (lane >> 5) + j;
+    v = k < kIn ? aflat[kPW1 + n * kIn + k] : 0.f;
+    b = (short*)(out + sksplit::kOffW1);
+    plane = sksplit::kW1Plane;
+  } else if (t < sksplit::kW1Plane + sksplit::kW2Plane) {
+    idx = t - sksplit::kW1Plane;
+    const int j = idx & 7, lane = (idx >> 3) & 63, kk = (idx >> 9) & 15, nt = idx >> 13;
+    const int o = 32 * nt + (lane & 31), i = 16 * kk + 8 * (lane >> 5) + j;
+    v = aflat[kPW2 + o * kALd + i];
+    b = (short*)(out + sksplit::kOffW2);
+    plane = sksplit::kW2Plane;
+  } else {
+    return;
+  }
+  short hi, mid, lo, sq;
+  sksplit::split4(v, hi, mid, lo, sq);
+  b[idx] = hi;
+  b[plane + idx] = mid;
+  b[2 * plane + idx] = lo;
+  b[3 * plane + idx] = sq;
+}
+
 }  // namespace
 
 // csrc/sk_replay.hip
@@ -2009,8 +2017,8 @@ int replay_sample_excl(const float* ring, int64_t capacity, const int64_t* total
                        hipStream_t stream);
 
 // the self-play tick launch (sk_env_act_step, csrc/sk_engine.hip): a.n % 4 == 0
-int sk_launch_act_step32(const float* aflat, float* act_out, float sd, float action_sd, uint64_t seed,
-                         uint64_t* call_ctr, const sk::StepArgs& a, const sk::Cfg& c, hipStream_t st) {
+int sk_launch_act_step32(const float* aflat, const void* apack, float* act_out, float sd, float action_sd,
+                         uint64_t seed, uint64_t* call_ctr, const sk::StepArgs& a, const sk::Cfg& c, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
     set_lds32(k_act_step32<true>, kActStepLds);
@@ -2026,11 +2034,14 @@ int sk_launch_act_step32(const float* aflat, float* act_out, float sd, float act
                                                                   c);
     return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
   }
+  if (!apack || (((uintptr_t)apack) & 15)) return SK_EINVAL;  // the 32-row tile reads the split pack
   const unsigned G = (unsigned)((a.n + 15) / 16);
+  const char* pk = (const char*)apack;
   if (sd != 0.f)
-    k_act_step32<true><<<G, kFwdThreads, kActStepLds, st>>>(aflat, act_out, sd, action_sd, seed, call_ctr, a, c);
+    k_act_step32<true><<<G, kFwdThreads, kActStepLds, st>>>(aflat, pk, act_out, sd, action_sd, seed, call_ctr, a, c);
   else
-    k_act_step32<false><<<G, kFwdThreads, kActStepLds, st>>>(aflat, act_out, 0.f, action_sd, seed, call_ctr, a, c);
+    k_act_step32<false><<<G, kFwdThreads, kActStepLds, st>>>(aflat, pk, act_out, 0.f, action_sd, seed, call_ctr, a,
+                                                             c);
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
 }
 
@@ -2097,7 +2108,7 @@ static int critic_f32(const float* critic_flat, const float* obs, const float* a
       target_critic_flat);
   if (hipGetLastError() != hipSuccess) return SK_EHIP;
   if (!job) return SK_OK;
-  return sk_launch_act_step32(job->aflat, job->act_out, job->sd, job->action_sd, job->seed, job->call_ctr, job->a,
+  return sk_launch_act_step32(job->aflat, job->apack, job->act_out, job->sd, job->action_sd, job->seed, job->call_ctr, job->a,
                               job->c, (hipStream_t)stream);
 }
 
@@ -2163,7 +2174,7 @@ static int critic_sampled(const float* critic_flat, const sk_ring_sample* q, flo
                                      target_critic_flat, batch, row_offset, grad_scale, seed, call_counter, partials,
                                      step_counters, n_steps, loss_sum, dropout_mask, scratch, stream);
   if (rc2 != SK_OK || !job) return rc2;
-  return sk_launch_act_step32(job->aflat, job->act_out, job->sd, job->action_sd, job->seed, job->call_ctr, job->a,
+  return sk_launch_act_step32(job->aflat, job->apack, job->act_out, job->sd, job->action_sd, job->seed, job->call_ctr, job->a,
                               job->c, (hipStream_t)stream);
 }
 
@@ -2236,12 +2247,13 @@ int sk_actor_grad_f32_step(const float* actor_flat, const float* critic_flat, co
   const int rc = sk_actor_grad_f32(actor_flat, critic_flat, obs, batch, loss_scale, partials, step_counters, n_steps,
                                    q_sum, scratch, stream);
   if (rc != SK_OK) return rc;
-  return sk_launch_act_step32(j.aflat, j.act_out, j.sd, j.action_sd, j.seed, j.call_ctr, j.a, j.c,
+  return sk_launch_act_step32(j.aflat, j.apack, j.act_out, j.sd, j.action_sd, j.seed, j.call_ctr, j.a, j.c,
                               (hipStream_t)stream);
 }
 
-int sk_actor_forward_f32(const float* actor_flat, const float* obs, float* actions, int64_t rows, float noise_sd,
-                         float action_sd, uint64_t seed, uint64_t* call_counter, void* stream) {
+int sk_actor_forward_f32(const float* actor_flat, const void* actor_pack, const float* obs, float* actions,
+                         int64_t rows, float noise_sd, float action_sd, uint64_t seed, uint64_t* call_counter,
+                         void* stream) {
   if (!actor_flat || !obs || !actions || rows <= 0) return SK_EINVAL;
   if ((((uintptr_t)actions) & 7)) return SK_EINVAL;
   if (fwd16_rows(rows)) {
@@ -2254,13 +2266,31 @@ int sk_actor_forward_f32(const float* actor_flat, const float* obs, float* actio
                                                                            action_sd, seed, call_counter);
     return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
   }
+  if (!actor_pack || (((uintptr_t)actor_pack) & 15)) return SK_EINVAL;  // the 32-row tile reads the split pack
+  static bool attr = false;
+  if (!attr) {
+    set_lds32(k_actor_fwd32<true>, kActorTileLds);
+    set_lds32(k_actor_fwd32<false>, kActorTileLds);
+    attr = true;
+  }
   const unsigned G = (unsigned)((rows + 31) / 32);
+  const char* pk = (const char*)actor_pack;
   if (noise_sd != 0.f)
-    k_actor_fwd32<true><<<G, kFwdThreads, 0, (hipStream_t)stream>>>(actor_flat, obs, actions, rows, noise_sd,
-                                                                      action_sd, seed, call_counter);
+    k_actor_fwd32<true><<<G, kFwdThreads, kActorTileLds, (hipStream_t)stream>>>(actor_flat, pk, obs, actions, rows,
+                                                                                 noise_sd, action_sd, seed,
+                                                                                 call_counter);
   else
-    k_actor_fwd32<false><<<G, kFwdThreads, 0, (hipStream_t)stream>>>(actor_flat, obs, actions, rows, 0.f, action_sd,
-                                                                       seed, call_counter);
+    k_actor_fwd32<false><<<G, kFwdThreads, kActorTileLds, (hipStream_t)stream>>>(actor_flat, pk, obs, actions, rows,
+                                                                                  0.f, action_sd, seed, call_counter);
+  return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
+}
+
+size_t sk_actor_split_pack_bytes(void) { return sksplit::kBytes; }
+
+int sk_actor_split_pack_f32(const float* actor_flat, void* actor_pack, void* stream) {
+  if (!actor_flat || !actor_pack || (((uintptr_t)actor_pack) & 15)) return SK_EINVAL;
+  const int n = sksplit::kW1Plane + sksplit::kW2Plane;  // one thread per plane-0 element
+  k_split_pack32<<<(n + 255) / 256, 256, 0, (hipStream_t)stream>>>(actor_flat, (char*)actor_pack);
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
 }
 

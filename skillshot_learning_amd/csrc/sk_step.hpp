@@ -222,6 +222,7 @@ struct ActStepJob {
   StepArgs a;
   Cfg c;
   const float* aflat;
+  const char* apack;  // the actor's split pack (sk_split.hpp; the 32-row tile)
   float* act_out;
   float sd, action_sd;
   uint64_t seed;
@@ -462,5 +463,5 @@ __device__ __forceinline__ void split_finish(const StepArgs& a, const Cfg& c, co
 
 // k_act_step32 (csrc/sk_learn32.hip): the fp32 actor forward and k_step_split
 // in one launch, 16 games per 256-lane workgroup (sk_env_act_step)
-int sk_launch_act_step32(const float* aflat, float* act_out, float sd, float action_sd, uint64_t seed,
-                         uint64_t* call_ctr, const sk::StepArgs& a, const sk::Cfg& c, hipStream_t st);
+int sk_launch_act_step32(const float* aflat, const void* apack, float* act_out, float sd, float action_sd,
+                         uint64_t seed, uint64_t* call_ctr, const sk::StepArgs& a, const sk::Cfg& c, hipStream_t st);

@@ -39,6 +39,7 @@
 #include "../../include/skillshot.h"
 #include "sk_mlp.hpp"
 #include "sk_partial.hpp"
+#include "sk_split.hpp"
 
 namespace {
 
@@ -930,6 +931,7 @@ struct PackOut {
   char* tp;   // grad pack of its soft-updated target (nullable)
   char* fp;   // actor forward pack (sk_actor_pack layout; nullable, actor only)
   int ld2, n_out;
+  char* sp;   // the fp32 actor's split pack (sk_split.hpp; nullable, actor only)
 };
 
 __device__ __forceinline__ void scatter_grad_pack(char* out, int p, float v, int ld2, int n_out) {
@@ -1076,6 +1078,7 @@ __global__ void __launch_bounds__(kAdamParams * kAdamSlices) k_adam_flat(const f
   param[p] = w;
   if (po.gp) scatter_grad_pack(po.gp, p, w, po.ld2, po.n_out);
   if (po.fp) scatter_fwd_pack(po.fp, p, w);
+  if (po.sp) sksplit::scatter_split_pack(po.sp, p, w);
   if (target) {
     const float tw = tw0 + tau * (w - tw0);
     target[p] = tw;
@@ -1227,16 +1230,17 @@ int sk_adam_flat_sliced(const float* partial, int32_t n_partials, const float* p
   if (n_params <= 0 || n_partials < 0 || (n_partials > 0 && !partial)) return SK_EINVAL;
   if (n_w1 < 0 || (n_w1 > 0 && !partials_w1) || (partials_w1 && n_params < skpart::kPW2)) return SK_EINVAL;
   if (apply && (!param || !exp_avg || !exp_avg_sq || !step_counter)) return SK_EINVAL;
-  PackOut po = {nullptr, nullptr, nullptr, kH1, 1};
+  PackOut po = {nullptr, nullptr, nullptr, kH1, 1, nullptr};
   if (packs && apply) {
     const int ld2 = packs->ld2, n_out = packs->n_out;
     if ((ld2 != kH1 && ld2 != kH1 + 2) || (n_out != 1 && n_out != 2)) return SK_EINVAL;
     if (n_params != kPW2 + kH2 * ld2 + kH2 + n_out * kH2 + n_out) return SK_EINVAL;
-    if (packs->actor_fwd_pack && (ld2 != kH1 || n_out != kOut)) return SK_EINVAL;
+    if ((packs->actor_fwd_pack || packs->actor_split_pack) && (ld2 != kH1 || n_out != kOut)) return SK_EINVAL;
     if (packs->target_gpack && !target) return SK_EINVAL;
-    for (const void* b : {packs->param_gpack, packs->target_gpack, packs->actor_fwd_pack})
+    for (const void* b : {packs->param_gpack, packs->target_gpack, packs->actor_fwd_pack, packs->actor_split_pack})
       if (((uintptr_t)b) & 15) return SK_EINVAL;
-    po = {(char*)packs->param_gpack, (char*)packs->target_gpack, (char*)packs->actor_fwd_pack, ld2, n_out};
+    po = {(char*)packs->param_gpack, (char*)packs->target_gpack, (char*)packs->actor_fwd_pack, ld2, n_out,
+          (char*)packs->actor_split_pack};
   }
   k_adam_flat<<<(n_params + kAdamParams - 1) / kAdamParams, kAdamParams * kAdamSlices, 0, (hipStream_t)stream>>>(
       partial, n_partials, n_params, grad_in, grad_out, apply, param, exp_avg, exp_avg_sq, step_counter, lr, beta1,

@@ -754,8 +754,10 @@ class SkillshotLearner:
         self.actor_kernel = None
         if actor_kernel and self.device.type == "cuda":
             from .actor_kernel import ActorKernel, ActorKernel32
-            if precision == "fp32":  # reads the actor's flat fp32 parameters: nothing to repack
+            if precision == "fp32":  # flat fp32 parameters + the split pack the actor's Adam launch rewrites
                 self.actor_kernel = ActorKernel32(self.model_actor, seed=seed * 1000003 + env_offset)
+                if self.ddpg._fused is not None:
+                    self.ddpg._fused.split_pack = self.actor_kernel.pack
             else:
                 self.actor_kernel = ActorKernel(self.model_actor, seed=seed * 1000003 + env_offset)
                 if self.ddpg._fused is not None:  # the actor's Adam launch writes the forward pack too
@@ -779,7 +781,10 @@ class SkillshotLearner:
         if self.actor_kernel is None:
             return
         fu = self.ddpg._fused
-        if fu is not None and fu.fwd_pack is self.actor_kernel.buf:
+        if fu is not None and self.actor_kernel.buf is not None and fu.fwd_pack is self.actor_kernel.buf:
+            return
+        if fu is not None and getattr(self.actor_kernel, "pack", None) is not None and \
+                fu.split_pack is self.actor_kernel.pack:
             return
         self.actor_kernel.refresh()
 

@@ -41,7 +41,8 @@ class RingSample(ctypes.Structure):
 class PackTargets(ctypes.Structure):
     """sk_pack_targets (include/skillshot.h): the packed copies an Adam launch writes."""
     _fields_ = [("param_gpack", ctypes.c_void_p), ("target_gpack", ctypes.c_void_p),
-                ("actor_fwd_pack", ctypes.c_void_p), ("ld2", ctypes.c_int32), ("n_out", ctypes.c_int32)]
+                ("actor_fwd_pack", ctypes.c_void_p), ("ld2", ctypes.c_int32), ("n_out", ctypes.c_int32),
+                ("actor_split_pack", ctypes.c_void_p)]
 
 
 def flatten_module(module):
@@ -177,6 +178,9 @@ class FusedUpdate:
         # the actor forward kernel's weight pack (ActorKernel.buf), written by
         # the actor's Adam launch when bound (SkillshotLearner binds it)
         self.fwd_pack = None
+        # the fp32 actor's split pack (ActorKernel32.pack, sk_split.hpp),
+        # likewise written by the actor's Adam launch when bound
+        self.split_pack = None
         self.pack()
 
     def rebind_optimisers(self):
@@ -239,7 +243,9 @@ class FusedUpdate:
     def _packs(self, critic):
         """the packs the Adam launch of a step keeps current"""
         if self.f32:
-            return None
+            if critic or self.split_pack is None:
+                return None
+            return PackTargets(None, None, None, 256, 2, self.split_pack.data_ptr())
         if critic:
             return PackTargets(self.gpc.data_ptr(), self.gptc.data_ptr() if self.tc is not None else None, None,
                                258, 1)
@@ -251,7 +257,8 @@ class FusedUpdate:
         if not self.soft_update_in_adam:
             target = None
             if packs is not None:
-                packs = PackTargets(packs.param_gpack, None, packs.actor_fwd_pack, packs.ld2, packs.n_out)
+                packs = PackTargets(packs.param_gpack, None, packs.actor_fwd_pack, packs.ld2, packs.n_out,
+                                    packs.actor_split_pack)
         pk = ctypes.byref(packs) if packs is not None else None
         tau = float(self.d.tau) if target is not None else 0.0
         if self.d.multi():  # sum partials -> flat grad -> RCCL sum (losses are global-batch normalised) -> apply

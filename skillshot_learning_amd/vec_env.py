@@ -333,7 +333,8 @@ class VecSkillshotGame:
         ring_args = ((_ptr(ring.buf), ring.cap, _ptr(ring.total_t), _ptr(ring.arrivals()), _ptr(total_copy))
                      if ring is not None else (None, 0, None, None, None))
         actor.calls += 1
-        args = (self._h, _ptr(actor.flat), _ptr(s), _ptr(act), float(noise_sd), float(action_sd), actor.seed,
+        pack = actor.ensure_pack()
+        args = (self._h, _ptr(actor.flat), _ptr(pack), _ptr(s), _ptr(act), float(noise_sd), float(action_sd), actor.seed,
                 _ptr(actor._ctr), _ptr(obs_t), _ptr(rew_t), REWARD_KINDS[reward], _ptr(done), _ptr(win),
                 self.tick_limit, int(bool(auto_reset)), int(self.random_positions), _ptr(obs_r), *ring_args)
         if job is not None:

@@ -260,3 +260,26 @@ def test_actor_forward_f32_action_noise(mods, fwd):
     assert abs(float(z.mean())) < 0.01 and abs(float(z.std()) - 1.0) < 0.01
     assert abs(float((z.abs() < 1).double().mean()) - 0.6827) < 0.01  # normal, not uniform
     assert not torch.equal(a1, a2)
+
+
+def test_split_pack_follows_updates(mods):
+    """the fp32 actor's split pack (sk_split.hpp) stays the pack of the
+    current parameters: after fused updates (the actor's Adam launch rewrites
+    it) it equals a fresh sk_actor_split_pack_f32 bit for bit, and a change
+    made through torch is repacked at the next forward"""
+    learner, kr = mods
+    L = learner.SkillshotLearner(n_envs=512, device="cuda", seed=3, exploration="param_noise", gamma=0.9, tau=0.01,
+                                 replay_capacity=1 << 14, precision="fp32")
+    L.train_ticks(6, batch=128, warmup=128)
+    torch.cuda.synchronize()
+    k = L.actor_kernel
+    got = k.pack.clone()
+    k.refresh()
+    torch.cuda.synchronize()
+    assert torch.equal(got, k.pack)
+    with torch.no_grad():
+        L.model_actor.l2.weight.mul_(1.5)  # a torch-side change: the next call repacks
+    s = _obs(8192, 2)
+    out = k(s)
+    want, _ = kr.actor_forward(kr.from_module(L.model_actor), _np(s))
+    assert np.abs(_np(out) - want).max() <= 1e-5
