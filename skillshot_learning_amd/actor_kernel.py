@@ -115,53 +115,6 @@ class ActorKernel32:
             self.refresh()
         return self.pack
 
-    fused_action_noise = True  # model_act_action_noise's N(0, sd) is drawn in the kernel (sk_actor_forward_noise)
-
-    @torch.no_grad()
-    def __call__(self, obs, noise_sd=0.0, generator=None, out=None, action_sd=0.0):
-        """obs float32 [M, 12] -> actions float32 [M, 2]; noise_sd: parameter
-        noise, action_sd: action noise on the tanh outputs."""
-        x = obs if obs.dtype == torch.float32 else obs.float()
-        x = x.contiguous()
-        if x.dim() != 2 or x.shape[1] != 12:
-            raise ValueError("obs must be [M, 12]")
-        m = x.shape[0]
-        y = out if out is not None else torch.empty((m, 2), dtype=torch.float32, device=self.device)
-        self.calls += 1
-        rc = self.L.sk_actor_forward_noise(ctypes.c_void_p(self.buf.data_ptr()), ctypes.c_void_p(x.data_ptr()),
-                                           ctypes.c_void_p(y.data_ptr()), m, float(noise_sd), float(action_sd),
-                                           self.seed, ctypes.c_void_p(self._ctr.data_ptr()), self._stream())
-        if rc != 0:
-            raise SkillshotError(f"sk_actor_forward failed ({rc})")
-        return y
-
-
-class ActorKernel32:
-    """The actor forward at the reference's precision (csrc/sk_learn32.hip
-    k_actor_fwd32: fp32 operands on v_mfma_f32_32x32x2_f32), reading the
-    actor's flat fp32 parameter vector directly: no pack, nothing to refresh
-    after an update.  Same call interface as ActorKernel."""
-
-    buf = None  # no pack for an Adam launch to keep current
-
-    def __init__(self, actor, seed=0):
-        from .update_kernel import flatten_module
-        self.actor = actor
-        self.L = _capi.load()
-        p = next(actor.parameters())
-        if p.device.type != "cuda":
-            raise SkillshotError("ActorKernel32 needs the actor on a gfx950 GPU")
-        self.device = p.device
-        self.flat = flatten_module(actor)
-        self.seed = int(seed) & ((1 << 64) - 1)
-        self.calls = 0
-        self._ctr = torch.zeros(130, dtype=torch.int64, device=self.device)  # SK_ACTOR_COUNTER_WORDS
-        self.counter = self._ctr[:1]
-
-    def refresh(self):
-        from .update_kernel import flatten_module
-        self.flat = flatten_module(self.actor)  # idempotent: the parameters stay views of it
-
     fused_action_noise = True  # model_act_action_noise's N(0, sd) is drawn in the kernel
     fused_act_step = True  # the self-play tick runs it inside the step launch (VecSkillshotGame.act_step)
 
