@@ -246,6 +246,25 @@ int sk_env_act_step(sk_env* env, const float* actor_flat, const void* actor_pack
                     int32_t random_positions, float* obs_reset, float* ring, int64_t capacity, int64_t* total,
                     uint32_t* arrivals, int64_t* total_copy, void* stream);
 
+/* The reference rule's episode collection in ONE launch (ABI 9;
+ * SkillshotLearner.model_train :289-318 for every game at once): each game
+ * plays its episode from the current state — act with the fp32 actor
+ * (parameter noise noise_sd / action noise action_sd, fresh per tick: tick t
+ * draws as the t-th of n_ticks sk_env_act_step calls would), do_actions,
+ * game_tick, get_state — while game_live and ticks < tick_limit; a game
+ * that has ended is not stepped again.  states float[n_ticks + 1][2][N][12]
+ * (16-byte aligned): states[0] the caller's observation of the start
+ * (sk_env_observe); tick t reads states[t] and writes actions[t]
+ * (float[n_ticks][2][N][2]), states[t + 1] (the post-tick observation) and
+ * rewards[t] (float[n_ticks][2][N]; reward_kind as sk_env_step's); rows of
+ * ticks a game did not play are left unwritten.  lengths int32[N] = the
+ * ticks each game played.  N % 4 == 0; the step counter and the noise call
+ * number advance by n_ticks; no episode counters.  GPU backend only. */
+int sk_env_act_episode(sk_env* env, const float* actor_flat, const void* actor_pack, float* states, float* actions,
+                       float* rewards, int32_t* lengths, int32_t n_ticks, float noise_sd, float action_sd,
+                       uint64_t noise_seed, uint64_t* call_counter, int32_t reward_kind, int32_t tick_limit,
+                       void* stream);
+
 /* sk_env_act_step prepared, not launched (ABI 8): the same arguments
  * (N % 4 == 0, ring given or not) into *job, and the env advances its step
  * slot as if the launch had been issued.  The job is then run, exactly once

@@ -25,7 +25,7 @@ EXPORTS = (
     "sk_env_clear_counters", "sk_env_get_step_counter",
     "sk_env_set_step_counter", "sk_env_sync_step_counter", "sk_env_reset", "sk_player_move_direction", "sk_player_move_look",
     "sk_player_move_discrete", "sk_player_shoot", "sk_projectile_move", "sk_game_check_collision", "sk_game_tick", "sk_env_features", "sk_env_observe",
-    "sk_env_step", "sk_env_step_insert", "sk_env_act_step", "sk_env_act_step_job", "sk_env_step_multi", "sk_env_step_multi_obs", "sk_gen_random_actions", "sk_env_rollout_random",
+    "sk_env_step", "sk_env_step_insert", "sk_env_act_step", "sk_env_act_step_job", "sk_env_act_episode", "sk_env_step_multi", "sk_env_step_multi_obs", "sk_gen_random_actions", "sk_env_rollout_random",
     "sk_actor_packed_bytes", "sk_actor_pack", "sk_actor_forward", "sk_actor_forward_dev",
     "sk_actor_forward_advance", "sk_actor_forward_noise",
     "sk_critic_packed_bytes", "sk_critic_pack", "sk_critic_forward", "sk_target_q",
@@ -120,6 +120,7 @@ def load(build_if_missing=True):
         "sk_env_step_insert": ([P, P, P, P, i32, P, P, i32, i32, i32, P, P, P, i64, P, P, P, P], ctypes.c_int),
         "sk_env_act_step": ([P, P, P, P, P, f32, f32, u64, P, P, P, i32, P, P, i32, i32, i32, P, P, i64, P, P, P, P],
                             ctypes.c_int),
+        "sk_env_act_episode": ([P, P, P, P, P, P, P, i32, f32, f32, u64, P, i32, i32, P], ctypes.c_int),
         "sk_env_act_step_job": ([P, P, P, P, P, f32, f32, u64, P, P, P, i32, P, P, i32, i32, i32, P, P, i64, P, P, P,
                                  ctypes.POINTER(SkStepJob)], ctypes.c_int),
         "sk_env_step_multi": ([P, P, i64, i64, i32, P, P, i64, i32, i32, i32, P], ctypes.c_int),

@@ -1712,6 +1712,26 @@ int sk_env_act_step(sk_env* e, const float* actor_flat, const void* actor_pack, 
   return SK_OK;
 }
 
+int sk_env_act_episode(sk_env* e, const float* actor_flat, const void* actor_pack, float* states, float* actions,
+                       float* rewards, int32_t* lengths, int32_t n_ticks, float noise_sd, float action_sd,
+                       uint64_t noise_seed, uint64_t* call_counter, int32_t reward_kind, int32_t tick_limit,
+                       void* stream) {
+  int rc = act_step_common(e, actor_flat, states, actions);
+  if (rc != SK_OK) return rc;
+  if (!rewards || !lengths || n_ticks <= 0) return fail(SK_EINVAL, "rewards / lengths NULL or n_ticks <= 0");
+  if (e->n % 4) return fail(SK_EINVAL, "sk_env_act_episode needs N % 4 == 0");
+  if (((uintptr_t)lengths) & 3) return fail(SK_EINVAL, "lengths must be 4-byte aligned");
+  StepArgs a;
+  rc = act_step_args(e, states, actions, states + (size_t)24 * e->n, rewards, reward_kind, nullptr, nullptr,
+                     tick_limit, 0, 0, nullptr, nullptr, 0, nullptr, nullptr, nullptr, a);
+  if (rc != SK_OK) return rc;
+  rc = sk_launch_act_episode32(actor_flat, actor_pack, noise_sd, action_sd, noise_seed, call_counter, a, e->dcfg,
+                               states, actions, rewards, lengths, n_ticks, (hipStream_t)stream);
+  if (rc != SK_OK) return fail(rc, "k_act_episode32 launch failed");
+  e->parity ^= 1;
+  return SK_OK;
+}
+
 static_assert(sizeof(ActStepJob) <= sizeof(sk_step_job), "sk_step_job too small for ActStepJob");
 
 int sk_env_act_step_job(sk_env* e, const float* actor_flat, const void* actor_pack, const float* acting_obs,

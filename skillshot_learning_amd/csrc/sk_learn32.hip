@@ -1669,6 +1669,86 @@ __global__ void __launch_bounds__(kFwdThreads) k_act_step32(const float* __restr
 }
 
 
+// The reference rule's episode collection (model_train, SkillshotLearner.py
+// :289-318) in ONE launch: every game plays its episode
+// from the current state, act (the actor held fixed for the epoch, fresh
+// exploration noise per tick: tick t draws with call number call0 + 1 + t,
+// as t sk_env_act_step calls would) -> do_actions -> game_tick -> get_state
+// while game_live and ticks < tick_limit (:304); a game that has ended is
+// stepped no further, as the reference's loop stops.  Workgroup b owns
+// games 16b .. 16b + 15 for the whole episode (act_step32's geometry: no
+// workgroup waits for another) and leaves once all of them have ended.
+// Tick t reads the acting states at states[t] ([2][N][12], player-major;
+// states[0] is the caller's observation of the start) and writes the
+// actions to actions[t] ([2][N][2]), the post-tick observation to
+// states[t + 1] and the reward to rewards[t] ([2][N]); lengths[i] = the
+// ticks game i played.  The rows t < lengths[i] of both players are the
+// episode's (s, a, r) for models_fit (:320-357).  The step counter and the
+// noise call number advance by n_ticks (the launch's last workgroup stores
+// the call number, grouped arrival).
+struct EpisodeArgs {
+  float* states;
+  float* actions;
+  float* rewards;
+  int32_t* lengths;
+  int n_ticks;
+};
+template <bool NOISE>
+__global__ void __launch_bounds__(kFwdThreads) k_act_episode32(const float* __restrict__ aflat,
+                                                               const char* __restrict__ apack, float sd,
+                                                               float action_sd, uint64_t seed,
+                                                               uint64_t* __restrict__ call_ctr, sk::StepArgs a,
+                                                               sk::Cfg c, EpisodeArgs ep) {
+  extern __shared__ __attribute__((aligned(16))) float smem_sl[];
+  char* smem = (char*)smem_sl;
+  float2* sAct = (float2*)(smem + kActorTileLds);
+  int* sAlive = (int*)(sAct + 32);
+  const int lane = threadIdx.x & 63;
+  const bool w0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0;
+  const int64_t g0 = (int64_t)blockIdx.x * 16;
+  // no episode counters: a lane whose game has ended skips split_finish's
+  // count, and the slot line is stored by lane 0 (the episode's outcome is
+  // the final state and `lengths`)
+  sk_counters* const slot = nullptr;
+  const Net A = net_of(aflat, kALd, 2);
+  const bool draws = (NOISE || action_sd != 0.f) && call_ctr;
+  const uint64_t call0 = draws ? call_ctr[0] : 0;
+  const uint64_t step0 = sk::step_read(a.step);
+  const int64_t n = a.n, gt = 2 * g0 + lane, gi = gt >> 1;  // wave 0: lane -> (game, player)
+  if (w0 && lane < 32 && (lane & 1) == 0 && gi < n) ep.lengths[gi] = 0;
+  for (int t = 0; t < ep.n_ticks; ++t) {
+    sk::StepArgs at = a;
+    at.acting_obs = ep.states + (int64_t)t * 24 * n;
+    at.obs = ep.states + (int64_t)(t + 1) * 24 * n;
+    at.reward = ep.rewards + (int64_t)t * 2 * n;
+    sk::StepLane L;
+    if (w0) {
+      L = sk::split_load(at, lane < 32 ? gt : 2 * n, slot);
+      // the reference's loop test (:304) on the pre-tick state; both lanes of a game agree
+      const bool alive = L.in && ((L.mi.y >> 16) & 0xff) && L.mi.x < a.tick_limit;
+      L.in = alive;  // an ended game is neither stepped nor written
+      if (alive && L.p == 0) ep.lengths[L.i] = t + 1;
+      const uint64_t any = __ballot(alive);
+      if (lane == 0) *sAlive = any != 0;
+    }
+    __syncthreads();
+    if (!*sAlive) break;  // workgroup-uniform: every game of the workgroup has ended
+    actor_tile32<NOISE>(A, apack, at.acting_obs, ep.actions + (int64_t)t * 4 * n, RowsPlayers{g0, n}, sd,
+                        action_sd, seed, call0 + 1 + (uint64_t)t, actor_lds(smem), sAct);
+    __syncthreads();
+    if (w0) {
+      const float2 act = lane < 32 ? sAct[(lane & 1) * 16 + (lane >> 1)] : make_float2(0.f, 0.f);
+      sk::split_finish(at, c, L, act, slot);
+    }
+    __syncthreads();  // this tick's observations are the next tick's acting rows (this workgroup's own stores)
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.step.slots[1 - a.step.parity] = step0 + (uint64_t)ep.n_ticks;
+  if (draws) {
+    __syncthreads();
+    advance_call32(call_ctr, call0 + (uint64_t)ep.n_ticks, gridDim.x);
+  }
+}
+
 // ---------------------------------------------------------------- actor forward, 16-row tiles
 // The same forward for small row counts: a 32-row tile is a serial chain of
 // load latencies around 3.4 us of MFMA per workgroup (9.4 us at 256 rows);
@@ -2042,6 +2122,28 @@ int sk_launch_act_step32(const float* aflat, const void* apack, float* act_out, 
   else
     k_act_step32<false><<<G, kFwdThreads, kActStepLds, st>>>(aflat, pk, act_out, 0.f, action_sd, seed, call_ctr, a,
                                                              c);
+  return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
+}
+
+// the reference rule's episode collection (sk_env_act_episode, csrc/sk_engine.hip): a.n % 4 == 0
+int sk_launch_act_episode32(const float* aflat, const void* apack, float sd, float action_sd, uint64_t seed,
+                            uint64_t* call_ctr, const sk::StepArgs& a, const sk::Cfg& c, float* states,
+                            float* actions, float* rewards, int32_t* lengths, int n_ticks, hipStream_t st) {
+  constexpr size_t lds = kActStepLds + 16;
+  static bool attr = false;
+  if (!attr) {
+    set_lds32(k_act_episode32<true>, lds);
+    set_lds32(k_act_episode32<false>, lds);
+    attr = true;
+  }
+  if (!apack || (((uintptr_t)apack) & 15)) return SK_EINVAL;
+  const unsigned G = (unsigned)((a.n + 15) / 16);
+  const EpisodeArgs ep{states, actions, rewards, lengths, n_ticks};
+  const char* pk = (const char*)apack;
+  if (sd != 0.f)
+    k_act_episode32<true><<<G, kFwdThreads, lds, st>>>(aflat, pk, sd, action_sd, seed, call_ctr, a, c, ep);
+  else
+    k_act_episode32<false><<<G, kFwdThreads, lds, st>>>(aflat, pk, 0.f, action_sd, seed, call_ctr, a, c, ep);
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
 }
 

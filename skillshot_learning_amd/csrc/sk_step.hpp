@@ -465,3 +465,7 @@ __device__ __forceinline__ void split_finish(const StepArgs& a, const Cfg& c, co
 // in one launch, 16 games per 256-lane workgroup (sk_env_act_step)
 int sk_launch_act_step32(const float* aflat, const void* apack, float* act_out, float sd, float action_sd,
                          uint64_t seed, uint64_t* call_ctr, const sk::StepArgs& a, const sk::Cfg& c, hipStream_t st);
+// k_act_episode32 (csrc/sk_learn32.hip): the reference rule's episode, one launch
+int sk_launch_act_episode32(const float* aflat, const void* apack, float sd, float action_sd, uint64_t seed,
+                            uint64_t* call_ctr, const sk::StepArgs& a, const sk::Cfg& c, float* states,
+                            float* actions, float* rewards, int32_t* lengths, int n_ticks, hipStream_t st);

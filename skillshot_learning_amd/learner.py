@@ -570,17 +570,66 @@ class DDPG:
         idx = torch.randperm(states.shape[0], device=states.device, generator=self.gen)
         states, actions, rewards = states[idx], actions[idx], rewards[idx]
         b = self.model_param_batch_size
+        n = states.shape[0]
         fu = self._fused
         if fu is not None:
             fu.soft_update_in_adam = False
+        # graph-replayed chunks of FIT_CHUNK minibatches (the fused kernels,
+        # one rank): the same launches on the same rows, staged into fixed
+        # buffers, without ~0.1 ms of host time per minibatch; the first
+        # minibatch of each pass runs eagerly (it warms the launch path the
+        # capture records) and the remainder after the last whole chunk too
+        graph = (fu is not None and states.is_cuda and not self.multi() and n >= 2 * b and
+                 os.environ.get("SK_FIT_GRAPH", "1") != "0")
+        M = self.FIT_CHUNK
+        chunks = (n // b - 1) // M if graph else 0
         try:
-            for k in range(0, states.shape[0], b):
+            for k in range(0, n, b):
+                if chunks and k == b:
+                    self._fit_chunks(states, actions, rewards, b, M, chunks, critic=True)
+                if chunks and b <= k < b + chunks * M * b:
+                    continue
                 self.critic_step(states[k:k + b], actions[k:k + b], rewards[k:k + b])
-            for k in range(0, states.shape[0], b):
+            for k in range(0, n, b):
+                if chunks and k == b:
+                    self._fit_chunks(states, actions, rewards, b, M, chunks, critic=False)
+                if chunks and b <= k < b + chunks * M * b:
+                    continue
                 self.model_actor_fit_step(states[k:k + b])
         finally:
             if fu is not None:
                 fu.soft_update_in_adam = True
+
+    FIT_CHUNK = 64  # minibatches per captured models_fit graph
+
+    def _fit_chunks(self, states, actions, rewards, b, M, chunks, critic):
+        """rows [b, b + chunks M b) of one models_fit pass as `chunks` replays
+        of a captured graph of M critic (or actor) steps on staging buffers"""
+        key = (b, M, bool(critic))
+        cache = self.__dict__.setdefault("_fit_graphs", {})
+        if key not in cache:
+            dev = states.device
+            S = torch.empty((M * b, STATE_DIM), dtype=torch.float32, device=dev)
+            A = torch.empty((M * b, ACTION_DIM), dtype=torch.float32, device=dev)
+            R = torch.empty(M * b, dtype=torch.float32, device=dev)
+            g = torch.cuda.CUDAGraph()
+            torch.cuda.current_stream(dev).synchronize()
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                for m in range(M):
+                    sl = slice(m * b, (m + 1) * b)
+                    if critic:
+                        self.critic_step(S[sl], A[sl], R[sl])
+                    else:
+                        self.model_actor_fit_step(S[sl])
+            cache[key] = (g, S, A, R)
+        g, S, A, R = cache[key]
+        for j in range(chunks):
+            lo = b + j * M * b
+            S.copy_(states[lo:lo + M * b])
+            if critic:
+                A.copy_(actions[lo:lo + M * b])
+                R.copy_(rewards[lo:lo + M * b])
+            g.replay()
 
     def sample_local(self, batch, device_sampling=False):
         """this rank's minibatch of the replay ring"""
@@ -835,9 +884,21 @@ class SkillshotLearner:
         g = self.game_environment
         full = reward == "full"
         call = dict(epoch_ticks=[], epoch_winner=[], epoch_board_sequences=[])
+        # the episodes on device in one launch (sk_env_act_episode) where the
+        # fp32 acting kernel runs them; the per-tick loop below otherwise
+        # (bf16 / torch actors, the full reward's per-tick features, boards)
+        on_device = (not full and not save_boards and self.actor_kernel is not None and
+                     getattr(self.actor_kernel, "fused_act_step", False) and self.n_envs % 4 == 0 and
+                     os.environ.get("SK_EPISODE_KERNEL", "1") != "0")
         for _ in range(epochs):
             g.reset(random_positions=self.use_random_start)
             obs = self.prepare_states()
+            if on_device:
+                ticks, winner = self._episode_on_device(obs, reward)
+                for d in (self.progress, call):
+                    d["epoch_ticks"].append(ticks.cpu())
+                    d["epoch_winner"].append(winner.cpu())
+                continue
             alive = torch.ones(self.n_envs, dtype=torch.bool, device=self.device)
             S, A, R, K, FT, W = [], [], [], [], [], []
             ticks = torch.zeros(self.n_envs, dtype=torch.int32, device=self.device)
@@ -886,6 +947,24 @@ class SkillshotLearner:
         if save_boards:
             self.save_training_boards(call["epoch_board_sequences"])
         return self.progress
+
+    def _episode_on_device(self, obs, reward):
+        """one model_train epoch with the episodes collected in one launch
+        (VecSkillshotGame.act_episode: every game until it ends, the actor
+        fixed, fresh noise per tick), then models_fit on the played rows in
+        the per-tick loop's order (tick, player, game).  Returns the games'
+        final ticks and winners."""
+        g = self.game_environment
+        mode = self.exploration
+        ep = g.act_episode(self.actor_kernel, obs, noise_sd=self.param_noise_sd if mode == "param_noise" else 0.0,
+                           action_sd=self.action_noise_sd if mode == "action_noise" else 0.0, reward=reward,
+                           out=getattr(self, "_episode_bufs", None))
+        self._episode_bufs = ep
+        lengths = ep["lengths"].long()
+        T = int(lengths.max()) if self.n_envs else 0
+        keep = (torch.arange(T, device=self.device)[:, None] < lengths[None, :])[:, None, :].expand(T, 2, self.n_envs)
+        self.models_fit(ep["states"][:T][keep], ep["actions"][:T][keep], ep["rewards"][:T][keep])
+        return g.ticks.clone(), g.winner_id.clone()
 
     # ------------------------------------------------------------ on-disk formats (persist.py)
     def save_actor_critic_models(self, epochs):

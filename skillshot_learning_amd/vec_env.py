@@ -345,6 +345,38 @@ class VecSkillshotGame:
             ring.total += 2 * self.n  # host mirror
         return dict(obs=obs_t, reward=rew_t, done=done, winner=win, obs_reset=obs_r, actions=act)
 
+    def act_episode(self, actor, start_obs, n_ticks=None, noise_sd=0.0, action_sd=0.0, reward="looking",
+                    out=None):
+        """The reference rule's episode collection in ONE launch
+        (sk_env_act_episode; SkillshotLearner.model_train :289-318 for every
+        game): from the current state every game plays until it ends (hit or
+        tick limit), acting with `actor` (ActorKernel32) with fresh noise per
+        tick.  start_obs [2, N, 12]: the observation of the current state.
+        Returns dict(states [T+1, 2, N, 12], actions [T, 2, N, 2], rewards
+        [T, 2, N], lengths int32 [N]); rows t < lengths[i] are game i's
+        episode.  T = n_ticks (default: the tick limit)."""
+        T = int(self.tick_limit if n_ticks is None else n_ticks)
+        o = out or {}
+        st = o.get("states")
+        if st is None or st.shape[0] < T + 1:
+            st = torch.empty((T + 1, 2, self.n, 12), dtype=torch.float32, device=self.device)
+        ac = o.get("actions")
+        if ac is None or ac.shape[0] < T:
+            ac = torch.empty((T, 2, self.n, 2), dtype=torch.float32, device=self.device)
+        rw = o.get("rewards")
+        if rw is None or rw.shape[0] < T:
+            rw = torch.empty((T, 2, self.n), dtype=torch.float32, device=self.device)
+        ln = o.get("lengths")
+        if ln is None:
+            ln = torch.empty(self.n, dtype=torch.int32, device=self.device)
+        st[0].copy_(start_obs.reshape(2, self.n, 12))
+        actor.calls += T
+        pack = actor.ensure_pack()
+        check(self._L.sk_env_act_episode(self._h, _ptr(actor.flat), _ptr(pack), _ptr(st), _ptr(ac), _ptr(rw),
+                                         _ptr(ln), T, float(noise_sd), float(action_sd), actor.seed,
+                                         _ptr(actor._ctr), REWARD_KINDS[reward], self.tick_limit, self._stream()))
+        return dict(states=st[:T + 1], actions=ac[:T], rewards=rw[:T], lengths=ln)
+
     def step_raw(self, actions_ptr, done_ptr=None, obs_ptr=None, reward_ptr=None, winner_ptr=None,
                  auto_reset=True, stream=None):
         """Pointer-level fused step (bench / graph capture; no allocation)."""

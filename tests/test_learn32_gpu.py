@@ -283,3 +283,100 @@ def test_split_pack_follows_updates(mods):
     out = k(s)
     want, _ = kr.actor_forward(kr.from_module(L.model_actor), _np(s))
     assert np.abs(_np(out) - want).max() <= 1e-5
+
+
+@pytest.mark.parametrize("exploration", ["param_noise", "action_noise"])
+def test_act_episode_equals_per_tick_loop(mods, monkeypatch, exploration):
+    """sk_env_act_episode (the reference rule's episodes in one launch) against
+    the per-tick loop (the 32-row actor forward, then sk_env_step without
+    auto-reset, one launch each per tick): every played row's state, action
+    and reward bit for bit, each game's length, and the final ticks / winner
+    of every game at its end; the noise call number advances by n_ticks"""
+    learner, _ = mods
+    monkeypatch.setenv("SK_FWD16", "0")
+    n, limit = 1024, 150
+    L = learner.SkillshotLearner(n_envs=n, device="cuda", seed=5, exploration=exploration, tick_limit=limit,
+                                 precision="fp32")
+    g, k = L.game_environment, L.actor_kernel
+    g.reset(random_positions=True)
+    st0 = g.state_dict()
+    obs = L.prepare_states().clone()
+    c0 = int(k._ctr[0])
+    sd = L.param_noise_sd if exploration == "param_noise" else 0.0
+    asd = L.action_noise_sd if exploration == "action_noise" else 0.0
+    ep = g.act_episode(k, obs, noise_sd=sd, action_sd=asd)
+    torch.cuda.synchronize()
+    assert int(k._ctr[0]) == c0 + limit
+    got_len = ep["lengths"].long()
+    end_ticks, end_winner = g.ticks.clone(), g.winner_id.clone()
+    # the per-tick loop from the same start and call number
+    g.load_state_dict(st0)
+    k._ctr[0] = c0
+    alive = torch.ones(n, dtype=torch.bool, device="cuda")
+    length = torch.zeros(n, dtype=torch.long, device="cuda")
+    want_ticks = torch.zeros(n, dtype=torch.int32, device="cuda")
+    want_winner = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    s = obs
+    for t in range(limit):
+        a = k(s.reshape(-1, 12), noise_sd=sd, action_sd=asd).reshape(2, n, 2)
+        out = g.step(a, obs=True, reward="looking", auto_reset=False)
+        m = alive
+        assert torch.equal(ep["states"][t][:, m], s[:, m]), t
+        assert torch.equal(ep["actions"][t][:, m], a[:, m]), t
+        assert torch.equal(ep["rewards"][t][:, m], out["reward"][:, m]), t
+        assert torch.equal(ep["states"][t + 1][:, m], out["obs"][:, m]), t
+        length += alive.long()
+        newly = alive & out["done"].bool()
+        want_ticks = torch.where(newly, g.ticks, want_ticks)
+        want_winner = torch.where(newly, out["winner"], want_winner)
+        alive = alive & ~out["done"].bool()
+        s = out["obs"]
+        if not bool(alive.any()):
+            break
+    assert torch.equal(got_len, length)
+    assert torch.equal(end_ticks, want_ticks) and torch.equal(end_winner, want_winner)
+    assert int(got_len.max()) > 1 and int((got_len < limit).sum()) > 0  # both endings occur
+
+
+def test_model_train_on_device_equals_loop(mods, monkeypatch):
+    """model_train with the episodes in one launch (default) and with the
+    per-tick loop (SK_EPISODE_KERNEL=0): the same nets after two epochs, bit
+    for bit (same rows in the same order, the same shuffle)"""
+    learner, _ = mods
+    monkeypatch.setenv("SK_FWD16", "0")
+    nets = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SK_EPISODE_KERNEL", flag)
+        L = learner.SkillshotLearner(n_envs=256, device="cuda", seed=9, tick_limit=60, precision="fp32")
+        prog = L.model_train(2)
+        torch.cuda.synchronize()
+        nets.append((torch.cat([p.detach().flatten() for p in L.model_actor.parameters()]),
+                     torch.cat([p.detach().flatten() for p in L.model_critic.parameters()]),
+                     torch.stack(prog["epoch_ticks"]), torch.stack(prog["epoch_winner"])))
+    for x, y in zip(*nets):
+        assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_models_fit_graph_chunks_equal_eager(mods, monkeypatch, precision):
+    """models_fit with its minibatches replayed as captured chunks (default)
+    against one eager launch set per minibatch (SK_FIT_GRAPH=0): the same
+    nets and Adam moments bit for bit (3,000 rows: the first minibatch
+    eager, two chunks of 64, the remainder and the partial last batch eager)"""
+    learner, _ = mods
+    g = torch.Generator(device="cuda").manual_seed(3)
+    rows = 3000
+    s = torch.rand(rows, 12, device="cuda", generator=g)
+    a = torch.rand(rows, 2, device="cuda", generator=g) * 2 - 1
+    r = torch.randn(rows, device="cuda", generator=g)
+    out = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SK_FIT_GRAPH", flag)
+        d = learner.DDPG("cuda", seed=4, fused_update=True, precision=precision)
+        d.models_fit(s, a, r)
+        d.models_fit(s[:700], a[:700], r[:700])  # a second call reuses the captured graphs
+        torch.cuda.synchronize()
+        out.append([p.detach().clone() for m in (d.model_actor, d.model_critic) for p in m.parameters()] +
+                   [d._fused.sa.m.clone(), d._fused.sc.v.clone()])
+    for x, y in zip(*out):
+        assert torch.equal(x, y)
