@@ -78,6 +78,8 @@ def parse():
     p.add_argument("--leg-budget", type=float, default=480.0,
                    help="wall seconds for all legs beside the headline: a leg that would start past it is skipped "
                         "(reported in errors), so the headline line always prints")
+    p.add_argument("--no-reference-rule", action="store_true",
+                   help="skip the reference-rule (model_train) epoch leg at the metric's games")
     p.add_argument("--no-overlapped", action="store_true",
                    help="skip the opt-in overlapped learner tick reported beside each leg's reference-order tick")
     p.add_argument("--learner-child", default=None, help=argparse.SUPPRESS)
@@ -554,6 +556,76 @@ def learner_rate(envs, world, rank, ticks, batch=256, exploration="param_noise",
     return out
 
 
+def reference_rule_rate(envs, exploration="param_noise", precision="fp32", fit_chunks=20):
+    """The reference's own training rule at the metric's size (VERDICT r03
+    item 5; SkillshotLearner.model_train :289-361): one epoch = every game
+    plays its episode from a random start (the actor fixed, fresh noise per
+    tick) — one sk_env_act_episode launch — then models_fit on all played
+    rows: shuffle, critic one pass at batch 16, actor one pass at batch 16.
+    The collection is timed whole (HIP events and wall); the fit's 10^7-odd
+    sequential minibatch steps are timed over `fit_chunks` captured chunks of
+    64 per pass and the epoch's fit time projected from that rate."""
+    from skillshot_learning_amd.learner import SkillshotLearner
+    L = SkillshotLearner(n_envs=envs, seed=0, exploration=exploration, tick_limit=2000, precision=precision)
+    g = L.game_environment
+    mode = L.exploration
+    kw = dict(noise_sd=L.param_noise_sd if mode == "param_noise" else 0.0,
+              action_sd=L.action_noise_sd if mode == "action_noise" else 0.0)
+    st = torch.cuda.current_stream()
+    g.reset(random_positions=True)  # warm-up episode (allocations, code objects)
+    L._episode_bufs = g.act_episode(L.actor_kernel, L.prepare_states(), **kw)
+    g.reset(random_positions=True)
+    obs = L.prepare_states()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(st)
+    ep = g.act_episode(L.actor_kernel, obs, out=L._episode_bufs, **kw)
+    e1.record(st)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ev = e0.elapsed_time(e1) * 1e-3
+    lengths = ep["lengths"].long()
+    played = int(lengths.sum())
+    T = int(lengths.max())
+    keep = (torch.arange(T, device=L.device)[:, None] < lengths[None, :])[:, None, :].expand(T, 2, envs)
+    S, A, R = ep["states"][:T][keep], ep["actions"][:T][keep], ep["rewards"][:T][keep]
+    rows = S.shape[0]
+    # the fit's rate: fit_chunks captured chunks of 64 minibatches per pass
+    d = L.ddpg
+    b, M = d.model_param_batch_size, d.FIT_CHUNK
+    d._fused.soft_update_in_adam = False
+    try:
+        d.critic_step(S[:b], A[:b], R[:b])
+        d.model_actor_fit_step(S[:b])
+        d._fit_chunks(S, A, R, b, M, 1, critic=True)
+        d._fit_chunks(S, A, R, b, M, 1, critic=False)
+        torch.cuda.synchronize()
+        f0 = time.perf_counter()
+        d._fit_chunks(S, A, R, b, M, fit_chunks, critic=True)
+        d._fit_chunks(S, A, R, b, M, fit_chunks, critic=False)
+        torch.cuda.synchronize()
+        fit_s = time.perf_counter() - f0
+    finally:
+        d._fused.soft_update_in_adam = True
+    steps = 2 * fit_chunks * M
+    step_us = fit_s * 1e6 / steps
+    fit_epoch_s = 2 * ((rows + b - 1) // b) * step_us * 1e-6
+    out = dict(envs=envs, exploration=exploration, dtype=precision, episode_ticks_max=T, env_steps_played=played,
+               mean_episode=played / envs, rows=rows,
+               collection=dict(kernel="k_act_episode32 (sk_env_act_episode: the whole episode in one launch)",
+                               gpu_s=ev, wall_s=wall, env_steps_per_s=played / wall,
+                               gpu_us_per_tick=ev * 1e6 / T),
+               fit=dict(batch=b, minibatch_steps_timed=steps, us_per_minibatch_step=step_us,
+                        steps_per_epoch=2 * ((rows + b - 1) // b), projected_epoch_fit_s=fit_epoch_s,
+                        note="sequential SGD at batch 16 as the reference's models_fit: the epoch's fit is "
+                             "projected from the timed chunks (captured graphs of 64 fused minibatch steps)"),
+               projected_epoch_s=wall + fit_epoch_s)
+    del L, ep, S, A, R
+    torch.cuda.empty_cache()
+    return out
+
+
 ACTOR_FLOP_ROW = 72192   # SURVEY §8(a) A13: 2 x (12*256 + 256*128 + 128*2) multiply-adds per row
 CRITIC_FLOP_ROW = 72448  # A16: 2 x (12*256 + 258*128 + 128*1)
 MFMA_PEAK_TF = {"fp32": 157.3, "bf16": 2500.0}  # MI355X_MICROARCH.md: f32 MFMA 157.3 TF; bf16 ~2.5 PF dense
@@ -770,6 +842,9 @@ def leg_child_main(args, spec):
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     name, n = spec["leg"], spec["n"]
+    if name == "reference_rule":
+        print(json.dumps(reference_rule_rate(spec["envs"], precision=spec.get("precision", "fp32"))), flush=True)
+        return
     if name == "learner":
         for ov in spec.get("overlaps", [None]):
             r = learner_rate(spec["envs"], 1, 0, args.learner_ticks, batch=spec["batch"],
@@ -987,6 +1062,9 @@ def main():
             for name, cfg in legs:
                 spec = dict(cfg, leg="learner", n=n, batch=256, overlaps=overlaps)
                 learner[name] = forms(leg(f"learner.{name}", spec, args.learner_timeout))
+            if not args.no_reference_rule:
+                r = leg("learner.reference_rule", dict(leg="reference_rule", n=n, envs=total), args.learner_timeout)
+                learner["reference_rule"] = r[0] if r else None
         else:
             # every leg at the reference's fp32 (Keras) precision; config 5 at
             # bf16 beside it
