@@ -76,8 +76,10 @@ class ActorKernel32:
     fp32 products at the bf16 MFMA rate).  The pack follows the parameters:
     the fused update's Adam launch rewrites it (DDPG._fused.split_pack), and
     a change made through torch (optimizer steps, load_state_dict, copy_)
-    bumps the flat buffer's version counter, on which every call repacks
-    (ensure_pack).  Same call interface as ActorKernel."""
+    bumps the parameters' version counters, on which every call repacks
+    (ensure_pack; the parameters are views of the flat buffer through
+    `.data`, so each keeps its own counter).  Same call interface as
+    ActorKernel."""
 
     buf = None  # no bf16 forward pack
 
@@ -95,7 +97,7 @@ class ActorKernel32:
         self._ctr = torch.zeros(130, dtype=torch.int64, device=self.device)  # SK_ACTOR_COUNTER_WORDS
         self.counter = self._ctr[:1]
         self.pack = torch.zeros(int(self.L.sk_actor_split_pack_bytes()), dtype=torch.uint8, device=self.device)
-        self._packed = None  # (flat buffer, its version) the pack was last written from
+        self._packed = None  # (flat buffer, the parameters' versions) the pack was last written from
         self.ensure_pack()
 
     def refresh(self):
@@ -106,14 +108,17 @@ class ActorKernel32:
                                             ctypes.c_void_p(self.pack.data_ptr()), self._stream())
         if rc != 0:
             raise SkillshotError(f"sk_actor_split_pack_f32 failed ({rc})")
-        self._packed = (self.flat.data_ptr(), self.flat._version)
+        self._packed = self._key()
 
     def ensure_pack(self):
         """the split pack, repacked first if the parameters were changed
         through torch since it was written (returns it)"""
-        if self._packed != (self.flat.data_ptr(), self.flat._version):
+        if self._packed != self._key():
             self.refresh()
         return self.pack
+
+    def _key(self):
+        return (self.flat.data_ptr(),) + tuple(p._version for p in self.actor.parameters())
 
     fused_action_noise = True  # model_act_action_noise's N(0, sd) is drawn in the kernel
     fused_act_step = True  # the self-play tick runs it inside the step launch (VecSkillshotGame.act_step)

@@ -1412,6 +1412,40 @@ __device__ __forceinline__ void normals4(uint64_t seed, uint64_t call, uint32_t 
 #ifndef SK_F32_NOISE_ROUNDS
 #define SK_F32_NOISE_ROUNDS 7
 #endif
+// noisy4 in two parts, bit for bit the same: the draws (Philox words ->
+// the pairs' L and cos / sin; independent of the GEMM, so they can be issued
+// ahead of it and run under its MFMAs) and the combination with m and v
+#ifndef SK_NOISE_HOIST  // A/B builds: 0 draws layer 2's noise after its GEMM
+#define SK_NOISE_HOIST 1
+#endif
+struct Draw4 {
+  float L[2], c[2], s[2];
+};
+__device__ __forceinline__ Draw4 draw4n(uint64_t seed, uint64_t call, uint32_t r, uint32_t layer_unit, float k2) {
+  const uint4 u = skmlp::philox<SK_F32_NOISE_ROUNDS>(
+      make_uint4(r, layer_unit, (uint32_t)call, (uint32_t)(call >> 32)), (uint32_t)seed, (uint32_t)(seed >> 32));
+  const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
+  Draw4 d;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const float u1 = ((float)(wd[2 * q] >> 8) + 0.5f) * 0x1p-24f;  // (0, 1)
+    const float u2 = (float)(wd[2 * q + 1] >> 8) * 0x1p-24f;       // [0, 1) revolutions
+    d.L[q] = k2 * __builtin_amdgcn_logf(u1);                        // -2 ln(u1) sd^2
+    d.c[q] = __builtin_amdgcn_cosf(u2);
+    d.s[q] = __builtin_amdgcn_sinf(u2);
+  }
+  return d;
+}
+template <typename V>
+__device__ __forceinline__ void noisy4_apply(const Draw4& d, float b, const V& m, const V& v, int o, float y[4]) {
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    y[2 * q] = __builtin_fmaf(__builtin_amdgcn_sqrtf(__builtin_fmaf(b, b, v[o + 2 * q]) * d.L[q]), d.c[q],
+                              m[o + 2 * q] + b);
+    y[2 * q + 1] = __builtin_fmaf(__builtin_amdgcn_sqrtf(__builtin_fmaf(b, b, v[o + 2 * q + 1]) * d.L[q]), d.s[q],
+                                  m[o + 2 * q + 1] + b);
+  }
+}
 template <typename V>
 __device__ __forceinline__ void noisy4(uint64_t seed, uint64_t call, uint32_t r, uint32_t layer_unit, float k2,
                                        float b, const V& m, const V& v, int o, float y[4]) {
@@ -1525,16 +1559,24 @@ __device__ __forceinline__ void actor_tile32(const Net& A, const char* __restric
   TP32(3);
   {
     const int u = 32 * w + (lane & 31);
+    // layer 2's noise draws first: they do not depend on the GEMM, so their
+    // VALU work (Philox, log, sin / cos) issues among its MFMAs
+    Draw4 dr[4];
+    const float k2 = skmlp::noise_k2(sd);
+    if (NOISE && SK_NOISE_HOIST) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) dr[g] = draw4n(seed, call, (uint32_t)R(drow(4 * g, lane)), (uint32_t)(kH1 + u), k2);
+    }
     f32x16 m = {0}, var = {0};
     gemm6<16, NOISE>(m, var, T.H1, kLdX2, kX2Plane, W2 + 16 * 64 * w, sksplit::kW2Plane, lane);
     const float b = A.b2[u];
     __syncthreads();  // every wave has read the layer-1 planes: layer 2's outputs go over them
     if (NOISE) {
-      const float k2 = skmlp::noise_k2(sd);
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         float y[4];
-        noisy4(seed, call, (uint32_t)R(drow(4 * g, lane)), (uint32_t)(kH1 + u), k2, b, m, var, 4 * g, y);
+        if (!SK_NOISE_HOIST) dr[g] = draw4n(seed, call, (uint32_t)R(drow(4 * g, lane)), (uint32_t)(kH1 + u), k2);
+        noisy4_apply(dr[g], b, m, var, 4 * g, y);
 #pragma unroll
         for (int q = 0; q < 4; ++q) T.H2[drow(4 * g + q, lane) * kLdH2 + u] = fmaxf(y[q], 0.f);
       }
