@@ -1128,6 +1128,10 @@ def main():
                 "traffic_source": "profiles/traffic_k_step_multi.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
                                   "passes, per tick; not this run)",
                 "kernel": "k_step_multi<1> (write-through state port)",
+                "note": "bound labelled hbm as SURVEY 8(d) prescribes (193 B per env-step against 8 TB/s); at "
+                        "65,536 games the 5.8 MB of state crosses the L2 / fabric boundary every tick "
+                        "(write-through) but is served by the 256 MiB Infinity Cache, and only the per-tick "
+                        "1 MiB action slab streams from HBM: the HBM-bound regime is large_batch (369 MB state)",
                 "bytes_per_env_step": BYTES_PER_ENV_STEP,
                 "kernel_us_per_tick": kern_ms * 1e3,
             },
