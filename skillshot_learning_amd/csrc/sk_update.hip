@@ -1007,7 +1007,11 @@ __device__ __forceinline__ void scatter_fwd_pack(char* out, int p, float v) {  /
 #ifndef SK_ADAM_PARAMS
 #define SK_ADAM_PARAMS 64
 #endif
-constexpr int kAdamParams = SK_ADAM_PARAMS, kAdamSlices = SK_ADAM_SLICES;
+#ifndef SK_ADAM_INFLIGHT
+#define SK_ADAM_INFLIGHT 8
+#endif
+constexpr int kAdamParams = SK_ADAM_PARAMS, kAdamSlices = SK_ADAM_SLICES, kAdamInflight = SK_ADAM_INFLIGHT;
+static_assert(kAdamInflight >= 2 && (kAdamInflight & (kAdamInflight - 1)) == 0, "a power of two");
 static_assert(skpart::kPW2 % kAdamParams == 0, "the W1 rows stay workgroup-uniform");
 
 __global__ void __launch_bounds__(kAdamParams * kAdamSlices) k_adam_flat(const float* __restrict__ partial, int G, int P, const float* __restrict__ grad_in,
@@ -1050,16 +1054,25 @@ __global__ void __launch_bounds__(kAdamParams * kAdamSlices) k_adam_flat(const f
       if (target) tw0 = target[p];
     }
   }
-  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // 8 independent loads in flight
+  // kAdamInflight independent loads in flight per lane: the sliced fp32
+  // kernels' W1 / b1 gradient is 128 contribution rows at batch 256 (32 per
+  // slice), so 8 in flight made those workgroups wait four load latencies
+  float acc[kAdamInflight];
+#pragma unroll
+  for (int j = 0; j < kAdamInflight; ++j) acc[j] = 0.f;
   if (in) {
     int k = slice;
-    for (; k + 7 * kAdamSlices < GG; k += 8 * kAdamSlices) {
+    for (; k + (kAdamInflight - 1) * kAdamSlices < GG; k += kAdamInflight * kAdamSlices) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += src[(int64_t)(k + j * kAdamSlices) * ld + pp];
+      for (int j = 0; j < kAdamInflight; ++j) acc[j] += src[(int64_t)(k + j * kAdamSlices) * ld + pp];
     }
     for (; k < GG; k += kAdamSlices) acc[0] += src[(int64_t)k * ld + pp];
   }
-  const float part = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+#pragma unroll
+  for (int w = kAdamInflight / 2; w >= 1; w /= 2)
+#pragma unroll
+    for (int j = 0; j < w; ++j) acc[j] += acc[j + w];
+  const float part = acc[0];
   if (slice > 0) red[slice - 1][lane] = part;
   __syncthreads();
   if (slice > 0 || !in) return;
