@@ -257,7 +257,7 @@ int sk_env_act_step(sk_env* env, const float* actor_flat, const void* actor_pack
  * (sk_env_observe); tick t reads states[t] and writes actions[t]
  * (float[n_ticks][2][N][2]), states[t + 1] (the post-tick observation) and
  * rewards[t] (float[n_ticks][2][N]; reward_kind as sk_env_step's); rows of
- * ticks a game did not play are left unwritten.  lengths int32[N] = the
+ * ticks a game did not play are undefined.  lengths int32[N] = the
  * ticks each game played.  N % 4 == 0; the step counter and the noise call
  * number advance by n_ticks; no episode counters.  GPU backend only. */
 int sk_env_act_episode(sk_env* env, const float* actor_flat, const void* actor_pack, float* states, float* actions,

@@ -1725,7 +1725,7 @@ __global__ void __launch_bounds__(kFwdThreads) k_act_step32(const float* __restr
 // actions to actions[t] ([2][N][2]), the post-tick observation to
 // states[t + 1] and the reward to rewards[t] ([2][N]); lengths[i] = the
 // ticks game i played.  The rows t < lengths[i] of both players are the
-// episode's (s, a, r) for models_fit (:320-357).  The step counter and the
+// episode's (s, a, r) for models_fit (:320-357); later rows are undefined.  The step counter and the
 // noise call number advance by n_ticks (the launch's last workgroup stores
 // the call number, grouped arrival).
 struct EpisodeArgs {
@@ -1764,8 +1764,12 @@ __global__ void __launch_bounds__(kFwdThreads) k_act_episode32(const float* __re
     at.obs = ep.states + (int64_t)(t + 1) * 24 * n;
     at.reward = ep.rewards + (int64_t)t * 2 * n;
     sk::StepLane L;
+    // the state loads fly under the actor tile (act_step32's order); the
+    // loop test waits for them only after it
+    if (w0) L = sk::split_load(at, lane < 32 ? gt : 2 * n, slot);
+    actor_tile32<NOISE>(A, apack, at.acting_obs, ep.actions + (int64_t)t * 4 * n, RowsPlayers{g0, n}, sd,
+                        action_sd, seed, call0 + 1 + (uint64_t)t, actor_lds(smem), sAct);
     if (w0) {
-      L = sk::split_load(at, lane < 32 ? gt : 2 * n, slot);
       // the reference's loop test (:304) on the pre-tick state; both lanes of a game agree
       const bool alive = L.in && ((L.mi.y >> 16) & 0xff) && L.mi.x < a.tick_limit;
       L.in = alive;  // an ended game is neither stepped nor written
@@ -1775,9 +1779,6 @@ __global__ void __launch_bounds__(kFwdThreads) k_act_episode32(const float* __re
     }
     __syncthreads();
     if (!*sAlive) break;  // workgroup-uniform: every game of the workgroup has ended
-    actor_tile32<NOISE>(A, apack, at.acting_obs, ep.actions + (int64_t)t * 4 * n, RowsPlayers{g0, n}, sd,
-                        action_sd, seed, call0 + 1 + (uint64_t)t, actor_lds(smem), sAct);
-    __syncthreads();
     if (w0) {
       const float2 act = lane < 32 ? sAct[(lane & 1) * 16 + (lane >> 1)] : make_float2(0.f, 0.f);
       sk::split_finish(at, c, L, act, slot);
