@@ -305,9 +305,12 @@ def timed_ticks(dev, n, seed, env_offset, tick_limit, k, warmup, ring, chunk, wo
     with torch.cuda.stream(st):
         e1.record()
     torch.cuda.synchronize()
+    # this rank's time from the common start to its own finish; the job's is
+    # the max over ranks (below).  The closing barrier only aligns the ranks
+    # and is not part of the K steps
+    el = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    el = time.perf_counter() - t0
     if world > 1:
         tt = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -367,9 +370,12 @@ def timed_multi(dev, n, seed, env_offset, tick_limit, k, warmup, ring, world, pe
     run(k)
     e1.record(st)
     torch.cuda.synchronize()
+    # this rank's time from the common start to its own finish; the job's is
+    # the max over ranks (below).  The closing barrier only aligns the ranks
+    # and is not part of the K steps
+    el = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    el = time.perf_counter() - t0
     if world > 1:
         tt = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -526,9 +532,12 @@ def learner_rate(envs, world, rank, ticks, batch=256, exploration="param_noise",
     tg.run(max(1, ticks // tg.ticks))
     e1.record(tg.stream)
     torch.cuda.synchronize()
+    # this rank's time from the common start to its own finish; the job's is
+    # the max over ranks (below).  The closing barrier only aligns the ranks
+    # and is not part of the K steps
+    el = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    el = time.perf_counter() - t0
     if world > 1:
         tt = torch.tensor([el], dtype=torch.float64, device=L.device)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
