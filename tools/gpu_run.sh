@@ -9,6 +9,7 @@
 #   tests      pytest -m gpu (TESTS= to narrow, e.g. TESTS="tests/test_multi_gpu.py")
 #   smoke      __graft_entry__.smoke()
 #   traffic    PMC FETCH/WRITE passes of the headline kernel -> profiles/traffic_k_step_multi*.json
+#   trafficobs the same for the full-contract multi-tick kernel -> traffic_k_step_split_multi_obs.json
 #   prof       rocprofv3 --kernel-trace --stats of the headline leg, K = 4,000 and the driver's K = 20
 #   proflearn  rocprofv3 kernel stats of the learner ticks (config 3 / 5, fp32 / bf16)
 #   bench      python bench.py (every leg)                        -> $O/bench_default.json
@@ -59,6 +60,9 @@ for s in "${S[@]}"; do
     bash tools/gpu_traffic_multi.sh $TAG > $O/traffic.log 2>&1 || stop traffic $?
     cp gpurun_out/traffic_k_step_multi_pol1_$TAG.json $O/traffic_k_step_multi.json
     cp gpurun_out/traffic_k_step_multi_pol0_$TAG.json $O/traffic_k_step_multi_pol0.json;;
+  trafficobs)
+    bash tools/gpu_traffic_multi_obs.sh $TAG > $O/traffic_obs.log 2>&1 || stop trafficobs $?
+    cp gpurun_out/traffic_k_step_split_multi_obs_$TAG.json $O/traffic_k_step_split_multi_obs.json;;
   prof)
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o prof -- python3 bench.py \
       --no-learner --no-cpu-baseline --no-large --no-full --no-rollout --no-variants > $O/prof_bench.json \

@@ -22,6 +22,9 @@ def main():
     p.add_argument("--ring", type=int, default=300)
     p.add_argument("--obs", action="store_true")
     p.add_argument("--multi", type=int, default=0, help="k_step_multi launches of this many ticks instead")
+    p.add_argument("--multi-obs", type=int, default=0,
+                   help="sk_env_step_multi_obs launches (full contract) of this many ticks instead")
+    p.add_argument("--out-slabs", type=int, default=64, help="--multi-obs: output ring slabs")
     a = p.parse_args()
     from skillshot_learning_amd import VecSkillshotGame
     n = a.envs
@@ -32,6 +35,19 @@ def main():
     o = torch.empty((2, n, 12), dtype=torch.float32, device="cuda") if a.obs else None
     r = torch.empty((2, n), dtype=torch.float32, device="cuda") if a.obs else None
     torch.cuda.synchronize()
+    if a.multi_obs:
+        S = a.out_slabs
+        out = dict(obs=torch.empty((S, 2, n, 12), dtype=torch.float32, device="cuda"),
+                   reward=torch.empty((S, 2, n), dtype=torch.float32, device="cuda"),
+                   done=torch.empty((S, n), dtype=torch.uint8, device="cuda"), winner=None)
+        slab, so = 0, 0
+        for _ in range(a.launches):
+            env.step_multi_obs(acts, n_ticks=a.multi_obs, slab0=slab, out_slabs=S, out0=so, out=out)
+            slab = (slab + a.multi_obs) % a.ring
+            so = (so + a.multi_obs) % S
+        torch.cuda.synchronize()
+        print("multi_obs launches", a.launches, "x", a.multi_obs, "ticks, envs", n)
+        return
     if a.multi:
         slab = 0
         for _ in range(a.launches):
