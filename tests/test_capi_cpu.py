@@ -133,3 +133,18 @@ def test_sampled_critic_rejects_exclude_outside_ring(exclude):
     assert rc == _capi.SK_EINVAL
     assert L.sk_replay_sample_excl(fake, 64, fake, 0, 0, 16, fake, fake, fake, fake, fake, exclude,
                                    None) == _capi.SK_EINVAL
+
+
+def test_gpu_only_entry_points_refuse_the_cpu_backend():
+    """sk_env_act_step / sk_env_act_episode are GPU-only (the fused actor):
+    on a CPU-backend handle they return SK_EINVAL, never run a host
+    substitute; sk_actor_split_pack_bytes reports the split pack's size"""
+    L = ssa.load_library()
+    h = ctypes.c_void_p()
+    assert L.sk_env_create(ctypes.byref(h), 8, 0, 7, -1, None) == _capi.SK_OK
+    buf = (ctypes.c_float * 4096)()
+    ln = (ctypes.c_int32 * 8)()
+    rc = L.sk_env_act_episode(h, buf, buf, buf, buf, buf, ln, 10, 0.5, 0.0, 1, None, 0, 2000, None)
+    assert rc == _capi.SK_EINVAL and b"GPU" in L.sk_last_error()
+    assert L.sk_env_destroy(h) == _capi.SK_OK
+    assert L.sk_actor_split_pack_bytes() == 4 * (8 * 64 * 8 + 4 * 16 * 64 * 8) * 2
