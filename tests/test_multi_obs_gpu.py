@@ -5,7 +5,8 @@ tick's obs, reward, done and winner, the final state, the RNG step counter
 and the episode counters — for both state ports, both rewards, ragged
 batches, the 512-lane geometry, output rings shorter than the launch, and
 against the CPU backend (state bit-exact, obs within 1e-5: the CPU backend
-computes obs with libm's tan, the kernels from the tick's sin/cos)."""
+computes obs with libm's tan, the kernels from the tick's sin/cos), and
+launches of 1-3 ticks back to back."""
 import numpy as np
 import pytest
 import torch
@@ -61,6 +62,26 @@ def test_step_multi_obs_equals_stepwise(ssa, monkeypatch, reward, pol, n, T, S):
     assert a.step_counter == b.step_counter
     ca, cb = a.counters(), b.counters()
     assert ca == cb and ca["dones"] > n  # limit 50 over >= 60 ticks: every game restarts
+
+
+@pytest.mark.parametrize("T", [1, 2, 3])
+def test_step_multi_obs_short_launches(ssa, monkeypatch, T):
+    """launches of 1-3 ticks, back to back, into one output ring"""
+    n, R, S = 5000, 7, 5
+    a, b = _pair(ssa, n, 23, 4, monkeypatch, 1)
+    acts = a.gen_random_actions(R)
+    slab, so, want, out = 0, 0, {}, None
+    for _ in range(4):
+        out = a.step_multi_obs(acts, n_ticks=T, slab0=slab, out_slabs=S, out0=so, out=out)
+        for t in range(T):
+            o = b.step(acts[(slab + t) % R], obs=True, auto_reset=True)
+            want[(so + t) % S] = {k: o[k].clone() for k in ("obs", "reward", "done", "winner")}
+        torch.cuda.synchronize()
+        for s, w in want.items():
+            for k, v in w.items():
+                assert torch.equal(out[k][s], v.view(out[k][s].shape)), (s, k)
+        slab, so = (slab + T) % R, (so + T) % S
+    _same_state(a, b)
 
 
 def test_step_multi_obs_wide_and_ragged(ssa, monkeypatch):

@@ -1,4 +1,4 @@
-"""Host-side settings on the driver's short timed region (VERDICT r03 item 1:
+"""Host-side (and launch-shape) settings on the driver's short timed region (VERDICT r03 item 1:
 the K = 20 wall vs HIP-event gap).  The region is bench.timed_multi's: two
 stream events around one k_step_multi launch of K ticks, then a device
 synchronize.  Each setting runs in its own child process (the parent never
@@ -29,6 +29,10 @@ SETTINGS = {
     "dev_kernarg_1": {"HIP_FORCE_DEV_KERNARG": "1"},
     "dev_kernarg_0": {"HIP_FORCE_DEV_KERNARG": "0"},
     "schedule_spin": {"SK_KNOB_SCHEDULE_SPIN": "1"},
+    # the kernel's own launch shape: 256-lane workgroups (a quarter of the
+    # workgroups to dispatch) and the restart draw under the loads
+    "block_256": {"SK_MULTI_BLOCK": "256"},
+    "early_draw": {"SK_MULTI_EARLY": "1"},
 }
 
 
