@@ -1415,8 +1415,12 @@ __device__ __forceinline__ void normals4(uint64_t seed, uint64_t call, uint32_t 
 // noisy4 in two parts, bit for bit the same: the draws (Philox words ->
 // the pairs' L and cos / sin; independent of the GEMM, so they can be issued
 // ahead of it and run under its MFMAs) and the combination with m and v
-#ifndef SK_NOISE_HOIST  // A/B builds: 0 draws layer 2's noise after its GEMM
-#define SK_NOISE_HOIST 1
+// SK_NOISE_HOIST = 1 (A/B builds) draws layer 2's noise before its second
+// half's GEMM instead of after it: neutral at two workgroups per CU
+// (profiles/r04g_noise_hoist_ab.jsonl); at three its 24 live registers
+// spilled (config 5 acting 119 vs 112 us, profiles/r04p_hoist_ab.jsonl)
+#ifndef SK_NOISE_HOIST
+#define SK_NOISE_HOIST 0
 #endif
 struct Draw4 {
   float L[2], c[2], s[2];
@@ -1482,7 +1486,7 @@ struct RowsPlayers {
   __device__ bool valid(int i) const { return g0 + (i & 15) < n; }
 };
 
-// one 32-row tile per workgroup of 4 waves: layer 1 n-tiles 2w, 2w+1,
+// one 32-row tile per workgroup of 4 waves: layer 1 n-tiles w, 4 + w,
 // layer 2 n-tile w, layer 3 by all threads.  NOISE: per layer y = xW + b +
 // sd sqrt(x^2 W^2 + b^2) xi, xi ~ N(0,1) per (row, unit) (exact in
 // distribution for w' = w (1 + sd N(0,1)) drawn per row, each noisy weight
@@ -1496,8 +1500,27 @@ struct RowsPlayers {
 // every wave has read them.  Round 3's f32-MFMA tile (128 dependent 32x32x2
 // f32 MFMAs per wave in layer 2: 5.2 us of the 4,096-game acting launch,
 // profiles/r03t_*) and its variance GEMM's bf16 operands are replaced.
-constexpr int kLdX1 = 24, kLdX2 = 264;              // bf16 row strides (48 / 528 B: conflict-free 16-B reads)
-constexpr int kX1Plane = 32 * kLdX1, kX2Plane = 32 * kLdX2;
+// Layer 1 runs in two halves of 128 units (n-tile 4h + w per wave), each
+// followed by its 8 k-steps of layer 2 into the same accumulators (the k
+// order, hence every sum, of one 16-step chain): the planes hold one half,
+// 41 KB of LDS per tile instead of 74 KB, so three workgroups share a CU
+// instead of two.
+// waves per SIMD the acting kernels are compiled for (their VGPR budget:
+// 512 / waves): with the half-size planes three workgroups share a CU
+// (config 5 acting 127 -> 112 us with SK_NOISE_HOIST 0; at two waves, 185
+// VGPRs, no gain: profiles/r04o_act_waves_ab.jsonl).  The episode kernel at
+// two: it held every loop-invariant weight fragment of the tile across the
+// episode (512 VGPRs, one workgroup per CU, spills) until its weight
+// addresses were made opaque per tick (180 -> 110 us per tick,
+// profiles/r04o_episode_ab.jsonl)
+#ifndef SK_ACT_WAVES
+#define SK_ACT_WAVES 3
+#endif
+#ifndef SK_EPISODE_WAVES
+#define SK_EPISODE_WAVES 2
+#endif
+constexpr int kLdX1 = 24, kLdX2 = 136;              // bf16 row strides (48 / 272 B: conflict-free 16-B reads)
+constexpr int kX1Plane = 32 * kLdX1, kX2Plane = 32 * kLdX2;  // kX2Plane: one half of layer 1's units
 constexpr size_t kActorTileLds = (size_t)(4 * kX1Plane + 4 * kX2Plane) * 2;
 static_assert((size_t)32 * kLdH2 * 4 <= (size_t)4 * kX2Plane * 2, "layer 2's outputs fit over the layer-1 planes");
 struct ActorLds {
@@ -1535,54 +1558,54 @@ __device__ __forceinline__ void actor_tile32(const Net& A, const char* __restric
   __syncthreads();
   TP32(2);
   const gbf8 W1 = (gbf8)(pk + sksplit::kOffW1), W2 = (gbf8)(pk + sksplit::kOffW2);
+  const int u2 = 32 * w + (lane & 31);  // this wave's layer-2 unit
+  const float k2 = skmlp::noise_k2(sd);
+  Draw4 dr[4];
+  f32x16 m2 = {0}, var2 = {0};
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int nt = 2 * w + t, u = 32 * nt + (lane & 31);
-    f32x16 m = {0}, var = {0};
-    gemm6<1, NOISE>(m, var, T.S, kLdX1, kX1Plane, W1 + 64 * nt, sksplit::kW1Plane, lane);
-    const float b = A.b1[u];
-    if (NOISE) {
-      const float k2 = skmlp::noise_k2(sd);
+  for (int h = 0; h < 2; ++h) {
+    {  // layer 1, units 128 h .. 128 h + 127: n-tile 4 h + w, into the planes' column u - 128 h
+      const int nt = 4 * h + w, u = 32 * nt + (lane & 31), col = u - 128 * h;
+      f32x16 m = {0}, var = {0};
+      gemm6<1, NOISE>(m, var, T.S, kLdX1, kX1Plane, W1 + 64 * nt, sksplit::kW1Plane, lane);
+      const float b = A.b1[u];
+      if (NOISE) {
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        float y[4];
-        noisy4(seed, call, (uint32_t)R(drow(4 * g, lane)), (uint32_t)u, k2, b, m, var, 4 * g, y);
+        for (int g = 0; g < 4; ++g) {
+          float y[4];
+          noisy4(seed, call, (uint32_t)R(drow(4 * g, lane)), (uint32_t)u, k2, b, m, var, 4 * g, y);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) put4(T.H1, kX2Plane, drow(4 * g + q, lane) * kLdX2 + u, fmaxf(y[q], 0.f));
+          for (int q = 0; q < 4; ++q) put4(T.H1, kX2Plane, drow(4 * g + q, lane) * kLdX2 + col, fmaxf(y[q], 0.f));
+        }
+      } else {
+#pragma unroll
+        for (int v = 0; v < 16; ++v) put4(T.H1, kX2Plane, drow(v, lane) * kLdX2 + col, fmaxf(m[v] + b, 0.f));
       }
-    } else {
-#pragma unroll
-      for (int v = 0; v < 16; ++v) put4(T.H1, kX2Plane, drow(v, lane) * kLdX2 + u, fmaxf(m[v] + b, 0.f));
     }
+    __syncthreads();
+    if (h == 0) TP32(3);
+    if (NOISE && SK_NOISE_HOIST && h == 1) {  // layer 2's draws among the MFMAs (A/B only)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) dr[g] = draw4n(seed, call, (uint32_t)R(drow(4 * g, lane)), (uint32_t)(kH1 + u2), k2);
+    }
+    // layer 2, k = 128 h .. 128 h + 127 (k-steps 8 h .. 8 h + 7 of n-tile w)
+    gemm6<8, NOISE>(m2, var2, T.H1, kLdX2, kX2Plane, W2 + 16 * 64 * w + 8 * 64 * h, sksplit::kW2Plane, lane);
+    __syncthreads();  // every wave has read this half: the next half / layer 2's outputs go over it
   }
-  __syncthreads();
-  TP32(3);
   {
-    const int u = 32 * w + (lane & 31);
-    // layer 2's noise draws first: they do not depend on the GEMM, so their
-    // VALU work (Philox, log, sin / cos) issues among its MFMAs
-    Draw4 dr[4];
-    const float k2 = skmlp::noise_k2(sd);
-    if (NOISE && SK_NOISE_HOIST) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) dr[g] = draw4n(seed, call, (uint32_t)R(drow(4 * g, lane)), (uint32_t)(kH1 + u), k2);
-    }
-    f32x16 m = {0}, var = {0};
-    gemm6<16, NOISE>(m, var, T.H1, kLdX2, kX2Plane, W2 + 16 * 64 * w, sksplit::kW2Plane, lane);
-    const float b = A.b2[u];
-    __syncthreads();  // every wave has read the layer-1 planes: layer 2's outputs go over them
+    const float b = A.b2[u2];
     if (NOISE) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         float y[4];
-        if (!SK_NOISE_HOIST) dr[g] = draw4n(seed, call, (uint32_t)R(drow(4 * g, lane)), (uint32_t)(kH1 + u), k2);
-        noisy4_apply(dr[g], b, m, var, 4 * g, y);
+        if (!SK_NOISE_HOIST) dr[g] = draw4n(seed, call, (uint32_t)R(drow(4 * g, lane)), (uint32_t)(kH1 + u2), k2);
+        noisy4_apply(dr[g], b, m2, var2, 4 * g, y);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) T.H2[drow(4 * g + q, lane) * kLdH2 + u] = fmaxf(y[q], 0.f);
+        for (int q = 0; q < 4; ++q) T.H2[drow(4 * g + q, lane) * kLdH2 + u2] = fmaxf(y[q], 0.f);
       }
     } else {
 #pragma unroll
-      for (int v = 0; v < 16; ++v) T.H2[drow(v, lane) * kLdH2 + u] = fmaxf(m[v] + b, 0.f);
+      for (int v = 0; v < 16; ++v) T.H2[drow(v, lane) * kLdH2 + u2] = fmaxf(m2[v] + b, 0.f);
     }
   }
   __syncthreads();
@@ -1634,7 +1657,7 @@ __device__ __forceinline__ void actor_tile32(const Net& A, const char* __restric
 }
 
 template <bool NOISE>
-__global__ void __launch_bounds__(kFwdThreads) k_actor_fwd32(const float* __restrict__ aflat,
+__global__ void __launch_bounds__(kFwdThreads, SK_ACT_WAVES) k_actor_fwd32(const float* __restrict__ aflat,
                                                              const char* __restrict__ apack,
                                                              const float* __restrict__ X, float* __restrict__ out,
                                                              int64_t rows, float sd, float action_sd, uint64_t seed,
@@ -1701,7 +1724,7 @@ __device__ __forceinline__ void act_step32(const float* __restrict__ aflat, cons
 }
 
 template <bool NOISE>
-__global__ void __launch_bounds__(kFwdThreads) k_act_step32(const float* __restrict__ aflat,
+__global__ void __launch_bounds__(kFwdThreads, SK_ACT_WAVES) k_act_step32(const float* __restrict__ aflat,
                                                             const char* __restrict__ apack,
                                                             float* __restrict__ act_out, float sd, float action_sd,
                                                             uint64_t seed, uint64_t* __restrict__ call_ctr,
@@ -1736,7 +1759,7 @@ struct EpisodeArgs {
   int n_ticks;
 };
 template <bool NOISE>
-__global__ void __launch_bounds__(kFwdThreads) k_act_episode32(const float* __restrict__ aflat,
+__global__ void __launch_bounds__(kFwdThreads, SK_EPISODE_WAVES) k_act_episode32(const float* __restrict__ aflat,
                                                                const char* __restrict__ apack, float sd,
                                                                float action_sd, uint64_t seed,
                                                                uint64_t* __restrict__ call_ctr, sk::StepArgs a,
@@ -1752,13 +1775,19 @@ __global__ void __launch_bounds__(kFwdThreads) k_act_episode32(const float* __re
   // count, and the slot line is stored by lane 0 (the episode's outcome is
   // the final state and `lengths`)
   sk_counters* const slot = nullptr;
-  const Net A = net_of(aflat, kALd, 2);
   const bool draws = (NOISE || action_sd != 0.f) && call_ctr;
   const uint64_t call0 = draws ? call_ctr[0] : 0;
   const uint64_t step0 = sk::step_read(a.step);
   const int64_t n = a.n, gt = 2 * g0 + lane, gi = gt >> 1;  // wave 0: lane -> (game, player)
   if (w0 && lane < 32 && (lane & 1) == 0 && gi < n) ep.lengths[gi] = 0;
   for (int t = 0; t < ep.n_ticks; ++t) {
+    // the weights' addresses opaque per tick: otherwise every weight fragment
+    // and bias the tile loads is loop-invariant, hoisted out of the loop and
+    // held (or spilled) across the whole episode
+    const float* af = aflat;
+    const char* pk = apack;
+    asm volatile("" : "+s"(af), "+s"(pk));
+    const Net A = net_of(af, kALd, 2);
     sk::StepArgs at = a;
     at.acting_obs = ep.states + (int64_t)t * 24 * n;
     at.obs = ep.states + (int64_t)(t + 1) * 24 * n;
@@ -1767,7 +1796,7 @@ __global__ void __launch_bounds__(kFwdThreads) k_act_episode32(const float* __re
     // the state loads fly under the actor tile (act_step32's order); the
     // loop test waits for them only after it
     if (w0) L = sk::split_load(at, lane < 32 ? gt : 2 * n, slot);
-    actor_tile32<NOISE>(A, apack, at.acting_obs, ep.actions + (int64_t)t * 4 * n, RowsPlayers{g0, n}, sd,
+    actor_tile32<NOISE>(A, pk, at.acting_obs, ep.actions + (int64_t)t * 4 * n, RowsPlayers{g0, n}, sd,
                         action_sd, seed, call0 + 1 + (uint64_t)t, actor_lds(smem), sAct);
     if (w0) {
       // the reference's loop test (:304) on the pre-tick state; both lanes of a game agree
