@@ -1721,6 +1721,7 @@ int sk_env_act_episode(sk_env* e, const float* actor_flat, const void* actor_pac
   if (!rewards || !lengths || n_ticks <= 0) return fail(SK_EINVAL, "rewards / lengths NULL or n_ticks <= 0");
   if (e->n % 4) return fail(SK_EINVAL, "sk_env_act_episode needs N % 4 == 0");
   if (((uintptr_t)lengths) & 3) return fail(SK_EINVAL, "lengths must be 4-byte aligned");
+  if (!actor_pack || (((uintptr_t)actor_pack) & 15)) return fail(SK_EINVAL, "actor_pack is NULL or misaligned");
   StepArgs a;
   rc = act_step_args(e, states, actions, states + (size_t)24 * e->n, rewards, reward_kind, nullptr, nullptr,
                      tick_limit, 0, 0, nullptr, nullptr, 0, nullptr, nullptr, nullptr, a);
