@@ -15,6 +15,8 @@
 #   bench      python bench.py (every leg)                        -> $O/bench_default.json
 #   bench20    python bench.py --steps 20 --warmup 5 (the driver)  -> $O/bench_driver_k20.json
 #   pmclearn   PMC MFMA utilisation of the learner kernels
+#   pmcact     PMC MFMA / VALU / wait counters of the acting launch (tools/pmc_act_step.sh)
+#   pmcobs     SQ counters of the full-contract and headline multi-tick kernels (tools/pmc_multi_obs.sh)
 #   py:FILE    python3 FILE (a diagnostic script; ARGS= passed through)
 # Outputs under gpurun_out/$TAG; copy what is judged into profiles/.
 set -u
@@ -91,6 +93,12 @@ print(json.dumps(r))" > $O/prof_learn_${tg}_$pr.json 2> $O/prof_learn_${tg}_$pr.
     bash tools/pmc_learner.sh > $O/pmc.log 2>&1 || stop pmc $?
     python3 tools/pmc_summary.py gpurun_out/pmcl/u/pmc_counter_collection.csv gpurun_out/pmcl/f/pmc_counter_collection.csv \
       > $O/pmc_mfma_learner.json 2> $O/pmc_summary.err || echo "pmc summary failed";;
+  pmcact)
+    bash tools/pmc_act_step.sh $TAG > $O/pmc_act.log 2>&1 || stop pmcact $?
+    cp gpurun_out/pmca_$TAG/summary.json $O/pmc_act_step.json;;
+  pmcobs)
+    bash tools/pmc_multi_obs.sh $TAG > $O/pmc_obs.log 2>&1 || stop pmcobs $?
+    cp gpurun_out/pmco_$TAG/summary.json $O/pmc_sq_multi_obs.json;;
   py:*)
     f=${s#py:}; b=$(basename $f .py)
     timeout -k 10 ${PYTIMEOUT:-600} python3 -u $f ${ARGS:-} > $O/$b.out 2> $O/$b.err || stop $s $?
