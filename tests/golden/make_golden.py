@@ -336,6 +336,28 @@ def scenario_negrot(seed=11):
     pack("negrot", inits, acts, results, 2000, "learner", note="negative rotations (floored %)")
 
 
+def scenario_bigrot(seed=29):
+    """Rotations far from the game's usual +-500 (settable through the class
+    API's Player.rotation): 1e3 .. 1e8 rad, on both sides of the fast sin/cos
+    path's reduction range (|r| < 2^20 pi/2 = 1,647,099.3), with the
+    projectiles inheriting them when fired."""
+    rng = random.Random(seed)
+    inits, acts, results = [], [], []
+    T = 200
+    mags = [1.0e3, 7.5e4, 1.6e6, 1647099.0, 1647100.0, 3.3e6, 2.0e7, 1.0e8]
+    for e, mag in enumerate(mags):
+        g = SkillshotGame()
+        init = fixed_init()
+        init["pos"] = [[rng.randrange(25, 225), rng.randrange(25, 225)] for _ in range(2)]
+        init["rot"] = [mag * (1 if e % 2 else -1) + rng.uniform(-1, 1), -mag + rng.uniform(-1, 1)]
+        set_state(g, init)
+        a = f32_uniform(rng, (T, 2, 2))
+        inits.append(snapshot(g))
+        acts.append(a)
+        results.append(run_env(g, a, 2000))
+    pack("bigrot", inits, acts, results, 2000, "learner", note="rotations of 1e3 .. 1e8 rad (class-API settable)")
+
+
 def scenario_clamp(seed=13):
     rng = random.Random(seed)
     inits, acts, results = [], [], []
@@ -441,7 +463,9 @@ def scenario_raw(seed=19):
          note="per-method calls, sparse shooting, stepping continues 40 ticks after game end")
 
 
-if __name__ == "__main__" and "--boards" not in sys.argv:
+if __name__ == "__main__" and "--only" in sys.argv:  # one scenario: --only NAME (e.g. bigrot)
+    globals()["scenario_" + sys.argv[sys.argv.index("--only") + 1]]()
+elif __name__ == "__main__" and "--boards" not in sys.argv:
     scenario_random_policy("fixed_random", 8, 2000, 2000, "fixed", 1)
     scenario_random_policy("numpy_start", 8, 2000, 2000, "numpy", 2)
     scenario_random_policy("int_start_limit200", 12, 200, 200, "int", 3)
@@ -495,5 +519,5 @@ def scenario_boards():
     print(f"boards: {len(states)} states -> {os.path.getsize(path)} bytes")
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and "--only" not in sys.argv:
     scenario_boards()
