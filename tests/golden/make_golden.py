@@ -358,6 +358,36 @@ def scenario_bigrot(seed=29):
     pack("bigrot", inits, acts, results, 2000, "learner", note="rotations of 1e3 .. 1e8 rad (class-API settable)")
 
 
+def scenario_offboard(seed=31):
+    """Players and projectiles placed outside the 250 x 250 board (the class
+    API sets positions freely; Player.check_pos_valid only refuses moves):
+    negative and > 250 coordinates, a live projectile off the board, some
+    games starting with a projectile already in flight toward the other
+    player."""
+    rng = random.Random(seed)
+    inits, acts, results = [], [], []
+    T = 150
+    places = [([-40, 100], [120, 120]), ([300, -20], [10, 240]), ([125, 260], [125, -30]),
+              ([-5, -5], [255, 255]), ([0, 245], [245, 0]), ([-100, 400], [60, 60])]
+    for e, (p1, p2) in enumerate(places):
+        g = SkillshotGame()
+        init = fixed_init()
+        init["pos"] = [p1, p2]
+        init["rot"] = [rng.uniform(-4, 4), rng.uniform(-4, 4)]
+        if e % 2 == 0:  # player 1's projectile in flight, possibly off the board
+            init["qpos"] = [[p1[0] + rng.randrange(-30, 30), p1[1] + rng.randrange(-30, 30)], [0, 0]]
+            init["qrot"] = [rng.uniform(-4, 4), 0.0]
+            init["qcd"] = [rng.randrange(-5, 15), 0]
+            init["qage"] = [rng.randrange(0, 20), 0]
+            init["qvalid"] = [1, 0]
+        set_state(g, init)
+        a = f32_uniform(rng, (T, 2, 2))
+        inits.append(snapshot(g))
+        acts.append(a)
+        results.append(run_env(g, a, 2000))
+    pack("offboard", inits, acts, results, 2000, "learner", note="positions / projectiles outside the board")
+
+
 def scenario_clamp(seed=13):
     rng = random.Random(seed)
     inits, acts, results = [], [], []
