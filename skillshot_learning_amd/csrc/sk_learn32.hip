@@ -45,7 +45,7 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));  // W2 rows of the critic are 8-B aligned
 
 constexpr int kIn = 12, kH1 = 256, kH2 = 128;
-constexpr int kLdS = 36, kLdH1 = 260, kLdH2 = 132;  // LDS row strides (floats): 16-B aligned, banks rotated
+constexpr int kLdH1 = 260, kLdH2 = 132;  // LDS row strides (floats): 16-B aligned, banks rotated
 constexpr int kThreads = 512;                        // grad kernels: 8 waves per 32-row sub-tile
 constexpr int kFwdThreads = 256;                     // forward: 4 waves per 32-row tile
 
@@ -84,15 +84,6 @@ __device__ __forceinline__ int launder_lane(int lane) {
   return lane;
 }
 
-__device__ __forceinline__ f32x16 mf(float a, float b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
-}
-__device__ __forceinline__ f32x16 mf4(f4 a, f4 b, f32x16 c) {
-  c = mf(a.x, b.x, c);
-  c = mf(a.y, b.y, c);
-  c = mf(a.z, b.z, c);
-  return mf(a.w, b.w, c);
-}
 __device__ __forceinline__ int drow(int v, int lane) { return 8 * (v >> 2) + 4 * (lane >> 5) + (v & 3); }
 
 __device__ __forceinline__ uint4 philox(uint4 c, uint32_t k0, uint32_t k1) {
