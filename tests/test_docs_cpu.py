@@ -37,3 +37,16 @@ def test_cited_tools_exist():
     missing = [(d, p) for d, p in _refs("tools")
                if p.endswith((".py", ".sh")) and not glob.glob(os.path.join(ROOT, "tools", p))]
     assert not missing, missing
+
+
+def test_cited_tests_exist():
+    """test functions the docs name (a prefix may stand for a parametrised family)"""
+    names = set()
+    for f in glob.glob(os.path.join(ROOT, "tests", "*.py")):
+        names.update(re.findall(r"^def (test_\w+)", open(f).read(), re.M))
+    missing = []
+    for doc in DOCS:
+        for n in re.findall(r"`(test_\w+)", open(os.path.join(ROOT, doc)).read()):
+            if not any(x.startswith(n) for x in names):
+                missing.append((doc, n))
+    assert not missing, missing
