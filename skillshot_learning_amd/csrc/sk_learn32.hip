@@ -1070,6 +1070,7 @@ __device__ __forceinline__ void grad_slice_bwd(int bid, float* smem_sl, SK_SLICE
   const int64_t row0 = (int64_t)rt * kR;
   const float* fl[3] = {f0, f1, f2};
   const gfp W2 = (gfp)f0 + kPW2;
+  TP32(20);
   // ---- phase 0: every global load
   // the slice's W2 rows down the columns of n-tiles w + 4q (the dz1 GEMM of phase 3)
   float wd[4][4];
@@ -1130,6 +1131,7 @@ __device__ __forceinline__ void grad_slice_bwd(int bid, float* smem_sl, SK_SLICE
     }
   }
   lds_sync32();
+  TP32(21);
   // ---- phase 1: layer 1 of the trained net (MFMA) and the per-row reductions (VALU)
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -1216,6 +1218,7 @@ __device__ __forceinline__ void grad_slice_bwd(int bid, float* smem_sl, SK_SLICE
     }
   }
   lds_sync32();
+  TP32(22);
   // ---- phase 2: dz2 of the slice's units (thread = (row, j))
   {
     const int row = tid >> 4, j = tid & 15, u = kSliceU * s + j;
@@ -1255,6 +1258,7 @@ __device__ __forceinline__ void grad_slice_bwd(int bid, float* smem_sl, SK_SLICE
     if (lane < kSliceU) *(f4*)(sH2T + (w * kSliceU + j) * 4) = f4{v[0], v[1], v[2], v[3]};
   }
   lds_sync32();
+  TP32(23);
   // ---- phase 3: the slice's per-unit gradients; dW2 rows; dz1 share -> dW1, db1
   float* P = partial + (int64_t)rt * NPAR;
   float* PW = partial_w1 + (int64_t)bid * kW1Part;
@@ -1319,6 +1323,7 @@ __device__ __forceinline__ void grad_slice_bwd(int bid, float* smem_sl, SK_SLICE
       for (int r = 0; r < 4; ++r) PW[kPW1 + (16 * nt + 4 * g + r) * kIn + i] = gw1[r];
     }
   }
+  TP32(24);
 }
 
 template <int MODE>
