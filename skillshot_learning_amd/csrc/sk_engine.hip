@@ -56,6 +56,8 @@ struct sk_env {
   int multi_early;    // k_step_multi: the restart draw under the loads, 0 (default) / 1 (SK_MULTI_EARLY)
   int multi_block;    // workgroup lanes (SK_MULTI_BLOCK): split geometry -1 auto, 64 or 512; lane per game 64 or 256
   int multi_stagger;  // waves 4-7 of a 512-lane workgroup start this x 512 cycles late (SK_MULTI_STAGGER)
+  int multi_prefetch; // action-slab prefetch wave, ticks ahead (SK_MULTI_PREFETCH; 0 off, -1 auto): k_step_multi
+                      // (64-lane, 88-B form) and k_step_split_multi
   // k_step_multi's packed resident form between ticks: -1 auto (above one
   // wave per SIMD), 1 / 0 force (SK_MULTI_PACK)
   int multi_pack;
@@ -709,8 +711,58 @@ extern "C" int skdiag_set_multi_trace(void* buf) {
   } while (0)
 #endif
 
-template <int POL, bool PACK, int BLK>
-__global__ void __launch_bounds__(BLK) k_step_multi(MultiArgs a, Cfg c, int early) {
+// PF > 0: one more wave per workgroup pulls the action slab PF ticks ahead
+// into the CU's L1 / the XCD's L2 (global -> LDS copies into a scratch line
+// nobody reads: no VGPR results to wait for), so the tick's own action loads
+// hit cache instead of waiting for HBM.  The ring is larger than the
+// Infinity Cache, so every slab is still fetched from HBM once; only the
+// wait moves off the tick's dependency chain (the state loads cannot move:
+// tick t + 1 reads what tick t stored).  The two waves meet at one raw
+// s_barrier per tick, which keeps the prefetch PF ticks ahead and no more.
+// the workgroup's GAMES games of both action planes, 16 bytes (two games of
+// one plane) per lane and GAMES / 64 wave-instructions
+template <int GAMES>
+__device__ __forceinline__ void prefetch_slab(const MultiArgs& a, int64_t slab, int4* scratch) {
+  static_assert(GAMES % 32 == 0, "whole 16-byte lines per plane");
+  const int lane = threadIdx.x & 63;
+  const int64_t g0 = (int64_t)blockIdx.x * GAMES;
+#pragma unroll
+  for (int j = 0; j < (GAMES + 63) / 64; ++j) {
+    const int l = 64 * j + lane, pl = l / (GAMES / 2);
+    const int64_t g = g0 + 2 * (l - pl * (GAMES / 2));
+    if (l < GAMES && g + 1 < a.n)
+      __builtin_amdgcn_global_load_lds((void*)(a.actions + (slab * 2 + pl) * a.n + g), scratch, 16, 0, 0);
+  }
+}
+
+// the prefetch wave's loop (see k_step_multi): n_ticks raw barriers, slab of
+// tick t + PF after the t-th
+template <int GAMES, int PF>
+__device__ __forceinline__ void prefetch_wave(const MultiArgs& a, int4* scratch) {
+  int64_t s = a.slab0;  // the slab of tick t + PF (of tick 0 before the loop)
+  for (int t = 0; t < a.n_ticks; ++t) {
+    __builtin_amdgcn_s_barrier();
+    if (t == 0) {  // ticks 1 .. PF - 1 (tick 0 loads its own slab; past n_ticks s is never used)
+      for (int k = 1; k < PF && k < a.n_ticks; ++k) {
+        s = s + 1 == a.ring ? 0 : s + 1;
+        prefetch_slab<GAMES>(a, s, scratch);
+      }
+    }
+    s = s + 1 == a.ring ? 0 : s + 1;
+    if (t + PF < a.n_ticks) prefetch_slab<GAMES>(a, s, scratch);
+  }
+  __builtin_amdgcn_s_waitcnt(0);  // no LDS write outlives the workgroup
+}
+
+template <int POL, bool PACK, int BLK, int PF = 0>
+__global__ void __launch_bounds__(BLK + (PF > 0 ? 64 : 0)) k_step_multi(MultiArgs a, Cfg c, int early) {
+  if constexpr (PF > 0) {
+    __shared__ int4 pf_scratch[64];
+    if (threadIdx.x >= BLK) {  // the prefetch wave: n_ticks barriers, like the stepping waves
+      prefetch_wave<BLK, PF>(a, pf_scratch);
+      return;
+    }
+  }
   SK_MTS(0);
   MultiLane L;
   L.i = (int64_t)blockIdx.x * BLK + threadIdx.x;
@@ -725,6 +777,7 @@ __global__ void __launch_bounds__(BLK) k_step_multi(MultiArgs a, Cfg c, int earl
   int64_t slab = a.slab0, so = a.out0;
   bool packed = false;  // every launch starts from (and ends in) the exchange format
   for (int t = 0; t < a.n_ticks; ++t) {
+    if constexpr (PF > 0) __builtin_amdgcn_s_barrier();
     multi_tick<POL, PACK>(a, c, r, rp, L, wc, so, step0 + (uint64_t)t, slab, packed, t + 1 == a.n_ticks);
     slab = slab + 1 == a.ring ? 0 : slab + 1;
     so = so + 1 == a.out_slabs ? 0 : so + 1;
@@ -931,8 +984,15 @@ __device__ __forceinline__ void split_multi_tick(const MultiArgs& a, const Cfg& 
 // "Two waves per SIMD"); `stagger` > 0 starts waves 4-7 stagger x 512
 // cycles late, so the pair alternates a tick's memory round trip with the
 // partner's arithmetic instead of both waiting at once.
-template <int POL, int BLK, bool OBS = false>
-__global__ void __launch_bounds__(BLK) k_step_split_multi(MultiArgs a, Cfg c, int stagger) {
+template <int POL, int BLK, bool OBS = false, int PF = 0>
+__global__ void __launch_bounds__(BLK + (PF > 0 ? 64 : 0)) k_step_split_multi(MultiArgs a, Cfg c, int stagger) {
+  if constexpr (PF > 0) {  // the action-slab prefetch wave (k_step_multi)
+    __shared__ int4 pf_scratch[64];
+    if (threadIdx.x >= BLK) {
+      prefetch_wave<BLK / 2, PF>(a, pf_scratch);
+      return;
+    }
+  }
   SplitLane L;
   const int64_t gt = (int64_t)blockIdx.x * BLK + threadIdx.x;
   L.i = gt >> 1;
@@ -950,6 +1010,7 @@ __global__ void __launch_bounds__(BLK) k_step_split_multi(MultiArgs a, Cfg c, in
   const __amdgpu_buffer_rsrc_t r = raw_rsrc(a.base);
   int64_t slab = a.slab0, so = a.out0;
   for (int t = 0; t < a.n_ticks; ++t) {
+    if constexpr (PF > 0) __builtin_amdgcn_s_barrier();
     split_multi_tick<POL, OBS>(a, c, r, L, wc, so, step0 + (uint64_t)t, slab);
     slab = slab + 1 == a.ring ? 0 : slab + 1;
     so = so + 1 == a.out_slabs ? 0 : so + 1;
@@ -1119,6 +1180,18 @@ static hipError_t launch_timed(void (*k)(P...), dim3 grid, dim3 block, hipStream
   return hipExtLaunchKernel(reinterpret_cast<const void*>(k), grid, block, argv, 0, s, e0, e1, 0);
 }
 
+// k_step_split_multi<POL, BLK, OBS> with its action-slab prefetch wave pf
+// ticks ahead (1, 2 or 4; 0 none; write-through port only)
+template <int POL, int BLK, bool OBS>
+static hipError_t launch_split_multi(int pf, dim3 g, hipStream_t hs, const MultiArgs& a, const Cfg& c, int stagger) {
+  if constexpr (POL == 1) {
+    if (pf == 1) return launch_timed(k_step_split_multi<1, BLK, OBS, 1>, g, dim3(BLK + 64), hs, nullptr, nullptr, a, c, stagger);
+    if (pf == 2) return launch_timed(k_step_split_multi<1, BLK, OBS, 2>, g, dim3(BLK + 64), hs, nullptr, nullptr, a, c, stagger);
+    if (pf > 2) return launch_timed(k_step_split_multi<1, BLK, OBS, 4>, g, dim3(BLK + 64), hs, nullptr, nullptr, a, c, stagger);
+  }
+  return launch_timed(k_step_split_multi<POL, BLK, OBS>, g, dim3(BLK), hs, nullptr, nullptr, a, c, stagger);
+}
+
 // ------------------------------------------------------------------ host ABI
 extern "C" {
 
@@ -1222,6 +1295,8 @@ static int make_env(sk_env** out, const sk_state_view* view, int32_t n, int64_t 
   if (const char* mb = std::getenv("SK_MULTI_BLOCK")) e->multi_block = std::atoi(mb);
   e->multi_stagger = 0;
   if (const char* mg = std::getenv("SK_MULTI_STAGGER")) e->multi_stagger = std::atoi(mg);
+  e->multi_prefetch = -1;
+  if (const char* mp = std::getenv("SK_MULTI_PREFETCH")) e->multi_prefetch = std::atoi(mp);
   e->multi_pack = -1;
   if (const char* mk = std::getenv("SK_MULTI_PACK")) e->multi_pack = std::atoi(mk);
   e->d_pack = nullptr;
@@ -1863,27 +1938,24 @@ static int step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64
     const int64_t lanes = 2 * (int64_t)e->n;
     const bool wide = e->multi_block == 512 || (e->multi_block < 0 && lanes >= 512 * 256);
     const dim3 g512((unsigned)((lanes + 511) / 512)), g64(step_grid(lanes));
-    if (full) {
-      if (wide)
-        err = pol == 1 ? launch_timed(k_step_split_multi<1, 512, true>, g512, dim3(512), hs, e0, e1, a, e->dcfg,
-                                      e->multi_stagger)
-                       : launch_timed(k_step_split_multi<0, 512, true>, g512, dim3(512), hs, e0, e1, a, e->dcfg,
-                                      e->multi_stagger);
-      else
-        err = pol == 1 ? launch_timed(k_step_split_multi<1, kStepBlock, true>, g64, dim3(kStepBlock), hs, e0, e1, a,
-                                      e->dcfg, 0)
-                       : launch_timed(k_step_split_multi<0, kStepBlock, true>, g64, dim3(kStepBlock), hs, e0, e1, a,
-                                      e->dcfg, 0);
-    } else if (wide)
-      err = pol == 1 ? launch_timed(k_step_split_multi<1, 512>, g512, dim3(512), hs, e0, e1, a, e->dcfg,
-                                    e->multi_stagger)
-                     : launch_timed(k_step_split_multi<0, 512>, g512, dim3(512), hs, e0, e1, a, e->dcfg,
-                                    e->multi_stagger);
+    // the action-slab prefetch wave: SK_MULTI_PREFETCH, else, at 400 ticks
+    // per launch: the full contract 4 ticks ahead on 512-lane workgroups
+    // (65,536 games 4.35 -> 3.48-3.52 us per tick) and 1 on 64-lane ones
+    // (32,768 2.71 -> 2.59, 8,192 2.25 -> 2.24-2.25); the step-only tick 2
+    // (32,768 1.80 -> 1.68, 16,384 1.67 -> 1.645, 8,192 1.585 -> 1.58;
+    // profiles/r04ar_prefetch_*_sweep.jsonl, r04as_prefetch_obs64_sweep.jsonl)
+    const int pf = n_ticks < 2 ? 0 : e->multi_prefetch >= 0 ? e->multi_prefetch : full ? (wide ? 4 : 1) : 2;
+    const int sg = wide ? e->multi_stagger : 0;
+    if (full)
+      err = wide ? (pol == 1 ? launch_split_multi<1, 512, true>(pf, g512, hs, a, e->dcfg, sg)
+                             : launch_split_multi<0, 512, true>(pf, g512, hs, a, e->dcfg, sg))
+                 : (pol == 1 ? launch_split_multi<1, kStepBlock, true>(pf, g64, hs, a, e->dcfg, sg)
+                             : launch_split_multi<0, kStepBlock, true>(pf, g64, hs, a, e->dcfg, sg));
     else
-      err = pol == 1 ? launch_timed(k_step_split_multi<1, kStepBlock>, g64, dim3(kStepBlock), hs, e0, e1, a,
-                                    e->dcfg, 0)
-                     : launch_timed(k_step_split_multi<0, kStepBlock>, g64, dim3(kStepBlock), hs, e0, e1, a,
-                                    e->dcfg, 0);
+      err = wide ? (pol == 1 ? launch_split_multi<1, 512, false>(pf, g512, hs, a, e->dcfg, sg)
+                             : launch_split_multi<0, 512, false>(pf, g512, hs, a, e->dcfg, sg))
+                 : (pol == 1 ? launch_split_multi<1, kStepBlock, false>(pf, g64, hs, a, e->dcfg, sg)
+                             : launch_split_multi<0, kStepBlock, false>(pf, g64, hs, a, e->dcfg, sg));
   } else {
     // the restart draw under the loads (k_step's early draw) is off by
     // default here: 65,536 games 2.73 vs 2.81 us per tick at 20 ticks per
@@ -1908,6 +1980,19 @@ static int step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64
         err = pol == 1
                   ? launch_timed(k_step_multi<1, true, kStepBlock>, g, dim3(kStepBlock), hs, e0, e1, a, e->dcfg, early)
                   : launch_timed(k_step_multi<0, true, kStepBlock>, g, dim3(kStepBlock), hs, e0, e1, a, e->dcfg, early);
+      // the prefetch wave only on request here (auto: none): 65,536 games
+      // 2.36 vs 2.33-2.39 us per tick at PF 1-4 and slower at 20 ticks per
+      // launch, where actions held in cache (an 8-slab ring) give 2.0
+      // (profiles/r04aq_prefetch_sweep.jsonl, r04at_prefetch_ring_sweep.jsonl)
+      else if (pol == 1 && e->multi_prefetch > 0 && n_ticks > 1)
+        err = e->multi_prefetch == 1
+                  ? launch_timed(k_step_multi<1, false, kStepBlock, 1>, g, dim3(kStepBlock + 64), hs, e0, e1, a,
+                                 e->dcfg, early)
+                  : e->multi_prefetch == 2
+                        ? launch_timed(k_step_multi<1, false, kStepBlock, 2>, g, dim3(kStepBlock + 64), hs, e0, e1,
+                                       a, e->dcfg, early)
+                        : launch_timed(k_step_multi<1, false, kStepBlock, 4>, g, dim3(kStepBlock + 64), hs, e0, e1,
+                                       a, e->dcfg, early);
       else
         err = pol == 1
                   ? launch_timed(k_step_multi<1, false, kStepBlock>, g, dim3(kStepBlock), hs, e0, e1, a, e->dcfg,

@@ -3,7 +3,7 @@ VERDICT r03 item 5): n_ticks learner ticks with obs + reward in one launch
 must equal n_ticks sk_env_step(obs, reward) launches bit for bit — every
 tick's obs, reward, done and winner, the final state, the RNG step counter
 and the episode counters — for both state ports, both rewards, ragged
-batches, the 512-lane geometry, output rings shorter than the launch, and
+batches, the 512-lane geometry (with the action-slab prefetch wave), output rings shorter than the launch, and
 against the CPU backend (state bit-exact, obs within 1e-5: the CPU backend
 computes obs with libm's tan, the kernels from the tick's sin/cos), and
 launches of 1-3 ticks back to back."""
@@ -84,9 +84,12 @@ def test_step_multi_obs_short_launches(ssa, monkeypatch, T):
     _same_state(a, b)
 
 
-def test_step_multi_obs_wide_and_ragged(ssa, monkeypatch):
-    """the 512-lane workgroups (SK_MULTI_BLOCK=512) and a ragged batch"""
+@pytest.mark.parametrize("prefetch", ["0", "2", "4"])
+def test_step_multi_obs_wide_and_ragged(ssa, monkeypatch, prefetch):
+    """the 512-lane workgroups (SK_MULTI_BLOCK=512) and a ragged batch, with
+    and without the action-slab prefetch wave (SK_MULTI_PREFETCH)"""
     monkeypatch.setenv("SK_MULTI_BLOCK", "512")
+    monkeypatch.setenv("SK_MULTI_PREFETCH", prefetch)
     n, T, R = 131075, 40, 3
     a, b = _pair(ssa, n, 5, 30, monkeypatch, 1)
     acts = a.gen_random_actions(R)

@@ -11,6 +11,7 @@
 #   traffic    PMC FETCH/WRITE passes of the headline kernel -> profiles/traffic_k_step_multi*.json
 #   trafficobs the same for the full-contract multi-tick kernel -> traffic_k_step_split_multi_obs.json
 #   prof       rocprofv3 --kernel-trace --stats of the headline leg, K = 4,000 and the driver's K = 20
+#   proffull   rocprofv3 --kernel-trace --stats of the headline and full-contract legs (K = 4,000)
 #   proflearn  rocprofv3 kernel stats of the learner ticks (config 3 / 5, fp32 / bf16)
 #   bench      python bench.py (every leg)                        -> $O/bench_default.json
 #   bench20    python bench.py --steps 20 --warmup 5 (the driver)  -> $O/bench_driver_k20.json
@@ -73,6 +74,11 @@ for s in "${S[@]}"; do
       --steps 20 --warmup 5 --no-learner --no-cpu-baseline --no-large --no-full --no-rollout --no-variants \
       > $O/prof_bench_k20.json 2> $O/prof_bench_k20.err || stop prof20 $?
     summ prof_bench prof_bench_k20;;
+  proffull)
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_full -o prof -- python3 bench.py \
+      --no-learner --no-cpu-baseline --no-large --no-rollout --no-variants > $O/prof_full_bench.json \
+      2> $O/prof_full_bench.err || stop proffull $?
+    summ prof_full_bench;;
   proflearn)
     for cfg in ${LEARN_CFGS:-"4096:action_noise:fp32:c3" "4096:action_noise:bf16:c3" "65536:param_noise:fp32:c5" "65536:param_noise:bf16:c5"}; do
       IFS=: read -r n ex pr tg <<< "$cfg"

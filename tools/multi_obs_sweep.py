@@ -17,7 +17,8 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 
-def rate(n, T, block, stagger, pol, slabs, K=2000):
+def rate(n, T, block, stagger, pol, slabs, K=2000, prefetch=0):
+    os.environ["SK_MULTI_PREFETCH"] = str(prefetch)
     os.environ["SK_MULTI_BLOCK"] = str(block)
     os.environ["SK_MULTI_STAGGER"] = str(stagger)
     os.environ["SK_MULTI_POLICY"] = str(pol)
@@ -25,7 +26,7 @@ def rate(n, T, block, stagger, pol, slabs, K=2000):
     env.close()
     torch.cuda.empty_cache()
     us = ev * 1e3 / K
-    return dict(envs=n, ticks_per_launch=T, block=block, stagger=stagger, policy=pol, out_slabs=slabs,
+    return dict(envs=n, ticks_per_launch=T, block=block, prefetch=prefetch, stagger=stagger, policy=pol, out_slabs=slabs,
                 us_per_tick=us, env_steps_per_s=n / (us * 1e-6), frac=297 * n / (us * 1e-6) / 8e12)
 
 
@@ -37,6 +38,7 @@ def main():
     ap.add_argument("--staggers", default="0")
     ap.add_argument("--pols", default="1")
     ap.add_argument("--slabs", default="64")
+    ap.add_argument("--prefetches", default="0", help="SK_MULTI_PREFETCH values")
     ap.add_argument("--passes", type=int, default=2)
     a = ap.parse_args()
     L = lambda s: [int(x) for x in s.split(",")]  # noqa: E731
@@ -49,7 +51,9 @@ def main():
                             continue
                         for pol in L(a.pols):
                             for sl in L(a.slabs):
-                                print(json.dumps(dict(rate(n, T, b, sg, pol, sl), **{"pass": p})), flush=True)
+                                for pf in L(a.prefetches):
+                                    r = rate(n, T, b, sg, pol, sl, prefetch=pf)
+                                    print(json.dumps(dict(r, **{"pass": p})), flush=True)
 
 
 if __name__ == "__main__":
