@@ -324,12 +324,21 @@ __device__ __forceinline__ void lds_sync32() {
 // layout): b1 [256], b2 [128], critic action columns W2[u][256 + j] as [128][2],
 // W3 [n_out][128], b3
 constexpr int kT1 = 0, kT2 = 256, kTA = 384, kT3 = 640, kTB = 896;
+// One load per element from an index chosen by selects: a load per branch
+// put each element's candidate loads in one VGPR, and the write-after-write
+// between them cost an s_waitcnt vmcnt(0) -- a full round trip of every load
+// in flight -- per branch a wave took (profiles/r04ao_trace_slice_bwd.jsonl).
 __device__ __forceinline__ float tail_src(gfp f, int ld2, int n_out, int e) {
-  if (e < kT2) return f[kPB1 + e];
-  if (e < kTA) return f[pB2(ld2) + e - kT2];
-  if (e < kT3) return ld2 == kH1 ? 0.f : f[kPW2 + ((e - kTA) >> 1) * ld2 + kH1 + ((e - kTA) & 1)];
-  if (e < kTB) return e - kT3 < n_out * kH2 ? f[pW3(ld2) + e - kT3] : 0.f;
-  return e - kTB < n_out ? f[pB3(ld2, n_out) + e - kTB] : 0.f;
+  const int ea = e - kTA, e3 = e - kT3, eb = e - kTB;
+  int idx = e < kT2 ? kPB1 + e : pB2(ld2) + e - kT2;
+  // (a 24-bit product: the 32-bit one became a v_mad_u64_u32 whose unused
+  // high addend half was a register with a load in flight)
+  idx = e < kTA ? idx : kPW2 + (int)__umul24((unsigned)ea >> 1, (unsigned)ld2) + kH1 + (ea & 1);
+  idx = e < kT3 ? idx : pW3(ld2) + e3;
+  idx = e < kTB ? idx : pB3(ld2, n_out) + eb;
+  const bool ok = e < kTA || (e < kT3 ? ld2 != kH1 : e < kTB ? e3 < n_out * kH2 : eb < n_out);
+  const float v = f[ok ? idx : 0];
+  return ok ? v : 0.f;
 }
 
 struct G32 {
@@ -910,11 +919,21 @@ static_assert(sl_fwd_lds(kSlCriticBoot) <= 160 * 1024 && sl_bwd_lds(kSlCriticBoo
 
 // layer-1 fragment of unit n0 + i (g16_l1 with the weights already loaded:
 // the fragments are issued ahead of the staging barrier)
+// p[i] where ok, else 0, as one unconditional load (of p[0] where !ok) and a
+// select: a load under a branch put its value through a phi copy that the
+// waitcnt pass guarded with a vmcnt(0), a round trip of every load in flight
+__device__ __forceinline__ float ld_or0(const float* __restrict__ p, int64_t i, bool ok) {
+  const float v = p[ok ? i : 0];
+  return ok ? v : 0.f;
+}
+
+// (an unconditional load, zeroed by select where g = 3: the conditional load's
+// phi cost the actor's backward a vmcnt(0) right after it)
 __device__ __forceinline__ f4 w1_frag(gfp W1, int n0, int lane) {
   const int i = lane & 15, g = lane >> 4;
-  f4 w = {0.f, 0.f, 0.f, 0.f};
-  if (g < 3) w = *(gf4u)(W1 + (n0 + i) * kIn + 4 * g);
-  return w;
+  const f4 v = *(gf4u)(W1 + (n0 + i) * kIn + 4 * (g < 3 ? g : 0));
+  const bool ok = g < 3;
+  return f4{ok ? v.x : 0.f, ok ? v.y : 0.f, ok ? v.z : 0.f, ok ? v.w : 0.f};
 }
 __device__ __forceinline__ f32x4 g16_l1w(const float* S, f4 w, int lane) {
   const int i = lane & 15, g = lane >> 4;
@@ -1071,7 +1090,14 @@ __device__ __forceinline__ void grad_slice_bwd(int bid, float* smem_sl, SK_SLICE
   const float* fl[3] = {f0, f1, f2};
   const gfp W2 = (gfp)f0 + kPW2;
   TP32(20);
-  // ---- phase 0: every global load
+  // ---- phase 0: every global load; the tails first, their index arithmetic
+  // ahead of every load (after the others it shared registers with loads in
+  // flight and cost a full vmcnt(0) round trip)
+  float tv[NP][4];
+#pragma unroll
+  for (int p = 0; p < NP; ++p)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) tv[p][k] = tail_src((gfp)fl[p], sl_ld(MODE, p), sl_nout(MODE, p), tid + kSlThreads * k);
   // the slice's W2 rows down the columns of n-tiles w + 4q (the dz1 GEMM of phase 3)
   float wd[4][4];
 #pragma unroll
@@ -1088,16 +1114,11 @@ __device__ __forceinline__ void grad_slice_bwd(int bid, float* smem_sl, SK_SLICE
     for (int m = 0; m < 2; ++m)
       zv[p][m] = *(const f4*)(Z + ((int64_t)rt * NP + p) * kZPlane + 4 * (tid + kSlThreads * m));
   const int si = tid >> 4, sk = tid & 15;
-  const float sv = sk < kIn && row0 + si < B ? Sg[(row0 + si) * kIn + sk] : 0.f;
+  const float sv = ld_or0(Sg, (row0 + si) * kIn + sk, sk < kIn && row0 + si < B);
   const bool rok = tid < kR && row0 + tid < B;
   const float av = CRIT && tid < 32 && row0 + (tid >> 1) < B ? Ag[row0 * 2 + tid] : 0.f;
   const float rv = CRIT && rok ? (MODE == kSlCriticBoot ? Rg[row0 + tid] : Yg[row0 + tid]) : 0.f;
   const float dv = MODE == kSlCriticBoot && rok ? Dg[row0 + tid] : 0.f;
-  float tv[NP][4];
-#pragma unroll
-  for (int p = 0; p < NP; ++p)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) tv[p][k] = tail_src((gfp)fl[p], sl_ld(MODE, p), sl_nout(MODE, p), tid + kSlThreads * k);
   uint32_t keep0 = 0, keep1 = 0;
   if (CRIT) {
     const uint64_t call = (uint64_t)*call_ctr;
