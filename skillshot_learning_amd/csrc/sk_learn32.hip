@@ -973,6 +973,10 @@ __global__ void __launch_bounds__(kSlThreads) k_grad_slice_fwd(const float* __re
   const int ld = (MODE == kSlActor && p == 0) || (MODE == kSlCriticBoot && p == 1) ? kALd : kCLd;
   const float* Ssrc = MODE == kSlCriticBoot && p > 0 ? S2g : Sg;
   const bool drop = MODE != kSlActor && p == 0;
+  // the ring's insert count first: the row draw (Philox) needs it, and issued
+  // after the weight fragments it made the draw wait for all of them
+  const int64_t t_total = rs.ring ? *rs.total : 0;
+  const float bv = F[kPB1 + tid];  // b1, with the weight fragments
   // the slice's W2 fragments, rows 16 s + i, k = 64 w + 16 t + 4 g, and the
   // layer-1 fragments of n-tiles w + 4q: in flight under the staging
   f4 wv[4], w1v[4];
@@ -985,21 +989,21 @@ __global__ void __launch_bounds__(kSlThreads) k_grad_slice_fwd(const float* __re
   for (int q = 0; q < 4; ++q) w1v[q] = w1_frag((gfp)F + kPW1, 16 * (w + 4 * q), lane);
   const int si = tid >> 4, sk = tid & 15;
   float sv;
+  f4 rowv = {0.f, 0.f, 0.f, 0.f};
+  bool scat = false;
   if (rs.ring) {
-    const int64_t b = row0 + si, t = *rs.total;
+    const int64_t b = row0 + si, t = t_total;
     const bool ok = b < B && t > 0;
     const int64_t idx = ok ? ring_row(rs, b, t) : 0;
     const float* src = rs.ring + idx * 28;
-    sv = ok && sk < kIn ? src[(MODE == kSlCriticBoot && p > 0 ? 15 : 0) + sk] : 0.f;
-    if (ok && s == 0 && p == 0 && sk < 7) {  // the row into the sample buffers
-      const f4 v = *(const f4*)(src + 4 * sk);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) skmlp::ring_scatter(rs, b, 4 * sk + c, v[c]);
-    }
+    sv = ld_or0(src, (MODE == kSlCriticBoot && p > 0 ? 15 : 0) + sk, ok && sk < kIn);
+    // the row into the sample buffers (stored after the barrier below, so no
+    // wait for the sample's operands also waits for these stores)
+    scat = ok && s == 0 && p == 0 && sk < 7;
+    rowv = *(const f4*)(src + 4 * (sk < 7 ? sk : 0));
   } else {
-    sv = sk < kIn && row0 + si < B ? Ssrc[(row0 + si) * kIn + sk] : 0.f;
+    sv = ld_or0(Ssrc, (row0 + si) * kIn + sk, sk < kIn && row0 + si < B);
   }
-  const float bv = F[kPB1 + tid];
   uint32_t keep0 = 0, keep1 = 0;
   if (drop) {
     const uint64_t call = (uint64_t)*call_ctr;
@@ -1009,6 +1013,10 @@ __global__ void __launch_bounds__(kSlThreads) k_grad_slice_fwd(const float* __re
   sS[si * kLdS16 + sk] = sv;
   sB1[tid] = bv;
   lds_sync32();
+  if (scat) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) skmlp::ring_scatter(rs, row0 + si, 4 * sk + c, rowv[c]);
+  }
   // ---- layer 1, n-tiles w, w + 4, w + 8, w + 12
 #pragma unroll
   for (int q = 0; q < 4; ++q) {

@@ -204,13 +204,17 @@ __device__ __forceinline__ int64_t ring_row(const RingSample& q, int64_t b, int6
   const int64_t k = (int64_t)(((unsigned __int128)u53 * (uint64_t)el) >> 53);
   return (t - el + k) % q.cap;
 }
-// float f (0..27) of a gathered ring row into the sample buffers
+// float f (0..27) of a gathered ring row into the sample buffers: one store
+// to an address chosen by selects (a store per branch let the waitcnt pass,
+// its tracking lost across the branches, put a vmcnt(0) before each store, i.e.
+// wait for the previous store's acknowledgement)
 __device__ __forceinline__ void ring_scatter(const RingSample& q, int64_t b, int f, float v) {
-  if (f < 12) q.s[b * 12 + f] = v;
-  else if (f < 14) q.a[b * 2 + f - 12] = v;
-  else if (f == 14) q.r[b] = v;
-  else if (f < 27) q.s2[b * 12 + f - 15] = v;
-  else q.d[b] = v;
+  float* dst = f < 12 ? q.s + b * 12 + f
+               : f < 14 ? q.a + b * 2 + (f - 12)
+               : f == 14 ? q.r + b
+               : f < 27 ? q.s2 + b * 12 + (f - 15)
+               : q.d + b;
+  *dst = v;
 }
 
 }  // namespace skmlp
