@@ -174,10 +174,14 @@ __device__ __forceinline__ void step_advance(const StepRef& s, uint64_t base, ui
 // the slab streamed from HBM the tick takes 4.74 instead of 4.93 us
 // (profiles/r01x_act_nt_ab.jsonl, three alternating passes).
 __device__ __forceinline__ float2 load_action(const float2* p) {
+#ifdef SK_ACT_PLAIN  // A/B build only (multi-tick kernels: no gain, profiles/r04bc_act_nt_multi_ab.jsonl)
+  return *p;
+#else
   float2 v;
   v.x = __builtin_nontemporal_load(&p->x);
   v.y = __builtin_nontemporal_load(&p->y);
   return v;
+#endif
 }
 
 // ------------------------------------------------------------------ kernels
