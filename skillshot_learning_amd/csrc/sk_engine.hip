@@ -622,22 +622,105 @@ struct MultiLane {
 // order, so the next tick's state waited for the prefetched HBM loads anyway.
 // `packed` (wave-uniform): where the state lives now; `last`: the final tick
 // (its state goes to the exchange format).
+//
+// Round 5 (the K = 20 launch's fixed cost): the prologue
+// had waited on six serial scalar rounds (kernel-argument lines as the
+// scheduler reached them, the RNG step slot behind them) before its first
+// state load; now every argument line comes in one round (the kernel's
+// entry asm) and the step is formed only where a restart draws it
+// (multi_step).  The tick is split at its loads (multi_load: the raw
+// registers; multi_compute: decode and the rest).  Rotating the loop at
+// those loads (tick t + 1's loads at the end of tick t's body, the counts
+// summed in the last tick) measured slower (2.45-2.47 vs 2.38-2.42 us per
+// tick at K = 4,000; profiles/r05b_multi_prologue_ab.jsonl), as did the same
+// rotation in k_step_split_multi (8,192 games 1.68 vs 1.58 us), so the loop
+// keeps its loads at the top.
+struct MultiRaw {  // one tick's loads as issued, decoded at the tick's start
+  skb4i v[5];       // pos, rot, qpos, qrot, qcdage (packed form: R, Q, S in v[0..2])
+  skb2i m;          // misc
+  float2 act[2];    // both players' actions
+};
+
 template <int POL, bool PACK>
-__device__ __forceinline__ void multi_tick(const MultiArgs& a, const Cfg& c, __amdgpu_buffer_rsrc_t r,
-                                           __amdgpu_buffer_rsrc_t rp, MultiLane& L, WaveCtr& wc, int64_t t,
-                                           uint64_t step, int64_t slab, bool& packed, bool last) {
+__device__ __forceinline__ void multi_load(const MultiArgs& a, __amdgpu_buffer_rsrc_t r, __amdgpu_buffer_rsrc_t rp,
+                                           const MultiLane& L, int64_t slab, bool packed, MultiRaw& w) {
+  const uint32_t o16 = (uint32_t)L.ic * 16u, o8 = (uint32_t)L.ic * 8u;
+  if (PACK && packed) {
+    if constexpr (POL == 0) {
+      const skb4i* P = reinterpret_cast<const skb4i*>(a.pack);
+      w.v[0] = P[L.ic];
+      w.v[1] = P[a.n + L.ic];
+      w.v[2] = P[2 * a.n + L.ic];
+    } else {
+      const uint32_t plane = (uint32_t)a.n * 16u;
+      w.v[0] = __builtin_amdgcn_raw_buffer_load_b128(rp, o16, 0, 16);
+      w.v[1] = __builtin_amdgcn_raw_buffer_load_b128(rp, o16 + plane, 0, 16);
+      w.v[2] = __builtin_amdgcn_raw_buffer_load_b128(rp, o16 + 2u * plane, 0, 16);
+    }
+  } else if constexpr (POL == 0) {
+    w.v[0] = __builtin_bit_cast(skb4i, a.v.pos[L.ic]);
+    w.v[1] = __builtin_bit_cast(skb4i, a.v.rot[L.ic]);
+    w.v[2] = __builtin_bit_cast(skb4i, a.v.qpos[L.ic]);
+    w.v[3] = __builtin_bit_cast(skb4i, a.v.qrot[L.ic]);
+    w.v[4] = __builtin_bit_cast(skb4i, a.v.qcdage[L.ic]);
+    w.m = __builtin_bit_cast(skb2i, a.v.misc[L.ic]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) w.v[k] = __builtin_amdgcn_raw_buffer_load_b128(r, o16 + a.off[k], 0, 16);
+    w.m = __builtin_amdgcn_raw_buffer_load_b64(r, o8 + a.off[5], 0, 16);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  w.act[0] = load_action(a.actions + slab * 2 * a.n + L.ic);
+  w.act[1] = load_action(a.actions + slab * 2 * a.n + a.n + L.ic);
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <bool PACK>
+__device__ __forceinline__ void multi_decode(const MultiRaw& w, bool packed, Env& e) {
+  if (PACK && packed) {
+    const skb2d rr = __builtin_bit_cast(skb2d, w.v[0]), qr = __builtin_bit_cast(skb2d, w.v[1]);
+    e.rot[0] = rr.x; e.rot[1] = rr.y;
+    e.qrot[0] = qr.x; e.qrot[1] = qr.y;
+    const skb4i sb = w.v[2];
+    const unsigned s0 = (unsigned)sb.x, c0 = (unsigned)sb.y, s1 = (unsigned)sb.z, c1 = (unsigned)sb.w;
+    e.px[0] = s0 & 0xff; e.py[0] = (s0 >> 8) & 0xff; e.qx[0] = (s0 >> 16) & 0xff; e.qy[0] = s0 >> 24;
+    e.px[1] = s1 & 0xff; e.py[1] = (s1 >> 8) & 0xff; e.qx[1] = (s1 >> 16) & 0xff; e.qy[1] = s1 >> 24;
+    e.qcd[0] = (int)(signed char)(c0 & 0xff); e.qage[0] = (c0 >> 8) & 0xff;
+    e.qcd[1] = (int)(signed char)(c1 & 0xff); e.qage[1] = (c1 >> 8) & 0xff;
+    e.ticks = (int)(c0 >> 16);
+    const unsigned fl = c1 >> 16;
+    e.qvalid[0] = fl & 1; e.qvalid[1] = (fl >> 1) & 1; e.live = (fl >> 2) & 1; e.winner = (fl >> 3) & 3;
+  } else {
+    const skb4i p = w.v[0], q = w.v[2], ca = w.v[4];
+    const skb2d rr = __builtin_bit_cast(skb2d, w.v[1]), qr = __builtin_bit_cast(skb2d, w.v[3]);
+    decode_env(EnvRaw{make_int4(p.x, p.y, p.z, p.w), make_double2(rr.x, rr.y), make_int4(q.x, q.y, q.z, q.w),
+                      make_double2(qr.x, qr.y), make_int4(ca.x, ca.y, ca.z, ca.w), make_int2(w.m.x, w.m.y)},
+               e);
+  }
+}
+
+// The RNG step of a tick, step0 + tick, formed only where a draw needs it:
+// the empty asm keeps the sum (and the Philox products of it) from being
+// hoisted to the loop's head, where the wait for the step slot's load would
+// sit in front of every tick's compute.
+__device__ __forceinline__ uint64_t multi_step(uint64_t step0, int tick) {
+  asm volatile("" : "+v"(step0));
+  return step0 + (uint64_t)tick;
+}
+
+// the rest of the tick on the loaded state; `last`: the launch's final tick
+template <int POL, bool PACK>
+__device__ __forceinline__ void multi_compute(const MultiArgs& a, const Cfg& c, __amdgpu_buffer_rsrc_t r,
+                                              __amdgpu_buffer_rsrc_t rp, MultiLane& L, WaveCtr& wc, int64_t t,
+                                              uint64_t step0, int tick, const MultiRaw& w, bool& packed,
+                                              bool last) {
   Env e;
-  if (PACK && packed) load_env_pack<POL>(a, rp, L.ic, e);
-  else load_env_port<POL>(a, r, L.ic, e);
+  multi_decode<PACK>(w, packed, e);
+  const float2* acts = w.act;
   const double q_old0 = e.qrot[0], q_old1 = e.qrot[1];
-  __builtin_amdgcn_sched_barrier(0);
-  float2 acts[2];
-  acts[0] = load_action(a.actions + slab * 2 * a.n + L.ic);
-  acts[1] = load_action(a.actions + slab * 2 * a.n + a.n + L.ic);
-  __builtin_amdgcn_sched_barrier(0);
   U4 ru = {0u, 0u, 0u, 0u};
   if (L.early) {  // the restart's draw under the loads (k_step)
-    ru = draw4(a.seed, (uint64_t)(a.env_offset + L.i), step, 1u);
+    ru = draw4(a.seed, (uint64_t)(a.env_offset + L.i), multi_step(step0, tick), 1u);
     asm volatile("" : "+v"(ru.x), "+v"(ru.y), "+v"(ru.z), "+v"(ru.w));
   }
   __builtin_amdgcn_sched_barrier(0);
@@ -665,7 +748,7 @@ __device__ __forceinline__ void multi_tick(const MultiArgs& a, const Cfg& c, __a
   if (d && a.auto_reset) {
     if (a.random_positions) {
       if (L.early) reset_random_u(c, e, ru);
-      else reset_random(c, e, a.seed, (uint64_t)(a.env_offset + L.i), step);
+      else reset_random(c, e, a.seed, (uint64_t)(a.env_offset + L.i), multi_step(step0, tick));
     } else {
       reset_fixed(c, e);
     }
@@ -692,8 +775,8 @@ __device__ __forceinline__ void multi_tick(const MultiArgs& a, const Cfg& c, __a
 
 // Measurement build only (-DSK_TRACE_MULTI; tools/trace_multi.py): lane 0 of
 // every k_step_multi wave records s_memrealtime (100 MHz) at entry, after
-// each of the first 30 ticks and at exit into sk_multi_trace[wave][32]
-// (vector stores).
+// each of the first 29 ticks and at exit into sk_multi_trace[wave][32], and
+// its hardware slot (HW_ID, XCC_ID) in word 30 (vector stores).
 #ifdef SK_TRACE_MULTI
 __device__ unsigned long long* sk_multi_trace;
 extern "C" int skdiag_set_multi_trace(void* buf) {
@@ -764,33 +847,50 @@ __global__ void __launch_bounds__(BLK + (PF > 0 ? 64 : 0)) k_step_multi(MultiArg
     }
   }
   SK_MTS(0);
+#ifdef SK_TRACE_MULTI  // slot 30: where the wave runs (HW_ID | XCC_ID << 32)
+  if ((threadIdx.x & 63) == 0)
+    sk_multi_trace[((size_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * 32 + 30] =
+        (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
+        ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32);
+#endif
+  // every kernel-argument line the launch reads, fetched in ONE scalar round
+  // before anything else (the empty asm consumes a word of each 64-B line of
+  // MultiArgs; left to the scheduler, the lines came in three dependent rounds
+  // around tick 0's loads)
+  asm volatile("" ::"s"(a.n), "s"(a.out_stride), "s"(a.off[0]), "s"(a.off[5]), "s"(c.cdmax), "s"(early));
   MultiLane L;
   L.i = (int64_t)blockIdx.x * BLK + threadIdx.x;
   L.in = L.i < a.n;
   L.ic = L.in ? L.i : 0;
   L.early = a.random_positions && early;
   L.n_done = L.n_h1 = L.n_h2 = L.t_sum = 0;
-  WaveCtr wc = ctr_load<BLK>(a.ctr);
-  const uint64_t step0 = step_read(a.step);
-  step_advance(a.step, step0, (uint64_t)a.n_ticks);
   const __amdgpu_buffer_rsrc_t r = raw_rsrc(a.base), rp = raw_rsrc(a.pack);
   int64_t slab = a.slab0, so = a.out0;
   bool packed = false;  // every launch starts from (and ends in) the exchange format
-  for (int t = 0; t < a.n_ticks; ++t) {
+  // the counter slot and the RNG step slot load first (their values are
+  // needed at the launch's end, or only on a restart: multi_step), the step
+  // slot's advance at the launch's end (it had been a store in the prologue)
+  WaveCtr wc = ctr_load<BLK>(a.ctr);
+  const uint64_t step0 = step_read(a.step);
+  int t = 0;
+  do {  // n_ticks >= 1 (host-checked): every path to the counter store passes ctr_settle
+    MultiRaw w;
     if constexpr (PF > 0) __builtin_amdgcn_s_barrier();
-    multi_tick<POL, PACK>(a, c, r, rp, L, wc, so, step0 + (uint64_t)t, slab, packed, t + 1 == a.n_ticks);
+    multi_load<POL, PACK>(a, r, rp, L, slab, packed, w);
+    multi_compute<POL, PACK>(a, c, r, rp, L, wc, so, step0, t, w, packed, t + 1 == a.n_ticks);
+#ifdef SK_TRACE_MULTI
+    if (t < 29) SK_MTS(1 + t);
+#endif
     slab = slab + 1 == a.ring ? 0 : slab + 1;
     so = so + 1 == a.out_slabs ? 0 : so + 1;
-#ifdef SK_TRACE_MULTI
-    if (t < 30) SK_MTS(1 + t);
-#endif
-  }
+  } while (++t < a.n_ticks);
   if (a.ctr) {
     const unsigned c4[4] = {L.n_done, L.n_h1, L.n_h2, L.t_sum};
     uint64_t v[4];
     wave_sum4_u32(c4, v);
     ctr_store<BLK>(a.ctr, wc, v[0], v[1], v[2], v[3]);
   }
+  step_advance(a.step, step0, (uint64_t)a.n_ticks);
   SK_MTS(31);
 }
 

@@ -5,7 +5,8 @@
 
 Runs the bench's launch pattern (one warm-up launch, then timed launches of
 --ticks ticks on a 400-slab action ring) and reads the last launch's stamps
-(10 ns): per wave entry, end of ticks 0..29, exit.  Prints one JSON line:
+(10 ns): per wave entry, end of ticks 0..28, exit, and its hardware slot (XCC,
+SE, CU, SIMD: waves sharing a SIMD, their spans and exits).  Prints one JSON line:
 entry spread, per-tick medians and maxima over waves (tick 0 holds the cold
 start), the exit spread and the span first entry -> last exit."""
 import argparse
@@ -25,6 +26,7 @@ def main():
     p.add_argument("--envs", type=int, default=65536)
     p.add_argument("--ticks", type=int, default=20)
     p.add_argument("--launches", type=int, default=5)
+    p.add_argument("--dump", default="", help="save the last launch's raw stamps [waves][32] (.npy)")
     a = p.parse_args()
     from skillshot_learning_amd import VecSkillshotGame
     n, T = a.envs, a.ticks
@@ -52,13 +54,32 @@ def main():
         if k == 0:
             continue
         ts = buf.view(waves, 32).cpu().numpy().astype(np.int64)
+        if a.dump and k == a.launches - 1:
+            np.save(a.dump, ts)
         t0 = ts[:, 0].min()
         e = ts[:, 0] - t0
-        nt = min(T, 30)
+        nt = min(T, 29)
         ends = ts[:, 1:1 + nt] - t0
         per = np.diff(np.concatenate([ts[:, :1] - t0, ends], axis=1), axis=1) * 10 / 1e3  # us
         x = ts[:, 31] - t0
-        out.append(dict(entry_spread_us=float(e.max() - e.min()) * 0.01, entry_p50_us=float(np.median(e)) * 0.01,
+        hw = ts[:, 30].astype(np.uint64)
+        hwid, xcc = hw & np.uint64(0xffffffff), hw >> np.uint64(32)
+        simd = (hwid >> np.uint64(4)) & np.uint64(3)
+        cu = (hwid >> np.uint64(8)) & np.uint64(15)
+        sh = (hwid >> np.uint64(12)) & np.uint64(1)
+        se = (hwid >> np.uint64(13)) & np.uint64(7)
+        slot = (((xcc * np.uint64(8) + se) * np.uint64(2) + sh) * np.uint64(16) + cu) * np.uint64(4) + simd
+        _, inv, cnt = np.unique(slot, return_inverse=True, return_counts=True)
+        share = cnt[inv]  # waves of this launch on the same SIMD
+        cuslot = slot // np.uint64(4)
+        _, cinv, ccnt = np.unique(cuslot, return_inverse=True, return_counts=True)
+        span_w = (x - e) * 0.01
+        out.append(dict(simds_used=int(len(cnt)), waves_per_simd_hist={int(k): int((cnt == k).sum()) for k in np.unique(cnt)},
+                        cus_used=int(len(ccnt)), waves_per_cu_hist={int(k): int((ccnt == k).sum()) for k in np.unique(ccnt)},
+                        xcc_hist={int(k): int((xcc == k).sum()) for k in np.unique(xcc)},
+                        wave_span_us_by_share={int(k): round(float(np.median(span_w[share == k])), 3) for k in np.unique(share)},
+                        exit_us_by_share={int(k): round(float(np.max(x[share == k])) * 0.01, 3) for k in np.unique(share)},
+                        entry_spread_us=float(e.max() - e.min()) * 0.01, entry_p50_us=float(np.median(e)) * 0.01,
                         tick_p50_us=[round(float(v), 3) for v in np.median(per, axis=0)],
                         tick_max_us=[round(float(v), 3) for v in per.max(axis=0)],
                         last_tick_to_exit_p50_us=float(np.median(x - ends[:, -1])) * 0.01,
