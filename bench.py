@@ -394,7 +394,8 @@ def large_batch_rate(dev, args, rank, n=1 << 22, launches=60, ring=8):
     gbs = BYTES_PER_ENV_STEP * n / (us * 1e-6) / 1e9
     torch.cuda.empty_cache()
     return dict(envs_per_gpu=n, kernel="k_step (auto variant)", us_per_launch=us, env_steps_per_s_per_gpu=n / (us * 1e-6),
-                achieved_gbs=gbs, frac=gbs / HBM_PEAK_GBS,
+                achieved_gbs=gbs, frac=gbs / HBM_PEAK_GBS, clock="HIP events over the graph-replayed launches",
+                memory_level="hbm (369 MB of state, past the 256 MiB Infinity Cache)",
                 note="state 369 MB > Infinity Cache: the HBM-bound regime; reported beside, not as, the headline")
 
 
@@ -481,6 +482,9 @@ def full_contract_rate(dev, args, rank, n, ticks=2000):
                 env_steps_per_s_per_gpu=n / (us * 1e-6), wall_env_steps_per_s=n * ticks / el, episodes=counters,
                 roofline=dict(bound="hbm", achieved=gbs, peak=HBM_PEAK_GBS, unit="GB/s", frac=gbs / HBM_PEAK_GBS,
                               traffic=traffic, traffic_source=traffic_src or "not measured for this kernel yet",
+                              clock="HIP events on the launch stream (2,000 ticks)",
+                              memory_level="hbm (action slab in, obs / reward ring out, both past the Infinity "
+                                           "Cache) + Infinity Cache (the 5.8 MB of state, write-through every tick)",
                               bytes_per_env_step=BYTES_FULL_CONTRACT,
                               bytes="state 88 read + 88 written, actions 16, obs 96, reward 8, done 1"),
                 per_tick_launch=dict(kernel="k_step_split (one graph-replayed launch per tick)", us_per_tick=us1,
@@ -547,8 +551,10 @@ def learner_rate(envs, world, rank, ticks, batch=256, exploration="param_noise",
     # the fp32 parameter noise's variance GEMM runs on bf16 MFMA (DESIGN §7;
     # the mean GEMM, i.e. the actions' own arithmetic, is fp32)
     dtype = precision
-    if precision == "fp32" and exploration == "param_noise":
-        dtype = "fp32 (noise-variance GEMM on bf16 MFMA)"
+    if precision == "fp32":  # what the acting tile executes
+        dtype = ("fp32 (the acting tile's products from three-piece bf16 splits on bf16 MFMA, each within ~2^-25 "
+                 "relative of the fp32 product; the gradient kernels on f32 MFMA")
+        dtype += "; the noise-variance GEMM on bf16 MFMA)" if exploration == "param_noise" else ")"
     out = dict(envs_per_gpu=envs, total_envs=envs * world, n_gpus=world, ticks=n_ticks, batch_per_rank=batch,
                exploration=exploration, updates_per_tick=1, dtype=dtype, multi_rank=tg.multi_rank_mode,
                tick_mode=tg.mode, draw_order="reference (after the tick's insert)" if tg.mode == "sequential"
@@ -636,6 +642,12 @@ def reference_rule_rate(envs, exploration="param_noise", precision="fp32", fit_c
 
 
 ACTOR_FLOP_ROW = 72192   # 2 x (12*256 + 256*128 + 128*2) multiply-adds per row
+# what the fp32 acting tile executes per row (csrc/sk_learn32.hip gemm6,
+# csrc/sk_split.hpp): layers 1 (K padded 12 -> 16) and 2 as six bf16 MFMA
+# products of the split pieces, 2 x (16*256 + 256*128) x 6; with parameter
+# noise one more bf16 GEMM of the same shapes (the variance); layer 3 (128 ->
+# 2) is left out
+SPLIT_GEMM_ROW = 2 * (16 * 256 + 256 * 128)
 CRITIC_FLOP_ROW = 72448  # A16: 2 x (12*256 + 258*128 + 128*1)
 MFMA_PEAK_TF = {"fp32": 157.3, "bf16": 2500.0}  # MI355X_MICROARCH.md: f32 MFMA 157.3 TF; bf16 ~2.5 PF dense
 
@@ -720,16 +732,30 @@ def learner_roofline(L, tg, batch, precision, exploration, gpu_ms_per_tick, reps
             del g
             us = e0.elapsed_time(e1) * 1e3 / reps
             kern[name] = dict(us=us, flop=flop, tflops=flop / (us * 1e-6) / 1e12, kernels=names[name])
+    if precision == "fp32":  # the acting set executes on bf16 MFMA
+        k = kern["acting"]
+        ex = rows * SPLIT_GEMM_ROW * (6 + (1 if noise else 0))
+        k["executed"] = dict(pipe="bf16 MFMA (v_mfma_f32_32x32x16_bf16: fp32 products as six split-piece products"
+                                  + (", the noise variance once" if noise else "") + ")",
+                             flop=ex, tflops=ex / (k["us"] * 1e-6) / 1e12, peak=MFMA_PEAK_TF["bf16"],
+                             frac=ex / (k["us"] * 1e-6) / 1e12 / MFMA_PEAK_TF["bf16"])
     dom = max(kern, key=lambda k: kern[k]["us"])
     peak = MFMA_PEAK_TF[precision]
     tick_flop = sum(v["flop"] for v in kern.values())
-    return dict(bound="mfma", achieved=kern[dom]["tflops"], peak=peak, unit="TFLOP/s",
-                frac=kern[dom]["tflops"] / peak, traffic=None, kernel=names[dom], launch_set=dom,
-                kernel_us=kern[dom]["us"], kernels=kern, tick_flop=tick_flop,
-                tick_tflops=tick_flop / (gpu_ms_per_tick * 1e-3) / 1e12,
-                tick_frac=tick_flop / (gpu_ms_per_tick * 1e-3) / 1e12 / peak,
-                note="the reference-order tick's three launch sets, each timed with HIP events over a graph of "
-                     f"{reps}; FLOP per row from SURVEY §8(a)/(d)")
+    out = dict(bound="mfma", achieved=kern[dom]["tflops"], peak=peak, unit="TFLOP/s",
+               frac=kern[dom]["tflops"] / peak, traffic=None, kernel=names[dom], launch_set=dom,
+               kernel_us=kern[dom]["us"], kernels=kern, tick_flop=tick_flop,
+               tick_tflops=tick_flop / (gpu_ms_per_tick * 1e-3) / 1e12,
+               tick_frac=tick_flop / (gpu_ms_per_tick * 1e-3) / 1e12 / peak,
+               clock=f"HIP events over one graph replay of {reps} launch sets on the leg's stream",
+               memory_level="n/a (MFMA-bound launch sets; the nets and minibatch sit in L2)",
+               note="the reference-order tick's three launch sets, each timed with HIP events over a graph of "
+                    f"{reps}; FLOP per row from SURVEY §8(a)/(d)")
+    ex = kern[dom].get("executed")
+    if ex is not None:  # frac against the pipe the dominant set runs on, the fp32-equivalent beside
+        out["fp32_equivalent"] = dict(achieved=out["achieved"], peak=peak, frac=out["frac"], flop=kern[dom]["flop"])
+        out.update(achieved=ex["tflops"], peak=ex["peak"], frac=ex["frac"], executed_pipe=ex["pipe"])
+    return out
 
 
 def _log(msg):
@@ -889,7 +915,8 @@ def per_tick_rate(dev, args, n):
     gbs = BYTES_PER_ENV_STEP * n / (us * 1e-6) / 1e9
     return dict(kernel="k_step (one graph-replayed launch per tick; the round-2 headline)", ticks=k2,
                 us_per_tick=us, env_steps_per_s_per_gpu=n / (us * 1e-6), achieved_gbs=gbs,
-                frac=gbs / HBM_PEAK_GBS)
+                frac=gbs / HBM_PEAK_GBS, clock="HIP events over the graph-replayed launches",
+                memory_level="Infinity Cache (state) + hbm (action slab), as the headline")
 
 
 def l2_rate(dev, args, n):
@@ -907,6 +934,7 @@ def l2_rate(dev, args, n):
     gbs = BYTES_PER_ENV_STEP * n / (us * 1e-6) / 1e9
     return dict(kernel="k_step_multi<0> (plain state port)", ticks=k2, us_per_tick=us,
                 env_steps_per_s_per_gpu=n / (us * 1e-6), contract_gbs=gbs,
+                clock="HIP events on the launch stream", memory_level="L2 (state) + hbm (action slab)",
                 note="state stores and reloads stay in the XCD's L2 (PMC: profiles/"
                      "traffic_k_step_multi_pol0.json), so this is not an HBM-roofline figure")
 
@@ -980,6 +1008,7 @@ def main():
     # duration / ticks per launch).
     kern_ms = ev_ms / K
     achieved = BYTES_PER_ENV_STEP * n / (kern_ms * 1e-3) / 1e9
+    achieved_wall = BYTES_PER_ENV_STEP * n / (elapsed / K) / 1e9  # per GPU, on the clock of `value`
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
@@ -1137,10 +1166,17 @@ def main():
                 "traffic_source": "profiles/traffic_k_step_multi.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
                                   "passes, per tick; not this run)",
                 "kernel": "k_step_multi<1> (write-through state port)",
-                "note": "bound labelled hbm as SURVEY 8(d) prescribes (193 B per env-step against 8 TB/s); at "
-                        "65,536 games the 5.8 MB of state crosses the L2 / fabric boundary every tick "
-                        "(write-through) but is served by the 256 MiB Infinity Cache, and only the per-tick "
-                        "1 MiB action slab streams from HBM: the HBM-bound regime is large_batch (369 MB state)",
+                "clock": "HIP events: the launch stream's span of the timed region / K (rocprofv3 --stats: the "
+                         "average launch duration / ticks per launch); frac_wall beside it on the wall clock "
+                         "of `value`",
+                "achieved_wall": achieved_wall,
+                "frac_wall": achieved_wall / HBM_PEAK_GBS,
+                "memory_level": "Infinity Cache / fabric: the 5.8 MB of state crosses the L2 / fabric boundary "
+                                "every tick (write-through) and is served by the 256 MiB Infinity Cache; only the "
+                                "per-tick 1 MiB action slab streams from HBM",
+                "hbm_evidence": "large_batch (369 MB of state, past the Infinity Cache)",
+                "note": "bound labelled hbm as SURVEY 8(d) prescribes (193 B per env-step against 8 TB/s); the "
+                        "genuinely HBM-bound regime is large_batch",
                 "bytes_per_env_step": BYTES_PER_ENV_STEP,
                 "kernel_us_per_tick": kern_ms * 1e3,
             },

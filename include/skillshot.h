@@ -259,7 +259,9 @@ int sk_env_act_step(sk_env* env, const float* actor_flat, const void* actor_pack
  * rewards[t] (float[n_ticks][2][N]; reward_kind as sk_env_step's); rows of
  * ticks a game did not play are undefined.  lengths int32[N] = the
  * ticks each game played.  N % 4 == 0; the step counter and the noise call
- * number advance by n_ticks; no episode counters.  GPU backend only. */
+ * number advance by max_i lengths[i], the iterations of the per-tick loop
+ * this replaces (a second one-workgroup launch on the stream reduces the
+ * lengths); no episode counters.  GPU backend only. */
 int sk_env_act_episode(sk_env* env, const float* actor_flat, const void* actor_pack, float* states, float* actions,
                        float* rewards, int32_t* lengths, int32_t n_ticks, float noise_sd, float action_sd,
                        uint64_t noise_seed, uint64_t* call_counter, int32_t reward_kind, int32_t tick_limit,

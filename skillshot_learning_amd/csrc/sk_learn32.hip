@@ -1774,8 +1774,11 @@ __global__ void __launch_bounds__(kFwdThreads, SK_ACT_WAVES) k_act_step32(const 
 // states[t + 1] and the reward to rewards[t] ([2][N]); lengths[i] = the
 // ticks game i played.  The rows t < lengths[i] of both players are the
 // episode's (s, a, r) for models_fit (:320-357); later rows are undefined.  The step counter and the
-// noise call number advance by n_ticks (the launch's last workgroup stores
-// the call number, grouped arrival).
+// noise call number advance by the ticks the per-tick loop would have run,
+// max_i lengths[i] (it had been n_ticks, so the next epoch's
+// restarts and noise diverged from the loop's whenever every game ended
+// before the limit): k_episode_finish, one workgroup launched after this
+// kernel on the same stream, reduces the lengths and stores both.
 struct EpisodeArgs {
   float* states;
   float* actions;
@@ -1802,7 +1805,6 @@ __global__ void __launch_bounds__(kFwdThreads, SK_EPISODE_WAVES) k_act_episode32
   sk_counters* const slot = nullptr;
   const bool draws = (NOISE || action_sd != 0.f) && call_ctr;
   const uint64_t call0 = draws ? call_ctr[0] : 0;
-  const uint64_t step0 = sk::step_read(a.step);
   const int64_t n = a.n, gt = 2 * g0 + lane, gi = gt >> 1;  // wave 0: lane -> (game, player)
   if (w0 && lane < 32 && (lane & 1) == 0 && gi < n) ep.lengths[gi] = 0;
   for (int t = 0; t < ep.n_ticks; ++t) {
@@ -1839,10 +1841,26 @@ __global__ void __launch_bounds__(kFwdThreads, SK_EPISODE_WAVES) k_act_episode32
     }
     __syncthreads();  // this tick's observations are the next tick's acting rows (this workgroup's own stores)
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) a.step.slots[1 - a.step.parity] = step0 + (uint64_t)ep.n_ticks;
-  if (draws) {
-    __syncthreads();
-    advance_call32(call_ctr, call0 + (uint64_t)ep.n_ticks, gridDim.x);
+}
+
+// The episode's counter advance (see k_act_episode32): T = max lengths[i]
+// (the per-tick loop's iterations: it runs while any game lives), then the
+// step slot step0 + T and, when the episode drew, the call number call0 + T.
+// Both start values are read here: the episode kernel leaves the counters
+// alone, and this launch follows it on the stream.
+__global__ void __launch_bounds__(256) k_episode_finish(const int32_t* __restrict__ lengths, int64_t n,
+                                                        sk::StepRef step, uint64_t* __restrict__ call_ctr) {
+  __shared__ int red[4];
+  int m = 0;
+  for (int64_t i = threadIdx.x; i < n; i += 256) m = max(m, lengths[i]);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = max(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint64_t T = (uint64_t)max(max(red[0], red[1]), max(red[2], red[3]));
+    step.slots[1 - step.parity] = step.slots[step.parity] + T;
+    if (call_ctr) call_ctr[0] = call_ctr[0] + T;
   }
 }
 
@@ -2241,6 +2259,9 @@ int sk_launch_act_episode32(const float* aflat, const void* apack, float sd, flo
     k_act_episode32<true><<<G, kFwdThreads, lds, st>>>(aflat, pk, sd, action_sd, seed, call_ctr, a, c, ep);
   else
     k_act_episode32<false><<<G, kFwdThreads, lds, st>>>(aflat, pk, 0.f, action_sd, seed, call_ctr, a, c, ep);
+  if (hipGetLastError() != hipSuccess) return SK_EHIP;
+  const bool draws = (sd != 0.f || action_sd != 0.f) && call_ctr;
+  k_episode_finish<<<1, 256, 0, st>>>(lengths, a.n, a.step, draws ? call_ctr : nullptr);
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
 }
 

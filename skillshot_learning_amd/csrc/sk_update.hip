@@ -1068,10 +1068,13 @@ __global__ void __launch_bounds__(kAdamParams * kAdamSlices) k_adam_flat(const f
     }
     for (; k < GG; k += kAdamSlices) acc[0] += src[(int64_t)k * ld + pp];
   }
+  // adjacent pairs first, ((a0 + a1) + (a2 + a3)) + ((a4 + a5) + (a6 + a7)):
+  // the round-3 summation order, so Adam results stay bit-identical to it
+  // (round 4's halving tree summed (a0 + a4) + ... first)
 #pragma unroll
-  for (int w = kAdamInflight / 2; w >= 1; w /= 2)
+  for (int s = 1; s < kAdamInflight; s *= 2)
 #pragma unroll
-    for (int j = 0; j < w; ++j) acc[j] += acc[j + w];
+    for (int j = 0; j + s < kAdamInflight; j += 2 * s) acc[j] += acc[j + s];
   const float part = acc[0];
   if (slice > 0) red[slice - 1][lane] = part;
   __syncthreads();

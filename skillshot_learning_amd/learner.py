@@ -614,15 +614,18 @@ class DDPG:
             R = torch.empty(M * b, dtype=torch.float32, device=dev)
             g = torch.cuda.CUDAGraph()
             torch.cuda.current_stream(dev).synchronize()
-            with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                for m in range(M):
-                    sl = slice(m * b, (m + 1) * b)
-                    if critic:
-                        self.critic_step(S[sl], A[sl], R[sl])
-                    else:
-                        self.model_actor_fit_step(S[sl])
-            cache[key] = (g, S, A, R)
-        g, S, A, R = cache[key]
+            # the captured steps' losses go to slots of their own (every
+            # replay rewrites them), not to the eager steps' history
+            with self._fused.private_loss_slots(M) as losses:
+                with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                    for m in range(M):
+                        sl = slice(m * b, (m + 1) * b)
+                        if critic:
+                            self.critic_step(S[sl], A[sl], R[sl])
+                        else:
+                            self.model_actor_fit_step(S[sl])
+            cache[key] = (g, S, A, R, losses)
+        g, S, A, R, _ = cache[key]
         for j in range(chunks):
             lo = b + j * M * b
             S.copy_(states[lo:lo + M * b])
@@ -956,15 +959,42 @@ class SkillshotLearner:
         final ticks and winners."""
         g = self.game_environment
         mode = self.exploration
-        ep = g.act_episode(self.actor_kernel, obs, noise_sd=self.param_noise_sd if mode == "param_noise" else 0.0,
-                           action_sd=self.action_noise_sd if mode == "action_noise" else 0.0, reward=reward,
-                           out=getattr(self, "_episode_bufs", None))
-        self._episode_bufs = ep
-        lengths = ep["lengths"].long()
-        T = int(lengths.max()) if self.n_envs else 0
-        keep = (torch.arange(T, device=self.device)[:, None] < lengths[None, :])[:, None, :].expand(T, 2, self.n_envs)
-        self.models_fit(ep["states"][:T][keep], ep["actions"][:T][keep], ep["rewards"][:T][keep])
+        kw = dict(noise_sd=self.param_noise_sd if mode == "param_noise" else 0.0,
+                  action_sd=self.action_noise_sd if mode == "action_noise" else 0.0, reward=reward)
+        # chunks of C ticks (ADVICE r04): the launch's buffers hold C + 1
+        # state slabs (120 B per game-tick with actions and rewards), so a
+        # large batch does not allocate tick_limit of them up front; each
+        # chunk's played rows are compacted, in the loop's (tick, player,
+        # game) order, and a chunk that ends short of C ends the episode
+        C = self.episode_chunk_ticks()
+        S, A, R = [], [], []
+        while True:
+            ep = g.act_episode(self.actor_kernel, obs, n_ticks=C, out=getattr(self, "_episode_bufs", None), **kw)
+            self._episode_bufs = ep
+            lengths = ep["lengths"].long()
+            T = int(lengths.max()) if self.n_envs else 0
+            self.actor_kernel.calls += T  # the host mirror of the device call number
+            keep = (torch.arange(T, device=self.device)[:, None] < lengths[None, :])[:, None, :].expand(
+                T, 2, self.n_envs)
+            S.append(ep["states"][:T][keep])
+            A.append(ep["actions"][:T][keep])
+            R.append(ep["rewards"][:T][keep])
+            if T < C:
+                break
+            obs = ep["states"][C]
+        self.models_fit(torch.cat(S), torch.cat(A), torch.cat(R))
         return g.ticks.clone(), g.winner_id.clone()
+
+    def episode_chunk_ticks(self, share=0.125):
+        """ticks per episode launch: the tick limit, or fewer where the
+        launch's buffers (120 B per game-tick) would pass `share` of the
+        device's free memory; SK_EPISODE_CHUNK overrides"""
+        env = os.environ.get("SK_EPISODE_CHUNK")
+        if env:
+            return max(1, int(env))
+        free, _ = torch.cuda.mem_get_info(self.device)
+        per_tick = 120 * max(1, self.n_envs)
+        return int(max(1, min(self.game_environment.tick_limit, (share * free) // per_tick)))
 
     # ------------------------------------------------------------ on-disk formats (persist.py)
     def save_actor_critic_models(self, epochs):

@@ -16,6 +16,7 @@ torch path step the same numbers and `state_dict()` sees the kernel's Adam
 moments.  Multi-rank: the gradient is written flat, all-reduced (mean) over
 RCCL, then applied (two Adam launches).
 """
+import contextlib
 import ctypes
 
 import torch
@@ -173,6 +174,7 @@ class FusedUpdate:
         self.stats = torch.zeros(2, dtype=torch.float32, device=dev)
         self.loss_hist = torch.zeros(2, self.LOSS_HIST, dtype=torch.float32, device=dev)
         self._li = [0, 0]
+        self._loss_private = None
         self._partials = {}
         self.grad_flat = None
         # the actor forward kernel's weight pack (ActorKernel.buf), written by
@@ -236,9 +238,28 @@ class FusedUpdate:
         self._pack_flat(jobs)
 
     def _loss_slot(self, k):
+        if self._loss_private is not None:  # a captured graph's own slots (private_loss_slots)
+            buf, idx = self._loss_private
+            i = idx[k]
+            idx[k] = (i + 1) % buf.shape[1]
+            return buf[k, i]
         i = self._li[k]
         self._li[k] = (i + 1) % self.LOSS_HIST
         return self.loss_hist[k, i]
+
+    @contextlib.contextmanager
+    def private_loss_slots(self, n):
+        """Steps recorded inside this context write their losses into a
+        buffer of their own ([2][n], yielded; the caller keeps it with the
+        graph), not into loss_hist: a captured graph rewrites its slots on
+        every replay, which must not overwrite a loss an eager step returned
+        (the LOSS_HIST promise)."""
+        buf = torch.zeros(2, n, dtype=torch.float32, device=self.dev)
+        self._loss_private = (buf, [0, 0])
+        try:
+            yield buf
+        finally:
+            self._loss_private = None
 
     def _packs(self, critic):
         """the packs the Adam launch of a step keeps current"""

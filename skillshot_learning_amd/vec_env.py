@@ -354,7 +354,10 @@ class VecSkillshotGame:
         tick.  start_obs [2, N, 12]: the observation of the current state.
         Returns dict(states [T+1, 2, N, 12], actions [T, 2, N, 2], rewards
         [T, 2, N], lengths int32 [N]); rows t < lengths[i] are game i's
-        episode.  T = n_ticks (default: the tick limit)."""
+        episode.  T = n_ticks (default: the tick limit); a game still live
+        after T ticks continues in the next call (from states[T]).  The
+        device step counter and the actor's noise call number advance by
+        max(lengths), the ticks the per-tick loop would have run."""
         T = int(self.tick_limit if n_ticks is None else n_ticks)
         o = out or {}
         st = o.get("states")
@@ -370,7 +373,6 @@ class VecSkillshotGame:
         if ln is None:
             ln = torch.empty(self.n, dtype=torch.int32, device=self.device)
         st[0].copy_(start_obs.reshape(2, self.n, 12))
-        actor.calls += T
         pack = actor.ensure_pack()
         check(self._L.sk_env_act_episode(self._h, _ptr(actor.flat), _ptr(pack), _ptr(st), _ptr(ac), _ptr(rw),
                                          _ptr(ln), T, float(noise_sd), float(action_sd), actor.seed,

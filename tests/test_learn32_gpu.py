@@ -291,8 +291,10 @@ def test_act_episode_equals_per_tick_loop(mods, monkeypatch, exploration, n):
     the per-tick loop (the 32-row actor forward, then sk_env_step without
     auto-reset, one launch each per tick): every played row's state, action
     and reward bit for bit, each game's length, and the final ticks / winner
-    of every game at its end; the noise call number advances by n_ticks
-    (1,028 games: the last workgroup holds 4 of its 16)"""
+    of every game at its end; the launch asks for more ticks than the limit
+    allows, so every game ends before them, and the noise call number and
+    the step counter advance by the loop's iterations, max(lengths), not by
+    n_ticks (1,028 games: the last workgroup holds 4 of its 16)"""
     learner, _ = mods
     monkeypatch.setenv("SK_FWD16", "0")
     limit = 150
@@ -305,10 +307,15 @@ def test_act_episode_equals_per_tick_loop(mods, monkeypatch, exploration, n):
     c0 = int(k._ctr[0])
     sd = L.param_noise_sd if exploration == "param_noise" else 0.0
     asd = L.action_noise_sd if exploration == "action_noise" else 0.0
-    ep = g.act_episode(k, obs, noise_sd=sd, action_sd=asd)
+    step0 = g.step_counter
+    ep = g.act_episode(k, obs, n_ticks=limit + 50, noise_sd=sd, action_sd=asd)
     torch.cuda.synchronize()
-    assert int(k._ctr[0]) == c0 + limit
     got_len = ep["lengths"].long()
+    T = int(got_len.max())
+    assert T <= limit < limit + 50
+    assert int(k._ctr[0]) == c0 + (T if sd or asd else 0)
+    got_step = g.step_counter
+    assert got_step == step0 + T
     end_ticks, end_winner = g.ticks.clone(), g.winner_id.clone()
     # the per-tick loop from the same start and call number
     g.load_state_dict(st0)
@@ -336,15 +343,24 @@ def test_act_episode_equals_per_tick_loop(mods, monkeypatch, exploration, n):
             break
     assert torch.equal(got_len, length)
     assert torch.equal(end_ticks, want_ticks) and torch.equal(end_winner, want_winner)
+    torch.cuda.synchronize()
+    assert int(k._ctr[0]) == c0 + (T if sd or asd else 0) and g.step_counter == got_step  # the loop's advance
     assert int(got_len.max()) > 1 and int((got_len < limit).sum()) > 0  # both endings occur
 
 
-def test_model_train_on_device_equals_loop(mods, monkeypatch):
+@pytest.mark.parametrize("chunk", ["", "7"])
+def test_model_train_on_device_equals_loop(mods, monkeypatch, chunk):
     """model_train with the episodes in one launch (default) and with the
     per-tick loop (SK_EPISODE_KERNEL=0): the same nets after two epochs, bit
-    for bit (same rows in the same order, the same shuffle)"""
+    for bit (same rows in the same order, the same shuffle, the next epoch's
+    restarts and noise from the same counters).  chunk "7": the episodes in
+    launches of 7 ticks (SK_EPISODE_CHUNK), each continuing from the last;
+    the final one ends short of its 7, i.e. every game ends before the
+    launch's tick count"""
     learner, _ = mods
     monkeypatch.setenv("SK_FWD16", "0")
+    if chunk:
+        monkeypatch.setenv("SK_EPISODE_CHUNK", chunk)
     nets = []
     for flag in ("1", "0"):
         monkeypatch.setenv("SK_EPISODE_KERNEL", flag)
@@ -381,3 +397,27 @@ def test_models_fit_graph_chunks_equal_eager(mods, monkeypatch, precision):
                    [d._fused.sa.m.clone(), d._fused.sc.v.clone()])
     for x, y in zip(*out):
         assert torch.equal(x, y)
+
+
+def test_models_fit_graph_losses_private(mods):
+    """the captured models_fit chunks write their steps' losses into a buffer
+    of their own: the eager steps' history (loss_hist, whose
+    returned scalars stay valid for LOSS_HIST further steps) holds only the
+    eager steps' losses.  1,200 rows at batch 16: 75 minibatches per pass =
+    the first eager, one captured chunk of 64, ten eager"""
+    learner, _ = mods
+    g = torch.Generator(device="cuda").manual_seed(6)
+    s = torch.rand(1200, 12, device="cuda", generator=g)
+    a = torch.rand(1200, 2, device="cuda", generator=g) * 2 - 1
+    r = torch.randn(1200, device="cuda", generator=g)
+    d = learner.DDPG("cuda", seed=4, fused_update=True, precision="fp32")
+    fu = d._fused
+    d.models_fit(s, a, r)
+    torch.cuda.synchronize()
+    hist = fu.loss_hist.cpu()
+    assert fu._li == [11, 11]
+    assert bool((hist[:, :11] != 0).all()) and bool((hist[:, 11:] == 0).all())
+    assert len(d._fit_graphs) == 2
+    for (_, _, critic), v in d._fit_graphs.items():  # row 0: the critic steps' losses, row 1: the actor's
+        k = 0 if critic else 1
+        assert bool((v[4][k] != 0).all()) and bool((v[4][1 - k] == 0).all())
