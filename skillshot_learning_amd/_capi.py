@@ -16,7 +16,7 @@ from . import build as _build
 
 SK_OK, SK_EINVAL, SK_EHIP, SK_ENOMEM, SK_ENODEV = 0, -1, -2, -3, -4
 SK_REWARD_LOOKING, SK_REWARD_SIMPLE = 0, 1
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 # every symbol include/skillshot.h declares
 EXPORTS = (
@@ -36,6 +36,7 @@ EXPORTS = (
     "sk_update_partials_f32", "sk_actor_forward_f32", "sk_actor_split_pack_bytes", "sk_actor_split_pack_f32", "sk_critic_grad_f32", "sk_critic_grad_f32_sampled",
     "sk_critic_grad_bootstrap_sampled", "sk_actor_grad_f32", "sk_actor_grad_f32_step",
     "sk_critic_grad_f32_sampled_step", "sk_critic_grad_f32_step", "sk_replay_sample_excl",
+    "sk_fit_xbuf_bytes", "sk_fit_critic_f32", "sk_fit_actor_f32",
 )
 
 
@@ -174,6 +175,9 @@ def load(build_if_missing=True):
         "sk_update_scratch_f32": ([i64, P], ctypes.c_int64),
         "sk_adam_flat_sliced": ([P, i32, P, i32, i32, P, P, i32, P, P, P, P, f32, f32, f32, f32, P, f32, P, f32, P, P,
                                  P, P], ctypes.c_int),
+        "sk_fit_xbuf_bytes": ([], ctypes.c_size_t),
+        "sk_fit_critic_f32": ([P, P, P, P, i32, P, P, P, i32, u64, P, f32, f32, f32, f32, P, P, P, P, P], ctypes.c_int),
+        "sk_fit_actor_f32": ([P, P, P, P, i32, P, P, i32, f32, f32, f32, f32, P, P, P, P], ctypes.c_int),
     }
     for name, (argt, rest) in sig.items():
         fn = getattr(L, name)

@@ -20,6 +20,7 @@ LIB_PATH = os.environ.get("SK_LIB_PATH") or os.path.join(LIB_DIR, "libskillshot.
 SOURCES = [os.path.join(HERE, "csrc", "sk_engine.hip"), os.path.join(HERE, "csrc", "sk_actor.hip"),
            os.path.join(HERE, "csrc", "sk_critic.hip"), os.path.join(HERE, "csrc", "sk_update.hip"),
            os.path.join(HERE, "csrc", "sk_replay.hip"), os.path.join(HERE, "csrc", "sk_learn32.hip"),
+           os.path.join(HERE, "csrc", "sk_fit.hip"),
            os.path.join(HERE, "csrc", "sk_host.cpp")]
 DEPS = SOURCES + [os.path.join(HERE, "csrc", f) for f in os.listdir(os.path.join(HERE, "csrc"))
                   if f.endswith((".hpp", ".h", ".cpp"))] + [os.path.join(ROOT, "include", "skillshot.h")]

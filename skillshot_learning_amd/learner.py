@@ -574,6 +574,21 @@ class DDPG:
         fu = self._fused
         if fu is not None:
             fu.soft_update_in_adam = False
+        # the resident passes (csrc/sk_fit.hip; fp32, one rank, batch 16):
+        # every full minibatch of a pass in launches that hold the net on
+        # chip; SK_FIT_RESIDENT=0 keeps the three-launch steps
+        resident = (fu is not None and fu.f32 and states.is_cuda and not self.multi() and b == fu.FIT_ROWS and
+                    os.environ.get("SK_FIT_RESIDENT", "1") != "0")
+        if resident:
+            try:
+                done = fu.fit_critic(states, actions, rewards) * b
+                for k in range(done, n, b):  # the partial last minibatch
+                    self.critic_step(states[k:k + b], actions[k:k + b], rewards[k:k + b])
+                self._actor_pass(states, b, n)
+                fu.fit_check()
+            finally:
+                fu.soft_update_in_adam = True
+            return
         # graph-replayed chunks of FIT_CHUNK minibatches (the fused kernels,
         # one rank): the same launches on the same rows, staged into fixed
         # buffers, without ~0.1 ms of host time per minibatch; the first
@@ -599,6 +614,28 @@ class DDPG:
         finally:
             if fu is not None:
                 fu.soft_update_in_adam = True
+
+    def _actor_pass(self, states, b, n):
+        """models_fit's actor pass (:436-443) on the fused kernels: resident
+        launches (sk_fit_actor_f32) for every full minibatch and the partial
+        last one eager; SK_FIT_RESIDENT=critic keeps the three-launch steps
+        for this pass (the first minibatch eager, captured chunks of
+        FIT_CHUNK, the rest eager)"""
+        if os.environ.get("SK_FIT_RESIDENT", "1") != "critic":
+            done = self._fused.fit_actor(states) * b
+            for k in range(done, n, b):
+                self.model_actor_fit_step(states[k:k + b])
+            return
+        graph = self._fused is not None and states.is_cuda and not self.multi() and n >= 2 * b and \
+            os.environ.get("SK_FIT_GRAPH", "1") != "0"
+        M = self.FIT_CHUNK
+        chunks = (n // b - 1) // M if graph else 0
+        for k in range(0, n, b):
+            if chunks and k == b:
+                self._fit_chunks(states, None, None, b, M, chunks, critic=False)
+            if chunks and b <= k < b + chunks * M * b:
+                continue
+            self.model_actor_fit_step(states[k:k + b])
 
     FIT_CHUNK = 64  # minibatches per captured models_fit graph
 

@@ -329,6 +329,80 @@ class FusedUpdate:
                    packs=self._packs(critic=True))
         return loss
 
+    # ------------------------------------------------------------ models_fit, resident
+    FIT_ROWS = 16              # the resident kernels' minibatch (SkillshotLearner.py:434 batch_size=16)
+    FIT_STEPS_PER_LAUNCH = 4096  # minibatch steps per resident launch (~20 ms; a progress-sized unit)
+
+    def _fit_buffers(self):
+        if getattr(self, "fit_x", None) is None:
+            nb = int(self.L.sk_fit_xbuf_bytes())
+            self.fit_x = torch.zeros(nb // 8, dtype=torch.int64, device=self.dev)  # granule slots, zeroed once
+            self.fit_epoch = torch.zeros(1, dtype=torch.int64, device=self.dev)     # their epoch, across launches
+            self.fit_timeout = torch.zeros(1, dtype=torch.int32, device=self.dev)
+
+    @torch.no_grad()
+    def fit_critic(self, s, a, y, losses=None):
+        """models_fit's critic pass (SkillshotLearner.py:419-434) over the
+        full 16-row minibatches of the rows (s, a, y) in the order given:
+        each minibatch one Adam step on MSE(Q(s, a), y) with Dropout active,
+        in resident launches of up to FIT_STEPS_PER_LAUNCH steps
+        (sk_fit_critic_f32, csrc/sk_fit.hip: the net and its moments held
+        on chip by 8 workgroups).  Equal up to fp32 summation order to one
+        critic_step per minibatch (no soft update: models_fit has no target
+        nets).  Returns the number of minibatch steps taken; rows past the
+        last full minibatch are the caller's.  losses: float [steps] (each
+        step's loss) or None.  Call fit_check() before trusting the net."""
+        if not self.f32:
+            raise ValueError("the resident fit runs the fp32 kernels")
+        b = self.FIT_ROWS
+        n = int(s.shape[0]) // b
+        if n == 0:
+            return 0
+        s, a, y = s.float().contiguous(), a.float().contiguous(), y.float().contiguous()
+        self._fit_buffers()
+        st = self.sc
+        for k0 in range(0, n, self.FIT_STEPS_PER_LAUNCH):
+            m = min(self.FIT_STEPS_PER_LAUNCH, n - k0)
+            r0 = k0 * b
+            _capi.check(self.L.sk_fit_critic_f32(
+                _p(self.fc), _p(st.m), _p(st.v), _p(st.steps), st.steps.numel(), _p(s[r0:]), _p(a[r0:]), _p(y[r0:]),
+                m, self.seed, _p(self.calls), st.lr, st.b1, st.b2, st.eps, _p(self.fit_x), _p(self.fit_epoch),
+                _p(self.fit_timeout), _p(losses[k0:]) if losses is not None else None, self._stream()))
+        return n
+
+    @torch.no_grad()
+    def fit_actor(self, s):
+        """models_fit's actor pass (SkillshotLearner.py:386-417, 436-443) over
+        the full 16-row minibatches of s: each one Adam step of the actor on
+        -sum Q(s, mu(s)) with the critic as it stands (inference), in
+        resident launches (sk_fit_actor_f32); then the actor's split pack is
+        rewritten once (the three-launch steps rewrite it in every Adam
+        launch).  Returns the number of minibatch steps taken."""
+        if not self.f32:
+            raise ValueError("the resident fit runs the fp32 kernels")
+        b = self.FIT_ROWS
+        n = int(s.shape[0]) // b
+        if n == 0:
+            return 0
+        s = s.float().contiguous()
+        self._fit_buffers()
+        st = self.sa
+        for k0 in range(0, n, self.FIT_STEPS_PER_LAUNCH):
+            m = min(self.FIT_STEPS_PER_LAUNCH, n - k0)
+            _capi.check(self.L.sk_fit_actor_f32(
+                _p(self.fa), _p(st.m), _p(st.v), _p(st.steps), st.steps.numel(), _p(self.fc), _p(s[k0 * b:]), m,
+                st.lr, st.b1, st.b2, st.eps, _p(self.fit_x), _p(self.fit_epoch), _p(self.fit_timeout),
+                self._stream()))
+        if self.split_pack is not None:
+            _capi.check(self.L.sk_actor_split_pack_f32(_p(self.fa), _p(self.split_pack), self._stream()))
+        return n
+
+    def fit_check(self):
+        """raise if a resident fit launch lost an in-launch exchange (host sync)"""
+        t = getattr(self, "fit_timeout", None)
+        if t is not None and int(t.item()):
+            raise SkillshotError("resident models_fit: an in-launch exchange timed out; the nets are undefined")
+
     @torch.no_grad()
     def critic_step_sampled(self, ring, batch, gamma=0.0, row_offset=0, global_batch=None, total=None, exclude=0,
                             step_job=None):

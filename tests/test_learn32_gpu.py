@@ -376,11 +376,13 @@ def test_model_train_on_device_equals_loop(mods, monkeypatch, chunk):
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 def test_models_fit_graph_chunks_equal_eager(mods, monkeypatch, precision):
-    """models_fit with its minibatches replayed as captured chunks (default)
+    """models_fit's three-launch steps (SK_FIT_RESIDENT=0) with its
+    minibatches replayed as captured chunks (default)
     against one eager launch set per minibatch (SK_FIT_GRAPH=0): the same
     nets and Adam moments bit for bit (3,000 rows: the first minibatch
     eager, two chunks of 64, the remainder and the partial last batch eager)"""
     learner, _ = mods
+    monkeypatch.setenv("SK_FIT_RESIDENT", "0")
     g = torch.Generator(device="cuda").manual_seed(3)
     rows = 3000
     s = torch.rand(rows, 12, device="cuda", generator=g)
@@ -399,7 +401,7 @@ def test_models_fit_graph_chunks_equal_eager(mods, monkeypatch, precision):
         assert torch.equal(x, y)
 
 
-def test_models_fit_graph_losses_private(mods):
+def test_models_fit_graph_losses_private(mods, monkeypatch):
     """the captured models_fit chunks write their steps' losses into a buffer
     of their own: the eager steps' history (loss_hist, whose
     returned scalars stay valid for LOSS_HIST further steps) holds only the
@@ -410,6 +412,7 @@ def test_models_fit_graph_losses_private(mods):
     s = torch.rand(1200, 12, device="cuda", generator=g)
     a = torch.rand(1200, 2, device="cuda", generator=g) * 2 - 1
     r = torch.randn(1200, device="cuda", generator=g)
+    monkeypatch.setenv("SK_FIT_RESIDENT", "0")  # the three-launch steps and their captured chunks
     d = learner.DDPG("cuda", seed=4, fused_update=True, precision="fp32")
     fu = d._fused
     d.models_fit(s, a, r)
@@ -421,3 +424,122 @@ def test_models_fit_graph_losses_private(mods):
     for (_, _, critic), v in d._fit_graphs.items():  # row 0: the critic steps' losses, row 1: the actor's
         k = 0 if critic else 1
         assert bool((v[4][k] != 0).all()) and bool((v[4][1 - k] == 0).all())
+
+
+def _fit_rows(n, seed):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    s = torch.rand(n, 12, device="cuda", generator=g) * torch.tensor(
+        [1, 1, 1, 1, 9.8, 1, 1, 1, 1, 9.8, 1, 1.0], device="cuda")
+    return s, torch.rand(n, 2, device="cuda", generator=g) * 2 - 1, torch.randn(n, device="cuda", generator=g) * 0.5
+
+
+@pytest.mark.parametrize("p", ["8", "4"])
+def test_fit_critic_resident_equals_eager_and_keras(mods, monkeypatch, p):
+    """models_fit's critic pass in resident launches (sk_fit_critic_f32,
+    csrc/sk_fit.hip: the net split over P workgroups by layer-2 input
+    columns, three in-launch exchanges per step) against one three-launch
+    critic_step per minibatch (sk_critic_grad_f32 + sk_adam_flat) and the
+    fp64 Keras restatement, over 96 minibatch steps in two launches (64 +
+    32): parameters within 1e-5, Adam moments, step counts, the Dropout call
+    number and the per-step losses"""
+    learner, kr = mods
+    from skillshot_learning_amd import rng
+    monkeypatch.setenv("SK_FIT_P", p)
+    n = 96
+    s, a, y = _fit_rows(16 * n, 7)
+    dr = _ddpg(learner, seed=3, scale=2.0)
+    de = _ddpg(learner, seed=3, scale=2.0)
+    fr, fe = dr._fused, de._fused
+    C0 = kr.from_module(de.model_critic)
+    call0 = int(de.drop_calls)
+    losses = torch.zeros(n, device="cuda")
+    fr.FIT_STEPS_PER_LAUNCH = 64
+    assert fr.fit_critic(s, a, y, losses=losses) == n
+    fr.fit_check()
+    want_loss = []
+    for k in range(n):
+        sl = slice(16 * k, 16 * k + 16)
+        want_loss.append(float(de.critic_step(s[sl], a[sl], y[sl])))
+    torch.cuda.synchronize()
+    assert int(dr.drop_calls) == int(de.drop_calls) == call0 + n
+    assert torch.equal(fr.sc.steps, fe.sc.steps)
+    got, want = fr.fc.double().cpu().numpy(), fe.fc.double().cpu().numpy()
+    assert np.abs(got - want).max() <= PARAM_ABS, np.abs(got - want).max()
+    for x, z in ((fr.sc.m, fe.sc.m), (fr.sc.v, fe.sc.v)):
+        assert (x - z).abs().max().item() <= 1e-4 * z.abs().max().item()
+    assert np.allclose(losses.cpu().numpy(), want_loss, rtol=1e-4, atol=1e-6)
+    # the fp64 Keras restatement, step by step (Dropout keys of each step's call)
+    C = C0
+    oc = kr.Adam(C)
+    sn, an, yn = _np(s), _np(a), _np(y)
+    for k in range(n):
+        sl = slice(16 * k, 16 * k + 16)
+        keep = rng.dropout_keep(de.drop_seed, call0 + k, 0, 16).double().numpy()
+        gc, _ = kr.critic_grads(C, sn[sl], an[sl], yn[sl], keep)
+        C = oc.step(C, gc)
+    ref = np.concatenate([C[name].reshape(-1) for name, _ in de.model_critic.named_parameters()])
+    assert np.abs(got - ref).max() <= PARAM_ABS, np.abs(got - ref).max()
+
+
+def test_models_fit_resident_equals_three_launch(mods, monkeypatch):
+    """models_fit with the resident critic pass (default) and with the
+    three-launch steps (SK_FIT_RESIDENT=0): the same nets within 1e-5 after a
+    pass over 1,613 rows (100 full minibatches and a partial one), and the
+    same Dropout call number and Adam step counts"""
+    learner, _ = mods
+    s, a, y = _fit_rows(1613, 9)
+    out = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SK_FIT_RESIDENT", flag)
+        d = learner.DDPG("cuda", seed=4, fused_update=True, precision="fp32")
+        d.models_fit(s, a, y)
+        torch.cuda.synchronize()
+        out.append((d._fused.fc.clone(), d._fused.fa.clone(), int(d.drop_calls), d._fused.sc.steps.clone(),
+                    d._fused.sa.steps.clone()))
+    (c1, a1, k1, s1, t1), (c0, a0, k0, s0, t0) = out
+    assert k1 == k0 and torch.equal(s1, s0) and torch.equal(t1, t0)
+    assert (c1 - c0).abs().max().item() <= PARAM_ABS
+    assert (a1 - a0).abs().max().item() <= PARAM_ABS
+
+
+def test_fit_actor_resident_equals_eager_and_keras(mods):
+    """models_fit's actor pass in resident launches (sk_fit_actor_f32: the
+    actor and the frozen critic split over 8 workgroups by layer-2 input
+    columns, four in-launch exchanges per step) against one three-launch
+    model_actor_fit_step per minibatch and the fp64 Keras restatement, over
+    96 minibatch steps in two launches: parameters within 1e-5, Adam step
+    counts equal, the critic untouched, the split pack rewritten"""
+    learner, kr = mods
+    n = 96
+    s, _, _ = _fit_rows(16 * n, 11)
+    dr = _ddpg(learner, seed=5, scale=2.0)
+    de = _ddpg(learner, seed=5, scale=2.0)
+    fr, fe = dr._fused, de._fused
+    A0, C0 = kr.from_module(de.model_actor), kr.from_module(de.model_critic)
+    crit0 = fr.fc.clone()
+    from skillshot_learning_amd.actor_kernel import ActorKernel32
+    k = ActorKernel32(dr.model_actor, seed=3)
+    fr.split_pack = k.ensure_pack()
+    fr.FIT_STEPS_PER_LAUNCH = 64
+    assert fr.fit_actor(s) == n
+    fr.fit_check()
+    for j in range(n):
+        de.model_actor_fit_step(s[16 * j:16 * j + 16])
+    torch.cuda.synchronize()
+    assert torch.equal(fr.fc, crit0)
+    assert torch.equal(fr.sa.steps, fe.sa.steps)
+    got, want = fr.fa.double().cpu().numpy(), fe.fa.double().cpu().numpy()
+    assert np.abs(got - want).max() <= PARAM_ABS, np.abs(got - want).max()
+    A = A0
+    oa = kr.Adam(A)
+    sn = _np(s)
+    for j in range(n):
+        ga, _ = kr.actor_grads(A, C0, sn[16 * j:16 * j + 16])
+        A = oa.step(A, ga)
+    ref = np.concatenate([A[name].reshape(-1) for name, _ in de.model_actor.named_parameters()])
+    assert np.abs(got - ref).max() <= PARAM_ABS, np.abs(got - ref).max()
+    # the acting kernel reads the rewritten pack: its forward equals a fresh pack's
+    x = _obs(64, 12)
+    out = k(x)
+    k2 = ActorKernel32(dr.model_actor, seed=3)
+    assert torch.equal(out, k2(x))

@@ -1,0 +1,203 @@
+// The in-launch exchange floor of the resident models_fit step (VERDICT r04
+// item 6: measure an XCD-local seam before building the persistent update).
+// P workgroups (256 threads; blockIdx % S == 0 of a P*S grid works, the rest
+// leave: S = 8 puts them on one XCD under round-robin placement, S = 1
+// spreads them) run `rounds` steps of exchanges and nothing else.  Two
+// layer-2 partitions of the 16-row batch step:
+//   row partition (v1: which 1 / 2 / 4, 8-byte granules, one load in flight
+//   per lane per pass):
+//     A  all-gather of 16 x 256 activations (publish 512, read P x 512),
+//     Q  all-reduce of 16 partials (publish 16, read P x 16),
+//     D  reduce-scatter of the 16 x 256 dX2 partials (publish 4,096, read 4,096);
+//   column partition (v2: which 8 / 16 / 32, granule PAIRS in 16-byte sc1
+//   stores and loads, every load of a pass in flight before the tag checks):
+//     R  reduce-scatter of the 16 x 128 layer-2 partials (publish and read
+//        P x 256 granules: a 16 x 16 slice per owner),
+//     Q2 the all-reduce of 16 partials,
+//     G  all-gather of 16 x 128 gradients (publish 256, read P x 256).
+// Built standalone (tools/seam_bench.py --build, into ab_run/); the granule
+// primitives are csrc/sk_xchg.hpp's.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../skillshot_learning_amd/csrc/sk_xchg.hpp"
+
+using skx::gu64;
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ bool sweep(gu64* base, int n, unsigned epoch, float& acc, unsigned* tmo) {
+  for (unsigned spins = 0;; ++spins) {
+    bool ok = true;
+    float s = 0.f;
+    for (int i = threadIdx.x; i < n; i += 256) {
+      const unsigned long long x = skx::peek(base + i);
+      s += __uint_as_float((unsigned)x);
+      ok &= (unsigned)(x >> 32) == epoch;
+    }
+    if (__all(ok)) {
+      acc += s;
+      return true;
+    }
+    if (spins >= skx::kSpinLimit) {
+      if ((threadIdx.x & 63) == 0) atomicMax(tmo, 1u);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+__device__ __forceinline__ bool sweep_rs(gu64* base, int P, int w, int gd, unsigned epoch, float& acc, unsigned* tmo) {
+  for (unsigned spins = 0;; ++spins) {
+    bool ok = true;
+    float s = 0.f;
+    for (int i = threadIdx.x; i < P * gd; i += 256) {
+      const int src = i / gd, j = i - src * gd;
+      const unsigned long long x = skx::peek(base + ((size_t)src * P + w) * gd + j);
+      s += __uint_as_float((unsigned)x);
+      ok &= (unsigned)(x >> 32) == epoch;
+    }
+    if (__all(ok)) {
+      acc += s;
+      return true;
+    }
+    if (spins >= skx::kSpinLimit) {
+      if ((threadIdx.x & 63) == 0) atomicMax(tmo, 1u);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// ---- v2: granule pairs, 16-byte sc1 accesses through one buffer resource
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, -1, 0x00020000);
+}
+__device__ __forceinline__ void put2(__amdgpu_buffer_rsrc_t r, uint32_t byte_off, unsigned epoch, float a, float b) {
+  const u4v v = {__float_as_uint(a), epoch, __float_as_uint(b), epoch};
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, byte_off, 0, 16);  // aux 16: sc1
+}
+// N pairs per lane at byte offsets off[k]; every load issued, then the checks
+template <int N>
+__device__ __forceinline__ bool get2(__amdgpu_buffer_rsrc_t r, const uint32_t (&off)[N], unsigned epoch, float (&v)[2 * N],
+                                     unsigned* tmo) {
+  for (unsigned spins = 0;; ++spins) {
+    u4v x[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) x[k] = __builtin_amdgcn_raw_buffer_load_b128(r, off[k], 0, 16);
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      v[2 * k] = __uint_as_float(x[k].x);
+      v[2 * k + 1] = __uint_as_float(x[k].z);
+      ok &= (x[k].y == epoch) & (x[k].w == epoch);
+    }
+    if (__all(ok)) return true;
+    if (spins >= skx::kSpinLimit) {
+      if ((threadIdx.x & 63) == 0) atomicMax(tmo, 1u);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+template <int P>
+__device__ void rounds_v2(unsigned long long* xbuf, unsigned* tmo, int w, int rounds, unsigned epoch0, int which,
+                          float& acc) {
+  // per buffer: R [P src][P dst][256], Q [P][16], G [P][256] granules
+  constexpr int nR = P * P * 256, nQ = P * 16, nG = P * 256, nB = nR + nQ + nG;
+  const __amdgpu_buffer_rsrc_t rs = rsrc_of(xbuf);
+  const int t = threadIdx.x;
+  for (int r = 0; r < rounds; ++r) {
+    const uint32_t b0 = (uint32_t)((r & 1) * nB) * 8u;
+    const unsigned e = epoch0 + 3u * (unsigned)r;
+    if (which & 8) {  // R: publish P slices of 256 (128 pairs each): P / 2 pairs per lane
+      static_assert(P % 2 == 0, "");
+#pragma unroll
+      for (int k = 0; k < P / 2; ++k) {
+        const int pr = t + 256 * k;  // pair index over [P dst][128 pairs]
+        put2(rs, b0 + ((uint32_t)w * P * 256 + 2 * pr) * 8u, e + 1, 1.f, 2.f);
+      }
+      uint32_t off[P / 2];
+#pragma unroll
+      for (int k = 0; k < P / 2; ++k) {
+        const int pr = t + 256 * k, src = pr / 128, j = pr - 128 * src;
+        off[k] = b0 + ((uint32_t)(src * P + w) * 256 + 2 * j) * 8u;
+      }
+      float v[P];
+      if (!get2<P / 2>(rs, off, e + 1, v, tmo)) return;
+#pragma unroll
+      for (int k = 0; k < P; ++k) acc += v[k];
+    }
+    if (which & 16) {  // Q2: 16 granules, read P x 16
+      if (t < 8) put2(rs, b0 + ((uint32_t)nR + w * 16 + 2 * t) * 8u, e + 2, 1.f, 1.f);
+      if (t < P * 8) {
+        uint32_t off[1] = {b0 + ((uint32_t)nR + 2 * t) * 8u};
+        float v[2];
+        if (!get2<1>(rs, off, e + 2, v, tmo)) return;
+        acc += v[0] + v[1];
+      }
+    }
+    if (which & 32) {  // G: publish 256 (128 pairs: lanes < 128), read P x 256 (P / 2 pairs per lane)
+      if (t < 128) put2(rs, b0 + ((uint32_t)nR + nQ + w * 256 + 2 * t) * 8u, e + 3, 3.f, 4.f);
+      uint32_t off[P / 2];
+#pragma unroll
+      for (int k = 0; k < P / 2; ++k) off[k] = b0 + ((uint32_t)nR + nQ + 2 * (t + 256 * k)) * 8u;
+      float v[P];
+      if (!get2<P / 2>(rs, off, e + 3, v, tmo)) return;
+#pragma unroll
+      for (int k = 0; k < P; ++k) acc += v[k];
+    }
+    __syncthreads();
+  }
+}
+
+extern "C" __global__ void __launch_bounds__(256) k_seam(unsigned long long* xbuf, unsigned* tmo, unsigned* xcc,
+                                                         float* sink, int P, int S, int rounds, unsigned epoch0,
+                                                         int which) {
+  if (blockIdx.x % S) return;
+  const int w = blockIdx.x / S;
+  if (w >= P) return;
+  if (threadIdx.x == 0) xcc[w] = __builtin_amdgcn_s_getreg(20 | (31 << 11));
+  float acc = 0.f;
+  if (which >= 8) {
+    if (P == 2) rounds_v2<2>(xbuf, tmo, w, rounds, epoch0, which, acc);
+    else if (P == 4) rounds_v2<4>(xbuf, tmo, w, rounds, epoch0, which, acc);
+    else if (P == 8) rounds_v2<8>(xbuf, tmo, w, rounds, epoch0, which, acc);
+    else if (P == 16) rounds_v2<16>(xbuf, tmo, w, rounds, epoch0, which, acc);
+    if (acc == 123.456f) sink[0] = acc;
+    return;
+  }
+  gu64* X = skx::g64(xbuf);
+  const size_t nA = (size_t)P * 512, nQ = (size_t)P * 16, nD = (size_t)P * 4096;
+  for (int r = 0; r < rounds; ++r) {
+    gu64* b = X + (size_t)(r & 1) * (nA + nQ + nD);
+    gu64* A = b;
+    gu64* Q = b + nA;
+    gu64* D = Q + nQ;
+    const unsigned e = epoch0 + 3u * (unsigned)r;
+    if (which & 1) {
+      for (int i = threadIdx.x; i < 512; i += 256) skx::put(A + (size_t)w * 512 + i, e + 1, (float)i);
+      if (!sweep(A, P * 512, e + 1, acc, tmo)) break;
+    }
+    if (which & 2) {
+      if (threadIdx.x < 16) skx::put(Q + (size_t)w * 16 + threadIdx.x, e + 2, 1.f);
+      if (!sweep(Q, P * 16, e + 2, acc, tmo)) break;
+    }
+    if (which & 4) {
+      const int gd = 16 * (256 / P);
+      for (int i = threadIdx.x; i < P * gd; i += 256) skx::put(D + (size_t)w * P * gd + i, e + 3, 0.5f);
+      if (!sweep_rs(D, P, w, gd, e + 3, acc, tmo)) break;
+    }
+    __syncthreads();
+  }
+  if (acc == 123.456f) sink[0] = acc;  // keep the reads live
+}
+
+extern "C" int seam_launch(unsigned long long* xbuf, unsigned* tmo, unsigned* xcc, float* sink, int P, int S,
+                           int rounds, unsigned epoch0, int which, void* stream) {
+  if (P < 1 || P > 16 || S < 1 || (256 % P)) return -1;
+  if (which >= 8 && P != 2 && P != 4 && P != 8 && P != 16) return -1;
+  hipLaunchKernelGGL(k_seam, dim3(P * S), dim3(256), 0, (hipStream_t)stream, xbuf, tmo, xcc, (float*)sink, P, S,
+                     rounds, epoch0, which);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}

@@ -1,0 +1,59 @@
+"""Phase timeline of the resident models_fit kernels from the -DSK_TRACE_FIT
+build (tools/build_variant.sh ab_run/trace_fit.so -DSK_TRACE_FIT): lane 0 of
+wave 0 of every workgroup stamps 11 points of steps 64..95; prints, per
+kernel, the median duration of each phase over steps and workgroups, the
+median step and the spread of the step boundaries across workgroups.
+
+    SK_LIB_PATH=$PWD/ab_run/trace_fit.so python tools/trace_fit.py"""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+NAMES = {"critic": ["L1", "P1 publish", "R gather", "Q", "G publish", "unit Adam", "G gather", "dh1 GEMM",
+                    "dW2 GEMM + Adam", "dW1 + Adam"],
+         "actor": ["L1 x2", "P1 publish x2", "R gather", "Q1 (a)", "Q2 (dQ/da)", "G publish + unit Adam",
+                   "G gather", "dh1 GEMM", "dW2 GEMM + Adam", "dW1 + Adam"]}
+
+
+def main():
+    from skillshot_learning_amd import learner
+    dev = torch.device("cuda", 0)
+    d = learner.DDPG("cuda", seed=0, fused_update=True, precision="fp32")
+    fu = d._fused
+    fu.soft_update_in_adam = False
+    L = fu.L
+    L.skdiag_set_fit_trace.argtypes = [ctypes.c_void_p]
+    buf = torch.zeros(8 * 32 * 12, dtype=torch.int64, device=dev)
+    assert L.skdiag_set_fit_trace(ctypes.c_void_p(buf.data_ptr())) == 0
+    n = 256
+    g = torch.Generator(device=dev).manual_seed(1)
+    S = torch.rand(16 * n, 12, device=dev, generator=g)
+    A = torch.rand(16 * n, 2, device=dev, generator=g) * 2 - 1
+    R = torch.randn(16 * n, device=dev, generator=g)
+    fu.FIT_STEPS_PER_LAUNCH = n
+    out = {}
+    for kind, fn in (("critic", lambda: fu.fit_critic(S, A, R)), ("actor", lambda: fu.fit_actor(S))):
+        fn()
+        buf.zero_()
+        fn()
+        torch.cuda.synchronize()
+        fu.fit_check()
+        ts = buf.view(8, 32, 12).cpu().numpy().astype(np.int64)
+        ph = np.diff(ts[:, :, :11], axis=2) * 0.01  # us: phases 0..9
+        step = (ts[:, 1:, 0] - ts[:, :-1, 0]) * 0.01
+        out[kind] = dict(step_us_p50=round(float(np.median(step)), 3),
+                         phases_us_p50={nm: round(float(np.median(ph[:, :, i])), 3) for i, nm in enumerate(NAMES[kind])},
+                         phases_us_max={nm: round(float(np.max(np.median(ph[:, :, i], axis=1))), 3)
+                                        for i, nm in enumerate(NAMES[kind])},
+                         step_start_spread_us_p50=round(float(np.median(ts[:, :, 0].max(0) - ts[:, :, 0].min(0))) * 0.01, 3))
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
