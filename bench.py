@@ -571,15 +571,16 @@ def learner_rate(envs, world, rank, ticks, batch=256, exploration="param_noise",
     return out
 
 
-def reference_rule_rate(envs, exploration="param_noise", precision="fp32", fit_chunks=20):
+def reference_rule_rate(envs, exploration="param_noise", precision="fp32", fit_chunks=20, fit_steps=8192):
     """The reference's own training rule at the metric's size (VERDICT r03
     item 5; SkillshotLearner.model_train :289-361): one epoch = every game
     plays its episode from a random start (the actor fixed, fresh noise per
     tick) — one sk_env_act_episode launch — then models_fit on all played
     rows: shuffle, critic one pass at batch 16, actor one pass at batch 16.
     The collection is timed whole (HIP events and wall); the fit's 10^7-odd
-    sequential minibatch steps are timed over `fit_chunks` captured chunks of
-    64 per pass and the epoch's fit time projected from that rate."""
+    sequential minibatch steps are timed over `fit_steps` resident steps per
+    pass (the three-launch chunks beside them) and the epoch's fit time
+    projected from that rate."""
     from skillshot_learning_amd.learner import SkillshotLearner
     L = SkillshotLearner(n_envs=envs, seed=0, exploration=exploration, tick_limit=2000, precision=precision)
     g = L.game_environment
@@ -606,13 +607,29 @@ def reference_rule_rate(envs, exploration="param_noise", precision="fp32", fit_c
     keep = (torch.arange(T, device=L.device)[:, None] < lengths[None, :])[:, None, :].expand(T, 2, envs)
     S, A, R = ep["states"][:T][keep], ep["actions"][:T][keep], ep["rewards"][:T][keep]
     rows = S.shape[0]
-    # the fit's rate: fit_chunks captured chunks of 64 minibatches per pass
+    # the fit's rate: the resident passes (sk_fit_critic_f32 / sk_fit_actor_f32,
+    # models_fit's default path) over `fit_steps` minibatches each, HIP events;
+    # the round-4 path (captured chunks of 64 three-launch steps) beside it
     d = L.ddpg
+    fu = d._fused
     b, M = d.model_param_batch_size, d.FIT_CHUNK
-    d._fused.soft_update_in_adam = False
+    n_fit = min(fit_steps, rows // b)
+    fu.soft_update_in_adam = False
     try:
-        d.critic_step(S[:b], A[:b], R[:b])
-        d.model_actor_fit_step(S[:b])
+        fu.fit_critic(S[:b * 64], A[:b * 64], R[:b * 64])
+        fu.fit_actor(S[:b * 64])
+        fu.fit_check()
+        torch.cuda.synchronize()
+        ev3 = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        ev3[0].record(st)
+        fu.fit_critic(S[:b * n_fit], A[:b * n_fit], R[:b * n_fit])
+        ev3[1].record(st)
+        fu.fit_actor(S[:b * n_fit])
+        ev3[2].record(st)
+        torch.cuda.synchronize()
+        fu.fit_check()
+        critic_us = ev3[0].elapsed_time(ev3[1]) * 1e3 / n_fit
+        actor_us = ev3[1].elapsed_time(ev3[2]) * 1e3 / n_fit
         d._fit_chunks(S, A, R, b, M, 1, critic=True)
         d._fit_chunks(S, A, R, b, M, 1, critic=False)
         torch.cuda.synchronize()
@@ -622,19 +639,25 @@ def reference_rule_rate(envs, exploration="param_noise", precision="fp32", fit_c
         torch.cuda.synchronize()
         fit_s = time.perf_counter() - f0
     finally:
-        d._fused.soft_update_in_adam = True
-    steps = 2 * fit_chunks * M
-    step_us = fit_s * 1e6 / steps
-    fit_epoch_s = 2 * ((rows + b - 1) // b) * step_us * 1e-6
+        fu.soft_update_in_adam = True
+    steps_per_pass = (rows + b - 1) // b
+    step_us = (critic_us + actor_us) / 2
+    fit_epoch_s = steps_per_pass * (critic_us + actor_us) * 1e-6
+    three_us = fit_s * 1e6 / (2 * fit_chunks * M)
     out = dict(envs=envs, exploration=exploration, dtype=precision, episode_ticks_max=T, env_steps_played=played,
                mean_episode=played / envs, rows=rows,
                collection=dict(kernel="k_act_episode32 (sk_env_act_episode: the whole episode in one launch)",
                                gpu_s=ev, wall_s=wall, env_steps_per_s=played / wall,
                                gpu_us_per_tick=ev * 1e6 / T),
-               fit=dict(batch=b, minibatch_steps_timed=steps, us_per_minibatch_step=step_us,
-                        steps_per_epoch=2 * ((rows + b - 1) // b), projected_epoch_fit_s=fit_epoch_s,
+               fit=dict(batch=b, kernel="k_fit_critic / k_fit_actor (resident: 8 workgroups, one launch per "
+                                        "pass chunk of up to %d minibatches)" % fu.FIT_STEPS_PER_LAUNCH,
+                        minibatch_steps_timed=2 * n_fit, us_per_critic_step=critic_us, us_per_actor_step=actor_us,
+                        us_per_minibatch_step=step_us, steps_per_epoch=2 * steps_per_pass,
+                        projected_epoch_fit_s=fit_epoch_s,
+                        three_launch=dict(minibatch_steps_timed=2 * fit_chunks * M, us_per_minibatch_step=three_us,
+                                          projected_epoch_fit_s=2 * steps_per_pass * three_us * 1e-6),
                         note="sequential SGD at batch 16 as the reference's models_fit: the epoch's fit is "
-                             "projected from the timed chunks (captured graphs of 64 fused minibatch steps)"),
+                             "projected from the timed resident passes over the epoch's first rows"),
                projected_epoch_s=wall + fit_epoch_s)
     del L, ep, S, A, R
     torch.cuda.empty_cache()

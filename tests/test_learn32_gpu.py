@@ -433,18 +433,19 @@ def _fit_rows(n, seed):
     return s, torch.rand(n, 2, device="cuda", generator=g) * 2 - 1, torch.randn(n, device="cuda", generator=g) * 0.5
 
 
-@pytest.mark.parametrize("p", ["8", "4"])
-def test_fit_critic_resident_equals_eager_and_keras(mods, monkeypatch, p):
+@pytest.mark.parametrize("xcd", ["1", "0"])
+def test_fit_critic_resident_equals_eager_and_keras(mods, monkeypatch, xcd):
     """models_fit's critic pass in resident launches (sk_fit_critic_f32,
-    csrc/sk_fit.hip: the net split over P workgroups by layer-2 input
-    columns, three in-launch exchanges per step) against one three-launch
+    csrc/sk_fit.hip: the net split over 8 workgroups by layer-2 input
+    columns, three in-launch exchanges per step; on one XCD and spread over
+    the XCDs, SK_FIT_XCD) against one three-launch
     critic_step per minibatch (sk_critic_grad_f32 + sk_adam_flat) and the
     fp64 Keras restatement, over 96 minibatch steps in two launches (64 +
     32): parameters within 1e-5, Adam moments, step counts, the Dropout call
     number and the per-step losses"""
     learner, kr = mods
     from skillshot_learning_amd import rng
-    monkeypatch.setenv("SK_FIT_P", p)
+    monkeypatch.setenv("SK_FIT_XCD", xcd)
     n = 96
     s, a, y = _fit_rows(16 * n, 7)
     dr = _ddpg(learner, seed=3, scale=2.0)

@@ -15,10 +15,10 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-NAMES = {"critic": ["L1", "P1 publish", "R gather", "Q", "G publish", "unit Adam", "G gather", "dh1 GEMM",
-                    "dW2 GEMM + Adam", "dW1 + Adam"],
-         "actor": ["L1 x2", "P1 publish x2", "R gather", "Q1 (a)", "Q2 (dQ/da)", "G publish + unit Adam",
-                   "G gather", "dh1 GEMM", "dW2 GEMM + Adam", "dW1 + Adam"]}
+NAMES = {"critic": ["L1 + Dropout", "P1 publish", "R sum + H publish", "H gather", "q + dz2", "unit Adam",
+                    "dh1 GEMM", "dW1 + Adam", "dW2 GEMM + Adam", "-", "to the next step"],
+         "actor": ["L1 x2", "P1 publish x2", "R sums + H publish", "H gather", "a, dQ/da, dz2", "unit Adam",
+                   "dh1 GEMM", "dW1 + Adam", "dW2 GEMM + Adam", "-", "to the next step"]}
 
 
 def main():
@@ -46,6 +46,10 @@ def main():
         fu.fit_check()
         ts = buf.view(8, 32, 12).cpu().numpy().astype(np.int64)
         ph = np.diff(ts[:, :, :11], axis=2) * 0.01  # us: phases 0..9
+        tail = np.zeros_like(ph[:, :, :1])
+        tail[:, :-1, 0] = (ts[:, 1:, 0] - ts[:, :-1, 10]) * 0.01  # stamp 10 to the next step's 0
+        tail[:, -1, 0] = tail[:, -2, 0]
+        ph = np.concatenate([ph, tail], axis=2)
         step = (ts[:, 1:, 0] - ts[:, :-1, 0]) * 0.01
         out[kind] = dict(step_us_p50=round(float(np.median(step)), 3),
                          phases_us_p50={nm: round(float(np.median(ph[:, :, i])), 3) for i, nm in enumerate(NAMES[kind])},
