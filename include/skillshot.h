@@ -706,12 +706,15 @@ int sk_fit_critic_f32(float* critic_flat, float* adam_m, float* adam_v, float* s
  * mu(s)) with the critic (critic_flat, unchanged) at inference, in ONE launch
  * of 8 workgroups.  Equal up to fp32 summation order to n_minibatches
  * sk_actor_grad_f32 + sk_adam_flat steps (tests: 1e-5); step_counters as
- * sk_fit_critic_f32's; the same xbuf / epoch / timeout.  The actor's packed
- * copies (sk_actor_split_pack_f32) are NOT rewritten: repack after the pass.
- * GPU backend only. */
+ * sk_fit_critic_f32's; the same xbuf / epoch / timeout.  zbuf: float
+ * [16 n_minibatches][128] device scratch, overwritten (the frozen critic's
+ * layer-2 pre-activations of every row, computed by a first launch).  The
+ * actor's packed copies (sk_actor_split_pack_f32) are NOT rewritten: repack
+ * after the pass.  GPU backend only. */
 int sk_fit_actor_f32(float* actor_flat, float* adam_m, float* adam_v, float* step_counters, int32_t n_steps,
                      const float* critic_flat, const float* states, int32_t n_minibatches, float lr, float beta1,
-                     float beta2, float eps, void* xbuf, uint64_t* epoch, uint32_t* timeout, void* stream);
+                     float beta2, float eps, void* xbuf, uint64_t* epoch, uint32_t* timeout, float* zbuf,
+                     void* stream);
 
 #ifdef __cplusplus
 }

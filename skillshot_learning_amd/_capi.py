@@ -177,7 +177,7 @@ def load(build_if_missing=True):
                                  P, P], ctypes.c_int),
         "sk_fit_xbuf_bytes": ([], ctypes.c_size_t),
         "sk_fit_critic_f32": ([P, P, P, P, i32, P, P, P, i32, u64, P, f32, f32, f32, f32, P, P, P, P, P], ctypes.c_int),
-        "sk_fit_actor_f32": ([P, P, P, P, i32, P, P, i32, f32, f32, f32, f32, P, P, P, P], ctypes.c_int),
+        "sk_fit_actor_f32": ([P, P, P, P, i32, P, P, i32, f32, f32, f32, f32, P, P, P, P, P], ctypes.c_int),
     }
     for name, (argt, rest) in sig.items():
         fn = getattr(L, name)

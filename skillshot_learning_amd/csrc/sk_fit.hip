@@ -154,8 +154,6 @@ __device__ __forceinline__ float sum16(float v) {
   v += dpp<0x141>(v);
   return v + dpp<0x140>(v);
 }
-// the sum of v and the neighbouring lane's (lane ^ 1)
-__device__ __forceinline__ float sum2(float v) { return v + dpp<0xB1>(v); }
 
 // Keras Adam (learner.KerasAdam, k_adam_flat) on registers; returns the new
 // parameter.  The square root and the quotient by the hardware's v_sqrt_f32
@@ -428,6 +426,13 @@ __device__ __forceinline__ void dw1_adam(f4& w1, f4& m1, f4& v1, f4 dz1, const f
   }
 }
 
+// the Dropout bits of layer-1 unit C d + c, rows 4 g .. 4 g + 3, for call
+// number `call` (rng.dropout_keep's keys: (row >> 2, unit, call); word row & 3)
+__device__ __forceinline__ uint4 drop_bits(const FitArgs& a, uint64_t call, int d, int c, int lg) {
+  return skmlp::philox<10>(make_uint4((uint32_t)lg, (uint32_t)(C * d + c), (uint32_t)call, (uint32_t)(call >> 32)),
+                           (uint32_t)a.drop_seed, (uint32_t)(a.drop_seed >> 32));
+}
+
 __device__ __forceinline__ float keras_alpha(const FitArgs& a, float tk) {
   return a.lr * sqrtf(1.f - powf(a.beta2, tk)) / (1.f - powf(a.beta1, tk));
 }
@@ -513,10 +518,12 @@ __global__ void __launch_bounds__(kT) k_fit_critic(FitArgs a) {
   if (t < kB) sm[cRows + kB * LS + 2 * kB + t] = a.targets[t];
   const float b1c = 1.f - a.beta1, b2c = 1.f - a.beta2;
   bool fail = false;  // this thread's exchange ran out of spins (decided uniformly at the barriers)
+  // waves 0 / 1: this step's Dropout bits (the next step's are drawn in the R wait)
+  uint4 bits = {0u, 0u, 0u, 0u};
+  if (wv < 2) bits = drop_bits(a, (uint64_t)call0, d, 16 * wv + li, lg);
 
   for (int k = 0; k < a.M; ++k) {
     const unsigned E = ep0 + 2u * (unsigned)k;
-    const uint64_t call = (uint64_t)(call0 + k);
     if (k % kAlphaN == 0) alpha_fill(a, sAlpha, tk0, k);  // (its barrier also publishes step 0's rows)
     const float alpha = sAlpha[k % kAlphaN];
     float* sS = sm + cRows + (k & 1) * kRowsN;
@@ -541,14 +548,11 @@ __global__ void __launch_bounds__(kT) k_fit_critic(FitArgs a) {
     if (wv < 2) {
       const f32x4 z = layer1(sS, W1, li, lg);
       const int c = 16 * wv + li;
-      const uint4 u = skmlp::philox<10>(make_uint4((uint32_t)lg, (uint32_t)(C * d + c), (uint32_t)call,
-                                                   (uint32_t)(call >> 32)),
-                                        (uint32_t)a.drop_seed, (uint32_t)(a.drop_seed >> 32));
-      const uint32_t bits[4] = {u.x, u.y, u.z, u.w};
+      const uint32_t bw[4] = {bits.x, bits.y, bits.z, bits.w};
       f4 hd;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const bool keep = bits[r] >= kDropThreshold;
+        const bool keep = bw[r] >= kDropThreshold;
         hd[r] = keep ? fmaxf(z[r], 0.f) * 1.25f : 0.f;
         mask[r] = (keep && z[r] > 0.f) ? 1.25f : 0.f;
         sHD[(4 * lg + r) * LH + c] = hd[r];
@@ -564,8 +568,10 @@ __global__ void __launch_bounds__(kT) k_fit_critic(FitArgs a) {
     SK_FT(k, 2);
 
     // (3) workgroup d sums the 8 slices of units U_d (source order), adds b2
-    //     and the action columns: h2 = relu(z2), published to all (H)
+    //     and the action columns: h2 = relu(z2), published to all (H); the
+    //     next step's Dropout bits first (VALU work hidden by the wait)
     if (t < U * 8) {
+      if (more) bits = drop_bits(a, (uint64_t)(call0 + k + 1), d, 16 * wv + li, lg);
       float z0, z1;
       fail |= !r_sum(xr, E + 1, t, [&](int s) { return cxR + (s * P + d) * U * 16; }, z0, z1, a.timeout);
       const int ug = U * d + (2 * t) / 16, r0 = (2 * t) % 16;
@@ -619,49 +625,40 @@ __global__ void __launch_bounds__(kT) k_fit_critic(FitArgs a) {
       a.losses[k] = l / kB;
     }
 
-    // (6) the unit parameters' gradients (lane pair per unit, 8 rows each)
-    //     and Adam steps (every W3 / b2 / W2A read of this step is behind the
-    //     barrier above)
-    {
-      const int u = t >> 1, h = t & 1;
+    // (7) dL/dh1d of the own columns (waves 0 / 1 end with layer 1's layout),
+    //     dz1 = dh1d x the Dropout / relu mask, (8) dW1 | db1 and their Adam
+    //     steps on registers; (9) dW2[:, C_d] and its Adam steps in the
+    //     epilogue (the W2 mirror's reads by (7) are behind its barrier)
+    const f32x4 dh = backward_dh1(sDZ, sW2, sPart, wv, lane, li, lg);
+    SK_FT(k, 6);
+    if (wv < 2) {
+      const f4 dz1 = {dh[0] * mask[0], dh[1] * mask[1], dh[2] * mask[2], dh[3] * mask[3]};
+      dw1_adam(W1, M1, V1, dz1, sS, alpha, b1c, b2c, a.eps, li, lg);
+    } else {
+      // (6) meanwhile waves 2 / 3: the unit parameters' 16-row gradient sums
+      //     (one unit per lane) and Adam steps (every W3 / b2 / W2A read of
+      //     this step is behind the barriers above; the next are behind the
+      //     next step's first)
+      const int u = t - 2 * 64;
       float gw3 = 0.f, gb2 = 0.f, ga0 = 0.f, ga1 = 0.f;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int r = 8 * h + i;
+      for (int r = 0; r < kB; ++r) {
         const float dz = sDZ[r * LZ + u];
         gw3 += sDQ[r] * sH2[r * LZ + u];
         gb2 += dz;
         ga0 += dz * sA[2 * r];
         ga1 += dz * sA[2 * r + 1];
       }
-      gw3 = sum2(gw3);
-      gb2 = sum2(gb2);
-      ga0 = sum2(ga0);
-      ga1 = sum2(ga1);
-      if (h == 0) {
-        adam_lds(uW, uM, uV, uW3 + u, gw3, alpha, b1c, b2c, a.eps);
-        adam_lds(uW, uM, uV, uB2 + u, gb2, alpha, b1c, b2c, a.eps);
-      } else {
-        adam_lds(uW, uM, uV, uWA + 2 * u, ga0, alpha, b1c, b2c, a.eps);
-        adam_lds(uW, uM, uV, uWA + 2 * u + 1, ga1, alpha, b1c, b2c, a.eps);
-      }
-      if (wv == 0) {  // b3: the 16 rows' dL/dq in row 0 of wave 0
+      adam_lds(uW, uM, uV, uW3 + u, gw3, alpha, b1c, b2c, a.eps);
+      adam_lds(uW, uM, uV, uB2 + u, gb2, alpha, b1c, b2c, a.eps);
+      adam_lds(uW, uM, uV, uWA + 2 * u, ga0, alpha, b1c, b2c, a.eps);
+      adam_lds(uW, uM, uV, uWA + 2 * u + 1, ga1, alpha, b1c, b2c, a.eps);
+      if (wv == 2) {  // b3: the 16 rows' dL/dq in row 0 of wave 2
         const float gb3 = sum16(lane < kB ? sDQ[lane] : 0.f);
         if (lane == 0) adam_lds(uW, uM, uV, uB3, gb3, alpha, b1c, b2c, a.eps);
       }
     }
-    SK_FT(k, 6);
-
-    // (7) dL/dh1d of the own columns (waves 0 / 1 end with layer 1's layout),
-    //     dz1 = dh1d x the Dropout / relu mask, (8) dW1 | db1 and their Adam
-    //     steps on registers; (9) dW2[:, C_d] and its Adam steps in the
-    //     epilogue (the W2 mirror's reads by (7) are behind its barrier)
-    const f32x4 dh = backward_dh1(sDZ, sW2, sPart, wv, lane, li, lg);
     SK_FT(k, 7);
-    if (wv < 2) {
-      const f4 dz1 = {dh[0] * mask[0], dh[1] * mask[1], dh[2] * mask[2], dh[3] * mask[3]};
-      dw1_adam(W1, M1, V1, dz1, sS, alpha, b1c, b2c, a.eps, li, lg);
-    }
     SK_FT(k, 8);
     dw2_adam(W2, M2, V2, sHDT, sDZT, sW2, alpha, b1c, b2c, a.eps, wv, li, lg);
     SK_FT(k, 9);
@@ -708,30 +705,84 @@ __global__ void __launch_bounds__(kT) k_fit_critic(FitArgs a) {
 // ------------------------------------------------------------------ actor
 // model_actor_fit_step (SkillshotLearner.py:386-417): the gradient of
 // -sum_b Q(s_b, mu(s_b)) with the critic fixed (inference: no Dropout), one
-// Adam step of the actor per minibatch.  The same column split for both
-// nets: workgroup d owns the actor's W1 | b1 of C_d and W2[:, C_d] in
-// registers (as the critic kernel) and holds the critic's matching frozen
-// slices (W1 | b1 on waves 2 / 3, W2[:, C_d] in registers); the unit
-// parameters of both (actor b2, W3, b3 with their moments; critic b2, W3,
-// action columns) are in every workgroup's LDS.  R carries both nets'
-// layer-2 partials; H both nets' sums of U_d (the actor's h2, the critic's
-// z2 before the action columns); then every workgroup forms a = tanh(z3),
-// the critic's dQ/da at (s, a), the actor's dL/dz2 and its unit parameters'
-// Adam steps itself.
+// Adam step of the actor per minibatch.  The critic is frozen for the whole
+// pass, so its part of Q that depends on s alone — the layer-2
+// pre-activations without the action columns, zc = b2 + W2[:, :256]
+// relu(W1 s + b1) — is computed for every row of the launch up front by one
+// parallel kernel (k_fit_critic_z2, one workgroup per minibatch), and each
+// step streams its 16 rows of zc in (prefetched a step ahead) instead of
+// running the critic's layers 1 and 2 in the chain.  The actor itself takes
+// the critic kernel's column split: workgroup d owns the actor's W1 | b1 of
+// C_d and W2[:, C_d] in registers; its unit parameters (b2, W3, b3 with their
+// moments) and the critic's (W3, action columns) are in every workgroup's
+// LDS.  R reduce-scatters the actor's layer-2 partials, H all-gathers its
+// h2; then every workgroup forms a = tanh(z3), the critic's dQ/da at (s, a),
+// the actor's dL/dz2 and its unit parameters' Adam steps itself.
+
+// zc[row][u] of the critic, for `M` minibatches of states (float [16 M][128])
+constexpr int LH1 = kH1 + 4;
+__global__ void __launch_bounds__(kT) k_fit_critic_z2(const float* __restrict__ critic,
+                                                      const float* __restrict__ states, float* __restrict__ zc) {
+  __shared__ __attribute__((aligned(16))) float sS[kB * LS];
+  __shared__ __attribute__((aligned(16))) float sH[kB * LH1];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, li = lane & 15, lg = lane >> 4;
+  const int64_t row0 = (int64_t)blockIdx.x * kB;
+  if (t < kB * LS) {
+    const int r = t / LS, j = t % LS;
+    sS[t] = j < kS ? states[(row0 + r) * kS + j] : (j == kS ? 1.f : 0.f);
+  }
+  __syncthreads();
+  // layer 1 (s with a column of ones against W1 | b1): wave w, unit tiles w + 4 q
+  const f4 x = *(const f4*)(sS + li * LS + 4 * lg);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int u = 16 * (wv + 4 * q) + li;
+    f4 w = {0.f, 0.f, 0.f, 0.f};
+    if (lg < 3) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[j] = critic[kW1 + u * kS + 4 * lg + j];
+    } else {
+      w[0] = critic[kB1 + u];
+    }
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    acc = m16x4(x, w, acc);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sH[(4 * lg + r) * LH1 + u] = fmaxf(acc[r], 0.f);
+  }
+  __syncthreads();
+  // layer 2 over the 256 h1 columns: wave w, unit tiles w, w + 4
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int u = 16 * (wv + 4 * q) + li;
+    const float* wr = critic + kW2 + u * kCLd;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+    for (int kk = 0; kk < kH1; kk += 16) {
+      const f4 h = *(const f4*)(sH + li * LH1 + kk + 4 * lg);
+      const f4 w = {wr[kk + 4 * lg], wr[kk + 4 * lg + 1], wr[kk + 4 * lg + 2], wr[kk + 4 * lg + 3]};
+      acc = m16x4(h, w, acc);
+    }
+    const float b2 = critic[kCB2 + u];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) zc[(row0 + 4 * lg + r) * kH2 + u] = acc[r] + b2;
+  }
+}
+
 constexpr int aW3 = 0, aB2 = 2 * kH2, aB3 = 3 * kH2, kAUN = 3 * kH2 + 4;  // actor units: W3 [128][2], b2, b3[2]
-constexpr int qB2 = 0, qW3 = kH2, qWA = 2 * kH2, kQUN = 4 * kH2;          // critic units (frozen)
+constexpr int qW3 = 0, qWA = kH2, kQUN = 3 * kH2;                         // critic units (frozen): W3, W2A [128][2]
 // two of each per-step buffer (as the critic's): rows [s_ext 16 x 16],
-// activations [actor h1 16 x LH | its transpose C x LHT | critic h1 16 x LH]
-constexpr int kARowsN = kB * LS, kAActN = 2 * kB * LH + C * LHT;
-constexpr int xS = 3 * kAUN + kQUN, xAct = xS + 2 * kARowsN, xDZ3 = xAct + 2 * kAActN, xH2 = xDZ3 + 2 * kB,
-              xZC = xH2 + kB * LZ, xDZ = xZC + kB * LZ, xDZT = xDZ + kB * LZ, xW2 = xDZT + kH2 * LZT,
+// activations [h1 16 x LH | its transpose C x LHT], the critic's zc [16 x LZ]
+constexpr int kARowsN = kB * LS, kAActN = kB * LH + C * LHT;
+constexpr int xS = 3 * kAUN + kQUN, xAct = xS + 2 * kARowsN, xZC = xAct + 2 * kAActN, xDZ3 = xZC + 2 * kB * LZ,
+              xH2 = xDZ3 + 2 * kB, xDZ = xH2 + kB * LZ, xDZT = xDZ + kB * LZ, xW2 = xDZT + kH2 * LZT,
               xPart = xW2 + kH2 * LW, xAlpha = xPart + 2 * 64 * 4, xEnd = xAlpha + kAlphaN;
 constexpr size_t kActorLds = (size_t)xEnd * 4;
-// exchanges: R [P src][P dst][2 nets][U][16], H [P][2 nets][U][16]
-constexpr int axR = 0, axH = axR + P * P * 2 * U * 16, axN = axH + P * 2 * U * 16;
+// exchanges: R [P src][P dst][U][16], H [P][U][16]
+constexpr int axR = 0, axH = axR + P * P * U * 16, axN = axH + P * U * 16;
 static_assert(kActorLds <= 150 * 1024, "LDS");
+constexpr int kZPer = kB * kH2 / kT;  // zc floats per thread and step
 
-__global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a) {
+__global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a, const float* __restrict__ zc) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   SK_FT_DECL
   if (blockIdx.x % a.stride) return;
@@ -741,30 +792,26 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a) {
   float* qU = sm + 3 * kAUN;
   float* sDZ3 = sm + xDZ3;
   float* sH2 = sm + xH2;
-  float* sAlpha = sm + xAlpha;
-  float* sZC = sm + xZC;
   float* sDZ = sm + xDZ;
   float* sDZT = sm + xDZT;
   float* sW2 = sm + xW2;
   float* sPart = sm + xPart;
+  float* sAlpha = sm + xAlpha;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, li = lane & 15, lg = lane >> 4;
   const int d = blockIdx.x / a.stride;
   const __amdgpu_buffer_rsrc_t xr = rsrc_of(a.xbuf);
 
-  W2Reg W2, M2, V2, CW2;
+  W2Reg W2, M2, V2;
   w2_load<kH1>(W2, a.flat, d, wv, li, lg);
   w2_load<kH1>(M2, a.m, d, wv, li, lg);
   w2_load<kH1>(V2, a.v, d, wv, li, lg);
-  w2_load<kCLd>(CW2, a.critic, d, wv, li, lg);
   w2_mirror(W2, sW2, wv, li, lg);
-  // waves 0 / 1: the actor's W1 | b1 (n-tile wv); waves 2 / 3: the critic's (n-tile wv - 2)
+  // waves 0 / 1: the actor's W1 | b1 (n-tile wv)
   f4 W1 = {0.f, 0.f, 0.f, 0.f}, M1 = W1, V1 = W1;
   if (wv < 2) {
     W1 = w1_load(a.flat, d, wv, li, lg);
     M1 = w1_load(a.m, d, wv, li, lg);
     V1 = w1_load(a.v, d, wv, li, lg);
-  } else {
-    W1 = w1_load(a.critic, d, wv - 2, li, lg);
   }
   if (t < kH2) {
     const int gi[3] = {kAW3 + t, kAW3 + kH2 + t, kAB2 + t};
@@ -775,7 +822,6 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a) {
       uM[l3[j]] = a.m[gi[j]];
       uV[l3[j]] = a.v[gi[j]];
     }
-    qU[qB2 + t] = a.critic[kCB2 + t];
     qU[qW3 + t] = a.critic[kCW3 + t];
     qU[qWA + 2 * t] = a.critic[kW2 + t * kCLd + kH1];
     qU[qWA + 2 * t + 1] = a.critic[kW2 + t * kCLd + kH1 + 1];
@@ -792,6 +838,11 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a) {
     sm[xS + t] = j < kS ? a.states[r * kS + j] : (j == kS ? 1.f : 0.f);
     sm[xS + kARowsN + t] = j == kS ? 1.f : 0.f;
   }
+#pragma unroll
+  for (int i = 0; i < kZPer; ++i) {
+    const int idx = t + kT * i;
+    sm[xZC + (idx / kH2) * LZ + idx % kH2] = zc[idx];
+  }
   const float b1c = 1.f - a.beta1, b2c = 1.f - a.beta2;
   bool fail = false;
 
@@ -802,71 +853,64 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a) {
     float* sS = sm + xS + (k & 1) * kARowsN;
     float* sH1 = sm + xAct + (k & 1) * kAActN;
     float* sH1T = sH1 + kB * LH;
-    float* sH1C = sH1T + C * LHT;
+    const float* sZC = sm + xZC + (k & 1) * kB * LZ;
     SK_FT(k, 0);
+    // the next step's rows and zc into registers (stored into the other buffers mid-step)
     float nx = 0.f;
+    float nz[kZPer];
     const bool more = k + 1 < a.M;
-    if (more && t < kB * kS) nx = a.states[(int64_t)(k + 1) * kB * kS + t];
+    if (more) {
+      if (t < kB * kS) nx = a.states[(int64_t)(k + 1) * kB * kS + t];
+#pragma unroll
+      for (int i = 0; i < kZPer; ++i) nz[i] = zc[(int64_t)(k + 1) * kB * kH2 + t + kT * i];
+    }
 
-    // (1) layer 1 of the own units: the actor on waves 0 / 1 (relu mask kept
-    //     in registers), the critic (inference) on waves 2 / 3
+    // (1) layer 1 of the own units on waves 0 / 1 (the relu mask kept in registers)
     f4 hmask = {0.f, 0.f, 0.f, 0.f};
-    {
+    if (wv < 2) {
       const f32x4 z = layer1(sS, W1, li, lg);
-      const int c = 16 * (wv & 1) + li;
+      const int c = 16 * wv + li;
       f4 h;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) h[r] = fmaxf(z[r], 0.f);
-      if (wv < 2) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          hmask[r] = z[r] > 0.f ? 1.f : 0.f;
-          sH1[(4 * lg + r) * LH + c] = h[r];
-        }
-        *(f4*)(sH1T + c * LHT + 4 * lg) = h;
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) sH1C[(4 * lg + r) * LH + c] = h[r];
+      for (int r = 0; r < 4; ++r) {
+        h[r] = fmaxf(z[r], 0.f);
+        hmask[r] = z[r] > 0.f ? 1.f : 0.f;
+        sH1[(4 * lg + r) * LH + c] = h[r];
       }
+      *(f4*)(sH1T + c * LHT + 4 * lg) = h;
     }
     __syncthreads();
     SK_FT(k, 1);
 
-    // (2) both nets' layer-2 partials over the own columns, to the unit summers
-    partials_publish(sH1, W2, xr, E + 1, wv, li, lg, [&](int e) { return axR + ((d * P + e) * 2 + 0) * U * 16; });
-    partials_publish(sH1C, CW2, xr, E + 1, wv, li, lg,
-                     [&](int e) { return axR + ((d * P + e) * 2 + 1) * U * 16; });
+    // (2) the layer-2 partials over the own columns, to the unit summers
+    partials_publish(sH1, W2, xr, E + 1, wv, li, lg, [&](int e) { return axR + (d * P + e) * U * 16; });
     SK_FT(k, 2);
 
-    // (3) the sums of U_d: the actor's h2 = relu(z2 + b2) (threads 0..127),
-    //     the critic's z2 + b2 without the action columns (128..255); to all
-    {
-      const int net = t / (U * 8), pr = t - net * U * 8;
+    // (3) the sums of U_d: h2 = relu(z2 + b2), published to all (H)
+    if (t < U * 8) {
       float z0, z1;
-      fail |= !r_sum(xr, E + 1, pr, [&](int s) { return axR + ((s * P + d) * 2 + net) * U * 16; }, z0, z1,
-                     a.timeout);
-      const int ug = U * d + (2 * pr) / 16;
-      if (net == 0) {
-        const float b2 = uW[aB2 + ug];
-        z0 = fmaxf(z0 + b2, 0.f);
-        z1 = fmaxf(z1 + b2, 0.f);
-      } else {
-        const float b2 = qU[qB2 + ug];
-        z0 = z0 + b2;
-        z1 = z1 + b2;
-      }
-      put2(xr, (uint32_t)(axH + (d * 2 + net) * U * 16 + 2 * pr) * 8u, E + 2, z0, z1);
+      fail |= !r_sum(xr, E + 1, t, [&](int s) { return axR + (s * P + d) * U * 16; }, z0, z1, a.timeout);
+      const float b2 = uW[aB2 + U * d + (2 * t) / 16];
+      put2(xr, (uint32_t)(axH + d * U * 16 + 2 * t) * 8u, E + 2, fmaxf(z0 + b2, 0.f), fmaxf(z1 + b2, 0.f));
     }
     SK_FT(k, 3);
 
-    // (4) both of all 128 units
+    // (4) h2 of all 128 units
     {
-      float* const dst[2] = {sH2, sZC};
-      fail |= !gather_h<2>(xr, axH, E + 2, dst, a.timeout);
+      float* const dst[1] = {sH2};
+      fail |= !gather_h<1>(xr, axH, E + 2, dst, a.timeout);
     }
     if (__syncthreads_or(fail)) break;
     SK_FT(k, 4);
-    if (more && t < kB * kS) sm[xS + ((k + 1) & 1) * kARowsN + (t / kS) * LS + t % kS] = nx;
+    if (more) {  // the next step's rows and zc (those buffers' last readers were in step k - 1)
+      if (t < kB * kS) sm[xS + ((k + 1) & 1) * kARowsN + (t / kS) * LS + t % kS] = nx;
+      float* nZ = sm + xZC + ((k + 1) & 1) * kB * LZ;
+#pragma unroll
+      for (int i = 0; i < kZPer; ++i) {
+        const int idx = t + kT * i;
+        nZ[(idx / kH2) * LZ + idx % kH2] = nz[i];
+      }
+    }
 
     // (5) every workgroup, lane (row t / 16, units t % 16 + 16 i), DPP row
     //     sums: z3 -> a = tanh(z3); the critic at (s, a): dQ/dz2 = W3 [z2 > 0],
@@ -908,43 +952,34 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a) {
     __syncthreads();
     SK_FT(k, 5);
 
-    // (6) the actor's unit parameters' gradients (lane pair per unit, 8 rows
-    //     each) and Adam steps
-    {
-      const int u = t >> 1, h = t & 1;
+    // (7) dL/dh1[:, C_d], dz1 = dh1 [h1 > 0], dW1 | db1 (waves 0 / 1) and
+    //     dW2[:, C_d] with their Adam steps
+    const f32x4 dh = backward_dh1(sDZ, sW2, sPart, wv, lane, li, lg);
+    SK_FT(k, 6);
+    if (wv < 2) {
+      const f4 dz1 = {dh[0] * hmask[0], dh[1] * hmask[1], dh[2] * hmask[2], dh[3] * hmask[3]};
+      dw1_adam(W1, M1, V1, dz1, sS, alpha, b1c, b2c, a.eps, li, lg);
+    } else {
+      // (6) meanwhile waves 2 / 3: the actor's unit parameters' 16-row
+      //     gradient sums (one unit per lane) and Adam steps
+      const int u = t - 2 * 64;
       float gw0 = 0.f, gw1 = 0.f, gb2 = 0.f;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int r = 8 * h + i;
+      for (int r = 0; r < kB; ++r) {
         const float hv = sH2[r * LZ + u];
         gw0 += sDZ3[2 * r] * hv;
         gw1 += sDZ3[2 * r + 1] * hv;
         gb2 += sDZ[r * LZ + u];
       }
-      gw0 = sum2(gw0);
-      gw1 = sum2(gw1);
-      gb2 = sum2(gb2);
-      if (h == 0) {
-        adam_lds(uW, uM, uV, aW3 + 2 * u, gw0, alpha, b1c, b2c, a.eps);
-        adam_lds(uW, uM, uV, aW3 + 2 * u + 1, gw1, alpha, b1c, b2c, a.eps);
-      } else {
-        adam_lds(uW, uM, uV, aB2 + u, gb2, alpha, b1c, b2c, a.eps);
-      }
-      if (wv == 0) {  // b3: dL/dz3 of the 16 rows, output j in row j of wave 0
+      adam_lds(uW, uM, uV, aW3 + 2 * u, gw0, alpha, b1c, b2c, a.eps);
+      adam_lds(uW, uM, uV, aW3 + 2 * u + 1, gw1, alpha, b1c, b2c, a.eps);
+      adam_lds(uW, uM, uV, aB2 + u, gb2, alpha, b1c, b2c, a.eps);
+      if (wv == 2) {  // b3: dL/dz3 of the 16 rows, output j in row j of wave 2
         const float gb3 = sum16(lane < 2 * kB ? sDZ3[2 * (lane & 15) + (lane >> 4)] : 0.f);
         if (lane == 0 || lane == 16) adam_lds(uW, uM, uV, aB3 + (lane >> 4), gb3, alpha, b1c, b2c, a.eps);
       }
     }
-    SK_FT(k, 6);
-
-    // (7) dL/dh1[:, C_d], dz1 = dh1 [h1 > 0], dW1 | db1 (waves 0 / 1) and
-    //     dW2[:, C_d] with their Adam steps
-    const f32x4 dh = backward_dh1(sDZ, sW2, sPart, wv, lane, li, lg);
     SK_FT(k, 7);
-    if (wv < 2) {
-      const f4 dz1 = {dh[0] * hmask[0], dh[1] * hmask[1], dh[2] * hmask[2], dh[3] * hmask[3]};
-      dw1_adam(W1, M1, V1, dz1, sS, alpha, b1c, b2c, a.eps, li, lg);
-    }
     SK_FT(k, 8);
     dw2_adam(W2, M2, V2, sH1T, sDZT, sW2, alpha, b1c, b2c, a.eps, wv, li, lg);
     SK_FT(k, 9);
@@ -983,13 +1018,13 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a) {
   }
 }
 
-template <typename K>
-int launch_fit(K kernel, size_t lds, bool& attr, const FitArgs& a, hipStream_t st) {
+template <typename K, typename... X>
+int launch_fit(K kernel, size_t lds, bool& attr, const FitArgs& a, hipStream_t st, X... extra) {
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  kernel<<<P * a.stride, kT, lds, st>>>(a);
+  kernel<<<P * a.stride, kT, lds, st>>>(a, extra...);
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
 }
 
@@ -1030,16 +1065,20 @@ int sk_fit_critic_f32(float* critic_flat, float* m, float* v, float* steps, int3
 
 int sk_fit_actor_f32(float* actor_flat, float* adam_m, float* adam_v, float* step_counters, int32_t n_steps,
                      const float* critic_flat, const float* states, int32_t n_minibatches, float lr, float beta1,
-                     float beta2, float eps, void* xbuf, uint64_t* epoch, uint32_t* timeout, void* stream) {
+                     float beta2, float eps, void* xbuf, uint64_t* epoch, uint32_t* timeout, float* zbuf,
+                     void* stream) {
   if (!actor_flat || !adam_m || !adam_v || !step_counters || n_steps < 1 || n_steps > 64 || !critic_flat ||
-      !states || n_minibatches < 1 || !xbuf || !epoch || !timeout)
+      !states || n_minibatches < 1 || !xbuf || !epoch || !timeout || !zbuf)
     return SK_EINVAL;
   if (((uintptr_t)xbuf) & 15) return SK_EINVAL;
+  const hipStream_t st = (hipStream_t)stream;
+  k_fit_critic_z2<<<n_minibatches, kT, 0, st>>>(critic_flat, states, zbuf);
+  if (hipGetLastError() != hipSuccess) return SK_EHIP;
   FitArgs a{actor_flat, adam_m, adam_v, step_counters, n_steps, states, nullptr, nullptr, n_minibatches, 0, nullptr,
             lr, beta1, beta2, eps, (unsigned long long*)xbuf, (unsigned long long*)epoch, timeout, nullptr,
             fit_stride(), critic_flat};
   static bool attr = false;
-  return launch_fit(k_fit_actor, kActorLds, attr, a, (hipStream_t)stream);
+  return launch_fit(k_fit_actor, kActorLds, attr, a, st, (const float*)zbuf);
 }
 
 }  // extern "C"

@@ -387,11 +387,15 @@ class FusedUpdate:
         s = s.float().contiguous()
         self._fit_buffers()
         st = self.sa
+        per = min(self.FIT_STEPS_PER_LAUNCH, n)
+        z = getattr(self, "fit_z", None)
+        if z is None or z.numel() < per * b * 128:  # the frozen critic's pre-activations, one launch's rows
+            z = self.fit_z = torch.empty(per * b * 128, dtype=torch.float32, device=self.dev)
         for k0 in range(0, n, self.FIT_STEPS_PER_LAUNCH):
             m = min(self.FIT_STEPS_PER_LAUNCH, n - k0)
             _capi.check(self.L.sk_fit_actor_f32(
                 _p(self.fa), _p(st.m), _p(st.v), _p(st.steps), st.steps.numel(), _p(self.fc), _p(s[k0 * b:]), m,
-                st.lr, st.b1, st.b2, st.eps, _p(self.fit_x), _p(self.fit_epoch), _p(self.fit_timeout),
+                st.lr, st.b1, st.b2, st.eps, _p(self.fit_x), _p(self.fit_epoch), _p(self.fit_timeout), _p(z),
                 self._stream()))
         if self.split_pack is not None:
             _capi.check(self.L.sk_actor_split_pack_f32(_p(self.fa), _p(self.split_pack), self._stream()))

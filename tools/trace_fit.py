@@ -15,10 +15,10 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-NAMES = {"critic": ["L1 + Dropout", "P1 publish", "R sum + H publish", "H gather", "q + dz2", "unit Adam",
-                    "dh1 GEMM", "dW1 + Adam", "dW2 GEMM + Adam", "-", "to the next step"],
-         "actor": ["L1 x2", "P1 publish x2", "R sums + H publish", "H gather", "a, dQ/da, dz2", "unit Adam",
-                   "dh1 GEMM", "dW1 + Adam", "dW2 GEMM + Adam", "-", "to the next step"]}
+NAMES = {"critic": ["L1 + Dropout", "P1 publish", "R sum + H publish", "H gather", "q + dz2", "dh1 GEMM",
+                    "dW1 + Adam (waves 2/3: unit Adam)", "-", "dW2 GEMM + Adam", "-", "to the next step"],
+         "actor": ["L1 x2", "P1 publish x2", "R sums + H publish", "H gather", "a, dQ/da, dz2", "dh1 GEMM",
+                   "dW1 + Adam (waves 2/3: unit Adam)", "-", "dW2 GEMM + Adam", "-", "to the next step"]}
 
 
 def main():
