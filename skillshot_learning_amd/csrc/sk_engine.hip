@@ -974,12 +974,22 @@ __device__ __forceinline__ void split_multi_tick(const MultiArgs& a, const Cfg& 
   const float2 act = load_action(a.actions + slab * 2 * a.n + (int64_t)p * a.n + L.ic);  // action last
   __builtin_amdgcn_sched_barrier(0);
   bool k0, k1, k2 = true;
+#ifdef SK_ABL_NOSC  // timing ablation only (tools/ab_split4.sh): no sincos at all
+  sktrig::SinCos m{rot * 1e-9, 1.0};
+  k0 = true;
+#else
   sktrig::SinCos m = sktrig::sincos_bf(rot, &k0);
+#endif
   const double q_old = qrot;
   // do_actions(p+1, ...)  SkillshotLearner.py:206-213 (both sincos up front)
   const double rn = rot + clamp_action((double)act.y) * c.look;
   const double qn = (qcd <= 0) ? rn : qrot;
+#if defined(SK_ABL_NOQSC) || defined(SK_ABL_NOSC)  // timing ablation only: no projectile sincos
+  sktrig::SinCos tq{qn * 1e-9, 1.0};
+  k1 = true;
+#else
   sktrig::SinCos tq = sktrig::sincos_bf(qn, &k1);
+#endif
   // the post-look rotation's sin/cos for the obs epilogue (fp32: obs12_sc)
   sktrig::SinCosF pr{0.0f, 1.0f};
   if constexpr (OBS) pr = sktrig::sincos_fast(rn, &k2);
