@@ -79,9 +79,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef unsigned u4v __attribute__((ext_vector_type(4)));
 
-constexpr int P = 8;                                              // workgroups
 constexpr int kB = 16, kS = 12, kH1 = 256, kH2 = 128, kT = 256;  // rows, inputs, units, threads
-constexpr int C = kH1 / P, U = kH2 / P;                           // own layer-1 units / columns, units per R slice
 constexpr int kCLd = kH1 + 2;                                     // critic W2 row: 256 h1 + 2 action
 // flat offsets (torch parameters() order; update_kernel.flatten_module)
 constexpr int kW1 = 0, kB1 = kH1 * kS, kW2 = kB1 + kH1;
@@ -92,11 +90,21 @@ constexpr unsigned kDropThreshold = 858993460u;  // rng.DROP_THRESHOLD: keep wit
 
 // LDS strides (floats)
 constexpr int LS = 16;       // s_ext rows: 12 inputs, 1 (the bias column), 3 zeros
-constexpr int LH = C + 4;    // [16 rows][C] activations
 constexpr int LHT = kB + 4;  // [C][16 rows]
 constexpr int LZ = kH2 + 4;  // [16 rows][128]
 constexpr int LZT = kB + 4;  // [128][16 rows]
-constexpr int LW = C + 4;    // the W2 mirror [128][C]
+
+// The split over PW workgroups (8 or 16, SK_FIT_P): C own layer-1 units (=
+// W2 input columns) per workgroup in NT1 16-unit tiles, U layer-2 units summed
+// per workgroup in the R exchange; the dL/dh1 GEMM splits its K = 128 over KS
+// waves per n-tile
+template <int PW>
+struct Geo {
+  static constexpr int P = PW, C = kH1 / P, U = kH2 / P, NT1 = C / 16, KS = 4 / NT1;
+  static constexpr int LH = C + 4;  // [16 rows][C] activations
+  static constexpr int LW = C + 4;  // the W2 mirror [128][C]
+  static_assert(C % 16 == 0 && NT1 <= 2 && U % 8 == 0, "geometry");
+};
 
 __device__ __forceinline__ f32x4 m16(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -233,47 +241,51 @@ __device__ unsigned long long* sk_fit_trace;
 
 // ---------------------------------------------------------------- shared pieces
 // The W2[:, C_d] slice in registers: r[q][mk][t] = W[u = 16 (w + 4 q) + i][c = 16 mk + 4 g + t]
+template <class G>
 struct W2Reg {
-  f4 w[2][2];
+  f4 w[2][G::NT1];
 };
 // flat index of W2 entry (u, own column c) for row length ld
-__device__ __forceinline__ int w2_index(int u, int c, int d, int ld) { return kW2 + u * ld + C * d + c; }
+template <class G>
+__device__ __forceinline__ int w2_index(int u, int c, int d, int ld) { return kW2 + u * ld + G::C * d + c; }
 
-template <int LD>
-__device__ __forceinline__ void w2_load(W2Reg& r, const float* src, int d, int wv, int li, int lg) {
+template <class G, int LD>
+__device__ __forceinline__ void w2_load(W2Reg<G>& r, const float* src, int d, int wv, int li, int lg) {
 #pragma unroll
   for (int q = 0; q < 2; ++q)
 #pragma unroll
-    for (int mk = 0; mk < 2; ++mk) {
+    for (int mk = 0; mk < G::NT1; ++mk) {
       const int u = 16 * (wv + 4 * q) + li;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) r.w[q][mk][t] = src[w2_index(u, 16 * mk + 4 * lg + t, d, LD)];
+      for (int t = 0; t < 4; ++t) r.w[q][mk][t] = src[w2_index<G>(u, 16 * mk + 4 * lg + t, d, LD)];
     }
 }
-template <int LD>
-__device__ __forceinline__ void w2_store(const W2Reg& r, float* dst, int d, int wv, int li, int lg) {
+template <class G, int LD>
+__device__ __forceinline__ void w2_store(const W2Reg<G>& r, float* dst, int d, int wv, int li, int lg) {
 #pragma unroll
   for (int q = 0; q < 2; ++q)
 #pragma unroll
-    for (int mk = 0; mk < 2; ++mk) {
+    for (int mk = 0; mk < G::NT1; ++mk) {
       const int u = 16 * (wv + 4 * q) + li;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) dst[w2_index(u, 16 * mk + 4 * lg + t, d, LD)] = r.w[q][mk][t];
+      for (int t = 0; t < 4; ++t) dst[w2_index<G>(u, 16 * mk + 4 * lg + t, d, LD)] = r.w[q][mk][t];
     }
 }
-__device__ __forceinline__ void w2_mirror(const W2Reg& r, float* sW2, int wv, int li, int lg) {
+template <class G>
+__device__ __forceinline__ void w2_mirror(const W2Reg<G>& r, float* sW2, int wv, int li, int lg) {
 #pragma unroll
   for (int q = 0; q < 2; ++q)
 #pragma unroll
-    for (int mk = 0; mk < 2; ++mk) {
+    for (int mk = 0; mk < G::NT1; ++mk) {
       const int u = 16 * (wv + 4 * q) + li;
-      *(f4*)(sW2 + u * LW + 16 * mk + 4 * lg) = r.w[q][mk];
+      *(f4*)(sW2 + u * G::LW + 16 * mk + 4 * lg) = r.w[q][mk];
     }
 }
 
-// W1 | b1 of n-tile wt (0 / 1) in registers: lane (i, g): W1[32 d + 16 wt + i][4 g + t], g = 3: {b1, 0, 0, 0}
+// W1 | b1 of n-tile wt in registers: lane (i, g): W1[C d + 16 wt + i][4 g + t], g = 3: {b1, 0, 0, 0}
+template <class G>
 __device__ __forceinline__ f4 w1_load(const float* src, int d, int wt, int li, int lg) {
-  const int cg = C * d + 16 * wt + li;
+  const int cg = G::C * d + 16 * wt + li;
   f4 r = {0.f, 0.f, 0.f, 0.f};
   if (lg < 3) {
 #pragma unroll
@@ -283,8 +295,9 @@ __device__ __forceinline__ f4 w1_load(const float* src, int d, int wt, int li, i
   }
   return r;
 }
+template <class G>
 __device__ __forceinline__ void w1_store(f4 r, float* dst, int d, int wt, int li, int lg) {
-  const int cg = C * d + 16 * wt + li;
+  const int cg = G::C * d + 16 * wt + li;
   if (lg < 3) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) dst[kW1 + cg * kS + 4 * lg + t] = r[t];
@@ -302,30 +315,33 @@ __device__ __forceinline__ f32x4 layer1(const float* sS, f4 w1, int li, int lg) 
 }
 
 // the layer-2 partial products of X [16][LH] (own columns) with the
-// register slice W for n-tiles wv and wv + 4, each tile published to its
-// units' summer at slot(e) (granule index of a [U units][16 rows] slice)
-template <typename Slot>
-__device__ __forceinline__ void partials_publish(const float* X, const W2Reg& W, __amdgpu_buffer_rsrc_t xr,
+// register slice W for n-tiles wv and wv + 4, each unit's row published to
+// its summer e at slot(e) (granule index of a [U units][16 rows] slice)
+template <class G, typename Slot>
+__device__ __forceinline__ void partials_publish(const float* X, const W2Reg<G>& W, __amdgpu_buffer_rsrc_t xr,
                                                  unsigned tag, int wv, int li, int lg, Slot slot) {
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int nt = wv + 4 * q;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int mk = 0; mk < 2; ++mk) acc = m16x4(*(const f4*)(X + li * LH + 16 * mk + 4 * lg), W.w[q][mk], acc);
-    // units 16 nt .. 16 nt + 15 are summed by workgroup nt (U = 16): slice row li
-    const uint32_t base = (uint32_t)(slot(nt) + li * 16 + 4 * lg) * 8u;
+    for (int mk = 0; mk < G::NT1; ++mk)
+      acc = m16x4(*(const f4*)(X + li * G::LH + 16 * mk + 4 * lg), W.w[q][mk], acc);
+    // unit 16 nt + li is summed by workgroup (16 nt + li) / U: its slice row
+    const int u = 16 * nt + li;
+    const uint32_t base = (uint32_t)(slot(u / G::U) + (u % G::U) * 16 + 4 * lg) * 8u;
     put2(xr, base, tag, acc[0], acc[1]);
     put2(xr, base + 16u, tag, acc[2], acc[3]);
   }
 }
 
-// the R sums of this workgroup's 16 units: lane t < 128 (net t / 128 for two
-// nets) sums granule pair t % 128 ([U][16]) of the 8 source slices in source
-// order; v = {rows r0, r0 + 1} of unit u (local)
-template <typename Slot>
+// the R sums of this workgroup's U units: lane pr < 8 U sums granule pair
+// pr ([U][16]) of the P source slices in source order; {rows r0, r0 + 1} of
+// unit 2 pr / 16 (local)
+template <class G, typename Slot>
 __device__ __forceinline__ bool r_sum(__amdgpu_buffer_rsrc_t xr, unsigned tag, int pr, Slot slot, float& z0,
                                       float& z1, unsigned* timeout) {
+  constexpr int P = G::P;
   uint32_t off[P];
 #pragma unroll
   for (int s = 0; s < P; ++s) off[s] = (uint32_t)(slot(s) + 2 * pr) * 8u;
@@ -342,10 +358,11 @@ __device__ __forceinline__ bool r_sum(__amdgpu_buffer_rsrc_t xr, unsigned tag, i
 }
 
 // the H all-gather ([P src][NETS][U][16] granules) into dst[net] [16][LZ]
-template <int NETS>
+template <class G, int NETS>
 __device__ __forceinline__ bool gather_h(__amdgpu_buffer_rsrc_t xr, int base, unsigned tag, float* const (&dst)[NETS],
                                          unsigned* timeout) {
-  constexpr int PER = (P * NETS * U * 8) / kT;  // granule pairs per lane
+  constexpr int U = G::U;
+  constexpr int PER = (G::P * NETS * U * 8) / kT;  // granule pairs per lane
   const int t = threadIdx.x;
   uint32_t off[PER];
 #pragma unroll
@@ -364,45 +381,51 @@ __device__ __forceinline__ bool gather_h(__amdgpu_buffer_rsrc_t xr, int base, un
 }
 
 // dL/dh1 of the own columns = dz2 W2[:, C_d] from the LDS mirror (the
-// weights before this step's update): waves (n-tile w % 2, k half w / 2);
-// waves 0 / 1 return their n-tile's result (lane (i, g): rows 4 g + r, column
-// 16 w + i — layer 1's output layout)
+// weights before this step's update): waves (n-tile w % NT1, k part w / NT1);
+// waves w < NT1 return their n-tile's result (lane (i, g): rows 4 g + r,
+// column 16 w + i — layer 1's output layout)
+template <class G>
 __device__ __forceinline__ f32x4 backward_dh1(const float* sDZ, const float* sW2, float* sPart, int wv, int lane,
                                               int li, int lg) {
-  const int nt = wv & 1, ks = wv >> 1;
+  constexpr int NT1 = G::NT1, KW = kH2 / G::KS, LW = G::LW;
+  const int nt = wv % NT1, ks = wv / NT1;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int kk = 0; kk < 64; kk += 16) {
-    const int k0 = 64 * ks + kk;
+  for (int kk = 0; kk < KW; kk += 16) {
+    const int k0 = KW * ks + kk;
     const f4 x = *(const f4*)(sDZ + li * LZ + k0 + 4 * lg);
     const float* wc = sW2 + (k0 + 4 * lg) * LW + 16 * nt + li;
     const f4 w = {wc[0], wc[LW], wc[2 * LW], wc[3 * LW]};
     acc = m16x4(x, w, acc);
   }
-  if (ks) *(f32x4*)(sPart + ((wv - 2) * 64 + lane) * 4) = acc;
+  if (ks) *(f32x4*)(sPart + ((wv - NT1) * 64 + lane) * 4) = acc;
   __syncthreads();
-  if (!ks) acc += *(const f32x4*)(sPart + (wv * 64 + lane) * 4);
+  if (!ks) {
+#pragma unroll
+    for (int j = 1; j < G::KS; ++j) acc += *(const f32x4*)(sPart + ((j * NT1 + wv - NT1) * 64 + lane) * 4);
+  }
   return acc;
 }
 
 // dW2^T tiles (column tile mk, unit tile nt = wv + 4 q) = h1^T dz2 and their
 // Adam steps on the register slice; the mirror rewritten
-__device__ __forceinline__ void dw2_adam(W2Reg& W, W2Reg& Mo, W2Reg& Vo, const float* sHT, const float* sDZT,
-                                         float* sW2, float alpha, float b1c, float b2c, float eps, int wv, int li,
-                                         int lg) {
+template <class G>
+__device__ __forceinline__ void dw2_adam(W2Reg<G>& W, W2Reg<G>& Mo, W2Reg<G>& Vo, const float* sHT,
+                                         const float* sDZT, float* sW2, float alpha, float b1c, float b2c, float eps,
+                                         int wv, int li, int lg) {
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int nt = wv + 4 * q;
     const f4 dz = *(const f4*)(sDZT + (16 * nt + li) * LZT + 4 * lg);
 #pragma unroll
-    for (int mk = 0; mk < 2; ++mk) {
+    for (int mk = 0; mk < G::NT1; ++mk) {
       const f4 h = *(const f4*)(sHT + (16 * mk + li) * LHT + 4 * lg);
       f32x4 g = {0.f, 0.f, 0.f, 0.f};
       g = m16x4(h, dz, g);
       adam4(W.w[q][mk], Mo.w[q][mk], Vo.w[q][mk], g, alpha, b1c, b2c, eps);
     }
   }
-  w2_mirror(W, sW2, wv, li, lg);
+  w2_mirror<G>(W, sW2, wv, li, lg);
 }
 
 // dW1^T of n-tile wv (waves 0 / 1) = s_ext^T dz1 and its Adam step: lane (i,
@@ -428,8 +451,9 @@ __device__ __forceinline__ void dw1_adam(f4& w1, f4& m1, f4& v1, f4 dz1, const f
 
 // the Dropout bits of layer-1 unit C d + c, rows 4 g .. 4 g + 3, for call
 // number `call` (rng.dropout_keep's keys: (row >> 2, unit, call); word row & 3)
+template <class G>
 __device__ __forceinline__ uint4 drop_bits(const FitArgs& a, uint64_t call, int d, int c, int lg) {
-  return skmlp::philox<10>(make_uint4((uint32_t)lg, (uint32_t)(C * d + c), (uint32_t)call, (uint32_t)(call >> 32)),
+  return skmlp::philox<10>(make_uint4((uint32_t)lg, (uint32_t)(G::C * d + c), (uint32_t)call, (uint32_t)(call >> 32)),
                            (uint32_t)a.drop_seed, (uint32_t)(a.drop_seed >> 32));
 }
 
@@ -451,45 +475,54 @@ constexpr int uW3 = 0, uB2 = kH2, uWA = 2 * kH2, uB3 = 4 * kH2, kUN = 4 * kH2 + 
 // per-step buffers, two of each (step k uses k & 1, so the next step's rows
 // and layer-1 activations never wait for this step's last readers):
 // rows [s_ext 16 x 16 | a 16 x 2 | y 16], activations [hd 16 x LH | hd^T C x LHT]
-constexpr int kRowsN = kB * LS + 2 * kB + kB, kActN = kB * LH + C * LHT;
-constexpr int cRows = 3 * kUN, cAct = cRows + 2 * kRowsN, cDQ = cAct + 2 * kActN, cL = cDQ + kB,
-              cH2 = cL + kB, cDZ = cH2 + kB * LZ, cDZT = cDZ + kB * LZ, cW2 = cDZT + kH2 * LZT,
-              cPart = cW2 + kH2 * LW, cAlpha = cPart + 2 * 64 * 4, cEnd = cAlpha + kAlphaN;
-constexpr size_t kCriticLds = (size_t)cEnd * 4;
-// exchanges (granules): R [P src][P dst][U][16], H [P][U][16]
-constexpr int cxR = 0, cxH = cxR + P * P * U * 16, cxN = cxH + P * U * 16;
-static_assert(kCriticLds <= 150 * 1024, "LDS");
+template <class G>
+struct CriticLayout {
+  static constexpr int kRowsN = kB * LS + 2 * kB + kB, kActN = kB * G::LH + G::C * LHT;
+  static constexpr int cRows = 3 * kUN, cAct = cRows + 2 * kRowsN, cDQ = cAct + 2 * kActN, cL = cDQ + kB,
+                       cH2 = cL + kB, cDZ = cH2 + kB * LZ, cDZT = cDZ + kB * LZ, cW2 = cDZT + kH2 * LZT,
+                       cPart = cW2 + kH2 * G::LW, cAlpha = cPart + 3 * 64 * 4, cEnd = cAlpha + kAlphaN;
+  static constexpr size_t kLds = (size_t)cEnd * 4;
+  // exchanges (granules): R [P src][P dst][U][16], H [P][U][16]
+  static constexpr int cxR = 0, cxH = cxR + G::P * G::P * G::U * 16, cxN = cxH + G::P * G::U * 16;
+  static_assert(kLds <= 150 * 1024 && cxN <= 65536, "LDS / xbuf");
+};
 
+template <int PW>
 __global__ void __launch_bounds__(kT) k_fit_critic(FitArgs a) {
+  using G = Geo<PW>;
+  using Y = CriticLayout<G>;
+  constexpr int P = G::P, U = G::U, LH = G::LH, NT1 = G::NT1;
+  constexpr int kRowsN = Y::kRowsN, kActN = Y::kActN, cRows = Y::cRows, cAct = Y::cAct, cxR = Y::cxR,
+                cxH = Y::cxH;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   SK_FT_DECL
   if (blockIdx.x % a.stride) return;
   float* uW = sm;
   float* uM = sm + kUN;
   float* uV = sm + 2 * kUN;
-  float* sDQ = sm + cDQ;
-  float* sL = sm + cL;
-  float* sH2 = sm + cH2;
-  float* sAlpha = sm + cAlpha;
-  float* sDZ = sm + cDZ;
-  float* sDZT = sm + cDZT;
-  float* sW2 = sm + cW2;
-  float* sPart = sm + cPart;
+  float* sDQ = sm + Y::cDQ;
+  float* sL = sm + Y::cL;
+  float* sH2 = sm + Y::cH2;
+  float* sAlpha = sm + Y::cAlpha;
+  float* sDZ = sm + Y::cDZ;
+  float* sDZT = sm + Y::cDZT;
+  float* sW2 = sm + Y::cW2;
+  float* sPart = sm + Y::cPart;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, li = lane & 15, lg = lane >> 4;
   const int d = blockIdx.x / a.stride;
   const __amdgpu_buffer_rsrc_t xr = rsrc_of(a.xbuf);
 
   // the owned slice: W2 (+ moments) and W1 | b1 in registers; every unit parameter in LDS
-  W2Reg W2, M2, V2;
-  w2_load<kCLd>(W2, a.flat, d, wv, li, lg);
-  w2_load<kCLd>(M2, a.m, d, wv, li, lg);
-  w2_load<kCLd>(V2, a.v, d, wv, li, lg);
-  w2_mirror(W2, sW2, wv, li, lg);
+  W2Reg<G> W2, M2, V2;
+  w2_load<G, kCLd>(W2, a.flat, d, wv, li, lg);
+  w2_load<G, kCLd>(M2, a.m, d, wv, li, lg);
+  w2_load<G, kCLd>(V2, a.v, d, wv, li, lg);
+  w2_mirror<G>(W2, sW2, wv, li, lg);
   f4 W1 = {0.f, 0.f, 0.f, 0.f}, M1 = W1, V1 = W1;
-  if (wv < 2) {
-    W1 = w1_load(a.flat, d, wv, li, lg);
-    M1 = w1_load(a.m, d, wv, li, lg);
-    V1 = w1_load(a.v, d, wv, li, lg);
+  if (wv < NT1) {
+    W1 = w1_load<G>(a.flat, d, wv, li, lg);
+    M1 = w1_load<G>(a.m, d, wv, li, lg);
+    V1 = w1_load<G>(a.v, d, wv, li, lg);
   }
   if (t < kH2) {
     const int gi[4] = {kCW3 + t, kCB2 + t, kW2 + t * kCLd + kH1, kW2 + t * kCLd + kH1 + 1};
@@ -518,9 +551,9 @@ __global__ void __launch_bounds__(kT) k_fit_critic(FitArgs a) {
   if (t < kB) sm[cRows + kB * LS + 2 * kB + t] = a.targets[t];
   const float b1c = 1.f - a.beta1, b2c = 1.f - a.beta2;
   bool fail = false;  // this thread's exchange ran out of spins (decided uniformly at the barriers)
-  // waves 0 / 1: this step's Dropout bits (the next step's are drawn in the R wait)
+  // waves w < NT1: this step's Dropout bits (the next step's are drawn in the R wait)
   uint4 bits = {0u, 0u, 0u, 0u};
-  if (wv < 2) bits = drop_bits(a, (uint64_t)call0, d, 16 * wv + li, lg);
+  if (wv < NT1) bits = drop_bits<G>(a, (uint64_t)call0, d, 16 * wv + li, lg);
 
   for (int k = 0; k < a.M; ++k) {
     const unsigned E = ep0 + 2u * (unsigned)k;
@@ -543,9 +576,9 @@ __global__ void __launch_bounds__(kT) k_fit_critic(FitArgs a) {
     }
 
     // (1) layer 1 of the own units with Dropout (SkillshotLearner.py:106-108):
-    //     waves 0 / 1, one n-tile each; one Philox call gives the 4 rows' bits
+    //     waves w < NT1, one n-tile each; one Philox call gives the 4 rows' bits
     f4 mask = {0.f, 0.f, 0.f, 0.f};
-    if (wv < 2) {
+    if (wv < NT1) {
       const f32x4 z = layer1(sS, W1, li, lg);
       const int c = 16 * wv + li;
       const uint32_t bw[4] = {bits.x, bits.y, bits.z, bits.w};
@@ -564,16 +597,18 @@ __global__ void __launch_bounds__(kT) k_fit_critic(FitArgs a) {
 
     // (2) the layer-2 partial products of the own columns for all 128 units,
     //     each 16-unit tile to its summer: slice (d -> e) = [U units][16 rows]
-    partials_publish(sHD, W2, xr, E + 1, wv, li, lg, [&](int e) { return cxR + (d * P + e) * U * 16; });
+    partials_publish<G>(sHD, W2, xr, E + 1, wv, li, lg, [&](int e) { return cxR + (d * P + e) * U * 16; });
     SK_FT(k, 2);
 
-    // (3) workgroup d sums the 8 slices of units U_d (source order), adds b2
+    // (3) workgroup d sums the P slices of units U_d (source order), adds b2
     //     and the action columns: h2 = relu(z2), published to all (H); the
-    //     next step's Dropout bits first (VALU work hidden by the wait)
+    //     next step's Dropout bits first (VALU work hidden by the wait; the
+    //     summing lanes t < 8 U are the layer-1 waves w < NT1)
+    static_assert(U * 8 == NT1 * 64, "the summing waves are the layer-1 waves");
     if (t < U * 8) {
-      if (more) bits = drop_bits(a, (uint64_t)(call0 + k + 1), d, 16 * wv + li, lg);
+      if (more) bits = drop_bits<G>(a, (uint64_t)(call0 + k + 1), d, 16 * wv + li, lg);
       float z0, z1;
-      fail |= !r_sum(xr, E + 1, t, [&](int s) { return cxR + (s * P + d) * U * 16; }, z0, z1, a.timeout);
+      fail |= !r_sum<G>(xr, E + 1, t, [&](int s) { return cxR + (s * P + d) * U * 16; }, z0, z1, a.timeout);
       const int ug = U * d + (2 * t) / 16, r0 = (2 * t) % 16;
       const float b2 = uW[uB2 + ug], wa0 = uW[uWA + 2 * ug], wa1 = uW[uWA + 2 * ug + 1];
       z0 = z0 + sA[2 * r0] * wa0 + sA[2 * r0 + 1] * wa1 + b2;
@@ -585,7 +620,7 @@ __global__ void __launch_bounds__(kT) k_fit_critic(FitArgs a) {
     // (4) h2 of all 128 units
     {
       float* const dst[1] = {sH2};
-      fail |= !gather_h<1>(xr, cxH, E + 2, dst, a.timeout);
+      fail |= !gather_h<G, 1>(xr, cxH, E + 2, dst, a.timeout);
     }
     if (__syncthreads_or(fail)) break;  // a lost exchange ends the launch (uniformly)
     SK_FT(k, 4);
@@ -629,12 +664,13 @@ __global__ void __launch_bounds__(kT) k_fit_critic(FitArgs a) {
     //     dz1 = dh1d x the Dropout / relu mask, (8) dW1 | db1 and their Adam
     //     steps on registers; (9) dW2[:, C_d] and its Adam steps in the
     //     epilogue (the W2 mirror's reads by (7) are behind its barrier)
-    const f32x4 dh = backward_dh1(sDZ, sW2, sPart, wv, lane, li, lg);
+    const f32x4 dh = backward_dh1<G>(sDZ, sW2, sPart, wv, lane, li, lg);
     SK_FT(k, 6);
-    if (wv < 2) {
+    if (wv < NT1) {
       const f4 dz1 = {dh[0] * mask[0], dh[1] * mask[1], dh[2] * mask[2], dh[3] * mask[3]};
       dw1_adam(W1, M1, V1, dz1, sS, alpha, b1c, b2c, a.eps, li, lg);
-    } else {
+    }
+    if (wv >= 2) {
       // (6) meanwhile waves 2 / 3: the unit parameters' 16-row gradient sums
       //     (one unit per lane) and Adam steps (every W3 / b2 / W2A read of
       //     this step is behind the barriers above; the next are behind the
@@ -660,7 +696,7 @@ __global__ void __launch_bounds__(kT) k_fit_critic(FitArgs a) {
     }
     SK_FT(k, 7);
     SK_FT(k, 8);
-    dw2_adam(W2, M2, V2, sHDT, sDZT, sW2, alpha, b1c, b2c, a.eps, wv, li, lg);
+    dw2_adam<G>(W2, M2, V2, sHDT, sDZT, sW2, alpha, b1c, b2c, a.eps, wv, li, lg);
     SK_FT(k, 9);
     SK_FT(k, 10);
     // no barrier: the next step writes only the other buffers before its first
@@ -670,13 +706,13 @@ __global__ void __launch_bounds__(kT) k_fit_critic(FitArgs a) {
   SK_FT_FLUSH();
 
   // the owned slice back; workgroup 0 the unit parameters and the counters
-  w2_store<kCLd>(W2, a.flat, d, wv, li, lg);
-  w2_store<kCLd>(M2, a.m, d, wv, li, lg);
-  w2_store<kCLd>(V2, a.v, d, wv, li, lg);
-  if (wv < 2) {
-    w1_store(W1, a.flat, d, wv, li, lg);
-    w1_store(M1, a.m, d, wv, li, lg);
-    w1_store(V1, a.v, d, wv, li, lg);
+  w2_store<G, kCLd>(W2, a.flat, d, wv, li, lg);
+  w2_store<G, kCLd>(M2, a.m, d, wv, li, lg);
+  w2_store<G, kCLd>(V2, a.v, d, wv, li, lg);
+  if (wv < NT1) {
+    w1_store<G>(W1, a.flat, d, wv, li, lg);
+    w1_store<G>(M1, a.m, d, wv, li, lg);
+    w1_store<G>(V1, a.v, d, wv, li, lg);
   }
   __syncthreads();
   if (d == 0) {
@@ -772,17 +808,27 @@ constexpr int aW3 = 0, aB2 = 2 * kH2, aB3 = 3 * kH2, kAUN = 3 * kH2 + 4;  // act
 constexpr int qW3 = 0, qWA = kH2, kQUN = 3 * kH2;                         // critic units (frozen): W3, W2A [128][2]
 // two of each per-step buffer (as the critic's): rows [s_ext 16 x 16],
 // activations [h1 16 x LH | its transpose C x LHT], the critic's zc [16 x LZ]
-constexpr int kARowsN = kB * LS, kAActN = kB * LH + C * LHT;
-constexpr int xS = 3 * kAUN + kQUN, xAct = xS + 2 * kARowsN, xZC = xAct + 2 * kAActN, xDZ3 = xZC + 2 * kB * LZ,
-              xH2 = xDZ3 + 2 * kB, xDZ = xH2 + kB * LZ, xDZT = xDZ + kB * LZ, xW2 = xDZT + kH2 * LZT,
-              xPart = xW2 + kH2 * LW, xAlpha = xPart + 2 * 64 * 4, xEnd = xAlpha + kAlphaN;
-constexpr size_t kActorLds = (size_t)xEnd * 4;
-// exchanges: R [P src][P dst][U][16], H [P][U][16]
-constexpr int axR = 0, axH = axR + P * P * U * 16, axN = axH + P * U * 16;
-static_assert(kActorLds <= 150 * 1024, "LDS");
+template <class G>
+struct ActorLayout {
+  static constexpr int kARowsN = kB * LS, kAActN = kB * G::LH + G::C * LHT;
+  static constexpr int xS = 3 * kAUN + kQUN, xAct = xS + 2 * kARowsN, xZC = xAct + 2 * kAActN,
+                       xDZ3 = xZC + 2 * kB * LZ, xH2 = xDZ3 + 2 * kB, xDZ = xH2 + kB * LZ, xDZT = xDZ + kB * LZ,
+                       xW2 = xDZT + kH2 * LZT, xPart = xW2 + kH2 * G::LW, xAlpha = xPart + 3 * 64 * 4,
+                       xEnd = xAlpha + kAlphaN;
+  static constexpr size_t kLds = (size_t)xEnd * 4;
+  // exchanges: R [P src][P dst][U][16], H [P][U][16]
+  static constexpr int axR = 0, axH = axR + G::P * G::P * G::U * 16, axN = axH + G::P * G::U * 16;
+  static_assert(kLds <= 150 * 1024 && axN <= 65536, "LDS / xbuf");
+};
 constexpr int kZPer = kB * kH2 / kT;  // zc floats per thread and step
 
+template <int PW>
 __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a, const float* __restrict__ zc) {
+  using G = Geo<PW>;
+  using Y = ActorLayout<G>;
+  constexpr int P = G::P, U = G::U, LH = G::LH, NT1 = G::NT1;
+  constexpr int kARowsN = Y::kARowsN, kAActN = Y::kAActN, xS = Y::xS, xAct = Y::xAct, xZC = Y::xZC,
+                axR = Y::axR, axH = Y::axH;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   SK_FT_DECL
   if (blockIdx.x % a.stride) return;
@@ -790,28 +836,28 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a, const float* __rest
   float* uM = sm + kAUN;
   float* uV = sm + 2 * kAUN;
   float* qU = sm + 3 * kAUN;
-  float* sDZ3 = sm + xDZ3;
-  float* sH2 = sm + xH2;
-  float* sDZ = sm + xDZ;
-  float* sDZT = sm + xDZT;
-  float* sW2 = sm + xW2;
-  float* sPart = sm + xPart;
-  float* sAlpha = sm + xAlpha;
+  float* sDZ3 = sm + Y::xDZ3;
+  float* sH2 = sm + Y::xH2;
+  float* sDZ = sm + Y::xDZ;
+  float* sDZT = sm + Y::xDZT;
+  float* sW2 = sm + Y::xW2;
+  float* sPart = sm + Y::xPart;
+  float* sAlpha = sm + Y::xAlpha;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, li = lane & 15, lg = lane >> 4;
   const int d = blockIdx.x / a.stride;
   const __amdgpu_buffer_rsrc_t xr = rsrc_of(a.xbuf);
 
-  W2Reg W2, M2, V2;
-  w2_load<kH1>(W2, a.flat, d, wv, li, lg);
-  w2_load<kH1>(M2, a.m, d, wv, li, lg);
-  w2_load<kH1>(V2, a.v, d, wv, li, lg);
-  w2_mirror(W2, sW2, wv, li, lg);
-  // waves 0 / 1: the actor's W1 | b1 (n-tile wv)
+  W2Reg<G> W2, M2, V2;
+  w2_load<G, kH1>(W2, a.flat, d, wv, li, lg);
+  w2_load<G, kH1>(M2, a.m, d, wv, li, lg);
+  w2_load<G, kH1>(V2, a.v, d, wv, li, lg);
+  w2_mirror<G>(W2, sW2, wv, li, lg);
+  // waves w < NT1: the actor's W1 | b1 (n-tile wv)
   f4 W1 = {0.f, 0.f, 0.f, 0.f}, M1 = W1, V1 = W1;
-  if (wv < 2) {
-    W1 = w1_load(a.flat, d, wv, li, lg);
-    M1 = w1_load(a.m, d, wv, li, lg);
-    V1 = w1_load(a.v, d, wv, li, lg);
+  if (wv < NT1) {
+    W1 = w1_load<G>(a.flat, d, wv, li, lg);
+    M1 = w1_load<G>(a.m, d, wv, li, lg);
+    V1 = w1_load<G>(a.v, d, wv, li, lg);
   }
   if (t < kH2) {
     const int gi[3] = {kAW3 + t, kAW3 + kH2 + t, kAB2 + t};
@@ -865,9 +911,9 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a, const float* __rest
       for (int i = 0; i < kZPer; ++i) nz[i] = zc[(int64_t)(k + 1) * kB * kH2 + t + kT * i];
     }
 
-    // (1) layer 1 of the own units on waves 0 / 1 (the relu mask kept in registers)
+    // (1) layer 1 of the own units on waves w < NT1 (the relu mask kept in registers)
     f4 hmask = {0.f, 0.f, 0.f, 0.f};
-    if (wv < 2) {
+    if (wv < NT1) {
       const f32x4 z = layer1(sS, W1, li, lg);
       const int c = 16 * wv + li;
       f4 h;
@@ -883,13 +929,13 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a, const float* __rest
     SK_FT(k, 1);
 
     // (2) the layer-2 partials over the own columns, to the unit summers
-    partials_publish(sH1, W2, xr, E + 1, wv, li, lg, [&](int e) { return axR + (d * P + e) * U * 16; });
+    partials_publish<G>(sH1, W2, xr, E + 1, wv, li, lg, [&](int e) { return axR + (d * P + e) * U * 16; });
     SK_FT(k, 2);
 
     // (3) the sums of U_d: h2 = relu(z2 + b2), published to all (H)
     if (t < U * 8) {
       float z0, z1;
-      fail |= !r_sum(xr, E + 1, t, [&](int s) { return axR + (s * P + d) * U * 16; }, z0, z1, a.timeout);
+      fail |= !r_sum<G>(xr, E + 1, t, [&](int s) { return axR + (s * P + d) * U * 16; }, z0, z1, a.timeout);
       const float b2 = uW[aB2 + U * d + (2 * t) / 16];
       put2(xr, (uint32_t)(axH + d * U * 16 + 2 * t) * 8u, E + 2, fmaxf(z0 + b2, 0.f), fmaxf(z1 + b2, 0.f));
     }
@@ -898,7 +944,7 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a, const float* __rest
     // (4) h2 of all 128 units
     {
       float* const dst[1] = {sH2};
-      fail |= !gather_h<1>(xr, axH, E + 2, dst, a.timeout);
+      fail |= !gather_h<G, 1>(xr, axH, E + 2, dst, a.timeout);
     }
     if (__syncthreads_or(fail)) break;
     SK_FT(k, 4);
@@ -954,12 +1000,13 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a, const float* __rest
 
     // (7) dL/dh1[:, C_d], dz1 = dh1 [h1 > 0], dW1 | db1 (waves 0 / 1) and
     //     dW2[:, C_d] with their Adam steps
-    const f32x4 dh = backward_dh1(sDZ, sW2, sPart, wv, lane, li, lg);
+    const f32x4 dh = backward_dh1<G>(sDZ, sW2, sPart, wv, lane, li, lg);
     SK_FT(k, 6);
-    if (wv < 2) {
+    if (wv < NT1) {
       const f4 dz1 = {dh[0] * hmask[0], dh[1] * hmask[1], dh[2] * hmask[2], dh[3] * hmask[3]};
       dw1_adam(W1, M1, V1, dz1, sS, alpha, b1c, b2c, a.eps, li, lg);
-    } else {
+    }
+    if (wv >= 2) {
       // (6) meanwhile waves 2 / 3: the actor's unit parameters' 16-row
       //     gradient sums (one unit per lane) and Adam steps
       const int u = t - 2 * 64;
@@ -981,20 +1028,20 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a, const float* __rest
     }
     SK_FT(k, 7);
     SK_FT(k, 8);
-    dw2_adam(W2, M2, V2, sH1T, sDZT, sW2, alpha, b1c, b2c, a.eps, wv, li, lg);
+    dw2_adam<G>(W2, M2, V2, sH1T, sDZT, sW2, alpha, b1c, b2c, a.eps, wv, li, lg);
     SK_FT(k, 9);
     SK_FT(k, 10);
   }
   const float tk = tk0 + (float)a.M;
   SK_FT_FLUSH();
 
-  w2_store<kH1>(W2, a.flat, d, wv, li, lg);
-  w2_store<kH1>(M2, a.m, d, wv, li, lg);
-  w2_store<kH1>(V2, a.v, d, wv, li, lg);
-  if (wv < 2) {
-    w1_store(W1, a.flat, d, wv, li, lg);
-    w1_store(M1, a.m, d, wv, li, lg);
-    w1_store(V1, a.v, d, wv, li, lg);
+  w2_store<G, kH1>(W2, a.flat, d, wv, li, lg);
+  w2_store<G, kH1>(M2, a.m, d, wv, li, lg);
+  w2_store<G, kH1>(V2, a.v, d, wv, li, lg);
+  if (wv < NT1) {
+    w1_store<G>(W1, a.flat, d, wv, li, lg);
+    w1_store<G>(M1, a.m, d, wv, li, lg);
+    w1_store<G>(V1, a.v, d, wv, li, lg);
   }
   __syncthreads();
   if (d == 0) {
@@ -1019,13 +1066,19 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a, const float* __rest
 }
 
 template <typename K, typename... X>
-int launch_fit(K kernel, size_t lds, bool& attr, const FitArgs& a, hipStream_t st, X... extra) {
+int launch_fit(K kernel, int P, size_t lds, bool& attr, const FitArgs& a, hipStream_t st, X... extra) {
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   kernel<<<P * a.stride, kT, lds, st>>>(a, extra...);
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
+}
+
+// SK_FIT_P: the workgroups per pass (8 or 16; default 16)
+int fit_p() {
+  const char* e = getenv("SK_FIT_P");
+  return (e && atoi(e) == 8) ? 8 : 16;
 }
 
 // SK_FIT_XCD=0 spreads the workgroups over the XCDs (8 blocks); default one
@@ -1046,7 +1099,6 @@ int skdiag_set_fit_trace(void* buf) {
 #endif
 
 size_t sk_fit_xbuf_bytes(void) { return (size_t)65536 * 8; }
-static_assert(cxN <= 65536 && axN <= 65536, "xbuf");
 
 int sk_fit_critic_f32(float* critic_flat, float* m, float* v, float* steps, int32_t n_steps, const float* states,
                       const float* actions, const float* targets, int32_t n_minibatches, uint64_t drop_seed,
@@ -1059,8 +1111,10 @@ int sk_fit_critic_f32(float* critic_flat, float* m, float* v, float* steps, int3
   FitArgs a{critic_flat, m, v, steps, n_steps, states, actions, targets, n_minibatches, drop_seed, drop_calls,
             lr, beta1, beta2, eps, (unsigned long long*)xbuf, (unsigned long long*)epoch, timeout, losses,
             fit_stride(), nullptr};
-  static bool attr = false;
-  return launch_fit(k_fit_critic, kCriticLds, attr, a, (hipStream_t)stream);
+  static bool attr8 = false, attr16 = false;
+  if (fit_p() == 8)
+    return launch_fit(k_fit_critic<8>, 8, CriticLayout<Geo<8>>::kLds, attr8, a, (hipStream_t)stream);
+  return launch_fit(k_fit_critic<16>, 16, CriticLayout<Geo<16>>::kLds, attr16, a, (hipStream_t)stream);
 }
 
 int sk_fit_actor_f32(float* actor_flat, float* adam_m, float* adam_v, float* step_counters, int32_t n_steps,
@@ -1077,8 +1131,10 @@ int sk_fit_actor_f32(float* actor_flat, float* adam_m, float* adam_v, float* ste
   FitArgs a{actor_flat, adam_m, adam_v, step_counters, n_steps, states, nullptr, nullptr, n_minibatches, 0, nullptr,
             lr, beta1, beta2, eps, (unsigned long long*)xbuf, (unsigned long long*)epoch, timeout, nullptr,
             fit_stride(), critic_flat};
-  static bool attr = false;
-  return launch_fit(k_fit_actor, kActorLds, attr, a, st, (const float*)zbuf);
+  static bool attr8 = false, attr16 = false;
+  if (fit_p() == 8)
+    return launch_fit(k_fit_actor<8>, 8, ActorLayout<Geo<8>>::kLds, attr8, a, st, (const float*)zbuf);
+  return launch_fit(k_fit_actor<16>, 16, ActorLayout<Geo<16>>::kLds, attr16, a, st, (const float*)zbuf);
 }
 
 }  // extern "C"

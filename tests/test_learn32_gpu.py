@@ -433,12 +433,12 @@ def _fit_rows(n, seed):
     return s, torch.rand(n, 2, device="cuda", generator=g) * 2 - 1, torch.randn(n, device="cuda", generator=g) * 0.5
 
 
-@pytest.mark.parametrize("xcd", ["1", "0"])
-def test_fit_critic_resident_equals_eager_and_keras(mods, monkeypatch, xcd):
+@pytest.mark.parametrize("p,xcd", [("16", "1"), ("8", "1"), ("16", "0")])
+def test_fit_critic_resident_equals_eager_and_keras(mods, monkeypatch, p, xcd):
     """models_fit's critic pass in resident launches (sk_fit_critic_f32,
-    csrc/sk_fit.hip: the net split over 8 workgroups by layer-2 input
-    columns, three in-launch exchanges per step; on one XCD and spread over
-    the XCDs, SK_FIT_XCD) against one three-launch
+    csrc/sk_fit.hip: the net split over 16 or 8 workgroups by layer-2 input
+    columns, SK_FIT_P, two in-launch exchanges per step; on one XCD and
+    spread over the XCDs, SK_FIT_XCD) against one three-launch
     critic_step per minibatch (sk_critic_grad_f32 + sk_adam_flat) and the
     fp64 Keras restatement, over 96 minibatch steps in two launches (64 +
     32): parameters within 1e-5, Adam moments, step counts, the Dropout call
@@ -446,6 +446,7 @@ def test_fit_critic_resident_equals_eager_and_keras(mods, monkeypatch, xcd):
     learner, kr = mods
     from skillshot_learning_amd import rng
     monkeypatch.setenv("SK_FIT_XCD", xcd)
+    monkeypatch.setenv("SK_FIT_P", p)
     n = 96
     s, a, y = _fit_rows(16 * n, 7)
     dr = _ddpg(learner, seed=3, scale=2.0)
@@ -503,14 +504,17 @@ def test_models_fit_resident_equals_three_launch(mods, monkeypatch):
     assert (a1 - a0).abs().max().item() <= PARAM_ABS
 
 
-def test_fit_actor_resident_equals_eager_and_keras(mods):
+@pytest.mark.parametrize("p", ["16", "8"])
+def test_fit_actor_resident_equals_eager_and_keras(mods, monkeypatch, p):
     """models_fit's actor pass in resident launches (sk_fit_actor_f32: the
-    actor and the frozen critic split over 8 workgroups by layer-2 input
-    columns, four in-launch exchanges per step) against one three-launch
+    frozen critic's pre-activations computed up front, the actor split over
+    16 or 8 workgroups by layer-2 input columns, two in-launch exchanges per
+    step) against one three-launch
     model_actor_fit_step per minibatch and the fp64 Keras restatement, over
     96 minibatch steps in two launches: parameters within 1e-5, Adam step
     counts equal, the critic untouched, the split pack rewritten"""
     learner, kr = mods
+    monkeypatch.setenv("SK_FIT_P", p)
     n = 96
     s, _, _ = _fit_rows(16 * n, 11)
     dr = _ddpg(learner, seed=5, scale=2.0)

@@ -1,7 +1,7 @@
 """models_fit's per-minibatch-step time (the reference rule's fit,
 SkillshotLearner.py:419-443): the resident critic and
-actor passes (sk_fit_critic_f32, sk_fit_actor_f32) per workgroup placement
-(SK_FIT_XCD), against the
+actor passes (sk_fit_critic_f32, sk_fit_actor_f32) per workgroup count
+(SK_FIT_P) and placement (SK_FIT_XCD), against the
 three-launch steps replayed as captured chunks of 64 (the round-4 path);
 HIP events, one JSON line per configuration.
 
@@ -45,15 +45,15 @@ def main():
         return e0.elapsed_time(e1) * 1e3 / steps
 
     for rep in range(a.reps):
-        for xcd in ("1", "0"):
-            os.environ["SK_FIT_XCD"] = xcd
+        for P, xcd in (("16", "1"), ("8", "1"), ("16", "0")):
+            os.environ["SK_FIT_P"], os.environ["SK_FIT_XCD"] = P, xcd
             us = timed(lambda: fu.fit_critic(S, A, R), n)
             fu.fit_check()
-            print(json.dumps(dict(kind="resident critic", P=8, one_xcd=xcd == "1", steps=n,
+            print(json.dumps(dict(kind="resident critic", P=int(P), one_xcd=xcd == "1", steps=n,
                                   us_per_step=round(us, 3), rep=rep)), flush=True)
             us = timed(lambda: fu.fit_actor(S), n)
             fu.fit_check()
-            print(json.dumps(dict(kind="resident actor", P=8, one_xcd=xcd == "1", steps=n,
+            print(json.dumps(dict(kind="resident actor", P=int(P), one_xcd=xcd == "1", steps=n,
                                   us_per_step=round(us, 3), rep=rep)), flush=True)
         M = d.FIT_CHUNK
         chunks = n // M - 1

@@ -29,7 +29,8 @@ def main():
     fu.soft_update_in_adam = False
     L = fu.L
     L.skdiag_set_fit_trace.argtypes = [ctypes.c_void_p]
-    buf = torch.zeros(8 * 32 * 12, dtype=torch.int64, device=dev)
+    P = int(os.environ.get("SK_FIT_P", "16"))
+    buf = torch.zeros(P * 32 * 12, dtype=torch.int64, device=dev)
     assert L.skdiag_set_fit_trace(ctypes.c_void_p(buf.data_ptr())) == 0
     n = 256
     g = torch.Generator(device=dev).manual_seed(1)
@@ -44,7 +45,7 @@ def main():
         fn()
         torch.cuda.synchronize()
         fu.fit_check()
-        ts = buf.view(8, 32, 12).cpu().numpy().astype(np.int64)
+        ts = buf.view(P, 32, 12).cpu().numpy().astype(np.int64)
         ph = np.diff(ts[:, :, :11], axis=2) * 0.01  # us: phases 0..9
         tail = np.zeros_like(ph[:, :, :1])
         tail[:, :-1, 0] = (ts[:, 1:, 0] - ts[:, :-1, 10]) * 0.01  # stamp 10 to the next step's 0
