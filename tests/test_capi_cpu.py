@@ -148,3 +148,26 @@ def test_gpu_only_entry_points_refuse_the_cpu_backend():
     assert rc == _capi.SK_EINVAL and b"GPU" in L.sk_last_error()
     assert L.sk_env_destroy(h) == _capi.SK_OK
     assert L.sk_actor_split_pack_bytes() == 4 * (8 * 64 * 8 + 4 * 16 * 64 * 8) * 2
+
+
+def test_resident_fit_rejects_bad_arguments():
+    """sk_fit_critic_f32 / sk_fit_actor_f32 (ABI 10, models_fit's resident
+    passes) check their arguments before any launch: missing buffers, no
+    minibatch, a step-counter count outside [1, 64] or an exchange buffer off
+    its 16-byte alignment are SK_EINVAL (the dummy pointers are never
+    dereferenced, so no GPU is needed); the exchange buffer's size is fixed"""
+    L = ssa.load_library()
+    f = ctypes.c_void_p(0x1000)
+    off = ctypes.c_void_p(0x1008)
+    assert L.sk_fit_xbuf_bytes() == 65536 * 8
+
+    def critic(xbuf=f, n=4, n_steps=1, targets=f):
+        return L.sk_fit_critic_f32(f, f, f, f, n_steps, f, f, targets, n, 0, f, 1e-3, 0.9, 0.999, 1e-7, xbuf, f, f,
+                                   None, None)
+
+    def actor(xbuf=f, n=4, n_steps=1, zbuf=f):
+        return L.sk_fit_actor_f32(f, f, f, f, n_steps, f, f, n, 1e-3, 0.9, 0.999, 1e-7, xbuf, f, f, zbuf, None)
+
+    for rc in (critic(n=0), critic(n_steps=0), critic(n_steps=65), critic(xbuf=None), critic(xbuf=off),
+               critic(targets=None), actor(n=0), actor(n_steps=0), actor(xbuf=off), actor(zbuf=None)):
+        assert rc == _capi.SK_EINVAL
