@@ -207,7 +207,7 @@ struct FitArgs {
   unsigned long long* epoch;
   unsigned* timeout;
   float* losses;         // [M] per-step MSE (nullable; critic)
-  int stride;            // grid = 8 x stride; blocks b % stride == 0 work (stride 8: one XCD under
+  int stride;            // grid = P x stride; blocks b % stride == 0 work (stride 8: one XCD under
                          // round-robin placement, a speed choice only, never correctness)
   const float* critic;   // the actor pass: the (frozen) critic's flat parameters
 };
@@ -750,8 +750,9 @@ __global__ void __launch_bounds__(kT) k_fit_critic(FitArgs a) {
 // running the critic's layers 1 and 2 in the chain.  The actor itself takes
 // the critic kernel's column split: workgroup d owns the actor's W1 | b1 of
 // C_d and W2[:, C_d] in registers; its unit parameters (b2, W3, b3 with their
-// moments) and the critic's (W3, action columns) are in every workgroup's
-// LDS.  R reduce-scatters the actor's layer-2 partials, H all-gathers its
+// moments) are in every workgroup's LDS, and each lane holds the critic's
+// (W3, action columns) of the 8 units it reduces over in registers for the
+// launch.  R reduce-scatters the actor's layer-2 partials, H all-gathers its
 // h2; then every workgroup forms a = tanh(z3), the critic's dQ/da at (s, a),
 // the actor's dL/dz2 and its unit parameters' Adam steps itself.
 
@@ -805,13 +806,12 @@ __global__ void __launch_bounds__(kT) k_fit_critic_z2(const float* __restrict__ 
 }
 
 constexpr int aW3 = 0, aB2 = 2 * kH2, aB3 = 3 * kH2, kAUN = 3 * kH2 + 4;  // actor units: W3 [128][2], b2, b3[2]
-constexpr int qW3 = 0, qWA = kH2, kQUN = 3 * kH2;                         // critic units (frozen): W3, W2A [128][2]
 // two of each per-step buffer (as the critic's): rows [s_ext 16 x 16],
 // activations [h1 16 x LH | its transpose C x LHT], the critic's zc [16 x LZ]
 template <class G>
 struct ActorLayout {
   static constexpr int kARowsN = kB * LS, kAActN = kB * G::LH + G::C * LHT;
-  static constexpr int xS = 3 * kAUN + kQUN, xAct = xS + 2 * kARowsN, xZC = xAct + 2 * kAActN,
+  static constexpr int xS = 3 * kAUN, xAct = xS + 2 * kARowsN, xZC = xAct + 2 * kAActN,
                        xDZ3 = xZC + 2 * kB * LZ, xH2 = xDZ3 + 2 * kB, xDZ = xH2 + kB * LZ, xDZT = xDZ + kB * LZ,
                        xW2 = xDZT + kH2 * LZT, xPart = xW2 + kH2 * G::LW, xAlpha = xPart + 3 * 64 * 4,
                        xEnd = xAlpha + kAlphaN;
@@ -835,7 +835,6 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a, const float* __rest
   float* uW = sm;
   float* uM = sm + kAUN;
   float* uV = sm + 2 * kAUN;
-  float* qU = sm + 3 * kAUN;
   float* sDZ3 = sm + Y::xDZ3;
   float* sH2 = sm + Y::xH2;
   float* sDZ = sm + Y::xDZ;
@@ -868,9 +867,6 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a, const float* __rest
       uM[l3[j]] = a.m[gi[j]];
       uV[l3[j]] = a.v[gi[j]];
     }
-    qU[qW3 + t] = a.critic[kCW3 + t];
-    qU[qWA + 2 * t] = a.critic[kW2 + t * kCLd + kH1];
-    qU[qWA + 2 * t + 1] = a.critic[kW2 + t * kCLd + kH1 + 1];
   } else if (t < kH2 + 2) {
     const int j = t - kH2;
     uW[aB3 + j] = a.flat[kAB3 + j];
@@ -891,6 +887,15 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a, const float* __rest
   }
   const float b1c = 1.f - a.beta1, b2c = 1.f - a.beta2;
   bool fail = false;
+  // the frozen critic's unit parameters of this lane's 8 units (t % 16 + 16 i), held for the launch
+  float cwa0[8], cwa1[8], cw3[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int u = (t & 15) + 16 * i;
+    cw3[i] = a.critic[kCW3 + u];
+    cwa0[i] = a.critic[kW2 + u * kCLd + kH1];
+    cwa1[i] = a.critic[kW2 + u * kCLd + kH1 + 1];
+  }
 
   for (int k = 0; k < a.M; ++k) {
     const unsigned E = ep0 + 2u * (unsigned)k;
@@ -976,9 +981,9 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a, const float* __rest
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int u = j + 16 * i;
-        const float wa0 = qU[qWA + 2 * u], wa1 = qU[qWA + 2 * u + 1];
+        const float wa0 = cwa0[i], wa1 = cwa1[i];
         const float z = sZC[r * LZ + u] + a0 * wa0 + a1 * wa1;
-        const float dz = z > 0.f ? qU[qW3 + u] : 0.f;
+        const float dz = z > 0.f ? cw3[i] : 0.f;
         g0 += dz * wa0;
         g1 += dz * wa1;
       }
@@ -1081,11 +1086,14 @@ int fit_p() {
   return (e && atoi(e) == 8) ? 8 : 16;
 }
 
-// SK_FIT_XCD=0 spreads the workgroups over the XCDs (8 blocks); default one
-// XCD (tools/seam_bench.py: a step's column exchanges 2.9 vs 3.4 us)
+// SK_FIT_XCD=1 places the workgroups on one XCD (a grid of 8 P blocks, every
+// 8th working); default spread over the XCDs (P blocks).  At 8 workgroups the
+// exchanges alone favour one XCD (tools/seam_bench.py: 2.9 vs 3.4 us per
+// step), but the 16-workgroup passes run faster spread: critic 5.25-5.30 vs
+// 5.32-5.36 us, actor 5.87-5.91 vs 6.0-6.5 (profiles/r05u_bench_fit.jsonl)
 int fit_stride() {
   const char* e = getenv("SK_FIT_XCD");
-  return (e && atoi(e) == 0) ? 1 : 8;
+  return (e && atoi(e) == 1) ? 8 : 1;
 }
 
 }  // namespace
