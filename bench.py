@@ -649,8 +649,9 @@ def reference_rule_rate(envs, exploration="param_noise", precision="fp32", fit_c
                collection=dict(kernel="k_act_episode32 (sk_env_act_episode: the whole episode in one launch)",
                                gpu_s=ev, wall_s=wall, env_steps_per_s=played / wall,
                                gpu_us_per_tick=ev * 1e6 / T),
-               fit=dict(batch=b, kernel="k_fit_critic / k_fit_actor (resident: 8 workgroups, one launch per "
-                                        "pass chunk of up to %d minibatches)" % fu.FIT_STEPS_PER_LAUNCH,
+               fit=dict(batch=b, kernel="k_fit_critic / k_fit_actor (resident: %s workgroups, one launch per "
+                                        "pass chunk of up to %d minibatches)"
+                                        % ("8" if os.environ.get("SK_FIT_P") == "8" else "16", fu.FIT_STEPS_PER_LAUNCH),
                         minibatch_steps_timed=2 * n_fit, us_per_critic_step=critic_us, us_per_actor_step=actor_us,
                         us_per_minibatch_step=step_us, steps_per_epoch=2 * steps_per_pass,
                         projected_epoch_fit_s=fit_epoch_s,
