@@ -357,26 +357,39 @@ __device__ __forceinline__ bool r_sum(__amdgpu_buffer_rsrc_t xr, unsigned tag, i
   return ok;
 }
 
-// the H all-gather ([P src][NETS][U][16] granules) into dst[net] [16][LZ]
-template <class G, int NETS>
-__device__ __forceinline__ bool gather_h(__amdgpu_buffer_rsrc_t xr, int base, unsigned tag, float* const (&dst)[NETS],
-                                         unsigned* timeout) {
-  constexpr int U = G::U;
-  constexpr int PER = (G::P * NETS * U * 8) / kT;  // granule pairs per lane
-  const int t = threadIdx.x;
+// The H exchange: each source's [8 row pairs][U units] granule pairs (row
+// pair major), so the rows 4 w .. 4 w + 3 a wave works on are 2 U contiguous
+// pairs per source.  h_pair: the pair index of (source s, row pair rp, unit ul)
+template <class G>
+__device__ __forceinline__ int h_pair(int s, int rp, int ul) {
+  return s * G::U * 8 + rp * G::U + ul;
+}
+// wave w gathers its own rows' h2 (row pairs 2 w, 2 w + 1 of all 128 units)
+// into dst [16][LZ]: its phase-5 reads need no workgroup barrier
+template <class G>
+__device__ __forceinline__ bool gather_h_rows(__amdgpu_buffer_rsrc_t xr, int base, unsigned tag, float* dst, int wv,
+                                              int lane, unsigned* timeout) {
+  constexpr int U = G::U, PER = (G::P * 2 * U) / 64;  // granule pairs per lane
+  static_assert(PER == 4, "256 pairs per wave");
   uint32_t off[PER];
 #pragma unroll
-  for (int j = 0; j < PER; ++j) off[j] = (uint32_t)(base + 2 * (t + kT * j)) * 8u;
+  for (int j = 0; j < PER; ++j) {
+    const int q = lane + 64 * j, s = q / (2 * U), w = q % (2 * U);
+    off[j] = (uint32_t)(base + 2 * h_pair<G>(s, 2 * wv + w / U, w % U)) * 8u;
+  }
   float v[2 * PER];
   const bool ok = get2<PER>(xr, off, tag, v, timeout);
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
-    const int gi = 2 * (t + kT * j);
-    const int s = gi / (NETS * U * 16), rem = gi - s * NETS * U * 16, net = rem / (U * 16),
-              r2 = rem - net * U * 16, u = U * s + r2 / 16, r0 = r2 % 16;
-    dst[net][r0 * LZ + u] = v[2 * j];
-    dst[net][(r0 + 1) * LZ + u] = v[2 * j + 1];
+    const int q = lane + 64 * j, s = q / (2 * U), w = q % (2 * U);
+    const int r0 = 2 * (2 * wv + w / U), u = U * s + w % U;
+    dst[r0 * LZ + u] = v[2 * j];
+    dst[(r0 + 1) * LZ + u] = v[2 * j + 1];
   }
+  // the wave's own LDS writes, in order before its reads (no other wave reads these rows this phase)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   return ok;
 }
 
@@ -613,25 +626,17 @@ __global__ void __launch_bounds__(kT) k_fit_critic(FitArgs a) {
       const float b2 = uW[uB2 + ug], wa0 = uW[uWA + 2 * ug], wa1 = uW[uWA + 2 * ug + 1];
       z0 = z0 + sA[2 * r0] * wa0 + sA[2 * r0 + 1] * wa1 + b2;
       z1 = z1 + sA[2 * r0 + 2] * wa0 + sA[2 * r0 + 3] * wa1 + b2;
-      put2(xr, (uint32_t)(cxH + d * U * 16 + 2 * t) * 8u, E + 2, fmaxf(z0, 0.f), fmaxf(z1, 0.f));
+      put2(xr, (uint32_t)(cxH + 2 * h_pair<G>(d, r0 / 2, ug - U * d)) * 8u, E + 2, fmaxf(z0, 0.f), fmaxf(z1, 0.f));
     }
     SK_FT(k, 3);
 
-    // (4) h2 of all 128 units
-    {
-      float* const dst[1] = {sH2};
-      fail |= !gather_h<G, 1>(xr, cxH, E + 2, dst, a.timeout);
-    }
-    if (__syncthreads_or(fail)) break;  // a lost exchange ends the launch (uniformly)
+    // (4) h2 of all 128 units for this wave's rows
+    fail |= !gather_h_rows<G>(xr, cxH, E + 2, sH2, wv, lane, a.timeout);
     SK_FT(k, 4);
-    if (more) {  // the next step's rows (that buffer's last readers were in step k - 1)
-      float* nS = sm + cRows + ((k + 1) & 1) * kRowsN;
-      if (t < kB * kS) nS[(t / kS) * LS + t % kS] = nx;
-      else if (t < kB * kS + 3 * kB) nS[kB * LS + (t - kB * kS)] = nx;
-    }
 
     // (5) q of the 16 rows, every workgroup: lane (row t / 16, units t % 16 +
-    //     16 i), a DPP row sum; dL/dq = 2 (q - y) / 16; dL/dz2 of all units
+    //     16 i; each wave its own gathered rows), a DPP row sum; dL/dq =
+    //     2 (q - y) / 16; dL/dz2 of all units
     {
       const int r = t >> 4, j = t & 15;
       float qp = 0.f;
@@ -651,8 +656,13 @@ __global__ void __launch_bounds__(kT) k_fit_critic(FitArgs a) {
         sDZT[u * LZT + r] = g;
       }
     }
-    __syncthreads();
+    if (__syncthreads_or(fail)) break;  // a lost exchange ends the launch (uniformly)
     SK_FT(k, 5);
+    if (more) {  // the next step's rows (that buffer's last readers were in step k - 1)
+      float* nS = sm + cRows + ((k + 1) & 1) * kRowsN;
+      if (t < kB * kS) nS[(t / kS) * LS + t % kS] = nx;
+      else if (t < kB * kS + 3 * kB) nS[kB * LS + (t - kB * kS)] = nx;
+    }
     if (a.losses && d == 0 && t == 0) {
       float l = 0.f;
 #pragma unroll
@@ -942,26 +952,14 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a, const float* __rest
       float z0, z1;
       fail |= !r_sum<G>(xr, E + 1, t, [&](int s) { return axR + (s * P + d) * U * 16; }, z0, z1, a.timeout);
       const float b2 = uW[aB2 + U * d + (2 * t) / 16];
-      put2(xr, (uint32_t)(axH + d * U * 16 + 2 * t) * 8u, E + 2, fmaxf(z0 + b2, 0.f), fmaxf(z1 + b2, 0.f));
+      put2(xr, (uint32_t)(axH + 2 * h_pair<G>(d, (t % 8), t / 8)) * 8u, E + 2, fmaxf(z0 + b2, 0.f),
+           fmaxf(z1 + b2, 0.f));
     }
     SK_FT(k, 3);
 
-    // (4) h2 of all 128 units
-    {
-      float* const dst[1] = {sH2};
-      fail |= !gather_h<G, 1>(xr, axH, E + 2, dst, a.timeout);
-    }
-    if (__syncthreads_or(fail)) break;
+    // (4) h2 of all 128 units for this wave's rows
+    fail |= !gather_h_rows<G>(xr, axH, E + 2, sH2, wv, lane, a.timeout);
     SK_FT(k, 4);
-    if (more) {  // the next step's rows and zc (those buffers' last readers were in step k - 1)
-      if (t < kB * kS) sm[xS + ((k + 1) & 1) * kARowsN + (t / kS) * LS + t % kS] = nx;
-      float* nZ = sm + xZC + ((k + 1) & 1) * kB * LZ;
-#pragma unroll
-      for (int i = 0; i < kZPer; ++i) {
-        const int idx = t + kT * i;
-        nZ[(idx / kH2) * LZ + idx % kH2] = nz[i];
-      }
-    }
 
     // (5) every workgroup, lane (row t / 16, units t % 16 + 16 i), DPP row
     //     sums: z3 -> a = tanh(z3); the critic at (s, a): dQ/dz2 = W3 [z2 > 0],
@@ -1000,8 +998,17 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a, const float* __rest
         sDZT[u * LZT + r] = g;
       }
     }
-    __syncthreads();
+    if (__syncthreads_or(fail)) break;  // a lost exchange ends the launch (uniformly)
     SK_FT(k, 5);
+    if (more) {  // the next step's rows and zc (those buffers' last readers were in step k - 1)
+      if (t < kB * kS) sm[xS + ((k + 1) & 1) * kARowsN + (t / kS) * LS + t % kS] = nx;
+      float* nZ = sm + xZC + ((k + 1) & 1) * kB * LZ;
+#pragma unroll
+      for (int i = 0; i < kZPer; ++i) {
+        const int idx = t + kT * i;
+        nZ[(idx / kH2) * LZ + idx % kH2] = nz[i];
+      }
+    }
 
     // (7) dL/dh1[:, C_d], dz1 = dh1 [h1 > 0], dW1 | db1 (waves 0 / 1) and
     //     dW2[:, C_d] with their Adam steps
