@@ -537,6 +537,10 @@ __global__ void __launch_bounds__(kT) k_fit_critic(FitArgs a) {
     M1 = w1_load<G>(a.m, d, wv, li, lg);
     V1 = w1_load<G>(a.v, d, wv, li, lg);
   }
+  // a use of the loaded slice here, so their vmcnt wait is placed before the
+  // step loop (first used inside it, the wait went inside it: a vmcnt(0) at
+  // every step's layer-1 MFMAs, behind whatever memory traffic was in flight)
+  asm volatile("" ::"v"(W1), "v"(M1), "v"(V1));
   if (t < kH2) {
     const int gi[4] = {kCW3 + t, kCB2 + t, kW2 + t * kCLd + kH1, kW2 + t * kCLd + kH1 + 1};
     const int l4[4] = {uW3 + t, uB2 + t, uWA + 2 * t, uWA + 2 * t + 1};
@@ -578,15 +582,7 @@ __global__ void __launch_bounds__(kT) k_fit_critic(FitArgs a) {
     float* sHD = sm + cAct + (k & 1) * kActN;
     float* sHDT = sHD + kB * LH;
     SK_FT(k, 0);
-    // the next step's rows into registers (stored into the other buffer mid-step)
-    float nx = 0.f;
     const bool more = k + 1 < a.M;
-    if (more) {
-      const int64_t r0 = (int64_t)(k + 1) * kB;
-      if (t < kB * kS) nx = a.states[r0 * kS + t];
-      else if (t < kB * kS + 2 * kB) nx = a.actions[r0 * 2 + (t - kB * kS)];
-      else if (t < kB * kS + 3 * kB) nx = a.targets[r0 + (t - kB * kS - 2 * kB)];
-    }
 
     // (1) layer 1 of the own units with Dropout (SkillshotLearner.py:106-108):
     //     waves w < NT1, one n-tile each; one Philox call gives the 4 rows' bits
@@ -612,6 +608,16 @@ __global__ void __launch_bounds__(kT) k_fit_critic(FitArgs a) {
     //     each 16-unit tile to its summer: slice (d -> e) = [U units][16 rows]
     partials_publish<G>(sHD, W2, xr, E + 1, wv, li, lg, [&](int e) { return cxR + (d * P + e) * U * 16; });
     SK_FT(k, 2);
+    // the next step's rows into registers, stored into the other buffer after
+    // phase 5: issued here they land under the exchange waits (at the top of
+    // the step the layer-1 MFMAs' vmcnt(0) waited for them)
+    float nx = 0.f;
+    if (more) {
+      const int64_t r0 = (int64_t)(k + 1) * kB;
+      if (t < kB * kS) nx = a.states[r0 * kS + t];
+      else if (t < kB * kS + 2 * kB) nx = a.actions[r0 * 2 + (t - kB * kS)];
+      else if (t < kB * kS + 3 * kB) nx = a.targets[r0 + (t - kB * kS - 2 * kB)];
+    }
 
     // (3) workgroup d sums the P slices of units U_d (source order), adds b2
     //     and the action columns: h2 = relu(z2), published to all (H); the
@@ -868,6 +874,10 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a, const float* __rest
     M1 = w1_load<G>(a.m, d, wv, li, lg);
     V1 = w1_load<G>(a.v, d, wv, li, lg);
   }
+  // a use of the loaded slice here, so their vmcnt wait is placed before the
+  // step loop (first used inside it, the wait went inside it: a vmcnt(0) at
+  // every step's layer-1 MFMAs, behind whatever memory traffic was in flight)
+  asm volatile("" ::"v"(W1), "v"(M1), "v"(V1));
   if (t < kH2) {
     const int gi[3] = {kAW3 + t, kAW3 + kH2 + t, kAB2 + t};
     const int l3[3] = {aW3 + 2 * t, aW3 + 2 * t + 1, aB2 + t};
@@ -916,15 +926,7 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a, const float* __rest
     float* sH1T = sH1 + kB * LH;
     const float* sZC = sm + xZC + (k & 1) * kB * LZ;
     SK_FT(k, 0);
-    // the next step's rows and zc into registers (stored into the other buffers mid-step)
-    float nx = 0.f;
-    float nz[kZPer];
     const bool more = k + 1 < a.M;
-    if (more) {
-      if (t < kB * kS) nx = a.states[(int64_t)(k + 1) * kB * kS + t];
-#pragma unroll
-      for (int i = 0; i < kZPer; ++i) nz[i] = zc[(int64_t)(k + 1) * kB * kH2 + t + kT * i];
-    }
 
     // (1) layer 1 of the own units on waves w < NT1 (the relu mask kept in registers)
     f4 hmask = {0.f, 0.f, 0.f, 0.f};
@@ -945,6 +947,15 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a, const float* __rest
 
     // (2) the layer-2 partials over the own columns, to the unit summers
     partials_publish<G>(sH1, W2, xr, E + 1, wv, li, lg, [&](int e) { return axR + (d * P + e) * U * 16; });
+    // the next step's rows and zc into registers (stored after phase 5;
+    // issued here they land under the exchange waits)
+    float nx = 0.f;
+    float nz[kZPer];
+    if (more) {
+      if (t < kB * kS) nx = a.states[(int64_t)(k + 1) * kB * kS + t];
+#pragma unroll
+      for (int i = 0; i < kZPer; ++i) nz[i] = zc[(int64_t)(k + 1) * kB * kH2 + t + kT * i];
+    }
     SK_FT(k, 2);
 
     // (3) the sums of U_d: h2 = relu(z2 + b2), published to all (H)
