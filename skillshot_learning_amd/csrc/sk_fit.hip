@@ -182,6 +182,13 @@ __device__ __forceinline__ void adam4(f4& w, f4& m, f4& v, f4 g, float alpha, fl
   for (int t = 0; t < 4; ++t) r[t] = __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(v[t]) + eps);
   w = w - (m * alpha) * r;
 }
+// tanh without branches: sign(x) (1 - 2 / (e^{2|x|} + 1)) on v_exp_f32 and
+// v_rcp_f32, absolutely within ~1e-7 of tanhf (whose range split made both
+// outputs' chains run both paths under exec masks, one after the other)
+__device__ __forceinline__ float tanh_nb(float x) {
+  const float e = __builtin_amdgcn_exp2f(fabsf(x) * 2.8853900817779268f);  // 2 log2(e) |x|
+  return copysignf(1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f), x);
+}
 __device__ __forceinline__ void adam_lds(float* w, float* m, float* v, int i, float g, float alpha, float b1c,
                                          float b2c, float eps) {
   float mm = m[i], vv = v[i];
@@ -985,7 +992,8 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a, const float* __rest
         p0 += uW[aW3 + 2 * u] * h;
         p1 += uW[aW3 + 2 * u + 1] * h;
       }
-      const float a0 = tanhf(sum16(p0) + uW[aB3]), a1 = tanhf(sum16(p1) + uW[aB3 + 1]);
+      const float2 b3 = *(const float2*)(uW + aB3);
+      const float a0 = tanh_nb(sum16(p0) + b3.x), a1 = tanh_nb(sum16(p1) + b3.y);
       float g0 = 0.f, g1 = 0.f;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
