@@ -642,6 +642,11 @@ def reference_rule_rate(envs, exploration="param_noise", precision="fp32", fit_c
         fu.soft_update_in_adam = True
     steps_per_pass = (rows + b - 1) // b
     step_us = (critic_us + actor_us) / 2
+    # algorithmic FLOPs per batch-16 step: a net's forward + backward is ~6 flops per parameter and row;
+    # the actor step adds the critic's forward and its backward to the action (~4 per critic parameter)
+    n_c, n_a = sum(p.numel() for p in d.model_critic.parameters()), sum(p.numel() for p in d.model_actor.parameters())
+    fl_c, fl_a = 6.0 * b * n_c, 6.0 * b * n_a + 4.0 * b * n_c
+    fit_tf = (fl_c + fl_a) / ((critic_us + actor_us) * 1e-6) / 1e12
     fit_epoch_s = steps_per_pass * (critic_us + actor_us) * 1e-6
     three_us = fit_s * 1e6 / (2 * fit_chunks * M)
     out = dict(envs=envs, exploration=exploration, dtype=precision, episode_ticks_max=T, env_steps_played=played,
@@ -657,6 +662,14 @@ def reference_rule_rate(envs, exploration="param_noise", precision="fp32", fit_c
                         projected_epoch_fit_s=fit_epoch_s,
                         three_launch=dict(minibatch_steps_timed=2 * fit_chunks * M, us_per_minibatch_step=three_us,
                                           projected_epoch_fit_s=2 * steps_per_pass * three_us * 1e-6),
+                        roofline=dict(bound="latency (two in-launch hand-offs and a dependent phase chain per "
+                                            "step; one wave per SIMD on 16 CUs)",
+                                      kernel="k_fit_critic + k_fit_actor", achieved=fit_tf,
+                                      peak=MFMA_PEAK_TF["fp32"], unit="TFLOP/s", frac=fit_tf / MFMA_PEAK_TF["fp32"],
+                                      flops_per_step=dict(critic=fl_c, actor=fl_a),
+                                      clock="HIP events on the launch stream over the timed passes",
+                                      memory_level="on chip: weights and moments in registers / LDS for the "
+                                                   "launch; exchanges through L2 (sc1 write-through granules)"),
                         note="sequential SGD at batch 16 as the reference's models_fit: the epoch's fit is "
                              "projected from the timed resident passes over the epoch's first rows"),
                projected_epoch_s=wall + fit_epoch_s)
