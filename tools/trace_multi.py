@@ -84,7 +84,19 @@ def main():
                         tick_max_us=[round(float(v), 3) for v in per.max(axis=0)],
                         last_tick_to_exit_p50_us=float(np.median(x - ends[:, -1])) * 0.01,
                         exit_min_us=float(x.min()) * 0.01, exit_p50_us=float(np.median(x)) * 0.01,
-                        span_us=float(x.max()) * 0.01))
+                        span_us=float(x.max()) * 0.01,
+                        # is the slow-wave tail systematic? per XCD: exit p50 / max, wave span p50 / max,
+                        # mean per-tick time, entry p50 (us)
+                        by_xcc={int(k): dict(exit_p50=round(float(np.median(x[xcc == k])) * 0.01, 2),
+                                             exit_max=round(float(np.max(x[xcc == k])) * 0.01, 2),
+                                             span_p50=round(float(np.median(span_w[xcc == k])), 2),
+                                             span_max=round(float(np.max(span_w[xcc == k])), 2),
+                                             tick_mean=round(float(per[xcc == k].mean()), 3),
+                                             entry_p50=round(float(np.median(e[xcc == k])) * 0.01, 2))
+                                for k in np.unique(xcc)},
+                        # the slowest 5 % of waves: their XCD and CU-slot spread
+                        slow_waves_xcc_hist={int(k): int(v) for k, v in zip(*np.unique(
+                            xcc[span_w >= np.quantile(span_w, 0.95)], return_counts=True))}))
     print(json.dumps(dict(envs=n, ticks=T, launches=out[-2:])))
 
 
