@@ -9,32 +9,36 @@
 // parameters); as three launches per step (gradient forward, backward, Adam)
 // a step costs 13-14 us of launch boundaries and dependent phase chains.
 //
-// Here ONE launch runs M consecutive steps of a pass on 8 workgroups (one CU
-// each, on one XCD where round-robin placement allows) that keep the net,
-// its Adam moments and the step's activations on chip for the whole launch.
-// The 36 k weights of layers 1 and 2 are split by LAYER-2 INPUT COLUMNS (the
-// layer-1 units): workgroup d owns
-//   layer-1 units C_d = [32 d, 32 d + 32): W1 rows and b1, and the Dropout
-//     mask of those units (keyed by the global unit, as rng.dropout_keep);
+// Here ONE launch runs M consecutive steps of a pass on P workgroups (P = 16
+// by default, 8 with SK_FIT_P=8; one CU each, spread over the XCDs or on one
+// with SK_FIT_XCD=1) that keep the net, its Adam moments and the step's
+// activations on chip for the whole launch.  The 36 k weights of layers 1
+// and 2 are split by LAYER-2 INPUT COLUMNS (the layer-1 units): workgroup d
+// owns
+//   layer-1 units C_d = [C d, C d + C), C = 256 / P: W1 rows and b1, and the
+//     Dropout mask of those units (keyed by the global unit, as
+//     rng.dropout_keep);
 //   W2[:, C_d], the layer-2 weights of those inputs for all 128 units;
 // with their Adam moments.  The few hundred "unit" parameters after layer 2
 // (b2, W3, b3 and the critic's action columns W2[:, 256:258]) are held and
 // stepped by EVERY workgroup, redundantly and bit-identically.  A step then
-// needs two in-launch exchanges (csrc/sk_xchg.hpp: data-tagged 8-byte
-// granules in pairs, 16-byte write-through stores, every load of a sweep in
-// flight):
+// needs two in-launch exchanges (data-tagged 8-byte granules in pairs, 16-byte
+// write-through stores, every load of a sweep in flight, as csrc/sk_xchg.hpp
+// describes):
 //   R  reduce-scatter of the layer-2 partial products (each workgroup's
-//      16 x 128 over its own input columns; workgroup e sums the 8 slices of
-//      units U_e = [16 e, 16 e + 16) in source order and adds b2 and the
-//      action columns),
-//   H  all-gather of those 16 x 16 sums (the critic's h2 = relu(z2); the
-//      actor's h2 and the critic's action-free z2): every workgroup then forms
-//      q (critic) or a = tanh(z3) and dQ/da (actor), dL/dz2 of all 128
-//      units and the unit parameters' gradients and Adam steps itself, and
-//      dW2[:, C_d], dL/dh1[:, C_d] with its own columns.
+//      16 x 128 over its own input columns; workgroup e sums the P slices of
+//      units U_e = [U e, U e + U), U = 128 / P, in source order and adds b2
+//      and the action columns),
+//   H  all-gather of those 16 x U sums (the critic's h2 = relu(z2); the
+//      actor's h2), each wave gathering its own four rows: every workgroup
+//      then forms q (critic) or a = tanh(z3) and dQ/da (actor), dL/dz2 of all
+//      128 units and the unit parameters' gradients and Adam steps itself,
+//      and dW2[:, C_d], dL/dh1[:, C_d] with its own columns.
 // Two round trips per step instead of the four (critic) or six (actor) of a
 // per-quantity exchange (all-reduce q, all-gather dz2, ...); the bytes are
 // half the row split's (tools/seam_bench.py, profiles/r05f_seam_bench.jsonl).
+// The actor pass reads the frozen critic's action-free layer-2
+// pre-activations from a parallel launch ahead of it (k_fit_critic_z2).
 //
 // The rest of a step is a phase chain (tools/trace_fit.py, -DSK_TRACE_FIT):
 // a first version holding everything in LDS spent 9 of its 12.8 us per
@@ -43,17 +47,17 @@
 // gradient GEMM is oriented to produce its output in that same layout, so
 // Adam runs in the GEMM's epilogue on registers:
 //   W2[:, C_d]  lane (i, g) of wave w holds W2[16 nt + i][16 mk + 4 g .. + 3]
-//               for n-tiles nt = w, w + 4 and column tiles mk = 0, 1: the B
+//               for n-tiles nt = w, w + 4 and column tiles mk < C / 16: the B
 //               operand of the forward partials (h1 W2^T) and the output of
 //               dW2^T = h1^T dz2 (v_mfma_f32_16x16x4_f32: lane (i, g) holds
 //               A[i][k = g], B[k = g][i], D[4 g + r][i]); an LDS mirror feeds
 //               the backward dz2 W2;
-//   W1 | b1     lane (i, g) of wave 0 / 1 holds W1[32 d + 16 w + i][4 g .. +3]
-//               (g = 3: b1 and zeros): the B operand of layer 1 as a K = 16
-//               GEMM on s with a column of ones (the bias folded in), and the
-//               output of dW1^T = s^T dz1; layer 1's output rows 4 g .. 4 g + 3
-//               of one unit per lane also make ONE Philox call per lane give
-//               the four rows' Dropout bits;
+//   W1 | b1     lane (i, g) of wave w < C / 16 holds W1[C d + 16 w + i][4 g ..
+//               + 3] (g = 3: b1 and zeros): the B operand of layer 1 as a
+//               K = 16 GEMM on s with a column of ones (the bias folded in),
+//               and the output of dW1^T = s^T dz1; layer 1's output rows
+//               4 g .. 4 g + 3 of one unit per lane also make ONE Philox call
+//               per lane give the four rows' Dropout bits;
 // 16-lane sums are DPP row operations.  GEMMs are exact fp32 products with
 // fp32 sums in another order than the three-launch chain: the tests hold both
 // to 1e-5 of each other and of the fp64 Keras restatement.  Adam is Keras'
