@@ -483,6 +483,33 @@ def test_fit_critic_resident_equals_eager_and_keras(mods, monkeypatch, p, xcd):
     assert np.abs(got - ref).max() <= PARAM_ABS, np.abs(got - ref).max()
 
 
+def test_fit_critic_launch_longer_than_step_size_table(mods):
+    """one resident critic launch of 2,100 minibatch steps (past the
+    2,048-step table of Adam step sizes each launch refills in LDS,
+    csrc/sk_fit.hip alpha_fill) equals, bit for bit, the same pass cut into
+    launches of 512 steps (no refill): nets, Adam moments and step counts,
+    the Dropout call number.  (Against the three-launch chain a pass this long
+    is not a parity bar: a pre-activation within the two summation orders'
+    ~1e-7 of zero flips a relu somewhere in ~10^7 decisions and the two
+    trajectories part, tools/diag_fit_long.py.)"""
+    learner, _ = mods
+    n = 2100
+    s, a, y = _fit_rows(16 * n, 13)
+    out = []
+    for per in (4096, 512):
+        d = _ddpg(learner, seed=6, scale=1.0)
+        d._fused.FIT_STEPS_PER_LAUNCH = per
+        assert d._fused.fit_critic(s, a, y) == n
+        d._fused.fit_check()
+        torch.cuda.synchronize()
+        f = d._fused
+        out.append((f.fc.clone(), f.sc.m.clone(), f.sc.v.clone(), f.sc.steps.clone(), int(d.drop_calls)))
+    (c1, m1, v1, t1, k1), (c2, m2, v2, t2, k2) = out
+    assert k1 == k2 and torch.equal(t1, t2)
+    assert torch.equal(c1, c2) and torch.equal(m1, m2) and torch.equal(v1, v2)
+    assert bool(torch.isfinite(c1).all())
+
+
 def test_models_fit_resident_equals_three_launch(mods, monkeypatch):
     """models_fit with the resident critic pass (default) and with the
     three-launch steps (SK_FIT_RESIDENT=0): the same nets within 1e-5 after a
