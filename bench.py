@@ -630,6 +630,7 @@ def reference_rule_rate(envs, exploration="param_noise", precision="fp32", fit_c
         fu.fit_check()
         critic_us = ev3[0].elapsed_time(ev3[1]) * 1e3 / n_fit
         actor_us = ev3[1].elapsed_time(ev3[2]) * 1e3 / n_fit
+        place = int(fu.fit_timeout[1].item())
         d._fit_chunks(S, A, R, b, M, 1, critic=True)
         d._fit_chunks(S, A, R, b, M, 1, critic=False)
         torch.cuda.synchronize()
@@ -669,7 +670,9 @@ def reference_rule_rate(envs, exploration="param_noise", precision="fp32", fit_c
                                       flops_per_step=dict(critic=fl_c, actor=fl_a),
                                       clock="HIP events on the launch stream over the timed passes",
                                       memory_level="on chip: weights and moments in registers / LDS for the "
-                                                   "launch; exchanges through L2 (sc1 write-through granules)"),
+                                                   "launch; exchanges through L2 (%s)"
+                                                   % ("one XCD: plain stores, the XCD's L2" if place == 2 else
+                                                      "spread: sc1 write-through granules")),
                         note="sequential SGD at batch 16 as the reference's models_fit: the epoch's fit is "
                              "projected from the timed resident passes over the epoch's first rows"),
                projected_epoch_s=wall + fit_epoch_s)

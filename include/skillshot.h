@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define SK_ABI_VERSION 10
+#define SK_ABI_VERSION 11
 
 enum {
   SK_OK = 0,
@@ -679,32 +679,34 @@ int sk_critic_grad_f32_sampled_step(const float* critic_flat, const sk_ring_samp
                                     int32_t n_steps, float* loss_sum, uint8_t* dropout_mask, float* scratch,
                                     const sk_step_job* job, void* stream);
 
-/* models_fit's critic pass as resident launches (ABI 10; the reference rule,
+/* models_fit's critic pass as resident launches (ABI 11; the reference rule,
  * SkillshotLearner.py:419-443, critic.fit at batch 16, :434): n_minibatches
  * consecutive 16-row minibatches (states float[16 n][12], actions [16 n][2],
  * targets [16 n], the rows in the shuffled order the pass visits them) each
  * take one Adam step of the critic on MSE(Q(s, a), target) with Dropout(0.2)
- * active, in ONE launch of 8 workgroups that hold the net and its Adam
- * moments on chip (csrc/sk_fit.hip).  Equal, up to fp32 summation order
+ * active, in ONE launch of 16 workgroups that hold the net and its Adam
+ * moments on chip (csrc/sk_fit.hip; SK_FIT_P=8: 8).  Equal, up to fp32 summation order
  * (tests: 1e-5), to n_minibatches sk_critic_grad_f32 + sk_adam_flat steps:
  * the same Dropout keys (seed, *drop_calls + step, row, unit), Keras Adam
  * with step counts step_counters[0 .. n_steps) (+1 each per step, fp32),
  * *drop_calls += n_minibatches.  xbuf: sk_fit_xbuf_bytes() of device memory
  * (16-byte aligned, zeroed once when allocated) with its epoch word
- * uint64 *epoch, both owned by the caller across calls; *timeout (uint32,
- * zeroed by the caller) becomes nonzero if an in-launch exchange was lost,
- * and the nets are then undefined.  losses float[n_minibatches] (nullable):
+ * uint64 *epoch, both owned by the caller across calls.  timeout: uint32[2],
+ * timeout[0] zeroed by the caller, becomes nonzero if an in-launch exchange
+ * was lost (the nets are then undefined); timeout[1] is set to the launch's
+ * placement (2: every workgroup on one XCD, the exchanges through its L2;
+ * 1: spread, write-through exchanges; 0: a workgroup never arrived).  losses float[n_minibatches] (nullable):
  * each step's loss.  GPU backend only. */
 size_t sk_fit_xbuf_bytes(void);
 int sk_fit_critic_f32(float* critic_flat, float* adam_m, float* adam_v, float* step_counters, int32_t n_steps,
                       const float* states, const float* actions, const float* targets, int32_t n_minibatches,
                       uint64_t drop_seed, int64_t* drop_calls, float lr, float beta1, float beta2, float eps,
                       void* xbuf, uint64_t* epoch, uint32_t* timeout, float* losses, void* stream);
-/* models_fit's actor pass likewise (ABI 10; model_actor_fit_step at batch 16,
+/* models_fit's actor pass likewise (ABI 11; model_actor_fit_step at batch 16,
  * SkillshotLearner.py:386-417, 436-443): n_minibatches consecutive 16-row
  * minibatches of states each take one Adam step of the actor on -sum Q(s,
  * mu(s)) with the critic (critic_flat, unchanged) at inference, in ONE launch
- * of 8 workgroups.  Equal up to fp32 summation order to n_minibatches
+ * of 16 workgroups.  Equal up to fp32 summation order to n_minibatches
  * sk_actor_grad_f32 + sk_adam_flat steps (tests: 1e-5); step_counters as
  * sk_fit_critic_f32's; the same xbuf / epoch / timeout.  zbuf: float
  * [16 n_minibatches][128] device scratch, overwritten (the frozen critic's

@@ -16,7 +16,7 @@ from . import build as _build
 
 SK_OK, SK_EINVAL, SK_EHIP, SK_ENOMEM, SK_ENODEV = 0, -1, -2, -3, -4
 SK_REWARD_LOOKING, SK_REWARD_SIMPLE = 0, 1
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 # every symbol include/skillshot.h declares
 EXPORTS = (

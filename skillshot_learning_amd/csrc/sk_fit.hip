@@ -10,9 +10,9 @@
 // a step costs 13-14 us of launch boundaries and dependent phase chains.
 //
 // Here ONE launch runs M consecutive steps of a pass on P workgroups (P = 16
-// by default, 8 with SK_FIT_P=8; one CU each, spread over the XCDs or on one
-// with SK_FIT_XCD=1) that keep the net, its Adam moments and the step's
-// activations on chip for the whole launch.  The 36 k weights of layers 1
+// by default, 8 with SK_FIT_P=8; one CU each, on one XCD by default, spread
+// over the XCDs with SK_FIT_XCD=0) that keep the net, its Adam moments and the
+// step's activations on chip for the whole launch.  The 36 k weights of layers 1
 // and 2 are split by LAYER-2 INPUT COLUMNS (the layer-1 units): workgroup d
 // owns
 //   layer-1 units C_d = [C d, C d + C), C = 256 / P: W1 rows and b1, and the
@@ -23,8 +23,9 @@
 // (b2, W3, b3 and the critic's action columns W2[:, 256:258]) are held and
 // stepped by EVERY workgroup, redundantly and bit-identically.  A step then
 // needs two in-launch exchanges (data-tagged 8-byte granules in pairs, 16-byte
-// write-through stores, every load of a sweep in flight, as csrc/sk_xchg.hpp
-// describes):
+// stores, every load of a sweep in flight, as csrc/sk_xchg.hpp describes; the
+// stores plain when the launch finds all its workgroups on one XCD, whose L2
+// then carries the exchange, write-through otherwise: fit_placement):
 //   R  reduce-scatter of the layer-2 partial products (each workgroup's
 //      16 x 128 over its own input columns; workgroup e sums the P slices of
 //      units U_e = [U e, U e + U), U = 128 / P, in source order and adds b2
@@ -123,10 +124,19 @@ __device__ __forceinline__ f32x4 m16x4(f4 a, f4 b, f32x4 c) {
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, -1, 0x00020000);
 }
-// one granule pair {a, tag, b, tag}: ONE 16-byte write-through store (aux 16 = sc1)
-__device__ __forceinline__ void put2(__amdgpu_buffer_rsrc_t r, uint32_t byte_off, unsigned tag, float a, float b) {
+// one granule pair {a, tag, b, tag}: ONE 16-byte store.  local (every
+// workgroup of the launch on one XCD, fit_placement): a plain store, which
+// keeps the line in that XCD's L2, where the readers' sc1 loads find it;
+// otherwise write-through (aux 16 = sc1), which drops the line from the
+// writer's L2 so the other XCDs' readers see it (a same-XCD reader then pays
+// the cross-XCD rate: critic 5.1 vs 4.4 us per step)
+__device__ __forceinline__ void put2(__amdgpu_buffer_rsrc_t r, uint32_t byte_off, unsigned tag, float a, float b,
+                                     bool local) {
   const u4v v = {__float_as_uint(a), tag, __float_as_uint(b), tag};
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, byte_off, 0, 16);
+  if (local)
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, byte_off, 0, 0);
+  else
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, byte_off, 0, 16);
 }
 // N granule pairs per lane at byte offsets off[k], every load issued before
 // the checks, re-read until the wave's tags all equal `tag` (bounded spin)
@@ -151,6 +161,31 @@ __device__ __forceinline__ bool get2(__amdgpu_buffer_rsrc_t r, const uint32_t (&
     }
     __builtin_amdgcn_s_sleep(1);
   }
+}
+
+// The launch's placement, decided once before the first step: every
+// workgroup publishes its XCD (HW_REG_XCC_ID) in granule pair kXPlace + 2 d
+// (write-through; tag ~epoch, which no earlier launch's slot and no zeroed
+// slot holds) and wave 0 reads all P of them.  Every workgroup sees the same P
+// values, so all pick the same store flavour (put2): correct under any
+// block -> XCD map, fast when the stride-8 grid lands on one XCD.  Returns
+// 2 (one XCD), 1 (spread) or 0 (a workgroup never arrived: *timeout is set).
+constexpr int kXPlace = 65536 - 64;  // granules: the placement slots, past every step exchange
+template <int P>
+__device__ __forceinline__ int fit_placement(__amdgpu_buffer_rsrc_t xr, int d, unsigned ep0, unsigned* timeout) {
+  __shared__ int s_place;
+  const unsigned tag = ~ep0;
+  const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u;  // HW_REG_XCC_ID [3:0]
+  if (threadIdx.x == 0) put2(xr, (uint32_t)(kXPlace + 2 * d) * 8u, tag, __uint_as_float(xcc), 0.f, false);
+  if (threadIdx.x < 64) {
+    const uint32_t off[1] = {(uint32_t)(kXPlace + 2 * (int)(threadIdx.x % P)) * 8u};
+    float v[2];
+    const bool ok = get2<1>(xr, off, tag, v, timeout);
+    const bool same = __all(__float_as_uint(v[0]) == xcc);
+    if (threadIdx.x == 0) s_place = ok ? (same ? 2 : 1) : 0;
+  }
+  __syncthreads();
+  return __builtin_amdgcn_readfirstlane(s_place);
 }
 
 // DPP row (16-lane) moves: quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror
@@ -216,7 +251,7 @@ struct FitArgs {
   float lr, beta1, beta2, eps;
   unsigned long long* xbuf;
   unsigned long long* epoch;
-  unsigned* timeout;
+  unsigned* timeout;      // [0] a lost exchange (atomicMax 1); [1] the placement (fit_placement's value)
   float* losses;         // [M] per-step MSE (nullable; critic)
   int stride;            // grid = P x stride; blocks b % stride == 0 work (stride 8: one XCD under
                          // round-robin placement, a speed choice only, never correctness)
@@ -330,7 +365,7 @@ __device__ __forceinline__ f32x4 layer1(const float* sS, f4 w1, int li, int lg) 
 // its summer e at slot(e) (granule index of a [U units][16 rows] slice)
 template <class G, typename Slot>
 __device__ __forceinline__ void partials_publish(const float* X, const W2Reg<G>& W, __amdgpu_buffer_rsrc_t xr,
-                                                 unsigned tag, int wv, int li, int lg, Slot slot) {
+                                                 unsigned tag, bool local, int wv, int li, int lg, Slot slot) {
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int nt = wv + 4 * q;
@@ -341,8 +376,8 @@ __device__ __forceinline__ void partials_publish(const float* X, const W2Reg<G>&
     // unit 16 nt + li is summed by workgroup (16 nt + li) / U: its slice row
     const int u = 16 * nt + li;
     const uint32_t base = (uint32_t)(slot(u / G::U) + (u % G::U) * 16 + 4 * lg) * 8u;
-    put2(xr, base, tag, acc[0], acc[1]);
-    put2(xr, base + 16u, tag, acc[2], acc[3]);
+    put2(xr, base, tag, acc[0], acc[1], local);
+    put2(xr, base + 16u, tag, acc[2], acc[3], local);
   }
 }
 
@@ -508,7 +543,7 @@ struct CriticLayout {
   static constexpr size_t kLds = (size_t)cEnd * 4;
   // exchanges (granules): R [P src][P dst][U][16], H [P][U][16]
   static constexpr int cxR = 0, cxH = cxR + G::P * G::P * G::U * 16, cxN = cxH + G::P * G::U * 16;
-  static_assert(kLds <= 150 * 1024 && cxN <= 65536, "LDS / xbuf");
+  static_assert(kLds <= 150 * 1024 && cxN <= kXPlace, "LDS / xbuf");
 };
 
 template <int PW>
@@ -569,6 +604,9 @@ __global__ void __launch_bounds__(kT) k_fit_critic(FitArgs a) {
   const int64_t call0 = a.drop_calls[0];
   const unsigned ep0 = (unsigned)a.epoch[0];
   const float tk0 = a.steps[0];
+  const int place = fit_placement<P>(xr, d, ep0, a.timeout);
+  const bool local = place == 2;
+  const int M = place ? a.M : 0;  // a lost workgroup: no step runs (*timeout is set)
   // s_ext: 12 inputs, the bias column (1), zeros (both buffers); step 0's rows
   if (t < kB * LS) {
     const int r = t / LS, j = t % LS;
@@ -583,7 +621,7 @@ __global__ void __launch_bounds__(kT) k_fit_critic(FitArgs a) {
   uint4 bits = {0u, 0u, 0u, 0u};
   if (wv < NT1) bits = drop_bits<G>(a, (uint64_t)call0, d, 16 * wv + li, lg);
 
-  for (int k = 0; k < a.M; ++k) {
+  for (int k = 0; k < M; ++k) {
     const unsigned E = ep0 + 2u * (unsigned)k;
     if (k % kAlphaN == 0) alpha_fill(a, sAlpha, tk0, k);  // (its barrier also publishes step 0's rows)
     const float alpha = sAlpha[k % kAlphaN];
@@ -617,7 +655,7 @@ __global__ void __launch_bounds__(kT) k_fit_critic(FitArgs a) {
 
     // (2) the layer-2 partial products of the own columns for all 128 units,
     //     each 16-unit tile to its summer: slice (d -> e) = [U units][16 rows]
-    partials_publish<G>(sHD, W2, xr, E + 1, wv, li, lg, [&](int e) { return cxR + (d * P + e) * U * 16; });
+    partials_publish<G>(sHD, W2, xr, E + 1, local, wv, li, lg, [&](int e) { return cxR + (d * P + e) * U * 16; });
     SK_FT(k, 2);
     // the next step's rows into registers, stored into the other buffer after
     // phase 5: issued here they land under the exchange waits (at the top of
@@ -643,7 +681,8 @@ __global__ void __launch_bounds__(kT) k_fit_critic(FitArgs a) {
       const float b2 = uW[uB2 + ug], wa0 = uW[uWA + 2 * ug], wa1 = uW[uWA + 2 * ug + 1];
       z0 = z0 + sA[2 * r0] * wa0 + sA[2 * r0 + 1] * wa1 + b2;
       z1 = z1 + sA[2 * r0 + 2] * wa0 + sA[2 * r0 + 3] * wa1 + b2;
-      put2(xr, (uint32_t)(cxH + 2 * h_pair<G>(d, r0 / 2, ug - U * d)) * 8u, E + 2, fmaxf(z0, 0.f), fmaxf(z1, 0.f));
+      put2(xr, (uint32_t)(cxH + 2 * h_pair<G>(d, r0 / 2, ug - U * d)) * 8u, E + 2, fmaxf(z0, 0.f), fmaxf(z1, 0.f),
+           local);
     }
     SK_FT(k, 3);
 
@@ -760,6 +799,7 @@ __global__ void __launch_bounds__(kT) k_fit_critic(FitArgs a) {
     if (t == 0) {
       a.drop_calls[0] = call0 + a.M;
       a.epoch[0] = (unsigned long long)(ep0 + 2u * (unsigned)a.M);
+      a.timeout[1] = (unsigned)place;  // the placement report
     }
     if (t < a.n_steps) a.steps[t] = tk;
   }
@@ -845,7 +885,7 @@ struct ActorLayout {
   static constexpr size_t kLds = (size_t)xEnd * 4;
   // exchanges: R [P src][P dst][U][16], H [P][U][16]
   static constexpr int axR = 0, axH = axR + G::P * G::P * G::U * 16, axN = axH + G::P * G::U * 16;
-  static_assert(kLds <= 150 * 1024 && axN <= 65536, "LDS / xbuf");
+  static_assert(kLds <= 150 * 1024 && axN <= kXPlace, "LDS / xbuf");
 };
 constexpr int kZPer = kB * kH2 / kT;  // zc floats per thread and step
 
@@ -906,6 +946,9 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a, const float* __rest
   }
   const unsigned ep0 = (unsigned)a.epoch[0];
   const float tk0 = a.steps[0];
+  const int place = fit_placement<P>(xr, d, ep0, a.timeout);
+  const bool local = place == 2;
+  const int M = place ? a.M : 0;  // a lost workgroup: no step runs (*timeout is set)
   if (t < kB * LS) {
     const int r = t / LS, j = t % LS;
     sm[xS + t] = j < kS ? a.states[r * kS + j] : (j == kS ? 1.f : 0.f);
@@ -928,7 +971,7 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a, const float* __rest
     cwa1[i] = a.critic[kW2 + u * kCLd + kH1 + 1];
   }
 
-  for (int k = 0; k < a.M; ++k) {
+  for (int k = 0; k < M; ++k) {
     const unsigned E = ep0 + 2u * (unsigned)k;
     if (k % kAlphaN == 0) alpha_fill(a, sAlpha, tk0, k);
     const float alpha = sAlpha[k % kAlphaN];
@@ -957,7 +1000,7 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a, const float* __rest
     SK_FT(k, 1);
 
     // (2) the layer-2 partials over the own columns, to the unit summers
-    partials_publish<G>(sH1, W2, xr, E + 1, wv, li, lg, [&](int e) { return axR + (d * P + e) * U * 16; });
+    partials_publish<G>(sH1, W2, xr, E + 1, local, wv, li, lg, [&](int e) { return axR + (d * P + e) * U * 16; });
     // the next step's rows and zc into registers (stored after phase 5;
     // issued here they land under the exchange waits)
     float nx = 0.f;
@@ -975,7 +1018,7 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a, const float* __rest
       fail |= !r_sum<G>(xr, E + 1, t, [&](int s) { return axR + (s * P + d) * U * 16; }, z0, z1, a.timeout);
       const float b2 = uW[aB2 + U * d + (2 * t) / 16];
       put2(xr, (uint32_t)(axH + 2 * h_pair<G>(d, (t % 8), t / 8)) * 8u, E + 2, fmaxf(z0 + b2, 0.f),
-           fmaxf(z1 + b2, 0.f));
+           fmaxf(z1 + b2, 0.f), local);
     }
     SK_FT(k, 3);
 
@@ -1095,7 +1138,10 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a, const float* __rest
       a.m[kAB3 + j] = uM[aB3 + j];
       a.v[kAB3 + j] = uV[aB3 + j];
     }
-    if (t == 0) a.epoch[0] = (unsigned long long)(ep0 + 2u * (unsigned)a.M);
+    if (t == 0) {
+      a.epoch[0] = (unsigned long long)(ep0 + 2u * (unsigned)a.M);
+      a.timeout[1] = (unsigned)place;  // the placement report
+    }
     if (t < a.n_steps) a.steps[t] = tk;
   }
 }
@@ -1116,14 +1162,16 @@ int fit_p() {
   return (e && atoi(e) == 8) ? 8 : 16;
 }
 
-// SK_FIT_XCD=1 places the workgroups on one XCD (a grid of 8 P blocks, every
-// 8th working); default spread over the XCDs (P blocks).  At 8 workgroups the
-// exchanges alone favour one XCD (tools/seam_bench.py: 2.9 vs 3.4 us per
-// step), but the 16-workgroup passes run faster spread: critic 5.25-5.30 vs
-// 5.32-5.36 us, actor 5.87-5.91 vs 6.0-6.5 (profiles/r05u_bench_fit.jsonl)
+// The workgroups' placement: by default a grid of 8 P blocks, every 8th
+// working, which the round-robin dispatch puts on ONE XCD, so the exchanges
+// run through that XCD's L2 (fit_placement checks it in every launch; with
+// write-through stores one XCD had been no faster than spread: critic
+// 5.25-5.30 vs 5.32-5.36 us, profiles/r05u_bench_fit.jsonl; with plain stores
+// 4.4 / 4.6 us, profiles/r05zi_bench_fit_local.jsonl).  SK_FIT_XCD=0: P blocks,
+// spread over the XCDs (write-through stores).
 int fit_stride() {
   const char* e = getenv("SK_FIT_XCD");
-  return (e && atoi(e) == 1) ? 8 : 1;
+  return (e && atoi(e) == 0) ? 1 : 8;
 }
 
 }  // namespace

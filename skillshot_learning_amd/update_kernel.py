@@ -338,7 +338,8 @@ class FusedUpdate:
             nb = int(self.L.sk_fit_xbuf_bytes())
             self.fit_x = torch.zeros(nb // 8, dtype=torch.int64, device=self.dev)  # granule slots, zeroed once
             self.fit_epoch = torch.zeros(1, dtype=torch.int64, device=self.dev)     # their epoch, across launches
-            self.fit_timeout = torch.zeros(1, dtype=torch.int32, device=self.dev)
+            # [0] a lost exchange, [1] the last launch's placement (2: one XCD, 1: spread)
+            self.fit_timeout = torch.zeros(2, dtype=torch.int32, device=self.dev)
 
     @torch.no_grad()
     def fit_critic(self, s, a, y, losses=None):
@@ -347,7 +348,7 @@ class FusedUpdate:
         each minibatch one Adam step on MSE(Q(s, a), y) with Dropout active,
         in resident launches of up to FIT_STEPS_PER_LAUNCH steps
         (sk_fit_critic_f32, csrc/sk_fit.hip: the net and its moments held
-        on chip by 8 workgroups).  Equal up to fp32 summation order to one
+        on chip by 16 workgroups).  Equal up to fp32 summation order to one
         critic_step per minibatch (no soft update: models_fit has no target
         nets).  Returns the number of minibatch steps taken; rows past the
         last full minibatch are the caller's.  losses: float [steps] (each
@@ -404,7 +405,7 @@ class FusedUpdate:
     def fit_check(self):
         """raise if a resident fit launch lost an in-launch exchange (host sync)"""
         t = getattr(self, "fit_timeout", None)
-        if t is not None and int(t.item()):
+        if t is not None and int(t[0].item()):
             raise SkillshotError("resident models_fit: an in-launch exchange timed out; the nets are undefined")
 
     @torch.no_grad()

@@ -151,7 +151,7 @@ def test_gpu_only_entry_points_refuse_the_cpu_backend():
 
 
 def test_resident_fit_rejects_bad_arguments():
-    """sk_fit_critic_f32 / sk_fit_actor_f32 (ABI 10, models_fit's resident
+    """sk_fit_critic_f32 / sk_fit_actor_f32 (ABI 11, models_fit's resident
     passes) check their arguments before any launch: missing buffers, no
     minibatch, a step-counter count outside [1, 64] or an exchange buffer off
     its 16-byte alignment are SK_EINVAL (the dummy pointers are never

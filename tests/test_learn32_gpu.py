@@ -433,6 +433,15 @@ def _fit_rows(n, seed):
     return s, torch.rand(n, 2, device="cuda", generator=g) * 2 - 1, torch.randn(n, device="cuda", generator=g) * 0.5
 
 
+def _check_placement(fu, xcd):
+    """the launch's placement report (timeout word 1, csrc/sk_fit.hip
+    fit_placement): the default stride-8 grid lands on one XCD (2: plain
+    exchange stores through its L2); the spread grid on several (1:
+    write-through), or on one where the device is a single XCD"""
+    place = int(fu.fit_timeout[1].item())
+    assert place == 2 if xcd == "1" else place in (1, 2), place
+
+
 @pytest.mark.parametrize("p,xcd", [("16", "0"), ("16", "1"), ("8", "1")])
 def test_fit_critic_resident_equals_eager_and_keras(mods, monkeypatch, p, xcd):
     """models_fit's critic pass in resident launches (sk_fit_critic_f32,
@@ -458,6 +467,7 @@ def test_fit_critic_resident_equals_eager_and_keras(mods, monkeypatch, p, xcd):
     fr.FIT_STEPS_PER_LAUNCH = 64
     assert fr.fit_critic(s, a, y, losses=losses) == n
     fr.fit_check()
+    _check_placement(fr, xcd)
     want_loss = []
     for k in range(n):
         sl = slice(16 * k, 16 * k + 16)
@@ -510,6 +520,31 @@ def test_fit_critic_launch_longer_than_step_size_table(mods):
     assert bool(torch.isfinite(c1).all())
 
 
+def test_fit_placements_equal_bit_for_bit(mods, monkeypatch):
+    """the exchange's two store flavours (plain stores through one XCD's L2,
+    write-through stores spread over the XCDs) carry the same values in the
+    same summation order: a 700-step critic pass and actor pass on each give
+    the same nets, moments and losses bit for bit"""
+    learner, _ = mods
+    n = 700
+    s, a, y = _fit_rows(16 * n, 17)
+    out = []
+    for xcd in ("1", "0"):
+        monkeypatch.setenv("SK_FIT_XCD", xcd)
+        d = _ddpg(learner, seed=8, scale=1.0)
+        f = d._fused
+        losses = torch.zeros(n, device="cuda")
+        assert f.fit_critic(s, a, y, losses=losses) == n
+        assert f.fit_actor(s) == n
+        f.fit_check()
+        _check_placement(f, xcd)
+        torch.cuda.synchronize()
+        out.append([f.fc.clone(), f.sc.m.clone(), f.sc.v.clone(), f.fa.clone(), f.sa.m.clone(), f.sa.v.clone(),
+                    losses])
+    for x, z in zip(*out):
+        assert torch.equal(x, z)
+
+
 def test_models_fit_resident_equals_three_launch(mods, monkeypatch):
     """models_fit with the resident critic pass (default) and with the
     three-launch steps (SK_FIT_RESIDENT=0): the same nets within 1e-5 after a
@@ -531,17 +566,18 @@ def test_models_fit_resident_equals_three_launch(mods, monkeypatch):
     assert (a1 - a0).abs().max().item() <= PARAM_ABS
 
 
-@pytest.mark.parametrize("p", ["16", "8"])
-def test_fit_actor_resident_equals_eager_and_keras(mods, monkeypatch, p):
+@pytest.mark.parametrize("p,xcd", [("16", "1"), ("16", "0"), ("8", "1")])
+def test_fit_actor_resident_equals_eager_and_keras(mods, monkeypatch, p, xcd):
     """models_fit's actor pass in resident launches (sk_fit_actor_f32: the
     frozen critic's pre-activations computed up front, the actor split over
     16 or 8 workgroups by layer-2 input columns, two in-launch exchanges per
-    step) against one three-launch
+    step; on one XCD and spread) against one three-launch
     model_actor_fit_step per minibatch and the fp64 Keras restatement, over
     96 minibatch steps in two launches: parameters within 1e-5, Adam step
     counts equal, the critic untouched, the split pack rewritten"""
     learner, kr = mods
     monkeypatch.setenv("SK_FIT_P", p)
+    monkeypatch.setenv("SK_FIT_XCD", xcd)
     n = 96
     s, _, _ = _fit_rows(16 * n, 11)
     dr = _ddpg(learner, seed=5, scale=2.0)
@@ -555,6 +591,7 @@ def test_fit_actor_resident_equals_eager_and_keras(mods, monkeypatch, p):
     fr.FIT_STEPS_PER_LAUNCH = 64
     assert fr.fit_actor(s) == n
     fr.fit_check()
+    _check_placement(fr, xcd)
     for j in range(n):
         de.model_actor_fit_step(s[16 * j:16 * j + 16])
     torch.cuda.synchronize()

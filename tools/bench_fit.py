@@ -45,7 +45,8 @@ def main():
         return e0.elapsed_time(e1) * 1e3 / steps
 
     for rep in range(a.reps):
-        for P, xcd in (("16", "0"), ("16", "1"), ("8", "1")):
+        cfgs = os.environ.get("BENCH_FIT_CFG", "16:0,16:1,8:1")
+        for P, xcd in (c.split(":") for c in cfgs.split(",")):
             os.environ["SK_FIT_P"], os.environ["SK_FIT_XCD"] = P, xcd
             us = timed(lambda: fu.fit_critic(S, A, R), n)
             fu.fit_check()
