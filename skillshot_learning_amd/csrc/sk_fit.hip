@@ -188,6 +188,18 @@ __device__ __forceinline__ int fit_placement(__amdgpu_buffer_rsrc_t xr, int d, u
   return __builtin_amdgcn_readfirstlane(s_place);
 }
 
+// whether any thread of the workgroup has f set, at a workgroup barrier: one
+// barrier (__syncthreads_or is two and an LDS atomic).  slot: 4 ints of LDS
+// per call site, alternated by the caller so the next write to a slot is
+// behind barriers after this call's reads
+__device__ __forceinline__ bool wg_any(bool f, int* slot) {
+  const bool w = __any(f);
+  if ((threadIdx.x & 63) == 0) slot[threadIdx.x >> 6] = w;
+  __syncthreads();
+  const int4 v = *(const int4*)slot;
+  return (v.x | v.y | v.z | v.w) != 0;
+}
+
 // DPP row (16-lane) moves: quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror
 template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
@@ -280,6 +292,18 @@ __device__ unsigned long long* sk_fit_trace;
 #define SK_FT(k, i) \
   do {              \
   } while (0)
+#endif
+// -DSK_TRACE_FIT_P5 moves stamps 7 .. 9 into phase 5 (tools/trace_fit.py --p5)
+#ifdef SK_TRACE_FIT_P5
+#define SK_FT5(k, i) SK_FT(k, i)
+#define SK_FT7(k, i) \
+  do {               \
+  } while (0)
+#else
+#define SK_FT5(k, i) \
+  do {               \
+  } while (0)
+#define SK_FT7(k, i) SK_FT(k, i)
 #define SK_FT_FLUSH() \
   do {                \
   } while (0)
@@ -554,6 +578,7 @@ __global__ void __launch_bounds__(kT) k_fit_critic(FitArgs a) {
   constexpr int kRowsN = Y::kRowsN, kActN = Y::kActN, cRows = Y::cRows, cAct = Y::cAct, cxR = Y::cxR,
                 cxH = Y::cxH;
   extern __shared__ __attribute__((aligned(16))) float sm[];
+  __shared__ __attribute__((aligned(16))) int sFail[8];
   SK_FT_DECL
   if (blockIdx.x % a.stride) return;
   float* uW = sm;
@@ -693,13 +718,27 @@ __global__ void __launch_bounds__(kT) k_fit_critic(FitArgs a) {
     // (5) q of the 16 rows, every workgroup: lane (row t / 16, units t % 16 +
     //     16 i; each wave its own gathered rows), a DPP row sum; dL/dq =
     //     2 (q - y) / 16; dL/dz2 of all units
+    //     (every operand read into registers first: read again after the
+    //     first stores, each re-read waited for its own round trip)
     {
       const int r = t >> 4, j = t & 15;
+      float h[8], w3[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        h[i] = sH2[r * LZ + j + 16 * i];
+        w3[i] = uW[uW3 + j + 16 * i];
+      }
+      const float b3 = uW[uB3], yr = sY[r];
       float qp = 0.f;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) qp += uW[uW3 + j + 16 * i] * sH2[r * LZ + j + 16 * i];
-      const float q = sum16(qp) + uW[uB3];
-      const float e = q - sY[r], dq = e * (2.f / kB);
+      for (int i = 0; i < 8; ++i) qp += w3[i] * h[i];
+      SK_FT5(k, 7);
+      const float q = sum16(qp) + b3;
+      const float e = q - yr, dq = e * (2.f / kB);
+      SK_FT5(k, 8);
+      float g[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g[i] = h[i] > 0.f ? dq * w3[i] : 0.f;
       if (j == 0) {
         sDQ[r] = dq;
         sL[r] = e * e;
@@ -707,12 +746,12 @@ __global__ void __launch_bounds__(kT) k_fit_critic(FitArgs a) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int u = j + 16 * i;
-        const float g = sH2[r * LZ + u] > 0.f ? dq * uW[uW3 + u] : 0.f;
-        sDZ[r * LZ + u] = g;
-        sDZT[u * LZT + r] = g;
+        sDZ[r * LZ + u] = g[i];
+        sDZT[u * LZT + r] = g[i];
       }
     }
-    if (__syncthreads_or(fail)) break;  // a lost exchange ends the launch (uniformly)
+    SK_FT5(k, 9);
+    if (wg_any(fail, sFail + 4 * (k & 1))) break;  // a lost exchange ends the launch (uniformly)
     SK_FT(k, 5);
     if (more) {  // the next step's rows (that buffer's last readers were in step k - 1)
       float* nS = sm + cRows + ((k + 1) & 1) * kRowsN;
@@ -760,10 +799,10 @@ __global__ void __launch_bounds__(kT) k_fit_critic(FitArgs a) {
         if (lane == 0) adam_lds(uW, uM, uV, uB3, gb3, alpha, b1c, b2c, a.eps);
       }
     }
-    SK_FT(k, 7);
-    SK_FT(k, 8);
+    SK_FT7(k, 7);
+    SK_FT7(k, 8);
     dw2_adam<G>(W2, M2, V2, sHDT, sDZT, sW2, alpha, b1c, b2c, a.eps, wv, li, lg);
-    SK_FT(k, 9);
+    SK_FT7(k, 9);
     SK_FT(k, 10);
     // no barrier: the next step writes only the other buffers before its first
     // one; the W2 mirror's next reader (dh1) is behind three more
@@ -897,6 +936,7 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a, const float* __rest
   constexpr int kARowsN = Y::kARowsN, kAActN = Y::kAActN, xS = Y::xS, xAct = Y::xAct, xZC = Y::xZC,
                 axR = Y::axR, axH = Y::axH;
   extern __shared__ __attribute__((aligned(16))) float sm[];
+  __shared__ __attribute__((aligned(16))) int sFail[8];
   SK_FT_DECL
   if (blockIdx.x % a.stride) return;
   float* uW = sm;
@@ -1029,29 +1069,42 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a, const float* __rest
     // (5) every workgroup, lane (row t / 16, units t % 16 + 16 i), DPP row
     //     sums: z3 -> a = tanh(z3); the critic at (s, a): dQ/dz2 = W3 [z2 > 0],
     //     dQ/da; dL/dz3 = -dQ/da (1 - a^2) (L = -sum Q); the actor's dL/dz2
+    //     (every operand read into registers first: read again after the
+    //     first stores, each re-read waited for its own round trip)
     {
       const int r = t >> 4, j = t & 15;
-      float p0 = 0.f, p1 = 0.f;
+      float h[8], zr[8];
+      float2 w3[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int u = j + 16 * i;
-        const float h = sH2[r * LZ + u];
-        p0 += uW[aW3 + 2 * u] * h;
-        p1 += uW[aW3 + 2 * u + 1] * h;
+        h[i] = sH2[r * LZ + u];
+        w3[i] = *(const float2*)(uW + aW3 + 2 * u);
+        zr[i] = sZC[r * LZ + u];
       }
       const float2 b3 = *(const float2*)(uW + aB3);
+      float p0 = 0.f, p1 = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        p0 += w3[i].x * h[i];
+        p1 += w3[i].y * h[i];
+      }
+      SK_FT5(k, 7);
       const float a0 = tanh_nb(sum16(p0) + b3.x), a1 = tanh_nb(sum16(p1) + b3.y);
       float g0 = 0.f, g1 = 0.f;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const int u = j + 16 * i;
         const float wa0 = cwa0[i], wa1 = cwa1[i];
-        const float z = sZC[r * LZ + u] + a0 * wa0 + a1 * wa1;
+        const float z = zr[i] + a0 * wa0 + a1 * wa1;
         const float dz = z > 0.f ? cw3[i] : 0.f;
         g0 += dz * wa0;
         g1 += dz * wa1;
       }
+      SK_FT5(k, 8);
       const float e0 = -sum16(g0) * (1.f - a0 * a0), e1 = -sum16(g1) * (1.f - a1 * a1);
+      float g[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g[i] = h[i] > 0.f ? e0 * w3[i].x + e1 * w3[i].y : 0.f;
       if (j == 0) {
         sDZ3[2 * r] = e0;
         sDZ3[2 * r + 1] = e1;
@@ -1059,12 +1112,12 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a, const float* __rest
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int u = j + 16 * i;
-        const float g = sH2[r * LZ + u] > 0.f ? e0 * uW[aW3 + 2 * u] + e1 * uW[aW3 + 2 * u + 1] : 0.f;
-        sDZ[r * LZ + u] = g;
-        sDZT[u * LZT + r] = g;
+        sDZ[r * LZ + u] = g[i];
+        sDZT[u * LZT + r] = g[i];
       }
     }
-    if (__syncthreads_or(fail)) break;  // a lost exchange ends the launch (uniformly)
+    SK_FT5(k, 9);
+    if (wg_any(fail, sFail + 4 * (k & 1))) break;  // a lost exchange ends the launch (uniformly)
     SK_FT(k, 5);
     if (more) {  // the next step's rows and zc (those buffers' last readers were in step k - 1)
       if (t < kB * kS) sm[xS + ((k + 1) & 1) * kARowsN + (t / kS) * LS + t % kS] = nx;
@@ -1104,10 +1157,10 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a, const float* __rest
         if (lane == 0 || lane == 16) adam_lds(uW, uM, uV, aB3 + (lane >> 4), gb3, alpha, b1c, b2c, a.eps);
       }
     }
-    SK_FT(k, 7);
-    SK_FT(k, 8);
+    SK_FT7(k, 7);
+    SK_FT7(k, 8);
     dw2_adam<G>(W2, M2, V2, sH1T, sDZT, sW2, alpha, b1c, b2c, a.eps, wv, li, lg);
-    SK_FT(k, 9);
+    SK_FT7(k, 9);
     SK_FT(k, 10);
   }
   const float tk = tk0 + (float)a.M;
