@@ -247,6 +247,27 @@ __device__ __forceinline__ void adam_lds(float* w, float* m, float* v, int i, fl
   m[i] = mm;
   v[i] = vv;
 }
+// N parameters at once: every read issued before the first write (one LDS
+// round trip; one adam_lds after another waited for each in turn)
+template <int N>
+__device__ __forceinline__ void adam_lds_n(float* w, float* m, float* v, const int (&i)[N], const float (&g)[N],
+                                           float alpha, float b1c, float b2c, float eps) {
+  float ww[N], mm[N], vv[N];
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    ww[n] = w[i[n]];
+    mm[n] = m[i[n]];
+    vv[n] = v[i[n]];
+  }
+#pragma unroll
+  for (int n = 0; n < N; ++n) ww[n] = adam(ww[n], mm[n], vv[n], g[n], alpha, b1c, b2c, eps);
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    w[i[n]] = ww[n];
+    m[i[n]] = mm[n];
+    v[i[n]] = vv[n];
+  }
+}
 
 struct FitArgs {
   float* flat;           // the net's flat parameters (in / out)
@@ -790,10 +811,8 @@ __global__ void __launch_bounds__(kT) k_fit_critic(FitArgs a) {
         ga0 += dz * sA[2 * r];
         ga1 += dz * sA[2 * r + 1];
       }
-      adam_lds(uW, uM, uV, uW3 + u, gw3, alpha, b1c, b2c, a.eps);
-      adam_lds(uW, uM, uV, uB2 + u, gb2, alpha, b1c, b2c, a.eps);
-      adam_lds(uW, uM, uV, uWA + 2 * u, ga0, alpha, b1c, b2c, a.eps);
-      adam_lds(uW, uM, uV, uWA + 2 * u + 1, ga1, alpha, b1c, b2c, a.eps);
+      adam_lds_n<4>(uW, uM, uV, {uW3 + u, uB2 + u, uWA + 2 * u, uWA + 2 * u + 1}, {gw3, gb2, ga0, ga1}, alpha, b1c,
+                    b2c, a.eps);
       if (wv == 2) {  // b3: the 16 rows' dL/dq in row 0 of wave 2
         const float gb3 = sum16(lane < kB ? sDQ[lane] : 0.f);
         if (lane == 0) adam_lds(uW, uM, uV, uB3, gb3, alpha, b1c, b2c, a.eps);
@@ -1149,9 +1168,7 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a, const float* __rest
         gw1 += sDZ3[2 * r + 1] * hv;
         gb2 += sDZ[r * LZ + u];
       }
-      adam_lds(uW, uM, uV, aW3 + 2 * u, gw0, alpha, b1c, b2c, a.eps);
-      adam_lds(uW, uM, uV, aW3 + 2 * u + 1, gw1, alpha, b1c, b2c, a.eps);
-      adam_lds(uW, uM, uV, aB2 + u, gb2, alpha, b1c, b2c, a.eps);
+      adam_lds_n<3>(uW, uM, uV, {aW3 + 2 * u, aW3 + 2 * u + 1, aB2 + u}, {gw0, gw1, gb2}, alpha, b1c, b2c, a.eps);
       if (wv == 2) {  // b3: dL/dz3 of the 16 rows, output j in row j of wave 2
         const float gb3 = sum16(lane < 2 * kB ? sDZ3[2 * (lane & 15) + (lane >> 4)] : 0.f);
         if (lane == 0 || lane == 16) adam_lds(uW, uM, uV, aB3 + (lane >> 4), gb3, alpha, b1c, b2c, a.eps);
