@@ -10,7 +10,8 @@
 //     Q  all-reduce of 16 partials (publish 16, read P x 16),
 //     D  reduce-scatter of the 16 x 256 dX2 partials (publish 4,096, read 4,096);
 //   column partition (v2: which 8 / 16 / 32, granule PAIRS in 16-byte sc1
-//   stores and loads, every load of a pass in flight before the tag checks):
+//   stores and loads, every load of a pass in flight before the tag checks;
+//   --plain: plain stores, the reads through one XCD's L2, S = 8 only):
 //     R  reduce-scatter of the 16 x 128 layer-2 partials (publish and read
 //        P x 256 granules: a 16 x 16 slice per owner),
 //     Q2 the all-reduce of 16 partials,
@@ -72,9 +73,16 @@ __device__ __forceinline__ bool sweep_rs(gu64* base, int P, int w, int gd, unsig
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, -1, 0x00020000);
 }
-__device__ __forceinline__ void put2(__amdgpu_buffer_rsrc_t r, uint32_t byte_off, unsigned epoch, float a, float b) {
+// plain: a plain store, which keeps the line in the writer's XCD L2 (only
+// correct when every reader runs on that XCD: S = 8 under round-robin
+// placement, the workgroups' XCC ids printed beside); else aux 16 = sc1
+__device__ __forceinline__ void put2(__amdgpu_buffer_rsrc_t r, uint32_t byte_off, unsigned epoch, float a, float b,
+                                     bool plain) {
   const u4v v = {__float_as_uint(a), epoch, __float_as_uint(b), epoch};
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, byte_off, 0, 16);  // aux 16: sc1
+  if (plain)
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, byte_off, 0, 0);
+  else
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, byte_off, 0, 16);
 }
 // N pairs per lane at byte offsets off[k]; every load issued, then the checks
 template <int N>
@@ -102,7 +110,7 @@ __device__ __forceinline__ bool get2(__amdgpu_buffer_rsrc_t r, const uint32_t (&
 
 template <int P>
 __device__ void rounds_v2(unsigned long long* xbuf, unsigned* tmo, int w, int rounds, unsigned epoch0, int which,
-                          float& acc) {
+                          bool plain, float& acc) {
   // per buffer: R [P src][P dst][256], Q [P][16], G [P][256] granules
   constexpr int nR = P * P * 256, nQ = P * 16, nG = P * 256, nB = nR + nQ + nG;
   const __amdgpu_buffer_rsrc_t rs = rsrc_of(xbuf);
@@ -115,7 +123,7 @@ __device__ void rounds_v2(unsigned long long* xbuf, unsigned* tmo, int w, int ro
 #pragma unroll
       for (int k = 0; k < P / 2; ++k) {
         const int pr = t + 256 * k;  // pair index over [P dst][128 pairs]
-        put2(rs, b0 + ((uint32_t)w * P * 256 + 2 * pr) * 8u, e + 1, 1.f, 2.f);
+        put2(rs, b0 + ((uint32_t)w * P * 256 + 2 * pr) * 8u, e + 1, 1.f, 2.f, plain);
       }
       uint32_t off[P / 2];
 #pragma unroll
@@ -129,7 +137,7 @@ __device__ void rounds_v2(unsigned long long* xbuf, unsigned* tmo, int w, int ro
       for (int k = 0; k < P; ++k) acc += v[k];
     }
     if (which & 16) {  // Q2: 16 granules, read P x 16
-      if (t < 8) put2(rs, b0 + ((uint32_t)nR + w * 16 + 2 * t) * 8u, e + 2, 1.f, 1.f);
+      if (t < 8) put2(rs, b0 + ((uint32_t)nR + w * 16 + 2 * t) * 8u, e + 2, 1.f, 1.f, plain);
       if (t < P * 8) {
         uint32_t off[1] = {b0 + ((uint32_t)nR + 2 * t) * 8u};
         float v[2];
@@ -138,7 +146,7 @@ __device__ void rounds_v2(unsigned long long* xbuf, unsigned* tmo, int w, int ro
       }
     }
     if (which & 32) {  // G: publish 256 (128 pairs: lanes < 128), read P x 256 (P / 2 pairs per lane)
-      if (t < 128) put2(rs, b0 + ((uint32_t)nR + nQ + w * 256 + 2 * t) * 8u, e + 3, 3.f, 4.f);
+      if (t < 128) put2(rs, b0 + ((uint32_t)nR + nQ + w * 256 + 2 * t) * 8u, e + 3, 3.f, 4.f, plain);
       uint32_t off[P / 2];
 #pragma unroll
       for (int k = 0; k < P / 2; ++k) off[k] = b0 + ((uint32_t)nR + nQ + 2 * (t + 256 * k)) * 8u;
@@ -153,17 +161,17 @@ __device__ void rounds_v2(unsigned long long* xbuf, unsigned* tmo, int w, int ro
 
 extern "C" __global__ void __launch_bounds__(256) k_seam(unsigned long long* xbuf, unsigned* tmo, unsigned* xcc,
                                                          float* sink, int P, int S, int rounds, unsigned epoch0,
-                                                         int which) {
+                                                         int which, int plain) {
   if (blockIdx.x % S) return;
   const int w = blockIdx.x / S;
   if (w >= P) return;
   if (threadIdx.x == 0) xcc[w] = __builtin_amdgcn_s_getreg(20 | (31 << 11));
   float acc = 0.f;
   if (which >= 8) {
-    if (P == 2) rounds_v2<2>(xbuf, tmo, w, rounds, epoch0, which, acc);
-    else if (P == 4) rounds_v2<4>(xbuf, tmo, w, rounds, epoch0, which, acc);
-    else if (P == 8) rounds_v2<8>(xbuf, tmo, w, rounds, epoch0, which, acc);
-    else if (P == 16) rounds_v2<16>(xbuf, tmo, w, rounds, epoch0, which, acc);
+    if (P == 2) rounds_v2<2>(xbuf, tmo, w, rounds, epoch0, which, plain != 0, acc);
+    else if (P == 4) rounds_v2<4>(xbuf, tmo, w, rounds, epoch0, which, plain != 0, acc);
+    else if (P == 8) rounds_v2<8>(xbuf, tmo, w, rounds, epoch0, which, plain != 0, acc);
+    else if (P == 16) rounds_v2<16>(xbuf, tmo, w, rounds, epoch0, which, plain != 0, acc);
     if (acc == 123.456f) sink[0] = acc;
     return;
   }
@@ -194,10 +202,10 @@ extern "C" __global__ void __launch_bounds__(256) k_seam(unsigned long long* xbu
 }
 
 extern "C" int seam_launch(unsigned long long* xbuf, unsigned* tmo, unsigned* xcc, float* sink, int P, int S,
-                           int rounds, unsigned epoch0, int which, void* stream) {
+                           int rounds, unsigned epoch0, int which, int plain, void* stream) {
   if (P < 1 || P > 16 || S < 1 || (256 % P)) return -1;
   if (which >= 8 && P != 2 && P != 4 && P != 8 && P != 16) return -1;
   hipLaunchKernelGGL(k_seam, dim3(P * S), dim3(256), 0, (hipStream_t)stream, xbuf, tmo, xcc, (float*)sink, P, S,
-                     rounds, epoch0, which);
+                     rounds, epoch0, which, plain);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
