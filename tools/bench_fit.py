@@ -20,6 +20,7 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--steps", type=int, default=4096)
     p.add_argument("--reps", type=int, default=3)
+    p.add_argument("--resident-only", action="store_true", help="skip the three-launch chunks (PMC passes)")
     a = p.parse_args()
     from skillshot_learning_amd import learner
     dev = torch.device("cuda", 0)
@@ -56,6 +57,8 @@ def main():
             fu.fit_check()
             print(json.dumps(dict(kind="resident actor", P=int(P), one_xcd=xcd == "1", steps=n,
                                   us_per_step=round(us, 3), rep=rep)), flush=True)
+        if a.resident_only:
+            continue
         M = d.FIT_CHUNK
         chunks = n // M - 1
         for critic in (True, False):
