@@ -313,6 +313,9 @@ __device__ unsigned long long* sk_fit_trace;
 #define SK_FT(k, i) \
   do {              \
   } while (0)
+#define SK_FT_FLUSH() \
+  do {                \
+  } while (0)
 #endif
 // -DSK_TRACE_FIT_P5 moves stamps 7 .. 9 into phase 5 (tools/trace_fit.py --p5)
 #ifdef SK_TRACE_FIT_P5
@@ -325,9 +328,6 @@ __device__ unsigned long long* sk_fit_trace;
   do {               \
   } while (0)
 #define SK_FT7(k, i) SK_FT(k, i)
-#define SK_FT_FLUSH() \
-  do {                \
-  } while (0)
 #endif
 
 // ---------------------------------------------------------------- shared pieces
