@@ -26,12 +26,18 @@ class ActorKernel:
         self.device = p.device
         self.buf = torch.empty(int(self.L.sk_actor_packed_bytes()), dtype=torch.uint8, device=self.device)
         self.seed = int(seed) & ((1 << 64) - 1)
-        self.calls = 0
         # device noise-call number, the launch's arrival slot and its 8 group
         # slots (sk_actor_forward_noise: SK_ACTOR_COUNTER_WORDS words)
         self._ctr = torch.zeros(130, dtype=torch.int64, device=self.device)
         self.counter = self._ctr[:1]
         self.refresh()
+
+    @property
+    def calls(self):
+        """the device's noise call number (the draws so far; a host sync).
+        No host mirror is kept: launches that draw advance it on device, an
+        episode launch by the ticks it played"""
+        return int(self._ctr[0].item())
 
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
@@ -59,7 +65,6 @@ class ActorKernel:
             raise ValueError("obs must be [M, 12]")
         m = x.shape[0]
         y = out if out is not None else torch.empty((m, 2), dtype=torch.float32, device=self.device)
-        self.calls += 1
         rc = self.L.sk_actor_forward_noise(ctypes.c_void_p(self.buf.data_ptr()), ctypes.c_void_p(x.data_ptr()),
                                            ctypes.c_void_p(y.data_ptr()), m, float(noise_sd), float(action_sd),
                                            self.seed, ctypes.c_void_p(self._ctr.data_ptr()), self._stream())
@@ -93,12 +98,18 @@ class ActorKernel32:
         self.device = p.device
         self.flat = flatten_module(actor)
         self.seed = int(seed) & ((1 << 64) - 1)
-        self.calls = 0
         self._ctr = torch.zeros(130, dtype=torch.int64, device=self.device)  # SK_ACTOR_COUNTER_WORDS
         self.counter = self._ctr[:1]
         self.pack = torch.zeros(int(self.L.sk_actor_split_pack_bytes()), dtype=torch.uint8, device=self.device)
         self._packed = None  # (flat buffer, the parameters' versions) the pack was last written from
         self.ensure_pack()
+
+    @property
+    def calls(self):
+        """the device's noise call number (the draws so far; a host sync).
+        No host mirror is kept: launches that draw advance it on device, an
+        episode launch by the ticks it played"""
+        return int(self._ctr[0].item())
 
     def refresh(self):
         """repack from the current flat parameters"""
@@ -133,7 +144,6 @@ class ActorKernel32:
             raise ValueError("obs must be [M, 12]")
         m = x.shape[0]
         y = out if out is not None else torch.empty((m, 2), dtype=torch.float32, device=self.device)
-        self.calls += 1
         pack = self.ensure_pack()
         rc = self.L.sk_actor_forward_f32(ctypes.c_void_p(self.flat.data_ptr()), ctypes.c_void_p(pack.data_ptr()),
                                          ctypes.c_void_p(x.data_ptr()),

@@ -595,6 +595,149 @@ __device__ __forceinline__ void tick_env_fast(const Cfg& c, Env& e, float a0_mov
   tick_env_fast(c, e, m0, m1, tq0, tq1, k0 & k1, k2, k3, a0_move, a0_look, a1_move, a1_look);
 }
 
+// ---------------------------------------------------------------- carried trig
+// k_step_multi's tick with its sincos off the dependent chain (round 6).
+// A lane steps the same game through every tick of a launch, and every sine
+// the tick needs is of a rotation the previous tick produced:
+//   * player p moves along its rotation at the START of the tick
+//     (Player.py:63-64), which is the rotation tick t - 1 ended with;
+//   * a projectile in flight keeps the rotation it was fired with
+//     (Projectile.py:28-29, :40-41), the player's rotation at that tick's end.
+// So tick t - 1's final rotations are the only new arguments: their exact
+// sincos (sincos_bf, the library past its range — the same values tick_env_m
+// computes) is evaluated at the top of tick t, after tick t's loads are
+// issued, in the shadow of the memory round trip.  Each value is KEYED by the
+// rotation it is the sincos of and used only where the key equals the
+// rotation just loaded (bitwise); any lane that misses (tick 0 of a launch)
+// sends its wave through the full evaluation.  The state still makes its
+// round trip through memory every tick; only derived values are reused.
+//
+// The one sine the chain still needs is that of a projectile FIRED this tick:
+// rotation rot + a*look (Player.py:33-39, :80-84), known only once the
+// action arrives.  It comes from the exact sincos of rot by angle addition in
+// fp32 (sktrig::sincos_add); the fp32 delta decides int(round(q - d)) unless
+// it lies within its error bound of a half-integer (sktrig::round_safe; the
+// budget of tick_env_fast: inputs here are exact values rounded to fp32,
+// better than SKT_FAST_ERR, and rot + a*look's own rounding is below 1.2e-10
+// for |rot| < 1.6e6).  A wave with any such lane, or with |rot| past that
+// range, or a NaN action, evaluates the fired projectiles' sincos exactly
+// (~1e-5 of waves).  Bit for bit tick_env_m's result.
+struct TrigCarry {
+  double kr[2], kq[2];          // keys: m[p] = sincos(kr[p]), tq[p] = sincos(kq[p])
+  sktrig::SinCos m[2], tq[2];
+  double pr[2];                 // the last tick's final rotations (evaluated at the next tick's top)
+  bool qs[2];                   // ... whose projectile's rotation equals it bitwise
+  bool have, pend;              // wave-uniform: keys valid / pr pending
+};
+
+__device__ __forceinline__ bool same_bits(double a, double b) {
+  return __double_as_longlong(a) == __double_as_longlong(b);
+}
+
+// tick t - 1's final rotations -> keys (top of tick t, under its loads)
+__device__ __forceinline__ void carry_advance(TrigCarry& t) {
+  bool k0, k1;
+  t.m[0] = sktrig::sincos_bf(t.pr[0], &k0);
+  t.m[1] = sktrig::sincos_bf(t.pr[1], &k1);
+  if (!(k0 & k1)) {
+    if (!k0) t.m[0] = sincos_lib(t.pr[0]);
+    if (!k1) t.m[1] = sincos_lib(t.pr[1]);
+  }
+  t.kr[0] = t.pr[0];
+  t.kr[1] = t.pr[1];
+  if (t.qs[0]) { t.tq[0] = t.m[0]; t.kq[0] = t.pr[0]; }
+  if (t.qs[1]) { t.tq[1] = t.m[1]; t.kq[1] = t.pr[1]; }
+  t.have = true;
+  t.pend = false;
+}
+
+// the end of a tick: its final rotations become the next tick's arguments
+__device__ __forceinline__ void carry_note(TrigCarry& t, const Env& e) {
+  t.pr[0] = e.rot[0];
+  t.pr[1] = e.rot[1];
+  t.qs[0] = same_bits(e.qrot[0], e.rot[0]);
+  t.qs[1] = same_bits(e.qrot[1], e.rot[1]);
+  t.pend = true;
+}
+
+__device__ __forceinline__ void tick_env_carry(const Cfg& c, Env& e, TrigCarry& t, bool in, float a0_move,
+                                               float a0_look, float a1_move, float a1_look) {
+  using sktrig::round_safe;
+  const bool f0 = e.qcd[0] <= 0, f1 = e.qcd[1] <= 0;  // fires this tick (Player.py:80)
+  const bool miss = !t.have || !same_bits(e.rot[0], t.kr[0]) || !same_bits(e.rot[1], t.kr[1]) ||
+                    (e.qvalid[0] && !f0 && !same_bits(e.qrot[0], t.kq[0])) ||
+                    (e.qvalid[1] && !f1 && !same_bits(e.qrot[1], t.kq[1]));
+  if (__ballot(in && miss) != 0) {  // the launch's first tick
+    bool k0, k1, k2, k3;
+    t.m[0] = sktrig::sincos_bf(e.rot[0], &k0);
+    t.m[1] = sktrig::sincos_bf(e.rot[1], &k1);
+    t.tq[0] = sktrig::sincos_bf(e.qrot[0], &k2);
+    t.tq[1] = sktrig::sincos_bf(e.qrot[1], &k3);
+    if (!(k0 & k1 & k2 & k3)) {
+      if (!k0) t.m[0] = sincos_lib(e.rot[0]);
+      if (!k1) t.m[1] = sincos_lib(e.rot[1]);
+      if (!k2) t.tq[0] = sincos_lib(e.qrot[0]);
+      if (!k3) t.tq[1] = sincos_lib(e.qrot[1]);
+    }
+    t.kr[0] = e.rot[0]; t.kr[1] = e.rot[1];
+    t.kq[0] = e.qrot[0]; t.kq[1] = e.qrot[1];
+    t.have = true;
+  }
+  const float l0 = clamp_action_f(a0_look), l1 = clamp_action_f(a1_look);
+  const double rn0 = e.rot[0] + (double)l0 * c.look;  // == move_look_s
+  const double rn1 = e.rot[1] + (double)l1 * c.look;
+  // a fired projectile's sincos(rn) = sincos(rot + l*look) by angle addition
+  const float lk = (float)c.look, qs = (float)c.qspeed, eq = 2e-6f * qs;
+  const sktrig::SinCosF u0 = sktrig::sincos_add(sktrig::SinCosF{(float)t.m[0].s, (float)t.m[0].c}, l0 * lk);
+  const sktrig::SinCosF u1 = sktrig::sincos_add(sktrig::SinCosF{(float)t.m[1].s, (float)t.m[1].c}, l1 * lk);
+  const float ex0 = u0.s * qs, ey0 = u0.c * qs, ex1 = u1.s * qs, ey1 = u1.c * qs;
+  const bool un0 = f0 && !((int)(fabs(e.rot[0]) < 1647099.3291652855) & (int)round_safe(ex0, eq) &
+                                 (int)round_safe(ey0, eq));
+  const bool un1 = f1 && !((int)(fabs(e.rot[1]) < 1647099.3291652855) & (int)round_safe(ex1, eq) &
+                                 (int)round_safe(ey1, eq));
+  sktrig::SinCos t0 = t.tq[0], t1 = t.tq[1];  // in flight: the carried exact values
+  bool fast0 = f0, fast1 = f1;
+  if (__builtin_expect(__ballot(in && (un0 | un1)) != 0, 0)) {  // the exact sincos of the fired projectiles
+    bool k0, k1;
+    sktrig::SinCos x0 = sktrig::sincos_bf(rn0, &k0), x1 = sktrig::sincos_bf(rn1, &k1);
+    if (!(k0 & k1)) {
+      if (!k0) x0 = sincos_lib(rn0);
+      if (!k1) x1 = sincos_lib(rn1);
+    }
+    if (f0) t0 = x0;
+    if (f1) t1 = x1;
+    fast0 = fast1 = false;
+  }
+  // do_actions(1, ...), do_actions(2, ...)  SkillshotLearner.py:206-213
+  move_direction_sc(c, e.px[0], e.py[0], t.m[0], (double)a0_move);
+  e.rot[0] = rn0;
+  shoot(c, e, 0);
+  move_direction_sc(c, e.px[1], e.py[1], t.m[1], (double)a1_move);
+  e.rot[1] = rn1;
+  shoot(c, e, 1);
+  // game_tick  SkillshotGame.py:115-122 (Projectile.py:38-53)
+  if (e.live) {
+    e.ticks += 1;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      if (e.qvalid[p]) {
+        const sktrig::SinCos tt = p ? t1 : t0;
+        const bool fast = p ? fast1 : fast0;
+        const float ex = p ? ex1 : ex0, ey = p ? ey1 : ey0;
+        const double sp = (double)c.qspeed;
+        const int nx = fast ? e.qx[p] - (int)rintf(ex) : (int)__builtin_rint((double)e.qx[p] - tt.s * sp);
+        const int ny = fast ? e.qy[p] - (int)rintf(ey) : (int)__builtin_rint((double)e.qy[p] - tt.c * sp);
+        bool ok = (nx + c.qsize <= c.W) & (nx >= 0) & (ny + c.qsize <= c.H) & (ny >= 0);
+        if (ok) { e.qx[p] = nx; e.qy[p] = ny; } else { e.qvalid[p] = 0; }
+      }
+      e.qcd[p] -= 1;
+      e.qage[p] += 1;
+    }
+    collide_s(c, e.px[0], e.py[0], e.qx[0], e.qy[0], e.qvalid[0], e.px[1], e.py[1], e.qx[1], e.qy[1],
+              e.qvalid[1], e.live, e.winner);
+  }
+}
+
 // ---------------------------------------------------------------- features
 // SkillshotGame.get_dist_line_point (SkillshotGame.py:124-130); g**2 as g*g
 __device__ __forceinline__ double dist_line_point(double g, int lx, int ly, int cx, int cy) {

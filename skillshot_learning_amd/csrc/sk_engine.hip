@@ -28,6 +28,12 @@
 
 using namespace sk;
 
+// k_step_multi carries each tick's sincos to the next (tick_env_carry); 0:
+// every tick evaluates its four (A/B: tools/build_variant.sh -DSK_MULTI_CARRY=0)
+#ifndef SK_MULTI_CARRY
+#define SK_MULTI_CARRY 1
+#endif
+
 struct sk_env {
   int32_t n;
   int64_t env_offset;
@@ -713,7 +719,7 @@ template <int POL, bool PACK>
 __device__ __forceinline__ void multi_compute(const MultiArgs& a, const Cfg& c, __amdgpu_buffer_rsrc_t r,
                                               __amdgpu_buffer_rsrc_t rp, MultiLane& L, WaveCtr& wc, int64_t t,
                                               uint64_t step0, int tick, const MultiRaw& w, bool& packed,
-                                              bool last) {
+                                              bool last, TrigCarry& tc) {
   Env e;
   multi_decode<PACK>(w, packed, e);
   const float2* acts = w.act;
@@ -727,11 +733,17 @@ __device__ __forceinline__ void multi_compute(const MultiArgs& a, const Cfg& c, 
   // k_step's fp64 tick.  k_step_fast's (fp32 trig, exact fp64 redo) was no
   // faster at 400 ticks per launch and 20 % slower at 20 (65,536 games:
   // 2.50 vs 2.51 and 3.37 vs 2.71 us per tick; profiles/
-  // r03i_multi_fast_early_sweep.jsonl)
+  // r03i_multi_fast_early_sweep.jsonl).  Round 6: the same values with
+  // the sincos carried from the previous tick (tick_env_carry, sk_device.hpp)
+#if SK_MULTI_CARRY
+  tick_env_carry(c, e, tc, L.in, acts[0].x, acts[0].y, acts[1].x, acts[1].y);
+#else
+  (void)tc;
   bool k0, k1;
   const sktrig::SinCos m0 = sktrig::sincos_bf(e.rot[0], &k0);
   const sktrig::SinCos m1 = sktrig::sincos_bf(e.rot[1], &k1);
   tick_env_m(c, e, m0, m1, k0 & k1, (double)acts[0].x, (double)acts[0].y, (double)acts[1].x, (double)acts[1].y);
+#endif
   // every load of this tick consumed (the counter slot's, issued first, with
   // them): without this the waitcnt pass, its tracking lost across the loop,
   // drains every store before the final counter store
@@ -753,6 +765,9 @@ __device__ __forceinline__ void multi_compute(const MultiArgs& a, const Cfg& c, 
       reset_fixed(c, e);
     }
   }
+#if SK_MULTI_CARRY
+  if (!last) carry_note(tc, e);
+#endif
   bool to_pack = false;
   if constexpr (PACK) {
     const bool fit =
@@ -873,11 +888,17 @@ __global__ void __launch_bounds__(BLK + (PF > 0 ? 64 : 0)) k_step_multi(MultiArg
   WaveCtr wc = ctr_load<BLK>(a.ctr);
   const uint64_t step0 = step_read(a.step);
   int t = 0;
+  TrigCarry tc;
+  tc.have = tc.pend = false;
   do {  // n_ticks >= 1 (host-checked): every path to the counter store passes ctr_settle
     MultiRaw w;
     if constexpr (PF > 0) __builtin_amdgcn_s_barrier();
     multi_load<POL, PACK>(a, r, rp, L, slab, packed, w);
-    multi_compute<POL, PACK>(a, c, r, rp, L, wc, so, step0, t, w, packed, t + 1 == a.n_ticks);
+#if SK_MULTI_CARRY
+    if (tc.pend) carry_advance(tc);  // the last tick's rotations, while this tick's loads fly
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+    multi_compute<POL, PACK>(a, c, r, rp, L, wc, so, step0, t, w, packed, t + 1 == a.n_ticks, tc);
 #ifdef SK_TRACE_MULTI
     if (t < 29) SK_MTS(1 + t);
 #endif

@@ -564,12 +564,22 @@ __device__ __forceinline__ uint4 drop_bits(const FitArgs& a, uint64_t call, int 
 __device__ __forceinline__ float keras_alpha(const FitArgs& a, float tk) {
   return a.lr * sqrtf(1.f - powf(a.beta2, tk)) / (1.f - powf(a.beta1, tk));
 }
+// The Adam step count after j steps from tk0, as the three-launch chain
+// produces it: j fp32 additions of 1 (k_grad_slice_fwd / k_critic_grad32),
+// which stop changing the count at 2^24 (2^24 + 1 rounds to even, 2^24).
+// Above 2^24 (a loaded count) only the first addition can change it (an odd
+// mantissa rounds up to even), so one addition stands for all
+__host__ __device__ __forceinline__ float adam_count(float tk0, int j) {
+  if (j <= 0) return tk0;
+  return tk0 < 16777216.f ? fminf(tk0 + (float)j, 16777216.f) : tk0 + 1.0f;
+}
 // Adam's step sizes of steps k0 .. k0 + kAlphaN - 1 into LDS, computed in
 // parallel once per kAlphaN steps (two powf per step off the step chain);
-// step k applies the count tk0 + k + 1 (k_adam_flat reads it incremented)
+// step k applies the count adam_count(tk0, k + 1) (k_adam_flat reads it incremented)
 constexpr int kAlphaN = 2048;
 __device__ __forceinline__ void alpha_fill(const FitArgs& a, float* sAlpha, float tk0, int k0) {
-  for (int j = threadIdx.x; j < kAlphaN && k0 + j < a.M; j += kT) sAlpha[j] = keras_alpha(a, tk0 + (float)(k0 + j + 1));
+  for (int j = threadIdx.x; j < kAlphaN && k0 + j < a.M; j += kT)
+    sAlpha[j] = keras_alpha(a, adam_count(tk0, k0 + j + 1));
   __syncthreads();
 }
 
@@ -826,7 +836,7 @@ __global__ void __launch_bounds__(kT) k_fit_critic(FitArgs a) {
     // no barrier: the next step writes only the other buffers before its first
     // one; the W2 mirror's next reader (dh1) is behind three more
   }
-  const float tk = tk0 + (float)a.M;
+  const float tk = adam_count(tk0, a.M);
   SK_FT_FLUSH();
 
   // the owned slice back; workgroup 0 the unit parameters and the counters
@@ -1180,7 +1190,7 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a, const float* __rest
     SK_FT7(k, 9);
     SK_FT(k, 10);
   }
-  const float tk = tk0 + (float)a.M;
+  const float tk = adam_count(tk0, a.M);
   SK_FT_FLUSH();
 
   w2_store<G, kH1>(W2, a.flat, d, wv, li, lg);
@@ -1216,10 +1226,21 @@ __global__ void __launch_bounds__(kT) k_fit_actor(FitArgs a, const float* __rest
   }
 }
 
+// The resident kernels need up to ~150 KB of dynamic LDS per workgroup and
+// their P workgroups resident together (include/skillshot.h,
+// INTEGRATION.md): a device whose opt-in LDS limit is smaller, or a failed
+// attribute call, is reported as SK_EHIP before anything is launched, and
+// the Python layer takes the three-launch steps instead
 template <typename K, typename... X>
 int launch_fit(K kernel, int P, size_t lds, bool& attr, const FitArgs& a, hipStream_t st, X... extra) {
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    int dev = 0, optin = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&optin, hipDeviceAttributeSharedMemPerBlockOptin, dev) != hipSuccess ||
+        (size_t)optin < lds)
+      return SK_EHIP;
+    if (hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+      return SK_EHIP;
     attr = true;
   }
   kernel<<<P * a.stride, kT, lds, st>>>(a, extra...);

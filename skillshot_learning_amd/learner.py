@@ -27,6 +27,7 @@ each rank's sampled minibatch all-gathered into a shared batch.
 import ctypes
 import math
 import os
+import warnings
 
 import numpy as np
 import torch
@@ -34,6 +35,7 @@ import torch.distributed as dist
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ._capi import SkillshotError
 from .rng import DROP_SCALE, dropout_keep
 
 STATE_DIM = 12   # SkillshotLearner.py:54
@@ -581,11 +583,10 @@ class DDPG:
                     os.environ.get("SK_FIT_RESIDENT", "1") != "0")
         if resident:
             try:
-                done = fu.fit_critic(states, actions, rewards) * b
-                for k in range(done, n, b):  # the partial last minibatch
+                done = self._resident_pass(fu, True, lambda: fu.fit_critic(states, actions, rewards)) * b
+                for k in range(done, n, b):  # the partial last minibatch (or the whole pass, after a failure)
                     self.critic_step(states[k:k + b], actions[k:k + b], rewards[k:k + b])
                 self._actor_pass(states, b, n)
-                fu.fit_check()
             finally:
                 fu.soft_update_in_adam = True
             return
@@ -615,6 +616,24 @@ class DDPG:
             if fu is not None:
                 fu.soft_update_in_adam = True
 
+    @staticmethod
+    def _resident_pass(fu, critic, run):
+        """one resident models_fit pass, checked before the next pass reads
+        its net (one host sync per pass).  A launch the device refuses
+        (SK_EHIP: its LDS limit or the attribute call, before anything ran)
+        or an in-launch exchange lost (fit_check) restores the net as it was
+        and returns 0 minibatches done: the caller runs the whole pass on the
+        three-launch steps"""
+        snap = fu.fit_snapshot(critic)
+        try:
+            done = run()
+            fu.fit_check()
+            return done
+        except SkillshotError as e:
+            fu.fit_restore(snap)
+            warnings.warn(f"resident models_fit pass failed ({e}); rerunning it on the three-launch steps")
+            return 0
+
     def _actor_pass(self, states, b, n):
         """models_fit's actor pass (:436-443) on the fused kernels: resident
         launches (sk_fit_actor_f32) for every full minibatch and the partial
@@ -622,7 +641,8 @@ class DDPG:
         for this pass (the first minibatch eager, captured chunks of
         FIT_CHUNK, the rest eager)"""
         if os.environ.get("SK_FIT_RESIDENT", "1") != "critic":
-            done = self._fused.fit_actor(states) * b
+            fu = self._fused
+            done = self._resident_pass(fu, False, lambda: fu.fit_actor(states)) * b
             for k in range(done, n, b):
                 self.model_actor_fit_step(states[k:k + b])
             return
@@ -1010,7 +1030,6 @@ class SkillshotLearner:
             self._episode_bufs = ep
             lengths = ep["lengths"].long()
             T = int(lengths.max()) if self.n_envs else 0
-            self.actor_kernel.calls += T  # the host mirror of the device call number
             keep = (torch.arange(T, device=self.device)[:, None] < lengths[None, :])[:, None, :].expand(
                 T, 2, self.n_envs)
             S.append(ep["states"][:T][keep])
@@ -1087,8 +1106,7 @@ class SkillshotLearner:
     def tick_graph(self, batch=256, updates_per_tick=1, ticks_per_graph=2, warmup=3, overlap=None):
         """The replay-rule tick of `train_ticks` captured as ONE hipGraph.
 
-        One replay runs `ticks_per_graph` ticks (even: the engine's device step
-        counter advances through two ping-pong slots): per tick the fused actor
+        One replay runs `ticks_per_graph` ticks: per tick the fused actor
         kernel (noise call number on device), the fused env step with
         obs/reward/auto-reset into static buffers, a device-side-head insert of
         the 2N transitions, `updates_per_tick` critic + actor updates on
@@ -1113,12 +1131,17 @@ class SkillshotLearner:
         with the fp32 kernels, inside the critic's backward launch.  Either way
         the overlapped update draws from the rows inserted before the tick
         (TickGraph.overlap), one tick later than the reference.
+
+        Any ticks_per_graph >= 1: the engine's step counter, the acting
+        observation and the overlapped tick's horizon each alternate between
+        two slots per tick, so an odd count is captured as two graphs, one
+        per starting slot, which run() replays alternately.
         """
         if self.device.type != "cuda":
             raise RuntimeError("tick_graph needs the GPU engine")
-        if ticks_per_graph % 2:
-            raise ValueError("ticks_per_graph must be even (step-counter ping-pong slots)")
-        return TickGraph(self, batch, updates_per_tick, ticks_per_graph, warmup, overlap)
+        if int(ticks_per_graph) < 1:
+            raise ValueError("ticks_per_graph must be >= 1")
+        return TickGraph(self, batch, updates_per_tick, int(ticks_per_graph), warmup, overlap)
 
     # ------------------------------------------------------------ persistence
     def state_dict(self):
@@ -1272,23 +1295,34 @@ class TickGraph:
         # replays cannot leave the captured slot stale
         g.sync_step_counter(ctypes.c_void_p(self.stream.cuda_stream))
         mirror = L.replay.total  # capture records the inserts without running them
-        if self.multi_rank_mode and self.multi_rank_mode.endswith("segmented"):
-            self.graph = None
-            self._segments = self._capture_segments()
-        else:
-            self.graph = torch.cuda.CUDAGraph()
-            self.graph.register_generator_state(L.gen)
+        # Every tick flips three two-slot alternations (the engine's step
+        # counter slot, the acting observation buffer, the overlapped tick's
+        # horizon), so a graph of an odd number of ticks ends in the other
+        # slot than it starts in: then a second graph is captured right after
+        # the first, starting where the first ends, and run() alternates the
+        # two (phase 0 / 1).  An even count needs one graph.
+        self._phases = []
+        for _ in range(1 if self.ticks % 2 == 0 else 2):
+            if self.multi_rank_mode and self.multi_rank_mode.endswith("segmented"):
+                self._phases.append(("segments", self._capture_segments()))
+                continue
+            graph = torch.cuda.CUDAGraph()
+            graph.register_generator_state(L.gen)
             # thread-local capture: only this thread's HIP calls are checked
             # against the capture, so RCCL's watchdog thread may keep
             # querying the events of eager collectives from the warm-up
             # (global mode aborted the process when it did, intermittently)
             self._capturing = True
             try:
-                with torch.cuda.graph(self.graph, stream=self.stream, capture_error_mode="thread_local"):
+                with torch.cuda.graph(graph, stream=self.stream, capture_error_mode="thread_local"):
                     for _ in range(self.ticks):
                         self._tick(update=True)
             finally:
                 self._capturing = False
+            self._phases.append(("graph", graph))
+        self.graph = self._phases[0][1] if self._phases[0][0] == "graph" else None
+        self._segments = self._phases[0][1] if self._phases[0][0] == "segments" else None
+        self._phase = 0  # which graph the next replay runs (the slot the current tick starts in)
         self.stream.synchronize()
         L.replay.total = mirror
         self.replays = 0
@@ -1328,8 +1362,8 @@ class TickGraph:
 
     @property
     def obs(self):
-        """the observation the next tick acts on"""
-        return self._obs[self._cur]
+        """the observation the next replayed tick acts on"""
+        return self._obs[getattr(self, "_phase", self._cur)]
 
     def _act_insert(self, obs, total_copy=None):
         """act -> do_actions -> game_tick -> get_state (SkillshotLearner.py
@@ -1470,18 +1504,21 @@ class TickGraph:
         cur = torch.cuda.current_stream(self.L.device)
         self.stream.wait_stream(cur)
         with torch.cuda.stream(self.stream):  # replay() launches on the current stream
+            # both step slots current: the graph of either phase reads its own
             self.L.game_environment.sync_step_counter(ctypes.c_void_p(self.stream.cuda_stream))
-            if self.overlap:  # a replay starts at parity 0: its first update samples the current count
-                self.L.replay.horizon[0].copy_(self.L.replay.total_t)
+            if self.overlap:  # the first replayed update samples the current count
+                self.L.replay.horizon[self._phase].copy_(self.L.replay.total_t)
             for _ in range(n):
-                if self._segments is None:
-                    self.graph.replay()
-                    continue
-                for it in self._segments:
-                    if callable(it) and not isinstance(it, torch.cuda.CUDAGraph):
-                        it()
-                    else:
-                        it.replay()
+                kind, g = self._phases[self._phase]
+                if kind == "graph":
+                    g.replay()
+                else:
+                    for it in g:
+                        if callable(it) and not isinstance(it, torch.cuda.CUDAGraph):
+                            it()
+                        else:
+                            it.replay()
+                self._phase = (self._phase + self.ticks) % 2
         cur.wait_stream(self.stream)
         self.replays += n
         # host mirrors of the ring (2N rows per tick)

@@ -403,10 +403,30 @@ class FusedUpdate:
         return n
 
     def fit_check(self):
-        """raise if a resident fit launch lost an in-launch exchange (host sync)"""
+        """raise if a resident fit launch lost an in-launch exchange (host
+        sync).  The flag is cleared as it is reported, so the next pass starts
+        clean; the net that pass wrote is undefined."""
         t = getattr(self, "fit_timeout", None)
         if t is not None and int(t[0].item()):
+            t[0].zero_()
             raise SkillshotError("resident models_fit: an in-launch exchange timed out; the nets are undefined")
+
+    def fit_snapshot(self, critic):
+        """a copy of what one resident pass rewrites (the net, its Adam
+        moments and step counts; the critic's Dropout call number), so a pass
+        that fails can be restored and rerun on the three-launch steps"""
+        st = self.sc if critic else self.sa
+        f = self.fc if critic else self.fa
+        return (critic, f.clone(), st.m.clone(), st.v.clone(), st.steps.clone(), self.calls.clone())
+
+    def fit_restore(self, snap):
+        critic, f, m, v, steps, calls = snap
+        st = self.sc if critic else self.sa
+        (self.fc if critic else self.fa).copy_(f)
+        st.m.copy_(m)
+        st.v.copy_(v)
+        st.steps.copy_(steps)
+        self.calls.copy_(calls)
 
     @torch.no_grad()
     def critic_step_sampled(self, ring, batch, gamma=0.0, row_offset=0, global_batch=None, total=None, exclude=0,

@@ -332,7 +332,6 @@ class VecSkillshotGame:
             raise ValueError("acting_obs must hold [2, N, 12] floats, actions [2, N, 2] (contiguous)")
         ring_args = ((_ptr(ring.buf), ring.cap, _ptr(ring.total_t), _ptr(ring.arrivals()), _ptr(total_copy))
                      if ring is not None else (None, 0, None, None, None))
-        actor.calls += 1
         pack = actor.ensure_pack()
         args = (self._h, _ptr(actor.flat), _ptr(pack), _ptr(s), _ptr(act), float(noise_sd), float(action_sd), actor.seed,
                 _ptr(actor._ctr), _ptr(obs_t), _ptr(rew_t), REWARD_KINDS[reward], _ptr(done), _ptr(win),
@@ -356,8 +355,9 @@ class VecSkillshotGame:
         [T, 2, N], lengths int32 [N]); rows t < lengths[i] are game i's
         episode.  T = n_ticks (default: the tick limit); a game still live
         after T ticks continues in the next call (from states[T]).  The
-        device step counter and the actor's noise call number advance by
-        max(lengths), the ticks the per-tick loop would have run."""
+        device step counter and the actor's noise call number (actor.calls)
+        advance on device by max(lengths), the ticks the per-tick loop would
+        have run."""
         T = int(self.tick_limit if n_ticks is None else n_ticks)
         o = out or {}
         st = o.get("states")

@@ -612,3 +612,68 @@ def test_fit_actor_resident_equals_eager_and_keras(mods, monkeypatch, p, xcd):
     out = k(x)
     k2 = ActorKernel32(dr.model_actor, seed=3)
     assert torch.equal(out, k2(x))
+
+
+def test_fit_step_counts_saturate_like_the_chain(mods):
+    """Adam step counts past 2^24: the three-launch chain adds
+    1.0f per step, which stops changing the count at 2^24; the resident
+    launches store the same saturated count (and take their step sizes at
+    it).  From 2^24 - 8, 32 critic and 32 actor steps: counts equal (2^24),
+    nets within PARAM_ABS of the chain's"""
+    learner, _ = mods
+    n = 32
+    s, a, y = _fit_rows(16 * n, 21)
+    dr = _ddpg(learner, seed=9, scale=1.0)
+    de = _ddpg(learner, seed=9, scale=1.0)
+    t0 = float(2 ** 24 - 8)
+    for d in (dr, de):
+        d._fused.sc.steps.fill_(t0)
+        d._fused.sa.steps.fill_(t0)
+    fr, fe = dr._fused, de._fused
+    assert fr.fit_critic(s, a, y) == n
+    assert fr.fit_actor(s) == n
+    fr.fit_check()
+    for k in range(n):
+        sl = slice(16 * k, 16 * k + 16)
+        de.critic_step(s[sl], a[sl], y[sl])
+    for k in range(n):
+        de.model_actor_fit_step(s[16 * k:16 * k + 16])
+    torch.cuda.synchronize()
+    assert float(fe.sc.steps[0]) == float(fe.sa.steps[0]) == float(2 ** 24)
+    assert torch.equal(fr.sc.steps, fe.sc.steps) and torch.equal(fr.sa.steps, fe.sa.steps)
+    assert (fr.fc - fe.fc).abs().max().item() <= PARAM_ABS
+    assert (fr.fa - fe.fa).abs().max().item() <= PARAM_ABS
+
+
+def test_models_fit_resident_failure_falls_back(mods, monkeypatch):
+    """a resident pass that loses an in-launch exchange (its timeout flag set
+    after it ran) is restored and rerun on the three-launch steps, with the
+    flag cleared: the same nets, moments, counts and Dropout
+    call number, bit for bit, as a models_fit whose resident critic launch
+    is refused outright"""
+    learner, _ = mods
+    from skillshot_learning_amd._capi import SkillshotError
+    s, a, y = _fit_rows(16 * 40 + 5, 23)
+    out = []
+    for mode in ("lost_exchange", "refused"):
+        d = learner.DDPG("cuda", seed=12, fused_update=True, precision="fp32")
+        fu = d._fused
+        real = fu.fit_critic
+
+        def lost(*args, **kw):
+            n = real(*args, **kw)
+            fu.fit_timeout[0] = 1
+            return n
+
+        def refused(*args, **kw):
+            raise SkillshotError("refused")
+
+        monkeypatch.setattr(fu, "fit_critic", lost if mode == "lost_exchange" else refused)
+        with pytest.warns(UserWarning, match="three-launch"):
+            d.models_fit(s, a, y)
+        torch.cuda.synchronize()
+        assert int(fu.fit_timeout[0]) == 0 if mode == "lost_exchange" else True
+        out.append((fu.fc.clone(), fu.sc.m.clone(), fu.sc.v.clone(), fu.sc.steps.clone(), fu.fa.clone(),
+                    fu.sa.steps.clone(), int(d.drop_calls)))
+    for x, z in zip(*out):
+        assert (x == z) if isinstance(x, int) else torch.equal(x, z)

@@ -1,6 +1,6 @@
 """BASELINE configs 4 and 5 at their per-rank workloads on the GPU (VERDICT
-r04 item 1): two ranks share the one GPU of the test box over gloo, each rank
-a fresh process holding its config's share of games.
+r04 item 1, r05 item 4): two ranks share the one GPU of the test box over
+gloo, each rank a fresh process holding its config's share of games.
 
   config 4: 32,768 games over 8 GPUs = 4,096 per rank, multi_rank="grad"
             (each rank samples its own ring, gradient all-reduce), action
@@ -10,18 +10,24 @@ a fresh process holding its config's share of games.
             parameter noise, batch 256, fp32.
 
 Each rank runs the captured learner tick (reference order, "segmented"
-capture: graph segments with the gloo collectives issued between them) for
-20 ticks, then one fused update on a fixed global batch, this rank's share of
-it.  Asserted:
+capture: graph segments with the gloo collectives issued between them; one
+tick per graph, so the odd-count phase graphs run too) for 20 ticks,
+recording each tick's actions, then ONE update through the replay rule's own
+sampled path (DDPG.update_sampled: grad draws from this rank's ring inside
+the critic launch; shared draws, all-gathers and steps rows r::world), and
+returns the rows it drew.  Asserted:
   * the ranks' nets (online and target) are identical after the replays and
     after the update; their games differ;
-  * the sharded fused update equals the ONE-rank fused update on the
-    concatenated batch (rows in the order the ranks numbered them) from the
-    same starting state (nets, target nets, Adam moments and steps, Dropout
-    call number) within 1e-5 — the GPU analogue of
+  * each rank's shard after the 20 ticks equals a one-rank VecSkillshotGame
+    over the same global env ids (CPU backend, the same start state and the
+    recorded actions), bit for bit: the shards need no exchange;
+  * the sharded update equals the ONE-rank fused update on exactly the rows
+    the ranks drew, concatenated in the order the ranks numbered them, from
+    the same starting state (nets, target nets, Adam moments and steps,
+    Dropout call number) within 1e-5 — the GPU analogue of
     tests/test_learner_keras_cpu.py::test_two_ranks_equal_one_rank_on_concatenated_batch;
   * the same update against the fp64 Keras restatement (oracle/keras_ref.py)
-    on the gathered rows within 1e-5 (parity unpinned against Keras itself:
+    on those rows within 1e-5 (parity unpinned against Keras itself:
     TensorFlow is absent).
 Reference: SkillshotLearner.py:419-443 (the update), SkillshotGame.py:58-94
 (games are independent, so the shards need no exchange)."""
@@ -38,21 +44,13 @@ PARAM_ABS = 1e-5  # parameters after one Adam step (1 % of an lr-sized step)
 CFGS = {"config4": (4096, "grad", "action_noise"), "config5": (8192, "shared", "param_noise")}
 BATCH = 256
 NETS = ("fa", "fc", "ta", "tc")
+TICKS = 20
 
 
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
-
-
-def _fixed_batch(rows, seed, device):
-    """a deterministic global minibatch (states in the observation ranges)"""
-    g = torch.Generator().manual_seed(seed)
-    s = torch.rand(rows, 12, generator=g) * torch.tensor([1, 1, 1, 1, 9.8, 1, 1, 1, 1, 9.8, 1, 1.0])
-    out = (s, torch.rand(rows, 2, generator=g) * 2 - 1, torch.randn(rows, generator=g) * 0.3,
-           torch.rand(rows, 12, generator=g), (torch.rand(rows, generator=g) < 0.2).float())
-    return [t.to(device) for t in out]
 
 
 def _state(d):
@@ -73,23 +71,45 @@ def _worker(rank, world, port, cfg, q):
         L = SkillshotLearner(n_envs=n, device="cuda", seed=41, env_offset=rank * n, exploration=expl, gamma=0.9,
                              tau=0.05, replay_capacity=1 << 20, multi_rank=mode, precision="fp32")
         assert L.ddpg._fused is not None and L.ddpg._fused.f32
-        tg = L.tick_graph(batch=BATCH, ticks_per_graph=4, warmup=2)
+        tg = L.tick_graph(batch=BATCH, ticks_per_graph=1, warmup=2)
         assert tg.multi_rank_mode == f"{mode}/segmented" and tg.mode == "sequential"
-        tg.run(5)
+        g = L.game_environment
         torch.cuda.synchronize()
+        st0 = g.state_dict()
+        acts = []
+        for _ in range(TICKS):
+            tg.run(1)
+            acts.append(tg.act.detach().cpu().clone())
+        torch.cuda.synchronize()
+        st1 = g.state_dict()
         d = L.ddpg
         before = _state(d)
-        full = _fixed_batch(world * BATCH, 1234, "cuda")
-        d.update_batch(*[t[rank * BATCH:(rank + 1) * BATCH] for t in full])
+        d.update_sampled(BATCH)  # the replay rule's own draw (grad: own ring in-launch; shared: drawn + gathered)
         torch.cuda.synchronize()
+        rows = [t.detach().cpu().clone() for t in L.replay._batch_bufs(BATCH)]
         after = _state(d)
-        q.put((rank, before, after, L.game_environment.pos.cpu().numpy(), int(L.replay.total_t)))
+        q.put((rank, before, after, int(L.replay.total_t), rows, st0, st1, acts, g.tick_limit))
     except Exception:  # surface the failure to the parent
         import traceback
-        q.put((rank, None, traceback.format_exc(), None, 0))
+        q.put((rank, None, traceback.format_exc(), 0, None, None, None, None, 0))
         raise
     finally:
         dist.destroy_process_group()
+
+
+def _shard_replay(rank, n, st0, acts, tick_limit):
+    """the shard's games on their own: a one-rank VecSkillshotGame over global
+    env ids rank*n .. rank*n + n - 1 (CPU backend), from the shard's start
+    state, stepped with the recorded actions (auto-reset, random starts)"""
+    from skillshot_learning_amd.vec_env import VecSkillshotGame
+    env = VecSkillshotGame(n, device="cpu", seed=41, env_offset=rank * n, tick_limit=tick_limit,
+                           random_positions=True)
+    env.load_state_dict(st0)
+    for a in acts:
+        env.step(a, obs=False, auto_reset=True)
+    out = env.state_dict()
+    env.close()
+    return out
 
 
 def _one_rank_update(state, rows):
@@ -161,24 +181,32 @@ def test_config_per_rank_workload_two_ranks(cfg):
         p.start()
     out = {}
     for _ in range(world):
-        rank, before, after, pos, total = q.get(timeout=600)
+        rank, before, after, total, rows, st0, st1, acts, lim = q.get(timeout=600)
         assert before is not None, after
-        out[rank] = (before, after, pos, total)
+        out[rank] = (before, after, total, rows, st0, st1, acts, lim)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    (b0, a0, p0, t0), (b1, a1, p1, t1) = out[0], out[1]
+    b0, a0, t0 = out[0][:3]
+    b1, a1, t1 = out[1][:3]
     n, mode, _ = CFGS[cfg]
     # identical nets (and Adam state) on both ranks after the replays and after the update
     for k in b0:
         assert np.array_equal(b0[k], b1[k]), ("before", k)
         assert np.array_equal(a0[k], a1[k]), ("after", k)
     assert np.isfinite(a0["fa"]).all() and np.isfinite(a0["fc"]).all()
-    assert not np.array_equal(p0, p1)  # different games on the two shards
-    assert p0.shape[0] == n and t0 == t1 > 0
+    assert t0 == t1 > 0
+    assert not np.array_equal(out[0][5]["pos"], out[1][5]["pos"])  # different games on the two shards
     assert int(a0["calls"][0]) == int(b0["calls"][0]) + 1  # one critic step's Dropout call
-    # the one-rank update on the concatenated batch from the same state
-    full = _fixed_batch(world * BATCH, 1234, "cuda")
+    # each shard equals its games run alone over the same global env ids
+    for r in range(world):
+        _, _, _, _, st0, st1, acts, lim = out[r]
+        assert st1["pos"].shape[0] == n and len(acts) == TICKS
+        want = _shard_replay(r, n, st0, acts, lim)
+        for k in want:
+            assert np.array_equal(np.asarray(want[k]), np.asarray(st1[k])), (cfg, r, k)
+    # the one-rank update on exactly the rows the ranks drew (rank order)
+    full = [torch.cat([out[r][3][j] for r in range(world)]).to("cuda") for j in range(5)]
     if mode == "shared":  # rank r stepped rows r::world of the gathered batch
         full = [torch.cat([t[r::world] for r in range(world)]) for t in full]
     d1, want = _one_rank_update(b0, full)
@@ -186,7 +214,7 @@ def test_config_per_rank_workload_two_ranks(cfg):
         err = np.abs(a0[k] - want[k]).max()
         assert err <= PARAM_ABS, (cfg, k, err)
         assert not np.array_equal(a0[k], b0[k]), (cfg, k)  # the update moved every net
-    # and against the fp64 Keras restatement on the gathered rows
+    # and against the fp64 Keras restatement on those rows
     ref = _keras_update(d1, b0, full)
     for k in NETS:
         err = np.abs(a0[k] - ref[k]).max()

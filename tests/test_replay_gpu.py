@@ -427,3 +427,32 @@ def test_sampled_rows_equal_restated_ring_row(learner, exclude):
             idx = (count - el + ((u53 * el) >> 53)) % cap
         want.append(idx + cap * ((count - 1 - idx) // cap))  # the id the ring row holds (latest write)
     assert got.tolist() == want
+
+
+@pytest.mark.parametrize("overlap", [None, "fused"])
+def test_tick_graph_odd_ticks_per_graph(learner, overlap):
+    """ticks_per_graph need not be even: an odd count is
+    two graphs replayed alternately.  Six ticks as 3 + 3 (two run() calls,
+    the second starting in the other phase), as 1 x 6 and as 2 x 3 end in the
+    same nets, ring, game state and next observation, bit for bit"""
+    out = []
+    for tpg, runs in ((3, (1, 1)), (1, (6,)), (2, (3,))):
+        L = learner.SkillshotLearner(n_envs=256, device="cuda", seed=7, exploration="action_noise", gamma=0.9,
+                                     tau=0.05, replay_capacity=4096, precision="fp32")
+        tg = L.tick_graph(batch=128, ticks_per_graph=tpg, warmup=2, overlap=overlap)
+        for r in runs:
+            tg.run(r)
+        torch.cuda.synchronize()
+        st = L.game_environment.state_dict()
+        out.append((torch.cat([p.detach().flatten() for p in L.model_actor.parameters()]),
+                    torch.cat([p.detach().flatten() for p in L.model_critic.parameters()]),
+                    L.replay.buf.clone(), int(L.replay.total_t), tg.obs.clone(),
+                    {k: v for k, v in st.items() if k != "step_counter"}, tg.mode))
+    a0, c0, b0, t0, o0, s0, m0 = out[0]
+    for a, c, b, t, o, s, m in out[1:]:
+        assert m == m0
+        assert t == t0 and torch.equal(b, b0)
+        assert torch.equal(a, a0) and torch.equal(c, c0)
+        assert torch.equal(o, o0)
+        for k in s0:
+            assert (s[k] == s0[k]).all(), k

@@ -9,6 +9,7 @@ grad, actor Adam, and the whole update.  One JSON line per (precision, batch).
 --slices sets SK_SLICE32 per pass (fp32: -1 automatic, 0 one-launch
 gradient kernels, 1 the sliced two-launch schedule at every batch)."""
 import argparse
+import copy
 import json
 import os
 import sys
@@ -48,6 +49,7 @@ def main():
     p.add_argument("--k", type=int, default=20)
     p.add_argument("--precisions", default="fp32,bf16")
     p.add_argument("--slices", default="-1")
+    p.add_argument("--w1-ablation", action="store_true")
     a = p.parse_args()
     for prec, sl, B in [(p_, s_, int(b)) for p_ in a.precisions.split(",") for s_ in a.slices.split(",")
                         for b in a.batches.split(",")]:
@@ -76,6 +78,14 @@ def main():
             out["critic_adam"] = timed(lambda: fu._adam(pc, fu.fc, fu.sc, fu.tc, stat=fu.stats[0:1], scale=1.0 / B,
                                                         out=fu.loss_hist[0, 0], counter=fu.calls,
                                                         packs=fu._packs(critic=True)), st, a.k)
+            if a.w1_ablation and pc.scratch is not None:
+                # timing ablation (wrong gradients): the critic's Adam launch
+                # summing 1/8 of the W1 / b1 contribution rows
+                pc8 = copy.copy(pc)
+                pc8.w1_rows = max(1, pc.w1_rows // 8)
+                out["critic_adam_w1_rows_div8"] = timed(
+                    lambda: fu._adam(pc8, fu.fc, fu.sc, fu.tc, stat=fu.stats[0:1], scale=1.0 / B,
+                                     out=fu.loss_hist[0, 0], counter=fu.calls, packs=fu._packs(critic=True)), st, a.k)
             out["actor_grad"] = timed(lambda: fu._actor_grad(bs, pa, fu.sa.steps, fu.stats[1:]), st, a.k)
             out["actor_adam"] = timed(lambda: fu._adam(pa, fu.fa, fu.sa, fu.ta, stat=fu.stats[1:], scale=-1.0,
                                                        out=fu.loss_hist[1, 0], packs=fu._packs(critic=False)),

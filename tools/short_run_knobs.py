@@ -33,6 +33,10 @@ SETTINGS = {
     # workgroups to dispatch) and the restart draw under the loads
     "block_256": {"SK_MULTI_BLOCK": "256"},
     "early_draw": {"SK_MULTI_EARLY": "1"},
+    # round 6: two lanes per game and the packed resident form at the K = 20 launch
+    "split_geometry": {"SK_MULTI_SPLIT": "1"},
+    "packed_form": {"SK_MULTI_PACK": "1"},
+    "split_prefetch1": {"SK_MULTI_SPLIT": "1", "SK_MULTI_PREFETCH": "1"},
 }
 
 
