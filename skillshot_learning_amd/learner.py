@@ -1295,6 +1295,11 @@ class TickGraph:
         # replays cannot leave the captured slot stale
         g.sync_step_counter(ctypes.c_void_p(self.stream.cuda_stream))
         mirror = L.replay.total  # capture records the inserts without running them
+        # Every captured tick samples with the same draw numbers (draw0 + u for
+        # its u-th update): the ring count in the sample's key already differs
+        # per tick, and a host counter advanced during capture would bake
+        # numbers that depend on where the ticks are cut into graphs
+        self._draw0 = L.replay._draws
         # Every tick flips three two-slot alternations (the engine's step
         # counter slot, the acting observation buffer, the overlapped tick's
         # horizon), so a graph of an odd number of ticks ends in the other
@@ -1325,6 +1330,7 @@ class TickGraph:
         self._phase = 0  # which graph the next replay runs (the slot the current tick starts in)
         self.stream.synchronize()
         L.replay.total = mirror
+        L.replay._draws = (self._draw0 + self.updates) & 0x7FFFFFFF
         self.replays = 0
 
     def _capture_segments(self):
@@ -1438,6 +1444,8 @@ class TickGraph:
 
     def _tick(self, update):
         L = self.L
+        if getattr(self, "_draw0", None) is not None:  # a captured tick (see __init__)
+            L.replay._draws = self._draw0
         if update and self.fuse_act:
             return self._tick_fused()
         if update and self.overlap:

@@ -79,14 +79,16 @@ def _worker(rank, world, port, cfg, q):
         acts = []
         for _ in range(TICKS):
             tg.run(1)
-            acts.append(tg.act.detach().cpu().clone())
+            acts.append(tg.act.detach().cpu().numpy().copy())
         torch.cuda.synchronize()
         st1 = g.state_dict()
         d = L.ddpg
         before = _state(d)
         d.update_sampled(BATCH)  # the replay rule's own draw (grad: own ring in-launch; shared: drawn + gathered)
         torch.cuda.synchronize()
-        rows = [t.detach().cpu().clone() for t in L.replay._batch_bufs(BATCH)]
+        # numpy, not tensors: a CPU tensor crosses the queue as a shared-memory fd
+        # that dies with this process, which may exit before the parent reads it
+        rows = [t.detach().cpu().numpy().copy() for t in L.replay._batch_bufs(BATCH)]
         after = _state(d)
         q.put((rank, before, after, int(L.replay.total_t), rows, st0, st1, acts, g.tick_limit))
     except Exception:  # surface the failure to the parent
@@ -106,7 +108,7 @@ def _shard_replay(rank, n, st0, acts, tick_limit):
                            random_positions=True)
     env.load_state_dict(st0)
     for a in acts:
-        env.step(a, obs=False, auto_reset=True)
+        env.step(torch.from_numpy(a), obs=False, auto_reset=True)
     out = env.state_dict()
     env.close()
     return out
@@ -180,13 +182,19 @@ def test_config_per_rank_workload_two_ranks(cfg):
     for p in procs:
         p.start()
     out = {}
-    for _ in range(world):
-        rank, before, after, total, rows, st0, st1, acts, lim = q.get(timeout=600)
-        assert before is not None, after
-        out[rank] = (before, after, total, rows, st0, st1, acts, lim)
-    for p in procs:
-        p.join(timeout=120)
-        assert p.exitcode == 0
+    try:
+        for _ in range(world):
+            rank, before, after, total, rows, st0, st1, acts, lim = q.get(timeout=600)
+            assert before is not None, after
+            out[rank] = (before, after, total, rows, st0, st1, acts, lim)
+        for p in procs:
+            p.join(timeout=120)
+            assert p.exitcode == 0
+    finally:  # never leave a rank behind (the interpreter would wait for it at exit)
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+                p.join(timeout=30)
     b0, a0, t0 = out[0][:3]
     b1, a1, t1 = out[1][:3]
     n, mode, _ = CFGS[cfg]
@@ -206,7 +214,7 @@ def test_config_per_rank_workload_two_ranks(cfg):
         for k in want:
             assert np.array_equal(np.asarray(want[k]), np.asarray(st1[k])), (cfg, r, k)
     # the one-rank update on exactly the rows the ranks drew (rank order)
-    full = [torch.cat([out[r][3][j] for r in range(world)]).to("cuda") for j in range(5)]
+    full = [torch.cat([torch.from_numpy(out[r][3][j]) for r in range(world)]).to("cuda") for j in range(5)]
     if mode == "shared":  # rank r stepped rows r::world of the gathered batch
         full = [torch.cat([t[r::world] for r in range(world)]) for t in full]
     d1, want = _one_rank_update(b0, full)
