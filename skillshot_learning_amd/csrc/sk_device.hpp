@@ -622,6 +622,11 @@ __device__ __forceinline__ void tick_env_fast(const Cfg& c, Env& e, float a0_mov
 // for |rot| < 1.6e6).  A wave with any such lane, or with |rot| past that
 // range, or a NaN action, evaluates the fired projectiles' sincos exactly
 // (~1e-5 of waves).  Bit for bit tick_env_m's result.
+// SK_CARRY_BRANCHFREE = 0 (A/B builds): tick_env_carry's commits as the
+// per-method helpers' branches
+#ifndef SK_CARRY_BRANCHFREE
+#define SK_CARRY_BRANCHFREE 1
+#endif
 struct TrigCarry {
   double kr[2], kq[2];          // keys: m[p] = sincos(kr[p]), tq[p] = sincos(kq[p])
   sktrig::SinCos m[2], tq[2];
@@ -708,6 +713,63 @@ __device__ __forceinline__ void tick_env_carry(const Cfg& c, Env& e, TrigCarry& 
     if (f1) t1 = x1;
     fast0 = fast1 = false;
   }
+#if SK_CARRY_BRANCHFREE
+  // The rest as selects, no branch: both players' chains (and both
+  // projectiles') are independent, and with one wave per SIMD the tick is a
+  // latency chain, so they must interleave; exec-mask branches around each
+  // player's shoot / projectile / hit test had serialised them (per-phase
+  // stamps, -DSK_TRACE_MULTI_WAIT: tools/trace_multi.py --wait).  Every value
+  // is the branchy form's expression; only the commits are selects.
+  const sktrig::SinCos mm[2] = {t.m[0], t.m[1]};
+  const float am[2] = {a0_move, a1_move};
+  const double rn[2] = {rn0, rn1};
+  const bool fired[2] = {f0, f1};
+  const double psp = (double)c.pspeed;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {  // do_actions(p + 1, ...)  SkillshotLearner.py:206-213
+    const double speed = clamp_action((double)am[p]);  // Player.move_direction_float, Player.py:57-68
+    const double nxf = __builtin_rint((double)e.px[p] - (mm[p].s * psp) * speed);
+    const double nyf = __builtin_rint((double)e.py[p] - (mm[p].c * psp) * speed);
+    const bool ok = (nxf >= 0.0) & (nxf + (double)c.psize <= (double)c.W) & (nyf >= 0.0) &
+                    (nyf + (double)c.psize <= (double)c.H);
+    e.px[p] = ok ? (int)(ok ? nxf : 0.0) : e.px[p];
+    e.py[p] = ok ? (int)(ok ? nyf : 0.0) : e.py[p];
+    e.rot[p] = rn[p];  // Player.move_look_float, Player.py:33-39
+    // Player.move_shoot_projectile, Player.py:78-89
+    e.qx[p] = fired[p] ? e.px[p] : e.qx[p];
+    e.qy[p] = fired[p] ? e.py[p] : e.qy[p];
+    e.qrot[p] = fired[p] ? e.rot[p] : e.qrot[p];
+    e.qvalid[p] = fired[p] ? 1 : e.qvalid[p];
+    e.qcd[p] = fired[p] ? c.cdmax : e.qcd[p];
+    e.qage[p] = fired[p] ? 0 : e.qage[p];
+  }
+  // game_tick  SkillshotGame.py:115-122 (Projectile.py:38-53), if live
+  const int live = e.live != 0;
+  e.ticks += live;
+  const sktrig::SinCos tt[2] = {t0, t1};
+  const bool fast[2] = {fast0, fast1};
+  const float exy[2][2] = {{ex0, ey0}, {ex1, ey1}};
+  const double qsp = (double)c.qspeed;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int nxF = e.qx[p] - (int)rintf(exy[p][0]), nyF = e.qy[p] - (int)rintf(exy[p][1]);
+    const int nxE = (int)__builtin_rint((double)e.qx[p] - tt[p].s * qsp);
+    const int nyE = (int)__builtin_rint((double)e.qy[p] - tt[p].c * qsp);
+    const int nx = fast[p] ? nxF : nxE, ny = fast[p] ? nyF : nyE;
+    const bool ok = (nx + c.qsize <= c.W) & (nx >= 0) & (ny + c.qsize <= c.H) & (ny >= 0);
+    const bool upd = live && e.qvalid[p];
+    e.qx[p] = (upd && ok) ? nx : e.qx[p];
+    e.qy[p] = (upd && ok) ? ny : e.qy[p];
+    e.qvalid[p] = (upd && !ok) ? 0 : e.qvalid[p];
+    e.qcd[p] -= live;
+    e.qage[p] += live;
+  }
+  // SkillshotGame.check_collision (:58-94): player 1 tested first
+  const bool h1 = live && hit_test_s(c, e.px[0], e.py[0], e.qx[1], e.qy[1], e.qvalid[1]);
+  const bool h2 = live && !h1 && hit_test_s(c, e.px[1], e.py[1], e.qx[0], e.qy[0], e.qvalid[0]);
+  e.winner = h1 ? 1 : (h2 ? 2 : e.winner);
+  e.live = (h1 || h2) ? 0 : e.live;
+#else
   // do_actions(1, ...), do_actions(2, ...)  SkillshotLearner.py:206-213
   move_direction_sc(c, e.px[0], e.py[0], t.m[0], (double)a0_move);
   e.rot[0] = rn0;
@@ -736,6 +798,7 @@ __device__ __forceinline__ void tick_env_carry(const Cfg& c, Env& e, TrigCarry& 
     collide_s(c, e.px[0], e.py[0], e.qx[0], e.qy[0], e.qvalid[0], e.px[1], e.py[1], e.qx[1], e.qy[1],
               e.qvalid[1], e.live, e.winner);
   }
+#endif
 }
 
 // ---------------------------------------------------------------- features

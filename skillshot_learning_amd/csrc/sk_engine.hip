@@ -28,6 +28,21 @@
 
 using namespace sk;
 
+// k_step_multi's action slabs are loaded SK_ACT_AHEAD ticks before their
+// tick, into registers, after that earlier tick's state loads (0: with the
+// tick's own state loads).  The 400-slab ring is larger than the Infinity
+// Cache, so a slab comes from HBM, later than the state from the fabric; a
+// tick's loads are consumed in issue order (vmcnt), so its wait was the
+// slab's HBM latency (65,536 games, 20-tick launches: 2.55 us per tick with
+// the HBM ring against 2.04 with an 8-slab ring held in cache;
+// profiles/r06f_multi_pack_pf_ring_sweep.jsonl).  Issued one tick ahead, the
+// slab's loads are older than the state loads its tick waits for by a whole
+// tick; more ticks ahead gain nothing, since tick t + 1 waits (in issue order)
+// for every load tick t issued.
+#ifndef SK_ACT_AHEAD
+#define SK_ACT_AHEAD 1
+#endif
+
 // k_step_multi carries each tick's sincos to the next (tick_env_carry); 0:
 // every tick evaluates its four (A/B: tools/build_variant.sh -DSK_MULTI_CARRY=0)
 #ifndef SK_MULTI_CARRY
@@ -647,7 +662,7 @@ struct MultiRaw {  // one tick's loads as issued, decoded at the tick's start
   float2 act[2];    // both players' actions
 };
 
-template <int POL, bool PACK>
+template <int POL, bool PACK, bool ACT = true>
 __device__ __forceinline__ void multi_load(const MultiArgs& a, __amdgpu_buffer_rsrc_t r, __amdgpu_buffer_rsrc_t rp,
                                            const MultiLane& L, int64_t slab, bool packed, MultiRaw& w) {
   const uint32_t o16 = (uint32_t)L.ic * 16u, o8 = (uint32_t)L.ic * 8u;
@@ -676,9 +691,11 @@ __device__ __forceinline__ void multi_load(const MultiArgs& a, __amdgpu_buffer_r
     w.m = __builtin_amdgcn_raw_buffer_load_b64(r, o8 + a.off[5], 0, 16);
   }
   __builtin_amdgcn_sched_barrier(0);
-  w.act[0] = load_action(a.actions + slab * 2 * a.n + L.ic);
-  w.act[1] = load_action(a.actions + slab * 2 * a.n + a.n + L.ic);
-  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (ACT) {
+    w.act[0] = load_action(a.actions + slab * 2 * a.n + L.ic);
+    w.act[1] = load_action(a.actions + slab * 2 * a.n + a.n + L.ic);
+    __builtin_amdgcn_sched_barrier(0);
+  }
 }
 
 template <bool PACK>
@@ -714,6 +731,43 @@ __device__ __forceinline__ uint64_t multi_step(uint64_t step0, int tick) {
   return step0 + (uint64_t)tick;
 }
 
+// Measurement build only (-DSK_TRACE_MULTI; tools/trace_multi.py): lane 0 of
+// every k_step_multi wave records s_memrealtime (100 MHz) at entry, after
+// each of the first 29 ticks and at exit into sk_multi_trace[wave][32], and
+// its hardware slot (HW_ID, XCC_ID) in word 30 (vector stores).
+#if defined(SK_TRACE_MULTI_WAIT) && !defined(SK_TRACE_MULTI)
+#define SK_TRACE_MULTI
+#endif
+#ifdef SK_TRACE_MULTI
+__device__ unsigned long long* sk_multi_trace;
+extern "C" int skdiag_set_multi_trace(void* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(sk_multi_trace), &buf, sizeof(buf)) == hipSuccess ? 0 : -1;
+}
+#define SK_MTS(k)                                                                                   \
+  do {                                                                                              \
+    if ((threadIdx.x & 63) == 0)                                                                    \
+      sk_multi_trace[((size_t)blockIdx.x * (blockDim.x == 128 ? 1 : blockDim.x / 64) + (threadIdx.x >> 6)) * 32 + (k)] = \
+          __builtin_amdgcn_s_memrealtime();                                                         \
+  } while (0)
+#else
+#define SK_MTS(k) \
+  do {            \
+  } while (0)
+#endif
+
+// SK_TRACE_MULTI_WAIT: ticks 0..4, five stamps each (loads issued, loads
+// arrived, tick_env done, done / reset done, state stored)
+#ifdef SK_TRACE_MULTI_WAIT
+#define SK_MTW(tick, k) \
+  do {                  \
+    if ((tick) < 5) SK_MTS(1 + 5 * (tick) + (k)); \
+  } while (0)
+#else
+#define SK_MTW(tick, k) \
+  do {                  \
+  } while (0)
+#endif
+
 // the rest of the tick on the loaded state; `last`: the launch's final tick
 template <int POL, bool PACK>
 __device__ __forceinline__ void multi_compute(const MultiArgs& a, const Cfg& c, __amdgpu_buffer_rsrc_t r,
@@ -744,6 +798,7 @@ __device__ __forceinline__ void multi_compute(const MultiArgs& a, const Cfg& c, 
   const sktrig::SinCos m1 = sktrig::sincos_bf(e.rot[1], &k1);
   tick_env_m(c, e, m0, m1, k0 & k1, (double)acts[0].x, (double)acts[0].y, (double)acts[1].x, (double)acts[1].y);
 #endif
+  SK_MTW(tick, 2);
   // every load of this tick consumed (the counter slot's, issued first, with
   // them): without this the waitcnt pass, its tracking lost across the loop,
   // drains every store before the final counter store
@@ -768,6 +823,7 @@ __device__ __forceinline__ void multi_compute(const MultiArgs& a, const Cfg& c, 
 #if SK_MULTI_CARRY
   if (!last) carry_note(tc, e);
 #endif
+  SK_MTW(tick, 3);
   bool to_pack = false;
   if constexpr (PACK) {
     const bool fit =
@@ -788,26 +844,6 @@ __device__ __forceinline__ void multi_compute(const MultiArgs& a, const Cfg& c, 
   packed = to_pack;
 }
 
-// Measurement build only (-DSK_TRACE_MULTI; tools/trace_multi.py): lane 0 of
-// every k_step_multi wave records s_memrealtime (100 MHz) at entry, after
-// each of the first 29 ticks and at exit into sk_multi_trace[wave][32], and
-// its hardware slot (HW_ID, XCC_ID) in word 30 (vector stores).
-#ifdef SK_TRACE_MULTI
-__device__ unsigned long long* sk_multi_trace;
-extern "C" int skdiag_set_multi_trace(void* buf) {
-  return hipMemcpyToSymbol(HIP_SYMBOL(sk_multi_trace), &buf, sizeof(buf)) == hipSuccess ? 0 : -1;
-}
-#define SK_MTS(k)                                                                                   \
-  do {                                                                                              \
-    if ((threadIdx.x & 63) == 0)                                                                    \
-      sk_multi_trace[((size_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * 32 + (k)] =    \
-          __builtin_amdgcn_s_memrealtime();                                                         \
-  } while (0)
-#else
-#define SK_MTS(k) \
-  do {            \
-  } while (0)
-#endif
 
 // PF > 0: one more wave per workgroup pulls the action slab PF ticks ahead
 // into the CU's L1 / the XCD's L2 (global -> LDS copies into a scratch line
@@ -852,19 +888,78 @@ __device__ __forceinline__ void prefetch_wave(const MultiArgs& a, int4* scratch)
   __builtin_amdgcn_s_waitcnt(0);  // no LDS write outlives the workgroup
 }
 
+// k_step_multi's feed wave (PF > 0; round 6): the action slabs come to the
+// stepping wave through LDS, not through its own vector-memory queue.  A
+// tick's loads are consumed in issue order (vmcnt), so a tick that loads its
+// slab waits for the slowest of its loads, the slab from HBM (the 400-slab
+// ring is larger than the Infinity Cache), and any slab load issued earlier
+// by the same wave is waited for by the next tick's state wait anyway.  A
+// second wave of the workgroup copies the slab of tick t + PF into LDS slot
+// (t + PF) % (PF + 1) (global -> LDS DMA, 16 B per lane: the workgroup's 64
+// games of both planes in one wave-instruction), waits for the copy of tick
+// t + 1 and meets the stepping wave at barrier t + 1; the stepping wave reads
+// its two float2 from slot t % (PF + 1) after barrier t.  The slot a copy
+// overwrites was read at tick t - 1, before the stepping wave reached barrier
+// t.  Needs n % 64 == 0 (whole 16-byte pairs; the host checks).  The state's
+// round trip is untouched: only the slab's HBM latency leaves the chain.
+struct FeedSlot {
+  float2 act[2][64];  // [plane][game of the workgroup]
+};
+
+__device__ __forceinline__ void feed_slab(const MultiArgs& a, int64_t slab, FeedSlot* dst) {
+  const int lane = threadIdx.x & 63, pl = lane >> 5;
+  const int64_t g = (int64_t)blockIdx.x * 64 + 2 * (lane & 31);
+  __builtin_amdgcn_global_load_lds((void*)(a.actions + (slab * 2 + pl) * a.n + g), (void*)dst, 16, 0, 0);
+}
+
+// wait until at most n (0..3) of this wave's vector-memory operations are outstanding
+__device__ __forceinline__ void wait_vm_upto(int n) {
+  if (n >= 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if (n == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if (n == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int PF>
+__device__ __forceinline__ void feed_wave(const MultiArgs& a, FeedSlot* slots) {
+  static_assert(PF >= 1 && PF <= 4, "vmcnt immediates cover PF <= 4");
+  constexpr int S = PF + 1;
+  int64_t s = a.slab0;  // the next slab to copy
+#pragma unroll
+  for (int k = 0; k < PF; ++k) {  // ticks 0 .. PF - 1
+    if (k < a.n_ticks) {
+      feed_slab(a, s, slots + k);
+      s = s + 1 == a.ring ? 0 : s + 1;
+    }
+  }
+  int put = PF;  // slot of tick t + PF
+  for (int t = 0; t < a.n_ticks; ++t) {
+    // tick t's copy done: the copies issued after it (ticks t + 1 .. t + PF - 1) may fly
+    const int younger = min(PF - 1, a.n_ticks - 1 - t);
+    wait_vm_upto(younger);
+    asm volatile("s_barrier" ::: "memory");  // barrier t: the stepping wave reads slot t % S
+    if (t + PF < a.n_ticks) {
+      feed_slab(a, s, slots + put);
+      s = s + 1 == a.ring ? 0 : s + 1;
+    }
+    put = put + 1 == S ? 0 : put + 1;
+  }
+}
+
 template <int POL, bool PACK, int BLK, int PF = 0>
 __global__ void __launch_bounds__(BLK + (PF > 0 ? 64 : 0)) k_step_multi(MultiArgs a, Cfg c, int early) {
+  static_assert(PF == 0 || BLK == 64, "the feed wave serves one 64-game wave");
+  __shared__ FeedSlot feed[PF > 0 ? PF + 1 : 1];
   if constexpr (PF > 0) {
-    __shared__ int4 pf_scratch[64];
-    if (threadIdx.x >= BLK) {  // the prefetch wave: n_ticks barriers, like the stepping waves
-      prefetch_wave<BLK, PF>(a, pf_scratch);
+    if (threadIdx.x >= BLK) {  // the feed wave: n_ticks barriers, like the stepping wave
+      feed_wave<PF>(a, feed);
       return;
     }
   }
   SK_MTS(0);
 #ifdef SK_TRACE_MULTI  // slot 30: where the wave runs (HW_ID | XCC_ID << 32)
   if ((threadIdx.x & 63) == 0)
-    sk_multi_trace[((size_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * 32 + 30] =
+    sk_multi_trace[((size_t)blockIdx.x * (blockDim.x == 128 ? 1 : blockDim.x / 64) + (threadIdx.x >> 6)) * 32 + 30] =
         (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
         ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32);
 #endif
@@ -890,20 +985,65 @@ __global__ void __launch_bounds__(BLK + (PF > 0 ? 64 : 0)) k_step_multi(MultiArg
   int t = 0;
   TrigCarry tc;
   tc.have = tc.pend = false;
-  do {  // n_ticks >= 1 (host-checked): every path to the counter store passes ctr_settle
+  // the action pipeline (SK_ACT_AHEAD): tick t reads the slab from one
+  // register pair while the next tick's slab loads into the other; the loop
+  // runs two ticks per iteration so the pairs alternate without a copy (a
+  // copy of the pair just loaded waits for that load)
+  constexpr bool AHEAD = PF == 0 && SK_ACT_AHEAD != 0;
+  float2 pa0[2], pa1[2];
+  if constexpr (AHEAD) {
+    pa0[0] = load_action(a.actions + slab * 2 * a.n + L.ic);
+    pa0[1] = load_action(a.actions + slab * 2 * a.n + a.n + L.ic);
+  }
+  int64_t pslab = slab + 1 == a.ring ? 0 : slab + 1;  // the slab of tick t + 1
+  int take = 0;  // the feed slot of tick t
+  auto one_tick = [&](float2 (&cur)[2], float2 (&nxt)[2]) {
     MultiRaw w;
-    if constexpr (PF > 0) __builtin_amdgcn_s_barrier();
-    multi_load<POL, PACK>(a, r, rp, L, slab, packed, w);
+    if constexpr (PF > 0) asm volatile("s_barrier" ::: "memory");  // barrier t (feed_wave)
+    multi_load<POL, PACK, !AHEAD && PF == 0>(a, r, rp, L, slab, packed, w);
+    if constexpr (PF > 0) {  // the slab from LDS (feed_wave)
+      const int gl = threadIdx.x & 63;
+      w.act[0] = feed[take].act[0][gl];
+      w.act[1] = feed[take].act[1][gl];
+      take = take == PF ? 0 : take + 1;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (AHEAD) {
+      // after this tick's state loads, unconditionally (a load under a
+      // branch made the waitcnt pass drain every load before the compute);
+      // past the launch's last tick it re-reads this tick's slab
+      const int64_t ls = t + 1 < a.n_ticks ? pslab : slab;
+      nxt[0] = load_action(a.actions + ls * 2 * a.n + L.ic);
+      nxt[1] = load_action(a.actions + ls * 2 * a.n + a.n + L.ic);
+      w.act[0] = cur[0];
+      w.act[1] = cur[1];
+      __builtin_amdgcn_sched_barrier(0);
+    }
 #if SK_MULTI_CARRY
     if (tc.pend) carry_advance(tc);  // the last tick's rotations, while this tick's loads fly
     __builtin_amdgcn_sched_barrier(0);
 #endif
+#ifdef SK_TRACE_MULTI_WAIT
+    if (t < 5) {
+      SK_MTW(t, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      SK_MTW(t, 1);
+    }
+#endif
     multi_compute<POL, PACK>(a, c, r, rp, L, wc, so, step0, t, w, packed, t + 1 == a.n_ticks, tc);
-#ifdef SK_TRACE_MULTI
+#if defined(SK_TRACE_MULTI_WAIT)
+    SK_MTW(t, 4);
+#elif defined(SK_TRACE_MULTI)
     if (t < 29) SK_MTS(1 + t);
 #endif
     slab = slab + 1 == a.ring ? 0 : slab + 1;
+    pslab = pslab + 1 == a.ring ? 0 : pslab + 1;
     so = so + 1 == a.out_slabs ? 0 : so + 1;
+  };
+  do {  // n_ticks >= 1 (host-checked): every path to the counter store passes ctr_settle
+    one_tick(pa0, pa1);
+    if (++t >= a.n_ticks) break;
+    one_tick(pa1, pa0);
   } while (++t < a.n_ticks);
   if (a.ctr) {
     const unsigned c4[4] = {L.n_done, L.n_h1, L.n_h2, L.t_sum};
@@ -2115,7 +2255,7 @@ static int step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64
       // 2.36 vs 2.33-2.39 us per tick at PF 1-4 and slower at 20 ticks per
       // launch, where actions held in cache (an 8-slab ring) give 2.0
       // (profiles/r04aq_prefetch_sweep.jsonl, r04at_prefetch_ring_sweep.jsonl)
-      else if (pol == 1 && e->multi_prefetch > 0 && n_ticks > 1)
+      else if (pol == 1 && e->multi_prefetch > 0 && n_ticks > 1 && e->n % 64 == 0)
         err = e->multi_prefetch == 1
                   ? launch_timed(k_step_multi<1, false, kStepBlock, 1>, g, dim3(kStepBlock + 64), hs, e0, e1, a,
                                  e->dcfg, early)

@@ -18,8 +18,10 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 
-def multi_rate(n, T, pol, split=-1, stagger=0, block=-1, fast=0, early=-1, K=2000, ring=400, seed=0, prefetch=0):
+def multi_rate(n, T, pol, split=-1, stagger=0, block=-1, fast=0, early=-1, K=2000, ring=400, seed=0, prefetch=0,
+               pack=-1):
     os.environ["SK_MULTI_PREFETCH"] = str(prefetch)
+    os.environ["SK_MULTI_PACK"] = str(pack)
     os.environ["SK_MULTI_FAST"] = str(fast)
     os.environ["SK_MULTI_EARLY"] = str(early)
     os.environ["SK_MULTI_BLOCK"] = str(block)
@@ -55,7 +57,7 @@ def multi_rate(n, T, pol, split=-1, stagger=0, block=-1, fast=0, early=-1, K=200
     st.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / (launches * T)
     env.close()
-    return dict(kind="multi", envs=n, ring=ring, prefetch=prefetch, ticks_per_launch=T, policy=pol, split=split, stagger=stagger, block=block, fast=fast, early=early, us_per_tick=us,
+    return dict(kind="multi", envs=n, ring=ring, prefetch=prefetch, pack=pack, ticks_per_launch=T, policy=pol, split=split, stagger=stagger, block=block, fast=fast, early=early, us_per_tick=us,
                 env_steps_per_s=n / (us * 1e-6), frac=193 * n / (us * 1e-6) / 8e12)
 
 
@@ -80,6 +82,7 @@ def main():
     p.add_argument("--earlys", default="-1")
     p.add_argument("--rings", default="400", help="action slabs in the ring (400: larger than the Infinity Cache)")
     p.add_argument("--prefetches", default="0", help="SK_MULTI_PREFETCH values (k_step_multi's prefetch wave)")
+    p.add_argument("--packs", default="-1", help="SK_MULTI_PACK values (-1 auto, 0 88-B form, 1 packed form)")
     p.add_argument("--no-graph", action="store_true")
     a = p.parse_args()
     torch.cuda.set_device(0)
@@ -96,8 +99,10 @@ def main():
                                     for ea in [int(x) for x in a.earlys.split(",")]:
                                         for rg in [int(x) for x in a.rings.split(",")]:
                                             for pf in [int(x) for x in a.prefetches.split(",")]:
-                                                r = multi_rate(n, T, pol, sp, sg, bk, fa, ea, ring=rg, prefetch=pf)
-                                                print(json.dumps(dict(r, rep=rep)), flush=True)
+                                                for pk in [int(x) for x in a.packs.split(",")]:
+                                                    r = multi_rate(n, T, pol, sp, sg, bk, fa, ea, ring=rg, prefetch=pf,
+                                                                   pack=pk)
+                                                    print(json.dumps(dict(r, rep=rep)), flush=True)
 
 
 if __name__ == "__main__":

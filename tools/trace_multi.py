@@ -27,6 +27,9 @@ def main():
     p.add_argument("--ticks", type=int, default=20)
     p.add_argument("--launches", type=int, default=5)
     p.add_argument("--dump", default="", help="save the last launch's raw stamps [waves][32] (.npy)")
+    p.add_argument("--wait", action="store_true",
+                   help="the -DSK_TRACE_MULTI_WAIT build: per tick 0..4 five stamps -> issue (+ carry) / load wait / "
+                        "tick_env / done + reset / state store medians")
     a = p.parse_args()
     from skillshot_learning_amd import VecSkillshotGame
     n, T = a.envs, a.ticks
@@ -58,6 +61,17 @@ def main():
             np.save(a.dump, ts)
         t0 = ts[:, 0].min()
         e = ts[:, 0] - t0
+        if a.wait:
+            nt = min(T, 5)
+            st5 = (ts[:, 1:1 + 5 * nt].reshape(-1, nt, 5) - t0) * 0.01  # us
+            prev = np.concatenate([e[:, None] * 0.01, st5[:, :-1, 4]], axis=1)
+            parts = dict(issue=st5[:, :, 0] - prev, wait=st5[:, :, 1] - st5[:, :, 0],
+                         tick=st5[:, :, 2] - st5[:, :, 1], done_reset=st5[:, :, 3] - st5[:, :, 2],
+                         store=st5[:, :, 4] - st5[:, :, 3])
+            out.append({k + "_p50_us": [round(float(v), 3) for v in np.median(x, axis=0)] for k, x in parts.items()}
+                       | {k + "_p90_us": [round(float(v), 3) for v in np.quantile(x, 0.9, axis=0)]
+                          for k, x in parts.items()})
+            continue
         nt = min(T, 29)
         ends = ts[:, 1:1 + nt] - t0
         per = np.diff(np.concatenate([ts[:, :1] - t0, ends], axis=1), axis=1) * 10 / 1e3  # us
