@@ -42,6 +42,9 @@ using namespace sk;
 #ifndef SK_ACT_AHEAD
 #define SK_ACT_AHEAD 1
 #endif
+#ifndef SK_EARLY_STORE
+#define SK_EARLY_STORE 1
+#endif
 
 // k_step_multi carries each tick's sincos to the next (tick_env_carry); 0:
 // every tick evaluates its four (A/B: tools/build_variant.sh -DSK_MULTI_CARRY=0)
@@ -799,6 +802,18 @@ __device__ __forceinline__ void multi_compute(const MultiArgs& a, const Cfg& c, 
   tick_env_m(c, e, m0, m1, k0 & k1, (double)acts[0].x, (double)acts[0].y, (double)acts[1].x, (double)acts[1].y);
 #endif
   SK_MTW(tick, 2);
+  // SK_EARLY_STORE (88-B form): the state goes out right after the tick,
+  // before the done outputs and the restart; a lane that restarts stores its
+  // planes again (its later stores win: same wave, same addresses, issue
+  // order).  The stores then drain while the wave finishes the tick instead
+  // of queueing in front of the next tick's loads (65,536 games: 2.22 -> 2.10
+  // us per tick at 400 ticks per launch, 2.6 -> 2.5 at 20; profiles/r06n_*).
+  // Storing pos / rot / qrot earlier still, between do_actions and game_tick,
+  // was slower (2.02 -> 2.13, 2.54 -> 2.59; profiles/r06o_*).
+  constexpr bool EARLY = SK_EARLY_STORE && !PACK;
+  if constexpr (EARLY) {
+    if (L.in) store_env_port<POL>(a, r, L.i, e, q_old0, q_old1, packed);
+  }
   // every load of this tick consumed (the counter slot's, issued first, with
   // them): without this the waitcnt pass, its tracking lost across the loop,
   // drains every store before the final counter store
@@ -832,7 +847,9 @@ __device__ __forceinline__ void multi_compute(const MultiArgs& a, const Cfg& c, 
                   (int)pack_fits_game(e.ticks, e.live, e.winner));
     to_pack = a.pack != nullptr && !last && __ballot(!fit) == 0;  // wave-uniform
   }
-  if (L.in) {
+  if constexpr (EARLY) {
+    if (d && a.auto_reset) store_env_port<POL>(a, r, L.i, e, q_old0, q_old1, true);  // the restarted game
+  } else if (L.in) {
     if (PACK && to_pack) {
       const bool qch = !packed || (__double_as_longlong(e.qrot[0]) != __double_as_longlong(q_old0)) ||
                        (__double_as_longlong(e.qrot[1]) != __double_as_longlong(q_old1));

@@ -29,6 +29,11 @@ def main():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--envs", type=int, default=65536)
     p.add_argument("--tag", default=os.path.basename(os.environ.get("SK_LIB_PATH", "lib")))
+    p.add_argument("--settle", choices=["none", "sweep", "long", "heat", "long_reset"], default="none",
+                   help="between the ring's generation and the warm-up: nothing (bench), a 512 MiB read "
+                        "sweep of another buffer (evicts the generation's dirty lines from the Infinity "
+                        "Cache), 400 more warm-up ticks (a long run's cache state), a ~3 ms matmul before the ring's "
+                        "generation (clocks), or 400 ticks then the env reset and the ring regenerated")
     a = p.parse_args()
     dev = torch.device("cuda", 0)
     n, ring = a.envs, 400
@@ -41,11 +46,24 @@ def main():
     e0.record(st)
     e1.record(st)
     us = []
+    big = torch.ones(128 << 20, dtype=torch.float32, device=dev) if a.settle == "sweep" else None
+    sink = torch.zeros((), dtype=torch.float32, device=dev)
+    mm = torch.randn(4096, 4096, device=dev) if a.settle == "heat" else None
     for rep in range(a.reps + 1):
         with torch.cuda.stream(st):
+            if a.settle == "heat":
+                sink.add_((mm @ mm).sum() + (mm @ mm).sum())
+            if a.settle == "long_reset":
+                fn(h, ap, ring, 0, 400, dp, None, 0, lim, 1, rp, sp)
             env.reset(random_positions=True)
             acts.copy_(env.gen_random_actions(ring))  # the ring rewritten: bench's cache state
         slab = 0
+        if a.settle == "sweep":
+            with torch.cuda.stream(st):
+                sink.add_(big.sum())
+        elif a.settle == "long":
+            fn(h, ap, ring, 0, 400, dp, None, 0, lim, 1, rp, sp)
+            slab = 400 % ring
         for t in (1, a.warmup):
             fn(h, ap, ring, slab, t, dp, None, 0, lim, 1, rp, sp)
             slab += t
@@ -60,7 +78,7 @@ def main():
     us.sort()
     q = lambda f: us[min(len(us) - 1, int(f * len(us)))]  # noqa: E731
     med = statistics.median(us)
-    print(json.dumps(dict(tag=a.tag, k=a.k, reps=a.reps, event_us_median=round(med, 4),
+    print(json.dumps(dict(tag=a.tag, settle=a.settle, k=a.k, reps=a.reps, event_us_median=round(med, 4),
                           event_us_mean=round(statistics.fmean(us), 4), p10=round(q(0.1), 4), p90=round(q(0.9), 4),
                           frac_median=round(193 * n / (med * 1e-6) / 8e12, 4))), flush=True)
     env.close()
