@@ -2249,12 +2249,14 @@ static int step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64
     // default here: 65,536 games 2.73 vs 2.81 us per tick at 20 ticks per
     // launch, 131,072 3.69 vs 3.70 / 3.33 vs 3.37 (profiles/r03i_multi_fast_early_sweep.jsonl)
     const int early = e->multi_early > 0;
-    // workgroup: one wave (default) or four (SK_MULTI_BLOCK=256: a quarter of
-    // the workgroups to dispatch, one wave per SIMD either way).  With the
-    // packed form 256 lanes won by ~0.6 %, with the 88-B form 64 lanes win by
-    // about as much (65,536 games, K = 4,000: 2.40 vs 2.415 us per tick;
-    // profiles/r03mb_multi_block_ab.jsonl, r03mb2_multi_block_early_ab.jsonl)
-    if (e->multi_block == 256) {
+    // workgroup: four waves (default; SK_MULTI_BLOCK=64: one).  A quarter of
+    // the workgroups to dispatch, one wave per SIMD either way.  Round 3 had
+    // 64 lanes ahead by ~0.6 % with the 88-B form (profiles/
+    // r03mb_multi_block_ab.jsonl, r03mb2_multi_block_early_ab.jsonl); with the
+    // round-6 tick (early stores, the slab a tick ahead) 256 lanes take the
+    // driver's 20-tick launch from 2.52-2.56 to 2.48-2.50 us per tick (median
+    // of 30 regions, three passes; profiles/r06p_k20_block_ab.jsonl)
+    if (e->multi_block == 256 || (e->multi_block < 0 && e->multi_prefetch <= 0)) {
       const dim3 g((unsigned)((e->n + 255) / 256));
       if (pk)
         err = pol == 1 ? launch_timed(k_step_multi<1, true, 256>, g, dim3(256), hs, e0, e1, a, e->dcfg, early)

@@ -1011,6 +1011,10 @@ __device__ __forceinline__ void scatter_fwd_pack(char* out, int p, float v) {  /
 #define SK_ADAM_INFLIGHT 8
 #endif
 constexpr int kAdamParams = SK_ADAM_PARAMS, kAdamSlices = SK_ADAM_SLICES, kAdamInflight = SK_ADAM_INFLIGHT;
+// partials per lane loaded in one round (k_adam_flat): 32 = the sliced fp32
+// kernels' W1 / b1 contributions at batch 256 (128 rows over 4 slices)
+constexpr int kAdamOnce = 32 + kAdamInflight;
+static_assert(kAdamParams == 64, "one wave per slice: the partial count is wave-uniform");
 static_assert(kAdamInflight >= 2 && (kAdamInflight & (kAdamInflight - 1)) == 0, "a power of two");
 static_assert(skpart::kPW2 % kAdamParams == 0, "the W1 rows stay workgroup-uniform");
 
@@ -1060,7 +1064,45 @@ __global__ void __launch_bounds__(kAdamParams * kAdamSlices) k_adam_flat(const f
   float acc[kAdamInflight];
 #pragma unroll
   for (int j = 0; j < kAdamInflight; ++j) acc[j] = 0.f;
-  if (in) {
+  // this lane's partials are k = slice + i * kAdamSlices, i < cnt (wave-uniform)
+  const int cnt = in && GG > slice ? (GG - slice + kAdamSlices - 1) / kAdamSlices : 0;
+  float alpha = 0.f;
+  if (cnt <= kAdamOnce) {
+    // every partial in flight at once (one load latency; the loop below
+    // waited for each group of kAdamInflight and the tail one load at a
+    // time: at batch 256 every W2 lane's 4 partials were 4 dependent round
+    // trips, every W1 lane's 32 were 4), summed in the loop's order:
+    // group g (i = 8g .. 8g + 7, while 8g + 7 < cnt) into acc[i % 8], the
+    // tail (i >= 8 * groups) into acc[0], each in increasing i.  Same sums.
+    float x[kAdamOnce];
+#pragma unroll
+    for (int g = 0; g < kAdamOnce / kAdamInflight; ++g) {
+      if (kAdamInflight * g < cnt) {  // wave-uniform (one wave per slice): only the groups in use
+#pragma unroll
+        for (int j = 0; j < kAdamInflight; ++j) {
+          const int i = kAdamInflight * g + j;
+          x[i] = src[(int64_t)(i < cnt ? slice + i * kAdamSlices : slice) * ld + pp];  // unconditional within the group
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < kAdamInflight; ++j) x[kAdamInflight * g + j] = 0.f;
+      }
+    }
+    // Adam's step size under the loads (it needs only the step count)
+    if (apply && in && slice == 0) {
+      alpha = lr * sqrtf(1.f - powf(beta2, t)) / (1.f - powf(beta1, t));
+      asm volatile("" : "+v"(alpha));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const int full = (cnt / kAdamInflight) * kAdamInflight;
+#pragma unroll
+    for (int i = 0; i < kAdamOnce; ++i) {
+      const int j = i % kAdamInflight;
+      acc[j] = i < full ? acc[j] + x[i] : acc[j];
+    }
+#pragma unroll
+    for (int i = 0; i < kAdamOnce; ++i) acc[0] = (i >= full && i < cnt) ? acc[0] + x[i] : acc[0];
+  } else if (in) {
     int k = slice;
     for (; k + (kAdamInflight - 1) * kAdamSlices < GG; k += kAdamInflight * kAdamSlices) {
 #pragma unroll
@@ -1085,7 +1127,7 @@ __global__ void __launch_bounds__(kAdamParams * kAdamSlices) k_adam_flat(const f
   for (int j = 0; j < kAdamSlices - 1; ++j) g += red[j][lane];
   if (grad_out) grad_out[p] = g;
   if (!apply) return;
-  const float alpha = lr * sqrtf(1.f - powf(beta2, t)) / (1.f - powf(beta1, t));
+  if (cnt > kAdamOnce) alpha = lr * sqrtf(1.f - powf(beta2, t)) / (1.f - powf(beta1, t));
   mm = mm + (g - mm) * (1.f - beta1);
   vv = vv + (g * g - vv) * (1.f - beta2);
   m[p] = mm;
