@@ -1267,6 +1267,194 @@ __device__ __forceinline__ void split_multi_tick(const MultiArgs& a, const Cfg& 
   }
 }
 
+// ---- the step-only split tick of round 6 (SK_SPLIT_CARRY): k_step_multi's
+// round-6 tick in the split geometry.  The lane's player's rotation sincos is
+// carried from the previous tick (evaluated at the top of the tick under its
+// loads, keyed by the rotation's bits), a projectile in flight keeps its
+// carried sincos, a fired one gets its step by fp32 angle addition with the
+// wave's exact fallback (tick_env_carry, sk_device.hpp); the commits are
+// selects; the action slab is loaded one tick ahead; the state halves are
+// stored right after the tick, before done / restart (a restarted game's
+// lanes store theirs again).  Bit for bit split_multi_tick<POL, false>.
+#ifndef SK_SPLIT_CARRY
+#define SK_SPLIT_CARRY 1
+#endif
+struct SplitCarry {
+  double kr, kq;  // keys: m = sincos(kr), tq = sincos(kq)
+  sktrig::SinCos m, tq;
+  double pr;      // the last tick's final rotation (evaluated at the next tick's top)
+  bool qs, have, pend;
+};
+__device__ __forceinline__ void split_carry_advance(SplitCarry& t) {
+  bool k;
+  t.m = sktrig::sincos_bf(t.pr, &k);
+  if (!k) t.m = sincos_lib(t.pr);
+  t.kr = t.pr;
+  if (t.qs) {
+    t.tq = t.m;
+    t.kq = t.pr;
+  }
+  t.have = true;
+  t.pend = false;
+}
+struct SplitRaw {
+  skb2i rot, qrot, pp, ca, qq, mi;
+};
+template <int POL>
+__device__ __forceinline__ skb2i ld_half_raw(const MultiArgs& a, __amdgpu_buffer_rsrc_t r, int k, const void* plane,
+                                             int64_t h) {
+  if constexpr (POL == 0) return reinterpret_cast<const skb2i*>(plane)[h];
+  else return __builtin_amdgcn_raw_buffer_load_b64(r, (uint32_t)h * 8u + a.off[k], 0, 16);
+}
+template <int POL>
+__device__ __forceinline__ void split_load_raw(const MultiArgs& a, __amdgpu_buffer_rsrc_t r, const SplitLane& L,
+                                               SplitRaw& w) {
+  // k_step_split's load order: rotation first
+  w.rot = ld_half_raw<POL>(a, r, 1, a.v.rot, L.hc);
+  w.qrot = ld_half_raw<POL>(a, r, 3, a.v.qrot, L.hc);
+  w.pp = ld_half_raw<POL>(a, r, 0, a.v.pos, L.hc);
+  w.ca = ld_half_raw<POL>(a, r, 4, a.v.qcdage, L.hc);
+  w.qq = ld_half_raw<POL>(a, r, 2, a.v.qpos, L.hc);
+  w.mi = ld_half_raw<POL>(a, r, 5, a.v.misc, L.ic);
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <int POL>
+__device__ __forceinline__ void split_store_state(const MultiArgs& a, __amdgpu_buffer_rsrc_t r, const SplitLane& L,
+                                                  int px, int py, double rot, int qx, int qy, double qrot, bool qch,
+                                                  int qcd, int qage, int ticks, unsigned f) {
+  st_half_i<POL>(a, r, 0, reinterpret_cast<int2*>(a.v.pos), L.h, px, py);
+  st_half_d<POL>(a, r, 1, reinterpret_cast<double*>(a.v.rot), L.h, rot);
+  st_half_i<POL>(a, r, 2, reinterpret_cast<int2*>(a.v.qpos), L.h, qx, qy);
+  if (qch) st_half_d<POL>(a, r, 3, reinterpret_cast<double*>(a.v.qrot), L.h, qrot);
+  st_half_i<POL>(a, r, 4, reinterpret_cast<int2*>(a.v.qcdage), L.h, qcd, qage);
+  if (L.p == 0) st_half_i<POL>(a, r, 5, a.v.misc, L.i, ticks, (int)f);
+}
+template <int POL>
+__device__ __forceinline__ void split_tick_carry(const MultiArgs& a, const Cfg& c, __amdgpu_buffer_rsrc_t r,
+                                                 SplitLane& L, WaveCtr& wc, int64_t so, uint64_t step,
+                                                 const SplitRaw& w, float2 act, SplitCarry& tc, bool last) {
+  using sktrig::round_safe;
+  const int p = L.p;
+  double rot = __builtin_bit_cast(double, w.rot), qrot = __builtin_bit_cast(double, w.qrot);
+  int px = w.pp.x, py = w.pp.y, qx = w.qq.x, qy = w.qq.y, qcd = w.ca.x, qage = w.ca.y, ticks = w.mi.x;
+  const unsigned flags = (unsigned)w.mi.y;
+  int qvalid = (flags >> (8 * p)) & 0xff, live = (flags >> 16) & 0xff, winner = (flags >> 24) & 0xff;
+  const double q_old = qrot;
+  const bool f = qcd <= 0;  // fires this tick (Player.py:80)
+  const bool miss = !tc.have || !same_bits(rot, tc.kr) || (qvalid && !f && !same_bits(qrot, tc.kq));
+  if (__ballot(L.in && miss) != 0) {  // the launch's first tick
+    bool k0, k1;
+    tc.m = sktrig::sincos_bf(rot, &k0);
+    tc.tq = sktrig::sincos_bf(qrot, &k1);
+    if (!(k0 & k1)) {
+      if (!k0) tc.m = sincos_lib(rot);
+      if (!k1) tc.tq = sincos_lib(qrot);
+    }
+    tc.kr = rot;
+    tc.kq = qrot;
+    tc.have = true;
+  }
+  const float l = clamp_action_f(act.y);
+  const double rn = rot + (double)l * c.look;  // == move_look_s
+  const float lk = (float)c.look, qsf = (float)c.qspeed, eq = 2e-6f * qsf;
+  const sktrig::SinCosF u = sktrig::sincos_add(sktrig::SinCosF{(float)tc.m.s, (float)tc.m.c}, l * lk);
+  const float ex = u.s * qsf, ey = u.c * qsf;
+  const bool un = f && !((int)(fabs(rot) < 1647099.3291652855) & (int)round_safe(ex, eq) & (int)round_safe(ey, eq));
+  sktrig::SinCos tt = tc.tq;  // in flight: the carried exact value
+  bool fast = f;
+  if (__builtin_expect(__ballot(L.in && un) != 0, 0)) {  // the exact sincos of the fired projectiles
+    bool k;
+    sktrig::SinCos x = sktrig::sincos_bf(rn, &k);
+    if (!k) x = sincos_lib(rn);
+    if (f) tt = x;
+    fast = false;
+  }
+  // do_actions(p + 1, ...)  SkillshotLearner.py:206-213 (Player.py:57-68, :33-39, :78-89)
+  {
+    const double speed = clamp_action((double)act.x), psp = (double)c.pspeed;
+    const double nxf = __builtin_rint((double)px - (tc.m.s * psp) * speed);
+    const double nyf = __builtin_rint((double)py - (tc.m.c * psp) * speed);
+    const bool ok = (nxf >= 0.0) & (nxf + (double)c.psize <= (double)c.W) & (nyf >= 0.0) &
+                    (nyf + (double)c.psize <= (double)c.H);
+    px = ok ? (int)(ok ? nxf : 0.0) : px;
+    py = ok ? (int)(ok ? nyf : 0.0) : py;
+  }
+  rot = rn;
+  qx = f ? px : qx;
+  qy = f ? py : qy;
+  qrot = f ? rot : qrot;
+  qvalid = f ? 1 : qvalid;
+  qcd = f ? c.cdmax : qcd;
+  qage = f ? 0 : qage;
+  // game_tick  SkillshotGame.py:115-122 (Projectile.py:38-53); live is the same in both lanes
+  const int lv = live != 0;
+  ticks += lv;
+  {
+    const double qsp = (double)c.qspeed;
+    const int nxF = qx - (int)rintf(ex), nyF = qy - (int)rintf(ey);
+    const int nxE = (int)__builtin_rint((double)qx - tt.s * qsp), nyE = (int)__builtin_rint((double)qy - tt.c * qsp);
+    const int nx = fast ? nxF : nxE, ny = fast ? nyF : nyE;
+    const bool ok = (nx + c.qsize <= c.W) & (nx >= 0) & (ny + c.qsize <= c.H) & (ny >= 0);
+    const bool upd = lv && qvalid;
+    qx = (upd && ok) ? nx : qx;
+    qy = (upd && ok) ? ny : qy;
+    qvalid = (upd && !ok) ? 0 : qvalid;
+    qcd -= lv;
+    qage += lv;
+  }
+  const int opx = pair_swap(px), opy = pair_swap(py);
+  const int oqx = pair_swap(qx), oqy = pair_swap(qy), oqv = pair_swap(qvalid);
+  {  // SkillshotGame.check_collision (:58-94): player 1 tested first
+    const int p1x = p ? opx : px, p1y = p ? opy : py, q1x = p ? oqx : qx, q1y = p ? oqy : qy, q1v = p ? oqv : qvalid;
+    const int p2x = p ? px : opx, p2y = p ? py : opy, q2x = p ? qx : oqx, q2y = p ? qy : oqy, q2v = p ? qvalid : oqv;
+    const bool h1 = lv && hit_test_s(c, p1x, p1y, q2x, q2y, q2v);
+    const bool h2 = lv && !h1 && hit_test_s(c, p2x, p2y, q1x, q1y, q1v);
+    winner = h1 ? 1 : (h2 ? 2 : winner);
+    live = (h1 || h2) ? 0 : live;
+  }
+  ctr_settle(wc);  // every load of this tick consumed (see multi_tick)
+  {  // the state out before done / restart (SK_EARLY_STORE's reason, k_step_multi)
+    const unsigned fl = (unsigned)(qvalid & 0xff) | ((unsigned)(oqv & 0xff) << 8) | ((unsigned)(live & 0xff) << 16) |
+                        ((unsigned)(winner & 0xff) << 24);
+    const bool qch = __double_as_longlong(qrot) != __double_as_longlong(q_old);
+    if (L.in) split_store_state<POL>(a, r, L, px, py, rot, qx, qy, qrot, qch, qcd, qage, ticks, fl);
+  }
+  const bool d = L.in && ((!live) || (ticks >= a.tick_limit));  // SkillshotLearner.py:302
+  if (L.in && p == 0) {
+    if (a.done) a.done[so * a.out_stride + L.i] = (uint8_t)d;
+    if (a.winner) a.winner[so * a.out_stride + L.i] = (uint8_t)winner;
+  }
+  const bool dc = d && p == 0;
+  L.n_done += dc;
+  L.n_h1 += dc && winner == 1;
+  L.n_h2 += dc && winner == 2;
+  L.t_sum += dc ? (unsigned)ticks : 0u;
+  const bool rs = d && a.auto_reset;  // SkillshotGame.__init__ :10-25 for this lane's player
+  if (rs) {
+    if (a.random_positions) {
+      const U4 u4 = draw4(a.seed, (uint64_t)(a.env_offset + L.i), step, 1u);
+      px = u32_to_pos(p ? u4.z : u4.x, c.rlo, c.rhi);
+      py = u32_to_pos(p ? u4.w : u4.y, c.rlo, c.rhi);
+    } else {
+      px = p ? c.f2x : c.f1x;
+      py = p ? c.f2y : c.f1y;
+    }
+    rot = 0.0; qx = 0; qy = 0; qrot = 0.0; qcd = 0; qage = 0; qvalid = 0;
+    ticks = 0; live = 1; winner = 0;
+  }
+  const int ov = pair_swap(qvalid);  // every lane active (top level)
+  if (rs) {
+    const unsigned fl = (unsigned)(qvalid & 0xff) | ((unsigned)(ov & 0xff) << 8) | ((unsigned)(live & 0xff) << 16) |
+                        ((unsigned)(winner & 0xff) << 24);
+    split_store_state<POL>(a, r, L, px, py, rot, qx, qy, qrot, true, qcd, qage, ticks, fl);
+  }
+  if (!last) {  // the tick's final rotation: the next tick's carried sincos
+    tc.pr = rot;
+    tc.qs = same_bits(qrot, rot);
+    tc.pend = true;
+  }
+}
+
 // BLK 512 (the 65,536-game geometry): one workgroup of 8 waves per CU, so
 // each SIMD hosts waves w and w + 4 of ONE workgroup (MI355X_MICROARCH.md
 // "Two waves per SIMD"); `stagger` > 0 starts waves 4-7 stagger x 512
@@ -1297,11 +1485,40 @@ __global__ void __launch_bounds__(BLK + (PF > 0 ? 64 : 0)) k_step_split_multi(Mu
   step_advance(a.step, step0, (uint64_t)a.n_ticks);
   const __amdgpu_buffer_rsrc_t r = raw_rsrc(a.base);
   int64_t slab = a.slab0, so = a.out0;
-  for (int t = 0; t < a.n_ticks; ++t) {
-    if constexpr (PF > 0) __builtin_amdgcn_s_barrier();
-    split_multi_tick<POL, OBS>(a, c, r, L, wc, so, step0 + (uint64_t)t, slab);
-    slab = slab + 1 == a.ring ? 0 : slab + 1;
-    so = so + 1 == a.out_slabs ? 0 : so + 1;
+  if constexpr (!OBS && PF == 0 && SK_SPLIT_CARRY) {
+    // the round-6 tick (split_tick_carry): the slab one tick ahead in the
+    // register pair this tick does not read, two ticks per iteration
+    const int64_t aoff = (int64_t)L.p * a.n + L.ic;
+    float2 pa0 = load_action(a.actions + slab * 2 * a.n + aoff), pa1;
+    int64_t pslab = slab + 1 == a.ring ? 0 : slab + 1;
+    SplitCarry tc;
+    tc.have = tc.pend = false;
+    int t = 0;
+    auto one_tick = [&](const float2& cur, float2& nxt) {
+      SplitRaw w;
+      split_load_raw<POL>(a, r, L, w);
+      const int64_t ls = t + 1 < a.n_ticks ? pslab : slab;  // unconditional (see k_step_multi)
+      nxt = load_action(a.actions + ls * 2 * a.n + aoff);
+      __builtin_amdgcn_sched_barrier(0);
+      if (tc.pend) split_carry_advance(tc);  // the last tick's rotation, while this tick's loads fly
+      __builtin_amdgcn_sched_barrier(0);
+      split_tick_carry<POL>(a, c, r, L, wc, so, step0 + (uint64_t)t, w, cur, tc, t + 1 == a.n_ticks);
+      slab = slab + 1 == a.ring ? 0 : slab + 1;
+      pslab = pslab + 1 == a.ring ? 0 : pslab + 1;
+      so = so + 1 == a.out_slabs ? 0 : so + 1;
+    };
+    do {  // n_ticks >= 1 (host-checked)
+      one_tick(pa0, pa1);
+      if (++t >= a.n_ticks) break;
+      one_tick(pa1, pa0);
+    } while (++t < a.n_ticks);
+  } else {
+    for (int t = 0; t < a.n_ticks; ++t) {
+      if constexpr (PF > 0) __builtin_amdgcn_s_barrier();
+      split_multi_tick<POL, OBS>(a, c, r, L, wc, so, step0 + (uint64_t)t, slab);
+      slab = slab + 1 == a.ring ? 0 : slab + 1;
+      so = so + 1 == a.out_slabs ? 0 : so + 1;
+    }
   }
   if (a.ctr) {
     const unsigned c4[4] = {L.n_done, L.n_h1, L.n_h2, L.t_sum};
@@ -2229,10 +2446,12 @@ static int step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64
     // the action-slab prefetch wave: SK_MULTI_PREFETCH, else, at 400 ticks
     // per launch: the full contract 4 ticks ahead on 512-lane workgroups
     // (65,536 games 4.35 -> 3.48-3.52 us per tick) and 1 on 64-lane ones
-    // (32,768 2.71 -> 2.59, 8,192 2.25 -> 2.24-2.25); the step-only tick 2
-    // (32,768 1.80 -> 1.68, 16,384 1.67 -> 1.645, 8,192 1.585 -> 1.58;
-    // profiles/r04ar_prefetch_*_sweep.jsonl, r04as_prefetch_obs64_sweep.jsonl)
-    const int pf = n_ticks < 2 ? 0 : e->multi_prefetch >= 0 ? e->multi_prefetch : full ? (wide ? 4 : 1) : 2;
+    // (32,768 2.71 -> 2.59, 8,192 2.25 -> 2.24-2.25; profiles/
+    // r04ar_prefetch_*_sweep.jsonl, r04as_prefetch_obs64_sweep.jsonl).  The
+    // step-only tick runs split_tick_carry (round 6), which loads the slab a
+    // tick ahead itself: no prefetch wave (8,192 games 1.58 -> 1.20 us per
+    // tick, 32,768 1.68 -> 1.46; profiles/r06x_split_carry_sweep.jsonl)
+    const int pf = n_ticks < 2 ? 0 : e->multi_prefetch >= 0 ? e->multi_prefetch : full ? (wide ? 4 : 1) : 0;
     const int sg = wide ? e->multi_stagger : 0;
     if (full)
       err = wide ? (pol == 1 ? launch_split_multi<1, 512, true>(pf, g512, hs, a, e->dcfg, sg)
