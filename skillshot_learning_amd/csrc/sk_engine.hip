@@ -1329,7 +1329,12 @@ __device__ __forceinline__ void split_store_state(const MultiArgs& a, __amdgpu_b
   st_half_i<POL>(a, r, 4, reinterpret_cast<int2*>(a.v.qcdage), L.h, qcd, qage);
   if (L.p == 0) st_half_i<POL>(a, r, 5, a.v.misc, L.i, ticks, (int)f);
 }
-template <int POL>
+// OBS (the full contract, sk_env_step_multi_obs): the tick also evaluates
+// the exact sincos of the post-look rotation (the obs epilogue's projectile
+// sincos when it fires, and the next tick's carried move sincos: no
+// evaluation at the next tick's top) and the fp32 one (obs12_sc's `pr`), and
+// writes the observation and reward after the state stores.
+template <int POL, bool OBS>
 __device__ __forceinline__ void split_tick_carry(const MultiArgs& a, const Cfg& c, __amdgpu_buffer_rsrc_t r,
                                                  SplitLane& L, WaveCtr& wc, int64_t so, uint64_t step,
                                                  const SplitRaw& w, float2 act, SplitCarry& tc, bool last) {
@@ -1362,13 +1367,32 @@ __device__ __forceinline__ void split_tick_carry(const MultiArgs& a, const Cfg& 
   const bool un = f && !((int)(fabs(rot) < 1647099.3291652855) & (int)round_safe(ex, eq) & (int)round_safe(ey, eq));
   sktrig::SinCos tt = tc.tq;  // in flight: the carried exact value
   bool fast = f;
+  sktrig::SinCos xn{0.0, 1.0};    // OBS: sincos(rn), exact
+  sktrig::SinCosF pr{0.0f, 1.0f};  // OBS: sincos(rn) in fp32 (obs12_sc)
+  if constexpr (OBS) {
+    bool kx, k2;
+    xn = sktrig::sincos_bf(rn, &kx);
+    pr = sktrig::sincos_fast(rn, &k2);
+    if (!(kx & k2)) {
+      if (!kx) xn = sincos_lib(rn);
+      if (!k2) {
+        const sktrig::SinCos rr = sincos_lib(rn);
+        pr.s = (float)rr.s;
+        pr.c = (float)rr.c;
+      }
+    }
+  }
   if (__builtin_expect(__ballot(L.in && un) != 0, 0)) {  // the exact sincos of the fired projectiles
-    bool k;
-    sktrig::SinCos x = sktrig::sincos_bf(rn, &k);
-    if (!k) x = sincos_lib(rn);
+    sktrig::SinCos x = xn;
+    if constexpr (!OBS) {
+      bool k;
+      x = sktrig::sincos_bf(rn, &k);
+      if (!k) x = sincos_lib(rn);
+    }
     if (f) tt = x;
     fast = false;
   }
+  const sktrig::SinCos tq_obs = f ? xn : tc.tq;  // OBS: the projectile's sincos after shoot
   // do_actions(p + 1, ...)  SkillshotLearner.py:206-213 (Player.py:57-68, :33-39, :78-89)
   {
     const double speed = clamp_action((double)act.x), psp = (double)c.pspeed;
@@ -1419,6 +1443,28 @@ __device__ __forceinline__ void split_tick_carry(const MultiArgs& a, const Cfg& 
     const bool qch = __double_as_longlong(qrot) != __double_as_longlong(q_old);
     if (L.in) split_store_state<POL>(a, r, L, px, py, rot, qx, qy, qrot, qch, qcd, qage, ticks, fl);
   }
+  bool amb = false;
+  double gq = 0.0;  // the fast projectile gradient (the ambiguous flag's interval check)
+  const int aqx = qx, aqy = qy;  // the post-tick projectile, for the flag's redo
+  const double aqrot = qrot;
+  if constexpr (OBS) {
+    if (L.in) {  // prepare_states / calculate_rewards_* (SkillshotLearner.py:512-603) of the post-tick state
+      float o[12], pd;
+      obs12_sc(c, px, py, rot, pr, qx, qy, qrot, tq_obs, qcd, qvalid, opx, opy, o, &pd, &amb, &gq);
+      if (a.obs) store_obs(a.obs + so * 24 * a.n, a.n, p, L.i, o);
+      if (a.reward) {
+        float rw;
+        if (a.reward_kind == SK_REWARD_SIMPLE) {  // a difference of distances: fp64 roots
+          const double mine = dist_point_point(qx, qy, opx, opy);
+          const double theirs = dist_point_point(oqx, oqy, px, py);
+          rw = (float)(mine - theirs);
+        } else {
+          rw = (float)(-(double)pd / (double)c.W);
+        }
+        a.reward[so * 2 * a.n + (int64_t)p * a.n + L.i] = rw;
+      }
+    }
+  }
   const bool d = L.in && ((!live) || (ticks >= a.tick_limit));  // SkillshotLearner.py:302
   if (L.in && p == 0) {
     if (a.done) a.done[so * a.out_stride + L.i] = (uint8_t)d;
@@ -1448,7 +1494,23 @@ __device__ __forceinline__ void split_tick_carry(const MultiArgs& a, const Cfg& 
                         ((unsigned)(winner & 0xff) << 24);
     split_store_state<POL>(a, r, L, px, py, rot, qx, qy, qrot, true, qcd, qage, ticks, fl);
   }
-  if (!last) {  // the tick's final rotation: the next tick's carried sincos
+  if constexpr (OBS) {
+    // the future-collision flag within its margin of an edge, settled after
+    // this tick's state stores (k_step_split's tail rule): by the interval
+    // check unless it depends on g's last bits (then the correctly rounded tan)
+    if (amb && a.obs) {
+      const int fi = future_flag_interval(c, aqx, aqy, opx, opy, gq);
+      const float fv = fi >= 0 ? (float)fi : future_flag_cr(c, aqx, aqy, aqrot, opx, opy);
+      a.obs[so * 24 * a.n + ((int64_t)p * a.n + L.i) * 12 + 11] = fv;
+    }
+    // the next tick's carried sincos, already evaluated: sincos(rn) for the
+    // move (sincos(0) = (0, 1) after a restart), the projectile's after shoot
+    tc.m = rs ? sktrig::SinCos{0.0, 1.0} : xn;
+    tc.kr = rot;
+    tc.tq = tq_obs;
+    tc.kq = qrot;
+    tc.have = true;
+  } else if (!last) {  // the tick's final rotation: the next tick's carried sincos
     tc.pr = rot;
     tc.qs = same_bits(qrot, rot);
     tc.pend = true;
@@ -1485,7 +1547,7 @@ __global__ void __launch_bounds__(BLK + (PF > 0 ? 64 : 0)) k_step_split_multi(Mu
   step_advance(a.step, step0, (uint64_t)a.n_ticks);
   const __amdgpu_buffer_rsrc_t r = raw_rsrc(a.base);
   int64_t slab = a.slab0, so = a.out0;
-  if constexpr (!OBS && PF == 0 && SK_SPLIT_CARRY) {
+  if constexpr ((PF == 0 || OBS) && SK_SPLIT_CARRY) {
     // the round-6 tick (split_tick_carry): the slab one tick ahead in the
     // register pair this tick does not read, two ticks per iteration
     const int64_t aoff = (int64_t)L.p * a.n + L.ic;
@@ -1496,13 +1558,14 @@ __global__ void __launch_bounds__(BLK + (PF > 0 ? 64 : 0)) k_step_split_multi(Mu
     int t = 0;
     auto one_tick = [&](const float2& cur, float2& nxt) {
       SplitRaw w;
+      if constexpr (PF > 0) __builtin_amdgcn_s_barrier();  // the prefetch wave (full contract at 512 lanes)
       split_load_raw<POL>(a, r, L, w);
       const int64_t ls = t + 1 < a.n_ticks ? pslab : slab;  // unconditional (see k_step_multi)
       nxt = load_action(a.actions + ls * 2 * a.n + aoff);
       __builtin_amdgcn_sched_barrier(0);
       if (tc.pend) split_carry_advance(tc);  // the last tick's rotation, while this tick's loads fly
       __builtin_amdgcn_sched_barrier(0);
-      split_tick_carry<POL>(a, c, r, L, wc, so, step0 + (uint64_t)t, w, cur, tc, t + 1 == a.n_ticks);
+      split_tick_carry<POL, OBS>(a, c, r, L, wc, so, step0 + (uint64_t)t, w, cur, tc, t + 1 == a.n_ticks);
       slab = slab + 1 == a.ring ? 0 : slab + 1;
       pslab = pslab + 1 == a.ring ? 0 : pslab + 1;
       so = so + 1 == a.out_slabs ? 0 : so + 1;
@@ -2450,8 +2513,12 @@ static int step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64
     // r04ar_prefetch_*_sweep.jsonl, r04as_prefetch_obs64_sweep.jsonl).  The
     // step-only tick runs split_tick_carry (round 6), which loads the slab a
     // tick ahead itself: no prefetch wave (8,192 games 1.58 -> 1.20 us per
-    // tick, 32,768 1.68 -> 1.46; profiles/r06x_split_carry_sweep.jsonl)
-    const int pf = n_ticks < 2 ? 0 : e->multi_prefetch >= 0 ? e->multi_prefetch : full ? (wide ? 4 : 1) : 0;
+    // tick, 32,768 1.68 -> 1.46; profiles/r06x_split_carry_sweep.jsonl).  The
+    // full contract on split_tick_carry: no prefetch wave on 64-lane
+    // workgroups (8,192 2.23 -> 1.96, 32,768 2.55 -> 2.29), and still 4 ticks
+    // ahead on 512-lane ones (65,536 3.38-3.57 -> 3.20-3.39; profiles/
+    // r06aa_obs_carry_sweep.jsonl, r06ab_obs_carry_pf_sweep.jsonl)
+    const int pf = n_ticks < 2 ? 0 : e->multi_prefetch >= 0 ? e->multi_prefetch : full ? (wide ? 4 : 0) : 0;
     const int sg = wide ? e->multi_stagger : 0;
     if (full)
       err = wide ? (pol == 1 ? launch_split_multi<1, 512, true>(pf, g512, hs, a, e->dcfg, sg)
