@@ -1547,7 +1547,7 @@ __global__ void __launch_bounds__(BLK + (PF > 0 ? 64 : 0)) k_step_split_multi(Mu
   step_advance(a.step, step0, (uint64_t)a.n_ticks);
   const __amdgpu_buffer_rsrc_t r = raw_rsrc(a.base);
   int64_t slab = a.slab0, so = a.out0;
-  if constexpr ((PF == 0 || OBS) && SK_SPLIT_CARRY) {
+  if constexpr (SK_SPLIT_CARRY) {
     // the round-6 tick (split_tick_carry): the slab one tick ahead in the
     // register pair this tick does not read, two ticks per iteration
     const int64_t aoff = (int64_t)L.p * a.n + L.ic;
@@ -2518,7 +2518,15 @@ static int step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64
     // workgroups (8,192 2.23 -> 1.96, 32,768 2.55 -> 2.29), and still 4 ticks
     // ahead on 512-lane ones (65,536 3.38-3.57 -> 3.20-3.39; profiles/
     // r06aa_obs_carry_sweep.jsonl, r06ab_obs_carry_pf_sweep.jsonl)
-    const int pf = n_ticks < 2 ? 0 : e->multi_prefetch >= 0 ? e->multi_prefetch : full ? (wide ? 4 : 0) : 0;
+    // With the step-only carried tick the prefetch wave still pays at 32,768
+    // games (2 ticks ahead: 1.46 -> 1.35 us at 400 ticks per launch, 1.64 ->
+    // 1.54 at 20), not at 8,192 (1.20 either way) nor 65,536
+    // (profiles/r06ad_split_carry_pf_sweep.jsonl)
+    const int pf = n_ticks < 2                ? 0
+                   : e->multi_prefetch >= 0   ? e->multi_prefetch
+                   : full                     ? (wide ? 4 : 0)
+                   : (e->n > 8192 && !wide) ? 2
+                                              : 0;
     const int sg = wide ? e->multi_stagger : 0;
     if (full)
       err = wide ? (pol == 1 ? launch_split_multi<1, 512, true>(pf, g512, hs, a, e->dcfg, sg)
