@@ -77,7 +77,7 @@ struct sk_env {
   int multi_policy;
   // k_step_multi geometry: -1 auto, 0 lane per game, 1 player per lane (SK_MULTI_SPLIT)
   int multi_split;
-  int multi_early;    // k_step_multi: the restart draw under the loads, 0 (default) / 1 (SK_MULTI_EARLY)
+  int multi_early;    // k_step_multi: the restart draw under the loads, -1 (default: on) / 0 / 1 (SK_MULTI_EARLY)
   int multi_block;    // workgroup lanes (SK_MULTI_BLOCK): split geometry -1 auto, 64 or 512; lane per game 64 or 256
   int multi_stagger;  // waves 4-7 of a 512-lane workgroup start this x 512 cycles late (SK_MULTI_STAGGER)
   int multi_prefetch; // action-slab prefetch wave, ticks ahead (SK_MULTI_PREFETCH; 0 off, -1 auto): k_step_multi
@@ -1857,7 +1857,7 @@ static int make_env(sk_env** out, const sk_state_view* view, int32_t n, int64_t 
   if (const char* mp = std::getenv("SK_MULTI_POLICY")) e->multi_policy = std::atoi(mp);
   e->multi_split = -1;
   if (const char* ms = std::getenv("SK_MULTI_SPLIT")) e->multi_split = std::atoi(ms);
-  e->multi_early = 0;
+  e->multi_early = -1;
   if (const char* me = std::getenv("SK_MULTI_EARLY")) e->multi_early = std::atoi(me);
   e->multi_block = -1;
   if (const char* mb = std::getenv("SK_MULTI_BLOCK")) e->multi_block = std::atoi(mb);
@@ -2539,10 +2539,14 @@ static int step_multi(sk_env* e, const float* actions, int64_t ring_slabs, int64
                  : (pol == 1 ? launch_split_multi<1, kStepBlock, false>(pf, g64, hs, a, e->dcfg, sg)
                              : launch_split_multi<0, kStepBlock, false>(pf, g64, hs, a, e->dcfg, sg));
   } else {
-    // the restart draw under the loads (k_step's early draw) is off by
-    // default here: 65,536 games 2.73 vs 2.81 us per tick at 20 ticks per
-    // launch, 131,072 3.69 vs 3.70 / 3.33 vs 3.37 (profiles/r03i_multi_fast_early_sweep.jsonl)
-    const int early = e->multi_early > 0;
+    // the restart draw under the loads (k_step's early draw): off in round 3
+    // (65,536 games 2.73 vs 2.81 us per tick at 20 ticks per launch;
+    // profiles/r03i_multi_fast_early_sweep.jsonl); with round 6's tick the
+    // wait it hides under has room, and the draw leaves the restarting waves'
+    // chain: on by default (SK_MULTI_EARLY=0 off), the driver's 20-tick
+    // region 2.53-2.55 -> 2.51-2.54 us, 20-tick launches back to back 2.35
+    // -> 2.30-2.33 (profiles/r06af_multi_early_ab.jsonl)
+    const int early = e->multi_early != 0;
     // workgroup: four waves (default; SK_MULTI_BLOCK=64: one).  A quarter of
     // the workgroups to dispatch, one wave per SIMD either way.  Round 3 had
     // 64 lanes ahead by ~0.6 % with the 88-B form (profiles/

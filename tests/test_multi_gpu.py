@@ -21,15 +21,16 @@ def ssa():
 
 
 @pytest.fixture(params=["0", "0e", "0p", "0q", "1", "1p", "1w"],
-                ids=["lane_per_game", "lane_per_game_early_draw", "lane_per_game_prefetch2", "lane_per_game_prefetch4",
+                ids=["lane_per_game_late_draw", "lane_per_game_early_draw", "lane_per_game_prefetch2", "lane_per_game_prefetch4",
                      "player_split", "player_split_prefetch2", "player_split_512"])
 def split(request, monkeypatch):
     """every multi-tick geometry (k_step_multi, with or without the restart
     draw under the loads, with or without the prefetch wave; k_step_split_multi on 64-lane workgroups, and on
     512-lane ones with waves 4-7 staggered) meets the same bar"""
     monkeypatch.setenv("SK_MULTI_SPLIT", request.param[0])
-    if request.param == "0e":
-        monkeypatch.setenv("SK_MULTI_EARLY", "1")
+    # the restart draw under the loads: on by default (round 6); "0" keeps the
+    # draw in the restart branch
+    monkeypatch.setenv("SK_MULTI_EARLY", "1" if request.param == "0e" else "0" if request.param == "0" else "-1")
     if request.param in ("0p", "0q", "1p"):  # the action-slab prefetch wave, 2 / 4 ticks ahead
         monkeypatch.setenv("SK_MULTI_PREFETCH", "4" if request.param == "0q" else "2")
     if request.param == "1w":
