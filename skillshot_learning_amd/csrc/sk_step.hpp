@@ -317,6 +317,11 @@ __device__ __forceinline__ StepLane split_load(const StepArgs& a, int64_t gt, sk
   return L;
 }
 
+// SK_SPLIT_FINISH_BF = 0 (A/B builds): the round-5 branches and one store
+// pass after the restart
+#ifndef SK_SPLIT_FINISH_BF
+#define SK_SPLIT_FINISH_BF 1
+#endif
 __device__ __forceinline__ void split_finish(const StepArgs& a, const Cfg& c, const StepLane& L, float2 act,
                                              sk_counters* slot) {
   const int64_t i = L.i, h = L.h;
@@ -350,6 +355,54 @@ __device__ __forceinline__ void split_finish(const StepArgs& a, const Cfg& c, co
       pr.c = (float)r.c;
     }
   }
+  const double q_old = qrot;
+#if SK_SPLIT_FINISH_BF
+  // round 6: the commits as selects (split_tick_carry's form: the tick is a
+  // latency chain and exec-mask branches serialise it)
+  {
+    const double speed = clamp_action((double)act.x), psp = (double)c.pspeed;  // Player.py:57-68
+    const double nxf = __builtin_rint((double)px - (m.s * psp) * speed);
+    const double nyf = __builtin_rint((double)py - (m.c * psp) * speed);
+    const bool ok = (nxf >= 0.0) & (nxf + (double)c.psize <= (double)c.W) & (nyf >= 0.0) &
+                    (nyf + (double)c.psize <= (double)c.H);
+    px = ok ? (int)(ok ? nxf : 0.0) : px;
+    py = ok ? (int)(ok ? nyf : 0.0) : py;
+  }
+  rot = rn;
+  {  // Player.move_shoot_projectile (Player.py:78-89)
+    const bool f = qcd <= 0;
+    qx = f ? px : qx;
+    qy = f ? py : qy;
+    qrot = f ? rot : qrot;
+    qvalid = f ? 1 : qvalid;
+    qcd = f ? c.cdmax : qcd;
+    qage = f ? 0 : qage;
+  }
+  // game_tick  SkillshotGame.py:115-122 (live is identical in both lanes)
+  const int lv = live != 0;
+  ticks += lv;
+  {  // Projectile.py:38-53
+    const double qsp = (double)c.qspeed;
+    const int nx = (int)__builtin_rint((double)qx - t.s * qsp), ny = (int)__builtin_rint((double)qy - t.c * qsp);
+    const bool ok = (nx + c.qsize <= c.W) & (nx >= 0) & (ny + c.qsize <= c.H) & (ny >= 0);
+    const bool upd = lv && qvalid;
+    qx = (upd && ok) ? nx : qx;
+    qy = (upd && ok) ? ny : qy;
+    qvalid = (upd && !ok) ? 0 : qvalid;
+    qcd -= lv;
+    qage += lv;
+  }
+  const int opx = pair_swap(px), opy = pair_swap(py);
+  const int oqx = pair_swap(qx), oqy = pair_swap(qy), oqv = pair_swap(qvalid);
+  {  // SkillshotGame.check_collision (:58-94): player 1 tested first
+    const int p1x = p ? opx : px, p1y = p ? opy : py, q1x = p ? oqx : qx, q1y = p ? oqy : qy, q1v = p ? oqv : qvalid;
+    const int p2x = p ? px : opx, p2y = p ? py : opy, q2x = p ? qx : oqx, q2y = p ? qy : oqy, q2v = p ? qvalid : oqv;
+    const bool h1 = lv && hit_test_s(c, p1x, p1y, q2x, q2y, q2v);
+    const bool h2 = lv && !h1 && hit_test_s(c, p2x, p2y, q1x, q1y, q1v);
+    winner = h1 ? 1 : (h2 ? 2 : winner);
+    live = (h1 || h2) ? 0 : live;
+  }
+#else
   move_direction_sc(c, px, py, m, (double)act.x);
   rot = rn;
   shoot_s(c, px, py, rot, qx, qy, qrot, qcd, qage, qvalid);
@@ -364,7 +417,26 @@ __device__ __forceinline__ void split_finish(const StepArgs& a, const Cfg& c, co
     if (p == 0) collide_s(c, px, py, qx, qy, qvalid, opx, opy, oqx, oqy, oqv, live, winner);
     else collide_s(c, opx, opy, oqx, oqy, oqv, px, py, qx, qy, qvalid, live, winner);
   }
+#endif
   ctr_settle(wc);  // every load consumed, no state store issued yet
+#if SK_SPLIT_FINISH_BF
+  // the state out before the obs, the ring row and the restart (k_step_multi's
+  // SK_EARLY_STORE); a restarted game's lanes store theirs again below
+  if (in) {
+    reinterpret_cast<int2*>(a.v.pos)[h] = make_int2(px, py);
+    reinterpret_cast<double*>(a.v.rot)[h] = rot;
+    reinterpret_cast<int2*>(a.v.qpos)[h] = make_int2(qx, qy);
+    if (__double_as_longlong(qrot) != __double_as_longlong(q_old)) reinterpret_cast<double*>(a.v.qrot)[h] = qrot;
+    reinterpret_cast<int2*>(a.v.qcdage)[h] = make_int2(qcd, qage);
+    if (p == 0) {
+      const unsigned f = (unsigned)(qvalid & 0xff) | ((unsigned)(oqv & 0xff) << 8) | ((unsigned)(live & 0xff) << 16) |
+                         ((unsigned)(winner & 0xff) << 24);
+      a.v.misc[i] = make_int2(ticks, (int)f);
+    }
+  }
+#else
+  (void)q_old;
+#endif
   const bool d = in && ((!live) || (ticks >= a.tick_limit));  // SkillshotLearner.py:302
   const bool want_obs = a.obs || a.reward || a.obs_reset;     // launch-uniform
   float o[12];
@@ -437,16 +509,18 @@ __device__ __forceinline__ void split_finish(const StepArgs& a, const Cfg& c, co
     }
     store_obs(a.obs_reset, a.n, p, i, o);
   }
-  reinterpret_cast<int2*>(a.v.pos)[h] = make_int2(px, py);
-  reinterpret_cast<double*>(a.v.rot)[h] = rot;
-  reinterpret_cast<int2*>(a.v.qpos)[h] = make_int2(qx, qy);
-  reinterpret_cast<double*>(a.v.qrot)[h] = qrot;
-  reinterpret_cast<int2*>(a.v.qcdage)[h] = make_int2(qcd, qage);
   const int ov = pair_swap(qvalid);
-  if (p == 0) {
-    unsigned f = (unsigned)(qvalid & 0xff) | ((unsigned)(ov & 0xff) << 8) | ((unsigned)(live & 0xff) << 16) |
-                 ((unsigned)(winner & 0xff) << 24);
-    a.v.misc[i] = make_int2(ticks, (int)f);
+  if (!SK_SPLIT_FINISH_BF || reset) {
+    reinterpret_cast<int2*>(a.v.pos)[h] = make_int2(px, py);
+    reinterpret_cast<double*>(a.v.rot)[h] = rot;
+    reinterpret_cast<int2*>(a.v.qpos)[h] = make_int2(qx, qy);
+    reinterpret_cast<double*>(a.v.qrot)[h] = qrot;
+    reinterpret_cast<int2*>(a.v.qcdage)[h] = make_int2(qcd, qage);
+    if (p == 0) {
+      unsigned f = (unsigned)(qvalid & 0xff) | ((unsigned)(ov & 0xff) << 8) | ((unsigned)(live & 0xff) << 16) |
+                   ((unsigned)(winner & 0xff) << 24);
+      a.v.misc[i] = make_int2(ticks, (int)f);
+    }
   }
   if (slot) wave_count_at(slot, wc, d && p == 0, fin_winner, fin_ticks);  // after the stores (see wave_count)
   // The future-collision flag within its margin of an edge is settled here,
