@@ -6,7 +6,9 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && export TMPDIR=/tmp
 TAG=${1:-pm}; OUT=gpurun_out/pmcm_$TAG; mkdir -p $OUT
 P1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_SCA SQ_BUSY_CYCLES SQ_WAVES"
 P2="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_MFMA SQ_INSTS_BRANCH"
-for V in "1 0 1" "1 1 1" "1 0 0" "0 0 1"; do
+# VARIANTS: "POL SPLIT PACK" triples (default: round 3's four)
+IFS=, read -ra VS <<< "${VARIANTS:-1 0 1,1 1 1,1 0 0,0 0 1}"
+for V in "${VS[@]}"; do
   set -- $V; POL=$1; SPL=$2; PK=$3
   i=0
   for P in "$P1" "$P2"; do
