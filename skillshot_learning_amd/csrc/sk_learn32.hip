@@ -899,7 +899,38 @@ __global__ void __launch_bounds__(kThreads) k_actor_grad32(const float* __restri
 constexpr int kSlices = 8, kSliceU = kH2 / kSlices;  // 16 units per slice
 constexpr int kSlThreads = 256;                       // 4 waves: one per SIMD
 constexpr int kZPlane = kR * kH2;                     // one net's z2 of a row tile
-constexpr int kLdZ = kH2 + 4;
+// LDS layouts of the sliced kernels, laid out against the gfx950 bank rules
+// (MI355X_MICROARCH.md §LDS; VERDICT r05: conflict cycles were 100 / 61 / 91 %
+// of the LDS instructions of fwd<1> / bwd<1> / fwd<2>).  SK_SL_SWZ=0 restores
+// the padded row-major layouts (A/B only); the arithmetic is the same either way.
+// Every XOR below touches only bits 2-3 of the column (which 16-B slot of a
+// fragment) and depends only on a lane's own row, so each lane computes its
+// addresses once and the unrolled accesses differ by immediate offsets (a
+// swizzle that mixed the unrolled indices in cost ~80 VALU per wave).
+//   [16][16] tiles read as 16-B MFMA fragments (lane (i, g): row i, floats
+//     4g..4g+3; ds_read_b128 serves 16 lanes per cycle over 64 banks): rows of
+//     16 floats, the slot XORed with (row >> 1) & 3 -- every lane group of the
+//     fragment read and of the 8-lane ds_write_b128 of a transposed row covers
+//     16 (8) distinct slots.  Also the [256][16] transposed layer 1.
+//   [16][260] layer-1 outputs (written one float per lane, rows 4g + r, the
+//     two 16-lane rows of a half 1,040 floats = 16 banks apart; read as
+//     fragments, row i): the slot XORed with f(row >> 2), f = 0, 1, 1, 0, which
+//     puts the four 4-row blocks of a ds_read_b128 lane group on disjoint slots.
+//   [16][128 + 16] z2 planes: the row reductions read rows r and r + 1 in one
+//     32-lane half, 16 banks apart.
+//   the forward's K-split partials [wave][row][unit]: row r at 16 (r + r / 4),
+//     so rows 4 apart (lanes g and g + 1 of one store) sit 16 banks apart.
+#ifndef SK_SL_SWZ
+#define SK_SL_SWZ 1
+#endif
+constexpr int kSlLdT = SK_SL_SWZ ? 16 : kLdT16;
+constexpr int kSlLdH = kLdH1;
+constexpr int kLdZ = SK_SL_SWZ ? kH2 + 16 : kH2 + 4;
+constexpr int kSlRed = SK_SL_SWZ ? 20 * kSliceU : kR * kSliceU;  // floats per wave
+__device__ __forceinline__ int sl_tmask(int row) { return SK_SL_SWZ ? ((row >> 1) & 3) << 2 : 0; }
+__device__ __forceinline__ int sl_t16(int row, int col) { return row * kSlLdT + (col ^ sl_tmask(row)); }
+__device__ __forceinline__ int sl_hmask(int row) { return SK_SL_SWZ ? (((row >> 2) ^ (row >> 3)) & 1) << 2 : 0; }
+__device__ __forceinline__ int sl_red(int row, int j) { return (SK_SL_SWZ ? row + (row >> 2) : row) * kSliceU + j; }
 constexpr int kW1Part = kPW2;                         // W1 + b1: floats per contribution row
 enum { kSlCriticY = 0, kSlCriticBoot = 1, kSlActor = 2 };
 __host__ __device__ constexpr int sl_planes(int mode) { return mode == kSlCriticBoot ? 3 : (mode == kSlActor ? 2 : 1); }
@@ -909,10 +940,10 @@ __host__ __device__ constexpr int sl_ld(int mode, int p) {
   return (mode == kSlActor && p == 0) || (mode == kSlCriticBoot && p == 1) ? kALd : kCLd;
 }
 __host__ __device__ constexpr int sl_nout(int mode, int p) { return sl_ld(mode, p) == kALd ? 2 : 1; }
-constexpr size_t sl_fwd_lds(int) { return (size_t)(kR * kLdS16 + kR * kLdH1 + kH1 + 4 * kR * kSliceU) * 4; }
+constexpr size_t sl_fwd_lds(int) { return (size_t)(kR * kSlLdT + kR * kSlLdH + kH1 + 4 * kSlRed) * 4; }
 constexpr size_t sl_bwd_lds(int mode) {
-  return (size_t)(2 * kR * kLdS16 + sl_planes(mode) * (kR * kLdZ + 1024) + kR * kLdH1 + kH1 * kLdT16 +
-                  3 * kSliceU * kLdT16 + 32 + 2 * kR + 2 * kR + kR + 4) *
+  return (size_t)(2 * kR * kSlLdT + sl_planes(mode) * (kR * kLdZ + 1024) + kR * kSlLdH + kH1 * kSlLdT +
+                  3 * kSliceU * kSlLdT + 32 + 2 * kR + 2 * kR + kR + 4) *
          4;
 }
 static_assert(sl_fwd_lds(kSlCriticBoot) <= 160 * 1024 && sl_bwd_lds(kSlCriticBoot) <= 160 * 1024, "LDS budget");
@@ -938,7 +969,29 @@ __device__ __forceinline__ f4 w1_frag(gfp W1, int n0, int lane) {
 __device__ __forceinline__ f32x4 g16_l1w(const float* S, f4 w, int lane) {
   const int i = lane & 15, g = lane >> 4;
   const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-  return m16x4(*(const f4*)(S + i * kLdS16 + 4 * g), w, z);
+  return m16x4(*(const f4*)(S + sl_t16(i, 4 * g)), w, z);
+}
+// (n = 16 nt + i: n's masks are i's)
+// l1_out on the sliced layouts
+__device__ __forceinline__ void l1_out_sl(f32x4 acc, const float* tl, int nt, int lane, float* H, float* HT, bool drop,
+                                          uint32_t bits4) {
+  const int i = lane & 15, g = lane >> 4, n = 16 * nt + i;
+  const float b = tl[kT1 + n];
+  f4 z;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float v = fmaxf(acc[r] + b, 0.f);
+    if (drop) v = (bits4 >> r) & 1u ? v * 1.25f : 0.f;
+    z[r] = v;
+    H[(4 * g + r) * kSlLdH + 16 * nt + (i ^ sl_hmask(4 * g))] = v;
+  }
+  if (HT) *(f4*)(HT + n * kSlLdT + (4 * g ^ sl_tmask(i))) = z;
+}
+// g16_wgrad on the sliced layouts
+__device__ __forceinline__ f32x4 g16_wgrad_sl(f32x4 acc, const float* AT, int m0, const float* BT, int n0, int lane) {
+  const int i = lane & 15, g = lane >> 4;
+  const int c = 4 * g ^ sl_tmask(i);  // m0, n0: multiples of 16
+  return m16x4(*(const f4*)(AT + (m0 + i) * kSlLdT + c), *(const f4*)(BT + (n0 + i) * kSlLdT + c), acc);
 }
 
 // The replay minibatch gathered inside the critic's first launch
@@ -959,10 +1012,10 @@ __global__ void __launch_bounds__(kSlThreads) k_grad_slice_fwd(const float* __re
                                                               RingSample rs) {
   constexpr int NP = sl_planes(MODE);
   extern __shared__ __attribute__((aligned(16))) float smem_sl[];
-  float* sS = smem_sl;              // [16][20]
-  float* sH = sS + kR * kLdS16;     // [16][260] layer-1 outputs
-  float* sB1 = sH + kR * kLdH1;     // [256]
-  float* sRed = sB1 + kH1;          // [4 waves][16 rows][16 units] K-split partials
+  float* sS = smem_sl;              // [16][16] (sl_t16)
+  float* sH = sS + kR * kSlLdT;     // [16][260] layer-1 outputs (sl_hmask)
+  float* sB1 = sH + kR * kSlLdH;    // [256]
+  float* sRed = sB1 + kH1;          // [4 waves][16 rows][16 units] K-split partials (sl_red)
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int tid = threadIdx.x, lane = tid & 63, i = lane & 15, g = lane >> 4;
   // block = (row tile, net, slice), slice fastest
@@ -1010,7 +1063,7 @@ __global__ void __launch_bounds__(kSlThreads) k_grad_slice_fwd(const float* __re
     keep0 = dropout_bits16(seed, call, key_row0 + row0, w, lane);      // n-tiles w, w + 8
     keep1 = dropout_bits16(seed, call, key_row0 + row0, w + 4, lane);  // n-tiles w + 4, w + 12
   }
-  sS[si * kLdS16 + sk] = sv;
+  sS[sl_t16(si, sk)] = sv;
   sB1[tid] = bv;
   lds_sync32();
   if (scat) {
@@ -1021,25 +1074,25 @@ __global__ void __launch_bounds__(kSlThreads) k_grad_slice_fwd(const float* __re
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const uint32_t bits = ((q & 1) ? keep1 : keep0) >> (4 * (q >> 1));
-    l1_out(g16_l1w(sS, w1v[q], lane), sB1, w + 4 * q, lane, sH, nullptr, drop, bits);
+    l1_out_sl(g16_l1w(sS, w1v[q], lane), sB1, w + 4 * q, lane, sH, nullptr, drop, bits);
   }
   lds_sync32();
   // ---- layer 2 of the slice: wave w contracts inputs 64 w .. 64 w + 63
   {
-    const float* xr = sH + i * kLdH1 + 64 * w + 4 * g;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const float* xr = sH + i * kSlLdH + 64 * w + (4 * g ^ sl_hmask(i));
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc = m16x4(*(const f4*)(xr + 16 * t), wv[t], acc);
-    float* red = sRed + w * kR * kSliceU;
+    float* red = sRed + w * kSlRed + sl_red(4 * g, i);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) red[(4 * g + r) * kSliceU + i] = acc[r];
+    for (int r = 0; r < 4; ++r) red[r * kSliceU] = acc[r];
   }
   lds_sync32();
   // ---- z2[row][16 s + j] = the 4 waves' partials (thread = (row, j))
   {
     const int row = tid >> 4, j = tid & 15;
-    const float* red = sRed + row * kSliceU + j;
-    const float z = (red[0] + red[kR * kSliceU]) + (red[2 * kR * kSliceU] + red[3 * kR * kSliceU]);
+    const float* red = sRed + sl_red(row, j);
+    const float z = (red[0] + red[kSlRed]) + (red[2 * kSlRed] + red[3 * kSlRed]);
     Z[((int64_t)rt * NP + p) * kZPlane + row * kH2 + kSliceU * s + j] = z;
   }
 }
@@ -1078,16 +1131,16 @@ __device__ __forceinline__ void grad_slice_bwd(int bid, float* smem_sl, SK_SLICE
   constexpr int NP = sl_planes(MODE);
   constexpr bool CRIT = MODE != kSlActor;
   constexpr int LD0 = sl_ld(MODE, 0), NPAR = CRIT ? kCP : kAP;
-  float* sS = smem_sl;                  // [16][20]
-  float* sST = sS + kR * kLdS16;        // [16 features][16 rows (+4)]
-  float* sZ = sST + kR * kLdS16;        // [NP][16][132]
+  float* sS = smem_sl;                  // [16][16] (sl_t16)
+  float* sST = sS + kR * kSlLdT;        // [16 features][16 rows] (sl_t16)
+  float* sZ = sST + kR * kSlLdT;        // [NP][16][kLdZ]
   float* sTL = sZ + NP * kR * kLdZ;     // [NP][1024] the nets' fp32 tails
-  float* sH1 = sTL + NP * 1024;         // [16][260] layer 1 of the trained net (after Dropout)
-  float* sH1T = sH1 + kR * kLdH1;       // [256][20]
-  float* sDZ2 = sH1T + kH1 * kLdT16;    // [16 rows][16 slice units (+4)]
-  float* sDZ2T = sDZ2 + kSliceU * kLdT16;  // [16 units][16 rows (+4)]
-  float* sH2T = sDZ2T + kSliceU * kLdT16;  // [4 waves][16 units][4] per-unit gradient sums
-  float* sA = sH2T + kSliceU * kLdT16;  // [16][2] actions (critic)
+  float* sH1 = sTL + NP * 1024;         // [16][260] layer 1 of the trained net, after Dropout (sl_hmask)
+  float* sH1T = sH1 + kR * kSlLdH;      // [256][16] (sl_t16)
+  float* sDZ2 = sH1T + kH1 * kSlLdT;    // [16 rows][16 slice units] (sl_t16)
+  float* sDZ2T = sDZ2 + kSliceU * kSlLdT;  // [16 units][16 rows] (sl_t16)
+  float* sH2T = sDZ2T + kSliceU * kSlLdT;  // [4 waves][16 units][4] per-unit gradient sums
+  float* sA = sH2T + kSliceU * kSlLdT;  // [16][2] actions (critic)
   float* sRD = sA + 32;                 // [16] r or y, [16] done
   float* sDQ = sRD + 2 * kR;            // [16][2] dL/dq (critic) or dL/dz3 (actor)
   float* sST8 = sDQ + 2 * kR;           // [16] per-row e^2 (critic) or Q (actor)
@@ -1133,8 +1186,8 @@ __device__ __forceinline__ void grad_slice_bwd(int bid, float* smem_sl, SK_SLICE
     keep0 = dropout_bits16(seed, call, key_row0 + row0, w, lane);
     keep1 = dropout_bits16(seed, call, key_row0 + row0, w + 4, lane);
   }
-  sS[si * kLdS16 + sk] = sv;
-  sST[sk * kLdT16 + si] = sv;
+  sS[sl_t16(si, sk)] = sv;
+  sST[sl_t16(sk, si)] = sv;
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
 #pragma unroll
@@ -1166,7 +1219,7 @@ __device__ __forceinline__ void grad_slice_bwd(int bid, float* smem_sl, SK_SLICE
   for (int q = 0; q < 4; ++q) {
     const int nt = w + 4 * q;
     const uint32_t bits = ((q & 1) ? keep1 : keep0) >> (4 * (q >> 1));
-    l1_out(g16_l1w(sS, w1v[q], lane), sTL, nt, lane, sH1, sH1T, CRIT, bits);
+    l1_out_sl(g16_l1w(sS, w1v[q], lane), sTL, nt, lane, sH1, sH1T, CRIT, bits);
   }
   {
     const int row = tid >> 4, c = tid & 15;
@@ -1263,8 +1316,8 @@ __device__ __forceinline__ void grad_slice_bwd(int bid, float* smem_sl, SK_SLICE
       dz = h2 > 0.f ? sDQ[2 * row] * T0[kT3 + u] + sDQ[2 * row + 1] * T0[kT3 + kH2 + u] : 0.f;
       h2x = h2;
     }
-    sDZ2[row * kLdT16 + j] = dz;
-    sDZ2T[j * kLdT16 + row] = dz;
+    sDZ2[sl_t16(row, j)] = dz;
+    sDZ2T[sl_t16(j, row)] = dz;
     // the unit's b2 and W3 (and, critic, action-column) gradients over the
     // wave's 4 rows (lanes j, j + 16, j + 32, j + 48), then across waves in phase 3
     float v[4];
@@ -1323,13 +1376,13 @@ __device__ __forceinline__ void grad_slice_bwd(int bid, float* smem_sl, SK_SLICE
     if (stat_out) atomicAdd(stat_out, st);
   }
   const float dscale = CRIT ? 1.25f : 1.f;  // Dropout(0.2): kept activations x 1.25
-  const f4 dzr = *(const f4*)(sDZ2 + i * kLdT16 + 4 * g);
-  const f4 sT = *(const f4*)(sST + i * kLdT16 + 4 * g);
+  const f4 dzr = *(const f4*)(sDZ2 + sl_t16(i, 4 * g));
+  const f4 sT = *(const f4*)(sST + sl_t16(i, 4 * g));
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int nt = w + 4 * q, n = 16 * nt + i;
     const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
-    const f32x4 gw2 = g16_wgrad(z4, sDZ2T, 0, sH1T, 16 * nt, lane);
+    const f32x4 gw2 = g16_wgrad_sl(z4, sDZ2T, 0, sH1T, 16 * nt, lane);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int o = kSliceU * s + 4 * g + r;
@@ -1340,7 +1393,7 @@ __device__ __forceinline__ void grad_slice_bwd(int bid, float* smem_sl, SK_SLICE
     float b = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      d[r] = sH1[(4 * g + r) * kLdH1 + n] > 0.f ? acc[r] * dscale : 0.f;
+      d[r] = sH1[(4 * g + r) * kSlLdH + 16 * nt + (i ^ sl_hmask(4 * g))] > 0.f ? acc[r] * dscale : 0.f;
       b += d[r];
     }
     b += __shfl_xor(b, 16, 64);
@@ -2063,7 +2116,7 @@ __global__ void __launch_bounds__(kFwdThreads) k_act_step16(const float* __restr
 // forward's z2; the acting half reads the actor and the observations and
 // writes the env, the actions and the ring (the minibatch was gathered
 // before, excluding the rows this insert writes).  LDS is the larger of the
-// two layouts: two workgroups per CU (the critic's 81,616 B twice fill the
+// two layouts: two workgroups per CU (the critic's 78,544 B twice fill the
 // CU's 160 KiB).
 constexpr size_t bwd_act_lds(int mode, bool a16 = false) {
   return (a16 ? kActStep16Lds : kActStepLds) > sl_bwd_lds(mode) ? (a16 ? kActStep16Lds : kActStepLds)
