@@ -528,13 +528,14 @@ def learner_rate(envs, world, rank, ticks, batch=256, exploration="param_noise",
     tg.run(10)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    st = torch.cuda.current_stream()  # TickGraph.run replays on the caller's stream
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    e0.record(tg.stream)
+    e0.record(st)
     tg.run(max(1, ticks // tg.ticks))
-    e1.record(tg.stream)
+    e1.record(st)
     torch.cuda.synchronize()
     # this rank's time from the common start to its own finish; the job's is
     # the max over ranks (below).  The closing barrier only aligns the ranks
@@ -560,7 +561,7 @@ def learner_rate(envs, world, rank, ticks, batch=256, exploration="param_noise",
                tick_mode=tg.mode, draw_order="reference (after the tick's insert)" if tg.mode == "sequential"
                else "one tick late (before the tick's insert)",
                env_steps_per_s=envs * world * n_ticks / el, ms_per_tick=el * 1e3 / n_ticks, gpu_ms_per_tick=gpu_ms,
-               episodes=L.game_environment.counters(stream=ctypes.c_void_p(tg.stream.cuda_stream)))
+               episodes=L.game_environment.counters(stream=ctypes.c_void_p(st.cuda_stream)))
     if roofline and world == 1 and tg.mode == "sequential":
         try:
             out["roofline"] = learner_roofline(L, tg, batch, precision, exploration, gpu_ms)

@@ -1508,26 +1508,30 @@ class TickGraph:
                 L._refresh_actor_pack()
 
     def run(self, n=1):
-        """n graph replays (n * ticks_per_graph ticks) on the graph's stream."""
+        """n graph replays (n * ticks_per_graph ticks) on the caller's current
+        stream.  Work queued on `self.stream` (the capture stream) before the
+        call is waited for first.  The replays are not put on the capture
+        stream: the form that did so ended with the caller's stream waiting
+        on it, and that wait, pending in another hardware queue while the
+        replays ran, slowed every replayed tick by ~5 us (config 3 52.0 ->
+        57.4 us per tick; tools/graph_host_rate.py, profiles/r06at_*)."""
         cur = torch.cuda.current_stream(self.L.device)
-        self.stream.wait_stream(cur)
-        with torch.cuda.stream(self.stream):  # replay() launches on the current stream
-            # both step slots current: the graph of either phase reads its own
-            self.L.game_environment.sync_step_counter(ctypes.c_void_p(self.stream.cuda_stream))
-            if self.overlap:  # the first replayed update samples the current count
-                self.L.replay.horizon[self._phase].copy_(self.L.replay.total_t)
-            for _ in range(n):
-                kind, g = self._phases[self._phase]
-                if kind == "graph":
-                    g.replay()
-                else:
-                    for it in g:
-                        if callable(it) and not isinstance(it, torch.cuda.CUDAGraph):
-                            it()
-                        else:
-                            it.replay()
-                self._phase = (self._phase + self.ticks) % 2
         cur.wait_stream(self.stream)
+        # both step slots current: the graph of either phase reads its own
+        self.L.game_environment.sync_step_counter(ctypes.c_void_p(cur.cuda_stream))
+        if self.overlap:  # the first replayed update samples the current count
+            self.L.replay.horizon[self._phase].copy_(self.L.replay.total_t)
+        for _ in range(n):
+            kind, g = self._phases[self._phase]
+            if kind == "graph":
+                g.replay()  # on the current stream
+            else:
+                for it in g:
+                    if callable(it) and not isinstance(it, torch.cuda.CUDAGraph):
+                        it()
+                    else:
+                        it.replay()
+            self._phase = (self._phase + self.ticks) % 2
         self.replays += n
         # host mirrors of the ring (2N rows per tick)
         r, rows = self.L.replay, n * self.ticks * 2 * self.obs.shape[1]

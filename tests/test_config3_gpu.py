@@ -34,7 +34,7 @@ def test_config3_tick_graph(learner_mod, exploration, precision):
     calls0 = int(L.ddpg.drop_calls)
     step0 = g.step_counter
     w0 = [p.clone() for p in L.model_actor.parameters()]
-    g.clear_counters(stream=ctypes.c_void_p(tg.stream.cuda_stream))  # ordered after the capture's warm-up ticks
+    g.clear_counters(stream=ctypes.c_void_p(tg.stream.cuda_stream))  # ordered after the capture's warm-up ticks (run() waits for the capture stream)
     tg.run(100)  # 200 ticks
     torch.cuda.synchronize()
     ticks = 200

@@ -288,7 +288,7 @@ def test_tick_overlap_equals_serial(learner, monkeypatch, precision, exploration
                     torch.cat([p.detach().flatten() for p in L.model_critic.parameters()]),
                     torch.cat([p.detach().flatten() for p in L.ddpg.target_actor.parameters()]),
                     L.replay.buf.clone(), int(L.replay.total_t), L.game_environment.counters(
-                        stream=ctypes.c_void_p(tg.stream.cuda_stream))))
+                        stream=ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))))
     (a1, c1, t1, b1, n1, k1) = out[0]
     assert k1["dones"] > 0
     for a2, c2, t2, b2, n2, k2 in out[1:]:

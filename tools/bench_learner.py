@@ -76,9 +76,9 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(tg.stream)
+        e0.record(torch.cuda.current_stream())  # TickGraph.run replays on the caller's stream
         tg.run(a.ticks // 2)
-        e1.record(tg.stream)
+        e1.record(torch.cuda.current_stream())
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         ticks = (a.ticks // 2) * 2
