@@ -1514,7 +1514,7 @@ class TickGraph:
         stream: the form that did so ended with the caller's stream waiting
         on it, and that wait, pending in another hardware queue while the
         replays ran, slowed every replayed tick by ~5 us (config 3 52.0 ->
-        57.4 us per tick; tools/graph_host_rate.py, profiles/r06at_*)."""
+        57.4 us per tick; tools/graph_host_rate.py, profiles/r06at_tickgraph_stream/)."""
         cur = torch.cuda.current_stream(self.L.device)
         cur.wait_stream(self.stream)
         # both step slots current: the graph of either phase reads its own
