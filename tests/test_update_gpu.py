@@ -244,6 +244,32 @@ def test_fused_tick_graph(mods):
     assert any((p - q).abs().max() > 0 for p, q in zip(L.model_actor.parameters(), w0))
 
 
+def test_tick_graph_runs_on_callers_stream(mods):
+    """TickGraph.run replays on the caller's current stream (no cross-stream
+    wait left pending while the replays run): the same learner
+    replayed under a side stream and on the default stream ends with the
+    same nets, ring and game state, bit for bit, and work the caller queues
+    on its stream after run() sees the replays' results."""
+    learner = mods
+    out = []
+    for side in (False, True):
+        L = learner.SkillshotLearner(n_envs=256, device="cuda", seed=21, gamma=0.9, tau=0.05,
+                                     replay_capacity=1 << 14, precision="fp32")
+        tg = L.tick_graph(batch=256, ticks_per_graph=2, warmup=2)
+        st = torch.cuda.Stream() if side else torch.cuda.current_stream()
+        with torch.cuda.stream(st):
+            tg.run(3)
+            # queued on the caller's stream right behind the replays
+            snap = torch.cat([p.detach().flatten() for p in L.model_actor.parameters()]).clone()
+        torch.cuda.synchronize()
+        now = torch.cat([p.detach().flatten() for p in L.model_actor.parameters()])
+        assert torch.equal(snap, now)
+        out.append((now, torch.cat([p.detach().flatten() for p in L.model_critic.parameters()]),
+                    L.replay.buf.clone(), L.game_environment.pos.clone()))
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
+
+
 def test_adam_launches_keep_every_pack_current(mods):
     """The Adam launches write the packed copies of what they produce
     (sk_adam_flat_packed): after training ticks, the critic / actor /
