@@ -15,6 +15,7 @@ import json
 import os
 import statistics
 import sys
+import time
 
 import torch
 
@@ -34,10 +35,14 @@ def main():
                         "sweep of another buffer (evicts the generation's dirty lines from the Infinity "
                         "Cache), 400 more warm-up ticks (a long run's cache state), a ~3 ms matmul before the ring's "
                         "generation (clocks), or 400 ticks then the env reset and the ring regenerated")
+    p.add_argument("--stream", choices=["side", "default"], default="side",
+                   help="launch on bench's side stream or on the default (null) stream")
     a = p.parse_args()
     dev = torch.device("cuda", 0)
     n, ring = a.envs, 400
     env, st, acts = bench._env_and_actions(dev, n, 0, 0, 2000, ring)
+    if a.stream == "default":
+        st = torch.cuda.current_stream(dev)
     sp = ctypes.c_void_p(st.cuda_stream)
     done = torch.empty(n, dtype=torch.uint8, device=dev)
     ap, dp = ctypes.c_void_p(acts.data_ptr()), ctypes.c_void_p(done.data_ptr())
@@ -45,7 +50,7 @@ def main():
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(st)
     e1.record(st)
-    us = []
+    us, wall = [], []
     big = torch.ones(128 << 20, dtype=torch.float32, device=dev) if a.settle == "sweep" else None
     sink = torch.zeros((), dtype=torch.float32, device=dev)
     mm = torch.randn(4096, 4096, device=dev) if a.settle == "heat" else None
@@ -69,16 +74,19 @@ def main():
             slab += t
         st.synchronize()
         torch.cuda.synchronize()
+        t0 = time.perf_counter()
         e0.record(st)
         fn(h, ap, ring, slab, a.k, dp, None, 0, lim, 1, rp, sp)
         e1.record(st)
         torch.cuda.synchronize()
+        el = time.perf_counter() - t0
         if rep:  # the first rep loads code objects
             us.append(e0.elapsed_time(e1) * 1e3 / a.k)
+            wall.append(el * 1e6 / a.k)
     us.sort()
     q = lambda f: us[min(len(us) - 1, int(f * len(us)))]  # noqa: E731
     med = statistics.median(us)
-    print(json.dumps(dict(tag=a.tag, settle=a.settle, k=a.k, reps=a.reps, event_us_median=round(med, 4),
+    print(json.dumps(dict(tag=a.tag, settle=a.settle, stream=a.stream, wall_us_median=round(statistics.median(wall), 4), k=a.k, reps=a.reps, event_us_median=round(med, 4),
                           event_us_mean=round(statistics.fmean(us), 4), p10=round(q(0.1), 4), p90=round(q(0.9), 4),
                           frac_median=round(193 * n / (med * 1e-6) / 8e12, 4))), flush=True)
     env.close()
