@@ -1126,6 +1126,20 @@ __device__ __forceinline__ float rowall16(float v) {
 #define SK_SLICE_BWD_ARGS \
   f0, f1, f2, Sg, Ag, Yg, Rg, Dg, gamma, B, key_row0, scale, seed, call_ctr, Z, partial, partial_w1, stat_out, mask_out
 
+// The backward of a (row tile, slice) in SK_BWD_HALVES workgroups: half hq
+// owns n-tiles w + 4q for q = hq, hq + 2 (layer 1 of the trained net, the
+// dW2 columns, the dz1 share and its dW1 / db1 contributions), each half
+// redoing the loads, the per-row reductions and dz2 that both need.  Every
+// output entry is computed by exactly one workgroup with the same operations
+// in the same order as by the one-workgroup form (SK_BWD_HALVES=1), so the
+// results are the same bits; the launch has twice the workgroups on the 256
+// CUs its 128 left half idle.
+#ifndef SK_BWD_HALVES
+#define SK_BWD_HALVES 2
+#endif
+constexpr int kBwdH = SK_BWD_HALVES, kBwdQ = 4 / kBwdH;
+static_assert(kBwdH == 1 || kBwdH == 2, "one or two workgroups per (row tile, slice)");
+
 template <int MODE>
 __device__ __forceinline__ void grad_slice_bwd(int bid, float* smem_sl, SK_SLICE_BWD_PARAMS) {
   constexpr int NP = sl_planes(MODE);
@@ -1146,7 +1160,8 @@ __device__ __forceinline__ void grad_slice_bwd(int bid, float* smem_sl, SK_SLICE
   float* sST8 = sDQ + 2 * kR;           // [16] per-row e^2 (critic) or Q (actor)
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int tid = threadIdx.x, lane = tid & 63, i = lane & 15, g = lane >> 4;
-  const int rt = bid / kSlices, s = bid - rt * kSlices;
+  // block = (row tile, half, slice), slice fastest (slice s on XCD s)
+  const int s = bid % kSlices, hq = (bid / kSlices) % kBwdH, rt = bid / (kSlices * kBwdH);
   const int64_t row0 = (int64_t)rt * kR;
   const float* fl[3] = {f0, f1, f2};
   const gfp W2 = (gfp)f0 + kPW2;
@@ -1159,15 +1174,17 @@ __device__ __forceinline__ void grad_slice_bwd(int bid, float* smem_sl, SK_SLICE
   for (int p = 0; p < NP; ++p)
 #pragma unroll
     for (int k = 0; k < 4; ++k) tv[p][k] = tail_src((gfp)fl[p], sl_ld(MODE, p), sl_nout(MODE, p), tid + kSlThreads * k);
-  // the slice's W2 rows down the columns of n-tiles w + 4q (the dz1 GEMM of phase 3)
-  float wd[4][4];
+  // the slice's W2 rows down the columns of n-tiles w + 4q (the dz1 GEMM of
+  // phase 3), q = hq + kBwdH k: this workgroup's n-tiles
+  float wd[kBwdQ][4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
+  for (int k = 0; k < kBwdQ; ++k)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) wd[q][c] = W2[(size_t)(kSliceU * s + 4 * g + c) * LD0 + 16 * (w + 4 * q) + i];
-  f4 w1v[4];
+    for (int c = 0; c < 4; ++c)
+      wd[k][c] = W2[(size_t)(kSliceU * s + 4 * g + c) * LD0 + 16 * (w + 4 * (hq + kBwdH * k)) + i];
+  f4 w1v[kBwdQ];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) w1v[q] = w1_frag((gfp)f0 + kPW1, 16 * (w + 4 * q), lane);
+  for (int k = 0; k < kBwdQ; ++k) w1v[k] = w1_frag((gfp)f0 + kPW1, 16 * (w + 4 * (hq + kBwdH * k)), lane);
   f4 zv[NP][2];
 #pragma unroll
   for (int p = 0; p < NP; ++p)
@@ -1180,11 +1197,12 @@ __device__ __forceinline__ void grad_slice_bwd(int bid, float* smem_sl, SK_SLICE
   const float av = CRIT && tid < 32 && row0 + (tid >> 1) < B ? Ag[row0 * 2 + tid] : 0.f;
   const float rv = CRIT && rok ? (MODE == kSlCriticBoot ? Rg[row0 + tid] : Yg[row0 + tid]) : 0.f;
   const float dv = MODE == kSlCriticBoot && rok ? Dg[row0 + tid] : 0.f;
+  // keep0: n-tiles w, w + 8 (q = 0, 2); keep1: w + 4, w + 12 (q = 1, 3)
   uint32_t keep0 = 0, keep1 = 0;
   if (CRIT) {
     const uint64_t call = (uint64_t)*call_ctr;
-    keep0 = dropout_bits16(seed, call, key_row0 + row0, w, lane);
-    keep1 = dropout_bits16(seed, call, key_row0 + row0, w + 4, lane);
+    if (kBwdH == 1 || hq == 0) keep0 = dropout_bits16(seed, call, key_row0 + row0, w, lane);
+    if (kBwdH == 1 || hq == 1) keep1 = dropout_bits16(seed, call, key_row0 + row0, w + 4, lane);
   }
   sS[sl_t16(si, sk)] = sv;
   sST[sl_t16(sk, si)] = sv;
@@ -1205,7 +1223,8 @@ __device__ __forceinline__ void grad_slice_bwd(int bid, float* smem_sl, SK_SLICE
   }
   if (CRIT && mask_out && s == 0) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int k = 0; k < kBwdQ; ++k) {
+      const int q = hq + kBwdH * k;
       const uint32_t bits = ((q & 1) ? keep1 : keep0) >> (4 * (q >> 1));
 #pragma unroll
       for (int r = 0; r < 4; ++r)
@@ -1216,10 +1235,10 @@ __device__ __forceinline__ void grad_slice_bwd(int bid, float* smem_sl, SK_SLICE
   TP32(21);
   // ---- phase 1: layer 1 of the trained net (MFMA) and the per-row reductions (VALU)
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int nt = w + 4 * q;
+  for (int k = 0; k < kBwdQ; ++k) {
+    const int q = hq + kBwdH * k, nt = w + 4 * q;
     const uint32_t bits = ((q & 1) ? keep1 : keep0) >> (4 * (q >> 1));
-    l1_out_sl(g16_l1w(sS, w1v[q], lane), sTL, nt, lane, sH1, sH1T, CRIT, bits);
+    l1_out_sl(g16_l1w(sS, w1v[k], lane), sTL, nt, lane, sH1, sH1T, CRIT, bits);
   }
   {
     const int row = tid >> 4, c = tid & 15;
@@ -1343,8 +1362,10 @@ __device__ __forceinline__ void grad_slice_bwd(int bid, float* smem_sl, SK_SLICE
   TP32(23);
   // ---- phase 3: the slice's per-unit gradients; dW2 rows; dz1 share -> dW1, db1
   float* P = partial + (int64_t)rt * NPAR;
-  float* PW = partial_w1 + (int64_t)bid * kW1Part;
-  if (tid < kSliceU) {
+  float* PW = partial_w1 + (int64_t)(rt * kSlices + s) * kW1Part;  // one contribution row per (row tile, slice)
+  if (hq != 0) {
+    // the slice's per-unit gradients and b3 / the stat: half 0's
+  } else if (tid < kSliceU) {
     const int j = tid, u = kSliceU * s + j;
     const f4 v = (*(const f4*)(sH2T + j * 4) + *(const f4*)(sH2T + (kSliceU + j) * 4)) +
                  (*(const f4*)(sH2T + (2 * kSliceU + j) * 4) + *(const f4*)(sH2T + (3 * kSliceU + j) * 4));
@@ -1379,8 +1400,8 @@ __device__ __forceinline__ void grad_slice_bwd(int bid, float* smem_sl, SK_SLICE
   const f4 dzr = *(const f4*)(sDZ2 + sl_t16(i, 4 * g));
   const f4 sT = *(const f4*)(sST + sl_t16(i, 4 * g));
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int nt = w + 4 * q, n = 16 * nt + i;
+  for (int k = 0; k < kBwdQ; ++k) {
+    const int q = hq + kBwdH * k, nt = w + 4 * q, n = 16 * nt + i;
     const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
     const f32x4 gw2 = g16_wgrad_sl(z4, sDZ2T, 0, sH1T, 16 * nt, lane);
 #pragma unroll
@@ -1388,7 +1409,7 @@ __device__ __forceinline__ void grad_slice_bwd(int bid, float* smem_sl, SK_SLICE
       const int o = kSliceU * s + 4 * g + r;
       P[CRIT ? skpart::critic_w2_main(o, n) : kPW2 + o * kALd + n] = gw2[r];
     }
-    const f32x4 acc = m16x4(dzr, f4{wd[q][0], wd[q][1], wd[q][2], wd[q][3]}, z4);
+    const f32x4 acc = m16x4(dzr, f4{wd[k][0], wd[k][1], wd[k][2], wd[k][3]}, z4);
     f4 d;
     float b = 0.f;
 #pragma unroll
@@ -2205,7 +2226,7 @@ int launch_sliced(const float* f0, const float* f1, const float* f2, const float
     a.grid_blocks = GA;
     const size_t lds = bwd_act_lds(MODE, a16);
 #define SK_BWD_ACT(NZ, A6)                                                                                          \
-  k_bwd_act_step32<MODE, NZ, A6><<<GA + G, kFwdThreads, lds, st>>>(                                                 \
+  k_bwd_act_step32<MODE, NZ, A6><<<GA + G * kBwdH, kFwdThreads, lds, st>>>(                                         \
       f0, f1, f2, S, A, Y, R, D, gamma, B, key_row0, scale, seed, call_ctr, Z, partials, scratch, stat_out, mask_out, \
       GA, job->aflat, job->apack, job->act_out, NZ ? job->sd : 0.f, job->action_sd, job->seed, job->call_ctr, a, \
       job->c)
@@ -2219,7 +2240,7 @@ int launch_sliced(const float* f0, const float* f1, const float* f2, const float
 #undef SK_BWD_ACT
     return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;
   }
-  k_grad_slice_bwd<MODE><<<G, kSlThreads, sl_bwd_lds(MODE), st>>>(f0, f1, f2, S, A, Y, R, D, gamma, B, key_row0,
+  k_grad_slice_bwd<MODE><<<G * kBwdH, kSlThreads, sl_bwd_lds(MODE), st>>>(f0, f1, f2, S, A, Y, R, D, gamma, B, key_row0,
                                                                   scale, seed, call_ctr, Z, partials, scratch,
                                                                   stat_out, mask_out);
   return hipGetLastError() == hipSuccess ? SK_OK : SK_EHIP;

@@ -1,6 +1,7 @@
 #!/bin/bash
 # LDS layouts of the sliced update kernels (k_grad_slice_fwd / _bwd), new
-# (default build) against the padded row-major ones (a -DSK_SL_SWZ=0 variant):
+# (default build) against the padded row-major ones (a -DSK_SL_SWZ=0 variant;
+# OLD= names another variant, e.g. -DSK_BWD_HALVES=1):
 #  * bit identity of the nets, targets and ring after a graph-replayed learner
 #    run (tools/learner_bits.py), the layouts must not change the arithmetic;
 #  * LDS instruction and bank-conflict counters and the MFMA / wait counters
@@ -10,7 +11,7 @@
 #   bash tools/lds_ab.sh TAG     -> gpurun_out/lds_TAG/...
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && export TMPDIR=/tmp PYTHONUNBUFFERED=1
 OUT=gpurun_out/lds_${1:-ab}; mkdir -p $OUT
-OLD=$PWD/gpuab/swz0.so
+OLD=${OLD:-$PWD/gpuab/swz0.so}  # any variant build: OLD=$PWD/gpuab/h1.so for the one-workgroup backward
 [ -f "$OLD" ] || { echo "missing $OLD"; exit 1; }
 P1="SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU"
 P2="SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH SQ_WAVES"
