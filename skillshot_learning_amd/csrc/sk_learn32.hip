@@ -1138,7 +1138,7 @@ __device__ __forceinline__ float rowall16(float v) {
 #define SK_BWD_HALVES 2
 #endif
 constexpr int kBwdH = SK_BWD_HALVES, kBwdQ = 4 / kBwdH;
-static_assert(kBwdH == 1 || kBwdH == 2, "one or two workgroups per (row tile, slice)");
+static_assert(kBwdH == 1 || kBwdH == 2 || kBwdH == 4, "1, 2 or 4 workgroups per (row tile, slice)");
 
 template <int MODE>
 __device__ __forceinline__ void grad_slice_bwd(int bid, float* smem_sl, SK_SLICE_BWD_PARAMS) {
@@ -1201,8 +1201,9 @@ __device__ __forceinline__ void grad_slice_bwd(int bid, float* smem_sl, SK_SLICE
   uint32_t keep0 = 0, keep1 = 0;
   if (CRIT) {
     const uint64_t call = (uint64_t)*call_ctr;
-    if (kBwdH == 1 || hq == 0) keep0 = dropout_bits16(seed, call, key_row0 + row0, w, lane);
-    if (kBwdH == 1 || hq == 1) keep1 = dropout_bits16(seed, call, key_row0 + row0, w + 4, lane);
+    // (this workgroup's q = hq + kBwdH k all share hq's parity)
+    if (kBwdH == 1 || (hq & 1) == 0) keep0 = dropout_bits16(seed, call, key_row0 + row0, w, lane);
+    if (kBwdH == 1 || (hq & 1) == 1) keep1 = dropout_bits16(seed, call, key_row0 + row0, w + 4, lane);
   }
   sS[sl_t16(si, sk)] = sv;
   sST[sl_t16(sk, si)] = sv;
